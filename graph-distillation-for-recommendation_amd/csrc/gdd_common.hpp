@@ -1,0 +1,105 @@
+// gdd_common.hpp — shared host/device helpers for libgdd (gfx950 only).
+//
+// Every kernel file is compiled with -ffp-contract=off: fp32/fp64 expressions round exactly as
+// written, and every fused multiply-add in the library is an explicit fmaf()/fma(). The reference
+// arithmetic being restated (OpenBLAS sgemm = fma chains; Cython loops = separate mul/add) is
+// spelled out per kernel in that way, which is what makes the results bit-reproducible.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "gdd.h"
+
+namespace gdd {
+
+// ---------------------------------------------------------------------------------------------
+// error reporting (thread-local message, int return codes)
+// ---------------------------------------------------------------------------------------------
+void set_error(const char* fmt, ...);
+int fail(int code, const char* fmt, ...);
+
+#define GDD_HIP(expr)                                                                           \
+  do {                                                                                          \
+    hipError_t _e = (expr);                                                                     \
+    if (_e != hipSuccess)                                                                       \
+      return ::gdd::fail((int)_e, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),         \
+                         __FILE__, __LINE__);                                                   \
+  } while (0)
+
+#define GDD_REQUIRE(cond, ...)                                                                  \
+  do {                                                                                          \
+    if (!(cond)) return ::gdd::fail(GDD_E_INVALID, __VA_ARGS__);                                \
+  } while (0)
+
+// launch check: catches bad launch configurations immediately (no host sync)
+#define GDD_LAUNCHED() GDD_HIP(hipGetLastError())
+
+inline hipStream_t to_hip(gdd_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------------------------------------
+// workspace carving: 256-byte aligned sub-allocations out of one caller buffer
+// ---------------------------------------------------------------------------------------------
+struct Carver {
+  char* base;
+  size_t cap;
+  size_t off = 0;
+  Carver(void* b, size_t c) : base(static_cast<char*>(b)), cap(c) {}
+  template <class T>
+  T* take(size_t count) {
+    off = (off + 255) & ~size_t(255);
+    T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+    off += count * sizeof(T);
+    return p;
+  }
+  bool ok() const { return off <= cap; }
+};
+// size-only variant used by the *_ws_bytes queries
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// ---------------------------------------------------------------------------------------------
+// device-wide exclusive scans (hipcub), declared here, defined in gdd_scan.hip
+// ---------------------------------------------------------------------------------------------
+size_t scan_i32_ws_bytes(int64_t n);
+int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, void* ws, size_t ws_bytes,
+                       hipStream_t s);
+size_t sort_pairs_ws_bytes(int64_t n);
+int sort_pairs_i32(const int32_t* keys_in, int32_t* keys_out, const int32_t* vals_in,
+                   int32_t* vals_out, int64_t n, int end_bit, void* ws, size_t ws_bytes,
+                   hipStream_t s);
+
+// ---------------------------------------------------------------------------------------------
+// numerics shared by kernels and documented in DESIGN.md
+// ---------------------------------------------------------------------------------------------
+// correctly rounded fp64 x^-1/2 (numpy np.power(x, -0.5) agrees with this on ~95% of inputs, with
+// the rest off by one fp64 ulp; the fp32 values derived from it agree with numpy's except w.p.~1e-8)
+__host__ __device__ inline double cr_rsqrt(double x) {
+  if (!(x > 0.0)) {
+    if (x == 0.0) return __builtin_inf();  // caller maps inf -> 0 (deep_robust_utils.py:202)
+    return __builtin_nan("");
+  }
+  if (__builtin_isinf(x)) return 0.0;
+  double y = 1.0 / __builtin_sqrt(x);
+  // residual r(y) = x*y*y - 1 evaluated with error-free products; pick the neighbour with the
+  // smaller |r| (the exact value is irrational unless x is an even power of two)
+  auto resid = [x](double v) {
+    double hi = v * v;
+    double lo = __builtin_fma(v, v, -hi);  // v*v = hi + lo exactly
+    double p = x * hi;
+    double pe = __builtin_fma(x, hi, -p);  // x*hi = p + pe exactly
+    return (p - 1.0) + (pe + x * lo);
+  };
+  double r0 = resid(y);
+  // y > 0: the neighbouring doubles are one unit of the bit pattern away
+  union { double d; unsigned long long u; } b{y};
+  b.u = r0 < 0.0 ? b.u + 1ull : b.u - 1ull;
+  double y1 = b.d;
+  double r1 = resid(y1);
+  return (__builtin_fabs(r1) < __builtin_fabs(r0)) ? y1 : y;
+}
+
+}  // namespace gdd

@@ -1,0 +1,628 @@
+// gdd_kmeans.hip — (a5/a6/a8) the WCSS k-means building blocks, scikit-learn 1.7.2 semantics.
+//
+// What is restated (sklearn/cluster/…):
+//   row norms        utils/extmath.py:76  np.einsum("ij,ij->i") — numpy SSE3 float32 kernel order
+//   assignment       _k_means_lloyd.pyx:172-213 — ||C||² then sgemm(-2·X·Cᵀ, beta=1), row argmin
+//                    with strict '<' (first index wins). OpenBLAS sgemm computes every element as a
+//                    k-ordered fp32 fma chain finished by fma(-2, acc, ||c||²) (verified bit-exact in
+//                    oracle/ tests); v_mfma_f32_32x32x2_f32 is exactly such a chain, so the MFMA
+//                    distance tile reproduces it bit for bit.
+//   sample distance  _k_means_common.pyx:26-48 _euclidean_dense_dense (4-term groups, no fma)
+//   inertia          _k_means_common.pyx:92-121 (one OpenMP thread: sequential fp32)
+//   minibatch update _k_means_minibatch.pyx:59-108
+//   Lloyd M-step     _k_means_lloyd.pyx:111-160 (one OpenMP thread: sequential per cluster)
+//   average / shift  _k_means_common.pyx:215-251
+// Loop control, RNG draws and rare branches (reassignment, relocation) live in the host layer.
+#include <algorithm>
+#include <climits>
+
+#include "gdd_common.hpp"
+
+namespace gdd {
+namespace {
+
+using floatx16 = __attribute__((ext_vector_type(16))) float;
+
+// ---------------------------------------------------------------------------------------------
+// row norms in numpy einsum float32 SSE order (sum_of_products_contig_contig_outstride0_two):
+// 4 lanes; per 16-element block acc_l = x[12+l]^2 + acc_l, then x[8+l]^2, x[4+l]^2, x[l]^2
+// (separate mul and add); 4-element zero-padded tail blocks; result (a0+a1)+(a2+a3).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float npy_sumsq(const float* __restrict__ x, int dim) {
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  int j = 0;
+  for (; dim - j >= 16; j += 16) {
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      float t = x[j + 12 + l] * x[j + 12 + l] + a[l];
+      t = x[j + 8 + l] * x[j + 8 + l] + t;
+      t = x[j + 4 + l] * x[j + 4 + l] + t;
+      a[l] = x[j + l] * x[j + l] + t;
+    }
+  }
+  for (; j < dim; j += 4) {
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      float v = (j + l < dim) ? x[j + l] : 0.f;
+      a[l] = v * v + a[l];
+    }
+  }
+  return (a[0] + a[1]) + (a[2] + a[3]);
+}
+
+__global__ void k_row_norms(int64_t n, int dim, const float* __restrict__ X, float* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = npy_sumsq(X + i * dim, dim);
+}
+
+// sklearn _euclidean_dense_dense(a, b, n_features, squared=True): groups of 4 summed left to right,
+// added to the running result; remainder added one by one. Separate mul/add (no fma).
+__device__ __forceinline__ float skl_sqdist(const float* __restrict__ a, const float* __restrict__ b,
+                                            int dim) {
+  float r = 0.f;
+  int j = 0;
+  for (; j + 4 <= dim; j += 4) {
+    float d0 = a[j] - b[j], d1 = a[j + 1] - b[j + 1], d2 = a[j + 2] - b[j + 2],
+          d3 = a[j + 3] - b[j + 3];
+    r = r + (((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
+  }
+  for (; j < dim; ++j) {
+    float d0 = a[j] - b[j];
+    r = r + d0 * d0;
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// assignment: MFMA distance tiles + lexicographic (distance, index) argmin
+// ---------------------------------------------------------------------------------------------
+// (d, c) packed so that unsigned 64-bit order == lexicographic order on (d as float, c)
+__device__ __forceinline__ unsigned long long pack_key(float d, int c) {
+  unsigned u = __float_as_uint(d);
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)u << 32) | (unsigned)c;
+}
+
+__global__ void k_fill_u64(int64_t n, unsigned long long* p, unsigned long long v) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// One block = WAVES waves x 32 points; blockIdx.y = a chunk of `cch` centers. A wave computes the
+// 32x32 tile D[center][point] = sum_t C[center][t] * X[point][t] with dimp/2 chained
+// v_mfma_f32_32x32x2_f32 (lanes 0-31 feed feature 2s, lanes 32-63 feature 2s+1 of each step, so the
+// chain visits features in order 0,1,2,...). Lane l then holds point l&31 against the 16 centers
+// (r&3)+8(r>>2)+4(l>>5), r = 0..15, and keeps a running lexicographic minimum; the two half-waves
+// merge with one xor-shuffle and the block's result enters keys[] through a 64-bit atomicMin.
+// LDS rows use an odd stride (dimp+1 floats) so the 32 rows read by one ds_read_b32 hit 32 banks.
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_assign(int64_t n, int dim, int dimp,
+                                                       const float* __restrict__ X,
+                                                       const int64_t* __restrict__ rows, int k,
+                                                       const float* __restrict__ C,
+                                                       const float* __restrict__ cn2, int cch,
+                                                       unsigned long long* __restrict__ keys) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int kPts = 32 * WAVES;
+  const int S = dimp + 1;
+  const int c0 = blockIdx.y * cch;
+  const int nc = min(k, c0 + cch) - c0;
+  const int ncp = (nc + 31) & ~31;
+  float* Cl = lds;
+  float* Pl = Cl + (size_t)ncp * S;
+  float* Nl = Pl + (size_t)kPts * S;
+  const int tid = threadIdx.x;
+  const int64_t p0 = (int64_t)blockIdx.x * kPts;
+
+  for (int idx = tid; idx < kPts * dimp; idx += blockDim.x) {
+    const int r = idx / dimp, c = idx - r * dimp;
+    const int64_t pi = p0 + r;
+    float v = 0.f;
+    if (pi < n && c < dim) {
+      const int64_t src = rows ? rows[pi] : pi;
+      v = X[src * dim + c];
+    }
+    Pl[r * S + c] = v;
+  }
+  for (int idx = tid; idx < ncp * dimp; idx += blockDim.x) {
+    const int r = idx / dimp, c = idx - r * dimp;
+    Cl[r * S + c] = (r < nc && c < dim) ? C[(int64_t)(c0 + r) * dim + c] : 0.f;
+  }
+  for (int idx = tid; idx < ncp; idx += blockDim.x) Nl[idx] = idx < nc ? cn2[c0 + idx] : 0.f;
+  __syncthreads();
+
+  const int wave = tid >> 6, lane = tid & 63;
+  const int kh = lane >> 5;
+  const float* bp = Pl + (wave * 32 + (lane & 31)) * S + kh;
+  unsigned long long best = ~0ull;
+  for (int ct = 0; ct < ncp; ct += 32) {
+    const float* ap = Cl + (ct + (lane & 31)) * S + kh;
+    floatx16 acc = {};
+    for (int s2 = 0; s2 < dimp; s2 += 2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[s2], bp[s2], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ci = ct + (r & 3) + 8 * (r >> 2) + 4 * kh;
+      if (ci < nc) {
+        const float d = __builtin_fmaf(-2.f, acc[r], Nl[ci]);
+        const unsigned long long key = pack_key(d, c0 + ci);
+        best = key < best ? key : best;
+      }
+    }
+  }
+  const unsigned long long other = __shfl_xor(best, 32);
+  best = other < best ? other : best;
+  if (lane < 32) {
+    const int64_t pi = p0 + wave * 32 + lane;
+    if (pi < n && best != ~0ull) atomicMin(keys + pi, best);
+  }
+}
+
+__global__ void k_assign_finalize(int64_t n, int dim, const float* __restrict__ X,
+                                  const int64_t* __restrict__ rows, const float* __restrict__ C,
+                                  const unsigned long long* __restrict__ keys,
+                                  int32_t* __restrict__ labels, float* __restrict__ sq_dist) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long key = keys[i];
+  const int lab = (key == ~0ull) ? 0 : (int)(unsigned)(key & 0xffffffffull);
+  labels[i] = lab;
+  if (sq_dist) {
+    const int64_t src = rows ? rows[i] : i;
+    sq_dist[i] = skl_sqdist(X + src * dim, C + (int64_t)lab * dim, dim);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// inertia: sequential fp32 sum in sample order (one lane; the values are staged per 64 by the wave)
+// ---------------------------------------------------------------------------------------------
+__global__ void k_inertia(int64_t n, const float* __restrict__ sq, const float* __restrict__ w,
+                          float* __restrict__ out) {
+  __shared__ float buf[256];
+  float acc = 0.f;
+  for (int64_t b = 0; b < n; b += 256) {
+    const int64_t i = b + threadIdx.x;
+    if (i < n) buf[threadIdx.x] = w ? sq[i] * w[i] : sq[i] * 1.0f;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int m = (int)min<int64_t>(256, n - b);
+      for (int t = 0; t < m; ++t) acc = acc + buf[t];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = acc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// MiniBatchKMeans update (one wave per cluster)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, const float* __restrict__ X,
+                                                        const int64_t* __restrict__ rows,
+                                                        const float* __restrict__ w,
+                                                        const int32_t* __restrict__ labels, int k,
+                                                        const float* __restrict__ C_old,
+                                                        float* __restrict__ C_new,
+                                                        float* __restrict__ Wsum,
+                                                        int32_t* __restrict__ members_ws) {
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x;
+  int32_t* mem = members_ws + (int64_t)c * b;  // worst case: every batch sample in this cluster
+  int count = 0;
+  for (int64_t base = 0; base < b; base += 64) {
+    const int64_t i = base + lane;
+    const bool is = i < b && labels[i] == c;
+    const unsigned long long m = __ballot(is);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (is) mem[count + before] = (int32_t)i;
+    count += __popcll(m);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __syncthreads();
+  // wsum: sequential fp32 in batch order (update_center_dense :78-83)
+  float wsum = 0.f;
+  if (w) {
+    for (int t = 0; t < count; ++t) {
+      const int32_t i = mem[t];
+      wsum = wsum + w[i];
+    }
+  } else {
+    for (int t = 0; t < count; ++t) wsum = wsum + 1.0f;
+  }
+  const float W = Wsum[c];
+  const int64_t cb = (int64_t)c * dim;
+  if (wsum > 0.f) {
+    const float Wn = W + wsum;
+    const float alpha = 1.0f / Wn;  // Cython `1 / weight_sums[c]` with float operands
+    for (int f = lane; f < dim; f += 64) {
+      float acc = C_old[cb + f] * W;
+      for (int t = 0; t < count; ++t) {
+        const int32_t i = mem[t];
+        const int64_t src = rows ? rows[i] : (int64_t)i;
+        const float wi = w ? w[i] : 1.0f;
+        acc = acc + X[src * dim + f] * wi;
+      }
+      C_new[cb + f] = acc * alpha;
+    }
+    __syncthreads();
+    if (lane == 0) Wsum[c] = Wn;
+  } else {
+    for (int f = lane; f < dim; f += 64) C_new[cb + f] = C_old[cb + f];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// grouping: offsets from sorted labels
+// ---------------------------------------------------------------------------------------------
+__global__ void k_iota(int64_t n, int32_t* p) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = (int32_t)i;
+}
+
+__global__ void k_offsets(int64_t n, const int32_t* __restrict__ skeys, int k,
+                          int32_t* __restrict__ offsets) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  // offsets[c] = first sorted position with key >= c
+  const int prev = (i == 0) ? -1 : skeys[i - 1];
+  const int cur = (i == n) ? k : skeys[i];
+  for (int c = prev + 1; c <= cur && c <= k; ++c) offsets[c] = (int32_t)i;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Lloyd accumulation (sequential per cluster, sample order) and fixed-point variant
+// ---------------------------------------------------------------------------------------------
+__global__ void k_segment_sum_f32(int dim, const float* __restrict__ X, const float* __restrict__ w,
+                                  const int32_t* __restrict__ perm,
+                                  const int32_t* __restrict__ offsets, float* __restrict__ sums,
+                                  float* __restrict__ wsum) {
+  const int c = blockIdx.x;
+  const int32_t b = offsets[c], e = offsets[c + 1];
+  for (int f = threadIdx.x; f < dim; f += blockDim.x) {
+    float acc = 0.f;
+    for (int32_t t = b; t < e; ++t) {
+      const int32_t i = perm[t];
+      acc = acc + X[(int64_t)i * dim + f] * (w ? w[i] : 1.0f);
+    }
+    sums[(int64_t)c * dim + f] = acc;
+  }
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int32_t t = b; t < e; ++t) s = s + (w ? w[perm[t]] : 1.0f);
+    wsum[c] = s;
+  }
+}
+
+__global__ void k_segment_sum_fixed(int64_t n, int dim, const float* __restrict__ X,
+                                    const float* __restrict__ w, const int32_t* __restrict__ labels,
+                                    int scale_exp, long long* __restrict__ sums,
+                                    long long* __restrict__ counts) {
+  const int64_t total = n * dim;
+  const double sc = ldexp(1.0, scale_exp);
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / dim;
+    const int f = (int)(t - i * dim);
+    const int c = labels[i];
+    const double v = (double)X[t] * (double)(w ? w[i] : 1.0f) * sc;
+    atomicAdd((unsigned long long*)(sums + (int64_t)c * dim + f),
+              (unsigned long long)(long long)__builtin_rint(v));
+    if (f == 0) atomicAdd((unsigned long long*)(counts + c), 1ull);
+  }
+}
+
+__global__ void k_fixed_to_centers(int k, int dim, const long long* __restrict__ sums,
+                                   const long long* __restrict__ counts, int scale_exp,
+                                   float* __restrict__ C) {
+  const int64_t total = (int64_t)k * dim;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(t / dim);
+    const long long cnt = counts[c];
+    if (cnt > 0) C[t] = (float)(ldexp((double)sums[t], -scale_exp) / (double)cnt);
+  }
+}
+
+// _average_centers + _center_shift, one block per cluster
+__global__ void k_average_centers(int k, int dim, float* __restrict__ C_new,
+                                  const float* __restrict__ wsum, const float* __restrict__ C_old,
+                                  float* __restrict__ shift, int argmax_w) {
+  const int c = blockIdx.x;
+  const float wc = wsum[c];
+  const int64_t cb = (int64_t)c * dim;
+  if (wc > 0.f) {
+    const float alpha = (float)(1.0 / (double)wc);  // `1.0 / weight` is a C double division
+    for (int f = threadIdx.x; f < dim; f += blockDim.x) C_new[cb + f] = C_new[cb + f] * alpha;
+  } else {
+    // sklearn copies centers[argmax_weight] (already averaged or not, by loop order); the host only
+    // takes this path after relocation left no empty cluster, so it is effectively unreachable
+    const int64_t ab = (int64_t)argmax_w * dim;
+    for (int f = threadIdx.x; f < dim; f += blockDim.x) C_new[cb + f] = C_new[ab + f];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && shift) shift[c] = sqrtf(skl_sqdist(C_new + cb, C_old + cb, dim));
+}
+
+__global__ void k_point_center_sqdist(int64_t n, int dim, const float* __restrict__ X,
+                                      const int32_t* __restrict__ labels,
+                                      const float* __restrict__ C, float* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = skl_sqdist(X + i * dim, C + (int64_t)labels[i] * dim, dim);
+}
+
+__global__ void k_labels_changed(int64_t n, const int32_t* __restrict__ labels,
+                                 int32_t* __restrict__ old, int32_t* __restrict__ changed) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t a = labels[i];
+  if (a != old[i]) {
+    *changed = 1;
+    old[i] = a;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// cluster feature mean (fp64 sequential per cluster, sample order) and row argmax
+// ---------------------------------------------------------------------------------------------
+__global__ void k_cluster_mean(int d, const float* __restrict__ feat, const int32_t* __restrict__ perm,
+                               const int32_t* __restrict__ offsets, int empty_as_zero,
+                               float* __restrict__ out, long long* __restrict__ counts) {
+  const int c = blockIdx.y;
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t b = offsets[c], e = offsets[c + 1];
+  if (f == 0 && counts) counts[c] = e - b;
+  if (f >= d) return;
+  double acc = 0.0;
+  int32_t t = b;
+  // 4 independent gathers in flight ahead of the (ordered) fp64 adds
+  for (; t + 4 <= e; t += 4) {
+    const float v0 = feat[(int64_t)perm[t] * d + f];
+    const float v1 = feat[(int64_t)perm[t + 1] * d + f];
+    const float v2 = feat[(int64_t)perm[t + 2] * d + f];
+    const float v3 = feat[(int64_t)perm[t + 3] * d + f];
+    acc = acc + (double)v0;
+    acc = acc + (double)v1;
+    acc = acc + (double)v2;
+    acc = acc + (double)v3;
+  }
+  for (; t < e; ++t) acc = acc + (double)feat[(int64_t)perm[t] * d + f];
+  const int32_t cnt = e - b;
+  float r;
+  if (cnt == 0)
+    r = empty_as_zero ? 0.f : __builtin_nanf("");
+  else
+    r = (float)(acc / (double)cnt);
+  out[(int64_t)c * d + f] = r;
+}
+
+__global__ void k_argmax_rows(int k, int dim, const float* __restrict__ C, int64_t* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= k) return;
+  const float* r = C + (int64_t)c * dim;
+  int best = 0;
+  float bv = r[0];
+  for (int j = 1; j < dim; ++j) {
+    const float v = r[j];
+    if (v > bv || (v != v && bv == bv)) {  // torch.argmax: NaN counts as the maximum
+      bv = v;
+      best = j;
+    }
+  }
+  out[c] = best;
+}
+
+inline unsigned blocks_for(int64_t n, int t = 256) { return (unsigned)((n + t - 1) / t); }
+
+}  // namespace
+}  // namespace gdd
+
+using namespace gdd;
+
+// -------------------------------------------------------------------------------------------------
+extern "C" int gdd_row_norms(int64_t n, int dim, const float* X, float* out, gdd_stream_t stream) {
+  GDD_REQUIRE(n >= 0 && dim > 0 && (n == 0 || (X && out)), "row_norms: bad arguments");
+  if (n == 0) return GDD_OK;
+  k_row_norms<<<blocks_for(n), 256, 0, to_hip(stream)>>>(n, dim, X, out);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+namespace {
+// LDS bytes of k_assign for a given geometry
+size_t assign_lds(int waves, int dimp, int cch) {
+  const int S = dimp + 1;
+  const int ncp = (cch + 31) & ~31;
+  return sizeof(float) * ((size_t)ncp * S + (size_t)32 * waves * S + ncp);
+}
+}  // namespace
+
+extern "C" size_t gdd_kmeans_assign_ws_bytes(int64_t n) {
+  return align256(sizeof(unsigned long long) * (size_t)std::max<int64_t>(n, 1));
+}
+
+extern "C" int gdd_kmeans_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k,
+                                 const float* C, const float* c_norm2, int32_t* labels,
+                                 float* sq_dist, void* ws, size_t ws_bytes, gdd_stream_t stream) {
+  GDD_REQUIRE(n >= 0 && dim > 0 && dim <= 512 && k > 0, "assign: n=%lld dim=%d k=%d unsupported",
+              (long long)n, dim, k);
+  GDD_REQUIRE(n == 0 || (X && C && c_norm2 && labels && ws), "assign: null pointer");
+  if (n == 0) return GDD_OK;
+  if (ws_bytes < gdd_kmeans_assign_ws_bytes(n))
+    return fail(GDD_E_WORKSPACE, "assign: workspace %zu too small", ws_bytes);
+  hipStream_t s = to_hip(stream);
+  unsigned long long* keys = static_cast<unsigned long long*>(ws);
+  const int dimp = (dim + 1) & ~1;
+  const int waves = dimp <= 96 ? 4 : (dimp <= 224 ? 2 : 1);
+  const int64_t gx = (n + 32 * waves - 1) / (32 * waves);
+  // centers per block: as many as fit the LDS budget (>= 32), then fewer while the grid is too
+  // small to occupy 256 CUs (minibatch batches have only ~8 point tiles)
+  const size_t budget = dimp <= 224 ? 65536 : 160000;
+  const int kp = (k + 31) & ~31;
+  int cch = 32;
+  while (cch + 32 <= kp && assign_lds(waves, dimp, cch + 32) <= budget) cch += 32;
+  int64_t gy = (k + cch - 1) / cch;
+  while (gx * gy < 1024 && cch > 32) {
+    cch -= 32;
+    gy = (k + cch - 1) / cch;
+  }
+  GDD_REQUIRE(gx < (1ll << 31) && gy < 65536, "assign: grid too large");
+  const size_t lds = assign_lds(waves, dimp, cch);
+  k_fill_u64<<<blocks_for(n), 256, 0, s>>>(n, keys, ~0ull);
+  GDD_LAUNCHED();
+  dim3 grid((unsigned)gx, (unsigned)gy);
+  if (lds > 65536) {
+    // gfx950 has 160 KiB of LDS per CU; opt the kernel in to more than the 64 KiB default
+    if (waves == 2)
+      GDD_HIP(hipFuncSetAttribute((const void*)k_assign<2>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    else if (waves == 1)
+      GDD_HIP(hipFuncSetAttribute((const void*)k_assign<1>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  }
+  if (waves == 4)
+    k_assign<4><<<grid, 256, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys);
+  else if (waves == 2)
+    k_assign<2><<<grid, 128, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys);
+  else
+    k_assign<1><<<grid, 64, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys);
+  GDD_LAUNCHED();
+  k_assign_finalize<<<blocks_for(n), 256, 0, s>>>(n, dim, X, rows, C, keys, labels, sq_dist);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" int gdd_inertia(int64_t n, const float* sq_dist, const float* w, float* out,
+                           gdd_stream_t stream) {
+  GDD_REQUIRE(n >= 0 && out && (n == 0 || sq_dist), "inertia: bad arguments");
+  k_inertia<<<1, 256, 0, to_hip(stream)>>>(n, sq_dist, w, out);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" size_t gdd_minibatch_update_ws_bytes(int64_t b, int k) {
+  return align256(sizeof(int32_t) * (size_t)std::max<int64_t>(b, 1) * (size_t)std::max(k, 1));
+}
+
+extern "C" int gdd_minibatch_update(int64_t b, int dim, const float* X, const int64_t* rows,
+                                    const float* w, const int32_t* labels, int k,
+                                    const float* C_old, float* C_new, float* weight_sums, void* ws,
+                                    size_t ws_bytes, gdd_stream_t stream) {
+  GDD_REQUIRE(b > 0 && dim > 0 && k > 0, "minibatch_update: bad shape");
+  GDD_REQUIRE(X && labels && C_old && C_new && weight_sums && ws, "minibatch_update: null pointer");
+  GDD_REQUIRE(C_old != C_new, "minibatch_update: C_old and C_new must differ");
+  if (ws_bytes < gdd_minibatch_update_ws_bytes(b, k))
+    return fail(GDD_E_WORKSPACE, "minibatch_update: workspace too small");
+  k_minibatch_update<<<k, 64, 0, to_hip(stream)>>>(b, dim, X, rows, w, labels, k, C_old, C_new,
+                                                   weight_sums, static_cast<int32_t*>(ws));
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" size_t gdd_group_ws_bytes(int64_t n, int k) {
+  (void)k;
+  return align256(sizeof(int32_t) * (size_t)n) * 2 + sort_pairs_ws_bytes(n) + 1024;
+}
+
+extern "C" int gdd_group_by_label(int64_t n, const int32_t* labels, int k, int32_t* perm,
+                                  int32_t* offsets, void* ws, size_t ws_bytes,
+                                  gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && k > 0 && labels && perm && offsets && ws, "group_by_label: bad arguments");
+  hipStream_t s = to_hip(stream);
+  Carver cv(ws, ws_bytes);
+  int32_t* iota = cv.take<int32_t>(n);
+  int32_t* skeys = cv.take<int32_t>(n);
+  size_t sb = sort_pairs_ws_bytes(n);
+  void* sws = cv.take<char>(sb);
+  if (!cv.ok()) return fail(GDD_E_WORKSPACE, "group_by_label: workspace too small");
+  int bits = 1;
+  while ((1ll << bits) < (long long)k) ++bits;
+  k_iota<<<blocks_for(n), 256, 0, s>>>(n, iota);
+  GDD_LAUNCHED();
+  int rc = sort_pairs_i32(labels, skeys, iota, perm, n, bits, sws, sb, s);
+  if (rc) return rc;
+  k_offsets<<<blocks_for(n + 1), 256, 0, s>>>(n, skeys, k, offsets);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" int gdd_segment_sum_f32(int64_t n, int dim, const float* X, const float* w,
+                                   const int32_t* perm, const int32_t* offsets, int k, float* sums,
+                                   float* wsum, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && dim > 0 && k > 0 && X && perm && offsets && sums && wsum,
+              "segment_sum_f32: bad arguments");
+  k_segment_sum_f32<<<k, 64, 0, to_hip(stream)>>>(dim, X, w, perm, offsets, sums, wsum);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" int gdd_segment_sum_fixed(int64_t n, int dim, const float* X, const float* w,
+                                     const int32_t* labels, int k, int scale_exp,
+                                     long long* sums_fx, long long* counts, gdd_stream_t stream) {
+  GDD_REQUIRE(n >= 0 && dim > 0 && k > 0 && sums_fx && counts, "segment_sum_fixed: bad arguments");
+  if (n == 0) return GDD_OK;
+  GDD_REQUIRE(X && labels, "segment_sum_fixed: null pointer");
+  const int64_t total = n * dim;
+  const unsigned g = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
+  k_segment_sum_fixed<<<g, 256, 0, to_hip(stream)>>>(n, dim, X, w, labels, scale_exp, sums_fx,
+                                                     counts);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" int gdd_fixed_to_centers(int k, int dim, const long long* sums_fx,
+                                    const long long* counts, int scale_exp, float* centers,
+                                    gdd_stream_t stream) {
+  GDD_REQUIRE(k > 0 && dim > 0 && sums_fx && counts && centers, "fixed_to_centers: bad arguments");
+  const int64_t total = (int64_t)k * dim;
+  k_fixed_to_centers<<<blocks_for(total), 256, 0, to_hip(stream)>>>(k, dim, sums_fx, counts,
+                                                                    scale_exp, centers);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" int gdd_average_centers(int k, int dim, float* C_new, const float* wsum,
+                                   const float* C_old, float* center_shift, gdd_stream_t stream) {
+  GDD_REQUIRE(k > 0 && dim > 0 && C_new && wsum && C_old, "average_centers: bad arguments");
+  k_average_centers<<<k, 64, 0, to_hip(stream)>>>(k, dim, C_new, wsum, C_old, center_shift, 0);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" int gdd_point_center_sqdist(int64_t n, int dim, const float* X, const int32_t* labels,
+                                       const float* C, float* out, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && dim > 0 && X && labels && C && out, "point_center_sqdist: bad arguments");
+  k_point_center_sqdist<<<blocks_for(n), 256, 0, to_hip(stream)>>>(n, dim, X, labels, C, out);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" int gdd_labels_changed(int64_t n, const int32_t* labels, int32_t* labels_old,
+                                  int32_t* changed, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && labels && labels_old && changed, "labels_changed: bad arguments");
+  hipStream_t s = to_hip(stream);
+  GDD_HIP(hipMemsetAsync(changed, 0, sizeof(int32_t), s));
+  k_labels_changed<<<blocks_for(n), 256, 0, s>>>(n, labels, labels_old, changed);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" int gdd_cluster_mean(int64_t n, int d, const float* feat, const int32_t* perm,
+                                const int32_t* offsets, int k, int empty_as_zero, float* feat_syn,
+                                long long* counts, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && d > 0 && k > 0 && feat && perm && offsets && feat_syn,
+              "cluster_mean: bad arguments");
+  GDD_REQUIRE(k < 65536, "cluster_mean: k=%d too large", k);
+  dim3 grid((unsigned)((d + 127) / 128), (unsigned)k);
+  k_cluster_mean<<<grid, 128, 0, to_hip(stream)>>>(d, feat, perm, offsets, empty_as_zero, feat_syn,
+                                                   counts);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" int gdd_argmax_rows(int k, int dim, const float* centers, int64_t* out,
+                               gdd_stream_t stream) {
+  GDD_REQUIRE(k > 0 && dim > 0 && centers && out, "argmax_rows: bad arguments");
+  k_argmax_rows<<<blocks_for(k), 256, 0, to_hip(stream)>>>(k, dim, centers, out);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}

@@ -1,0 +1,241 @@
+// gdd_normalize.hip — (a2) Â = D^-1/2 (A + I) D^-1/2 on a canonical CSR, on the device.
+//
+// Restates deep_robust_utils.normalize_adj (ClustGDD/deep_robust_utils.py:180-207) as called through
+// normalize_adj_tensor(adj, sparse=True) (:245-256):
+//   * I is added iff A[0,0] == 0 (:199-200) unless the caller forces it; adding it promotes the
+//     matrix to float64 (sp.eye), so row sums, r = rowsum^-1/2 (inf -> 0, :201-202) and both
+//     diagonal scalings run in fp64 and the result is rounded to fp32 once
+//     (sparse_mx_to_torch_sparse_tensor, :391);
+//   * without I the matrix stays float32 and the same steps run in fp32;
+//   * value(i,j) = (r_i * a'_ij) * r_j — two rounded products, the order of scipy's two csr_matmat
+//     calls (r_mat_inv.dot(mx), then .dot(r_mat_inv)); exact zeros are dropped as csr_matmat does.
+// HBM layout: rowptr int32[n+1], col int32[nnz], val fp32[nnz] in; the same (+ diagonal) out.
+// Kernels: probe (A[0,0]) -> row scale r -> per-row output counts -> scan -> fill.
+// The fill and count kernels give 16 lanes to a row and compact with a group prefix sum, so the
+// col/val streams are read and written coalesced.
+#include "gdd_common.hpp"
+
+namespace gdd {
+namespace {
+
+constexpr int kGroup = 16;  // lanes per row in count/fill
+
+__global__ void k_probe(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                        const float* __restrict__ val, int self_loops, int32_t* flag) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (self_loops >= 0) {
+    *flag = self_loops;
+    return;
+  }
+  float a00 = 0.f;  // absent entry reads as 0 (lil mx[0, 0])
+  for (int32_t e = rowptr[0]; e < rowptr[1]; ++e) {
+    if (col[e] == 0) {
+      a00 = val ? val[e] : 1.f;
+      break;
+    }
+    if (col[e] > 0) break;
+  }
+  *flag = (a00 == 0.f) ? 1 : 0;
+}
+
+// r_i = rowsum_i^-1/2 (inf -> 0). fp64 path keeps r in r64, fp32 path in r32.
+__global__ void k_row_scale(int64_t n, const int32_t* __restrict__ rowptr,
+                            const int32_t* __restrict__ col, const float* __restrict__ val,
+                            const int32_t* __restrict__ flag, double* __restrict__ r64,
+                            float* __restrict__ r32) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int add = *flag;
+  const int32_t s = rowptr[i], e = rowptr[i + 1];
+  if (add) {
+    double deg;
+    if (!val) {
+      deg = (double)(e - s) + 1.0;  // binary: a_ii+1 or inserted 1 — integer sum, exact
+    } else {
+      // sequential fp64 sum in column order of row i of (A + I) (scipy csr_matvec order)
+      deg = 0.0;
+      bool diag_done = false;
+      for (int32_t p = s; p < e; ++p) {
+        int32_t j = col[p];
+        if (!diag_done && j >= i) {
+          if (j == i) {
+            deg = deg + ((double)val[p] + 1.0);
+            diag_done = true;
+            continue;
+          }
+          deg = deg + 1.0;
+          diag_done = true;
+        }
+        deg = deg + (double)val[p];
+      }
+      if (!diag_done) deg = deg + 1.0;
+    }
+    double r = cr_rsqrt(deg);
+    r64[i] = __builtin_isinf(r) ? 0.0 : r;
+  } else {
+    float deg = 0.f;
+    if (!val) {
+      deg = (float)(e - s);
+    } else {
+      for (int32_t p = s; p < e; ++p) deg = deg + val[p];
+    }
+    float r = (float)cr_rsqrt((double)deg);
+    r32[i] = __builtin_isinf(r) ? 0.f : r;
+  }
+}
+
+// value of stored entry (i, j) after scaling, exactly as scipy computes it
+struct Scaled {
+  float v;
+  bool keep;
+};
+
+__device__ __forceinline__ Scaled scaled_value(int add, int64_t i, int32_t j, float a,
+                                               const double* __restrict__ r64,
+                                               const float* __restrict__ r32) {
+  Scaled out;
+  if (add) {
+    double v = (double)a + ((j == i) ? 1.0 : 0.0);
+    double t = r64[i] * v;  // r_mat_inv.dot(mx)   (zero results dropped)
+    double u = t * r64[j];  // (.).dot(r_mat_inv)  (zero results dropped)
+    out.keep = (t != 0.0) && (u != 0.0);
+    out.v = (float)u;
+  } else {
+    float t = r32[i] * a;
+    float u = t * r32[j];
+    out.keep = (t != 0.f) && (u != 0.f);
+    out.v = u;
+  }
+  return out;
+}
+
+// inclusive prefix sum over a 16-lane group
+__device__ __forceinline__ int group_incl_scan(int x, int lane) {
+#pragma unroll
+  for (int o = 1; o < kGroup; o <<= 1) {
+    int y = __shfl_up(x, o, kGroup);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
+// Emits (or counts, when col_out == nullptr) the output entries of one row. The missing diagonal
+// of (A + I) is inserted before the first stored column > i, or appended.
+template <bool kFill>
+__global__ void k_rows_emit(int64_t n, const int32_t* __restrict__ rowptr,
+                            const int32_t* __restrict__ col, const float* __restrict__ val,
+                            const int32_t* __restrict__ flag, const double* __restrict__ r64,
+                            const float* __restrict__ r32, int32_t* __restrict__ cnt,
+                            const int32_t* __restrict__ rowptr_out, int32_t* __restrict__ col_out,
+                            float* __restrict__ val_out) {
+  const int lane = threadIdx.x & (kGroup - 1);
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kGroup;
+  if (i >= n) return;  // whole group exits together
+  const int add = *flag;
+  const int32_t s = rowptr[i], e = rowptr[i + 1];
+  int32_t base = kFill ? rowptr_out[i] : 0;
+  int32_t written = 0;
+  bool diag_pending = add != 0;  // becomes false once the diagonal has been accounted for
+  for (int32_t c0 = s; c0 < e; c0 += kGroup) {
+    int32_t p = c0 + lane;
+    bool in = p < e;
+    int32_t j = in ? col[p] : 0x7fffffff;
+    float a = in ? (val ? val[p] : 1.f) : 0.f;
+    int32_t jprev = (p > s && p - 1 < e) ? col[p - 1] : -1;
+    // the stored diagonal absorbs the +1; a missing one is emitted before the first j > i
+    if (diag_pending) {
+      unsigned long long has = __ballot(in && j == i);
+      if (has & (0xffffull << (threadIdx.x & 48))) diag_pending = false;
+    }
+    bool emit_diag = diag_pending && in && j > i && jprev < i;
+    Scaled sv = in ? scaled_value(add, i, j, a, r64, r32) : Scaled{0.f, false};
+    Scaled dv = emit_diag ? scaled_value(add, i, (int32_t)i, 0.f, r64, r32) : Scaled{0.f, false};
+    int mine = (int)sv.keep + (int)dv.keep;
+    int incl = group_incl_scan(mine, lane);
+    int total = __shfl(incl, kGroup - 1, kGroup);
+    if (kFill) {
+      int32_t pos = base + written + incl - mine;
+      if (dv.keep) {
+        col_out[pos] = (int32_t)i;
+        val_out[pos] = dv.v;
+        ++pos;
+      }
+      if (sv.keep) {
+        col_out[pos] = j;
+        val_out[pos] = sv.v;
+      }
+    }
+    written += total;
+    if (diag_pending && __ballot(emit_diag) & (0xffffull << (threadIdx.x & 48)))
+      diag_pending = false;
+  }
+  if (diag_pending) {  // every stored column < i (or empty row): append the diagonal
+    Scaled dv = scaled_value(add, i, (int32_t)i, 0.f, r64, r32);
+    if (dv.keep) {
+      if (kFill && lane == 0) {
+        col_out[base + written] = (int32_t)i;
+        val_out[base + written] = dv.v;
+      }
+      written += 1;
+    }
+  }
+  if (!kFill && lane == 0) cnt[i] = written;
+}
+
+__global__ void k_set_last(int64_t n, const int32_t* __restrict__ cnt, int32_t* rowptr_out) {
+  // rowptr_out holds the exclusive scan of cnt; close it with the total
+  if (threadIdx.x == 0 && blockIdx.x == 0) rowptr_out[n] = rowptr_out[n - 1] + cnt[n - 1];
+}
+
+}  // namespace
+}  // namespace gdd
+
+using namespace gdd;
+
+extern "C" size_t gdd_normalize_ws_bytes(int64_t n, int64_t nnz) {
+  (void)nnz;
+  size_t b = 256;                               // flag
+  b += align256(sizeof(double) * (size_t)n);    // r64
+  b += align256(sizeof(float) * (size_t)n);     // r32
+  b += align256(sizeof(int32_t) * (size_t)n);   // cnt
+  b += scan_i32_ws_bytes(n) + 256;
+  return b;
+}
+
+extern "C" int gdd_normalize_csr(int64_t n, int64_t nnz, const int32_t* rowptr,
+                                 const int32_t* col, const float* val, int self_loops,
+                                 int32_t* rowptr_out, int32_t* col_out, float* val_out, void* ws,
+                                 size_t ws_bytes, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && n < INT32_MAX, "normalize: n=%lld out of range", (long long)n);
+  GDD_REQUIRE(nnz >= 0 && nnz + n < INT32_MAX, "normalize: nnz=%lld out of range",
+              (long long)nnz);
+  GDD_REQUIRE(rowptr && rowptr_out && col_out && val_out && ws, "normalize: null pointer");
+  GDD_REQUIRE(nnz == 0 || col, "normalize: null col");
+  GDD_REQUIRE(self_loops >= -1 && self_loops <= 1, "normalize: self_loops must be -1, 0 or 1");
+  hipStream_t s = to_hip(stream);
+  Carver cv(ws, ws_bytes);
+  int32_t* flag = cv.take<int32_t>(1);
+  double* r64 = cv.take<double>(n);
+  float* r32 = cv.take<float>(n);
+  int32_t* cnt = cv.take<int32_t>(n);
+  size_t scan_bytes = scan_i32_ws_bytes(n);
+  void* scan_ws = cv.take<char>(scan_bytes);
+  if (!cv.ok()) return fail(GDD_E_WORKSPACE, "normalize: workspace %zu too small", ws_bytes);
+
+  k_probe<<<1, 64, 0, s>>>(rowptr, col, val, self_loops, flag);
+  GDD_LAUNCHED();
+  k_row_scale<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(n, rowptr, col, val, flag, r64, r32);
+  GDD_LAUNCHED();
+  const unsigned grid = (unsigned)((n * kGroup + 255) / 256);
+  k_rows_emit<false><<<grid, 256, 0, s>>>(n, rowptr, col, val, flag, r64, r32, cnt, nullptr,
+                                          nullptr, nullptr);
+  GDD_LAUNCHED();
+  int rc = exclusive_scan_i32(cnt, rowptr_out, n, scan_ws, scan_bytes, s);
+  if (rc) return rc;
+  k_set_last<<<1, 64, 0, s>>>(n, cnt, rowptr_out);
+  GDD_LAUNCHED();
+  k_rows_emit<true><<<grid, 256, 0, s>>>(n, rowptr, col, val, flag, r64, r32, cnt, rowptr_out,
+                                         col_out, val_out);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}

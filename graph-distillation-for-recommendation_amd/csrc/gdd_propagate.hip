@@ -1,0 +1,364 @@
+// gdd_propagate.hip — (a3) k-hop feature propagation over a normalised CSR adjacency.
+//
+// Restates the loop of ClustGDD/clustgdd_agent_transduct.py:59-65 (same loop three times in
+// clustgdd_agent_induct.py:72-94):
+//     t = 0       : p = X;                    target = fp32(1-alpha) * X
+//     t = 1..T-1  : p = (fp32(alpha) * Â) @ p; target = target + fp32(1-alpha) * p
+// `alpha*adj_norm` scales the stored values in fp32 (fp32(alpha) * v, rounded) before the SpMM;
+// `(1-alpha)` is a Python double rounded to fp32 when it multiplies the fp32 tensor.
+//
+// Canonical summation order (the reference's cuSPARSE/torch-CPU order is unspecified, so parity
+// with it is a tolerance; parity with oracle/ is bit-exact): the stored entries of a row, in CSR
+// order, are cut into segments of GDD_PROP_SEG; a segment is an fp32 fma chain from +0; segment
+// partials are added left to right.
+//
+// Work decomposition: one work item per row segment (short rows = one item, hub rows several), a
+// group of G lanes per item, each lane owning V consecutive features (float4/float2/float loads
+// of the neighbour rows of p), grid.y walking d in chunks of G*V features. Column indices and
+// values are read cooperatively (one coalesced load per G entries) and broadcast with shuffles;
+// neighbour-row gathers are issued kUnroll at a time ahead of the dependent fma chain. Rows that
+// fit one segment write p and update target in the epilogue; split rows write partials that a
+// second kernel folds in order.
+#include <algorithm>
+
+#include "gdd_common.hpp"
+
+namespace gdd {
+namespace {
+
+constexpr int kSeg = GDD_PROP_SEG;
+constexpr int kUnroll = 8;
+
+struct Item {
+  int32_t row, begin, end, pslot;  // pslot < 0: the item is the whole row
+};
+
+template <int V>
+struct VecT;
+template <>
+struct VecT<4> {
+  using T = float4;
+};
+template <>
+struct VecT<2> {
+  using T = float2;
+};
+template <>
+struct VecT<1> {
+  using T = float;
+};
+
+template <int V>
+__device__ __forceinline__ void vload(const float* p, float (&r)[V]) {
+  if constexpr (V == 4) {
+    float4 t = *reinterpret_cast<const float4*>(p);
+    r[0] = t.x; r[1] = t.y; r[2] = t.z; r[3] = t.w;
+  } else if constexpr (V == 2) {
+    float2 t = *reinterpret_cast<const float2*>(p);
+    r[0] = t.x; r[1] = t.y;
+  } else {
+    r[0] = *p;
+  }
+}
+template <int V>
+__device__ __forceinline__ void vstore(float* p, const float (&r)[V]) {
+  if constexpr (V == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(r[0], r[1], r[2], r[3]);
+  } else if constexpr (V == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(r[0], r[1]);
+  } else {
+    *p = r[0];
+  }
+}
+
+// ---- plan: per-row segment counts -> item offsets / partial offsets -> item records ----------
+__global__ void k_seg_counts(int64_t n, const int32_t* __restrict__ rowptr, int32_t* nseg,
+                             int32_t* npart) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int32_t len = rowptr[i + 1] - rowptr[i];
+  int32_t s = len <= kSeg ? 1 : (len + kSeg - 1) / kSeg;
+  nseg[i] = s;
+  npart[i] = s > 1 ? s : 0;
+}
+
+__global__ void k_make_items(int64_t n, const int32_t* __restrict__ rowptr,
+                             const int32_t* __restrict__ nseg, const int32_t* __restrict__ item_off,
+                             const int32_t* __restrict__ part_off, Item* items,
+                             int32_t* long_rows, int32_t* long_off, int32_t* counts) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t b = rowptr[i], e = rowptr[i + 1], s = nseg[i], o = item_off[i];
+  if (s == 1) {
+    items[o] = Item{(int32_t)i, b, e, -1};
+  } else {
+    const int32_t po = part_off[i];
+    for (int32_t k = 0; k < s; ++k) {
+      int32_t lo = b + k * kSeg, hi = min(e, lo + kSeg);
+      items[o + k] = Item{(int32_t)i, lo, hi, po + k};
+    }
+    // list of split rows for the fixup pass; list order is irrelevant (each entry is independent)
+    int32_t r = atomicAdd(&counts[1], 1);
+    long_rows[r] = (int32_t)i;
+    long_off[r] = po;
+  }
+  if (i == n - 1) counts[0] = o + s;  // number of items
+}
+
+// ---- one hop -----------------------------------------------------------------------------------
+template <int V, int G>
+__global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
+                                             const int32_t* __restrict__ counts,
+                                             const int32_t* __restrict__ col,
+                                             const float* __restrict__ val, float scale, int d,
+                                             const float* __restrict__ x, float* __restrict__ y,
+                                             float* __restrict__ acc_out, float acc_scale,
+                                             float* __restrict__ partials) {
+  const int lane = threadIdx.x & (G - 1);
+  const int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  if (g >= counts[0]) return;
+  const Item it = items[g];
+  const int f = (blockIdx.y * G + lane) * V;
+  const bool fa = f < d;
+  float acc[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) acc[v] = 0.f;
+
+  for (int32_t c0 = it.begin; c0 < it.end; c0 += G) {
+    const int32_t p = c0 + lane;
+    const bool in = p < it.end;
+    const int32_t cj = in ? col[p] : 0;
+    const float vj = in ? scale * val[p] : 0.f;  // fp32(alpha) * v, rounded (agent :64)
+    const int cnt = min(G, it.end - c0);
+    for (int t = 0; t < cnt; t += kUnroll) {
+      float xv[kUnroll][V];
+      float vv[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int src = t + u;
+        const int32_t jj = __shfl(cj, src < G ? src : 0, G);
+        vv[u] = __shfl(vj, src < G ? src : 0, G);
+        if (src < cnt && fa) {
+          vload<V>(x + (int64_t)jj * d + f, xv[u]);
+        } else {
+#pragma unroll
+          for (int v = 0; v < V; ++v) xv[u][v] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        if (t + u < cnt) {
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[v] = __builtin_fmaf(vv[u], xv[u][v], acc[v]);
+        }
+      }
+    }
+  }
+  if (!fa) return;
+  if (it.pslot < 0) {
+    const int64_t o = (int64_t)it.row * d + f;
+    vstore<V>(y + o, acc);
+    if (acc_out) {
+      float t[V];
+      vload<V>(acc_out + o, t);
+#pragma unroll
+      for (int v = 0; v < V; ++v) t[v] = t[v] + acc_scale * acc[v];  // two roundings (agent :65)
+      vstore<V>(acc_out + o, t);
+    }
+  } else {
+    vstore<V>(partials + (int64_t)it.pslot * d + f, acc);
+  }
+}
+
+// fold the partials of split rows left to right, then the same epilogue
+__global__ void k_fixup(const int32_t* __restrict__ counts, const int32_t* __restrict__ long_rows,
+                        const int32_t* __restrict__ long_off, const int32_t* __restrict__ rowptr,
+                        int d, const float* __restrict__ partials, float* __restrict__ y,
+                        float* __restrict__ acc_out, float acc_scale) {
+  const int r = blockIdx.x;
+  if (r >= counts[1]) return;
+  const int32_t row = long_rows[r], po = long_off[r];
+  const int32_t len = rowptr[row + 1] - rowptr[row];
+  const int32_t s = (len + kSeg - 1) / kSeg;
+  for (int f = threadIdx.x; f < d; f += blockDim.x) {
+    float sum = partials[(int64_t)po * d + f];
+    for (int32_t k = 1; k < s; ++k) sum = sum + partials[(int64_t)(po + k) * d + f];
+    const int64_t o = (int64_t)row * d + f;
+    y[o] = sum;
+    if (acc_out) acc_out[o] = acc_out[o] + acc_scale * sum;
+  }
+}
+
+__global__ void k_scale_copy(int64_t total, const float* __restrict__ x, float w,
+                             float* __restrict__ target, float* __restrict__ copy) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < total; i += stride) {
+    float v = x[i];
+    target[i] = w * v;
+    if (copy) copy[i] = v;
+  }
+}
+
+// ---- dispatch ----------------------------------------------------------------------------------
+struct Plan {
+  Item* items;
+  int32_t* counts;  // [0] items, [1] long rows
+  int32_t* long_rows;
+  int32_t* long_off;
+  float* partials;
+  int64_t max_items;
+  int64_t max_long;
+};
+
+inline int64_t max_items_for(int64_t n, int64_t nnz) { return n + nnz / kSeg + 1; }
+inline int64_t max_parts_for(int64_t nnz) { return 2 * (nnz / kSeg) + 2; }
+
+size_t plan_ws_bytes(int64_t n, int64_t nnz, int d) {
+  size_t b = 0;
+  b += align256(sizeof(int32_t) * n) * 4;                // nseg, npart, item_off, part_off
+  b += align256(sizeof(Item) * max_items_for(n, nnz));   // items
+  b += align256(sizeof(int32_t) * 4);                    // counts
+  b += align256(sizeof(int32_t) * (nnz / kSeg + 1)) * 2; // long rows
+  b += align256(sizeof(float) * max_parts_for(nnz) * (size_t)d);
+  b += scan_i32_ws_bytes(n) + 256;
+  return b + 4096;
+}
+
+int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv, Plan& pl,
+               hipStream_t s) {
+  int32_t* nseg = cv.take<int32_t>(n);
+  int32_t* npart = cv.take<int32_t>(n);
+  int32_t* item_off = cv.take<int32_t>(n);
+  int32_t* part_off = cv.take<int32_t>(n);
+  pl.max_items = max_items_for(n, nnz);
+  pl.max_long = nnz / kSeg + 1;
+  pl.items = cv.take<Item>(pl.max_items);
+  pl.counts = cv.take<int32_t>(4);
+  pl.long_rows = cv.take<int32_t>(pl.max_long);
+  pl.long_off = cv.take<int32_t>(pl.max_long);
+  pl.partials = cv.take<float>(max_parts_for(nnz) * (size_t)d);
+  size_t sb = scan_i32_ws_bytes(n);
+  void* scan_ws = cv.take<char>(sb);
+  if (!cv.ok()) return fail(GDD_E_WORKSPACE, "propagate: workspace too small");
+  const unsigned gb = (unsigned)((n + 255) / 256);
+  GDD_HIP(hipMemsetAsync(pl.counts, 0, sizeof(int32_t) * 4, s));
+  k_seg_counts<<<gb, 256, 0, s>>>(n, rowptr, nseg, npart);
+  GDD_LAUNCHED();
+  int rc = exclusive_scan_i32(nseg, item_off, n, scan_ws, sb, s);
+  if (rc) return rc;
+  rc = exclusive_scan_i32(npart, part_off, n, scan_ws, sb, s);
+  if (rc) return rc;
+  k_make_items<<<gb, 256, 0, s>>>(n, rowptr, nseg, item_off, part_off, pl.items, pl.long_rows,
+                                  pl.long_off, pl.counts);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+template <int V, int G>
+void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float scale, int d,
+                   const float* x, float* y, float* acc, float acc_scale, hipStream_t s) {
+  constexpr int kGroups = 256 / G;
+  dim3 grid((unsigned)((pl.max_items + kGroups - 1) / kGroups), (unsigned)((d + G * V - 1) / (G * V)));
+  k_hop<V, G><<<grid, 256, 0, s>>>(pl.items, pl.counts, col, val, scale, d, x, y, acc, acc_scale,
+                                   pl.partials);
+}
+
+template <int V>
+void launch_hop_v(const Plan& pl, const int32_t* col, const float* val, float scale, int d,
+                  const float* x, float* y, float* acc, float acc_scale, hipStream_t s) {
+  const int lanes = (d + V - 1) / V;
+  if (lanes <= 16)
+    launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+  else if (lanes <= 32)
+    launch_hop_vg<V, 32>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+  else
+    launch_hop_vg<V, 64>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+}
+
+int run_hop(const Plan& pl, const int32_t* rowptr, const int32_t* col, const float* val,
+            float scale, int d, const float* x, float* y, float* acc, float acc_scale,
+            hipStream_t s) {
+  // float4 rows need 16-byte aligned row starts: d % 4 == 0 and 16-byte aligned bases
+  auto aligned = [](const void* p, int a) { return ((uintptr_t)p % a) == 0; };
+  const bool a16 = aligned(x, 16) && aligned(y, 16) && (!acc || aligned(acc, 16)) &&
+                   aligned(pl.partials, 16);
+  const bool a8 = aligned(x, 8) && aligned(y, 8) && (!acc || aligned(acc, 8));
+  if (d % 4 == 0 && a16)
+    launch_hop_v<4>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+  else if (d % 2 == 0 && a8)
+    launch_hop_v<2>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+  else
+    launch_hop_v<1>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+  GDD_LAUNCHED();
+  k_fixup<<<(unsigned)pl.max_long, 256, 0, s>>>(pl.counts, pl.long_rows, pl.long_off, rowptr, d,
+                                                pl.partials, y, acc, acc_scale);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+int check_csr_args(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
+                   const float* val, int d) {
+  GDD_REQUIRE(n > 0 && n < INT32_MAX, "propagate: n=%lld out of range", (long long)n);
+  GDD_REQUIRE(nnz >= 0 && nnz < INT32_MAX, "propagate: nnz=%lld out of range", (long long)nnz);
+  GDD_REQUIRE(d > 0, "propagate: d=%d must be positive", d);
+  GDD_REQUIRE(rowptr && (nnz == 0 || (col && val)), "propagate: null CSR pointer");
+  return GDD_OK;
+}
+
+}  // namespace
+}  // namespace gdd
+
+using namespace gdd;
+
+extern "C" size_t gdd_propagate_ws_bytes(int64_t n, int64_t nnz, int d) {
+  return plan_ws_bytes(n, nnz, d);
+}
+
+extern "C" int gdd_spmm(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
+                        const float* val, int d, float scale, const float* x, float* y, float* acc,
+                        float acc_scale, void* ws, size_t ws_bytes, gdd_stream_t stream) {
+  int rc = check_csr_args(n, nnz, rowptr, col, val, d);
+  if (rc) return rc;
+  GDD_REQUIRE(x && y && ws, "spmm: null pointer");
+  hipStream_t s = to_hip(stream);
+  Carver cv(ws, ws_bytes);
+  Plan pl;
+  rc = build_plan(n, nnz, d, rowptr, cv, pl, s);
+  if (rc) return rc;
+  return run_hop(pl, rowptr, col, val, scale, d, x, y, acc, acc_scale, s);
+}
+
+extern "C" int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
+                             const float* val, int d, const float* X, int T, float alpha,
+                             float* target, float* p_last, float* p_tmp, void* ws,
+                             size_t ws_bytes, gdd_stream_t stream) {
+  int rc = check_csr_args(n, nnz, rowptr, col, val, d);
+  if (rc) return rc;
+  GDD_REQUIRE(T >= 1, "propagate: T=%d must be >= 1", T);
+  GDD_REQUIRE(X && target && p_last && ws && (T <= 2 || p_tmp), "propagate: null pointer");
+  hipStream_t s = to_hip(stream);
+  // the reference's Python doubles, rounded where they meet fp32 tensors
+  const float a32 = alpha;
+  const float w32 = (float)(1.0 - (double)alpha);
+  const int64_t total = n * (int64_t)d;
+  const unsigned eb = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
+  k_scale_copy<<<eb, 256, 0, s>>>(total, X, w32, target, T == 1 ? p_last : nullptr);
+  GDD_LAUNCHED();
+  if (T == 1) return GDD_OK;
+  Carver cv(ws, ws_bytes);
+  Plan pl;
+  rc = build_plan(n, nnz, d, rowptr, cv, pl, s);
+  if (rc) return rc;
+  // ping-pong so that hop T-1 lands in p_last
+  const int hops = T - 1;
+  float* bufs[2] = {(hops % 2 == 1) ? p_last : p_tmp, (hops % 2 == 1) ? p_tmp : p_last};
+  const float* in = X;
+  for (int h = 0; h < hops; ++h) {
+    float* out = bufs[h % 2];
+    rc = run_hop(pl, rowptr, col, val, a32, d, in, out, target, w32, s);
+    if (rc) return rc;
+    in = out;
+  }
+  return GDD_OK;
+}

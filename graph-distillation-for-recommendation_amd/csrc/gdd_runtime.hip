@@ -1,0 +1,82 @@
+// gdd_runtime.hip — error state, ABI version, device check, and the hipcub-backed scan/sort
+// primitives the kernels share.
+#include "gdd_common.hpp"
+
+#include <hipcub/hipcub.hpp>
+
+namespace gdd {
+
+static thread_local std::string g_last_error;
+
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+}
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+size_t scan_i32_ws_bytes(int64_t n) {
+  size_t bytes = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                   (int)n);
+  return align256(bytes);
+}
+
+int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, void* ws, size_t ws_bytes,
+                       hipStream_t s) {
+  size_t need = 0;
+  GDD_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need, in, out, (int)n, s));
+  if (need > ws_bytes) return fail(GDD_E_WORKSPACE, "scan workspace %zu < %zu", ws_bytes, need);
+  GDD_HIP(hipcub::DeviceScan::ExclusiveSum(ws, need, in, out, (int)n, s));
+  return GDD_OK;
+}
+
+size_t sort_pairs_ws_bytes(int64_t n) {
+  size_t bytes = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                     (const int32_t*)nullptr, (int32_t*)nullptr, (int)n);
+  return align256(bytes);
+}
+
+// stable LSD radix sort of (key, value) pairs on bits [0, end_bit)
+int sort_pairs_i32(const int32_t* keys_in, int32_t* keys_out, const int32_t* vals_in,
+                   int32_t* vals_out, int64_t n, int end_bit, void* ws, size_t ws_bytes,
+                   hipStream_t s) {
+  size_t need = 0;
+  GDD_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, need, keys_in, keys_out, vals_in, vals_out,
+                                             (int)n, 0, end_bit, s));
+  if (need > ws_bytes) return fail(GDD_E_WORKSPACE, "sort workspace %zu < %zu", ws_bytes, need);
+  GDD_HIP(hipcub::DeviceRadixSort::SortPairs(ws, need, keys_in, keys_out, vals_in, vals_out,
+                                             (int)n, 0, end_bit, s));
+  return GDD_OK;
+}
+
+}  // namespace gdd
+
+extern "C" {
+
+const char* gdd_last_error(void) { return gdd::g_last_error.c_str(); }
+
+int gdd_abi_version(void) { return 1; }
+
+int gdd_device_ok(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+  return std::string(prop.gcnArchName).rfind("gfx950", 0) == 0 ? 1 : 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,120 @@
+"""ctypes binding of libgdd.so (the C ABI declared in include/gdd.h).
+
+PyTorch provides device memory and the stream; every call passes raw device pointers and the
+current HIP stream to the library. There is no CPU fallback: if the library or a gfx950 device is
+missing, the first call raises.
+
+torch is imported before the library is loaded on purpose: torch ships its own libamdhip64.so
+(SONAME libamdhip64.so.7); loading libgdd.so afterwards makes the dynamic loader reuse that same
+runtime instead of pulling a second copy from /opt/rocm.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgdd.so")
+
+_c_i64 = ctypes.c_int64
+_c_int = ctypes.c_int
+_c_f32 = ctypes.c_float
+_c_size = ctypes.c_size_t
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); kept in the order of include/gdd.h
+SIGNATURES = {
+    "gdd_last_error": (ctypes.c_char_p, []),
+    "gdd_abi_version": (_c_int, []),
+    "gdd_device_ok": (_c_int, []),
+    "gdd_normalize_ws_bytes": (_c_size, [_c_i64, _c_i64]),
+    "gdd_normalize_csr": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp,
+                                   _c_size, _vp]),
+    "gdd_propagate_ws_bytes": (_c_size, [_c_i64, _c_i64, _c_int]),
+    "gdd_propagate": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _c_int, _vp, _c_int, _c_f32, _vp,
+                               _vp, _vp, _vp, _c_size, _vp]),
+    "gdd_spmm": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _c_int, _c_f32, _vp, _vp, _vp, _c_f32,
+                          _vp, _c_size, _vp]),
+    "gdd_row_norms": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp]),
+    "gdd_kmeans_assign_ws_bytes": (_c_size, [_c_i64]),
+    "gdd_kmeans_assign": (_c_int, [_c_i64, _c_int, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _vp,
+                                   _c_size, _vp]),
+    "gdd_inertia": (_c_int, [_c_i64, _vp, _vp, _vp, _vp]),
+    "gdd_minibatch_update_ws_bytes": (_c_size, [_c_i64, _c_int]),
+    "gdd_minibatch_update": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp,
+                                      _vp, _c_size, _vp]),
+    "gdd_group_ws_bytes": (_c_size, [_c_i64, _c_int]),
+    "gdd_group_by_label": (_c_int, [_c_i64, _vp, _c_int, _vp, _vp, _vp, _c_size, _vp]),
+    "gdd_segment_sum_f32": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp]),
+    "gdd_segment_sum_fixed": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _c_int, _c_int, _vp, _vp,
+                                       _vp]),
+    "gdd_fixed_to_centers": (_c_int, [_c_int, _c_int, _vp, _vp, _c_int, _vp, _vp]),
+    "gdd_average_centers": (_c_int, [_c_int, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "gdd_point_center_sqdist": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "gdd_labels_changed": (_c_int, [_c_i64, _vp, _vp, _vp, _vp]),
+    "gdd_kmeans_plusplus_ws_bytes": (_c_size, [_c_i64, _c_int]),
+    "gdd_kmeans_plusplus": (_c_int, [_c_i64, _c_int, _vp, _vp, _c_int, _c_int, _c_i64, _vp, _vp,
+                                     _vp, _vp, _c_size, _vp]),
+    "gdd_cluster_mean": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _c_int, _c_int, _vp, _vp, _vp]),
+    "gdd_argmax_rows": (_c_int, [_c_int, _c_int, _vp, _vp, _vp]),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libgdd.so and attach signatures (no device work)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"libgdd.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; "
+            "g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+_device_checked = False
+
+
+def device_lib() -> ctypes.CDLL:
+    """The library, after checking that the current device is a gfx950 GPU."""
+    global _device_checked
+    lib = load()
+    if not _device_checked:
+        if not torch.cuda.is_available():
+            raise RuntimeError("gdd: no HIP device visible; the MI355X path has no CPU fallback")
+        torch.cuda.current_device()
+        if lib.gdd_device_ok() != 1:
+            name = torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName
+            raise RuntimeError(f"gdd: device arch {name!r} is not gfx950")
+        _device_checked = True
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = load().gdd_last_error().decode(errors="replace")
+        raise RuntimeError(f"libgdd error {rc:#x}: {msg}")
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)

@@ -1,0 +1,174 @@
+"""Graph side of the ClustGDD hot path on MI355X: CSR upload, normalisation, propagation.
+
+Drop-in for
+* ``deep_robust_utils.to_tensor`` / ``sparse_mx_to_torch_sparse_tensor`` (ClustGDD/deep_robust_utils.py:85-113,
+  :389-396) — :func:`to_csr` takes the same inputs (scipy sparse, torch sparse, dense array) and
+  keeps CSR (int32 rowptr/col, fp32 values) resident in HBM instead of an int64 COO tensor;
+* ``deep_robust_utils.normalize_adj_tensor(adj, sparse=True)`` (:245-256) — :func:`normalize_adj_tensor`;
+* the propagation loop of ``ClustGDD.pretrained_clustering`` (clustgdd_agent_transduct.py:55-65,
+  clustgdd_agent_induct.py:67-94) — :func:`propagate`.
+All arithmetic runs in libgdd (HIP, gfx950); this module only moves buffers and checks shapes.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from . import _lib
+
+
+@dataclass
+class CSRGraph:
+    """A square sparse matrix resident on the GPU as canonical CSR."""
+
+    rowptr: torch.Tensor  # int32 [n+1]
+    col: torch.Tensor  # int32 [nnz]
+    val: Optional[torch.Tensor]  # fp32 [nnz]; None = all ones (binary adjacency)
+    n: int
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.shape[0])
+
+    @property
+    def device(self) -> torch.device:
+        return self.rowptr.device
+
+    @property
+    def shape(self):
+        return (self.n, self.n)
+
+    def values(self) -> torch.Tensor:
+        if self.val is None:
+            return torch.ones(self.nnz, dtype=torch.float32, device=self.device)
+        return self.val
+
+    def to_scipy(self) -> sp.csr_matrix:
+        return sp.csr_matrix((self.values().cpu().numpy(), self.col.cpu().numpy(),
+                              self.rowptr.cpu().numpy()), shape=self.shape)
+
+    def to_torch_sparse(self) -> torch.Tensor:
+        """COO view with the reference's index/value dtypes (int64 / fp32)."""
+        rp = self.rowptr.long()
+        rows = torch.repeat_interleave(torch.arange(self.n, device=self.device),
+                                       rp[1:] - rp[:-1])
+        idx = torch.stack([rows, self.col.long()])
+        return torch.sparse_coo_tensor(idx, self.values(), self.shape).coalesce()
+
+
+def to_csr(adj, device="cuda", binary: Optional[bool] = None) -> CSRGraph:
+    """Upload an adjacency matrix (scipy sparse / torch sparse / dense) as canonical CSR.
+
+    Duplicates are summed and columns sorted, as scipy's csr_matrix construction in
+    ``deep_robust_utils.to_scipy`` (:408-417) does. ``binary=None`` detects an all-ones value
+    array and then stores no values (the kernels read 1.0f).
+    """
+    if isinstance(adj, torch.Tensor):
+        if adj.is_sparse:
+            a = adj.coalesce()
+            idx = a.indices().cpu().numpy()
+            m = sp.csr_matrix((a.values().cpu().numpy().astype(np.float32), (idx[0], idx[1])),
+                              shape=tuple(a.shape))
+        elif adj.layout == torch.sparse_csr:
+            m = sp.csr_matrix((adj.values().cpu().numpy(), adj.col_indices().cpu().numpy(),
+                               adj.crow_indices().cpu().numpy()), shape=tuple(adj.shape))
+        else:
+            m = sp.csr_matrix(adj.detach().cpu().numpy())
+    elif sp.issparse(adj):
+        m = sp.csr_matrix(adj)
+    else:
+        m = sp.csr_matrix(np.asarray(adj))
+    if m.shape[0] != m.shape[1]:
+        raise ValueError(f"adjacency must be square, got {m.shape}")
+    m = m.astype(np.float32)
+    m.sum_duplicates()
+    m.sort_indices()
+    if m.nnz >= 2**31 - m.shape[0]:
+        raise ValueError("graph too large for int32 CSR")
+    dev = torch.device(device)
+    vals = m.data
+    if binary is None:
+        binary = bool(np.all(vals == 1.0))
+    rowptr = torch.from_numpy(m.indptr.astype(np.int32)).to(dev)
+    col = torch.from_numpy(m.indices.astype(np.int32)).to(dev)
+    val = None if binary else torch.from_numpy(vals.astype(np.float32)).to(dev)
+    return CSRGraph(rowptr, col, val, m.shape[0])
+
+
+def normalize_adj(adj: CSRGraph, self_loops: int = -1) -> CSRGraph:
+    """Â = D^-1/2 (A + I) D^-1/2 (deep_robust_utils.normalize_adj, :180-207).
+
+    self_loops=-1 is the reference rule: I is added only if A[0,0] == 0 (:199-200); fp64 math
+    then, fp32 otherwise. Output is canonical CSR with fp32 values.
+    """
+    lib = _lib.device_lib()
+    dev = adj.device
+    n, nnz = adj.n, adj.nnz
+    rowptr_out = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    col_out = torch.empty(nnz + n, dtype=torch.int32, device=dev)
+    val_out = torch.empty(nnz + n, dtype=torch.float32, device=dev)
+    ws = _lib.workspace(lib.gdd_normalize_ws_bytes(n, nnz), dev)
+    _lib.check(lib.gdd_normalize_csr(n, nnz, adj.rowptr.data_ptr(), _lib.ptr(adj.col),
+                                     _lib.ptr(adj.val), int(self_loops), rowptr_out.data_ptr(),
+                                     col_out.data_ptr(), val_out.data_ptr(), ws.data_ptr(),
+                                     ws.numel(), _lib.stream_ptr(dev)))
+    nnz_out = int(rowptr_out[n].item())
+    return CSRGraph(rowptr_out, col_out[:nnz_out], val_out[:nnz_out], n)
+
+
+def normalize_adj_tensor(adj, sparse: bool = True, device=None) -> CSRGraph:
+    """Drop-in for deep_robust_utils.normalize_adj_tensor(adj, sparse=True) (:245-256)."""
+    if not sparse:
+        raise NotImplementedError("dense normalisation is outside the MI355X hot path")
+    if not isinstance(adj, CSRGraph):
+        adj = to_csr(adj, device=device or "cuda")
+    return normalize_adj(adj)
+
+
+def _ws_propagate(adj: CSRGraph, d: int):
+    lib = _lib.device_lib()
+    return lib, _lib.workspace(lib.gdd_propagate_ws_bytes(adj.n, adj.nnz, d), adj.device)
+
+
+def propagate(adj_norm: CSRGraph, features: torch.Tensor, T: int, alpha: float):
+    """The closed-form feature denoising loop of pretrained_clustering (transduct:55-65).
+
+    Returns ``(target_feat, prop_feat)`` exactly as the loop leaves them: ``target_feat =
+    (1-α)·Σ_{t<T} (αÂ)^t X`` accumulated hop by hop in fp32, ``prop_feat`` = the last hop.
+    """
+    if T < 1:
+        raise ValueError("prop_num must be >= 1 (the reference loop leaves target undefined)")
+    X = features.contiguous()
+    if X.dtype != torch.float32:
+        raise TypeError("features must be float32")
+    if X.device != adj_norm.device:
+        raise ValueError("features and adjacency must be on the same device")
+    n, d = X.shape
+    if n != adj_norm.n:
+        raise ValueError(f"features have {n} rows, adjacency {adj_norm.n}")
+    lib, ws = _ws_propagate(adj_norm, d)
+    target = torch.empty_like(X)
+    p_last = torch.empty_like(X)
+    p_tmp = torch.empty_like(X) if T > 2 else None
+    _lib.check(lib.gdd_propagate(n, adj_norm.nnz, adj_norm.rowptr.data_ptr(),
+                                 _lib.ptr(adj_norm.col), _lib.ptr(adj_norm.values()), d,
+                                 X.data_ptr(), int(T), float(alpha), target.data_ptr(),
+                                 p_last.data_ptr(), _lib.ptr(p_tmp), ws.data_ptr(), ws.numel(),
+                                 _lib.stream_ptr(X.device)))
+    return target, p_last
+
+
+def spmm(adj: CSRGraph, x: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    """y = (scale·A) @ x in the canonical order (also the GCN evaluator's torch.spmm)."""
+    x = x.contiguous()
+    lib, ws = _ws_propagate(adj, x.shape[1])
+    y = torch.empty_like(x)
+    _lib.check(lib.gdd_spmm(adj.n, adj.nnz, adj.rowptr.data_ptr(), _lib.ptr(adj.col),
+                            _lib.ptr(adj.values()), x.shape[1], float(scale), x.data_ptr(),
+                            y.data_ptr(), None, 0.0, ws.data_ptr(), ws.numel(),
+                            _lib.stream_ptr(x.device)))
+    return y

@@ -1,0 +1,403 @@
+"""scikit-learn-compatible KMeans / MiniBatchKMeans whose arithmetic runs in libgdd on MI355X.
+
+Drop-in for the estimators the reference constructs at
+``clustgdd_agent_transduct.py:102-105``, ``clustgdd_agent_induct.py:131-134`` and
+``distill_recsys.py:174-180``: same constructor arguments, ``fit`` / ``fit_predict`` /
+``predict``, and the fitted attributes ``labels_``, ``cluster_centers_``, ``inertia_``,
+``n_iter_`` (and ``n_steps_`` for MiniBatchKMeans) as numpy arrays/scalars.
+
+Semantics are scikit-learn 1.7.2's (sklearn/cluster/_kmeans.py) run with one OpenMP thread:
+* the RNG is numpy's legacy RandomState from ``check_random_state(random_state)`` — the
+  reference's own generator — drawn in sklearn's order on the host;
+* every O(n·k·d) and O(n·d) step runs on the device: k-means++ seeding, the MFMA distance GEMM
+  with row argmin, inertia, the minibatch/Lloyd centre updates, the full labels pass;
+* the host keeps the O(k) control: early stopping on the EWA inertia, the low-count reassignment
+  test (numpy on a k-vector), Lloyd's convergence test.
+Under those conditions labels, centres, inertia and step counts equal scikit-learn's bit for bit
+(tests/test_gpu_kmeans.py against tests/golden/).
+
+``n_init="auto"`` follows sklearn >= 1.4 (one init for k-means++). The README of the reference
+pins scikit-learn 1.3.2, whose default was 10 (KMeans) / 3 (MiniBatchKMeans); pass ``n_init``
+explicitly to reproduce that.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def check_random_state(seed):
+    """sklearn.utils.check_random_state."""
+    if seed is None or seed is np.random:
+        return np.random.mtrand._rand
+    if isinstance(seed, (int, np.integer)):
+        return np.random.RandomState(seed)
+    if isinstance(seed, np.random.RandomState):
+        return seed
+    raise ValueError(f"{seed!r} cannot be used to seed a numpy.random.RandomState instance")
+
+
+def _as_device_f32(X, device):
+    if isinstance(X, torch.Tensor):
+        return X.detach().to(device=device, dtype=torch.float32).contiguous()
+    return torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to(device)
+
+
+class _Ops:
+    """Device primitives with their workspaces (one instance per fit)."""
+
+    def __init__(self, device, n_max: int, k: int, dim: int):
+        self.lib = _lib.device_lib()
+        self.device = torch.device(device)
+        self.k, self.dim = k, dim
+        self.ws_assign = _lib.workspace(self.lib.gdd_kmeans_assign_ws_bytes(n_max), self.device)
+        self.cn2 = torch.empty(k, dtype=torch.float32, device=self.device)
+        self.scalar = torch.empty(1, dtype=torch.float32, device=self.device)
+
+    @property
+    def stream(self):
+        return _lib.stream_ptr(self.device)
+
+    def row_norms(self, C):
+        _lib.check(self.lib.gdd_row_norms(C.shape[0], self.dim, C.data_ptr(), self.cn2.data_ptr(),
+                                          self.stream))
+        return self.cn2
+
+    def assign(self, X, C, rows=None, labels=None, sq=None, n=None):
+        n = (rows.shape[0] if rows is not None else X.shape[0]) if n is None else n
+        cn2 = self.row_norms(C)
+        _lib.check(self.lib.gdd_kmeans_assign(
+            n, self.dim, X.data_ptr(), _lib.ptr(rows), C.shape[0], C.data_ptr(), cn2.data_ptr(),
+            labels.data_ptr(), _lib.ptr(sq), self.ws_assign.data_ptr(), self.ws_assign.numel(),
+            self.stream))
+
+    def inertia(self, sq, n=None):
+        n = sq.shape[0] if n is None else n
+        _lib.check(self.lib.gdd_inertia(n, sq.data_ptr(), None, self.scalar.data_ptr(), self.stream))
+        return self.scalar
+
+    def kmeans_plusplus(self, Xi, k, rs, n_local_trials=None):
+        """_kmeans_plusplus (sklearn/cluster/_kmeans.py:174-272) with unit sample weights."""
+        n = Xi.shape[0]
+        T = 2 + int(np.log(k)) if n_local_trials is None else int(n_local_trials)
+        w = np.ones(n, dtype=np.float32)
+        first = rs.choice(n, p=w / w.sum())
+        if k > 1:
+            u = np.concatenate([rs.uniform(size=T) for _ in range(k - 1)])
+        else:
+            u = np.zeros(1)
+        u_d = torch.from_numpy(u.astype(np.float64)).to(self.device)
+        centers = torch.empty((k, self.dim), dtype=torch.float32, device=self.device)
+        idx = torch.empty(k, dtype=torch.int64, device=self.device)
+        ws = _lib.workspace(self.lib.gdd_kmeans_plusplus_ws_bytes(n, T), self.device)
+        _lib.check(self.lib.gdd_kmeans_plusplus(n, self.dim, Xi.data_ptr(), None, k, T, int(first),
+                                                u_d.data_ptr(), centers.data_ptr(), idx.data_ptr(),
+                                                ws.data_ptr(), ws.numel(), self.stream))
+        return centers, idx
+
+
+class _BaseKMeans:
+    def __init__(self, n_clusters=8, *, init="k-means++", n_init="auto", max_iter=300, tol=1e-4,
+                 verbose=0, random_state=None, device="cuda"):
+        if init != "k-means++":
+            raise NotImplementedError("only init='k-means++' (the reference's) is implemented")
+        self.n_clusters = n_clusters
+        self.init = init
+        self.n_init = n_init
+        self.max_iter = max_iter
+        self.tol = tol
+        self.verbose = verbose
+        self.random_state = random_state
+        self.device = device
+
+    def _n_init(self, default):
+        if self.n_init == "auto":
+            return 1  # k-means++ with 'auto' (sklearn >= 1.4, _kmeans.py:879-889)
+        return int(self.n_init)
+
+    def fit_predict(self, X, y=None, sample_weight=None):
+        return self.fit(X, sample_weight=sample_weight).labels_
+
+    def predict(self, X):
+        Xd = _as_device_f32(X, self.device)
+        C = torch.from_numpy(np.ascontiguousarray(self.cluster_centers_, np.float32)).to(Xd.device)
+        ops = _Ops(Xd.device, Xd.shape[0], C.shape[0], Xd.shape[1])
+        labels = torch.empty(Xd.shape[0], dtype=torch.int32, device=Xd.device)
+        ops.assign(Xd, C, labels=labels)
+        return labels.cpu().numpy()
+
+    @staticmethod
+    def _check_weights(sample_weight):
+        if sample_weight is not None and not np.all(np.asarray(sample_weight) == 1):
+            raise NotImplementedError("non-unit sample_weight is not used by the reference")
+
+
+class MiniBatchKMeans(_BaseKMeans):
+    """sklearn.cluster.MiniBatchKMeans.fit (sklearn/cluster/_kmeans.py:2046-2200) on the device."""
+
+    def __init__(self, n_clusters=8, *, init="k-means++", max_iter=100, batch_size=1024, verbose=0,
+                 compute_labels=True, random_state=None, tol=0.0, max_no_improvement=10,
+                 init_size=None, n_init="auto", reassignment_ratio=0.01, device="cuda"):
+        super().__init__(n_clusters, init=init, n_init=n_init, max_iter=max_iter, tol=tol,
+                         verbose=verbose, random_state=random_state, device=device)
+        self.batch_size = batch_size
+        self.compute_labels = compute_labels
+        self.max_no_improvement = max_no_improvement
+        self.init_size = init_size
+        self.reassignment_ratio = reassignment_ratio
+
+    def fit(self, X, y=None, sample_weight=None):
+        self._check_weights(sample_weight)
+        Xd = _as_device_f32(X, self.device)
+        dev = Xd.device
+        n, dim = Xd.shape
+        k = self.n_clusters
+        if k > n:
+            raise ValueError(f"n_samples={n} should be >= n_clusters={k}.")
+        rs = check_random_state(self.random_state)
+        bs = min(self.batch_size, n)
+        isz = self.init_size
+        if isz is None:
+            isz = 3 * bs
+            if isz < k:
+                isz = 3 * k
+        elif isz < k:
+            isz = 3 * k
+        isz = min(isz, n)
+        n_init = self._n_init(3)
+        ops = _Ops(dev, max(n, isz, bs), k, dim)
+
+        # Validation set for the init (:2128-2131)
+        validation_indices = rs.randint(0, n, isz)
+        best_inertia, init_centers = None, None
+        for _ in range(n_init):
+            if isz < n:
+                init_indices = torch.from_numpy(rs.randint(0, n, isz)).to(dev)
+                Xi = Xd.index_select(0, init_indices)
+            else:
+                Xi = Xd
+            centers, _ = ops.kmeans_plusplus(Xi, k, rs)
+            if n_init > 1:
+                vrows = torch.from_numpy(validation_indices).to(dev)
+                lab = torch.empty(isz, dtype=torch.int32, device=dev)
+                sq = torch.empty(isz, dtype=torch.float32, device=dev)
+                ops.assign(Xd, centers, rows=vrows, labels=lab, sq=sq)
+                inertia = float(ops.inertia(sq).item())
+            else:
+                inertia = 0.0
+            if best_inertia is None or inertia < best_inertia:
+                init_centers, best_inertia = centers, inertia
+
+        C = init_centers.contiguous()
+        C_new = torch.empty_like(C)
+        counts = torch.zeros(k, dtype=torch.float32, device=dev)
+        ws_mb = _lib.workspace(ops.lib.gdd_minibatch_update_ws_bytes(bs, k), dev)
+        labels_b = torch.empty(bs, dtype=torch.int32, device=dev)
+        sq_b = torch.empty(bs, dtype=torch.float32, device=dev)
+        rows_pinned = torch.empty(bs, dtype=torch.int64, pin_memory=True)
+        rows_d = torch.empty(bs, dtype=torch.int64, device=dev)
+        any_zero = True  # counts start at zero
+        ewa = ewa_min = None
+        no_improvement = 0
+        n_since = 0
+        n_steps = (self.max_iter * n) // bs
+        tol_ = 0.0
+        if self.tol > 0:
+            tol_ = float(torch.var(Xd, dim=0, unbiased=False).mean().item()) * self.tol
+        stream = ops.stream
+        i = 0
+        for i in range(n_steps):
+            mb = rs.randint(0, n, bs)
+            n_since += bs
+            if any_zero or n_since >= 10 * k:  # _random_reassign (:2029-2043)
+                n_since = 0
+                rr = True
+            else:
+                rr = False
+            rows_pinned.numpy()[:] = mb
+            rows_d.copy_(rows_pinned, non_blocking=True)
+            ops.assign(Xd, C, rows=rows_d, labels=labels_b, sq=sq_b)
+            bi_d = ops.inertia(sq_b)
+            _lib.check(ops.lib.gdd_minibatch_update(bs, dim, Xd.data_ptr(), rows_d.data_ptr(), None,
+                                                    labels_b.data_ptr(), k, C.data_ptr(),
+                                                    C_new.data_ptr(), counts.data_ptr(),
+                                                    ws_mb.data_ptr(), ws_mb.numel(), stream))
+            if rr and self.reassignment_ratio > 0:  # _mini_batch_step (:1640-1667)
+                W = counts.cpu().numpy()
+                to_reassign = W < self.reassignment_ratio * W.max()
+                if to_reassign.sum() > 0.5 * bs:
+                    dont = np.argsort(W)[int(0.5 * bs):]
+                    to_reassign[dont] = False
+                n_re = int(to_reassign.sum())
+                if n_re:
+                    new_centers = rs.choice(bs, replace=False, size=n_re)
+                    dst = torch.from_numpy(np.where(to_reassign)[0]).to(dev)
+                    src = rows_d.index_select(0, torch.from_numpy(new_centers).to(dev))
+                    C_new.index_copy_(0, dst, Xd.index_select(0, src))
+                W[to_reassign] = np.min(W[~to_reassign])
+                counts.copy_(torch.from_numpy(W))
+                any_zero = bool((W == 0).any())
+            if tol_ > 0:
+                sq_diff = float(((C_new - C) ** 2).sum().item())
+            else:
+                sq_diff = 0
+            C, C_new = C_new, C
+            # _mini_batch_convergence (:1960-2027), Python floats as in sklearn
+            bi = float(bi_d.item()) / bs
+            step = i + 1
+            if step == 1:
+                continue
+            if ewa is None:
+                ewa = bi
+            else:
+                a = min(bs * 2.0 / (n + 1), 1)
+                ewa = ewa * (1 - a) + bi * a
+            if tol_ > 0.0 and sq_diff <= tol_:
+                break
+            if ewa_min is None or ewa < ewa_min:
+                no_improvement = 0
+                ewa_min = ewa
+            else:
+                no_improvement += 1
+            if self.max_no_improvement is not None and no_improvement >= self.max_no_improvement:
+                break
+        self.n_steps_ = i + 1
+        self.n_iter_ = int(np.ceil(((i + 1) * bs) / n))
+        self.cluster_centers_device_ = C
+        self.cluster_centers_ = C.cpu().numpy()
+        if self.compute_labels:
+            labels = torch.empty(n, dtype=torch.int32, device=dev)
+            sq = torch.empty(n, dtype=torch.float32, device=dev)
+            ops.assign(Xd, C, labels=labels, sq=sq)
+            self.inertia_ = float(ops.inertia(sq).item())
+            self.labels_device_ = labels
+            self.labels_ = labels.cpu().numpy()
+        else:
+            self.inertia_ = ewa * n if ewa is not None else 0.0
+        return self
+
+
+class KMeans(_BaseKMeans):
+    """sklearn.cluster.KMeans(algorithm='lloyd').fit (sklearn/cluster/_kmeans.py:1427-1530)."""
+
+    def __init__(self, n_clusters=8, *, init="k-means++", n_init="auto", max_iter=300, tol=1e-4,
+                 verbose=0, random_state=None, copy_x=True, algorithm="lloyd", device="cuda"):
+        super().__init__(n_clusters, init=init, n_init=n_init, max_iter=max_iter, tol=tol,
+                         verbose=verbose, random_state=random_state, device=device)
+        if algorithm != "lloyd":
+            raise NotImplementedError("only algorithm='lloyd' (the default) is implemented")
+        self.copy_x = copy_x
+        self.algorithm = algorithm
+
+    def fit(self, X, y=None, sample_weight=None):
+        self._check_weights(sample_weight)
+        # host copy for the O(d) preprocessing sklearn does with numpy (mean, var -> tol)
+        if isinstance(X, torch.Tensor):
+            Xh = X.detach().cpu().numpy().astype(np.float32)
+        else:
+            Xh = np.array(X, dtype=np.float32, order="C", copy=True)
+        n, dim = Xh.shape
+        k = self.n_clusters
+        if k > n:
+            raise ValueError(f"n_samples={n} should be >= n_clusters={k}.")
+        rs = check_random_state(self.random_state)
+        X_mean = Xh.mean(axis=0)
+        Xh = Xh - X_mean
+        tol_ = 0 if self.tol == 0 else np.mean(np.var(Xh, axis=0)) * self.tol
+        Xd = _as_device_f32(Xh, self.device)
+        dev = Xd.device
+        ops = _Ops(dev, n, k, dim)
+        lib = ops.lib
+        stream = ops.stream
+        ws_group = _lib.workspace(lib.gdd_group_ws_bytes(n, k), dev)
+        perm = torch.empty(n, dtype=torch.int32, device=dev)
+        offsets = torch.empty(k + 1, dtype=torch.int32, device=dev)
+        labels = torch.empty(n, dtype=torch.int32, device=dev)
+        labels_old = torch.empty(n, dtype=torch.int32, device=dev)
+        changed = torch.empty(1, dtype=torch.int32, device=dev)
+        wic = torch.empty(k, dtype=torch.float32, device=dev)
+        shift = torch.empty(k, dtype=torch.float32, device=dev)
+        sq = torch.empty(n, dtype=torch.float32, device=dev)
+
+        best = None
+        for _ in range(self._n_init(10)):
+            C, _ = ops.kmeans_plusplus(Xd, k, rs)
+            C_new = torch.empty_like(C)
+            labels_old.fill_(-1)
+            strict = False
+            it = 0
+            for it in range(self.max_iter):  # _kmeans_single_lloyd (:690-735)
+                ops.assign(Xd, C, labels=labels)
+                _lib.check(lib.gdd_group_by_label(n, labels.data_ptr(), k, perm.data_ptr(),
+                                                  offsets.data_ptr(), ws_group.data_ptr(),
+                                                  ws_group.numel(), stream))
+                _lib.check(lib.gdd_segment_sum_f32(n, dim, Xd.data_ptr(), None, perm.data_ptr(),
+                                                   offsets.data_ptr(), k, C_new.data_ptr(),
+                                                   wic.data_ptr(), stream))
+                wic_h = wic.cpu().numpy()
+                if (wic_h == 0).any():
+                    self._relocate(Xh, C, C_new, wic, wic_h, labels)
+                _lib.check(lib.gdd_average_centers(k, dim, C_new.data_ptr(), wic.data_ptr(),
+                                                   C.data_ptr(), shift.data_ptr(), stream))
+                _lib.check(lib.gdd_labels_changed(n, labels.data_ptr(), labels_old.data_ptr(),
+                                                  changed.data_ptr(), stream))
+                C, C_new = C_new, C
+                if int(changed.item()) == 0:
+                    strict = True
+                    break
+                sh = shift.cpu().numpy()
+                if (sh ** 2).sum() <= tol_:
+                    break
+            if not strict:
+                ops.assign(Xd, C, labels=labels)
+            _lib.check(lib.gdd_point_center_sqdist(n, dim, Xd.data_ptr(), labels.data_ptr(),
+                                                   C.data_ptr(), sq.data_ptr(), stream))
+            inertia = float(ops.inertia(sq).item())
+            lab_h = labels.cpu().numpy()
+            if best is None or (inertia < best[1] and not _same_clustering(lab_h, best[0], k)):
+                best = (lab_h, inertia, C.clone(), it + 1)
+        lab_h, inertia, C, n_iter = best
+        self.labels_ = lab_h
+        self.inertia_ = inertia
+        self.cluster_centers_ = C.cpu().numpy() + X_mean
+        self.cluster_centers_device_ = torch.from_numpy(self.cluster_centers_).to(dev)
+        self.labels_device_ = torch.from_numpy(lab_h).to(dev)
+        self.n_iter_ = n_iter
+        return self
+
+    @staticmethod
+    def _relocate(Xh, C_old, C_new, wic, wic_h, labels):
+        """_relocate_empty_clusters_dense (_k_means_common.pyx:124-164). Rare: runs the same numpy
+        expressions as sklearn on the host copy of X so the far-point ranking (argpartition) is
+        identical, then writes the few changed rows back."""
+        lab = labels.cpu().numpy()
+        co = C_old.cpu().numpy()
+        cn = C_new.cpu().numpy()
+        empty = np.where(np.equal(wic_h, 0))[0].astype(np.int32)
+        ne = empty.shape[0]
+        distances = ((Xh - co[lab]) ** 2).sum(axis=1)
+        far = np.argpartition(distances, -ne)[:-ne - 1:-1].astype(np.int32)
+        if np.max(distances) == 0:
+            return
+        for idx in range(ne):
+            new_id, far_idx = empty[idx], far[idx]
+            old_id = lab[far_idx]
+            cn[old_id] -= Xh[far_idx]
+            cn[new_id] = Xh[far_idx]
+            wic_h[new_id] = 1.0
+            wic_h[old_id] -= 1.0
+        C_new.copy_(torch.from_numpy(cn))
+        wic.copy_(torch.from_numpy(wic_h))
+
+
+def _same_clustering(l1, l2, k):
+    """sklearn _is_same_clustering (_k_means_common.pyx:254-266)."""
+    mapping = np.full(k, -1, np.int64)
+    for a, b in zip(l1, l2):
+        if mapping[a] == -1:
+            mapping[a] = b
+        elif mapping[a] != b:
+            return False
+    return True

@@ -1,0 +1,186 @@
+/*
+ * gdd.h — C ABI of libgdd, the MI355X-native (gfx950) hot path of ClustGDD graph distillation.
+ *
+ * The reference (Tyler-Linchenwei/Graph-Distillation-for-Recommendation, ClustGDD/) has no FFI layer:
+ * its hot path is inline Python inside ClustGDD.pretrained_clustering and distill_recsys.kmeans_cluster.
+ * Each entry point below replaces one of those call sites; the cited file:line is the reference code
+ * whose arithmetic the entry point restates (paths relative to the reference's ClustGDD/ directory,
+ * or to scikit-learn 1.7.2 for the k-means internals the reference calls).
+ *
+ * Conventions (all entry points):
+ *   - every array argument is a DEVICE pointer, caller-owned (PyTorch allocates), row-major, dense;
+ *   - work is enqueued on `stream` (the caller's torch.cuda.current_stream()); no entry point
+ *     synchronises the host except where its comment says so;
+ *   - the library keeps no device memory and no global mutable state; scratch comes from a caller
+ *     workspace sized by the matching *_ws_bytes() query;
+ *   - return 0 on success, otherwise a GDD_E_* code or a hipError_t value; gdd_last_error() gives a
+ *     thread-local message. Shapes are validated on the host before any launch.
+ */
+#ifndef GDD_H_
+#define GDD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* gdd_stream_t; /* == hipStream_t */
+
+#define GDD_OK 0
+#define GDD_E_INVALID 0x10001   /* bad shape / null pointer / unsupported parameter */
+#define GDD_E_WORKSPACE 0x10002 /* workspace too small */
+#define GDD_E_NODEVICE 0x10003  /* no gfx950 device visible */
+
+/* ---------------------------------------------------------------------------------------------- */
+/* Library                                                                                          */
+/* ---------------------------------------------------------------------------------------------- */
+const char* gdd_last_error(void);
+int gdd_abi_version(void); /* bumps on any signature change */
+/* 1 if the current HIP device is gfx950 and the embedded code objects can run on it. */
+int gdd_device_ok(void);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* (a2) normalisation:  Â = D^-1/2 (A + I) D^-1/2                                                   */
+/* Replaces deep_robust_utils.normalize_adj_tensor(adj, sparse=True)  (deep_robust_utils.py:245-256)  */
+/*   -> to_scipy (:408-417) -> normalize_adj (:180-207) -> sparse_mx_to_torch_sparse_tensor (:389-396) */
+/* Input: canonical CSR of A (rows ascending, columns strictly ascending per row, no duplicates);    */
+/*   val == NULL means every stored value is 1.0f (binary adjacency).                               */
+/* self_loops: -1 = reference rule (add I iff A[0,0] == 0, deep_robust_utils.py:199-200),            */
+/*              0 = never, 1 = always.                                                              */
+/* When I is added the row sums, r = rowsum^-1/2 (inf -> 0) and both scalings are done in fp64 and    */
+/* the result is rounded to fp32 (sp.eye promotes the matrix to float64); otherwise in fp32.         */
+/* Output: canonical CSR; entries whose scaled value is exactly 0 are dropped (scipy csr_matmat       */
+/* drops them). col_out / val_out must hold nnz + n entries; rowptr_out[n] receives nnz_out.         */
+/* ---------------------------------------------------------------------------------------------- */
+size_t gdd_normalize_ws_bytes(int64_t n, int64_t nnz);
+int gdd_normalize_csr(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
+                      const float* val, int self_loops, int32_t* rowptr_out, int32_t* col_out,
+                      float* val_out, void* ws, size_t ws_bytes, gdd_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* (a3) feature propagation                                                                         */
+/* Replaces the loop clustgdd_agent_transduct.py:59-65 (and clustgdd_agent_induct.py:72-94):          */
+/*   t = 0:      p = X,                 target = fp32(1-alpha) * X                                   */
+/*   t = 1..T-1: p = (fp32(alpha) * Â) @ p,  target = target + fp32(1-alpha) * p                    */
+/* Canonical summation order of one output row: its stored entries in CSR order are cut into         */
+/* segments of GDD_PROP_SEG entries; each segment is an fp32 fma chain from +0 in entry order; the   */
+/* segment partials are added left to right. `p_last` receives p after the last hop (X if T == 1).   */
+/* X, target, p_last, p_tmp: n x d fp32; p_tmp is scratch (may alias nothing else).                  */
+/* ---------------------------------------------------------------------------------------------- */
+#define GDD_PROP_SEG 256
+size_t gdd_propagate_ws_bytes(int64_t n, int64_t nnz, int d);
+int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* val,
+                  int d, const float* X, int T, float alpha, float* target, float* p_last,
+                  float* p_tmp, void* ws, size_t ws_bytes, gdd_stream_t stream);
+/* one hop: y = (scale * Â) @ x with the canonical order above; if acc != NULL also                   */
+/*   acc = acc + acc_scale * y  (two fp32 roundings, no contraction).                               */
+int gdd_spmm(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* val,
+             int d, float scale, const float* x, float* y, float* acc, float acc_scale, void* ws,
+             size_t ws_bytes, gdd_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* (a5/a6/a8) k-means building blocks (scikit-learn 1.7.2 semantics, fp32 data)                      */
+/* Replace MiniBatchKMeans/KMeans(...).fit at clustgdd_agent_transduct.py:102-105,                    */
+/* clustgdd_agent_induct.py:131-134, distill_recsys.py:174-180. Loop control and the MT19937 draws    */
+/* stay on the host (numpy RandomState is the reference's own RNG).                                 */
+/* ---------------------------------------------------------------------------------------------- */
+
+/* out[i] = sum_j X[i,j]^2 in numpy's einsum("ij,ij->i") float32 order (sklearn row_norms,           */
+/* sklearn/utils/extmath.py:76): 4 lanes, 16-element blocks fed in reverse vector order, mul+add     */
+/* (no fma), lanes reduced (l0+l1)+(l2+l3). Bit-exact with numpy on x86-64 SSE3 builds.              */
+int gdd_row_norms(int64_t n, int dim, const float* X, float* out, gdd_stream_t stream);
+
+/* Assignment (E-step) of sklearn _update_chunk_dense (sklearn/cluster/_k_means_lloyd.pyx:172-213):  */
+/*   d[i,j] = fma(-2, sum_t X[i,t]*C[j,t] as a t-ordered fp32 fma chain, c_norm2[j])                */
+/*   labels[i] = first j with minimal d  (strict <, lowest index wins)                              */
+/* computed with v_mfma_f32_32x32x2_f32 (exact k-ordered fma chain = OpenBLAS sgemm, bit-exact).     */
+/* rows == NULL: rows are 0..n-1; otherwise row i of the batch is X[rows[i]] (minibatch gather).     */
+/* sq_dist (nullable): per-sample ||x - c_label||^2 in sklearn _euclidean_dense_dense order          */
+/* (sklearn/cluster/_k_means_common.pyx:26-48: 4-term groups, mul+add, no fma).                      */
+/* dim <= 512. Workspace: gdd_kmeans_assign_ws_bytes(n) (one 64-bit key per sample).              */
+size_t gdd_kmeans_assign_ws_bytes(int64_t n);
+int gdd_kmeans_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k,
+                      const float* C, const float* c_norm2, int32_t* labels, float* sq_dist,
+                      void* ws, size_t ws_bytes, gdd_stream_t stream);
+
+/* out[0] = sequential fp32 sum of sq_dist[i] * w[i] in sample order (w == NULL: ones); this is      */
+/* sklearn _inertia_dense with one OpenMP thread (_k_means_common.pyx:92-121).                       */
+int gdd_inertia(int64_t n, const float* sq_dist, const float* w, float* out, gdd_stream_t stream);
+
+/* MiniBatchKMeans center update, sklearn _minibatch_update_dense (_k_means_minibatch.pyx:11-108):    */
+/* for each cluster c with batch weight ws > 0: C_new[c] = (C_old[c]*W[c] + sum_{i in c, batch order} */
+/* X_i*w_i) * fp32(1/(W[c]+ws)), W[c] += ws; otherwise C_new[c] = C_old[c].                        */
+size_t gdd_minibatch_update_ws_bytes(int64_t b, int k);
+int gdd_minibatch_update(int64_t b, int dim, const float* X, const int64_t* rows, const float* w,
+                         const int32_t* labels, int k, const float* C_old, float* C_new,
+                         float* weight_sums, void* ws, size_t ws_bytes, gdd_stream_t stream);
+
+/* Stable grouping of samples by label: perm[offsets[c] .. offsets[c+1]) lists the samples of        */
+/* cluster c in ascending sample order; counts[c] = offsets[c+1]-offsets[c].                         */
+size_t gdd_group_ws_bytes(int64_t n, int k);
+int gdd_group_by_label(int64_t n, const int32_t* labels, int k, int32_t* perm, int32_t* offsets,
+                       void* ws, size_t ws_bytes, gdd_stream_t stream);
+
+/* Lloyd M-step accumulation, sklearn lloyd_iter_chunked_dense with one OpenMP thread                */
+/* (_k_means_lloyd.pyx:111-160, 208-213): sums[c,:] = sequential fp32 sum over the samples of c in    */
+/* sample order of X_i*w_i, wsum[c] = sequential fp32 sum of w_i.  Uses gdd_group_by_label output.    */
+int gdd_segment_sum_f32(int64_t n, int dim, const float* X, const float* w, const int32_t* perm,
+                        const int32_t* offsets, int k, float* sums, float* wsum, gdd_stream_t stream);
+
+/* Order-independent accumulation for sharded k-means: sums_fx[c,j] += llrint(X[i,j]*w_i * 2^scale)   */
+/* (int64, exact integer adds => identical on any rank count / order), counts[c] += 1. Zero both     */
+/* outputs first. rows == NULL: rows 0..n-1.                                                        */
+int gdd_segment_sum_fixed(int64_t n, int dim, const float* X, const float* w, const int32_t* labels,
+                          int k, int scale_exp, long long* sums_fx, long long* counts,
+                          gdd_stream_t stream);
+/* centers[c,j] = fp32( (double)sums_fx[c,j] * 2^-scale / counts[c] ); counts[c]==0 -> leaves row.   */
+int gdd_fixed_to_centers(int k, int dim, const long long* sums_fx, const long long* counts,
+                         int scale_exp, float* centers, gdd_stream_t stream);
+
+/* sklearn _average_centers (_k_means_common.pyx:215-236): w>0: C[c,:] *= fp32(1.0/(double)w);       */
+/* w==0: C[c,:] = C[argmax_w,:]. Then center_shift[c] = sqrt(||C_new[c]-C_old[c]||^2) in the          */
+/* _euclidean_dense_dense order (_center_shift :239-251).                                           */
+int gdd_average_centers(int k, int dim, float* C_new, const float* wsum, const float* C_old,
+                        float* center_shift, gdd_stream_t stream);
+
+/* Per-sample squared distance to a given center: out[i] = ||X[i] - C[labels[i]]||^2 in the          */
+/* _euclidean_dense_dense order; with the final labels this is the per-sample term of sklearn        */
+/* _inertia_dense (_k_means_common.pyx:92-121) used after the last Lloyd iteration.                  */
+int gdd_point_center_sqdist(int64_t n, int dim, const float* X, const int32_t* labels,
+                            const float* C, float* out, gdd_stream_t stream);
+
+/* 1 if any labels[i] != labels_old[i] (written to *changed as int32); then labels_old = labels.     */
+int gdd_labels_changed(int64_t n, const int32_t* labels, int32_t* labels_old, int32_t* changed,
+                       gdd_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* Greedy k-means++ seeding, sklearn _kmeans_plusplus (sklearn/cluster/_kmeans.py:174-272) on the    */
+/* device. Host supplies the reference RNG draws: first_id (random_state.choice) and                 */
+/* uniforms[(k-1) * n_trials] (random_state.uniform(size=n_trials) per center, concatenated).        */
+/* Distances: fp64 upcast -2<x_c,x> + |x_c|^2 + |x|^2, stored fp32, clipped at 0 (pairwise.py:582-650). */
+/* Potentials: fp32 sums (see DESIGN.md for their order). Writes centers (k x dim) and indices.      */
+/* ---------------------------------------------------------------------------------------------- */
+size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int n_trials);
+int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const float* w, int k, int n_trials,
+                        int64_t first_id, const double* uniforms, float* centers, int64_t* indices,
+                        void* ws, size_t ws_bytes, gdd_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* (a7) cluster-feature mean. Replaces clustgdd_agent_transduct.py:116-127 (induct :143-154) and the  */
+/* teacher index_add_/bincount means of distill_recsys.py:623-636.                                   */
+/* feat_syn[c,:] = fp32( (sequential fp64 sum over members of c in sample order) / count_c );         */
+/* count_c == 0 -> NaN row (reference: mean of an empty selection) unless empty_as_zero != 0          */
+/* (distill_recsys clamp_min(1) semantics -> zero row). counts: int64 per cluster.                   */
+/* ---------------------------------------------------------------------------------------------- */
+int gdd_cluster_mean(int64_t n, int d, const float* feat, const int32_t* perm, const int32_t* offsets,
+                     int k, int empty_as_zero, float* feat_syn, long long* counts,
+                     gdd_stream_t stream);
+/* labels_syn[c] = argmax_j centers[c,j] (first max wins, torch.argmax; transduct:126).              */
+int gdd_argmax_rows(int k, int dim, const float* centers, int64_t* out, gdd_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GDD_H_ */

@@ -1,0 +1,103 @@
+"""HIP normalisation / propagation vs the CPU oracle (bit-exact) — needs a gfx950 GPU."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+import gdd  # noqa: E402
+from gdd import synth  # noqa: E402
+
+
+def _graph(n, deg, seed, kind="chung_lu"):
+    return synth.chung_lu(n, deg, seed) if kind == "chung_lu" else synth.uniform_graph(n, deg, seed)
+
+
+def _csr_host(A):
+    A = sp.csr_matrix(A)
+    return A.indptr.astype(np.int32), A.indices.astype(np.int32), A.data.astype(np.float32)
+
+
+@pytest.mark.parametrize("case", ["binary", "selfloop0", "weighted", "isolated", "empty_rows"])
+def test_normalize_bitexact(case):
+    n = 700
+    A = _graph(n, 6.0, 3).tolil()
+    self_loops = -1
+    if case == "selfloop0":  # A[0,0] != 0 -> reference keeps fp32 and adds no I
+        A[0, 0] = 1.0
+    if case == "weighted":
+        A = sp.csr_matrix(A)
+        A.data = np.random.default_rng(0).uniform(0.1, 3.0, A.nnz).astype(np.float32)
+    if case == "isolated":
+        A = sp.csr_matrix(A)
+        A[5, :] = 0
+        A[:, 5] = 0
+        A.eliminate_zeros()
+    if case == "empty_rows":
+        self_loops = 0
+        A = sp.csr_matrix(A)
+        A[7, :] = 0
+        A.eliminate_zeros()
+    A = sp.csr_matrix(A)
+    A.sort_indices()
+    rp, col, val = _csr_host(A)
+    binary = case in ("binary", "isolated", "empty_rows")
+    ro, co, vo = O.normalize_csr(rp, col, None if binary else val, self_loops)
+    g = gdd.to_csr(A, binary=binary)
+    gn = gdd.normalize_adj(g, self_loops=self_loops)
+    assert np.array_equal(gn.rowptr.cpu().numpy(), ro)
+    assert np.array_equal(gn.col.cpu().numpy(), co)
+    assert np.array_equal(gn.val.cpu().numpy().view(np.uint32), vo.view(np.uint32))
+
+
+@pytest.mark.parametrize("d,T,alpha", [(128, 18, 0.91), (64, 5, 0.8), (7, 3, 0.5), (41, 4, 0.95),
+                                       (602, 3, 0.95), (100, 2, 0.91), (1, 1, 0.8)])
+def test_propagate_bitexact(d, T, alpha):
+    n = 3000
+    A = _graph(n, 12.0, 5)
+    # a hub row long enough to be split into several segments (GDD_PROP_SEG = 256)
+    A = A.tolil()
+    A[11, :] = 0
+    A[11, np.arange(0, n, 4)] = 1
+    A = sp.csr_matrix(A)
+    A.sort_indices()
+    rp, col, _ = _csr_host(A)
+    ro, co, vo = O.normalize_csr(rp, col, None, -1)
+    X = synth.features(n, d, 9)
+    t_ref, p_ref = O.propagate(ro, co, vo, X, T, alpha)
+    g = gdd.normalize_adj(gdd.to_csr(A))
+    t, p = gdd.propagate(g, torch.from_numpy(X).cuda(), T, alpha)
+    assert np.array_equal(t.cpu().numpy().view(np.uint32), t_ref.view(np.uint32))
+    assert np.array_equal(p.cpu().numpy().view(np.uint32), p_ref.view(np.uint32))
+
+
+def test_propagate_vs_torch_reference_loop():
+    """The reference loop with torch sparse mm (transduct:59-65) agrees within fp32 tolerance."""
+    n, d, T, alpha = 2000, 32, 10, 0.9
+    A = _graph(n, 8.0, 2)
+    g = gdd.normalize_adj(gdd.to_csr(A))
+    adj = g.to_torch_sparse()
+    X = torch.from_numpy(synth.features(n, d, 4)).cuda()
+    prop = X
+    target = (1 - alpha) * prop
+    for _ in range(1, T):
+        prop = alpha * adj @ prop
+        target = target + (1 - alpha) * prop
+    t, p = gdd.propagate(g, X, T, alpha)
+    torch.testing.assert_close(t, target, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(p, prop, rtol=1e-5, atol=1e-6)
+
+
+def test_spmm_matches_oracle():
+    n, d = 1500, 48
+    A = _graph(n, 10.0, 8)
+    rp, col, _ = _csr_host(A)
+    ro, co, vo = O.normalize_csr(rp, col, None, -1)
+    x = synth.features(n, d, 1)
+    y_ref = O.spmm(ro, co, vo, x, scale=0.7)
+    g = gdd.normalize_adj(gdd.to_csr(A))
+    y = gdd.spmm(g, torch.from_numpy(x).cuda(), 0.7)
+    assert np.array_equal(y.cpu().numpy().view(np.uint32), y_ref.view(np.uint32))

@@ -1,0 +1,139 @@
+"""HIP k-means primitives and estimators vs the CPU oracle (bit-exact) — needs a gfx950 GPU."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+import gdd  # noqa: E402
+from gdd import _lib, synth  # noqa: E402
+from gdd.kmeans import _Ops  # noqa: E402
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+@pytest.mark.parametrize("n,dim,k", [(1000, 40, 454), (5000, 7, 70), (777, 64, 1773),
+                                     (4096, 41, 769), (300, 47, 196), (129, 3, 5), (64, 300, 33)])
+def test_assign_bitexact(n, dim, k):
+    X = synth.blobs(n, dim, max(2, k // 3), seed=n + dim)
+    C = X[np.random.default_rng(1).choice(n, size=k, replace=k > n)] + 0.01
+    lab_ref, sq_ref = O.assign(X, C)
+    ops = _Ops("cuda", n, k, dim)
+    Xd, Cd = torch.from_numpy(X).cuda(), torch.from_numpy(np.ascontiguousarray(C)).cuda()
+    lab = torch.empty(n, dtype=torch.int32, device="cuda")
+    sq = torch.empty(n, dtype=torch.float32, device="cuda")
+    ops.assign(Xd, Cd, labels=lab, sq=sq)
+    assert np.array_equal(ops.cn2.cpu().numpy().view(np.uint32), bits(O.row_norms(C)))
+    assert np.array_equal(lab.cpu().numpy(), lab_ref)
+    assert np.array_equal(bits(sq.cpu().numpy()), bits(sq_ref))
+    assert float(ops.inertia(sq).item()) == O.lib().oracle_inertia(n, sq_ref, None)
+
+
+def test_assign_ties_lowest_index():
+    """Duplicate centres: the first (lowest-index) one must win (strict '<' scan)."""
+    X = synth.blobs(500, 8, 4, seed=3)
+    C = np.repeat(X[:10], 3, axis=0)  # every centre present three times
+    lab_ref, _ = O.assign(X, C)
+    ops = _Ops("cuda", 500, C.shape[0], 8)
+    lab = torch.empty(500, dtype=torch.int32, device="cuda")
+    ops.assign(torch.from_numpy(X).cuda(), torch.from_numpy(C).cuda(), labels=lab)
+    assert np.array_equal(lab.cpu().numpy(), lab_ref)
+    assert (lab_ref % 3 == 0).all()
+
+
+def test_gathered_rows():
+    X = synth.blobs(4000, 40, 30, seed=5)
+    rows = np.random.default_rng(2).integers(0, 4000, 1000)
+    C = X[:50].copy()
+    lab_ref, sq_ref = O.assign(X, C, rows=rows)
+    ops = _Ops("cuda", 1000, 50, 40)
+    lab = torch.empty(1000, dtype=torch.int32, device="cuda")
+    sq = torch.empty(1000, dtype=torch.float32, device="cuda")
+    ops.assign(torch.from_numpy(X).cuda(), torch.from_numpy(C).cuda(),
+               rows=torch.from_numpy(rows).cuda(), labels=lab, sq=sq)
+    assert np.array_equal(lab.cpu().numpy(), lab_ref)
+    assert np.array_equal(bits(sq.cpu().numpy()), bits(sq_ref))
+
+
+@pytest.mark.parametrize("n,dim,k", [(3000, 40, 454), (2708, 7, 70), (5000, 64, 300)])
+def test_kmeans_plusplus_bitexact(n, dim, k):
+    X = synth.blobs(n, dim, max(2, k // 4), seed=11)
+    c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
+    ops = _Ops("cuda", n, k, dim)
+    c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(15))
+    assert np.array_equal(idx.cpu().numpy(), idx_ref)
+    assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref))
+
+
+def test_minibatch_update_bitexact():
+    rng = np.random.default_rng(4)
+    X = synth.blobs(3000, 40, 20, seed=4)
+    k = 60
+    C = X[:k].copy()
+    W = rng.integers(0, 5, k).astype(np.float32)
+    rows = rng.integers(0, 3000, 1000)
+    lab = rng.integers(0, k, 1000).astype(np.int32)
+    W_ref = W.copy()
+    C_ref = O.minibatch_update(X[rows], lab, C, W_ref)
+    lib = _lib.device_lib()
+    Xd = torch.from_numpy(X).cuda()
+    Cd = torch.from_numpy(C).cuda()
+    Cn = torch.empty_like(Cd)
+    Wd = torch.from_numpy(W).cuda()
+    ws = _lib.workspace(lib.gdd_minibatch_update_ws_bytes(1000, k), "cuda")
+    rows_d = torch.from_numpy(rows).cuda()  # keep the device buffers alive across the launch
+    lab_d = torch.from_numpy(lab).cuda()
+    _lib.check(lib.gdd_minibatch_update(1000, 40, Xd.data_ptr(), rows_d.data_ptr(), None,
+                                        lab_d.data_ptr(), k, Cd.data_ptr(), Cn.data_ptr(),
+                                        Wd.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_ptr()))
+    assert np.array_equal(bits(Cn.cpu().numpy()), bits(C_ref))
+    assert np.array_equal(bits(Wd.cpu().numpy()), bits(W_ref))
+
+
+@pytest.mark.parametrize("n,dim,k,bs", [(5000, 40, 50, 1000), (20000, 41, 300, 1000),
+                                        (3000, 16, 700, 256)])
+def test_minibatch_kmeans_bitexact(n, dim, k, bs):
+    X = synth.blobs(n, dim, k, seed=7)
+    ref = O.minibatch_kmeans(X, k, random_state=15, batch_size=bs)
+    m = gdd.MiniBatchKMeans(n_clusters=k, random_state=15, batch_size=bs).fit(X)
+    assert m.n_steps_ == ref["n_steps_"]
+    assert np.array_equal(m.labels_, ref["labels_"])
+    assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"]))
+    assert m.inertia_ == ref["inertia_"]
+
+
+@pytest.mark.parametrize("n,dim,k,n_init", [(2708, 7, 70, "auto"), (2000, 64, 200, "auto"),
+                                            (1500, 10, 30, 3)])
+def test_kmeans_lloyd_bitexact(n, dim, k, n_init):
+    X = synth.blobs(n, dim, k // 2, seed=8)
+    np.random.seed(15)
+    ref = O.kmeans(X, k, n_init=n_init)
+    np.random.seed(15)
+    m = gdd.KMeans(n_clusters=k, n_init=n_init).fit(X)
+    assert m.n_iter_ == ref["n_iter_"]
+    assert np.array_equal(m.labels_, ref["labels_"])
+    assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"]))
+    assert m.inertia_ == ref["inertia_"]
+
+
+def test_cluster_mean_and_argmax():
+    n, d, k = 5000, 96, 40
+    feat = synth.features(n, d, 3)
+    lab = np.random.default_rng(3).integers(0, k, n).astype(np.int32)
+    lab[lab == 17] = 18  # one empty cluster -> NaN row
+    ref, cnt_ref = O.cluster_mean(feat, lab, k)
+    out, cnt = gdd.cluster_mean(torch.from_numpy(feat).cuda(), lab, k)
+    o = out.cpu().numpy()
+    assert np.array_equal(cnt.cpu().numpy(), cnt_ref)
+    assert np.isnan(o[17]).all() and np.isnan(ref[17]).all()
+    m = np.arange(k) != 17
+    assert np.array_equal(bits(o[m]), bits(ref[m]))
+    ref0, _ = O.cluster_mean(feat, lab, k, empty_as_zero=True)
+    out0, _ = gdd.cluster_mean(torch.from_numpy(feat).cuda(), lab, k, empty_as_zero=True)
+    assert np.array_equal(bits(out0.cpu().numpy()), bits(ref0))
+    C = synth.blobs(k, 40, 5, seed=2)
+    assert np.array_equal(gdd.argmax_rows(torch.from_numpy(C).cuda()).cpu().numpy(), np.argmax(C, -1))
