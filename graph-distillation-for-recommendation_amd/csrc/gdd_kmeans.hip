@@ -50,7 +50,13 @@ __device__ __forceinline__ float npy_sumsq(const float* __restrict__ x, int dim)
   return (a[0] + a[1]) + (a[2] + a[3]);
 }
 
-__global__ void k_row_norms(int64_t n, int dim, const float* __restrict__ X, float* __restrict__ out) {
+// `stop` (nullable) lets a minibatch step become a no-op once the device-side convergence test
+// has fired, so the host can enqueue steps ahead of the stopping decision.
+__device__ __forceinline__ bool stopped(const int32_t* stop) { return stop && *stop; }
+
+__global__ void k_row_norms(int64_t n, int dim, const float* __restrict__ X, float* __restrict__ out,
+                            const int32_t* __restrict__ stop) {
+  if (stopped(stop)) return;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = npy_sumsq(X + i * dim, dim);
 }
@@ -83,7 +89,9 @@ __device__ __forceinline__ unsigned long long pack_key(float d, int c) {
   return ((unsigned long long)u << 32) | (unsigned)c;
 }
 
-__global__ void k_fill_u64(int64_t n, unsigned long long* p, unsigned long long v) {
+__global__ void k_fill_u64(int64_t n, unsigned long long* p, unsigned long long v,
+                           const int32_t* __restrict__ stop) {
+  if (stopped(stop)) return;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
 }
@@ -101,7 +109,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_assign(int64_t n, int dim, int d
                                                        const int64_t* __restrict__ rows, int k,
                                                        const float* __restrict__ C,
                                                        const float* __restrict__ cn2, int cch,
-                                                       unsigned long long* __restrict__ keys) {
+                                                       unsigned long long* __restrict__ keys,
+                                                       const int32_t* __restrict__ stop) {
+  if (stopped(stop)) return;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int kPts = 32 * WAVES;
   const int S = dimp + 1;
@@ -161,7 +171,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_assign(int64_t n, int dim, int d
 __global__ void k_assign_finalize(int64_t n, int dim, const float* __restrict__ X,
                                   const int64_t* __restrict__ rows, const float* __restrict__ C,
                                   const unsigned long long* __restrict__ keys,
-                                  int32_t* __restrict__ labels, float* __restrict__ sq_dist) {
+                                  int32_t* __restrict__ labels, float* __restrict__ sq_dist,
+                                  const int32_t* __restrict__ stop) {
+  if (stopped(stop)) return;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const unsigned long long key = keys[i];
@@ -174,23 +186,77 @@ __global__ void k_assign_finalize(int64_t n, int dim, const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------------
-// inertia: sequential fp32 sum in sample order (one lane; the values are staged per 64 by the wave)
+// inertia: sequential fp32 sum in sample order. The block stages 4096 products at a time in LDS;
+// one lane folds them in order (float4 LDS reads keep the dependent add chain fed).
 // ---------------------------------------------------------------------------------------------
-__global__ void k_inertia(int64_t n, const float* __restrict__ sq, const float* __restrict__ w,
-                          float* __restrict__ out) {
-  __shared__ float buf[256];
+constexpr int kInertiaChunk = 4096;
+__global__ __launch_bounds__(1024) void k_inertia(int64_t n, const float* __restrict__ sq,
+                                                  const float* __restrict__ w,
+                                                  float* __restrict__ out,
+                                                  const int32_t* __restrict__ stop) {
+  if (stopped(stop)) return;
+  __shared__ __attribute__((aligned(16))) float buf[kInertiaChunk];
   float acc = 0.f;
-  for (int64_t b = 0; b < n; b += 256) {
-    const int64_t i = b + threadIdx.x;
-    if (i < n) buf[threadIdx.x] = w ? sq[i] * w[i] : sq[i] * 1.0f;
+  for (int64_t b = 0; b < n; b += kInertiaChunk) {
+    const int m = (int)min<int64_t>(kInertiaChunk, n - b);
+    for (int t = threadIdx.x; t < m; t += blockDim.x) {
+      const int64_t i = b + t;
+      buf[t] = w ? sq[i] * w[i] : sq[i] * 1.0f;  // sq_dist * sample_weight[i]
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-      const int m = (int)min<int64_t>(256, n - b);
-      for (int t = 0; t < m; ++t) acc = acc + buf[t];
+      const float4* b4 = reinterpret_cast<const float4*>(buf);
+      int t = 0;
+      for (; t + 4 <= m; t += 4) {
+        const float4 v = b4[t >> 2];
+        acc = acc + v.x;
+        acc = acc + v.y;
+        acc = acc + v.z;
+        acc = acc + v.w;
+      }
+      for (; t < m; ++t) acc = acc + buf[t];
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) out[0] = acc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// MiniBatchKMeans early stopping on the device: _mini_batch_convergence (_kmeans.py:1960-2027)
+// with Python-float (fp64, unfused) arithmetic, so the host need not read the inertia every step.
+// ---------------------------------------------------------------------------------------------
+struct MBState {
+  double ewa, ewa_min;
+  int32_t stop;          // first member: the `stop` flag the step kernels test
+  int32_t has_ewa, has_min, no_improvement;
+  int32_t stop_step;     // 0-based step index at which the loop broke (valid when stop)
+  int32_t pad[3];
+};
+
+__global__ void k_mb_converge(int step_i, int64_t bs, int64_t n, int max_no_improvement,
+                              const float* __restrict__ batch_inertia, MBState* __restrict__ st) {
+  if (threadIdx.x != 0 || blockIdx.x != 0 || st->stop) return;
+  const double bi = (double)batch_inertia[0] / (double)bs;
+  if (step_i == 0) return;  // the first step's inertia is the init's
+  if (!st->has_ewa) {
+    st->ewa = bi;
+    st->has_ewa = 1;
+  } else {
+    double a = (double)bs * 2.0 / (double)(n + 1);
+    a = a < 1.0 ? a : 1.0;
+    st->ewa = st->ewa * (1.0 - a) + bi * a;
+  }
+  if (!st->has_min || st->ewa < st->ewa_min) {
+    st->no_improvement = 0;
+    st->ewa_min = st->ewa;
+    st->has_min = 1;
+  } else {
+    st->no_improvement += 1;
+  }
+  if (max_no_improvement >= 0 && st->no_improvement >= max_no_improvement) {
+    st->stop = 1;
+    st->stop_step = step_i;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -203,7 +269,9 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
                                                         const float* __restrict__ C_old,
                                                         float* __restrict__ C_new,
                                                         float* __restrict__ Wsum,
-                                                        int32_t* __restrict__ members_ws) {
+                                                        int32_t* __restrict__ members_ws,
+                                                        const int32_t* __restrict__ stop) {
+  if (stopped(stop)) return;
   const int c = blockIdx.x;
   const int lane = threadIdx.x;
   int32_t* mem = members_ws + (int64_t)c * b;  // worst case: every batch sample in this cluster
@@ -422,7 +490,7 @@ using namespace gdd;
 extern "C" int gdd_row_norms(int64_t n, int dim, const float* X, float* out, gdd_stream_t stream) {
   GDD_REQUIRE(n >= 0 && dim > 0 && (n == 0 || (X && out)), "row_norms: bad arguments");
   if (n == 0) return GDD_OK;
-  k_row_norms<<<blocks_for(n), 256, 0, to_hip(stream)>>>(n, dim, X, out);
+  k_row_norms<<<blocks_for(n), 256, 0, to_hip(stream)>>>(n, dim, X, out, nullptr);
   GDD_LAUNCHED();
   return GDD_OK;
 }
@@ -433,6 +501,51 @@ size_t assign_lds(int waves, int dimp, int cch) {
   const int S = dimp + 1;
   const int ncp = (cch + 31) & ~31;
   return sizeof(float) * ((size_t)ncp * S + (size_t)32 * waves * S + ncp);
+}
+
+// keys fill + MFMA tiles + finalize (labels, optional per-sample sq_dist)
+int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k, const float* C,
+                  const float* c_norm2, int32_t* labels, float* sq_dist,
+                  unsigned long long* keys, const int32_t* stop, hipStream_t s) {
+  const int dimp = (dim + 1) & ~1;
+  // small batches: one wave per block so the grid still spreads over the chip
+  const int waves = n <= 4096 ? 1 : (dimp <= 96 ? 4 : (dimp <= 224 ? 2 : 1));
+  const int64_t gx = (n + 32 * waves - 1) / (32 * waves);
+  // centers per block: as many as fit the LDS budget (>= 32), then fewer while the grid is too
+  // small to occupy 256 CUs
+  const size_t budget = dimp <= 224 ? 65536 : 160000;
+  const int kp = (k + 31) & ~31;
+  int cch = 32;
+  while (cch + 32 <= kp && assign_lds(waves, dimp, cch + 32) <= budget) cch += 32;
+  int64_t gy = (k + cch - 1) / cch;
+  while (gx * gy < 1024 && cch > 32) {
+    cch -= 32;
+    gy = (k + cch - 1) / cch;
+  }
+  GDD_REQUIRE(gx < (1ll << 31) && gy < 65536, "assign: grid too large");
+  const size_t lds = assign_lds(waves, dimp, cch);
+  k_fill_u64<<<blocks_for(n), 256, 0, s>>>(n, keys, ~0ull, stop);
+  GDD_LAUNCHED();
+  dim3 grid((unsigned)gx, (unsigned)gy);
+  if (lds > 65536) {
+    // gfx950 has 160 KiB of LDS per CU; opt the kernel in to more than the 64 KiB default
+    if (waves == 2)
+      GDD_HIP(hipFuncSetAttribute((const void*)k_assign<2>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    else if (waves == 1)
+      GDD_HIP(hipFuncSetAttribute((const void*)k_assign<1>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  }
+  if (waves == 4)
+    k_assign<4><<<grid, 256, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys, stop);
+  else if (waves == 2)
+    k_assign<2><<<grid, 128, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys, stop);
+  else
+    k_assign<1><<<grid, 64, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys, stop);
+  GDD_LAUNCHED();
+  k_assign_finalize<<<blocks_for(n), 256, 0, s>>>(n, dim, X, rows, C, keys, labels, sq_dist, stop);
+  GDD_LAUNCHED();
+  return GDD_OK;
 }
 }  // namespace
 
@@ -449,52 +562,14 @@ extern "C" int gdd_kmeans_assign(int64_t n, int dim, const float* X, const int64
   if (n == 0) return GDD_OK;
   if (ws_bytes < gdd_kmeans_assign_ws_bytes(n))
     return fail(GDD_E_WORKSPACE, "assign: workspace %zu too small", ws_bytes);
-  hipStream_t s = to_hip(stream);
-  unsigned long long* keys = static_cast<unsigned long long*>(ws);
-  const int dimp = (dim + 1) & ~1;
-  const int waves = dimp <= 96 ? 4 : (dimp <= 224 ? 2 : 1);
-  const int64_t gx = (n + 32 * waves - 1) / (32 * waves);
-  // centers per block: as many as fit the LDS budget (>= 32), then fewer while the grid is too
-  // small to occupy 256 CUs (minibatch batches have only ~8 point tiles)
-  const size_t budget = dimp <= 224 ? 65536 : 160000;
-  const int kp = (k + 31) & ~31;
-  int cch = 32;
-  while (cch + 32 <= kp && assign_lds(waves, dimp, cch + 32) <= budget) cch += 32;
-  int64_t gy = (k + cch - 1) / cch;
-  while (gx * gy < 1024 && cch > 32) {
-    cch -= 32;
-    gy = (k + cch - 1) / cch;
-  }
-  GDD_REQUIRE(gx < (1ll << 31) && gy < 65536, "assign: grid too large");
-  const size_t lds = assign_lds(waves, dimp, cch);
-  k_fill_u64<<<blocks_for(n), 256, 0, s>>>(n, keys, ~0ull);
-  GDD_LAUNCHED();
-  dim3 grid((unsigned)gx, (unsigned)gy);
-  if (lds > 65536) {
-    // gfx950 has 160 KiB of LDS per CU; opt the kernel in to more than the 64 KiB default
-    if (waves == 2)
-      GDD_HIP(hipFuncSetAttribute((const void*)k_assign<2>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    else if (waves == 1)
-      GDD_HIP(hipFuncSetAttribute((const void*)k_assign<1>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  }
-  if (waves == 4)
-    k_assign<4><<<grid, 256, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys);
-  else if (waves == 2)
-    k_assign<2><<<grid, 128, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys);
-  else
-    k_assign<1><<<grid, 64, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys);
-  GDD_LAUNCHED();
-  k_assign_finalize<<<blocks_for(n), 256, 0, s>>>(n, dim, X, rows, C, keys, labels, sq_dist);
-  GDD_LAUNCHED();
-  return GDD_OK;
+  return launch_assign(n, dim, X, rows, k, C, c_norm2, labels, sq_dist,
+                       static_cast<unsigned long long*>(ws), nullptr, to_hip(stream));
 }
 
 extern "C" int gdd_inertia(int64_t n, const float* sq_dist, const float* w, float* out,
                            gdd_stream_t stream) {
   GDD_REQUIRE(n >= 0 && out && (n == 0 || sq_dist), "inertia: bad arguments");
-  k_inertia<<<1, 256, 0, to_hip(stream)>>>(n, sq_dist, w, out);
+  k_inertia<<<1, 1024, 0, to_hip(stream)>>>(n, sq_dist, w, out, nullptr);
   GDD_LAUNCHED();
   return GDD_OK;
 }
@@ -513,7 +588,72 @@ extern "C" int gdd_minibatch_update(int64_t b, int dim, const float* X, const in
   if (ws_bytes < gdd_minibatch_update_ws_bytes(b, k))
     return fail(GDD_E_WORKSPACE, "minibatch_update: workspace too small");
   k_minibatch_update<<<k, 64, 0, to_hip(stream)>>>(b, dim, X, rows, w, labels, k, C_old, C_new,
-                                                   weight_sums, static_cast<int32_t*>(ws));
+                                                   weight_sums, static_cast<int32_t*>(ws), nullptr);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+// ---- fused MiniBatchKMeans step (_mini_batch_step + _mini_batch_convergence) ------------------
+extern "C" size_t gdd_minibatch_state_bytes(void) { return sizeof(MBState); }
+
+extern "C" size_t gdd_minibatch_step_ws_bytes(int64_t b, int k) {
+  return gdd_kmeans_assign_ws_bytes(b) + gdd_minibatch_update_ws_bytes(b, k) +
+         align256(sizeof(float) * (size_t)std::max(k, 1)) +            // ||C||^2
+         align256(sizeof(float) * (size_t)std::max<int64_t>(b, 1)) +   // sq_dist
+         align256(sizeof(float)) + 1024;                               // batch inertia
+}
+
+extern "C" int gdd_minibatch_step(int64_t b, int dim, const float* X, const int64_t* rows, int k,
+                                  const float* C_old, float* C_new, float* weight_sums,
+                                  int32_t* labels, int step_i, int64_t n_samples,
+                                  int max_no_improvement, int converge, void* state, void* ws,
+                                  size_t ws_bytes, gdd_stream_t stream) {
+  GDD_REQUIRE(b > 0 && dim > 0 && dim <= 512 && k > 0 && n_samples > 0, "minibatch_step: bad shape");
+  GDD_REQUIRE(X && rows && C_old && C_new && weight_sums && labels && state && ws,
+              "minibatch_step: null pointer");
+  GDD_REQUIRE(C_old != C_new, "minibatch_step: C_old and C_new must differ");
+  if (ws_bytes < gdd_minibatch_step_ws_bytes(b, k))
+    return fail(GDD_E_WORKSPACE, "minibatch_step: workspace too small");
+  hipStream_t s = to_hip(stream);
+  MBState* st = static_cast<MBState*>(state);
+  const int32_t* stop = &st->stop;
+  Carver cv(ws, ws_bytes);
+  auto* keys = cv.take<unsigned long long>(b);
+  int32_t* members = cv.take<int32_t>((size_t)b * k);
+  float* cn2 = cv.take<float>(k);
+  float* sq = cv.take<float>(b);
+  float* inertia = cv.take<float>(1);
+  k_row_norms<<<blocks_for(k), 256, 0, s>>>(k, dim, C_old, cn2, stop);
+  GDD_LAUNCHED();
+  int rc = launch_assign(b, dim, X, rows, k, C_old, cn2, labels, sq, keys, stop, s);
+  if (rc) return rc;
+  k_inertia<<<1, 1024, 0, s>>>(b, sq, nullptr, inertia, stop);
+  GDD_LAUNCHED();
+  k_minibatch_update<<<k, 64, 0, s>>>(b, dim, X, rows, nullptr, labels, k, C_old, C_new,
+                                      weight_sums, members, stop);
+  GDD_LAUNCHED();
+  if (converge) {
+    k_mb_converge<<<1, 64, 0, s>>>(step_i, b, n_samples, max_no_improvement, inertia, st);
+    GDD_LAUNCHED();
+  }
+  return GDD_OK;
+}
+
+extern "C" int gdd_minibatch_converge(int64_t b, int k, int step_i, int64_t n_samples,
+                                      int max_no_improvement, void* state, void* ws,
+                                      size_t ws_bytes, gdd_stream_t stream) {
+  GDD_REQUIRE(b > 0 && k > 0 && n_samples > 0 && state && ws, "minibatch_converge: bad arguments");
+  if (ws_bytes < gdd_minibatch_step_ws_bytes(b, k))
+    return fail(GDD_E_WORKSPACE, "minibatch_converge: workspace too small");
+  // the batch inertia of the preceding gdd_minibatch_step, at its fixed workspace offset
+  Carver cv(ws, ws_bytes);
+  cv.take<unsigned long long>(b);
+  cv.take<int32_t>((size_t)b * k);
+  cv.take<float>(k);
+  cv.take<float>(b);
+  float* inertia = cv.take<float>(1);
+  k_mb_converge<<<1, 64, 0, to_hip(stream)>>>(step_i, b, n_samples, max_no_improvement, inertia,
+                                              static_cast<MBState*>(state));
   GDD_LAUNCHED();
   return GDD_OK;
 }

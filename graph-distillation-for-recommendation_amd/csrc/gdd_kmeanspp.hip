@@ -1,15 +1,15 @@
 // gdd_kmeanspp.hip — greedy k-means++ seeding on the device (sklearn _kmeans_plusplus,
 // sklearn/cluster/_kmeans.py:174-272), with the host's RNG draws passed in.
 //
-// One persistent workgroup of 1024 threads runs all k-1 seeding rounds with block barriers only
-// (no host round trips); the working set (closest distances, candidate distances, the fp64
-// cumulative potential) stays in L2. Per round c = 1..k-1:
-//   1. cum[i]  = inclusive fp64 prefix of fp32(w_i * closest_i)       (stable_cumsum, fp64)
-//   2. cand[t] = searchsorted_left(cum, u[c-1][t] * (double)pot), clipped to n-1
-//   3. dist[t][i] = min(closest_i, fp32(max(0, ((-2<x_cand, x_i>) + |x_cand|^2) + |x_i|^2)))
-//      (fp64 upcast distances stored as fp32: sklearn/metrics/pairwise.py:582-650; np.minimum)
-//   4. pot[t] = fp32 dot(dist[t], w) in the OpenBLAS SkylakeX sdot order
-//   5. best = first argmin pot; pot = pot[best]; closest = dist[best]; centers[c] = X[cand[best]]
+// Per seeding round c = 1..k-1 (three launches, no host round trip; `best` and the current
+// potential live in device memory):
+//   scan_search  (1 block)  cum[i] = inclusive fp64 prefix of fp32(w_i * closest_i)   (stable_cumsum)
+//                           cand[t] = searchsorted_left(cum, u[c-1][t] * (double)pot), clip n-1
+//   dist         (grid)     dist[t][i] = np.minimum(closest_i, fp32(max(0, ((-2<x_cand,x_i>) +
+//                           |x_cand|^2) + |x_i|^2)))   (fp64 upcast, pairwise.py:582-650)
+//   select       (1 block)  pot[t] = OpenBLAS-SkylakeX-order fp32 dot(dist[t], w); best = first
+//                           argmin; centers[c] = X[cand[best]]; closest := dist[best] (by index)
+// `closest` is never copied: round c reads dist[(c-1)&1][best_{c-1}].
 #include <algorithm>
 
 #include "gdd_common.hpp"
@@ -17,15 +17,23 @@
 namespace gdd {
 namespace {
 
-constexpr int kThreads = 1024;
 constexpr int kMaxTrials = 16;
+constexpr int kScanThreads = 1024;
+
+struct KppState {
+  float pot;        // current potential (fp32, as sklearn keeps it)
+  int best;         // best trial of the previous round
+  int64_t cand[kMaxTrials];
+  double cnorm[kMaxTrials];
+};
 
 // OpenBLAS 0.3.28/29 SkylakeX sdot (kernel/x86_64/sdot.c + sdot_microk_skylakex-2.c), emulated by
 // one wave: the 64 lanes are the 4 x 16 AVX-512 accumulators of the 64-wide loop; they fold to
 // 4 x 8 AVX2 accumulators for the 32-wide remainder; lanes then combine ((a0+a1)+a2)+a3, 8 -> 4 by
-// halves, and (h0+h1)+(h2+h3); the scalar tail is added in double. Called by all 64 lanes of a wave.
+// halves, and (h0+h1)+(h2+h3); the scalar tail is added in double. All 64 lanes call it; lane 0
+// returns the value.
 __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restrict__ y, int64_t n,
-                               float* scratch /* 64 floats of LDS for this wave */) {
+                               float* scratch /* 64 floats of LDS owned by this wave */) {
   const int lane = threadIdx.x & 63;
   const int64_t n1 = n & ~31ll;
   const int64_t n64 = n1 & ~63ll;
@@ -38,14 +46,21 @@ __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restr
   float r = 0.f;
   if (lane == 0) {
     float acc[4][8];
+#pragma unroll
     for (int u = 0; u < 4; ++u)
+#pragma unroll
       for (int l = 0; l < 8; ++l) acc[u][l] = scratch[u * 16 + l] + scratch[u * 16 + l + 8];
     for (int64_t i = n64; i < n1; i += 32)
+#pragma unroll
       for (int u = 0; u < 4; ++u)
-        for (int l = 0; l < 8; ++l) acc[u][l] = __builtin_fmaf(x[i + u * 8 + l], y[i + u * 8 + l], acc[u][l]);
+#pragma unroll
+        for (int l = 0; l < 8; ++l)
+          acc[u][l] = __builtin_fmaf(x[i + u * 8 + l], y[i + u * 8 + l], acc[u][l]);
     float s[8];
+#pragma unroll
     for (int l = 0; l < 8; ++l) s[l] = ((acc[0][l] + acc[1][l]) + acc[2][l]) + acc[3][l];
     float h[4];
+#pragma unroll
     for (int l = 0; l < 4; ++l) h[l] = s[l] + s[l + 4];
     double dot = n1 ? (double)((h[0] + h[1]) + (h[2] + h[3])) : 0.0;
     for (int64_t i = n1; i < n; ++i) {
@@ -62,133 +77,136 @@ __device__ __forceinline__ float np_minimum(float a, float b) {
   return b < a ? b : a;
 }
 
-__global__ __launch_bounds__(kThreads) void k_kpp(int64_t n, int dim, const float* __restrict__ X,
-                                                  const float* __restrict__ w, int k, int T,
-                                                  int64_t first_id,
-                                                  const double* __restrict__ uniforms,
-                                                  float* __restrict__ centers,
-                                                  int64_t* __restrict__ indices,
-                                                  double* __restrict__ xsq,
-                                                  float* __restrict__ closest,
-                                                  float* __restrict__ dist,
-                                                  double* __restrict__ cum) {
-  __shared__ double s_part[kThreads];
-  __shared__ float s_scratch[kThreads];
-  __shared__ int64_t s_cand[kMaxTrials];
-  __shared__ float s_pot[kMaxTrials];
-  __shared__ double s_cnorm[kMaxTrials];
-  __shared__ float s_cur_pot;
-  __shared__ int s_best;
+// |x|^2 in fp64 (row_norms of the upcast chunk) and the distances to the first center
+__global__ void k_kpp_init(int64_t n, int dim, const float* __restrict__ X, int64_t first_id,
+                           double* __restrict__ xsq, float* __restrict__ closest) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* xi = X + i * dim;
+  const float* xc = X + first_id * dim;
+  double s = 0.0, sc = 0.0, dot = 0.0;
+  for (int j = 0; j < dim; ++j) {
+    const double v = (double)xi[j], c = (double)xc[j];
+    s = __builtin_fma(v, v, s);
+    sc = __builtin_fma(c, c, sc);
+    dot = __builtin_fma(c, v, dot);
+  }
+  xsq[i] = s;
+  const float f = (float)(((-2.0 * dot) + sc) + s);
+  closest[i] = f < 0.f ? 0.f : f;
+}
+
+__global__ __launch_bounds__(64) void k_kpp_first_pot(int64_t n, int dim, const float* __restrict__ X,
+                                                      const float* __restrict__ w,
+                                                      const float* __restrict__ closest,
+                                                      int64_t first_id, float* __restrict__ centers,
+                                                      int64_t* __restrict__ indices,
+                                                      KppState* __restrict__ st) {
+  __shared__ float scratch[64];
+  const float p = sdot_skx_wave(closest, w, n, scratch);
+  if (threadIdx.x == 0) {
+    st->pot = p;
+    st->best = 0;
+    indices[0] = first_id;
+  }
+  for (int j = threadIdx.x; j < dim; j += 64) centers[j] = X[first_id * dim + j];
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_kpp_scan_search(
+    int64_t n, const float* __restrict__ w, const float* __restrict__ closest0,
+    const float* __restrict__ dist_prev, int use_prev, const double* __restrict__ u, int T,
+    const double* __restrict__ xsq, double* __restrict__ cum, KppState* __restrict__ st) {
+  __shared__ double s_part[kScanThreads];
   const int tid = threadIdx.x;
-  const int wave = tid >> 6;
+  const float* closest = use_prev ? dist_prev + (int64_t)st->best * n : closest0;
+  const int64_t chunk = (n + kScanThreads - 1) / kScanThreads;
+  const int64_t lo = min<int64_t>(n, tid * chunk), hi = min<int64_t>(n, lo + chunk);
+  double run = 0.0;
+  for (int64_t i = lo; i < hi; ++i) run = run + (double)(w[i] * closest[i]);
+  s_part[tid] = run;
+  __syncthreads();
+  for (int off = 1; off < kScanThreads; off <<= 1) {
+    const double v = tid >= off ? s_part[tid - off] : 0.0;
+    __syncthreads();
+    s_part[tid] += v;
+    __syncthreads();
+  }
+  double base = tid ? s_part[tid - 1] : 0.0;
+  for (int64_t i = lo; i < hi; ++i) {
+    base = base + (double)(w[i] * closest[i]);
+    cum[i] = base;
+  }
+  __syncthreads();
+  __threadfence_block();
+  if (tid < T) {
+    const double r = u[tid] * (double)st->pot;
+    int64_t a = 0, b = n;  // first index with cum[idx] >= r  (np.searchsorted side='left')
+    while (a < b) {
+      const int64_t m = (a + b) >> 1;
+      if (cum[m] < r)
+        a = m + 1;
+      else
+        b = m;
+    }
+    if (a > n - 1) a = n - 1;
+    st->cand[tid] = a;
+    st->cnorm[tid] = xsq[a];
+  }
+}
 
-  // |x_i|^2 in fp64 (row_norms of the upcast chunk)
-  for (int64_t i = tid; i < n; i += kThreads) {
-    double s = 0.0;
-    for (int j = 0; j < dim; ++j) {
-      const double v = (double)X[i * dim + j];
-      s = __builtin_fma(v, v, s);
-    }
-    xsq[i] = s;
-  }
-  // first center
-  for (int j = tid; j < dim; j += kThreads) centers[j] = X[first_id * dim + j];
-  if (tid == 0) indices[0] = first_id;
+// dist[t][i] for a 256-point tile; the T candidate rows are staged in LDS as fp64
+__global__ __launch_bounds__(256) void k_kpp_dist(int64_t n, int dim, const float* __restrict__ X,
+                                                  const double* __restrict__ xsq,
+                                                  const float* __restrict__ closest0,
+                                                  const float* __restrict__ dist_prev, int use_prev,
+                                                  const KppState* __restrict__ st,
+                                                  float* __restrict__ dist, int T) {
+  extern __shared__ double s_c[];  // T x dim
+  const int t = blockIdx.y;
+  const int64_t ct = st->cand[t];
+  for (int j = threadIdx.x; j < dim; j += blockDim.x) s_c[j] = (double)X[ct * dim + j];
   __syncthreads();
-  // closest distances to the first center
-  {
-    const float* xc = X + first_id * dim;
-    const double cn = xsq[first_id];
-    for (int64_t i = tid; i < n; i += kThreads) {
-      double dot = 0.0;
-      for (int j = 0; j < dim; ++j) dot = __builtin_fma((double)xc[j], (double)X[i * dim + j], dot);
-      double d = ((-2.0 * dot) + cn) + xsq[i];
-      float f = (float)d;
-      closest[i] = f < 0.f ? 0.f : f;
-    }
-  }
-  __syncthreads();
-  if (wave == 0) {
-    float p = sdot_skx_wave(closest, w, n, s_scratch);
-    if (tid == 0) s_cur_pot = p;
-  }
-  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* closest = use_prev ? dist_prev + (int64_t)st->best * n : closest0;
+  const float* xi = X + i * dim;
+  double dot = 0.0;
+  for (int j = 0; j < dim; ++j) dot = __builtin_fma(s_c[j], (double)xi[j], dot);
+  const double d = ((-2.0 * dot) + st->cnorm[t]) + xsq[i];
+  float f = (float)d;
+  f = f < 0.f ? 0.f : f;
+  dist[(int64_t)t * n + i] = np_minimum(closest[i], f);
+}
 
-  const int64_t chunk = (n + kThreads - 1) / kThreads;
-  for (int c = 1; c < k; ++c) {
-    // 1. fp64 cumulative potential: per-thread contiguous chunks, block scan of chunk totals
-    const int64_t lo = tid * chunk, hi = min<int64_t>(n, lo + chunk);
-    double run = 0.0;
-    for (int64_t i = lo; i < hi; ++i) run = run + (double)(w[i] * closest[i]);
-    s_part[tid] = run;
-    __syncthreads();
-    for (int off = 1; off < kThreads; off <<= 1) {
-      double v = tid >= off ? s_part[tid - off] : 0.0;
-      __syncthreads();
-      s_part[tid] += v;
-      __syncthreads();
-    }
-    double base = tid ? s_part[tid - 1] : 0.0;
-    for (int64_t i = lo; i < hi; ++i) {
-      base = base + (double)(w[i] * closest[i]);
-      cum[i] = base;
-    }
-    __syncthreads();
-    // 2. candidates: np.searchsorted(cum, u * pot) (side='left'), clipped to n-1
-    if (tid < T) {
-      const double r = uniforms[(int64_t)(c - 1) * T + tid] * (double)s_cur_pot;
-      int64_t a = 0, b = n;  // first index with cum[idx] >= r
-      while (a < b) {
-        const int64_t m = (a + b) >> 1;
-        if (cum[m] < r)
-          a = m + 1;
-        else
-          b = m;
-      }
-      if (a > n - 1) a = n - 1;
-      s_cand[tid] = a;
-      s_cnorm[tid] = xsq[a];
-    }
-    __syncthreads();
-    // 3. distances to every candidate, min with closest
-    for (int64_t i = tid; i < n; i += kThreads) {
-      const float cl = closest[i];
-      for (int t = 0; t < T; ++t) {
-        const float* xc = X + s_cand[t] * dim;
-        double dot = 0.0;
-        for (int j = 0; j < dim; ++j)
-          dot = __builtin_fma((double)xc[j], (double)X[i * dim + j], dot);
-        const double d = ((-2.0 * dot) + s_cnorm[t]) + xsq[i];
-        float f = (float)d;
-        f = f < 0.f ? 0.f : f;
-        dist[(int64_t)t * n + i] = np_minimum(cl, f);
-      }
-    }
-    __syncthreads();
-    // 4. candidate potentials, one wave per candidate
-    if (wave < T) {
-      const float p = sdot_skx_wave(dist + (int64_t)wave * n, w, n, s_scratch + wave * 64);
-      if ((tid & 63) == 0) s_pot[wave] = p;
-    }
-    __syncthreads();
-    // 5. pick the best candidate (np.argmin: first minimum, NaN wins)
-    if (tid == 0) {
-      int b = 0;
-      for (int t = 1; t < T; ++t) {
-        const float pb = s_pot[b], pt = s_pot[t];
-        if (pb == pb && (pt < pb || pt != pt)) b = t;
-      }
-      s_best = b;
-      s_cur_pot = s_pot[b];
-      indices[c] = s_cand[b];
-    }
-    __syncthreads();
-    const int b = s_best;
-    const float* src = dist + (int64_t)b * n;
-    for (int64_t i = tid; i < n; i += kThreads) closest[i] = src[i];
-    for (int j = tid; j < dim; j += kThreads) centers[(int64_t)c * dim + j] = X[s_cand[b] * dim + j];
-    __syncthreads();
+__global__ __launch_bounds__(1024) void k_kpp_select(int64_t n, int dim, const float* __restrict__ X,
+                                                     const float* __restrict__ w,
+                                                     const float* __restrict__ dist, int T, int c,
+                                                     float* __restrict__ centers,
+                                                     int64_t* __restrict__ indices,
+                                                     KppState* __restrict__ st) {
+  __shared__ float scratch[kMaxTrials * 64];
+  __shared__ float s_pot[kMaxTrials];
+  __shared__ int s_best;
+  const int wave = threadIdx.x >> 6;
+  if (wave < T) {
+    const float p = sdot_skx_wave(dist + (int64_t)wave * n, w, n, scratch + wave * 64);
+    if ((threadIdx.x & 63) == 0) s_pot[wave] = p;
   }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int b = 0;  // np.argmin: first minimum; a NaN is returned as soon as it is met
+    for (int t = 1; t < T; ++t) {
+      const float pb = s_pot[b], pt = s_pot[t];
+      if (pb == pb && (pt < pb || pt != pt)) b = t;
+    }
+    s_best = b;
+    st->best = b;
+    st->pot = s_pot[b];
+    indices[c] = st->cand[b];
+  }
+  __syncthreads();
+  const int64_t src = st->cand[s_best];
+  for (int j = threadIdx.x; j < dim; j += blockDim.x) centers[(int64_t)c * dim + j] = X[src * dim + j];
 }
 
 __global__ void k_ones(int64_t n, float* p) {
@@ -203,12 +221,13 @@ using namespace gdd;
 
 extern "C" size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int n_trials) {
   size_t b = 0;
-  b += align256(sizeof(double) * n);                          // xsq
-  b += align256(sizeof(float) * n);                           // closest
-  b += align256(sizeof(float) * n * (size_t)std::max(n_trials, 1));  // dist
-  b += align256(sizeof(double) * n);                          // cum
-  b += align256(sizeof(float) * n);                           // ones (w == NULL)
-  return b + 1024;
+  b += align256(sizeof(KppState));
+  b += align256(sizeof(double) * n);                                        // xsq
+  b += align256(sizeof(float) * n);                                         // closest0
+  b += 2 * align256(sizeof(float) * n * (size_t)std::max(n_trials, 1));     // dist ping-pong
+  b += align256(sizeof(double) * n);                                        // cum
+  b += align256(sizeof(float) * n);                                         // ones (w == NULL)
+  return b + 2048;
 }
 
 extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const float* w, int k,
@@ -219,23 +238,45 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
               (long long)n, dim, k);
   GDD_REQUIRE(n_trials >= 1 && n_trials <= kMaxTrials, "kmeans++: n_trials=%d unsupported",
               n_trials);
+  GDD_REQUIRE(dim <= 4096, "kmeans++: dim=%d unsupported", dim);
   GDD_REQUIRE(first_id >= 0 && first_id < n, "kmeans++: first_id out of range");
   GDD_REQUIRE(X && centers && indices && ws && (k == 1 || uniforms), "kmeans++: null pointer");
   hipStream_t s = to_hip(stream);
   Carver cv(ws, ws_bytes);
+  KppState* st = cv.take<KppState>(1);
   double* xsq = cv.take<double>(n);
-  float* closest = cv.take<float>(n);
-  float* dist = cv.take<float>(n * (size_t)n_trials);
+  float* closest0 = cv.take<float>(n);
+  float* dist[2] = {cv.take<float>(n * (size_t)n_trials), cv.take<float>(n * (size_t)n_trials)};
   double* cum = cv.take<double>(n);
   float* ones = cv.take<float>(n);
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans++: workspace too small");
+  const unsigned nb = (unsigned)((n + 255) / 256);
   if (!w) {
-    k_ones<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(n, ones);
+    k_ones<<<nb, 256, 0, s>>>(n, ones);
     GDD_LAUNCHED();
     w = ones;
   }
-  k_kpp<<<1, kThreads, 0, s>>>(n, dim, X, w, k, n_trials, first_id, uniforms, centers, indices, xsq,
-                               closest, dist, cum);
+  k_kpp_init<<<nb, 256, 0, s>>>(n, dim, X, first_id, xsq, closest0);
   GDD_LAUNCHED();
+  k_kpp_first_pot<<<1, 64, 0, s>>>(n, dim, X, w, closest0, first_id, centers, indices, st);
+  GDD_LAUNCHED();
+  const size_t lds = sizeof(double) * (size_t)dim;
+  if (lds > 65536)
+    GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dist, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+  for (int c = 1; c < k; ++c) {
+    const int use_prev = c > 1;
+    const float* prev = dist[(c - 1) & 1];
+    float* cur = dist[c & 1];
+    k_kpp_scan_search<<<1, kScanThreads, 0, s>>>(n, w, closest0, prev, use_prev,
+                                                 uniforms + (int64_t)(c - 1) * n_trials, n_trials,
+                                                 xsq, cum, st);
+    GDD_LAUNCHED();
+    k_kpp_dist<<<dim3(nb, n_trials), 256, lds, s>>>(n, dim, X, xsq, closest0, prev, use_prev, st,
+                                                   cur, n_trials);
+    GDD_LAUNCHED();
+    k_kpp_select<<<1, 64 * n_trials, 0, s>>>(n, dim, X, w, cur, n_trials, c, centers, indices, st);
+    GDD_LAUNCHED();
+  }
   return GDD_OK;
 }

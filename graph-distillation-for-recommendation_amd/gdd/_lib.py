@@ -45,6 +45,12 @@ SIGNATURES = {
     "gdd_minibatch_update_ws_bytes": (_c_size, [_c_i64, _c_int]),
     "gdd_minibatch_update": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp,
                                       _vp, _c_size, _vp]),
+    "gdd_minibatch_state_bytes": (_c_size, []),
+    "gdd_minibatch_step_ws_bytes": (_c_size, [_c_i64, _c_int]),
+    "gdd_minibatch_step": (_c_int, [_c_i64, _c_int, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int,
+                                    _c_i64, _c_int, _c_int, _vp, _vp, _c_size, _vp]),
+    "gdd_minibatch_converge": (_c_int, [_c_i64, _c_int, _c_int, _c_i64, _c_int, _vp, _vp, _c_size,
+                                        _vp]),
     "gdd_group_ws_bytes": (_c_size, [_c_i64, _c_int]),
     "gdd_group_by_label": (_c_int, [_c_i64, _vp, _c_int, _vp, _vp, _vp, _c_size, _vp]),
     "gdd_segment_sum_f32": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp]),

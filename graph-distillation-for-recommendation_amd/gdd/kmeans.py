@@ -190,79 +190,11 @@ class MiniBatchKMeans(_BaseKMeans):
             if best_inertia is None or inertia < best_inertia:
                 init_centers, best_inertia = centers, inertia
 
-        C = init_centers.contiguous()
-        C_new = torch.empty_like(C)
-        counts = torch.zeros(k, dtype=torch.float32, device=dev)
-        ws_mb = _lib.workspace(ops.lib.gdd_minibatch_update_ws_bytes(bs, k), dev)
-        labels_b = torch.empty(bs, dtype=torch.int32, device=dev)
-        sq_b = torch.empty(bs, dtype=torch.float32, device=dev)
-        rows_pinned = torch.empty(bs, dtype=torch.int64, pin_memory=True)
-        rows_d = torch.empty(bs, dtype=torch.int64, device=dev)
-        any_zero = True  # counts start at zero
-        ewa = ewa_min = None
-        no_improvement = 0
-        n_since = 0
         n_steps = (self.max_iter * n) // bs
-        tol_ = 0.0
         if self.tol > 0:
-            tol_ = float(torch.var(Xd, dim=0, unbiased=False).mean().item()) * self.tol
-        stream = ops.stream
-        i = 0
-        for i in range(n_steps):
-            mb = rs.randint(0, n, bs)
-            n_since += bs
-            if any_zero or n_since >= 10 * k:  # _random_reassign (:2029-2043)
-                n_since = 0
-                rr = True
-            else:
-                rr = False
-            rows_pinned.numpy()[:] = mb
-            rows_d.copy_(rows_pinned, non_blocking=True)
-            ops.assign(Xd, C, rows=rows_d, labels=labels_b, sq=sq_b)
-            bi_d = ops.inertia(sq_b)
-            _lib.check(ops.lib.gdd_minibatch_update(bs, dim, Xd.data_ptr(), rows_d.data_ptr(), None,
-                                                    labels_b.data_ptr(), k, C.data_ptr(),
-                                                    C_new.data_ptr(), counts.data_ptr(),
-                                                    ws_mb.data_ptr(), ws_mb.numel(), stream))
-            if rr and self.reassignment_ratio > 0:  # _mini_batch_step (:1640-1667)
-                W = counts.cpu().numpy()
-                to_reassign = W < self.reassignment_ratio * W.max()
-                if to_reassign.sum() > 0.5 * bs:
-                    dont = np.argsort(W)[int(0.5 * bs):]
-                    to_reassign[dont] = False
-                n_re = int(to_reassign.sum())
-                if n_re:
-                    new_centers = rs.choice(bs, replace=False, size=n_re)
-                    dst = torch.from_numpy(np.where(to_reassign)[0]).to(dev)
-                    src = rows_d.index_select(0, torch.from_numpy(new_centers).to(dev))
-                    C_new.index_copy_(0, dst, Xd.index_select(0, src))
-                W[to_reassign] = np.min(W[~to_reassign])
-                counts.copy_(torch.from_numpy(W))
-                any_zero = bool((W == 0).any())
-            if tol_ > 0:
-                sq_diff = float(((C_new - C) ** 2).sum().item())
-            else:
-                sq_diff = 0
-            C, C_new = C_new, C
-            # _mini_batch_convergence (:1960-2027), Python floats as in sklearn
-            bi = float(bi_d.item()) / bs
-            step = i + 1
-            if step == 1:
-                continue
-            if ewa is None:
-                ewa = bi
-            else:
-                a = min(bs * 2.0 / (n + 1), 1)
-                ewa = ewa * (1 - a) + bi * a
-            if tol_ > 0.0 and sq_diff <= tol_:
-                break
-            if ewa_min is None or ewa < ewa_min:
-                no_improvement = 0
-                ewa_min = ewa
-            else:
-                no_improvement += 1
-            if self.max_no_improvement is not None and no_improvement >= self.max_no_improvement:
-                break
+            C, i, ewa = self._steps_sync(ops, Xd, init_centers, rs, n, bs, n_steps)
+        else:
+            C, i, ewa = self._steps_async(ops, Xd, init_centers, rs, n, bs, n_steps)
         self.n_steps_ = i + 1
         self.n_iter_ = int(np.ceil(((i + 1) * bs) / n))
         self.cluster_centers_device_ = C
@@ -277,6 +209,140 @@ class MiniBatchKMeans(_BaseKMeans):
         else:
             self.inertia_ = ewa * n if ewa is not None else 0.0
         return self
+
+    # -- the step loop -------------------------------------------------------------------------
+    def _reassign(self, ops, Xd, rows_d, C_new, counts, rs, bs):
+        """Low-count reassignment of _mini_batch_step (:1640-1667): numpy on the k-vector of counts
+        (same expressions as sklearn, so argsort tie order and RNG use are identical)."""
+        dev = Xd.device
+        W = counts.cpu().numpy()
+        to_reassign = W < self.reassignment_ratio * W.max()
+        if to_reassign.sum() > 0.5 * bs:
+            dont = np.argsort(W)[int(0.5 * bs):]
+            to_reassign[dont] = False
+        n_re = int(to_reassign.sum())
+        if n_re:
+            new_centers = rs.choice(bs, replace=False, size=n_re)
+            dst = torch.from_numpy(np.where(to_reassign)[0]).to(dev)
+            src = rows_d.index_select(0, torch.from_numpy(new_centers).to(dev))
+            C_new.index_copy_(0, dst, Xd.index_select(0, src))
+        W[to_reassign] = np.min(W[~to_reassign])
+        counts.copy_(torch.from_numpy(W))
+        return bool((W == 0).any())
+
+    def _steps_async(self, ops, Xd, C0, rs, n, bs, n_steps):
+        """Steps are enqueued in chunks that end at the next reassignment step (the only point the
+        host must look at device state); early stopping runs on the device (gdd_minibatch_step),
+        which turns the remaining enqueued steps into no-ops. One H2D copy of the chunk's batch
+        indices and one synchronisation per chunk."""
+        lib, dev, k, dim = ops.lib, Xd.device, self.n_clusters, Xd.shape[1]
+        stream = ops.stream
+        bufs = [C0.contiguous(), torch.empty_like(C0)]
+        counts = torch.zeros(k, dtype=torch.float32, device=dev)
+        labels_b = torch.empty(bs, dtype=torch.int32, device=dev)
+        state = torch.zeros(lib.gdd_minibatch_state_bytes(), dtype=torch.uint8, device=dev)
+        ws = _lib.workspace(lib.gdd_minibatch_step_ws_bytes(bs, k), dev)
+        max_ni = -1 if self.max_no_improvement is None else int(self.max_no_improvement)
+        chunk_cap = 64
+        rows_pin = torch.empty((chunk_cap, bs), dtype=torch.int64, pin_memory=True)
+        rows_d = torch.empty((chunk_cap, bs), dtype=torch.int64, device=dev)
+        any_zero, n_since = True, 0
+        i = 0
+        stop_step = None
+        while i < n_steps and stop_step is None:
+            snapshot = rs.get_state()
+            chunk = []
+            while i + len(chunk) < n_steps and len(chunk) < chunk_cap:
+                mb = rs.randint(0, n, bs)
+                n_since += bs
+                rr = any_zero or n_since >= 10 * k  # _random_reassign (:2029-2043)
+                if rr:
+                    n_since = 0
+                rows_pin[len(chunk)].numpy()[:] = mb
+                chunk.append(rr)
+                if rr:
+                    break
+            m = len(chunk)
+            rows_d[:m].copy_(rows_pin[:m], non_blocking=True)
+            for j, rr in enumerate(chunk):
+                s = i + j
+                c_old, c_new = bufs[s % 2], bufs[(s + 1) % 2]
+                do_re = rr and self.reassignment_ratio > 0
+                _lib.check(lib.gdd_minibatch_step(
+                    bs, dim, Xd.data_ptr(), rows_d[j].data_ptr(), k, c_old.data_ptr(),
+                    c_new.data_ptr(), counts.data_ptr(), labels_b.data_ptr(), s, n, max_ni,
+                    0 if do_re else 1, state.data_ptr(), ws.data_ptr(), ws.numel(), stream))
+                if do_re:
+                    st = state[16:36].cpu().view(torch.int32)
+                    if int(st[0]):
+                        stop_step = int(st[4])
+                        break
+                    any_zero = self._reassign(ops, Xd, rows_d[j], c_new, counts, rs, bs)
+                    _lib.check(lib.gdd_minibatch_converge(bs, k, s, n, max_ni, state.data_ptr(),
+                                                          ws.data_ptr(), ws.numel(), stream))
+            if stop_step is None:
+                st = state[16:36].cpu().view(torch.int32)
+                if int(st[0]):
+                    stop_step = int(st[4])
+            if stop_step is not None and stop_step < i + m - 1:
+                # sklearn drew batch indices only up to the stopping step: rewind the generator
+                rs.set_state(snapshot)
+                for _ in range(stop_step - i + 1):
+                    rs.randint(0, n, bs)
+            i += m
+        last = n_steps - 1 if stop_step is None else stop_step
+        ewa = float(state[0:8].cpu().view(torch.float64)[0])
+        return bufs[(last + 1) % 2], last, ewa
+
+    def _steps_sync(self, ops, Xd, C0, rs, n, bs, n_steps):
+        """tol > 0: one synchronisation per step (the centre-shift test needs the host)."""
+        dev, k, dim = Xd.device, self.n_clusters, Xd.shape[1]
+        C = C0.contiguous()
+        C_new = torch.empty_like(C)
+        counts = torch.zeros(k, dtype=torch.float32, device=dev)
+        ws_mb = _lib.workspace(ops.lib.gdd_minibatch_update_ws_bytes(bs, k), dev)
+        labels_b = torch.empty(bs, dtype=torch.int32, device=dev)
+        sq_b = torch.empty(bs, dtype=torch.float32, device=dev)
+        rows_d = torch.empty(bs, dtype=torch.int64, device=dev)
+        tol_ = float(torch.var(Xd, dim=0, unbiased=False).mean().item()) * self.tol
+        any_zero, n_since = True, 0
+        ewa = ewa_min = None
+        no_improvement = 0
+        i = 0
+        for i in range(n_steps):
+            mb = rs.randint(0, n, bs)
+            n_since += bs
+            rr = any_zero or n_since >= 10 * k
+            if rr:
+                n_since = 0
+            rows_d.copy_(torch.from_numpy(mb))
+            ops.assign(Xd, C, rows=rows_d, labels=labels_b, sq=sq_b)
+            bi_d = ops.inertia(sq_b)
+            _lib.check(ops.lib.gdd_minibatch_update(bs, dim, Xd.data_ptr(), rows_d.data_ptr(), None,
+                                                    labels_b.data_ptr(), k, C.data_ptr(),
+                                                    C_new.data_ptr(), counts.data_ptr(),
+                                                    ws_mb.data_ptr(), ws_mb.numel(), ops.stream))
+            if rr and self.reassignment_ratio > 0:
+                any_zero = self._reassign(ops, Xd, rows_d, C_new, counts, rs, bs)
+            sq_diff = float(((C_new - C) ** 2).sum().item())
+            C, C_new = C_new, C
+            bi = float(bi_d.item()) / bs
+            if i == 0:
+                continue
+            if ewa is None:
+                ewa = bi
+            else:
+                a = min(bs * 2.0 / (n + 1), 1)
+                ewa = ewa * (1 - a) + bi * a
+            if sq_diff <= tol_:
+                break
+            if ewa_min is None or ewa < ewa_min:
+                no_improvement, ewa_min = 0, ewa
+            else:
+                no_improvement += 1
+            if self.max_no_improvement is not None and no_improvement >= self.max_no_improvement:
+                break
+        return C, i, ewa
 
 
 class KMeans(_BaseKMeans):

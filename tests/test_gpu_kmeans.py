@@ -137,3 +137,24 @@ def test_cluster_mean_and_argmax():
     assert np.array_equal(bits(out0.cpu().numpy()), bits(ref0))
     C = synth.blobs(k, 40, 5, seed=2)
     assert np.array_equal(gdd.argmax_rows(torch.from_numpy(C).cuda()).cpu().numpy(), np.argmax(C, -1))
+
+
+def test_minibatch_rng_state_after_fit():
+    """A shared RandomState ends in the same state as under scikit-learn (early stop rewinds)."""
+    X = synth.blobs(20000, 40, 100, seed=9)
+    rs_ref, rs = np.random.RandomState(3), np.random.RandomState(3)
+    ref = O.minibatch_kmeans(X, 100, random_state=rs_ref, batch_size=1000)
+    m = gdd.MiniBatchKMeans(n_clusters=100, random_state=rs, batch_size=1000).fit(X)
+    assert m.n_steps_ == ref["n_steps_"] < (100 * 20000) // 1000  # stopped early
+    assert np.array_equal(m.labels_, ref["labels_"])
+    s1, s2 = rs_ref.get_state(), rs.get_state()
+    assert np.array_equal(s1[1], s2[1]) and s1[2] == s2[2]
+
+
+def test_minibatch_tol_path():
+    X = synth.blobs(5000, 16, 20, seed=2)
+    ref = O.minibatch_kmeans(X, 20, random_state=1, batch_size=500, tol=1e-3)
+    m = gdd.MiniBatchKMeans(n_clusters=20, random_state=1, batch_size=500, tol=1e-3).fit(X)
+    # the centre-shift sum is an fp32 device reduction (numpy's pairwise order is not restated):
+    # same result unless the stop test sits within rounding of the tolerance
+    assert abs(m.n_steps_ - ref["n_steps_"]) <= 1
