@@ -50,13 +50,19 @@ __device__ __forceinline__ float npy_sumsq(const float* __restrict__ x, int dim)
   return (a[0] + a[1]) + (a[2] + a[3]);
 }
 
-// `stop` (nullable) lets a minibatch step become a no-op once the device-side convergence test
-// has fired, so the host can enqueue steps ahead of the stopping decision.
-__device__ __forceinline__ bool stopped(const int32_t* stop) { return stop && *stop; }
+// `stop` (nullable) points at MBState::stop_at (0 = running, s+1 = the convergence test fired at
+// step s). Kernels of a later step return at once, so the host can enqueue steps ahead of the
+// stopping decision. One 32-bit word read with an agent-scope atomic load: the test written by a
+// sibling block of the same launch is never seen torn, and step s itself always completes.
+__device__ __forceinline__ bool stopped(const int32_t* stop, int step_i) {
+  if (!stop) return false;
+  const int v = __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return v != 0 && v - 1 < step_i;
+}
 
 __global__ void k_row_norms(int64_t n, int dim, const float* __restrict__ X, float* __restrict__ out,
-                            const int32_t* __restrict__ stop) {
-  if (stopped(stop)) return;
+                            const int32_t* __restrict__ stop, int step_i) {
+  if (stopped(stop, step_i)) return;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = npy_sumsq(X + i * dim, dim);
 }
@@ -90,8 +96,8 @@ __device__ __forceinline__ unsigned long long pack_key(float d, int c) {
 }
 
 __global__ void k_fill_u64(int64_t n, unsigned long long* p, unsigned long long v,
-                           const int32_t* __restrict__ stop) {
-  if (stopped(stop)) return;
+                           const int32_t* __restrict__ stop, int step_i) {
+  if (stopped(stop, step_i)) return;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
 }
@@ -110,8 +116,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_assign(int64_t n, int dim, int d
                                                        const float* __restrict__ C,
                                                        const float* __restrict__ cn2, int cch,
                                                        unsigned long long* __restrict__ keys,
-                                                       const int32_t* __restrict__ stop) {
-  if (stopped(stop)) return;
+                                                       const int32_t* __restrict__ stop, int step_i) {
+  if (stopped(stop, step_i)) return;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int kPts = 32 * WAVES;
   const int S = dimp + 1;
@@ -172,8 +178,8 @@ __global__ void k_assign_finalize(int64_t n, int dim, const float* __restrict__ 
                                   const int64_t* __restrict__ rows, const float* __restrict__ C,
                                   const unsigned long long* __restrict__ keys,
                                   int32_t* __restrict__ labels, float* __restrict__ sq_dist,
-                                  const int32_t* __restrict__ stop) {
-  if (stopped(stop)) return;
+                                  const int32_t* __restrict__ stop, int step_i) {
+  if (stopped(stop, step_i)) return;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const unsigned long long key = keys[i];
@@ -186,6 +192,92 @@ __global__ void k_assign_finalize(int64_t n, int dim, const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------------
+// small batches (minibatch steps): one block of 8 waves per 32 points. The waves split the
+// centres (wave w takes tiles w, w+8, ...), stage their own 32-centre tile and its numpy-order
+// norms in LDS, run the same MFMA chain and epilogue as k_assign, and the block merges the 8
+// partial minima in LDS — no atomics, no key buffer, labels and sq_dist written directly.
+// ---------------------------------------------------------------------------------------------
+constexpr int kSmallWaves = 8;
+__host__ __device__ inline size_t assign_small_lds(int dimp) {
+  const int S = dimp + 1;
+  return sizeof(float) * ((size_t)(32 + 32 * kSmallWaves) * S + 32 * kSmallWaves) +
+         sizeof(unsigned long long) * 32 * kSmallWaves + 16;
+}
+
+__global__ __launch_bounds__(64 * kSmallWaves) void k_assign_small(
+    int64_t n, int dim, int dimp, const float* __restrict__ X, const int64_t* __restrict__ rows,
+    int k, const float* __restrict__ C, int32_t* __restrict__ labels, float* __restrict__ sq_dist,
+    const int32_t* __restrict__ stop, int step_i) {
+  if (stopped(stop, step_i)) return;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int S = dimp + 1;
+  float* Pl = lds;                                   // 32 points x S
+  float* Cl = Pl + 32 * S;                           // kSmallWaves x 32 centres x S
+  float* Nl = Cl + (size_t)kSmallWaves * 32 * S;     // kSmallWaves x 32 norms
+  unsigned long long* Kl =
+      reinterpret_cast<unsigned long long*>(((uintptr_t)(Nl + 32 * kSmallWaves) + 15) & ~uintptr_t(15));
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t p0 = (int64_t)blockIdx.x * 32;
+  for (int idx = tid; idx < 32 * dimp; idx += blockDim.x) {
+    const int r = idx / dimp, c = idx - r * dimp;
+    const int64_t pi = p0 + r;
+    float v = 0.f;
+    if (pi < n && c < dim) v = X[(rows ? rows[pi] : pi) * dim + c];
+    Pl[r * S + c] = v;
+  }
+  __syncthreads();
+  float* Cw = Cl + (size_t)wave * 32 * S;
+  float* Nw = Nl + wave * 32;
+  const int kh = lane >> 5;
+  const float* bp = Pl + (lane & 31) * S + kh;
+  const float* ap = Cw + (lane & 31) * S + kh;
+  unsigned long long best = ~0ull;
+  for (int cb = wave * 32; cb < k; cb += 32 * kSmallWaves) {
+    for (int idx = lane; idx < 32 * dimp; idx += 64) {
+      const int r = idx / dimp, c = idx - r * dimp;
+      Cw[r * S + c] = (cb + r < k && c < dim) ? C[(int64_t)(cb + r) * dim + c] : 0.f;
+    }
+    if (lane < 32) Nw[lane] = (cb + lane < k) ? npy_sumsq(C + (int64_t)(cb + lane) * dim, dim) : 0.f;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    floatx16 acc = {};
+    for (int s2 = 0; s2 < dimp; s2 += 2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[s2], bp[s2], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ci = (r & 3) + 8 * (r >> 2) + 4 * kh;
+      if (cb + ci < k) {
+        const unsigned long long key = pack_key(__builtin_fmaf(-2.f, acc[r], Nw[ci]), cb + ci);
+        best = key < best ? key : best;
+      }
+    }
+    // the next tile overwrites Cw/Nw: every lane's reads of this one must have completed
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  const unsigned long long other = __shfl_xor(best, 32);
+  best = other < best ? other : best;
+  if (lane < 32) Kl[wave * 32 + lane] = best;
+  __syncthreads();
+  if (wave == 0 && lane < 32) {
+    unsigned long long b = Kl[lane];
+#pragma unroll
+    for (int w = 1; w < kSmallWaves; ++w) {
+      const unsigned long long o = Kl[w * 32 + lane];
+      b = o < b ? o : b;
+    }
+    const int64_t pi = p0 + lane;
+    if (pi < n) {
+      const int lab = (b == ~0ull) ? 0 : (int)(unsigned)(b & 0xffffffffull);
+      labels[pi] = lab;
+      if (sq_dist) sq_dist[pi] = skl_sqdist(Pl + lane * S, C + (int64_t)lab * dim, dim);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // inertia: sequential fp32 sum in sample order. The block stages 4096 products at a time in LDS;
 // one lane folds them in order (float4 LDS reads keep the dependent add chain fed).
 // ---------------------------------------------------------------------------------------------
@@ -193,8 +285,8 @@ constexpr int kInertiaChunk = 4096;
 __global__ __launch_bounds__(1024) void k_inertia(int64_t n, const float* __restrict__ sq,
                                                   const float* __restrict__ w,
                                                   float* __restrict__ out,
-                                                  const int32_t* __restrict__ stop) {
-  if (stopped(stop)) return;
+                                                  const int32_t* __restrict__ stop, int step_i) {
+  if (stopped(stop, step_i)) return;
   __shared__ __attribute__((aligned(16))) float buf[kInertiaChunk];
   float acc = 0.f;
   for (int64_t b = 0; b < n; b += kInertiaChunk) {
@@ -227,16 +319,16 @@ __global__ __launch_bounds__(1024) void k_inertia(int64_t n, const float* __rest
 // ---------------------------------------------------------------------------------------------
 struct MBState {
   double ewa, ewa_min;
-  int32_t stop;          // first member: the `stop` flag the step kernels test
+  int32_t stop_at;       // offset 16: 0 while running, s+1 once the test fired at step s
   int32_t has_ewa, has_min, no_improvement;
-  int32_t stop_step;     // 0-based step index at which the loop broke (valid when stop)
-  int32_t pad[3];
+  int32_t pad[4];
 };
 
-__global__ void k_mb_converge(int step_i, int64_t bs, int64_t n, int max_no_improvement,
-                              const float* __restrict__ batch_inertia, MBState* __restrict__ st) {
-  if (threadIdx.x != 0 || blockIdx.x != 0 || st->stop) return;
-  const double bi = (double)batch_inertia[0] / (double)bs;
+// one thread; st->stop_at is published with an agent-scope atomic store (read by sibling blocks)
+__device__ void mb_converge(int step_i, int64_t bs, int64_t n, int max_no_improvement, float inertia,
+                            MBState* __restrict__ st) {
+  if (__hip_atomic_load(&st->stop_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const double bi = (double)inertia / (double)bs;
   if (step_i == 0) return;  // the first step's inertia is the init's
   if (!st->has_ewa) {
     st->ewa = bi;
@@ -253,10 +345,29 @@ __global__ void k_mb_converge(int step_i, int64_t bs, int64_t n, int max_no_impr
   } else {
     st->no_improvement += 1;
   }
-  if (max_no_improvement >= 0 && st->no_improvement >= max_no_improvement) {
-    st->stop = 1;
-    st->stop_step = step_i;
+  if (max_no_improvement >= 0 && st->no_improvement >= max_no_improvement)
+    __hip_atomic_store(&st->stop_at, step_i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sequential fp32 inertia of one batch by a 64-lane block (staged in LDS 2048 at a time)
+__device__ float mb_batch_inertia(int64_t b, const float* __restrict__ sq, float* stage) {
+  float acc = 0.f;
+  for (int64_t base = 0; base < b; base += 2048) {
+    const int m = (int)min<int64_t>(2048, b - base);
+#pragma unroll 8
+    for (int t = threadIdx.x; t < m; t += 64) stage[t] = sq[base + t] * 1.0f;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int t = 0; t < m; ++t) acc = acc + stage[t];
+    __syncthreads();
   }
+  return acc;
+}
+
+__global__ void k_mb_converge(int step_i, int64_t bs, int64_t n, int max_no_improvement,
+                              const float* __restrict__ batch_inertia, MBState* __restrict__ st) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  mb_converge(step_i, bs, n, max_no_improvement, batch_inertia[0], st);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -270,23 +381,46 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
                                                         float* __restrict__ C_new,
                                                         float* __restrict__ Wsum,
                                                         int32_t* __restrict__ members_ws,
-                                                        const int32_t* __restrict__ stop) {
-  if (stopped(stop)) return;
+                                                        const int32_t* __restrict__ stop, int step_i,
+                                                        const float* __restrict__ sq,
+                                                        float* __restrict__ inertia_out,
+                                                        MBState* __restrict__ st, int converge,
+                                                        int64_t n_samples, int max_no_improvement) {
+  if (stopped(stop, step_i)) return;
   const int c = blockIdx.x;
   const int lane = threadIdx.x;
+  if (c == k) {
+    // tail block (launched only by the fused step): batch inertia, then the convergence test
+    __shared__ float stage[2048];
+    const float inertia = mb_batch_inertia(b, sq, stage);
+    if (lane == 0) {
+      inertia_out[0] = inertia;
+      if (converge) mb_converge(step_i, b, n_samples, max_no_improvement, inertia, st);
+    }
+    return;
+  }
   int32_t* mem = members_ws + (int64_t)c * b;  // worst case: every batch sample in this cluster
   int count = 0;
-  for (int64_t base = 0; base < b; base += 64) {
-    const int64_t i = base + lane;
-    const bool is = i < b && labels[i] == c;
-    const unsigned long long m = __ballot(is);
-    const int before = __popcll(m & ((1ull << lane) - 1ull));
-    if (is) mem[count + before] = (int32_t)i;
-    count += __popcll(m);
+  for (int64_t base = 0; base < b; base += 64 * 8) {
+    // eight independent label loads in flight per lane, then the ordered ballot compaction
+    int32_t lab[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t i = base + u * 64 + lane;
+      lab[u] = i < b ? labels[i] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool is = lab[u] == c;
+      const unsigned long long m = __ballot(is);
+      const int before = __popcll(m & ((1ull << lane) - 1ull));
+      if (is) mem[count + before] = (int32_t)(base + u * 64 + lane);
+      count += __popcll(m);
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
-  // wsum: sequential fp32 in batch order (update_center_dense :78-83)
+  // wsum: sequential fp32 in batch order (update_center_dense :78-83); unit weights sum exactly
   float wsum = 0.f;
   if (w) {
     for (int t = 0; t < count; ++t) {
@@ -294,7 +428,7 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
       wsum = wsum + w[i];
     }
   } else {
-    for (int t = 0; t < count; ++t) wsum = wsum + 1.0f;
+    wsum = (float)count;
   }
   const float W = Wsum[c];
   const int64_t cb = (int64_t)c * dim;
@@ -303,7 +437,20 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
     const float alpha = 1.0f / Wn;  // Cython `1 / weight_sums[c]` with float operands
     for (int f = lane; f < dim; f += 64) {
       float acc = C_old[cb + f] * W;
-      for (int t = 0; t < count; ++t) {
+      int t = 0;
+      for (; t + 4 <= count; t += 4) {  // four gathers in flight ahead of the ordered adds
+        float v[4], wi[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int32_t i = mem[t + u];
+          const int64_t src = rows ? rows[i] : (int64_t)i;
+          v[u] = X[src * dim + f];
+          wi[u] = w ? w[i] : 1.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = acc + v[u] * wi[u];
+      }
+      for (; t < count; ++t) {
         const int32_t i = mem[t];
         const int64_t src = rows ? rows[i] : (int64_t)i;
         const float wi = w ? w[i] : 1.0f;
@@ -490,7 +637,7 @@ using namespace gdd;
 extern "C" int gdd_row_norms(int64_t n, int dim, const float* X, float* out, gdd_stream_t stream) {
   GDD_REQUIRE(n >= 0 && dim > 0 && (n == 0 || (X && out)), "row_norms: bad arguments");
   if (n == 0) return GDD_OK;
-  k_row_norms<<<blocks_for(n), 256, 0, to_hip(stream)>>>(n, dim, X, out, nullptr);
+  k_row_norms<<<blocks_for(n), 256, 0, to_hip(stream)>>>(n, dim, X, out, nullptr, 0);
   GDD_LAUNCHED();
   return GDD_OK;
 }
@@ -503,13 +650,28 @@ size_t assign_lds(int waves, int dimp, int cch) {
   return sizeof(float) * ((size_t)ncp * S + (size_t)32 * waves * S + ncp);
 }
 
-// keys fill + MFMA tiles + finalize (labels, optional per-sample sq_dist)
+bool use_small_assign(int64_t n, int dimp) {
+  return n <= 16384 && assign_small_lds(dimp) <= 160 * 1024;
+}
+
+// labels (+ optional per-sample sq_dist) of n samples against k centres.
+// small n: fused k_assign_small; large n: centre chunks over grid.y + 64-bit atomicMin keys.
 int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k, const float* C,
                   const float* c_norm2, int32_t* labels, float* sq_dist,
-                  unsigned long long* keys, const int32_t* stop, hipStream_t s) {
+                  unsigned long long* keys, const int32_t* stop, int step_i, hipStream_t s) {
   const int dimp = (dim + 1) & ~1;
-  // small batches: one wave per block so the grid still spreads over the chip
-  const int waves = n <= 4096 ? 1 : (dimp <= 96 ? 4 : (dimp <= 224 ? 2 : 1));
+  if (use_small_assign(n, dimp)) {
+    const size_t lds = assign_small_lds(dimp);
+    if (lds > 65536)
+      GDD_HIP(hipFuncSetAttribute((const void*)k_assign_small,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    k_assign_small<<<(unsigned)((n + 31) / 32), 64 * kSmallWaves, lds, s>>>(
+        n, dim, dimp, X, rows, k, C, labels, sq_dist, stop, step_i);
+    GDD_LAUNCHED();
+    return GDD_OK;
+  }
+  GDD_REQUIRE(c_norm2 && keys, "assign: large-n path needs c_norm2 and the key workspace");
+  const int waves = dimp <= 96 ? 4 : (dimp <= 224 ? 2 : 1);
   const int64_t gx = (n + 32 * waves - 1) / (32 * waves);
   // centers per block: as many as fit the LDS budget (>= 32), then fewer while the grid is too
   // small to occupy 256 CUs
@@ -524,7 +686,7 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
   }
   GDD_REQUIRE(gx < (1ll << 31) && gy < 65536, "assign: grid too large");
   const size_t lds = assign_lds(waves, dimp, cch);
-  k_fill_u64<<<blocks_for(n), 256, 0, s>>>(n, keys, ~0ull, stop);
+  k_fill_u64<<<blocks_for(n), 256, 0, s>>>(n, keys, ~0ull, stop, step_i);
   GDD_LAUNCHED();
   dim3 grid((unsigned)gx, (unsigned)gy);
   if (lds > 65536) {
@@ -537,13 +699,14 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   }
   if (waves == 4)
-    k_assign<4><<<grid, 256, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys, stop);
+    k_assign<4><<<grid, 256, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys, stop, step_i);
   else if (waves == 2)
-    k_assign<2><<<grid, 128, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys, stop);
+    k_assign<2><<<grid, 128, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys, stop, step_i);
   else
-    k_assign<1><<<grid, 64, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys, stop);
+    k_assign<1><<<grid, 64, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys, stop, step_i);
   GDD_LAUNCHED();
-  k_assign_finalize<<<blocks_for(n), 256, 0, s>>>(n, dim, X, rows, C, keys, labels, sq_dist, stop);
+  k_assign_finalize<<<blocks_for(n), 256, 0, s>>>(n, dim, X, rows, C, keys, labels, sq_dist, stop,
+                                                  step_i);
   GDD_LAUNCHED();
   return GDD_OK;
 }
@@ -563,13 +726,13 @@ extern "C" int gdd_kmeans_assign(int64_t n, int dim, const float* X, const int64
   if (ws_bytes < gdd_kmeans_assign_ws_bytes(n))
     return fail(GDD_E_WORKSPACE, "assign: workspace %zu too small", ws_bytes);
   return launch_assign(n, dim, X, rows, k, C, c_norm2, labels, sq_dist,
-                       static_cast<unsigned long long*>(ws), nullptr, to_hip(stream));
+                       static_cast<unsigned long long*>(ws), nullptr, 0, to_hip(stream));
 }
 
 extern "C" int gdd_inertia(int64_t n, const float* sq_dist, const float* w, float* out,
                            gdd_stream_t stream) {
   GDD_REQUIRE(n >= 0 && out && (n == 0 || sq_dist), "inertia: bad arguments");
-  k_inertia<<<1, 1024, 0, to_hip(stream)>>>(n, sq_dist, w, out, nullptr);
+  k_inertia<<<1, 1024, 0, to_hip(stream)>>>(n, sq_dist, w, out, nullptr, 0);
   GDD_LAUNCHED();
   return GDD_OK;
 }
@@ -588,12 +751,33 @@ extern "C" int gdd_minibatch_update(int64_t b, int dim, const float* X, const in
   if (ws_bytes < gdd_minibatch_update_ws_bytes(b, k))
     return fail(GDD_E_WORKSPACE, "minibatch_update: workspace too small");
   k_minibatch_update<<<k, 64, 0, to_hip(stream)>>>(b, dim, X, rows, w, labels, k, C_old, C_new,
-                                                   weight_sums, static_cast<int32_t*>(ws), nullptr);
+                                                   weight_sums, static_cast<int32_t*>(ws), nullptr,
+                                                   0, nullptr, nullptr, nullptr, 0, 1, -1);
   GDD_LAUNCHED();
   return GDD_OK;
 }
 
 // ---- fused MiniBatchKMeans step (_mini_batch_step + _mini_batch_convergence) ------------------
+namespace {
+struct StepWs {
+  unsigned long long* keys;
+  int32_t* members;
+  float* cn2;
+  float* sq;
+  float* inertia;
+};
+StepWs carve_step(void* ws, size_t ws_bytes, int64_t b, int k) {
+  Carver cv(ws, ws_bytes);
+  StepWs w;
+  w.keys = cv.take<unsigned long long>(b);
+  w.members = cv.take<int32_t>((size_t)b * k);
+  w.cn2 = cv.take<float>(k);
+  w.sq = cv.take<float>(b);
+  w.inertia = cv.take<float>(1);
+  return w;
+}
+}  // namespace
+
 extern "C" size_t gdd_minibatch_state_bytes(void) { return sizeof(MBState); }
 
 extern "C" size_t gdd_minibatch_step_ws_bytes(int64_t b, int k) {
@@ -616,26 +800,20 @@ extern "C" int gdd_minibatch_step(int64_t b, int dim, const float* X, const int6
     return fail(GDD_E_WORKSPACE, "minibatch_step: workspace too small");
   hipStream_t s = to_hip(stream);
   MBState* st = static_cast<MBState*>(state);
-  const int32_t* stop = &st->stop;
-  Carver cv(ws, ws_bytes);
-  auto* keys = cv.take<unsigned long long>(b);
-  int32_t* members = cv.take<int32_t>((size_t)b * k);
-  float* cn2 = cv.take<float>(k);
-  float* sq = cv.take<float>(b);
-  float* inertia = cv.take<float>(1);
-  k_row_norms<<<blocks_for(k), 256, 0, s>>>(k, dim, C_old, cn2, stop);
-  GDD_LAUNCHED();
-  int rc = launch_assign(b, dim, X, rows, k, C_old, cn2, labels, sq, keys, stop, s);
-  if (rc) return rc;
-  k_inertia<<<1, 1024, 0, s>>>(b, sq, nullptr, inertia, stop);
-  GDD_LAUNCHED();
-  k_minibatch_update<<<k, 64, 0, s>>>(b, dim, X, rows, nullptr, labels, k, C_old, C_new,
-                                      weight_sums, members, stop);
-  GDD_LAUNCHED();
-  if (converge) {
-    k_mb_converge<<<1, 64, 0, s>>>(step_i, b, n_samples, max_no_improvement, inertia, st);
+  const int32_t* stop = &st->stop_at;
+  StepWs w = carve_step(ws, ws_bytes, b, k);
+  const int dimp = (dim + 1) & ~1;
+  if (!use_small_assign(b, dimp)) {  // the fused small kernel computes its own norms
+    k_row_norms<<<blocks_for(k), 256, 0, s>>>(k, dim, C_old, w.cn2, stop, step_i);
     GDD_LAUNCHED();
   }
+  int rc = launch_assign(b, dim, X, rows, k, C_old, w.cn2, labels, w.sq, w.keys, stop, step_i, s);
+  if (rc) return rc;
+  // k update blocks + one tail block (batch inertia, convergence test)
+  k_minibatch_update<<<k + 1, 64, 0, s>>>(b, dim, X, rows, nullptr, labels, k, C_old, C_new,
+                                          weight_sums, w.members, stop, step_i, w.sq, w.inertia, st,
+                                          converge, n_samples, max_no_improvement);
+  GDD_LAUNCHED();
   return GDD_OK;
 }
 
@@ -646,13 +824,8 @@ extern "C" int gdd_minibatch_converge(int64_t b, int k, int step_i, int64_t n_sa
   if (ws_bytes < gdd_minibatch_step_ws_bytes(b, k))
     return fail(GDD_E_WORKSPACE, "minibatch_converge: workspace too small");
   // the batch inertia of the preceding gdd_minibatch_step, at its fixed workspace offset
-  Carver cv(ws, ws_bytes);
-  cv.take<unsigned long long>(b);
-  cv.take<int32_t>((size_t)b * k);
-  cv.take<float>(k);
-  cv.take<float>(b);
-  float* inertia = cv.take<float>(1);
-  k_mb_converge<<<1, 64, 0, to_hip(stream)>>>(step_i, b, n_samples, max_no_improvement, inertia,
+  StepWs w = carve_step(ws, ws_bytes, b, k);
+  k_mb_converge<<<1, 64, 0, to_hip(stream)>>>(step_i, b, n_samples, max_no_improvement, w.inertia,
                                               static_cast<MBState*>(state));
   GDD_LAUNCHED();
   return GDD_OK;

@@ -1,15 +1,16 @@
 // gdd_kmeanspp.hip — greedy k-means++ seeding on the device (sklearn _kmeans_plusplus,
 // sklearn/cluster/_kmeans.py:174-272), with the host's RNG draws passed in.
 //
-// Per seeding round c = 1..k-1 (three launches, no host round trip; `best` and the current
+// Two launches per seeding round c = 1..k-1, no host round trip (the chosen trial and the current
 // potential live in device memory):
-//   scan_search  (1 block)  cum[i] = inclusive fp64 prefix of fp32(w_i * closest_i)   (stable_cumsum)
-//                           cand[t] = searchsorted_left(cum, u[c-1][t] * (double)pot), clip n-1
-//   dist         (grid)     dist[t][i] = np.minimum(closest_i, fp32(max(0, ((-2<x_cand,x_i>) +
-//                           |x_cand|^2) + |x_i|^2)))   (fp64 upcast, pairwise.py:582-650)
-//   select       (1 block)  pot[t] = OpenBLAS-SkylakeX-order fp32 dot(dist[t], w); best = first
-//                           argmin; centers[c] = X[cand[best]]; closest := dist[best] (by index)
-// `closest` is never copied: round c reads dist[(c-1)&1][best_{c-1}].
+//   dist(c)   grid      dist[t][i] = np.minimum(closest_i, fp32(max(0, ((-2<x_cand,x_i>) +
+//                       |x_cand|^2) + |x_i|^2)))   fp64 upcast distances (pairwise.py:582-650)
+//   tail(c)   1 block   pot[t] = fp32 dot(dist[t], w) in OpenBLAS SkylakeX sdot order; best =
+//                       first argmin; centers[c] = X[cand[best]]; then for round c+1:
+//                       cum = inclusive fp64 prefix of fp32(w * dist[best])   (stable_cumsum)
+//                       cand[t] = searchsorted_left(cum, u[c][t] * (double)pot), clipped to n-1
+// tail(0) seeds the loop from the first centre (random_state.choice on the host). `closest` is
+// never copied: round c reads dist[(c-1)&1][best_{c-1}].
 #include <algorithm>
 
 #include "gdd_common.hpp"
@@ -18,28 +19,37 @@ namespace gdd {
 namespace {
 
 constexpr int kMaxTrials = 16;
-constexpr int kScanThreads = 1024;
+constexpr int kTailThreads = 1024;
 
 struct KppState {
-  float pot;        // current potential (fp32, as sklearn keeps it)
-  int best;         // best trial of the previous round
+  float pot;   // current potential (fp32, as sklearn keeps it)
+  int best;    // trial chosen in the previous round; -1 = the distances to the first centre
   int64_t cand[kMaxTrials];
   double cnorm[kMaxTrials];
 };
 
 // OpenBLAS 0.3.28/29 SkylakeX sdot (kernel/x86_64/sdot.c + sdot_microk_skylakex-2.c), emulated by
-// one wave: the 64 lanes are the 4 x 16 AVX-512 accumulators of the 64-wide loop; they fold to
-// 4 x 8 AVX2 accumulators for the 32-wide remainder; lanes then combine ((a0+a1)+a2)+a3, 8 -> 4 by
-// halves, and (h0+h1)+(h2+h3); the scalar tail is added in double. All 64 lanes call it; lane 0
-// returns the value.
+// one wave: the 64 lanes are the 4 x 16 AVX-512 accumulators of the 64-wide loop (lane u*16+l
+// runs accumulator u, lane l); they fold to 4 x 8 AVX2 accumulators for the 32-wide remainder;
+// lanes then combine ((a0+a1)+a2)+a3, 8 -> 4 by halves, and (h0+h1)+(h2+h3); the scalar tail is
+// added in double. All 64 lanes call it; lane 0 returns the value.
 __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restrict__ y, int64_t n,
                                float* scratch /* 64 floats of LDS owned by this wave */) {
   const int lane = threadIdx.x & 63;
   const int64_t n1 = n & ~31ll;
   const int64_t n64 = n1 & ~63ll;
   float a = 0.f;
-  for (int64_t i = lane; i < n64; i += 64) a = __builtin_fmaf(x[i], y[i], a);
-  scratch[lane] = a;  // lane = u*16 + l  <->  accum_u5 lane l
+  int64_t i = lane;
+  for (; i + 192 < n64; i += 256) {  // four independent load pairs ahead of the ordered fmas
+    const float x0 = x[i], x1 = x[i + 64], x2 = x[i + 128], x3 = x[i + 192];
+    const float y0 = y[i], y1 = y[i + 64], y2 = y[i + 128], y3 = y[i + 192];
+    a = __builtin_fmaf(x0, y0, a);
+    a = __builtin_fmaf(x1, y1, a);
+    a = __builtin_fmaf(x2, y2, a);
+    a = __builtin_fmaf(x3, y3, a);
+  }
+  for (; i < n64; i += 64) a = __builtin_fmaf(x[i], y[i], a);
+  scratch[lane] = a;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -50,12 +60,13 @@ __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restr
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int l = 0; l < 8; ++l) acc[u][l] = scratch[u * 16 + l] + scratch[u * 16 + l + 8];
-    for (int64_t i = n64; i < n1; i += 32)
+    if (n64 < n1) {  // at most one 32-wide block remains
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int l = 0; l < 8; ++l)
-          acc[u][l] = __builtin_fmaf(x[i + u * 8 + l], y[i + u * 8 + l], acc[u][l]);
+          acc[u][l] = __builtin_fmaf(x[n64 + u * 8 + l], y[n64 + u * 8 + l], acc[u][l]);
+    }
     float s[8];
 #pragma unroll
     for (int l = 0; l < 8; ++l) s[l] = ((acc[0][l] + acc[1][l]) + acc[2][l]) + acc[3][l];
@@ -63,8 +74,8 @@ __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restr
 #pragma unroll
     for (int l = 0; l < 4; ++l) h[l] = s[l] + s[l + 4];
     double dot = n1 ? (double)((h[0] + h[1]) + (h[2] + h[3])) : 0.0;
-    for (int64_t i = n1; i < n; ++i) {
-      const float p = y[i] * x[i];
+    for (int64_t t = n1; t < n; ++t) {
+      const float p = y[t] * x[t];
       dot = dot + (double)p;
     }
     r = (float)dot;
@@ -96,36 +107,89 @@ __global__ void k_kpp_init(int64_t n, int dim, const float* __restrict__ X, int6
   closest[i] = f < 0.f ? 0.f : f;
 }
 
-__global__ __launch_bounds__(64) void k_kpp_first_pot(int64_t n, int dim, const float* __restrict__ X,
-                                                      const float* __restrict__ w,
-                                                      const float* __restrict__ closest,
-                                                      int64_t first_id, float* __restrict__ centers,
-                                                      int64_t* __restrict__ indices,
-                                                      KppState* __restrict__ st) {
-  __shared__ float scratch[64];
-  const float p = sdot_skx_wave(closest, w, n, scratch);
-  if (threadIdx.x == 0) {
-    st->pot = p;
-    st->best = 0;
-    indices[0] = first_id;
-  }
-  for (int j = threadIdx.x; j < dim; j += 64) centers[j] = X[first_id * dim + j];
+// dist[t][i] for a 256-point tile; the candidate row is staged in LDS as fp64
+__global__ __launch_bounds__(256) void k_kpp_dist(int64_t n, int dim, const float* __restrict__ X,
+                                                  const double* __restrict__ xsq,
+                                                  const float* __restrict__ closest0,
+                                                  const float* __restrict__ dist_prev,
+                                                  const KppState* __restrict__ st,
+                                                  float* __restrict__ dist) {
+  extern __shared__ double s_c[];  // dim
+  const int t = blockIdx.y;
+  const int64_t ct = st->cand[t];
+  for (int j = threadIdx.x; j < dim; j += blockDim.x) s_c[j] = (double)X[ct * dim + j];
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* closest = st->best < 0 ? closest0 : dist_prev + (int64_t)st->best * n;
+  const float* xi = X + i * dim;
+  double dot = 0.0;
+  for (int j = 0; j < dim; ++j) dot = __builtin_fma(s_c[j], (double)xi[j], dot);
+  const double d = ((-2.0 * dot) + st->cnorm[t]) + xsq[i];
+  float f = (float)d;
+  f = f < 0.f ? 0.f : f;
+  dist[(int64_t)t * n + i] = np_minimum(closest[i], f);
 }
 
-__global__ __launch_bounds__(kScanThreads) void k_kpp_scan_search(
-    int64_t n, const float* __restrict__ w, const float* __restrict__ closest0,
-    const float* __restrict__ dist_prev, int use_prev, const double* __restrict__ u, int T,
-    const double* __restrict__ xsq, double* __restrict__ cum, KppState* __restrict__ st) {
-  __shared__ double s_part[kScanThreads];
+// end of round c (c = 0: the first centre) and the candidate draw of round c+1
+__global__ __launch_bounds__(kTailThreads) void k_kpp_tail(
+    int64_t n, int dim, const float* __restrict__ X, const float* __restrict__ w,
+    const float* __restrict__ closest0, const float* __restrict__ dist, int T, int c, int k,
+    int64_t first_id, const double* __restrict__ uniforms, const double* __restrict__ xsq,
+    double* __restrict__ cum, float* __restrict__ centers, int64_t* __restrict__ indices,
+    KppState* __restrict__ st) {
+  __shared__ float scratch[kMaxTrials * 64];
+  __shared__ float s_pot[kMaxTrials];
+  __shared__ double s_part[kTailThreads];
+  __shared__ int s_best;
+  __shared__ int64_t s_src;
   const int tid = threadIdx.x;
-  const float* closest = use_prev ? dist_prev + (int64_t)st->best * n : closest0;
-  const int64_t chunk = (n + kScanThreads - 1) / kScanThreads;
+  const int wave = tid >> 6;
+  // ---- finish round c ----
+  if (c == 0) {
+    if (wave == 0) {
+      const float p = sdot_skx_wave(closest0, w, n, scratch);  // closest_dist_sq @ sample_weight
+      if (tid == 0) s_pot[0] = p;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      s_best = -1;
+      s_src = first_id;
+      st->best = -1;
+      st->pot = s_pot[0];
+      indices[0] = first_id;
+    }
+  } else {
+    if (wave < T) {
+      const float p = sdot_skx_wave(dist + (int64_t)wave * n, w, n, scratch + wave * 64);
+      if ((tid & 63) == 0) s_pot[wave] = p;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int b = 0;  // np.argmin: first minimum; a NaN is returned as soon as it is met
+      for (int t = 1; t < T; ++t) {
+        const float pb = s_pot[b], pt = s_pot[t];
+        if (pb == pb && (pt < pb || pt != pt)) b = t;
+      }
+      s_best = b;
+      s_src = st->cand[b];
+      st->best = b;
+      st->pot = s_pot[b];
+      indices[c] = st->cand[b];
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < dim; j += kTailThreads) centers[(int64_t)c * dim + j] = X[s_src * dim + j];
+  if (c + 1 >= k) return;
+  // ---- candidates of round c+1 ----
+  const float* closest = s_best < 0 ? closest0 : dist + (int64_t)s_best * n;
+  const int64_t chunk = (n + kTailThreads - 1) / kTailThreads;
   const int64_t lo = min<int64_t>(n, tid * chunk), hi = min<int64_t>(n, lo + chunk);
   double run = 0.0;
   for (int64_t i = lo; i < hi; ++i) run = run + (double)(w[i] * closest[i]);
   s_part[tid] = run;
   __syncthreads();
-  for (int off = 1; off < kScanThreads; off <<= 1) {
+  for (int off = 1; off < kTailThreads; off <<= 1) {
     const double v = tid >= off ? s_part[tid - off] : 0.0;
     __syncthreads();
     s_part[tid] += v;
@@ -136,10 +200,10 @@ __global__ __launch_bounds__(kScanThreads) void k_kpp_scan_search(
     base = base + (double)(w[i] * closest[i]);
     cum[i] = base;
   }
-  __syncthreads();
   __threadfence_block();
+  __syncthreads();
   if (tid < T) {
-    const double r = u[tid] * (double)st->pot;
+    const double r = uniforms[(int64_t)c * T + tid] * (double)st->pot;
     int64_t a = 0, b = n;  // first index with cum[idx] >= r  (np.searchsorted side='left')
     while (a < b) {
       const int64_t m = (a + b) >> 1;
@@ -152,61 +216,6 @@ __global__ __launch_bounds__(kScanThreads) void k_kpp_scan_search(
     st->cand[tid] = a;
     st->cnorm[tid] = xsq[a];
   }
-}
-
-// dist[t][i] for a 256-point tile; the T candidate rows are staged in LDS as fp64
-__global__ __launch_bounds__(256) void k_kpp_dist(int64_t n, int dim, const float* __restrict__ X,
-                                                  const double* __restrict__ xsq,
-                                                  const float* __restrict__ closest0,
-                                                  const float* __restrict__ dist_prev, int use_prev,
-                                                  const KppState* __restrict__ st,
-                                                  float* __restrict__ dist, int T) {
-  extern __shared__ double s_c[];  // T x dim
-  const int t = blockIdx.y;
-  const int64_t ct = st->cand[t];
-  for (int j = threadIdx.x; j < dim; j += blockDim.x) s_c[j] = (double)X[ct * dim + j];
-  __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float* closest = use_prev ? dist_prev + (int64_t)st->best * n : closest0;
-  const float* xi = X + i * dim;
-  double dot = 0.0;
-  for (int j = 0; j < dim; ++j) dot = __builtin_fma(s_c[j], (double)xi[j], dot);
-  const double d = ((-2.0 * dot) + st->cnorm[t]) + xsq[i];
-  float f = (float)d;
-  f = f < 0.f ? 0.f : f;
-  dist[(int64_t)t * n + i] = np_minimum(closest[i], f);
-}
-
-__global__ __launch_bounds__(1024) void k_kpp_select(int64_t n, int dim, const float* __restrict__ X,
-                                                     const float* __restrict__ w,
-                                                     const float* __restrict__ dist, int T, int c,
-                                                     float* __restrict__ centers,
-                                                     int64_t* __restrict__ indices,
-                                                     KppState* __restrict__ st) {
-  __shared__ float scratch[kMaxTrials * 64];
-  __shared__ float s_pot[kMaxTrials];
-  __shared__ int s_best;
-  const int wave = threadIdx.x >> 6;
-  if (wave < T) {
-    const float p = sdot_skx_wave(dist + (int64_t)wave * n, w, n, scratch + wave * 64);
-    if ((threadIdx.x & 63) == 0) s_pot[wave] = p;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int b = 0;  // np.argmin: first minimum; a NaN is returned as soon as it is met
-    for (int t = 1; t < T; ++t) {
-      const float pb = s_pot[b], pt = s_pot[t];
-      if (pb == pb && (pt < pb || pt != pt)) b = t;
-    }
-    s_best = b;
-    st->best = b;
-    st->pot = s_pot[b];
-    indices[c] = st->cand[b];
-  }
-  __syncthreads();
-  const int64_t src = st->cand[s_best];
-  for (int j = threadIdx.x; j < dim; j += blockDim.x) centers[(int64_t)c * dim + j] = X[src * dim + j];
 }
 
 __global__ void k_ones(int64_t n, float* p) {
@@ -258,24 +267,20 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   }
   k_kpp_init<<<nb, 256, 0, s>>>(n, dim, X, first_id, xsq, closest0);
   GDD_LAUNCHED();
-  k_kpp_first_pot<<<1, 64, 0, s>>>(n, dim, X, w, closest0, first_id, centers, indices, st);
+  k_kpp_tail<<<1, kTailThreads, 0, s>>>(n, dim, X, w, closest0, dist[1], n_trials, 0, k, first_id,
+                                        uniforms, xsq, cum, centers, indices, st);
   GDD_LAUNCHED();
   const size_t lds = sizeof(double) * (size_t)dim;
   if (lds > 65536)
     GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dist, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds));
   for (int c = 1; c < k; ++c) {
-    const int use_prev = c > 1;
     const float* prev = dist[(c - 1) & 1];
     float* cur = dist[c & 1];
-    k_kpp_scan_search<<<1, kScanThreads, 0, s>>>(n, w, closest0, prev, use_prev,
-                                                 uniforms + (int64_t)(c - 1) * n_trials, n_trials,
-                                                 xsq, cum, st);
+    k_kpp_dist<<<dim3(nb, n_trials), 256, lds, s>>>(n, dim, X, xsq, closest0, prev, st, cur);
     GDD_LAUNCHED();
-    k_kpp_dist<<<dim3(nb, n_trials), 256, lds, s>>>(n, dim, X, xsq, closest0, prev, use_prev, st,
-                                                   cur, n_trials);
-    GDD_LAUNCHED();
-    k_kpp_select<<<1, 64 * n_trials, 0, s>>>(n, dim, X, w, cur, n_trials, c, centers, indices, st);
+    k_kpp_tail<<<1, kTailThreads, 0, s>>>(n, dim, X, w, closest0, cur, n_trials, c, k, first_id,
+                                          uniforms, xsq, cum, centers, indices, st);
     GDD_LAUNCHED();
   }
   return GDD_OK;

@@ -267,23 +267,24 @@ class MiniBatchKMeans(_BaseKMeans):
             for j, rr in enumerate(chunk):
                 s = i + j
                 c_old, c_new = bufs[s % 2], bufs[(s + 1) % 2]
-                do_re = rr and self.reassignment_ratio > 0
                 _lib.check(lib.gdd_minibatch_step(
                     bs, dim, Xd.data_ptr(), rows_d[j].data_ptr(), k, c_old.data_ptr(),
-                    c_new.data_ptr(), counts.data_ptr(), labels_b.data_ptr(), s, n, max_ni,
-                    0 if do_re else 1, state.data_ptr(), ws.data_ptr(), ws.numel(), stream))
-                if do_re:
-                    st = state[16:36].cpu().view(torch.int32)
-                    if int(st[0]):
-                        stop_step = int(st[4])
+                    c_new.data_ptr(), counts.data_ptr(), labels_b.data_ptr(), s, n, max_ni, 1,
+                    state.data_ptr(), ws.data_ptr(), ws.numel(), stream))
+                if rr and self.reassignment_ratio > 0:
+                    stop_at = int(state[16:20].cpu().view(torch.int32)[0])
+                    if stop_at and stop_at - 1 < s:
+                        stop_step = stop_at - 1  # stopped earlier in this chunk: step s never ran
                         break
+                    # the reassignment precedes the convergence test in sklearn; the test only
+                    # reads this step's batch inertia, so it is still valid
                     any_zero = self._reassign(ops, Xd, rows_d[j], c_new, counts, rs, bs)
-                    _lib.check(lib.gdd_minibatch_converge(bs, k, s, n, max_ni, state.data_ptr(),
-                                                          ws.data_ptr(), ws.numel(), stream))
+                    if stop_at:
+                        stop_step = stop_at - 1
             if stop_step is None:
-                st = state[16:36].cpu().view(torch.int32)
-                if int(st[0]):
-                    stop_step = int(st[4])
+                stop_at = int(state[16:20].cpu().view(torch.int32)[0])
+                if stop_at:
+                    stop_step = stop_at - 1
             if stop_step is not None and stop_step < i + m - 1:
                 # sklearn drew batch indices only up to the stopping step: rewind the generator
                 rs.set_state(snapshot)
