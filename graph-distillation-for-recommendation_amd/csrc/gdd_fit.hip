@@ -1,0 +1,355 @@
+// gdd_fit.hip — native host loop of MiniBatchKMeans.fit (sklearn/cluster/_kmeans.py:2046-2200).
+//
+// Everything the Python loop in gdd/kmeans.py did per step now runs in C++: the numpy-legacy RNG
+// draws (gdd_rng.hpp), chunked H2D of the batch indices through pinned memory, two kernel launches
+// per step (gdd_minibatch_step), and the host's O(k) decisions at reassignment steps. The host
+// synchronises only at reassignment steps (every ceil(10k/b) steps, and while some count is zero)
+// and once at the end. Draw order, reassignment rule, early-stopping and the RNG state left behind
+// are sklearn's (one OpenMP thread).
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "gdd_common.hpp"
+#include "gdd_rng.hpp"
+
+namespace gdd {
+namespace {
+
+__global__ void k_gather_rows(int64_t m, int dim, const float* __restrict__ X,
+                              const int64_t* __restrict__ idx, float* __restrict__ out) {
+  const int64_t total = m * dim;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / dim;
+    out[t] = X[idx[r] * dim + (t - r * dim)];
+  }
+}
+
+// C[dst[j]] = X[rows[src[j]]]  (centers_new[to_reassign] = X_batch[new_centers], :1655-1662)
+__global__ void k_reassign_rows(int m, int dim, const float* __restrict__ X,
+                                const int64_t* __restrict__ rows, const int64_t* __restrict__ pairs,
+                                float* __restrict__ C) {
+  const int j = blockIdx.x;
+  if (j >= m) return;
+  const int64_t dst = pairs[2 * j], src = rows[pairs[2 * j + 1]];
+  for (int f = threadIdx.x; f < dim; f += blockDim.x) C[dst * dim + f] = X[src * dim + f];
+}
+
+constexpr int kChunkCap = 64;
+
+struct Pinned {
+  void* p = nullptr;
+  ~Pinned() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
+struct FitWs {
+  float* Xi;
+  void* kpp_ws;
+  size_t kpp_bytes;
+  void* step_ws;
+  size_t step_bytes;
+  void* state;
+  float* counts;
+  float* C[2];
+  int64_t* rows_d;
+  int32_t* labels_b;
+  int64_t* pairs;
+  double* uniforms;
+  int64_t* init_idx;
+  int64_t* val_idx;
+  int32_t* val_labels;
+  float* val_sq;
+  float* sq;
+  float* scalar;
+  void* assign_ws;
+  size_t assign_bytes;
+};
+
+size_t fit_ws(void* base, size_t cap, int64_t n, int dim, int k, int64_t bs, int64_t isz, int T,
+              FitWs* w) {
+  Carver cv(base, cap);
+  FitWs f;
+  f.Xi = cv.take<float>((size_t)isz * dim);
+  f.kpp_bytes = gdd_kmeans_plusplus_ws_bytes(isz, T);
+  f.kpp_ws = cv.take<char>(f.kpp_bytes);
+  f.step_bytes = gdd_minibatch_step_ws_bytes(bs, k);
+  f.step_ws = cv.take<char>(f.step_bytes);
+  f.state = cv.take<char>(gdd_minibatch_state_bytes());
+  f.counts = cv.take<float>(k);
+  f.C[0] = cv.take<float>((size_t)k * dim);
+  f.C[1] = cv.take<float>((size_t)k * dim);
+  f.rows_d = cv.take<int64_t>((size_t)kChunkCap * bs);
+  f.labels_b = cv.take<int32_t>(bs);
+  f.pairs = cv.take<int64_t>(2 * (size_t)k);
+  f.uniforms = cv.take<double>((size_t)std::max(k - 1, 1) * T);
+  f.init_idx = cv.take<int64_t>(isz);
+  f.val_idx = cv.take<int64_t>(isz);
+  f.val_labels = cv.take<int32_t>(isz);
+  f.val_sq = cv.take<float>(isz);
+  f.sq = cv.take<float>(n);
+  f.scalar = cv.take<float>(4);
+  f.assign_bytes = gdd_kmeans_assign_ws_bytes(std::max(n, isz));
+  f.assign_ws = cv.take<char>(f.assign_bytes);
+  if (w) *w = f;
+  return cv.off + 1024;
+}
+
+int local_trials(int k) { return 2 + (int)std::log((double)k); }
+
+}  // namespace
+}  // namespace gdd
+
+using namespace gdd;
+
+extern "C" size_t gdd_minibatch_kmeans_fit_ws_bytes(int64_t n, int dim, int k, int64_t batch_size,
+                                                   int64_t init_size) {
+  const int64_t bs = std::min<int64_t>(batch_size, n);
+  return fit_ws(nullptr, 0, n, dim, k, bs, init_size, local_trials(k), nullptr);
+}
+
+extern "C" int gdd_minibatch_kmeans_fit(
+    int64_t n, int dim, const float* X, int k, int64_t batch_size, int max_iter,
+    int max_no_improvement, float reassignment_ratio, int64_t init_size, int n_init,
+    int compute_labels, void* rng_state, void (*argsort_cb)(const float*, int64_t, int64_t*),
+    float* centers_out, int32_t* labels_out, float* inertia_out, int64_t* n_steps_out,
+    double* ewa_out, void* ws, size_t ws_bytes, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && dim > 0 && dim <= 512 && k > 0 && k <= n, "mbk_fit: bad shape");
+  GDD_REQUIRE(batch_size > 0 && max_iter >= 0 && n_init >= 1 && init_size >= k && init_size <= n,
+              "mbk_fit: bad parameters");
+  GDD_REQUIRE(X && rng_state && centers_out && n_steps_out && ws, "mbk_fit: null pointer");
+  GDD_REQUIRE(!compute_labels || (labels_out && inertia_out), "mbk_fit: labels/inertia needed");
+  hipStream_t s = to_hip(stream);
+  const int64_t bs = std::min<int64_t>(batch_size, n);
+  const int64_t isz = init_size;
+  const int T = local_trials(k);
+  GDD_REQUIRE(T <= 16, "mbk_fit: k too large for the k-means++ trial count");
+  FitWs w;
+  if (fit_ws(ws, ws_bytes, n, dim, k, bs, isz, T, &w) > ws_bytes)
+    return fail(GDD_E_WORKSPACE, "mbk_fit: workspace too small");
+  LegacyRNG rng(static_cast<MTState*>(rng_state));
+
+  // pinned staging: batch indices of one chunk, k-means++ uniforms, small read-backs
+  const size_t pin_bytes = sizeof(int64_t) * (size_t)kChunkCap * bs +
+                           sizeof(double) * (size_t)std::max(k - 1, 1) * T +
+                           sizeof(int64_t) * 2 * (size_t)isz + sizeof(float) * (size_t)k * 2 + 256 +
+                           sizeof(int64_t) * 2 * (size_t)k;
+  Pinned pin;
+  GDD_HIP(hipHostMalloc(&pin.p, pin_bytes, hipHostMallocDefault));
+  char* pp = static_cast<char*>(pin.p);
+  int64_t* h_rows = reinterpret_cast<int64_t*>(pp);
+  pp += sizeof(int64_t) * (size_t)kChunkCap * bs;
+  double* h_u = reinterpret_cast<double*>(pp);
+  pp += sizeof(double) * (size_t)std::max(k - 1, 1) * T;
+  int64_t* h_idx = reinterpret_cast<int64_t*>(pp);
+  pp += sizeof(int64_t) * 2 * (size_t)isz;
+  float* h_counts = reinterpret_cast<float*>(pp);
+  pp += sizeof(float) * (size_t)k * 2;
+  int32_t* h_flag = reinterpret_cast<int32_t*>(pp);
+  pp += 256;
+  int64_t* h_pairs = reinterpret_cast<int64_t*>(pp);
+
+  // ---- validation subset and initialisations (:2128-2163) ----------------------------------------
+  rng.randint(0, n, isz, h_idx + isz);  // validation_indices
+  GDD_HIP(hipMemcpyAsync(w.val_idx, h_idx + isz, sizeof(int64_t) * isz, hipMemcpyHostToDevice, s));
+  float best_inertia = 0.f;
+  bool have_best = false;
+  for (int init = 0; init < n_init; ++init) {
+    const float* Xi = X;
+    if (isz < n) {
+      rng.randint(0, n, isz, h_idx);
+      GDD_HIP(hipMemcpyAsync(w.init_idx, h_idx, sizeof(int64_t) * isz, hipMemcpyHostToDevice, s));
+      k_gather_rows<<<(unsigned)std::min<int64_t>((isz * dim + 255) / 256, 4096), 256, 0, s>>>(
+          isz, dim, X, w.init_idx, w.Xi);
+      GDD_LAUNCHED();
+      Xi = w.Xi;
+    }
+    const int64_t first = rng.choice_uniform_weights(isz);
+    for (int c = 0; c < k - 1; ++c)
+      for (int t = 0; t < T; ++t) h_u[(size_t)c * T + t] = rng.next_double();
+    if (k > 1)
+      GDD_HIP(hipMemcpyAsync(w.uniforms, h_u, sizeof(double) * (size_t)(k - 1) * T,
+                             hipMemcpyHostToDevice, s));
+    float* cand = (n_init > 1 && init > 0) ? w.C[1] : w.C[0];
+    int rc = gdd_kmeans_plusplus(isz, dim, Xi, nullptr, k, T, first, w.uniforms, cand, w.init_idx,
+                                 w.kpp_ws, w.kpp_bytes, stream);
+    if (rc) return rc;
+    if (n_init > 1) {  // inertia on the validation set (_labels_inertia_threadpool_limit)
+      rc = gdd_row_norms(k, dim, cand, reinterpret_cast<float*>(w.pairs), stream);
+      if (rc) return rc;
+      rc = gdd_kmeans_assign(isz, dim, X, w.val_idx, k, cand, reinterpret_cast<float*>(w.pairs),
+                             w.val_labels, w.val_sq, w.assign_ws, w.assign_bytes, stream);
+      if (rc) return rc;
+      rc = gdd_inertia(isz, w.val_sq, nullptr, w.scalar, stream);
+      if (rc) return rc;
+      GDD_HIP(hipMemcpyAsync(h_counts, w.scalar, sizeof(float), hipMemcpyDeviceToHost, s));
+      GDD_HIP(hipStreamSynchronize(s));
+      const float inertia = h_counts[0];
+      if (!have_best || inertia < best_inertia) {
+        best_inertia = inertia;
+        have_best = true;
+        if (cand != w.C[0])
+          GDD_HIP(hipMemcpyAsync(w.C[0], cand, sizeof(float) * (size_t)k * dim,
+                                 hipMemcpyDeviceToDevice, s));
+      }
+    }
+  }
+
+  // ---- the step loop (:2168-2189) -----------------------------------------------------------------
+  GDD_HIP(hipMemsetAsync(w.counts, 0, sizeof(float) * k, s));
+  GDD_HIP(hipMemsetAsync(w.state, 0, gdd_minibatch_state_bytes(), s));
+  const int64_t n_steps = ((int64_t)max_iter * n) / bs;
+  bool any_zero = true;
+  int64_t n_since = 0;
+  int64_t i = 0, stop_step = -1;
+  std::vector<float> W(k);
+  std::vector<int64_t> order;
+  while (i < n_steps && stop_step < 0) {
+    const MTState snapshot = *static_cast<MTState*>(rng_state);
+    std::vector<char> chunk_rr;
+    while (i + (int64_t)chunk_rr.size() < n_steps && (int)chunk_rr.size() < kChunkCap) {
+      rng.randint(0, n, bs, h_rows + chunk_rr.size() * bs);
+      n_since += bs;
+      const bool rr = any_zero || n_since >= 10 * (int64_t)k;  // _random_reassign (:2029-2043)
+      if (rr) n_since = 0;
+      chunk_rr.push_back(rr ? 1 : 0);
+      if (rr) break;
+    }
+    const int m = (int)chunk_rr.size();
+    // the previous chunk's copy has been consumed (stream order) before we overwrite h_rows: the
+    // sync at the end of every chunk guarantees it
+    GDD_HIP(hipMemcpyAsync(w.rows_d, h_rows, sizeof(int64_t) * (size_t)m * bs, hipMemcpyHostToDevice,
+                           s));
+    bool synced = false;
+    for (int j = 0; j < m; ++j) {
+      const int64_t st = i + j;
+      float* c_old = w.C[st % 2];
+      float* c_new = w.C[(st + 1) % 2];
+      const int64_t* rows = w.rows_d + (size_t)j * bs;
+      int rc = gdd_minibatch_step(bs, dim, X, rows, k, c_old, c_new, w.counts, w.labels_b, (int)st, n,
+                                  max_no_improvement, 1, w.state, w.step_ws, w.step_bytes, stream);
+      if (rc) return rc;
+      if (chunk_rr[j] && reassignment_ratio > 0.f) {
+        GDD_HIP(hipMemcpyAsync(h_flag, static_cast<char*>(w.state) + 16, sizeof(int32_t),
+                               hipMemcpyDeviceToHost, s));
+        GDD_HIP(hipMemcpyAsync(h_counts, w.counts, sizeof(float) * k, hipMemcpyDeviceToHost, s));
+        GDD_HIP(hipStreamSynchronize(s));
+        synced = true;
+        const int32_t stop_at = h_flag[0];
+        if (stop_at && stop_at - 1 < st) {  // stopped earlier in this chunk: step st never ran
+          stop_step = stop_at - 1;
+          break;
+        }
+        // _mini_batch_step reassignment (:1640-1667), numpy float32 semantics
+        float wmax = h_counts[0];
+        for (int c = 1; c < k; ++c) wmax = std::max(wmax, h_counts[c]);
+        const float thr = (float)reassignment_ratio * wmax;
+        std::vector<char> to(k);
+        int64_t cnt = 0;
+        for (int c = 0; c < k; ++c) {
+          to[c] = h_counts[c] < thr;
+          cnt += to[c];
+        }
+        if ((double)cnt > 0.5 * (double)bs) {
+          if (!argsort_cb) return fail(GDD_E_INVALID, "mbk_fit: argsort callback required (k > b/2)");
+          order.assign(k, 0);
+          argsort_cb(h_counts, k, order.data());  // np.argsort(weight_sums) (quicksort order)
+          for (int64_t q = (int64_t)(0.5 * (double)bs); q < k; ++q) to[order[q]] = 0;
+          cnt = 0;
+          for (int c = 0; c < k; ++c) cnt += to[c];
+        }
+        if (cnt) {
+          std::vector<int64_t> perm = rng.permutation(bs);  // choice(bs, replace=False, size=cnt)
+          int64_t q = 0;
+          for (int c = 0; c < k; ++c)
+            if (to[c]) {
+              h_pairs[2 * q] = c;
+              h_pairs[2 * q + 1] = perm[q];
+              ++q;
+            }
+          GDD_HIP(hipMemcpyAsync(w.pairs, h_pairs, sizeof(int64_t) * 2 * cnt, hipMemcpyHostToDevice,
+                                 s));
+          k_reassign_rows<<<(unsigned)cnt, 64, 0, s>>>((int)cnt, dim, X, rows, w.pairs, c_new);
+          GDD_LAUNCHED();
+        }
+        float mn = 0.f;
+        bool first_min = true;
+        for (int c = 0; c < k; ++c)
+          if (!to[c] && (first_min || h_counts[c] < mn)) {
+            mn = h_counts[c];
+            first_min = false;
+          }
+        bool zero = false;
+        for (int c = 0; c < k; ++c) {
+          if (to[c]) h_counts[c] = mn;
+          zero |= h_counts[c] == 0.f;
+        }
+        any_zero = zero;
+        GDD_HIP(hipMemcpyAsync(w.counts, h_counts, sizeof(float) * k, hipMemcpyHostToDevice, s));
+        if (stop_at) stop_step = stop_at - 1;
+      }
+    }
+    if (stop_step < 0) {
+      GDD_HIP(hipMemcpyAsync(h_flag, static_cast<char*>(w.state) + 16, sizeof(int32_t),
+                             hipMemcpyDeviceToHost, s));
+      GDD_HIP(hipStreamSynchronize(s));
+      if (h_flag[0]) stop_step = h_flag[0] - 1;
+    } else if (!synced) {
+      GDD_HIP(hipStreamSynchronize(s));
+    }
+    if (stop_step >= 0 && stop_step < i + m - 1) {
+      // sklearn drew batch indices only up to the stopping step: rewind the generator
+      *static_cast<MTState*>(rng_state) = snapshot;
+      for (int64_t q = i; q <= stop_step; ++q) rng.randint(0, n, bs, h_rows);
+    }
+    i += m;
+  }
+  const int64_t last = stop_step >= 0 ? stop_step : n_steps - 1;
+  *n_steps_out = last + 1;
+  const float* C = w.C[(last + 1) % 2];
+  GDD_HIP(hipMemcpyAsync(centers_out, C, sizeof(float) * (size_t)k * dim, hipMemcpyDeviceToDevice, s));
+  if (ewa_out) {
+    GDD_HIP(hipMemcpyAsync(h_counts, w.state, sizeof(double), hipMemcpyDeviceToHost, s));
+    GDD_HIP(hipStreamSynchronize(s));
+    std::memcpy(ewa_out, h_counts, sizeof(double));
+  }
+  if (compute_labels) {  // final labels pass + inertia (:2191-2197)
+    int rc = gdd_row_norms(k, dim, C, reinterpret_cast<float*>(w.pairs), stream);
+    if (rc) return rc;
+    rc = gdd_kmeans_assign(n, dim, X, nullptr, k, C, reinterpret_cast<float*>(w.pairs), labels_out,
+                           w.sq, w.assign_ws, w.assign_bytes, stream);
+    if (rc) return rc;
+    rc = gdd_inertia(n, w.sq, nullptr, inertia_out, stream);
+    if (rc) return rc;
+  }
+  return GDD_OK;
+}
+
+// ---- host RNG exposure for parity tests (numpy legacy RandomState draws) ---------------------------
+extern "C" int gdd_rng_randint(void* state, int64_t low, int64_t high, int64_t count, int64_t* out) {
+  GDD_REQUIRE(state && out && high > low && count >= 0, "rng_randint: bad arguments");
+  LegacyRNG(static_cast<MTState*>(state)).randint(low, high, count, out);
+  return GDD_OK;
+}
+
+extern "C" int gdd_rng_random_sample(void* state, int64_t count, double* out) {
+  GDD_REQUIRE(state && out && count >= 0, "rng_random_sample: bad arguments");
+  LegacyRNG r(static_cast<MTState*>(state));
+  for (int64_t i = 0; i < count; ++i) out[i] = r.next_double();
+  return GDD_OK;
+}
+
+extern "C" int gdd_rng_permutation(void* state, int64_t n, int64_t* out) {
+  GDD_REQUIRE(state && out && n >= 0, "rng_permutation: bad arguments");
+  std::vector<int64_t> p = LegacyRNG(static_cast<MTState*>(state)).permutation(n);
+  std::copy(p.begin(), p.end(), out);
+  return GDD_OK;
+}
+
+extern "C" int gdd_rng_choice_unit_weights(void* state, int64_t n, int64_t* out) {
+  GDD_REQUIRE(state && out && n > 0, "rng_choice: bad arguments");
+  out[0] = LegacyRNG(static_cast<MTState*>(state)).choice_uniform_weights(n);
+  return GDD_OK;
+}

@@ -51,6 +51,14 @@ SIGNATURES = {
                                     _c_i64, _c_int, _c_int, _vp, _vp, _c_size, _vp]),
     "gdd_minibatch_converge": (_c_int, [_c_i64, _c_int, _c_int, _c_i64, _c_int, _vp, _vp, _c_size,
                                         _vp]),
+    "gdd_minibatch_kmeans_fit_ws_bytes": (_c_size, [_c_i64, _c_int, _c_int, _c_i64, _c_i64]),
+    "gdd_minibatch_kmeans_fit": (_c_int, [_c_i64, _c_int, _vp, _c_int, _c_i64, _c_int, _c_int,
+                                          _c_f32, _c_i64, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp,
+                                          _vp, _vp, _vp, _c_size, _vp]),
+    "gdd_rng_randint": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp]),
+    "gdd_rng_random_sample": (_c_int, [_vp, _c_i64, _vp]),
+    "gdd_rng_permutation": (_c_int, [_vp, _c_i64, _vp]),
+    "gdd_rng_choice_unit_weights": (_c_int, [_vp, _c_i64, _vp]),
     "gdd_group_ws_bytes": (_c_size, [_c_i64, _c_int]),
     "gdd_group_by_label": (_c_int, [_c_i64, _vp, _c_int, _vp, _vp, _vp, _c_size, _vp]),
     "gdd_segment_sum_f32": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp]),
@@ -124,3 +132,40 @@ def ptr(t) -> int | None:
 
 def workspace(nbytes: int, device) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+class MTState(ctypes.Structure):
+    """gdd_mt_state: numpy's legacy RandomState state, passed to the native loops by pointer."""
+
+    _fields_ = [("key", ctypes.c_uint32 * 624), ("pos", ctypes.c_int32),
+                ("has_gauss", ctypes.c_int32), ("gauss", ctypes.c_double)]
+
+    @classmethod
+    def from_random_state(cls, rs):
+        name, key, pos, has_gauss, gauss = rs.get_state(legacy=True)
+        if name != "MT19937":
+            raise ValueError(f"unsupported bit generator {name}")
+        st = cls()
+        key32 = key.astype("uint32")  # keep the array alive across the copy
+        ctypes.memmove(st.key, key32.ctypes.data, 624 * 4)
+        st.pos, st.has_gauss, st.gauss = int(pos), int(has_gauss), float(gauss)
+        return st
+
+    def to_random_state(self, rs):
+        import numpy as np
+        key = np.ctypeslib.as_array(self.key).copy()
+        rs.set_state(("MT19937", key, int(self.pos), int(self.has_gauss), float(self.gauss)))
+
+
+ARGSORT_CB = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_float), ctypes.c_int64,
+                              ctypes.POINTER(ctypes.c_int64))
+
+
+def _np_argsort(w_ptr, k, out_ptr):
+    import numpy as np
+    w = np.ctypeslib.as_array(w_ptr, shape=(k,)).copy()
+    np.ctypeslib.as_array(out_ptr, shape=(k,))[:] = np.argsort(w)
+
+
+# np.argsort(weight_sums) for the native MiniBatchKMeans loop (kept alive for the process)
+argsort_callback = ARGSORT_CB(_np_argsort)

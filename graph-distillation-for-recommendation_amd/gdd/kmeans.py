@@ -22,6 +22,8 @@ explicitly to reproduce that.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
 
@@ -148,28 +150,65 @@ class MiniBatchKMeans(_BaseKMeans):
         self.init_size = init_size
         self.reassignment_ratio = reassignment_ratio
 
+    def _sizes(self, n):
+        bs = min(self.batch_size, n)
+        isz = self.init_size
+        if isz is None:
+            isz = 3 * bs
+            if isz < self.n_clusters:
+                isz = 3 * self.n_clusters
+        elif isz < self.n_clusters:
+            isz = 3 * self.n_clusters
+        return bs, min(isz, n)
+
     def fit(self, X, y=None, sample_weight=None):
         self._check_weights(sample_weight)
         Xd = _as_device_f32(X, self.device)
-        dev = Xd.device
         n, dim = Xd.shape
         k = self.n_clusters
         if k > n:
             raise ValueError(f"n_samples={n} should be >= n_clusters={k}.")
         rs = check_random_state(self.random_state)
-        bs = min(self.batch_size, n)
-        isz = self.init_size
-        if isz is None:
-            isz = 3 * bs
-            if isz < k:
-                isz = 3 * k
-        elif isz < k:
-            isz = 3 * k
-        isz = min(isz, n)
+        if self.tol > 0:
+            return self._fit_host_loop(Xd, rs)
+        bs, isz = self._sizes(n)
+        lib = _lib.device_lib()
+        dev = Xd.device
+        st = _lib.MTState.from_random_state(rs)
+        ws = _lib.workspace(lib.gdd_minibatch_kmeans_fit_ws_bytes(n, dim, k, bs, isz), dev)
+        centers = torch.empty((k, dim), dtype=torch.float32, device=dev)
+        labels = torch.empty(n, dtype=torch.int32, device=dev) if self.compute_labels else None
+        inertia = torch.empty(1, dtype=torch.float32, device=dev)
+        n_steps, ewa = ctypes.c_int64(0), ctypes.c_double(0.0)
+        max_ni = -1 if self.max_no_improvement is None else int(self.max_no_improvement)
+        _lib.check(lib.gdd_minibatch_kmeans_fit(
+            n, dim, Xd.data_ptr(), k, bs, int(self.max_iter), max_ni, float(self.reassignment_ratio),
+            isz, self._n_init(3), int(bool(self.compute_labels)), ctypes.addressof(st),
+            ctypes.cast(_lib.argsort_callback, ctypes.c_void_p).value, centers.data_ptr(),
+            _lib.ptr(labels), inertia.data_ptr(), ctypes.addressof(n_steps), ctypes.addressof(ewa),
+            ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev)))
+        st.to_random_state(rs)  # leave the generator where sklearn leaves it
+        self.n_steps_ = int(n_steps.value)
+        self.n_iter_ = int(np.ceil((self.n_steps_ * bs) / n))
+        self.cluster_centers_device_ = centers
+        self.cluster_centers_ = centers.cpu().numpy()
+        if self.compute_labels:
+            self.labels_device_ = labels
+            self.labels_ = labels.cpu().numpy()
+            self.inertia_ = float(inertia.item())
+        else:
+            self.inertia_ = ewa.value * n
+        return self
+
+    def _fit_host_loop(self, Xd, rs):
+        """tol > 0: the centre-shift test needs the host every step (Python loop over the same
+        device primitives)."""
+        dev = Xd.device
+        n, dim = Xd.shape
+        k = self.n_clusters
+        bs, isz = self._sizes(n)
         n_init = self._n_init(3)
         ops = _Ops(dev, max(n, isz, bs), k, dim)
-
-        # Validation set for the init (:2128-2131)
         validation_indices = rs.randint(0, n, isz)
         best_inertia, init_centers = None, None
         for _ in range(n_init):
@@ -189,12 +228,8 @@ class MiniBatchKMeans(_BaseKMeans):
                 inertia = 0.0
             if best_inertia is None or inertia < best_inertia:
                 init_centers, best_inertia = centers, inertia
-
         n_steps = (self.max_iter * n) // bs
-        if self.tol > 0:
-            C, i, ewa = self._steps_sync(ops, Xd, init_centers, rs, n, bs, n_steps)
-        else:
-            C, i, ewa = self._steps_async(ops, Xd, init_centers, rs, n, bs, n_steps)
+        C, i, ewa = self._steps_sync(ops, Xd, init_centers, rs, n, bs, n_steps)
         self.n_steps_ = i + 1
         self.n_iter_ = int(np.ceil(((i + 1) * bs) / n))
         self.cluster_centers_device_ = C
@@ -229,71 +264,6 @@ class MiniBatchKMeans(_BaseKMeans):
         W[to_reassign] = np.min(W[~to_reassign])
         counts.copy_(torch.from_numpy(W))
         return bool((W == 0).any())
-
-    def _steps_async(self, ops, Xd, C0, rs, n, bs, n_steps):
-        """Steps are enqueued in chunks that end at the next reassignment step (the only point the
-        host must look at device state); early stopping runs on the device (gdd_minibatch_step),
-        which turns the remaining enqueued steps into no-ops. One H2D copy of the chunk's batch
-        indices and one synchronisation per chunk."""
-        lib, dev, k, dim = ops.lib, Xd.device, self.n_clusters, Xd.shape[1]
-        stream = ops.stream
-        bufs = [C0.contiguous(), torch.empty_like(C0)]
-        counts = torch.zeros(k, dtype=torch.float32, device=dev)
-        labels_b = torch.empty(bs, dtype=torch.int32, device=dev)
-        state = torch.zeros(lib.gdd_minibatch_state_bytes(), dtype=torch.uint8, device=dev)
-        ws = _lib.workspace(lib.gdd_minibatch_step_ws_bytes(bs, k), dev)
-        max_ni = -1 if self.max_no_improvement is None else int(self.max_no_improvement)
-        chunk_cap = 64
-        rows_pin = torch.empty((chunk_cap, bs), dtype=torch.int64, pin_memory=True)
-        rows_d = torch.empty((chunk_cap, bs), dtype=torch.int64, device=dev)
-        any_zero, n_since = True, 0
-        i = 0
-        stop_step = None
-        while i < n_steps and stop_step is None:
-            snapshot = rs.get_state()
-            chunk = []
-            while i + len(chunk) < n_steps and len(chunk) < chunk_cap:
-                mb = rs.randint(0, n, bs)
-                n_since += bs
-                rr = any_zero or n_since >= 10 * k  # _random_reassign (:2029-2043)
-                if rr:
-                    n_since = 0
-                rows_pin[len(chunk)].numpy()[:] = mb
-                chunk.append(rr)
-                if rr:
-                    break
-            m = len(chunk)
-            rows_d[:m].copy_(rows_pin[:m], non_blocking=True)
-            for j, rr in enumerate(chunk):
-                s = i + j
-                c_old, c_new = bufs[s % 2], bufs[(s + 1) % 2]
-                _lib.check(lib.gdd_minibatch_step(
-                    bs, dim, Xd.data_ptr(), rows_d[j].data_ptr(), k, c_old.data_ptr(),
-                    c_new.data_ptr(), counts.data_ptr(), labels_b.data_ptr(), s, n, max_ni, 1,
-                    state.data_ptr(), ws.data_ptr(), ws.numel(), stream))
-                if rr and self.reassignment_ratio > 0:
-                    stop_at = int(state[16:20].cpu().view(torch.int32)[0])
-                    if stop_at and stop_at - 1 < s:
-                        stop_step = stop_at - 1  # stopped earlier in this chunk: step s never ran
-                        break
-                    # the reassignment precedes the convergence test in sklearn; the test only
-                    # reads this step's batch inertia, so it is still valid
-                    any_zero = self._reassign(ops, Xd, rows_d[j], c_new, counts, rs, bs)
-                    if stop_at:
-                        stop_step = stop_at - 1
-            if stop_step is None:
-                stop_at = int(state[16:20].cpu().view(torch.int32)[0])
-                if stop_at:
-                    stop_step = stop_at - 1
-            if stop_step is not None and stop_step < i + m - 1:
-                # sklearn drew batch indices only up to the stopping step: rewind the generator
-                rs.set_state(snapshot)
-                for _ in range(stop_step - i + 1):
-                    rs.randint(0, n, bs)
-            i += m
-        last = n_steps - 1 if stop_step is None else stop_step
-        ewa = float(state[0:8].cpu().view(torch.float64)[0])
-        return bufs[(last + 1) % 2], last, ewa
 
     def _steps_sync(self, ops, Xd, C0, rs, n, bs, n_steps):
         """tol > 0: one synchronisation per step (the centre-shift test needs the host)."""

@@ -135,6 +135,39 @@ int gdd_minibatch_step(int64_t b, int dim, const float* X, const int64_t* rows, 
 int gdd_minibatch_converge(int64_t b, int k, int step_i, int64_t n_samples, int max_no_improvement,
                            void* state, void* ws, size_t ws_bytes, gdd_stream_t stream);
 
+/* numpy legacy RandomState state: ('MT19937', key[624], pos, has_gauss, cached_gaussian).          */
+typedef struct gdd_mt_state {
+  uint32_t key[624];
+  int32_t pos;
+  int32_t has_gauss;
+  double gauss;
+} gdd_mt_state;
+
+/* MiniBatchKMeans(n_clusters=k, batch_size, max_iter, max_no_improvement (-1 = None),              */
+/* reassignment_ratio, init_size, n_init).fit(X) in one call (sklearn/cluster/_kmeans.py:2046-2200):  */
+/* validation/init subsets, k-means++ seeding, the step loop with reassignment and early stopping,   */
+/* and (compute_labels) the final labels pass + inertia. `rng` is the caller's RandomState, advanced */
+/* exactly as scikit-learn advances it. argsort_cb must reproduce np.argsort(weight_sums); it is    */
+/* only called when more than batch/2 centres are due for reassignment (possible only if k > b/2).   */
+/* Host syncs: one per reassignment step and one at the end. centers_out k x dim, labels_out n,      */
+/* inertia_out 1 float (device); n_steps_out, ewa_out (nullable) host.                              */
+size_t gdd_minibatch_kmeans_fit_ws_bytes(int64_t n, int dim, int k, int64_t batch_size,
+                                         int64_t init_size);
+int gdd_minibatch_kmeans_fit(int64_t n, int dim, const float* X, int k, int64_t batch_size,
+                             int max_iter, int max_no_improvement, float reassignment_ratio,
+                             int64_t init_size, int n_init, int compute_labels, void* rng,
+                             void (*argsort_cb)(const float*, int64_t, int64_t*), float* centers_out,
+                             int32_t* labels_out, float* inertia_out, int64_t* n_steps_out,
+                             double* ewa_out, void* ws, size_t ws_bytes, gdd_stream_t stream);
+
+/* Host-only numpy-legacy draws used by the native loops (exposed for parity tests):                */
+/* randint(low, high, count) (int64), random_sample(count), permutation(n), and                      */
+/* choice(n, p=w/w.sum()) for unit fp32 weights. `state` is a gdd_mt_state, advanced in place.       */
+int gdd_rng_randint(void* state, int64_t low, int64_t high, int64_t count, int64_t* out);
+int gdd_rng_random_sample(void* state, int64_t count, double* out);
+int gdd_rng_permutation(void* state, int64_t n, int64_t* out);
+int gdd_rng_choice_unit_weights(void* state, int64_t n, int64_t* out);
+
 /* Stable grouping of samples by label: perm[offsets[c] .. offsets[c+1]) lists the samples of        */
 /* cluster c in ascending sample order; counts[c] = offsets[c+1]-offsets[c].                         */
 size_t gdd_group_ws_bytes(int64_t n, int k);
