@@ -202,6 +202,7 @@ extern "C" int gdd_minibatch_kmeans_fit(
   GDD_HIP(hipMemsetAsync(w.state, 0, gdd_minibatch_state_bytes(), s));
   const int64_t n_steps = ((int64_t)max_iter * n) / bs;
   bool any_zero = true;
+  bool norms_valid = false;
   int64_t n_since = 0;
   int64_t i = 0, stop_step = -1;
   std::vector<float> W(k);
@@ -228,9 +229,12 @@ extern "C" int gdd_minibatch_kmeans_fit(
       float* c_old = w.C[st % 2];
       float* c_new = w.C[(st + 1) % 2];
       const int64_t* rows = w.rows_d + (size_t)j * bs;
+      const int flags = GDD_STEP_CONVERGE | (norms_valid ? GDD_STEP_NORMS_VALID : 0);
       int rc = gdd_minibatch_step(bs, dim, X, rows, k, c_old, c_new, w.counts, w.labels_b, (int)st, n,
-                                  max_no_improvement, 1, w.state, w.step_ws, w.step_bytes, stream);
+                                  max_no_improvement, flags, w.state, w.step_ws, w.step_bytes,
+                                  stream);
       if (rc) return rc;
+      norms_valid = true;  // the step left ||c_new||^2 behind
       if (chunk_rr[j] && reassignment_ratio > 0.f) {
         GDD_HIP(hipMemcpyAsync(h_flag, static_cast<char*>(w.state) + 16, sizeof(int32_t),
                                hipMemcpyDeviceToHost, s));
@@ -273,6 +277,7 @@ extern "C" int gdd_minibatch_kmeans_fit(
                                  s));
           k_reassign_rows<<<(unsigned)cnt, 64, 0, s>>>((int)cnt, dim, X, rows, w.pairs, c_new);
           GDD_LAUNCHED();
+          norms_valid = false;  // reassigned rows: the next step recomputes the norms
         }
         float mn = 0.f;
         bool first_min = true;

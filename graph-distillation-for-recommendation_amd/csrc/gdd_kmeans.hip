@@ -204,10 +204,38 @@ __host__ __device__ inline size_t assign_small_lds(int dimp) {
          sizeof(unsigned long long) * 32 * kSmallWaves + 16;
 }
 
+// Stage a 32-row tile (row r = src_row(r), `dim` floats, rows >= valid read as zero) into LDS rows
+// of stride S, zero-padding column dim when dimp > dim. Loads are issued eight per lane before
+// the LDS stores, so a tile costs ~one memory latency per 8*nlanes elements instead of one each.
+template <class RowPtr>
+__device__ __forceinline__ void stage_tile32(float* __restrict__ dst, int S, RowPtr src_row,
+                                             int valid, int dim, int dimp, int lane, int nlanes) {
+  const int total = 32 * dim;
+  for (int base = 0; base < total; base += nlanes * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = base + u * nlanes + lane;
+      const int r = idx / dim;
+      v[u] = (idx < total && r < valid) ? src_row(r)[idx - r * dim] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = base + u * nlanes + lane;
+      if (idx < total) {
+        const int r = idx / dim;
+        dst[r * S + (idx - r * dim)] = v[u];
+      }
+    }
+  }
+  if (dimp > dim)
+    for (int r = lane; r < 32; r += nlanes) dst[r * S + dim] = 0.f;
+}
+
 __global__ __launch_bounds__(64 * kSmallWaves) void k_assign_small(
     int64_t n, int dim, int dimp, const float* __restrict__ X, const int64_t* __restrict__ rows,
-    int k, const float* __restrict__ C, int32_t* __restrict__ labels, float* __restrict__ sq_dist,
-    const int32_t* __restrict__ stop, int step_i) {
+    int k, const float* __restrict__ C, const float* __restrict__ cn2, int32_t* __restrict__ labels,
+    float* __restrict__ sq_dist, const int32_t* __restrict__ stop, int step_i) {
   if (stopped(stop, step_i)) return;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int S = dimp + 1;
@@ -216,15 +244,13 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_assign_small(
   float* Nl = Cl + (size_t)kSmallWaves * 32 * S;     // kSmallWaves x 32 norms
   unsigned long long* Kl =
       reinterpret_cast<unsigned long long*>(((uintptr_t)(Nl + 32 * kSmallWaves) + 15) & ~uintptr_t(15));
+  __shared__ int64_t s_rows[32];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t p0 = (int64_t)blockIdx.x * 32;
-  for (int idx = tid; idx < 32 * dimp; idx += blockDim.x) {
-    const int r = idx / dimp, c = idx - r * dimp;
-    const int64_t pi = p0 + r;
-    float v = 0.f;
-    if (pi < n && c < dim) v = X[(rows ? rows[pi] : pi) * dim + c];
-    Pl[r * S + c] = v;
-  }
+  const int np = (int)min<int64_t>(32, n - p0);
+  if (tid < 32) s_rows[tid] = tid < np ? (rows ? rows[p0 + tid] : p0 + tid) : 0;
+  __syncthreads();
+  stage_tile32(Pl, S, [&](int r) { return X + s_rows[r] * dim; }, np, dim, dimp, tid, blockDim.x);
   __syncthreads();
   float* Cw = Cl + (size_t)wave * 32 * S;
   float* Nw = Nl + wave * 32;
@@ -233,11 +259,16 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_assign_small(
   const float* ap = Cw + (lane & 31) * S + kh;
   unsigned long long best = ~0ull;
   for (int cb = wave * 32; cb < k; cb += 32 * kSmallWaves) {
-    for (int idx = lane; idx < 32 * dimp; idx += 64) {
-      const int r = idx / dimp, c = idx - r * dimp;
-      Cw[r * S + c] = (cb + r < k && c < dim) ? C[(int64_t)(cb + r) * dim + c] : 0.f;
+    const float* Cb = C + (int64_t)cb * dim;
+    stage_tile32(Cw, S, [&](int r) { return Cb + (int64_t)r * dim; }, k - cb, dim, dimp, lane, 64);
+    if (cn2) {
+      if (lane < 32) Nw[lane] = (cb + lane < k) ? cn2[cb + lane] : 0.f;
+    } else {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane < 32) Nw[lane] = (cb + lane < k) ? npy_sumsq(Cw + lane * S, dim) : 0.f;
     }
-    if (lane < 32) Nw[lane] = (cb + lane < k) ? npy_sumsq(C + (int64_t)(cb + lane) * dim, dim) : 0.f;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -261,6 +292,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_assign_small(
   best = other < best ? other : best;
   if (lane < 32) Kl[wave * 32 + lane] = best;
   __syncthreads();
+  __shared__ int s_lab[32];
   if (wave == 0 && lane < 32) {
     unsigned long long b = Kl[lane];
 #pragma unroll
@@ -268,12 +300,39 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_assign_small(
       const unsigned long long o = Kl[w * 32 + lane];
       b = o < b ? o : b;
     }
-    const int64_t pi = p0 + lane;
-    if (pi < n) {
-      const int lab = (b == ~0ull) ? 0 : (int)(unsigned)(b & 0xffffffffull);
-      labels[pi] = lab;
-      if (sq_dist) sq_dist[pi] = skl_sqdist(Pl + lane * S, C + (int64_t)lab * dim, dim);
+    const int lab = (b == ~0ull) ? 0 : (int)(unsigned)(b & 0xffffffffull);
+    s_lab[lane] = lab;
+    if (lane < np) labels[p0 + lane] = lab;
+  }
+  if (!sq_dist) return;
+  __syncthreads();
+  // ||x - c_label||^2 in the _euclidean_dense_dense order: the terms (4-element groups, then the
+  // remainder elements) are formed by the whole block, then each point's lane adds them in order
+  const int ng = dim >> 2, nt = ng + (dim & 3);
+  float* terms = Cl;  // the centre tiles are no longer needed
+  for (int idx = tid; idx < 32 * nt; idx += blockDim.x) {
+    const int p = idx / nt, t = idx - p * nt;
+    if (p >= np) continue;
+    const float* x = Pl + p * S;
+    const float* c = C + (int64_t)s_lab[p] * dim;
+    float v;
+    if (t < ng) {
+      const int j = 4 * t;
+      const float d0 = x[j] - c[j], d1 = x[j + 1] - c[j + 1], d2 = x[j + 2] - c[j + 2],
+                  d3 = x[j + 3] - c[j + 3];
+      v = ((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3;
+    } else {
+      const int j = 4 * ng + (t - ng);
+      const float d0 = x[j] - c[j];
+      v = d0 * d0;
     }
+    terms[idx] = v;
+  }
+  __syncthreads();
+  if (tid < np) {
+    float r = 0.f;
+    for (int t = 0; t < nt; ++t) r = r + terms[tid * nt + t];
+    sq_dist[p0 + tid] = r;
   }
 }
 
@@ -349,7 +408,8 @@ __device__ void mb_converge(int step_i, int64_t bs, int64_t n, int max_no_improv
     __hip_atomic_store(&st->stop_at, step_i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// sequential fp32 inertia of one batch by a 64-lane block (staged in LDS 2048 at a time)
+// sequential fp32 inertia of one batch by a 64-lane block (staged in LDS 2048 at a time; lane 0
+// folds them in order reading 16 bytes per LDS access)
 __device__ float mb_batch_inertia(int64_t b, const float* __restrict__ sq, float* stage) {
   float acc = 0.f;
   for (int64_t base = 0; base < b; base += 2048) {
@@ -357,8 +417,18 @@ __device__ float mb_batch_inertia(int64_t b, const float* __restrict__ sq, float
 #pragma unroll 8
     for (int t = threadIdx.x; t < m; t += 64) stage[t] = sq[base + t] * 1.0f;
     __syncthreads();
-    if (threadIdx.x == 0)
-      for (int t = 0; t < m; ++t) acc = acc + stage[t];
+    if (threadIdx.x == 0) {
+      const float4* s4 = reinterpret_cast<const float4*>(stage);
+      int t = 0;
+      for (; t + 4 <= m; t += 4) {
+        const float4 v = s4[t >> 2];
+        acc = acc + v.x;
+        acc = acc + v.y;
+        acc = acc + v.z;
+        acc = acc + v.w;
+      }
+      for (; t < m; ++t) acc = acc + stage[t];
+    }
     __syncthreads();
   }
   return acc;
@@ -371,7 +441,10 @@ __global__ void k_mb_converge(int step_i, int64_t bs, int64_t n, int max_no_impr
 }
 
 // ---------------------------------------------------------------------------------------------
-// MiniBatchKMeans update (one wave per cluster)
+// MiniBatchKMeans update (one wave per cluster; block k, when launched, is the step's tail:
+// batch inertia + convergence test). The member list and the members' source rows live in LDS
+// (dynamic: 12*b bytes). cn2_out (nullable) receives the numpy-order norm of the new centre,
+// i.e. the ||C||^2 the next step's assignment needs.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, const float* __restrict__ X,
                                                         const int64_t* __restrict__ rows,
@@ -380,26 +453,27 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
                                                         const float* __restrict__ C_old,
                                                         float* __restrict__ C_new,
                                                         float* __restrict__ Wsum,
-                                                        int32_t* __restrict__ members_ws,
+                                                        float* __restrict__ cn2_out,
                                                         const int32_t* __restrict__ stop, int step_i,
                                                         const float* __restrict__ sq,
                                                         float* __restrict__ inertia_out,
                                                         MBState* __restrict__ st, int converge,
                                                         int64_t n_samples, int max_no_improvement) {
   if (stopped(stop, step_i)) return;
+  extern __shared__ __attribute__((aligned(16))) float mb_lds[];
   const int c = blockIdx.x;
   const int lane = threadIdx.x;
   if (c == k) {
     // tail block (launched only by the fused step): batch inertia, then the convergence test
-    __shared__ float stage[2048];
-    const float inertia = mb_batch_inertia(b, sq, stage);
+    const float inertia = mb_batch_inertia(b, sq, mb_lds);
     if (lane == 0) {
       inertia_out[0] = inertia;
       if (converge) mb_converge(step_i, b, n_samples, max_no_improvement, inertia, st);
     }
     return;
   }
-  int32_t* mem = members_ws + (int64_t)c * b;  // worst case: every batch sample in this cluster
+  int64_t* src = reinterpret_cast<int64_t*>(mb_lds);      // b source rows
+  int32_t* mem = reinterpret_cast<int32_t*>(src + b);     // b member positions
   int count = 0;
   for (int64_t base = 0; base < b; base += 64 * 8) {
     // eight independent label loads in flight per lane, then the ordered ballot compaction
@@ -418,20 +492,20 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
       count += __popcll(m);
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __syncthreads();
+  for (int t = lane; t < count; t += 64) src[t] = rows ? rows[mem[t]] : (int64_t)mem[t];
   __syncthreads();
   // wsum: sequential fp32 in batch order (update_center_dense :78-83); unit weights sum exactly
   float wsum = 0.f;
   if (w) {
-    for (int t = 0; t < count; ++t) {
-      const int32_t i = mem[t];
-      wsum = wsum + w[i];
-    }
+    for (int t = 0; t < count; ++t) wsum = wsum + w[mem[t]];
   } else {
     wsum = (float)count;
   }
   const float W = Wsum[c];
   const int64_t cb = (int64_t)c * dim;
+  // the new row goes to LDS after the member lists (12*b bytes >= 8 KiB; dim <= 512 floats)
+  float* row_out = reinterpret_cast<float*>(mem + b);
   if (wsum > 0.f) {
     const float Wn = W + wsum;
     const float alpha = 1.0f / Wn;  // Cython `1 / weight_sums[c]` with float operands
@@ -442,26 +516,29 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
         float v[4], wi[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int32_t i = mem[t + u];
-          const int64_t src = rows ? rows[i] : (int64_t)i;
-          v[u] = X[src * dim + f];
-          wi[u] = w ? w[i] : 1.0f;
+          v[u] = X[src[t + u] * dim + f];
+          wi[u] = w ? w[mem[t + u]] : 1.0f;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) acc = acc + v[u] * wi[u];
       }
-      for (; t < count; ++t) {
-        const int32_t i = mem[t];
-        const int64_t src = rows ? rows[i] : (int64_t)i;
-        const float wi = w ? w[i] : 1.0f;
-        acc = acc + X[src * dim + f] * wi;
-      }
-      C_new[cb + f] = acc * alpha;
+      for (; t < count; ++t) acc = acc + X[src[t] * dim + f] * (w ? w[mem[t]] : 1.0f);
+      const float v = acc * alpha;
+      C_new[cb + f] = v;
+      row_out[f] = v;
     }
     __syncthreads();
     if (lane == 0) Wsum[c] = Wn;
   } else {
-    for (int f = lane; f < dim; f += 64) C_new[cb + f] = C_old[cb + f];
+    for (int f = lane; f < dim; f += 64) {
+      const float v = C_old[cb + f];
+      C_new[cb + f] = v;
+      row_out[f] = v;
+    }
+  }
+  if (cn2_out) {  // the new row is also staged in LDS: lane 0 forms its norm without HBM reads
+    __syncthreads();
+    if (lane == 0) cn2_out[c] = npy_sumsq(row_out, dim);
   }
 }
 
@@ -666,7 +743,7 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
       GDD_HIP(hipFuncSetAttribute((const void*)k_assign_small,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     k_assign_small<<<(unsigned)((n + 31) / 32), 64 * kSmallWaves, lds, s>>>(
-        n, dim, dimp, X, rows, k, C, labels, sq_dist, stop, step_i);
+        n, dim, dimp, X, rows, k, C, c_norm2, labels, sq_dist, stop, step_i);
     GDD_LAUNCHED();
     return GDD_OK;
   }
@@ -738,30 +815,55 @@ extern "C" int gdd_inertia(int64_t n, const float* sq_dist, const float* w, floa
 }
 
 extern "C" size_t gdd_minibatch_update_ws_bytes(int64_t b, int k) {
-  return align256(sizeof(int32_t) * (size_t)std::max<int64_t>(b, 1) * (size_t)std::max(k, 1));
+  (void)b;
+  (void)k;
+  return 256;  // member lists live in LDS; kept for ABI stability
 }
+
+namespace {
+constexpr int64_t kMaxBatch = 13312;  // 12*b bytes of LDS per update block (<= 156 KiB)
+
+size_t update_lds(int64_t b) {
+  // src rows (8b) + member positions (4b) + the new centre row (<= 512 floats); the tail block
+  // reuses the region as its 2048-float inertia stage
+  return std::max<size_t>(12 * (size_t)b + 512 * sizeof(float), 2048 * sizeof(float));
+}
+
+int launch_update(int grid, int64_t b, int dim, const float* X, const int64_t* rows, const float* w,
+                  const int32_t* labels, int k, const float* C_old, float* C_new, float* Wsum,
+                  float* cn2_out, const int32_t* stop, int step_i, const float* sq, float* inertia,
+                  MBState* st, int converge, int64_t n_samples, int max_ni, hipStream_t s) {
+  GDD_REQUIRE(b <= kMaxBatch, "minibatch: batch %lld exceeds %lld", (long long)b,
+              (long long)kMaxBatch);
+  const size_t lds = update_lds(b);
+  if (lds > 65536)
+    GDD_HIP(hipFuncSetAttribute((const void*)k_minibatch_update,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  k_minibatch_update<<<grid, 64, lds, s>>>(b, dim, X, rows, w, labels, k, C_old, C_new, Wsum,
+                                           cn2_out, stop, step_i, sq, inertia, st, converge,
+                                           n_samples, max_ni);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+}  // namespace
 
 extern "C" int gdd_minibatch_update(int64_t b, int dim, const float* X, const int64_t* rows,
                                     const float* w, const int32_t* labels, int k,
                                     const float* C_old, float* C_new, float* weight_sums, void* ws,
                                     size_t ws_bytes, gdd_stream_t stream) {
   GDD_REQUIRE(b > 0 && dim > 0 && k > 0, "minibatch_update: bad shape");
-  GDD_REQUIRE(X && labels && C_old && C_new && weight_sums && ws, "minibatch_update: null pointer");
+  GDD_REQUIRE(X && labels && C_old && C_new && weight_sums, "minibatch_update: null pointer");
   GDD_REQUIRE(C_old != C_new, "minibatch_update: C_old and C_new must differ");
-  if (ws_bytes < gdd_minibatch_update_ws_bytes(b, k))
-    return fail(GDD_E_WORKSPACE, "minibatch_update: workspace too small");
-  k_minibatch_update<<<k, 64, 0, to_hip(stream)>>>(b, dim, X, rows, w, labels, k, C_old, C_new,
-                                                   weight_sums, static_cast<int32_t*>(ws), nullptr,
-                                                   0, nullptr, nullptr, nullptr, 0, 1, -1);
-  GDD_LAUNCHED();
-  return GDD_OK;
+  (void)ws;
+  (void)ws_bytes;
+  return launch_update(k, b, dim, X, rows, w, labels, k, C_old, C_new, weight_sums, nullptr,
+                       nullptr, 0, nullptr, nullptr, nullptr, 0, 1, -1, to_hip(stream));
 }
 
 // ---- fused MiniBatchKMeans step (_mini_batch_step + _mini_batch_convergence) ------------------
 namespace {
 struct StepWs {
   unsigned long long* keys;
-  int32_t* members;
   float* cn2;
   float* sq;
   float* inertia;
@@ -770,7 +872,6 @@ StepWs carve_step(void* ws, size_t ws_bytes, int64_t b, int k) {
   Carver cv(ws, ws_bytes);
   StepWs w;
   w.keys = cv.take<unsigned long long>(b);
-  w.members = cv.take<int32_t>((size_t)b * k);
   w.cn2 = cv.take<float>(k);
   w.sq = cv.take<float>(b);
   w.inertia = cv.take<float>(1);
@@ -781,16 +882,14 @@ StepWs carve_step(void* ws, size_t ws_bytes, int64_t b, int k) {
 extern "C" size_t gdd_minibatch_state_bytes(void) { return sizeof(MBState); }
 
 extern "C" size_t gdd_minibatch_step_ws_bytes(int64_t b, int k) {
-  return gdd_kmeans_assign_ws_bytes(b) + gdd_minibatch_update_ws_bytes(b, k) +
-         align256(sizeof(float) * (size_t)std::max(k, 1)) +            // ||C||^2
-         align256(sizeof(float) * (size_t)std::max<int64_t>(b, 1)) +   // sq_dist
-         align256(sizeof(float)) + 1024;                               // batch inertia
+  return gdd_kmeans_assign_ws_bytes(b) + align256(sizeof(float) * (size_t)std::max(k, 1)) +
+         align256(sizeof(float) * (size_t)std::max<int64_t>(b, 1)) + align256(sizeof(float)) + 1024;
 }
 
 extern "C" int gdd_minibatch_step(int64_t b, int dim, const float* X, const int64_t* rows, int k,
                                   const float* C_old, float* C_new, float* weight_sums,
                                   int32_t* labels, int step_i, int64_t n_samples,
-                                  int max_no_improvement, int converge, void* state, void* ws,
+                                  int max_no_improvement, int flags, void* state, void* ws,
                                   size_t ws_bytes, gdd_stream_t stream) {
   GDD_REQUIRE(b > 0 && dim > 0 && dim <= 512 && k > 0 && n_samples > 0, "minibatch_step: bad shape");
   GDD_REQUIRE(X && rows && C_old && C_new && weight_sums && labels && state && ws,
@@ -803,18 +902,22 @@ extern "C" int gdd_minibatch_step(int64_t b, int dim, const float* X, const int6
   const int32_t* stop = &st->stop_at;
   StepWs w = carve_step(ws, ws_bytes, b, k);
   const int dimp = (dim + 1) & ~1;
-  if (!use_small_assign(b, dimp)) {  // the fused small kernel computes its own norms
-    k_row_norms<<<blocks_for(k), 256, 0, s>>>(k, dim, C_old, w.cn2, stop, step_i);
-    GDD_LAUNCHED();
+  const bool norms_valid = (flags & GDD_STEP_NORMS_VALID) != 0;
+  const float* cn2 = w.cn2;
+  if (!norms_valid) {
+    if (use_small_assign(b, dimp)) {
+      cn2 = nullptr;  // the fused kernel computes them from its LDS tiles
+    } else {
+      k_row_norms<<<blocks_for(k), 256, 0, s>>>(k, dim, C_old, w.cn2, stop, step_i);
+      GDD_LAUNCHED();
+    }
   }
-  int rc = launch_assign(b, dim, X, rows, k, C_old, w.cn2, labels, w.sq, w.keys, stop, step_i, s);
+  int rc = launch_assign(b, dim, X, rows, k, C_old, cn2, labels, w.sq, w.keys, stop, step_i, s);
   if (rc) return rc;
-  // k update blocks + one tail block (batch inertia, convergence test)
-  k_minibatch_update<<<k + 1, 64, 0, s>>>(b, dim, X, rows, nullptr, labels, k, C_old, C_new,
-                                          weight_sums, w.members, stop, step_i, w.sq, w.inertia, st,
-                                          converge, n_samples, max_no_improvement);
-  GDD_LAUNCHED();
-  return GDD_OK;
+  // k update blocks (+ ||C_new||^2 for the next step) and one tail block (inertia, convergence)
+  return launch_update(k + 1, b, dim, X, rows, nullptr, labels, k, C_old, C_new, weight_sums, w.cn2,
+                       stop, step_i, w.sq, w.inertia, st, flags & GDD_STEP_CONVERGE, n_samples,
+                       max_no_improvement, s);
 }
 
 extern "C" int gdd_minibatch_converge(int64_t b, int k, int step_i, int64_t n_samples,

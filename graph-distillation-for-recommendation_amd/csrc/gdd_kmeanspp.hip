@@ -20,6 +20,7 @@ namespace {
 
 constexpr int kMaxTrials = 16;
 constexpr int kTailThreads = 1024;
+constexpr int kTailLdsCum = 6144;  // cumulative potential kept in LDS up to this n (48 KiB)
 
 struct KppState {
   float pot;   // current potential (fp32, as sklearn keeps it)
@@ -38,17 +39,20 @@ __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restr
   const int lane = threadIdx.x & 63;
   const int64_t n1 = n & ~31ll;
   const int64_t n64 = n1 & ~63ll;
+  // y == nullptr: unit sample weights (fma(x, 1, a) == a + x, one rounding either way)
   float a = 0.f;
   int64_t i = lane;
-  for (; i + 192 < n64; i += 256) {  // four independent load pairs ahead of the ordered fmas
-    const float x0 = x[i], x1 = x[i + 64], x2 = x[i + 128], x3 = x[i + 192];
-    const float y0 = y[i], y1 = y[i + 64], y2 = y[i + 128], y3 = y[i + 192];
-    a = __builtin_fmaf(x0, y0, a);
-    a = __builtin_fmaf(x1, y1, a);
-    a = __builtin_fmaf(x2, y2, a);
-    a = __builtin_fmaf(x3, y3, a);
+  for (; i + 64 * 7 < n64; i += 64 * 8) {  // eight independent loads ahead of the ordered fmas
+    float xv[8], yv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      xv[u] = x[i + 64 * u];
+      yv[u] = y ? y[i + 64 * u] : 1.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a = __builtin_fmaf(xv[u], yv[u], a);
   }
-  for (; i < n64; i += 64) a = __builtin_fmaf(x[i], y[i], a);
+  for (; i < n64; i += 64) a = __builtin_fmaf(x[i], y ? y[i] : 1.0f, a);
   scratch[lane] = a;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -65,7 +69,7 @@ __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restr
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int l = 0; l < 8; ++l)
-          acc[u][l] = __builtin_fmaf(x[n64 + u * 8 + l], y[n64 + u * 8 + l], acc[u][l]);
+          acc[u][l] = __builtin_fmaf(x[n64 + u * 8 + l], y ? y[n64 + u * 8 + l] : 1.0f, acc[u][l]);
     }
     float s[8];
 #pragma unroll
@@ -75,7 +79,7 @@ __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restr
     for (int l = 0; l < 4; ++l) h[l] = s[l] + s[l + 4];
     double dot = n1 ? (double)((h[0] + h[1]) + (h[2] + h[3])) : 0.0;
     for (int64_t t = n1; t < n; ++t) {
-      const float p = y[t] * x[t];
+      const float p = (y ? y[t] : 1.0f) * x[t];
       dot = dot + (double)p;
     }
     r = (float)dot;
@@ -140,7 +144,8 @@ __global__ __launch_bounds__(kTailThreads) void k_kpp_tail(
     KppState* __restrict__ st) {
   __shared__ float scratch[kMaxTrials * 64];
   __shared__ float s_pot[kMaxTrials];
-  __shared__ double s_part[kTailThreads];
+  __shared__ double s_part[kTailThreads / 64];
+  __shared__ double s_cum[kTailLdsCum];
   __shared__ int s_best;
   __shared__ int64_t s_src;
   const int tid = threadIdx.x;
@@ -186,19 +191,32 @@ __global__ __launch_bounds__(kTailThreads) void k_kpp_tail(
   const int64_t chunk = (n + kTailThreads - 1) / kTailThreads;
   const int64_t lo = min<int64_t>(n, tid * chunk), hi = min<int64_t>(n, lo + chunk);
   double run = 0.0;
-  for (int64_t i = lo; i < hi; ++i) run = run + (double)(w[i] * closest[i]);
-  s_part[tid] = run;
-  __syncthreads();
-  for (int off = 1; off < kTailThreads; off <<= 1) {
-    const double v = tid >= off ? s_part[tid - off] : 0.0;
-    __syncthreads();
-    s_part[tid] += v;
-    __syncthreads();
+  for (int64_t i = lo; i < hi; ++i) run = run + (double)((w ? w[i] : 1.0f) * closest[i]);
+  // exclusive scan of the per-thread chunk totals: wave shuffles, then the 16 wave totals
+  const int lane = tid & 63;
+  double incl = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
   }
-  double base = tid ? s_part[tid - 1] : 0.0;
+  if (lane == 63) s_part[wave] = incl;
+  __syncthreads();
+  if (tid == 0) {
+    double a = 0.0;
+    for (int q = 0; q < kTailThreads / 64; ++q) {
+      const double t = s_part[q];
+      s_part[q] = a;
+      a += t;
+    }
+  }
+  __syncthreads();
+  double base = s_part[wave] + (incl - run);
+  // small n: the cumulative potential stays in LDS for the binary searches
+  double* cs = (n <= kTailLdsCum) ? s_cum : cum;
   for (int64_t i = lo; i < hi; ++i) {
-    base = base + (double)(w[i] * closest[i]);
-    cum[i] = base;
+    base = base + (double)((w ? w[i] : 1.0f) * closest[i]);
+    cs[i] = base;
   }
   __threadfence_block();
   __syncthreads();
@@ -207,7 +225,7 @@ __global__ __launch_bounds__(kTailThreads) void k_kpp_tail(
     int64_t a = 0, b = n;  // first index with cum[idx] >= r  (np.searchsorted side='left')
     while (a < b) {
       const int64_t m = (a + b) >> 1;
-      if (cum[m] < r)
+      if (cs[m] < r)
         a = m + 1;
       else
         b = m;
@@ -260,11 +278,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   float* ones = cv.take<float>(n);
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans++: workspace too small");
   const unsigned nb = (unsigned)((n + 255) / 256);
-  if (!w) {
-    k_ones<<<nb, 256, 0, s>>>(n, ones);
-    GDD_LAUNCHED();
-    w = ones;
-  }
+  (void)ones;  // w == nullptr: unit sample weights, handled in the kernels
   k_kpp_init<<<nb, 256, 0, s>>>(n, dim, X, first_id, xsq, closest0);
   GDD_LAUNCHED();
   k_kpp_tail<<<1, kTailThreads, 0, s>>>(n, dim, X, w, closest0, dist[1], n_trials, 0, k, first_id,

@@ -119,18 +119,21 @@ int gdd_minibatch_update(int64_t b, int dim, const float* X, const int64_t* rows
 
 /* One MiniBatchKMeans step on the device: sklearn _mini_batch_step without the reassignment        */
 /* branch (_kmeans.py:1556-1638) — ||C_old||^2, MFMA assignment of the gathered batch X[rows],       */
-/* sequential batch inertia, centre update into C_new — followed, if converge != 0, by               */
+/* sequential batch inertia, centre update into C_new — followed, with GDD_STEP_CONVERGE, by         */
 /* _mini_batch_convergence (:1960-2027, EWA of inertia/b in unfused fp64, max_no_improvement; -1 =   */
-/* None). `state` (gdd_minibatch_state_bytes(), zero-initialised) carries the EWA state and a stop   */
-/* flag; once the flag is set every later step/converge call is a no-op, so the host may enqueue     */
-/* steps ahead of the stopping decision and read the flag (state int32 at offset 16) and the 0-based */
-/* stop step (int32 at offset 32) when it synchronises. Reassignment steps call step with            */
-/* converge = 0, apply the host's reassignment, then gdd_minibatch_converge.                        */
+/* None; the test reads only the batch inertia, so it may precede the host's reassignment).          */
+/* `state` (gdd_minibatch_state_bytes(), zero-initialised) carries the EWA state and, as an int32 at */
+/* offset 16, stop_at = 0 while running or s+1 once the test fired at step s: every kernel of a      */
+/* later step is then a no-op, so the host may enqueue steps ahead of the decision. Each step leaves */
+/* ||C_new||^2 in the workspace; pass GDD_STEP_NORMS_VALID when C_old is the previous step's C_new  */
+/* (unmodified by the host) to reuse them. batch b <= 13312.                                         */
+#define GDD_STEP_CONVERGE 1
+#define GDD_STEP_NORMS_VALID 2
 size_t gdd_minibatch_state_bytes(void);
 size_t gdd_minibatch_step_ws_bytes(int64_t b, int k);
 int gdd_minibatch_step(int64_t b, int dim, const float* X, const int64_t* rows, int k,
                        const float* C_old, float* C_new, float* weight_sums, int32_t* labels,
-                       int step_i, int64_t n_samples, int max_no_improvement, int converge,
+                       int step_i, int64_t n_samples, int max_no_improvement, int flags,
                        void* state, void* ws, size_t ws_bytes, gdd_stream_t stream);
 int gdd_minibatch_converge(int64_t b, int k, int step_i, int64_t n_samples, int max_no_improvement,
                            void* state, void* ws, size_t ws_bytes, gdd_stream_t stream);
