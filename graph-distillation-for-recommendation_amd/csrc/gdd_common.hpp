@@ -102,4 +102,27 @@ __host__ __device__ inline double cr_rsqrt(double x) {
   return (__builtin_fabs(r1) < __builtin_fabs(r0)) ? y1 : y;
 }
 
+// ---------------------------------------------------------------------------------------------
+// in-kernel phase stamps (diagnostic builds only: make STAMPS=1 builds libgdd_stamps.so).
+// GDD_STAMP_WHEN(table, who, slot) records s_memrealtime (100 MHz) from one thread into a per-file table
+// that gdd_dbg_stamps_<file>() copies out; in the product build it expands to nothing.
+// ---------------------------------------------------------------------------------------------
+#ifdef GDD_STAMPS
+#define GDD_STAMP_TABLE(file)                                                                   \
+  __device__ unsigned long long g_stamps_##file[256];                                           \
+  extern "C" int gdd_dbg_stamps_##file(unsigned long long* out) {                              \
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps_##file), sizeof(g_stamps_##file)); \
+  }
+// stamp from the thread for which `who` holds (e.g. threadIdx.x == 0 && blockIdx.x == 0)
+#define GDD_STAMP_WHEN(table, who, slot)                                                        \
+  do {                                                                                          \
+    if (who) table[(slot)] = __builtin_amdgcn_s_memrealtime();                                  \
+  } while (0)
+#else
+#define GDD_STAMP_TABLE(file)
+#define GDD_STAMP_WHEN(table, who, slot) \
+  do {                                   \
+  } while (0)
+#endif
+
 }  // namespace gdd

@@ -19,6 +19,7 @@
 #include "gdd_common.hpp"
 
 namespace gdd {
+GDD_STAMP_TABLE(kmeans)
 namespace {
 
 using floatx16 = __attribute__((ext_vector_type(16))) float;
@@ -192,39 +193,71 @@ __global__ void k_assign_finalize(int64_t n, int dim, const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------------
-// small batches (minibatch steps): one block of 8 waves per 32 points. The waves split the
-// centres (wave w takes tiles w, w+8, ...), stage their own 32-centre tile and its numpy-order
-// norms in LDS, run the same MFMA chain and epilogue as k_assign, and the block merges the 8
-// partial minima in LDS — no atomics, no key buffer, labels and sq_dist written directly.
+// small batches (minibatch steps): one block of WAVES waves per 32 points. Wave w owns centre tiles
+// w, w+WAVES, ...; it stages its tile (and, without cached norms, their numpy-order norms) in LDS,
+// runs the MFMA chain with all operands preloaded from LDS into registers (the chain then issues
+// back to back), and the block merges the per-wave minima in LDS — no atomics, no key buffer,
+// labels and sq_dist written directly. Latency plan (one launch ≈ two dependent memory trips):
+// the row indices and every wave's first centre tile are requested together; the point rows
+// follow once the indices land. VEC: dim % 4 == 0 and 16-byte aligned X/C (float4 loads).
 // ---------------------------------------------------------------------------------------------
-constexpr int kSmallWaves = 8;
-__host__ __device__ inline size_t assign_small_lds(int dimp) {
-  const int S = dimp + 1;
-  return sizeof(float) * ((size_t)(32 + 32 * kSmallWaves) * S + 32 * kSmallWaves) +
-         sizeof(unsigned long long) * 32 * kSmallWaves + 16;
+// LDS: points, WAVES centre tiles, their norms, the per-wave minima, the distance terms
+__host__ __device__ inline size_t assign_small_lds(int waves, int dim) {
+  const int dimp = (dim + 1) & ~1, S = dimp + 1;
+  const int nt = (dim >> 2) + (dim & 3);
+  return sizeof(float) * ((size_t)(32 + 32 * waves) * S + 32 * waves) + 16 +
+         sizeof(unsigned long long) * 32 * waves + sizeof(float) * 32 * (size_t)nt;
 }
 
-// Stage a 32-row tile (row r = src_row(r), `dim` floats, rows >= valid read as zero) into LDS rows
-// of stride S, zero-padding column dim when dimp > dim. Loads are issued eight per lane before
-// the LDS stores, so a tile costs ~one memory latency per 8*nlanes elements instead of one each.
-template <class RowPtr>
-__device__ __forceinline__ void stage_tile32(float* __restrict__ dst, int S, RowPtr src_row,
-                                             int valid, int dim, int dimp, int lane, int nlanes) {
-  const int total = 32 * dim;
-  for (int base = 0; base < total; base += nlanes * 8) {
-    float v[8];
+// rows [0, nrows) of a 32-row tile, row r at src(r) (dim floats), into LDS rows of stride S;
+// rows >= nrows and the pad column (dimp > dim) are zero. Up to 8 loads per lane are issued
+// before the first LDS store.
+template <bool VEC, int U = 8, class RowPtr>
+__device__ __forceinline__ void stage_rows32(float* __restrict__ dst, int S, RowPtr src, int nrows,
+                                             int dim, int dimp, int lane, int nlanes) {
+  if (VEC) {
+    const int q = dim >> 2;  // float4 per row
+    const int total = 32 * q;
+    for (int base = 0; base < total; base += nlanes * U) {
+      float4 v[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int idx = base + u * nlanes + lane;
-      const int r = idx / dim;
-      v[u] = (idx < total && r < valid) ? src_row(r)[idx - r * dim] : 0.f;
+      for (int u = 0; u < U; ++u) {
+        const int idx = base + u * nlanes + lane;
+        const int r = idx / q;
+        v[u] = (idx < total && r < nrows)
+                   ? *reinterpret_cast<const float4*>(src(r) + 4 * (idx - r * q))
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int idx = base + u * nlanes + lane;
+        if (idx < total) {
+          const int r = idx / q;
+          float* d = dst + r * S + 4 * (idx - r * q);
+          d[0] = v[u].x;
+          d[1] = v[u].y;
+          d[2] = v[u].z;
+          d[3] = v[u].w;
+        }
+      }
     }
+  } else {
+    const int total = 32 * dim;
+    for (int base = 0; base < total; base += nlanes * U) {
+      float v[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int idx = base + u * nlanes + lane;
-      if (idx < total) {
+      for (int u = 0; u < U; ++u) {
+        const int idx = base + u * nlanes + lane;
         const int r = idx / dim;
-        dst[r * S + (idx - r * dim)] = v[u];
+        v[u] = (idx < total && r < nrows) ? src(r)[idx - r * dim] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int idx = base + u * nlanes + lane;
+        if (idx < total) {
+          const int r = idx / dim;
+          dst[r * S + (idx - r * dim)] = v[u];
+        }
       }
     }
   }
@@ -232,38 +265,83 @@ __device__ __forceinline__ void stage_tile32(float* __restrict__ dst, int S, Row
     for (int r = lane; r < 32; r += nlanes) dst[r * S + dim] = 0.f;
 }
 
-__global__ __launch_bounds__(64 * kSmallWaves) void k_assign_small(
+// D = C_tile · P_tileᵀ over the feature axis in order 0,1,2,... as ONE fma chain per element
+// (bit-identical to the OpenBLAS sgemm element). Operands of up to P chain steps are read from
+// LDS into registers first, so the MFMAs issue back to back instead of one LDS latency apart.
+template <int P>
+__device__ __forceinline__ floatx16 mfma_chain(const float* __restrict__ ap,
+                                               const float* __restrict__ bp, int dimp) {
+  floatx16 acc = {};
+  for (int s0 = 0; s0 < dimp; s0 += 2 * P) {
+    const int ns = min(P, (dimp - s0) >> 1);
+    float av[P], bv[P];
+#pragma unroll
+    for (int u = 0; u < P; ++u)
+      if (u < ns) {
+        av[u] = ap[s0 + 2 * u];
+        bv[u] = bp[s0 + 2 * u];
+      }
+#pragma unroll
+    for (int u = 0; u < P; ++u)
+      if (u < ns) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+template <int WAVES, bool VEC>
+__global__ __launch_bounds__(64 * WAVES) void k_assign_small(
     int64_t n, int dim, int dimp, const float* __restrict__ X, const int64_t* __restrict__ rows,
     int k, const float* __restrict__ C, const float* __restrict__ cn2, int32_t* __restrict__ labels,
     float* __restrict__ sq_dist, const int32_t* __restrict__ stop, int step_i) {
   if (stopped(stop, step_i)) return;
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 0);
+  constexpr int kTileU = WAVES == 16 ? 6 : 8;  // 16 waves: 128 VGPRs per lane, fewer loads in flight
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int S = dimp + 1;
-  float* Pl = lds;                                   // 32 points x S
-  float* Cl = Pl + 32 * S;                           // kSmallWaves x 32 centres x S
-  float* Nl = Cl + (size_t)kSmallWaves * 32 * S;     // kSmallWaves x 32 norms
+  float* Pl = lds;                                 // 32 points x S
+  float* Cl = Pl + 32 * S;                         // WAVES x 32 centres x S (consecutive tiles)
+  float* Nl = Cl + (size_t)WAVES * 32 * S;         // WAVES x 32 norms
   unsigned long long* Kl =
-      reinterpret_cast<unsigned long long*>(((uintptr_t)(Nl + 32 * kSmallWaves) + 15) & ~uintptr_t(15));
+      reinterpret_cast<unsigned long long*>(((uintptr_t)(Nl + 32 * WAVES) + 15) & ~uintptr_t(15));
   __shared__ int64_t s_rows[32];
+  __shared__ int s_lab[32];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t p0 = (int64_t)blockIdx.x * 32;
   const int np = (int)min<int64_t>(32, n - p0);
-  if (tid < 32) s_rows[tid] = tid < np ? (rows ? rows[p0 + tid] : p0 + tid) : 0;
-  __syncthreads();
-  stage_tile32(Pl, S, [&](int r) { return X + s_rows[r] * dim; }, np, dim, dimp, tid, blockDim.x);
-  __syncthreads();
+  // trip 1: the batch's row indices and this wave's first centre tile, requested together
+  int64_t my_row = 0;
+  if (tid < 32 && tid < np) my_row = rows ? rows[p0 + tid] : p0 + tid;
   float* Cw = Cl + (size_t)wave * 32 * S;
   float* Nw = Nl + wave * 32;
+  if (wave * 32 < k) {
+    const float* Cb = C + (int64_t)wave * 32 * dim;
+    stage_rows32<VEC, kTileU>(Cw, S, [&](int r) { return Cb + (int64_t)r * dim; }, k - wave * 32,
+                              dim, dimp, lane, 64);
+    if (cn2 && lane < 32) Nw[lane] = (wave * 32 + lane < k) ? cn2[wave * 32 + lane] : 0.f;
+  }
+  if (tid < 32) s_rows[tid] = my_row;
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 2);
+  // trip 2: the point rows
+  stage_rows32<VEC, 4>(Pl, S, [&](int r) { return X + s_rows[r] * dim; }, np, dim, dimp, tid,
+                       64 * WAVES);
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 3);
   const int kh = lane >> 5;
   const float* bp = Pl + (lane & 31) * S + kh;
   const float* ap = Cw + (lane & 31) * S + kh;
   unsigned long long best = ~0ull;
-  for (int cb = wave * 32; cb < k; cb += 32 * kSmallWaves) {
-    const float* Cb = C + (int64_t)cb * dim;
-    stage_tile32(Cw, S, [&](int r) { return Cb + (int64_t)r * dim; }, k - cb, dim, dimp, lane, 64);
-    if (cn2) {
-      if (lane < 32) Nw[lane] = (cb + lane < k) ? cn2[cb + lane] : 0.f;
-    } else {
+  for (int cb = wave * 32; cb < k; cb += 32 * WAVES) {
+    if (cb != wave * 32) {  // k > 32*WAVES: later tiles of this wave (after its reads of the last)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const float* Cb = C + (int64_t)cb * dim;
+      stage_rows32<VEC, kTileU>(Cw, S, [&](int r) { return Cb + (int64_t)r * dim; }, k - cb, dim,
+                                dimp, lane, 64);
+      if (cn2 && lane < 32) Nw[lane] = (cb + lane < k) ? cn2[cb + lane] : 0.f;
+    }
+    if (!cn2) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -272,9 +350,8 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_assign_small(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    floatx16 acc = {};
-    for (int s2 = 0; s2 < dimp; s2 += 2)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[s2], bp[s2], acc, 0, 0, 0);
+    const floatx16 acc = mfma_chain<WAVES == 16 ? 10 : 16>(ap, bp, dimp);
+    GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 5);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int ci = (r & 3) + 8 * (r >> 2) + 4 * kh;
@@ -283,20 +360,16 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_assign_small(
         best = key < best ? key : best;
       }
     }
-    // the next tile overwrites Cw/Nw: every lane's reads of this one must have completed
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   const unsigned long long other = __shfl_xor(best, 32);
   best = other < best ? other : best;
   if (lane < 32) Kl[wave * 32 + lane] = best;
   __syncthreads();
-  __shared__ int s_lab[32];
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 13);
   if (wave == 0 && lane < 32) {
     unsigned long long b = Kl[lane];
 #pragma unroll
-    for (int w = 1; w < kSmallWaves; ++w) {
+    for (int w = 1; w < WAVES; ++w) {
       const unsigned long long o = Kl[w * 32 + lane];
       b = o < b ? o : b;
     }
@@ -306,15 +379,18 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_assign_small(
   }
   if (!sq_dist) return;
   __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 14);
   // ||x - c_label||^2 in the _euclidean_dense_dense order: the terms (4-element groups, then the
-  // remainder elements) are formed by the whole block, then each point's lane adds them in order
+  // remainder elements) are formed by the whole block, then each point's lane adds them in order.
+  // With k <= 32*WAVES every centre row is still in LDS (tile c/32 row c%32 = Cl + c*S).
+  const bool resident = k <= 32 * WAVES;
   const int ng = dim >> 2, nt = ng + (dim & 3);
-  float* terms = Cl;  // the centre tiles are no longer needed
+  float* tbuf = reinterpret_cast<float*>(Kl + 32 * WAVES);
   for (int idx = tid; idx < 32 * nt; idx += blockDim.x) {
     const int p = idx / nt, t = idx - p * nt;
     if (p >= np) continue;
     const float* x = Pl + p * S;
-    const float* c = C + (int64_t)s_lab[p] * dim;
+    const float* c = resident ? Cl + (size_t)s_lab[p] * S : C + (int64_t)s_lab[p] * dim;
     float v;
     if (t < ng) {
       const int j = 4 * t;
@@ -326,19 +402,52 @@ __global__ __launch_bounds__(64 * kSmallWaves) void k_assign_small(
       const float d0 = x[j] - c[j];
       v = d0 * d0;
     }
-    terms[idx] = v;
+    tbuf[idx] = v;
   }
   __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 15);
   if (tid < np) {
     float r = 0.f;
-    for (int t = 0; t < nt; ++t) r = r + terms[tid * nt + t];
+    for (int t = 0; t < nt; ++t) r = r + tbuf[tid * nt + t];
     sq_dist[p0 + tid] = r;
   }
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 16);
+}
+
+// Sequential fp32 fold acc = ((acc + b[0]) + b[1]) + ... of m LDS floats by ONE lane. The next
+// eight float4 reads are issued before the current 32 dependent adds, so the add chain (not the
+// LDS latency) bounds it. b must be 16-byte aligned.
+__device__ __forceinline__ float fold_seq_lds(const float* __restrict__ b, int m, float acc) {
+  const float4* b4 = reinterpret_cast<const float4*>(b);
+  const int g = m >> 5;
+  if (g > 0) {
+    float4 cur[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) cur[u] = b4[u];
+    for (int q = 0; q < g; ++q) {
+      float4 nxt[8];
+      if (q + 1 < g) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) nxt[u] = b4[(q + 1) * 8 + u];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc = acc + cur[u].x;
+        acc = acc + cur[u].y;
+        acc = acc + cur[u].z;
+        acc = acc + cur[u].w;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
+    }
+  }
+  for (int t = g << 5; t < m; ++t) acc = acc + b[t];
+  return acc;
 }
 
 // ---------------------------------------------------------------------------------------------
-// inertia: sequential fp32 sum in sample order. The block stages 4096 products at a time in LDS;
-// one lane folds them in order (float4 LDS reads keep the dependent add chain fed).
+// inertia: sequential fp32 sum in sample order. Two LDS buffers of 4096 products: while lane 0 of
+// wave 0 folds one (fold_seq_lds), the other waves stage the next.
 // ---------------------------------------------------------------------------------------------
 constexpr int kInertiaChunk = 4096;
 __global__ __launch_bounds__(1024) void k_inertia(int64_t n, const float* __restrict__ sq,
@@ -346,28 +455,28 @@ __global__ __launch_bounds__(1024) void k_inertia(int64_t n, const float* __rest
                                                   float* __restrict__ out,
                                                   const int32_t* __restrict__ stop, int step_i) {
   if (stopped(stop, step_i)) return;
-  __shared__ __attribute__((aligned(16))) float buf[kInertiaChunk];
+  __shared__ __attribute__((aligned(16))) float buf[2][kInertiaChunk];
+  const int nthr = blockDim.x - 64;  // waves 1.. stage
+  const int st = threadIdx.x - 64;
+  auto stage = [&](int64_t base, float* dst) {
+    const int m = (int)min<int64_t>(kInertiaChunk, n - base);
+    for (int t = st; t < m; t += nthr) {
+      const int64_t i = base + t;
+      dst[t] = w ? sq[i] * w[i] : sq[i] * 1.0f;  // sq_dist * sample_weight[i]
+    }
+  };
+  if (threadIdx.x >= 64 && n > 0) stage(0, buf[0]);
+  __syncthreads();
   float acc = 0.f;
+  int cur = 0;
   for (int64_t b = 0; b < n; b += kInertiaChunk) {
-    const int m = (int)min<int64_t>(kInertiaChunk, n - b);
-    for (int t = threadIdx.x; t < m; t += blockDim.x) {
-      const int64_t i = b + t;
-      buf[t] = w ? sq[i] * w[i] : sq[i] * 1.0f;  // sq_dist * sample_weight[i]
+    if (threadIdx.x >= 64) {
+      if (b + kInertiaChunk < n) stage(b + kInertiaChunk, buf[cur ^ 1]);
+    } else if (threadIdx.x == 0) {
+      acc = fold_seq_lds(buf[cur], (int)min<int64_t>(kInertiaChunk, n - b), acc);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      const float4* b4 = reinterpret_cast<const float4*>(buf);
-      int t = 0;
-      for (; t + 4 <= m; t += 4) {
-        const float4 v = b4[t >> 2];
-        acc = acc + v.x;
-        acc = acc + v.y;
-        acc = acc + v.z;
-        acc = acc + v.w;
-      }
-      for (; t < m; ++t) acc = acc + buf[t];
-    }
-    __syncthreads();
+    cur ^= 1;
   }
   if (threadIdx.x == 0) out[0] = acc;
 }
@@ -417,18 +526,7 @@ __device__ float mb_batch_inertia(int64_t b, const float* __restrict__ sq, float
 #pragma unroll 8
     for (int t = threadIdx.x; t < m; t += 64) stage[t] = sq[base + t] * 1.0f;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      const float4* s4 = reinterpret_cast<const float4*>(stage);
-      int t = 0;
-      for (; t + 4 <= m; t += 4) {
-        const float4 v = s4[t >> 2];
-        acc = acc + v.x;
-        acc = acc + v.y;
-        acc = acc + v.z;
-        acc = acc + v.w;
-      }
-      for (; t < m; ++t) acc = acc + stage[t];
-    }
+    if (threadIdx.x == 0) acc = fold_seq_lds(stage, m, acc);
     __syncthreads();
   }
   return acc;
@@ -460,18 +558,23 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
                                                         MBState* __restrict__ st, int converge,
                                                         int64_t n_samples, int max_no_improvement) {
   if (stopped(stop, step_i)) return;
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 20);
+  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0 && (int)blockIdx.x == k, 30);
   extern __shared__ __attribute__((aligned(16))) float mb_lds[];
   const int c = blockIdx.x;
   const int lane = threadIdx.x;
   if (c == k) {
     // tail block (launched only by the fused step): batch inertia, then the convergence test
     const float inertia = mb_batch_inertia(b, sq, mb_lds);
+    GDD_STAMP_WHEN(g_stamps_kmeans, lane == 0, 31);
     if (lane == 0) {
       inertia_out[0] = inertia;
       if (converge) mb_converge(step_i, b, n_samples, max_no_improvement, inertia, st);
     }
+    GDD_STAMP_WHEN(g_stamps_kmeans, lane == 0, 32);
     return;
   }
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 21);
   int64_t* src = reinterpret_cast<int64_t*>(mb_lds);      // b source rows
   int32_t* mem = reinterpret_cast<int32_t*>(src + b);     // b member positions
   int count = 0;
@@ -493,8 +596,10 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
     }
   }
   __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 22);
   for (int t = lane; t < count; t += 64) src[t] = rows ? rows[mem[t]] : (int64_t)mem[t];
   __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 23);
   // wsum: sequential fp32 in batch order (update_center_dense :78-83); unit weights sum exactly
   float wsum = 0.f;
   if (w) {
@@ -536,10 +641,12 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
       row_out[f] = v;
     }
   }
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 24);
   if (cn2_out) {  // the new row is also staged in LDS: lane 0 forms its norm without HBM reads
     __syncthreads();
     if (lane == 0) cn2_out[c] = npy_sumsq(row_out, dim);
   }
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 25);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -727,8 +834,38 @@ size_t assign_lds(int waves, int dimp, int cch) {
   return sizeof(float) * ((size_t)ncp * S + (size_t)32 * waves * S + ncp);
 }
 
-bool use_small_assign(int64_t n, int dimp) {
-  return n <= 16384 && assign_small_lds(dimp) <= 160 * 1024;
+constexpr size_t kLdsCap = 160 * 1024;
+
+bool use_small_assign(int64_t n, int dim) {
+  return n <= 16384 && assign_small_lds(4, dim) <= kLdsCap;
+}
+
+template <int W, bool VEC>
+int launch_assign_small_t(int64_t n, int dim, const float* X, const int64_t* rows, int k,
+                          const float* C, const float* cn2, int32_t* labels, float* sq_dist,
+                          const int32_t* stop, int step_i, hipStream_t s) {
+  const int dimp = (dim + 1) & ~1;
+  const size_t lds = assign_small_lds(W, dim);
+  if (lds > 65536)
+    GDD_HIP(hipFuncSetAttribute((const void*)k_assign_small<W, VEC>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  k_assign_small<W, VEC><<<(unsigned)((n + 31) / 32), 64 * W, lds, s>>>(
+      n, dim, dimp, X, rows, k, C, cn2, labels, sq_dist, stop, step_i);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+template <bool VEC>
+int launch_assign_small(int64_t n, int dim, const float* X, const int64_t* rows, int k,
+                        const float* C, const float* cn2, int32_t* labels, float* sq_dist,
+                        const int32_t* stop, int step_i, hipStream_t s) {
+  // one 32-centre tile per wave when LDS allows (k <= 512), else fewer waves looping over tiles
+  const int tiles = (k + 31) / 32;
+  if (tiles > 8 && assign_small_lds(16, dim) <= kLdsCap)
+    return launch_assign_small_t<16, VEC>(n, dim, X, rows, k, C, cn2, labels, sq_dist, stop, step_i, s);
+  if (tiles > 4 && assign_small_lds(8, dim) <= kLdsCap)
+    return launch_assign_small_t<8, VEC>(n, dim, X, rows, k, C, cn2, labels, sq_dist, stop, step_i, s);
+  return launch_assign_small_t<4, VEC>(n, dim, X, rows, k, C, cn2, labels, sq_dist, stop, step_i, s);
 }
 
 // labels (+ optional per-sample sq_dist) of n samples against k centres.
@@ -737,15 +874,10 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
                   const float* c_norm2, int32_t* labels, float* sq_dist,
                   unsigned long long* keys, const int32_t* stop, int step_i, hipStream_t s) {
   const int dimp = (dim + 1) & ~1;
-  if (use_small_assign(n, dimp)) {
-    const size_t lds = assign_small_lds(dimp);
-    if (lds > 65536)
-      GDD_HIP(hipFuncSetAttribute((const void*)k_assign_small,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    k_assign_small<<<(unsigned)((n + 31) / 32), 64 * kSmallWaves, lds, s>>>(
-        n, dim, dimp, X, rows, k, C, c_norm2, labels, sq_dist, stop, step_i);
-    GDD_LAUNCHED();
-    return GDD_OK;
+  if (use_small_assign(n, dim)) {
+    const bool vec = (dim % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(C)) & 15) == 0;
+    return vec ? launch_assign_small<true>(n, dim, X, rows, k, C, c_norm2, labels, sq_dist, stop, step_i, s)
+               : launch_assign_small<false>(n, dim, X, rows, k, C, c_norm2, labels, sq_dist, stop, step_i, s);
   }
   GDD_REQUIRE(c_norm2 && keys, "assign: large-n path needs c_norm2 and the key workspace");
   const int waves = dimp <= 96 ? 4 : (dimp <= 224 ? 2 : 1);
@@ -905,7 +1037,7 @@ extern "C" int gdd_minibatch_step(int64_t b, int dim, const float* X, const int6
   const bool norms_valid = (flags & GDD_STEP_NORMS_VALID) != 0;
   const float* cn2 = w.cn2;
   if (!norms_valid) {
-    if (use_small_assign(b, dimp)) {
+    if (use_small_assign(b, dim)) {
       cn2 = nullptr;  // the fused kernel computes them from its LDS tiles
     } else {
       k_row_norms<<<blocks_for(k), 256, 0, s>>>(k, dim, C_old, w.cn2, stop, step_i);

@@ -16,6 +16,7 @@
 #include "gdd_common.hpp"
 
 namespace gdd {
+GDD_STAMP_TABLE(kpp)
 namespace {
 
 constexpr int kMaxTrials = 16;
@@ -26,7 +27,6 @@ struct KppState {
   float pot;   // current potential (fp32, as sklearn keeps it)
   int best;    // trial chosen in the previous round; -1 = the distances to the first centre
   int64_t cand[kMaxTrials];
-  double cnorm[kMaxTrials];
 };
 
 // OpenBLAS 0.3.28/29 SkylakeX sdot (kernel/x86_64/sdot.c + sdot_microk_skylakex-2.c), emulated by
@@ -34,31 +34,25 @@ struct KppState {
 // runs accumulator u, lane l); they fold to 4 x 8 AVX2 accumulators for the 32-wide remainder;
 // lanes then combine ((a0+a1)+a2)+a3, 8 -> 4 by halves, and (h0+h1)+(h2+h3); the scalar tail is
 // added in double. All 64 lanes call it; lane 0 returns the value.
-__device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restrict__ y, int64_t n,
-                               float* scratch /* 64 floats of LDS owned by this wave */) {
+// The 64 lane chains of the 64-wide loop are independent: per round, k_kpp_dist runs them in the
+// blocks that produce the distances (no block ever re-reads a whole distance row), and the tail
+// only combines 64 accumulators per trial (sdot_skx_finish).
+// the combination after the 64-wide loop: `a` = this lane's accumulator of that loop; (rx, ry) =
+// element n64 + lane of x and y (zero past n). Lane 0 returns the dot.
+__device__ float sdot_skx_finish(float a, float rx, float ry, int64_t n, float* scratch) {
   const int lane = threadIdx.x & 63;
   const int64_t n1 = n & ~31ll;
   const int64_t n64 = n1 & ~63ll;
-  // y == nullptr: unit sample weights (fma(x, 1, a) == a + x, one rounding either way)
-  float a = 0.f;
-  int64_t i = lane;
-  for (; i + 64 * 7 < n64; i += 64 * 8) {  // eight independent loads ahead of the ordered fmas
-    float xv[8], yv[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      xv[u] = x[i + 64 * u];
-      yv[u] = y ? y[i + 64 * u] : 1.0f;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) a = __builtin_fmaf(xv[u], yv[u], a);
-  }
-  for (; i < n64; i += 64) a = __builtin_fmaf(x[i], y ? y[i] : 1.0f, a);
   scratch[lane] = a;
+  scratch[64 + lane] = rx;
+  scratch[128 + lane] = ry;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   float r = 0.f;
   if (lane == 0) {
+    const float* Rx = scratch + 64;
+    const float* Ry = scratch + 128;
     float acc[4][8];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -68,8 +62,7 @@ __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restr
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int l = 0; l < 8; ++l)
-          acc[u][l] = __builtin_fmaf(x[n64 + u * 8 + l], y ? y[n64 + u * 8 + l] : 1.0f, acc[u][l]);
+        for (int l = 0; l < 8; ++l) acc[u][l] = __builtin_fmaf(Rx[u * 8 + l], Ry[u * 8 + l], acc[u][l]);
     }
     float s[8];
 #pragma unroll
@@ -79,12 +72,37 @@ __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restr
     for (int l = 0; l < 4; ++l) h[l] = s[l] + s[l + 4];
     double dot = n1 ? (double)((h[0] + h[1]) + (h[2] + h[3])) : 0.0;
     for (int64_t t = n1; t < n; ++t) {
-      const float p = (y ? y[t] : 1.0f) * x[t];
+      const float p = Ry[t - n64] * Rx[t - n64];
       dot = dot + (double)p;
     }
     r = (float)dot;
   }
   return r;
+}
+
+// the whole dot by one wave (used once, for the first centre's potential)
+__device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restrict__ y, int64_t n,
+                               float* scratch /* 192 floats of LDS owned by this wave */) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n64 = n & ~63ll;
+  const int64_t ri = n64 + lane;
+  const float rx = ri < n ? x[ri] : 0.f;
+  const float ry = ri < n ? (y ? y[ri] : 1.0f) : 0.f;
+  // y == nullptr: unit sample weights (fma(x, 1, a) == a + x, one rounding either way)
+  float a = 0.f;
+  for (int64_t i0 = 0; i0 < n64; i0 += 64 * 32) {
+    float xv[32], yv[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int64_t i = i0 + 64 * u + lane;
+      xv[u] = i < n64 ? x[i] : 0.f;
+      yv[u] = (i < n64 && y) ? y[i] : 1.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 32; ++u)
+      if (i0 + 64 * u < n64) a = __builtin_fmaf(xv[u], yv[u], a);
+  }
+  return sdot_skx_finish(a, rx, ry, n, scratch);
 }
 
 __device__ __forceinline__ float np_minimum(float a, float b) {
@@ -111,38 +129,99 @@ __global__ void k_kpp_init(int64_t n, int dim, const float* __restrict__ X, int6
   closest[i] = f < 0.f ? 0.f : f;
 }
 
-// dist[t][i] for a 256-point tile; the candidate row is staged in LDS as fp64
+// Round c: distances of every point to trial t's candidate (fp64 upcast, pairwise.py:582-650),
+// np.minimum with the current closest distances, and the 64-wide-loop chains of the potential's
+// sdot. Grid (G, T): block (g, t) owns the sdot lanes l in [g*L, (g+1)*L), L = 64/G, i.e. the
+// points i = l + 64 j, j < J = n64/64; it writes their distances to dist[t][i] (the tail's cumsum
+// reads one row), runs its lanes' ordered fp32 chains over them and leaves acc[t][l]. Block 0 also
+// writes the remainder points n64 <= i < n. The candidate row is staged in LDS as fp64.
+template <bool kChainLds>
 __global__ __launch_bounds__(256) void k_kpp_dist(int64_t n, int dim, const float* __restrict__ X,
+                                                  const float* __restrict__ w,
                                                   const double* __restrict__ xsq,
                                                   const float* __restrict__ closest0,
                                                   const float* __restrict__ dist_prev,
                                                   const KppState* __restrict__ st,
-                                                  float* __restrict__ dist) {
-  extern __shared__ double s_c[];  // dim
-  const int t = blockIdx.y;
+                                                  float* __restrict__ dist, float* __restrict__ acc,
+                                                  int L) {
+  GDD_STAMP_WHEN(g_stamps_kpp, (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0), 20);
+  extern __shared__ double s_c[];  // dim doubles, then the block's chain distances (fp32)
+  const int t = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
+  const int64_t J = n >> 6, n64 = J << 6;
+  const int64_t nloc = (int64_t)L * J;
+  const int64_t ntot = nloc + (g == 0 ? n - n64 : 0);
+  const int best = st->best;
   const int64_t ct = st->cand[t];
-  for (int j = threadIdx.x; j < dim; j += blockDim.x) s_c[j] = (double)X[ct * dim + j];
+  const double cn = xsq[ct];
+  const float* closest = best < 0 ? closest0 : dist_prev + (int64_t)best * n;
+  for (int j = tid; j < dim; j += blockDim.x) s_c[j] = (double)X[ct * dim + j];
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float* closest = st->best < 0 ? closest0 : dist_prev + (int64_t)st->best * n;
-  const float* xi = X + i * dim;
-  double dot = 0.0;
-  for (int j = 0; j < dim; ++j) dot = __builtin_fma(s_c[j], (double)xi[j], dot);
-  const double d = ((-2.0 * dot) + st->cnorm[t]) + xsq[i];
-  float f = (float)d;
-  f = f < 0.f ? 0.f : f;
-  dist[(int64_t)t * n + i] = np_minimum(closest[i], f);
+  GDD_STAMP_WHEN(g_stamps_kpp, (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0), 21);
+  float* sd = reinterpret_cast<float*>(s_c + dim);
+  float* drow = dist + (int64_t)t * n;
+  for (int64_t q = tid; q < ntot; q += blockDim.x) {
+    int64_t i;
+    if (q < nloc) {
+      const int64_t j = q / L;
+      i = (int64_t)g * L + (q - j * L) + 64 * j;
+    } else {
+      i = n64 + (q - nloc);
+    }
+    const float* xi = X + i * dim;
+    const double xs = xsq[i];
+    const float cl = closest[i];
+    double dot = 0.0;
+    int j = 0;
+    for (; j + 8 <= dim; j += 8) {  // eight loads in flight ahead of the ordered fmas
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = xi[j + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) dot = __builtin_fma(s_c[j + u], (double)v[u], dot);
+    }
+    for (; j < dim; ++j) dot = __builtin_fma(s_c[j], (double)xi[j], dot);
+    const double d = ((-2.0 * dot) + cn) + xs;
+    float f = (float)d;
+    f = f < 0.f ? 0.f : f;
+    f = np_minimum(cl, f);
+    drow[i] = f;
+    if (kChainLds && q < nloc) sd[q] = f;
+  }
+  __syncthreads();  // also orders this block's global writes for the chain reads below
+  GDD_STAMP_WHEN(g_stamps_kpp, (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0), 22);
+  if (tid < L) {
+    const int l = g * L + tid;
+    float a = 0.f;
+    int64_t j = 0;
+    for (; j + 8 <= J; j += 8) {
+      float xv[8], yv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t i = l + 64 * (j + u);
+        xv[u] = kChainLds ? sd[(j + u) * L + tid] : drow[i];
+        yv[u] = w ? w[i] : 1.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a = __builtin_fmaf(xv[u], yv[u], a);
+    }
+    for (; j < J; ++j) {
+      const int64_t i = l + 64 * j;
+      a = __builtin_fmaf(kChainLds ? sd[j * L + tid] : drow[i], w ? w[i] : 1.0f, a);
+    }
+    acc[t * 64 + l] = a;
+  }
+  GDD_STAMP_WHEN(g_stamps_kpp, (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0), 23);
 }
 
 // end of round c (c = 0: the first centre) and the candidate draw of round c+1
 __global__ __launch_bounds__(kTailThreads) void k_kpp_tail(
     int64_t n, int dim, const float* __restrict__ X, const float* __restrict__ w,
-    const float* __restrict__ closest0, const float* __restrict__ dist, int T, int c, int k,
+    const float* __restrict__ closest0, const float* __restrict__ dist,
+    const float* __restrict__ acc, int T, int c, int k,
     int64_t first_id, const double* __restrict__ uniforms, const double* __restrict__ xsq,
     double* __restrict__ cum, float* __restrict__ centers, int64_t* __restrict__ indices,
     KppState* __restrict__ st) {
-  __shared__ float scratch[kMaxTrials * 64];
+  __shared__ float scratch[kMaxTrials * 192];
   __shared__ float s_pot[kMaxTrials];
   __shared__ double s_part[kTailThreads / 64];
   __shared__ double s_cum[kTailLdsCum];
@@ -150,6 +229,9 @@ __global__ __launch_bounds__(kTailThreads) void k_kpp_tail(
   __shared__ int64_t s_src;
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
+  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 0 + 10 * (c & 1));
+  // this round's draw for the next candidates, requested up front
+  const double u_mine = (tid < T && c + 1 < k) ? uniforms[(int64_t)c * T + tid] : 0.0;
   // ---- finish round c ----
   if (c == 0) {
     if (wave == 0) {
@@ -166,10 +248,15 @@ __global__ __launch_bounds__(kTailThreads) void k_kpp_tail(
     }
   } else {
     if (wave < T) {
-      const float p = sdot_skx_wave(dist + (int64_t)wave * n, w, n, scratch + wave * 64);
-      if ((tid & 63) == 0) s_pot[wave] = p;
+      const int lane = tid & 63;
+      const int64_t ri = (n & ~63ll) + lane;
+      const float rx = ri < n ? dist[(int64_t)wave * n + ri] : 0.f;
+      const float ry = ri < n ? (w ? w[ri] : 1.0f) : 0.f;
+      const float p = sdot_skx_finish(acc[wave * 64 + lane], rx, ry, n, scratch + wave * 192);
+      if (lane == 0) s_pot[wave] = p;
     }
     __syncthreads();
+    GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 1 + 10 * (c & 1));
     if (tid == 0) {
       int b = 0;  // np.argmin: first minimum; a NaN is returned as soon as it is met
       for (int t = 1; t < T; ++t) {
@@ -184,14 +271,29 @@ __global__ __launch_bounds__(kTailThreads) void k_kpp_tail(
     }
   }
   __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 2 + 10 * (c & 1));
   for (int j = tid; j < dim; j += kTailThreads) centers[(int64_t)c * dim + j] = X[s_src * dim + j];
   if (c + 1 >= k) return;
   // ---- candidates of round c+1 ----
   const float* closest = s_best < 0 ? closest0 : dist + (int64_t)s_best * n;
   const int64_t chunk = (n + kTailThreads - 1) / kTailThreads;
   const int64_t lo = min<int64_t>(n, tid * chunk), hi = min<int64_t>(n, lo + chunk);
+  // fp32 products w_i * closest_i of this thread's chunk (kept in registers when it is short)
+  constexpr int kReg = 8;
+  float pr[kReg];
+#pragma unroll
+  for (int u = 0; u < kReg; ++u) {
+    const int64_t i = lo + u;
+    pr[u] = (chunk <= kReg && i < hi) ? (w ? w[i] : 1.0f) * closest[i] : 0.f;
+  }
   double run = 0.0;
-  for (int64_t i = lo; i < hi; ++i) run = run + (double)((w ? w[i] : 1.0f) * closest[i]);
+  if (chunk <= kReg) {
+#pragma unroll
+    for (int u = 0; u < kReg; ++u)
+      if (lo + u < hi) run = run + (double)pr[u];
+  } else {
+    for (int64_t i = lo; i < hi; ++i) run = run + (double)((w ? w[i] : 1.0f) * closest[i]);
+  }
   // exclusive scan of the per-thread chunk totals: wave shuffles, then the 16 wave totals
   const int lane = tid & 63;
   double incl = run;
@@ -211,17 +313,28 @@ __global__ __launch_bounds__(kTailThreads) void k_kpp_tail(
     }
   }
   __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 4 + 10 * (c & 1));
   double base = s_part[wave] + (incl - run);
   // small n: the cumulative potential stays in LDS for the binary searches
   double* cs = (n <= kTailLdsCum) ? s_cum : cum;
-  for (int64_t i = lo; i < hi; ++i) {
-    base = base + (double)((w ? w[i] : 1.0f) * closest[i]);
-    cs[i] = base;
+  if (chunk <= kReg) {
+#pragma unroll
+    for (int u = 0; u < kReg; ++u)
+      if (lo + u < hi) {
+        base = base + (double)pr[u];
+        cs[lo + u] = base;
+      }
+  } else {
+    for (int64_t i = lo; i < hi; ++i) {
+      base = base + (double)((w ? w[i] : 1.0f) * closest[i]);
+      cs[i] = base;
+    }
   }
   __threadfence_block();
   __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 5 + 10 * (c & 1));
   if (tid < T) {
-    const double r = uniforms[(int64_t)c * T + tid] * (double)st->pot;
+    const double r = u_mine * (double)s_pot[s_best < 0 ? 0 : s_best];
     int64_t a = 0, b = n;  // first index with cum[idx] >= r  (np.searchsorted side='left')
     while (a < b) {
       const int64_t m = (a + b) >> 1;
@@ -232,8 +345,8 @@ __global__ __launch_bounds__(kTailThreads) void k_kpp_tail(
     }
     if (a > n - 1) a = n - 1;
     st->cand[tid] = a;
-    st->cnorm[tid] = xsq[a];
   }
+  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 6 + 10 * (c & 1));
 }
 
 __global__ void k_ones(int64_t n, float* p) {
@@ -253,7 +366,7 @@ extern "C" size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int n_trials) {
   b += align256(sizeof(float) * n);                                         // closest0
   b += 2 * align256(sizeof(float) * n * (size_t)std::max(n_trials, 1));     // dist ping-pong
   b += align256(sizeof(double) * n);                                        // cum
-  b += align256(sizeof(float) * n);                                         // ones (w == NULL)
+  b += align256(sizeof(float) * 64 * (size_t)std::max(n_trials, 1));       // lane accumulators
   return b + 2048;
 }
 
@@ -275,26 +388,39 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   float* closest0 = cv.take<float>(n);
   float* dist[2] = {cv.take<float>(n * (size_t)n_trials), cv.take<float>(n * (size_t)n_trials)};
   double* cum = cv.take<double>(n);
-  float* ones = cv.take<float>(n);
+  float* acc = cv.take<float>(64 * (size_t)n_trials);
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans++: workspace too small");
   const unsigned nb = (unsigned)((n + 255) / 256);
-  (void)ones;  // w == nullptr: unit sample weights, handled in the kernels
+  // w == nullptr: unit sample weights, handled in the kernels
   k_kpp_init<<<nb, 256, 0, s>>>(n, dim, X, first_id, xsq, closest0);
   GDD_LAUNCHED();
-  k_kpp_tail<<<1, kTailThreads, 0, s>>>(n, dim, X, w, closest0, dist[1], n_trials, 0, k, first_id,
-                                        uniforms, xsq, cum, centers, indices, st);
+  k_kpp_tail<<<1, kTailThreads, 0, s>>>(n, dim, X, w, closest0, dist[1], acc, n_trials, 0, k,
+                                        first_id, uniforms, xsq, cum, centers, indices, st);
   GDD_LAUNCHED();
-  const size_t lds = sizeof(double) * (size_t)dim;
+  // lanes per distance block: about one point per thread (L * J ~ 256), L a power of two
+  const int64_t J = n >> 6;
+  int L = 64;
+  while (L > 1 && (int64_t)L * J > 256) L >>= 1;
+  const int G = 64 / L;
+  // the block's chain distances stay in LDS when they fit next to the candidate row
+  const size_t lds_chain = sizeof(double) * (size_t)dim + sizeof(float) * (size_t)L * J;
+  const int chain_in_lds = lds_chain <= 65536 ? 1 : 0;
+  const size_t lds = chain_in_lds ? lds_chain : sizeof(double) * (size_t)dim;
   if (lds > 65536)
-    GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dist, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds));
+    GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dist<false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   for (int c = 1; c < k; ++c) {
     const float* prev = dist[(c - 1) & 1];
     float* cur = dist[c & 1];
-    k_kpp_dist<<<dim3(nb, n_trials), 256, lds, s>>>(n, dim, X, xsq, closest0, prev, st, cur);
+    if (chain_in_lds)
+      k_kpp_dist<true><<<dim3(G, n_trials), 256, lds, s>>>(n, dim, X, w, xsq, closest0, prev, st,
+                                                           cur, acc, L);
+    else
+      k_kpp_dist<false><<<dim3(G, n_trials), 256, lds, s>>>(n, dim, X, w, xsq, closest0, prev, st,
+                                                            cur, acc, L);
     GDD_LAUNCHED();
-    k_kpp_tail<<<1, kTailThreads, 0, s>>>(n, dim, X, w, closest0, cur, n_trials, c, k, first_id,
-                                          uniforms, xsq, cum, centers, indices, st);
+    k_kpp_tail<<<1, kTailThreads, 0, s>>>(n, dim, X, w, closest0, cur, acc, n_trials, c, k,
+                                          first_id, uniforms, xsq, cum, centers, indices, st);
     GDD_LAUNCHED();
   }
   return GDD_OK;

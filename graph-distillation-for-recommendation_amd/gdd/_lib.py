@@ -16,7 +16,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libgdd.so")
+# GDD_LIB_PATH selects a diagnostic build of the same library (e.g. lib/libgdd_stamps.so)
+LIB_PATH = os.environ.get("GDD_LIB_PATH") or os.path.join(_HERE, "lib", "libgdd.so")
 
 _c_i64 = ctypes.c_int64
 _c_int = ctypes.c_int

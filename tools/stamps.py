@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""In-kernel phase stamps of the MiniBatchKMeans step and k-means++ kernels (diagnostic build).
+
+Build: make -C graph-distillation-for-recommendation_amd/csrc STAMPS=1
+Run:   python tools/stamps.py   (uses lib/libgdd_stamps.so; stamps are s_memrealtime, 10 ns ticks)
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["GDD_LIB_PATH"] = os.path.join(ROOT, "graph-distillation-for-recommendation_amd", "gdd", "lib",
+                                          "libgdd_stamps.so")
+sys.path.insert(0, os.path.join(ROOT, "graph-distillation-for-recommendation_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import gdd  # noqa: E402
+from gdd import _lib, synth  # noqa: E402
+
+
+def read(lib, name):
+    buf = (ctypes.c_ulonglong * 256)()
+    fn = getattr(lib, "gdd_dbg_stamps_" + name)
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p]
+    assert fn(ctypes.addressof(buf)) == 0
+    return np.array(buf[:], dtype=np.int64)
+
+
+def show(title, st, slots, base):
+    t0 = st[base]
+    parts = [f"{s}:{(st[s] - t0) * 10 / 1000:.2f}" for s in slots if st[s] >= t0 and st[s] - t0 < 10 ** 7]
+    print(f"{title:22s} (us from slot {base}) " + " ".join(parts), flush=True)
+
+
+def main():
+    lib = _lib.device_lib()
+    cfg = synth.CONFIGS["arxiv"]
+    X = torch.from_numpy(synth.blobs(cfg.n, cfg.n_classes, cfg.k, seed=1)).cuda()
+    for rep in range(2):
+        torch.cuda.synchronize()
+        km = gdd.MiniBatchKMeans(n_clusters=cfg.k, random_state=cfg.seed, batch_size=cfg.batch).fit(X)
+        torch.cuda.synchronize()
+        a = read(lib, "kmeans")
+        p = read(lib, "kpp")
+        print(f"rep {rep}: steps={km.n_steps_}")
+        show("assign_small", a, [0, 2, 3, 5, 13, 14, 15, 16], 0)
+        show("update block0", a, list(range(20, 26)), 20)
+        show("update tail", a, list(range(30, 33)), 30)
+        bank = 10 * ((cfg.k - 2) & 1)  # round k-2 is the last complete tail
+        show("kpp_tail", p, [bank + i for i in range(7)], bank)
+        show("kpp_dist", p, list(range(20, 24)), 20)
+
+
+if __name__ == "__main__":
+    main()
