@@ -73,6 +73,22 @@ int sort_pairs_i32(const int32_t* keys_in, int32_t* keys_out, const int32_t* val
                    hipStream_t s);
 
 // ---------------------------------------------------------------------------------------------
+// internal entry points of the device-resident MiniBatchKMeans loop (gdd_kmeans.hip, used by
+// gdd_fit.hip); DevMT / RngNext are defined in gdd_devrng.hpp
+// ---------------------------------------------------------------------------------------------
+struct DevMT;
+struct RngNext;
+int minibatch_step_dev(int64_t b, int dim, const float* X, const int64_t* rows, int k,
+                       const float* C_old, float* C_new, float* weight_sums, int32_t* labels,
+                       int step_i, int64_t n_samples, int max_no_improvement, int flags,
+                       void* state, void* ws, size_t ws_bytes, const RngNext& rn, hipStream_t s);
+int mb_rng_launch(const DevMT* in, DevMT* out, int64_t n, int64_t bs, int64_t* rows, hipStream_t s);
+int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const float* X,
+                       const int64_t* rows, float* C_new, float* counts, void* step_ws,
+                       size_t step_ws_bytes, const DevMT* mt_in, DevMT* mt_mid, const RngNext& rn,
+                       void* state, hipStream_t s);
+
+// ---------------------------------------------------------------------------------------------
 // numerics shared by kernels and documented in DESIGN.md
 // ---------------------------------------------------------------------------------------------
 // correctly rounded fp64 x^-1/2 (numpy np.power(x, -0.5) agrees with this on ~95% of inputs, with

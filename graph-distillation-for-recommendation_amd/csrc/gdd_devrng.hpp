@@ -1,0 +1,255 @@
+// gdd_devrng.hpp — numpy legacy RandomState (MT19937) draws on the device, one workgroup at a time.
+//
+// The same draws as gdd_rng.hpp (host), restated for a cooperating workgroup so that the
+// MiniBatchKMeans loop can draw its batch indices and reassignment permutations without a host
+// round trip:
+//   twist      mt19937_gen (numpy/random/src/mt19937/mt19937.c) in four dependency phases:
+//              i < 227 reads only old words; 227 <= i < 454 reads new[i-227] from phase 1;
+//              454 <= i < 623 reads new[i-227] from phase 2; i = 623 reads new[0] and new[396]
+//   randint    RandomState.randint(low, high, size) int64, masked rejection on 32-bit draws
+//              (_bounded_integers.pyx _rand_int64 -> random_bounded_uint64_fill): each tempered
+//              word is accepted iff (w & mask) <= rng; a workgroup prefix count over the words of
+//              the current key block places the accepted values in draw order
+//   shuffle    RandomState.permutation(n) (legacy _shuffle_raw + random_interval): one lane walks
+//              the tempered words to get j_i for i = n-1..1; the first m entries of the permuted
+//              arange are then traced backwards through the swaps, one lane per entry
+// Requirements: blockDim.x is a multiple of 64 and >= 256; every thread of the block calls in.
+#pragma once
+
+#include <cstdint>
+
+namespace gdd {
+
+struct DevMT {  // key block + position, as gdd_mt_state without the gaussian cache
+  uint32_t key[624];
+  int32_t pos;
+  int32_t pad;
+};
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
+  const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+  return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// regenerate the 624-word key block in LDS (mt19937_gen)
+__device__ inline void mt_twist_block(uint32_t* key) {
+  const int t = threadIdx.x;
+  uint32_t v = 0;
+  if (t < 227) v = mt_mix(key[t], key[t + 1], key[t + 397]);
+  __syncthreads();
+  if (t < 227) key[t] = v;
+  __syncthreads();
+  if (t < 227) v = mt_mix(key[227 + t], key[228 + t], key[t]);
+  __syncthreads();
+  if (t < 227) key[227 + t] = v;
+  __syncthreads();
+  if (t < 169) v = mt_mix(key[454 + t], key[455 + t], key[227 + t]);
+  __syncthreads();
+  if (t < 169) key[454 + t] = v;
+  __syncthreads();
+  if (t == 0) key[623] = mt_mix(key[623], key[0], key[396]);
+  __syncthreads();
+}
+
+// exclusive prefix count of `flag` over the block; returns the prefix, *total = block count.
+// scratch: >= blockDim.x/64 + 1 ints of LDS.
+__device__ inline int block_prefix_count(bool flag, int* scratch, int* total) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = blockDim.x >> 6;
+  const unsigned long long m = __ballot(flag);
+  const int before = __popcll(m & ((1ull << lane) - 1ull));
+  if (lane == 0) scratch[wave] = __popcll(m);
+  __syncthreads();
+  int base = 0, tot = 0;
+  for (int w = 0; w < nw; ++w) {
+    const int c = scratch[w];
+    base += w < wave ? c : 0;
+    tot += c;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + before;
+}
+
+__device__ __forceinline__ uint32_t mask32(uint32_t x) {
+  x |= x >> 1;
+  x |= x >> 2;
+  x |= x >> 4;
+  x |= x >> 8;
+  x |= x >> 16;
+  return x;
+}
+
+// LDS scratch of the block draws: the key block, the position, the prefix-count scratch
+struct MTScratch {
+  uint32_t key[624];
+  int pos;
+  int last;
+  int cnt[20];
+};
+
+__device__ inline void mt_load(const DevMT* __restrict__ src, MTScratch* s) {
+  for (int i = threadIdx.x; i < 624; i += blockDim.x) s->key[i] = src->key[i];
+  if (threadIdx.x == 0) s->pos = src->pos;
+  __syncthreads();
+}
+
+__device__ inline void mt_store(const MTScratch* s, DevMT* __restrict__ dst) {
+  for (int i = threadIdx.x; i < 624; i += blockDim.x) dst->key[i] = s->key[i];
+  if (threadIdx.x == 0) {
+    dst->pos = s->pos;
+    dst->pad = 0;
+  }
+}
+
+// out[0..count) = randint(low, high, count) (high - low - 1 < 2^32)
+__device__ inline void mt_randint_block(MTScratch* s, int64_t low, int64_t high, int64_t count,
+                                 int64_t* __restrict__ out) {
+  const uint32_t rng = (uint32_t)(high - 1 - low);
+  if (rng == 0) {  // no draws
+    for (int64_t i = threadIdx.x; i < count; i += blockDim.x) out[i] = low;
+    return;
+  }
+  const uint32_t mask = mask32(rng);
+  const int t = threadIdx.x;
+  int64_t produced = 0;
+  while (produced < count) {
+    if (s->pos >= 624) {
+      mt_twist_block(s->key);
+      if (t == 0) s->pos = 0;
+      __syncthreads();
+    }
+    const int pos = s->pos;
+    const int avail = 624 - pos;
+    uint32_t v = 0;
+    bool ok = false;
+    if (t < avail) {
+      v = mt_temper(s->key[pos + t]) & mask;
+      ok = v <= rng;
+    }
+    int total;
+    const int e = block_prefix_count(ok, s->cnt, &total);
+    const int64_t need = count - produced;
+    if (ok && e < need) out[produced + e] = low + (int64_t)v;
+    if (total >= need) {
+      if (ok && e == need - 1) s->last = t;
+      __syncthreads();
+      if (t == 0) s->pos = pos + s->last + 1;
+      produced = count;
+    } else {
+      if (t == 0) s->pos = 624;
+      produced += total;
+    }
+    __syncthreads();
+  }
+}
+
+// perm[0..m) = RandomState.permutation(n)[:m]. J: n ints of 16-byte aligned LDS (swap partners).
+__device__ inline void mt_permutation_prefix_block(MTScratch* s, int64_t n, int m, int* J,
+                                            int64_t* __restrict__ perm) {
+  const int t = threadIdx.x;
+  // wave 0 walks the words 64 at a time; the block regenerates the key block when it runs dry.
+  // In a window of 64 words with i - 64 >= 1 and one mask for all of [i-64, i], word u is accepted
+  // iff v_u <= i - (accepted before u): v_u <= i - 63 is surely accepted, v_u > i surely rejected,
+  // and the few words in between are settled in order. Other windows go word by word on lane 0.
+  if (t == 0) s->last = (int)n - 1;  // the next i to draw for
+  __syncthreads();
+  const int lane = t & 63;
+  while (true) {
+    if (s->last < 1) break;
+    if (s->pos >= 624) {
+      mt_twist_block(s->key);
+      if (t == 0) s->pos = 0;
+      __syncthreads();
+    }
+    if (t < 64) {
+      int i = s->last, pos = s->pos;
+      while (i >= 1 && pos < 624) {
+        const int navail = min(64, 624 - pos);
+        const uint32_t mk = mask32((uint32_t)i);
+        const bool fast = navail == 64 && i - 64 >= 1 && mask32((uint32_t)(i - 64)) == mk;
+        if (fast) {
+          const uint32_t v = mt_temper(s->key[pos + lane]) & mk;
+          const unsigned long long sure = __ballot(v + 63u <= (uint32_t)i);
+          unsigned long long maybe = __ballot(v + 63u > (uint32_t)i && v <= (uint32_t)i);
+          unsigned long long acc = sure;
+          while (maybe) {
+            const int u = __ffsll((long long)maybe) - 1;
+            maybe &= maybe - 1;
+            const int c = __popcll(acc & ((1ull << u) - 1ull));
+            const uint32_t vu = (uint32_t)__shfl((int)v, u);
+            if (vu <= (uint32_t)(i - c)) acc |= 1ull << u;
+          }
+          if ((acc >> lane) & 1ull) J[i - __popcll(acc & ((1ull << lane) - 1ull))] = (int)v;
+          i -= __popcll(acc);
+          pos += 64;
+        } else {
+          int i0 = i, p0 = pos;
+          if (lane == 0) {
+            uint32_t m0 = mk;
+            const int end = pos + navail;
+            while (i0 >= 1 && p0 < end) {
+              const uint32_t v = mt_temper(s->key[p0++]) & m0;
+              if (v <= (uint32_t)i0) {
+                J[i0] = (int)v;
+                --i0;
+                m0 = mask32((uint32_t)(i0 > 0 ? i0 : 1));
+              }
+            }
+          }
+          i = __shfl(i0, 0);
+          pos = __shfl(p0, 0);
+        }
+      }
+      if (t == 0) {
+        s->last = i;
+        s->pos = pos;
+      }
+    }
+    __syncthreads();
+  }
+  // trace entry p of the permuted arange back through the swaps (applied for i = n-1 .. 1);
+  // J is read eight entries per step (two 16-byte LDS reads, one broadcast to all lanes)
+  if (t == 0) J[0] = 0;  // swap 0 <-> 0: the identity, so i = 0 can ride along in the batches
+  __syncthreads();
+  const int nn = (int)n;
+  for (int p = t; p < m; p += blockDim.x) {
+    int q = p;
+    int i0 = 0;
+    for (; i0 + 8 <= nn; i0 += 8) {
+      const int4 a = *reinterpret_cast<const int4*>(J + i0);
+      const int4 b = *reinterpret_cast<const int4*>(J + i0 + 4);
+      const int jj[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u;
+        q = (q == i) ? jj[u] : ((q == jj[u]) ? i : q);
+      }
+    }
+    for (int i = i0; i < nn; ++i) {
+      const int j = J[i];
+      q = (q == i) ? j : ((q == j) ? i : q);
+    }
+    perm[p] = q;
+  }
+  __syncthreads();
+}
+
+// "draw the next batch in this launch": an extra workgroup of the assignment kernel runs
+// randint(0, n, bs) from `in` into rows / `out` (rows == nullptr: nothing to draw)
+struct RngNext {
+  const DevMT* in;
+  DevMT* out;
+  int64_t* rows;
+  int64_t n;
+  int64_t bs;
+};
+
+}  // namespace gdd

@@ -8,9 +8,12 @@
 // are sklearn's (one OpenMP thread).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "gdd_common.hpp"
+#include "gdd_devrng.hpp"
 #include "gdd_rng.hpp"
 
 namespace gdd {
@@ -66,6 +69,7 @@ struct FitWs {
   float* scalar;
   void* assign_ws;
   size_t assign_bytes;
+  DevMT* mtb;  // 3 device MT states: slot s % 3 holds the state after step s's draws
 };
 
 size_t fit_ws(void* base, size_t cap, int64_t n, int dim, int k, int64_t bs, int64_t isz, int T,
@@ -93,11 +97,100 @@ size_t fit_ws(void* base, size_t cap, int64_t n, int dim, int k, int64_t bs, int
   f.scalar = cv.take<float>(4);
   f.assign_bytes = gdd_kmeans_assign_ws_bytes(std::max(n, isz));
   f.assign_ws = cv.take<char>(f.assign_bytes);
+  f.mtb = cv.take<DevMT>(3);
   if (w) *w = f;
   return cv.off + 1024;
 }
 
 int local_trials(int k) { return 2 + (int)std::log((double)k); }
+
+// The step loop with every draw and decision on the device (see the dev_loop comment in the fit).
+// Per step s: the assignment launch (plus, unless s reassigns, a workgroup drawing batch s+1), the
+// update launch (with the batch inertia and the convergence test), and at scheduled reassignment
+// steps the reassignment launch (which then draws batch s+1). Chunks of kDevChunk steps are
+// enqueued back to back; the host reads the stop word of chunk c while chunk c+1 runs.
+constexpr int kDevChunk = 16;
+
+int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n_steps,
+                int max_no_improvement, float reassignment_ratio, MTState* rng, const FitWs& w,
+                int32_t* h_flag /* pinned, >= 4 ints */, int64_t* stop_step, hipStream_t s) {
+  // the host RNG state after the initialisation draws becomes device slot 2 (= step -1)
+  static_assert(sizeof(DevMT) == 624 * 4 + 8, "DevMT layout");
+  DevMT* h_mt = reinterpret_cast<DevMT*>(h_flag + 64);  // pinned scratch after the flags
+  std::memcpy(h_mt->key, rng->key, sizeof(h_mt->key));
+  h_mt->pos = rng->pos;
+  h_mt->pad = 0;
+  GDD_HIP(hipMemcpyAsync(w.mtb + 2, h_mt, sizeof(DevMT), hipMemcpyHostToDevice, s));
+  int rc = mb_rng_launch(w.mtb + 2, w.mtb + 0, n, bs, w.rows_d, s);
+  if (rc) return rc;
+  const bool reassign = reassignment_ratio > 0.f;
+  hipEvent_t ev[2];
+  GDD_HIP(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+  GDD_HIP(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+  struct EvGuard {
+    hipEvent_t* e;
+    ~EvGuard() {
+      (void)hipEventDestroy(e[0]);
+      (void)hipEventDestroy(e[1]);
+    }
+  } guard{ev};
+  int32_t* stop_word = reinterpret_cast<int32_t*>(static_cast<char*>(w.state) + 16);
+  int64_t n_since = 0;
+  int64_t i = 0;
+  int slot = 0;
+  bool pending = false;
+  *stop_step = -1;
+  while (i < n_steps) {
+    const int64_t m = std::min<int64_t>(kDevChunk, n_steps - i);
+    for (int64_t j = 0; j < m; ++j) {
+      const int64_t st = i + j;
+      n_since += bs;
+      const bool rr = st == 0 || n_since >= 10 * (int64_t)k;  // _random_reassign (:2029-2043)
+      if (rr) n_since = 0;
+      const bool do_rr = rr && reassign;
+      const bool has_next = st + 1 < n_steps;
+      int64_t* rows_cur = w.rows_d + (st & 1) * bs;
+      int64_t* rows_nxt = w.rows_d + ((st + 1) & 1) * bs;
+      DevMT* mt_cur = w.mtb + st % 3;
+      DevMT* mt_nxt = w.mtb + (st + 1) % 3;
+      const RngNext none{nullptr, nullptr, nullptr, 0, 0};
+      const RngNext next{mt_cur, mt_nxt, rows_nxt, n, bs};
+      float* c_old = w.C[st % 2];
+      float* c_new = w.C[(st + 1) % 2];
+      const int flags = GDD_STEP_CONVERGE | (st > 0 ? GDD_STEP_NORMS_VALID : 0);
+      rc = minibatch_step_dev(bs, dim, X, rows_cur, k, c_old, c_new, w.counts, w.labels_b, (int)st, n,
+                              max_no_improvement, flags, w.state, w.step_ws, w.step_bytes,
+                              (!do_rr && has_next) ? next : none, s);
+      if (rc) return rc;
+      if (do_rr) {
+        rc = mb_reassign_launch((int)st, bs, dim, k, reassignment_ratio, X, rows_cur, c_new, w.counts,
+                                w.step_ws, w.step_bytes, mt_cur, mt_cur, has_next ? next : none,
+                                w.state, s);
+        if (rc) return rc;
+      }
+    }
+    i += m;
+    // this chunk's stop word, read back while the next chunk runs
+    GDD_HIP(hipMemcpyAsync(h_flag + slot, stop_word, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    GDD_HIP(hipEventRecord(ev[slot], s));
+    if (pending) {
+      GDD_HIP(hipEventSynchronize(ev[slot ^ 1]));
+      if (h_flag[slot ^ 1]) break;  // the later kernels already enqueued are no-ops
+    }
+    pending = true;
+    slot ^= 1;
+  }
+  GDD_HIP(hipMemcpyAsync(h_flag + 2, stop_word, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  GDD_HIP(hipStreamSynchronize(s));
+  if (h_flag[2]) *stop_step = h_flag[2] - 1;
+  const int64_t last = *stop_step >= 0 ? *stop_step : n_steps - 1;
+  // the caller's RandomState ends where sklearn's does: after the draws of the last step
+  GDD_HIP(hipMemcpyAsync(h_mt, w.mtb + last % 3, sizeof(DevMT), hipMemcpyDeviceToHost, s));
+  GDD_HIP(hipStreamSynchronize(s));
+  std::memcpy(rng->key, h_mt->key, sizeof(h_mt->key));
+  rng->pos = h_mt->pos;
+  return GDD_OK;
+}
 
 }  // namespace
 }  // namespace gdd
@@ -135,7 +228,7 @@ extern "C" int gdd_minibatch_kmeans_fit(
   const size_t pin_bytes = sizeof(int64_t) * (size_t)kChunkCap * bs +
                            sizeof(double) * (size_t)std::max(k - 1, 1) * T +
                            sizeof(int64_t) * 2 * (size_t)isz + sizeof(float) * (size_t)k * 2 + 256 +
-                           sizeof(int64_t) * 2 * (size_t)k;
+                           sizeof(DevMT) + sizeof(int64_t) * 2 * (size_t)k;
   Pinned pin;
   GDD_HIP(hipHostMalloc(&pin.p, pin_bytes, hipHostMallocDefault));
   char* pp = static_cast<char*>(pin.p);
@@ -147,8 +240,8 @@ extern "C" int gdd_minibatch_kmeans_fit(
   pp += sizeof(int64_t) * 2 * (size_t)isz;
   float* h_counts = reinterpret_cast<float*>(pp);
   pp += sizeof(float) * (size_t)k * 2;
-  int32_t* h_flag = reinterpret_cast<int32_t*>(pp);
-  pp += 256;
+  int32_t* h_flag = reinterpret_cast<int32_t*>(pp);  // 64 ints of flags, then a DevMT
+  pp += 256 + sizeof(DevMT);
   int64_t* h_pairs = reinterpret_cast<int64_t*>(pp);
 
   // ---- validation subset and initialisations (:2128-2163) ----------------------------------------
@@ -205,6 +298,17 @@ extern "C" int gdd_minibatch_kmeans_fit(
   bool norms_valid = false;
   int64_t n_since = 0;
   int64_t i = 0, stop_step = -1;
+  // Device-resident loop: when k <= b/2 at most b/2 centres can be due for reassignment, so the
+  // argsort branch never runs and, after step 0, no weight sum is ever zero — the reassignment
+  // steps are then known in advance (every ceil(10k/b) steps) and the whole loop, draws included,
+  // runs on the device with one host round trip per chunk of steps (overlapped with the next).
+  const bool dev_loop = 2 * (int64_t)k <= bs && n_steps > 0 && getenv("GDD_HOST_LOOP") == nullptr;
+  if (dev_loop) {
+    int rc = device_loop(n, dim, X, k, bs, n_steps, max_no_improvement, reassignment_ratio,
+                         static_cast<MTState*>(rng_state), w, h_flag, &stop_step, s);
+    if (rc) return rc;
+    i = n_steps;  // skip the host loop below
+  }
   std::vector<float> W(k);
   std::vector<int64_t> order;
   while (i < n_steps && stop_step < 0) {

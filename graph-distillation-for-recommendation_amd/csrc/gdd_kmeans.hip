@@ -17,6 +17,7 @@
 #include <climits>
 
 #include "gdd_common.hpp"
+#include "gdd_devrng.hpp"
 
 namespace gdd {
 GDD_STAMP_TABLE(kmeans)
@@ -292,11 +293,20 @@ template <int WAVES, bool VEC>
 __global__ __launch_bounds__(64 * WAVES) void k_assign_small(
     int64_t n, int dim, int dimp, const float* __restrict__ X, const int64_t* __restrict__ rows,
     int k, const float* __restrict__ C, const float* __restrict__ cn2, int32_t* __restrict__ labels,
-    float* __restrict__ sq_dist, const int32_t* __restrict__ stop, int step_i) {
+    float* __restrict__ sq_dist, const int32_t* __restrict__ stop, int step_i, RngNext rn) {
   if (stopped(stop, step_i)) return;
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 0);
   constexpr int kTileU = WAVES == 16 ? 6 : 8;  // 16 waves: 128 VGPRs per lane, fewer loads in flight
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (rn.rows && blockIdx.x == gridDim.x - 1) {
+    // extra workgroup: the next step's batch indices (randint(0, n, b)) from the device MT state,
+    // concurrently with this step's assignment
+    MTScratch* ms = reinterpret_cast<MTScratch*>(lds);
+    mt_load(rn.in, ms);
+    mt_randint_block(ms, 0, rn.n, rn.bs, rn.rows);
+    mt_store(ms, rn.out);
+    return;
+  }
   const int S = dimp + 1;
   float* Pl = lds;                                 // 32 points x S
   float* Cl = Pl + 32 * S;                         // WAVES x 32 centres x S (consecutive tiles)
@@ -446,14 +456,15 @@ __device__ __forceinline__ float fold_seq_lds(const float* __restrict__ b, int m
 }
 
 // ---------------------------------------------------------------------------------------------
-// inertia: sequential fp32 sum in sample order. Two LDS buffers of 4096 products: while lane 0 of
-// wave 0 folds one (fold_seq_lds), the other waves stage the next.
+// inertia: sequential fp32 sum in sample order. Four waves, one per SIMD: wave 0 folds one LDS
+// buffer of 4096 products (fold_seq_lds, bound by the dependent add chain) while waves 1-3, on the
+// other SIMDs so they never take wave 0's issue slots, stage the next buffer.
 // ---------------------------------------------------------------------------------------------
 constexpr int kInertiaChunk = 4096;
-__global__ __launch_bounds__(1024) void k_inertia(int64_t n, const float* __restrict__ sq,
-                                                  const float* __restrict__ w,
-                                                  float* __restrict__ out,
-                                                  const int32_t* __restrict__ stop, int step_i) {
+__global__ __launch_bounds__(256) void k_inertia(int64_t n, const float* __restrict__ sq,
+                                                 const float* __restrict__ w,
+                                                 float* __restrict__ out,
+                                                 const int32_t* __restrict__ stop, int step_i) {
   if (stopped(stop, step_i)) return;
   __shared__ __attribute__((aligned(16))) float buf[2][kInertiaChunk];
   const int nthr = blockDim.x - 64;  // waves 1.. stage
@@ -843,14 +854,15 @@ bool use_small_assign(int64_t n, int dim) {
 template <int W, bool VEC>
 int launch_assign_small_t(int64_t n, int dim, const float* X, const int64_t* rows, int k,
                           const float* C, const float* cn2, int32_t* labels, float* sq_dist,
-                          const int32_t* stop, int step_i, hipStream_t s) {
+                          const int32_t* stop, int step_i, const RngNext& rn, hipStream_t s) {
   const int dimp = (dim + 1) & ~1;
-  const size_t lds = assign_small_lds(W, dim);
+  const size_t lds = std::max(assign_small_lds(W, dim), sizeof(MTScratch) + 64);
   if (lds > 65536)
     GDD_HIP(hipFuncSetAttribute((const void*)k_assign_small<W, VEC>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  k_assign_small<W, VEC><<<(unsigned)((n + 31) / 32), 64 * W, lds, s>>>(
-      n, dim, dimp, X, rows, k, C, cn2, labels, sq_dist, stop, step_i);
+  const unsigned grid = (unsigned)((n + 31) / 32) + (rn.rows ? 1u : 0u);
+  k_assign_small<W, VEC><<<grid, 64 * W, lds, s>>>(n, dim, dimp, X, rows, k, C, cn2, labels,
+                                                   sq_dist, stop, step_i, rn);
   GDD_LAUNCHED();
   return GDD_OK;
 }
@@ -858,27 +870,35 @@ int launch_assign_small_t(int64_t n, int dim, const float* X, const int64_t* row
 template <bool VEC>
 int launch_assign_small(int64_t n, int dim, const float* X, const int64_t* rows, int k,
                         const float* C, const float* cn2, int32_t* labels, float* sq_dist,
-                        const int32_t* stop, int step_i, hipStream_t s) {
+                        const int32_t* stop, int step_i, const RngNext& rn, hipStream_t s) {
   // one 32-centre tile per wave when LDS allows (k <= 512), else fewer waves looping over tiles
   const int tiles = (k + 31) / 32;
   if (tiles > 8 && assign_small_lds(16, dim) <= kLdsCap)
-    return launch_assign_small_t<16, VEC>(n, dim, X, rows, k, C, cn2, labels, sq_dist, stop, step_i, s);
+    return launch_assign_small_t<16, VEC>(n, dim, X, rows, k, C, cn2, labels, sq_dist, stop, step_i,
+                                          rn, s);
   if (tiles > 4 && assign_small_lds(8, dim) <= kLdsCap)
-    return launch_assign_small_t<8, VEC>(n, dim, X, rows, k, C, cn2, labels, sq_dist, stop, step_i, s);
-  return launch_assign_small_t<4, VEC>(n, dim, X, rows, k, C, cn2, labels, sq_dist, stop, step_i, s);
+    return launch_assign_small_t<8, VEC>(n, dim, X, rows, k, C, cn2, labels, sq_dist, stop, step_i,
+                                         rn, s);
+  return launch_assign_small_t<4, VEC>(n, dim, X, rows, k, C, cn2, labels, sq_dist, stop, step_i,
+                                       rn, s);
 }
 
 // labels (+ optional per-sample sq_dist) of n samples against k centres.
 // small n: fused k_assign_small; large n: centre chunks over grid.y + 64-bit atomicMin keys.
+// rn.rows != nullptr (small n only): the launch also draws the next batch (see RngNext).
 int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k, const float* C,
                   const float* c_norm2, int32_t* labels, float* sq_dist,
-                  unsigned long long* keys, const int32_t* stop, int step_i, hipStream_t s) {
+                  unsigned long long* keys, const int32_t* stop, int step_i, hipStream_t s,
+                  const RngNext& rn = RngNext{nullptr, nullptr, nullptr, 0, 0}) {
   const int dimp = (dim + 1) & ~1;
   if (use_small_assign(n, dim)) {
     const bool vec = (dim % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(C)) & 15) == 0;
-    return vec ? launch_assign_small<true>(n, dim, X, rows, k, C, c_norm2, labels, sq_dist, stop, step_i, s)
-               : launch_assign_small<false>(n, dim, X, rows, k, C, c_norm2, labels, sq_dist, stop, step_i, s);
+    return vec ? launch_assign_small<true>(n, dim, X, rows, k, C, c_norm2, labels, sq_dist, stop,
+                                           step_i, rn, s)
+               : launch_assign_small<false>(n, dim, X, rows, k, C, c_norm2, labels, sq_dist, stop,
+                                            step_i, rn, s);
   }
+  GDD_REQUIRE(!rn.rows, "assign: in-launch batch draws need the small-batch path");
   GDD_REQUIRE(c_norm2 && keys, "assign: large-n path needs c_norm2 and the key workspace");
   const int waves = dimp <= 96 ? 4 : (dimp <= 224 ? 2 : 1);
   const int64_t gx = (n + 32 * waves - 1) / (32 * waves);
@@ -941,7 +961,7 @@ extern "C" int gdd_kmeans_assign(int64_t n, int dim, const float* X, const int64
 extern "C" int gdd_inertia(int64_t n, const float* sq_dist, const float* w, float* out,
                            gdd_stream_t stream) {
   GDD_REQUIRE(n >= 0 && out && (n == 0 || sq_dist), "inertia: bad arguments");
-  k_inertia<<<1, 1024, 0, to_hip(stream)>>>(n, sq_dist, w, out, nullptr, 0);
+  k_inertia<<<1, 256, 0, to_hip(stream)>>>(n, sq_dist, w, out, nullptr, 0);
   GDD_LAUNCHED();
   return GDD_OK;
 }
@@ -1023,17 +1043,25 @@ extern "C" int gdd_minibatch_step(int64_t b, int dim, const float* X, const int6
                                   int32_t* labels, int step_i, int64_t n_samples,
                                   int max_no_improvement, int flags, void* state, void* ws,
                                   size_t ws_bytes, gdd_stream_t stream) {
+  return gdd::minibatch_step_dev(b, dim, X, rows, k, C_old, C_new, weight_sums, labels, step_i,
+                                 n_samples, max_no_improvement, flags, state, ws, ws_bytes,
+                                 RngNext{nullptr, nullptr, nullptr, 0, 0}, to_hip(stream));
+}
+
+int gdd::minibatch_step_dev(int64_t b, int dim, const float* X, const int64_t* rows, int k,
+                            const float* C_old, float* C_new, float* weight_sums, int32_t* labels,
+                            int step_i, int64_t n_samples, int max_no_improvement, int flags,
+                            void* state, void* ws, size_t ws_bytes, const RngNext& rn,
+                            hipStream_t s) {
   GDD_REQUIRE(b > 0 && dim > 0 && dim <= 512 && k > 0 && n_samples > 0, "minibatch_step: bad shape");
   GDD_REQUIRE(X && rows && C_old && C_new && weight_sums && labels && state && ws,
               "minibatch_step: null pointer");
   GDD_REQUIRE(C_old != C_new, "minibatch_step: C_old and C_new must differ");
   if (ws_bytes < gdd_minibatch_step_ws_bytes(b, k))
     return fail(GDD_E_WORKSPACE, "minibatch_step: workspace too small");
-  hipStream_t s = to_hip(stream);
   MBState* st = static_cast<MBState*>(state);
   const int32_t* stop = &st->stop_at;
   StepWs w = carve_step(ws, ws_bytes, b, k);
-  const int dimp = (dim + 1) & ~1;
   const bool norms_valid = (flags & GDD_STEP_NORMS_VALID) != 0;
   const float* cn2 = w.cn2;
   if (!norms_valid) {
@@ -1044,7 +1072,7 @@ extern "C" int gdd_minibatch_step(int64_t b, int dim, const float* X, const int6
       GDD_LAUNCHED();
     }
   }
-  int rc = launch_assign(b, dim, X, rows, k, C_old, cn2, labels, w.sq, w.keys, stop, step_i, s);
+  int rc = launch_assign(b, dim, X, rows, k, C_old, cn2, labels, w.sq, w.keys, stop, step_i, s, rn);
   if (rc) return rc;
   // k update blocks (+ ||C_new||^2 for the next step) and one tail block (inertia, convergence)
   return launch_update(k + 1, b, dim, X, rows, nullptr, labels, k, C_old, C_new, weight_sums, w.cn2,
@@ -1174,3 +1202,152 @@ extern "C" int gdd_argmax_rows(int k, int dim, const float* centers, int64_t* ou
   GDD_LAUNCHED();
   return GDD_OK;
 }
+
+// ---- device-side MiniBatchKMeans control: batch draws and random reassignment ------------------
+namespace gdd {
+namespace {
+
+// randint(0, n, b) for one step from the device MT state (single workgroup)
+__global__ __launch_bounds__(1024) void k_mb_rng(const DevMT* __restrict__ in, DevMT* __restrict__ out,
+                                                 int64_t n, int64_t bs, int64_t* __restrict__ rows) {
+  __shared__ MTScratch ms;
+  mt_load(in, &ms);
+  mt_randint_block(&ms, 0, n, bs, rows);
+  mt_store(&ms, out);
+}
+
+// The reassignment branch of _mini_batch_step (sklearn/cluster/_kmeans.py:1640-1667) at a step
+// the host scheduled (_random_reassign :2029-2043), one workgroup, after that step's update:
+//   to = counts < fp32(ratio) * max(counts); with m = |to| > 0:
+//   new = permutation(b)[:m]  (random_state.choice(b, replace=False, size=m), legacy draws);
+//   C_new[to] = X[rows[new]] in cluster order; ||C_new[c]||^2 refreshed for those rows;
+//   counts[to] = min(counts[~to]).
+// `mid` receives the MT state after the permutation draws (the state sklearn leaves if this is
+// the last step); with rn.rows the workgroup then draws the next step's batch.
+// Requires m <= b/2 (true whenever k <= b/2; the host keeps other shapes on its own loop).
+__global__ __launch_bounds__(1024) void k_mb_reassign(
+    int step, int64_t bs, int dim, int k, float ratio, const float* __restrict__ X,
+    const int64_t* __restrict__ rows, float* __restrict__ C_new, float* __restrict__ counts,
+    float* __restrict__ cn2, const DevMT* __restrict__ mt_in, DevMT* __restrict__ mt_mid,
+    RngNext rn, const int32_t* __restrict__ stop) {
+  if (stopped(stop, step)) return;
+  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 40);
+  extern __shared__ int J[];  // bs swap partners, then the permutation prefix (int64)
+  __shared__ MTScratch ms;
+  __shared__ float s_f[32];
+  __shared__ int s_i[2];
+  __shared__ int s_cw[16];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = blockDim.x >> 6;
+  // max(counts)
+  float mx = -__builtin_inff();
+  for (int c = t; c < k; c += blockDim.x) mx = fmaxf(mx, counts[c]);
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (lane == 0) s_f[wave] = mx;
+  __syncthreads();
+  if (t == 0) {
+    float m = s_f[0];
+    for (int w = 1; w < nw; ++w) m = fmaxf(m, s_f[w]);
+    s_f[31] = m;
+  }
+  __syncthreads();
+  const float thr = ratio * s_f[31];  // NEP 50: fp32(ratio) * fp32 max, rounded to fp32
+  // |to| and min(counts[~to])
+  int cnt = 0;
+  float mn = __builtin_inff();
+  for (int c = t; c < k; c += blockDim.x) {
+    const float v = counts[c];
+    if (v < thr)
+      ++cnt;
+    else
+      mn = fminf(mn, v);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o);
+    mn = fminf(mn, __shfl_xor(mn, o));
+  }
+  __syncthreads();
+  if (lane == 0) {
+    s_f[wave] = mn;
+    s_cw[wave] = cnt;
+  }
+  __syncthreads();
+  if (t == 0) {
+    int c2 = 0;
+    float m2 = __builtin_inff();
+    for (int w = 0; w < nw; ++w) {
+      c2 += s_cw[w];
+      m2 = fminf(m2, s_f[w]);
+    }
+    s_i[0] = c2;
+    s_f[30] = m2;
+  }
+  __syncthreads();
+  const int m = s_i[0];
+  const float cmin = s_f[30];
+  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 41);
+  mt_load(mt_in, &ms);
+  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 42);
+  if (m > 0) {
+    int64_t* perm = reinterpret_cast<int64_t*>(J + ((bs + 1) & ~1ll));
+    mt_permutation_prefix_block(&ms, bs, m, J, perm);
+    GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 43);
+    // rank of each reassigned cluster in cluster order -> its new row
+    int base = 0;
+    for (int c0 = 0; c0 < k; c0 += blockDim.x) {
+      const int c = c0 + t;
+      const bool to = c < k && counts[c] < thr;
+      int total;
+      const int r = block_prefix_count(to, ms.cnt, &total);
+      if (to) {
+        const int64_t src = rows[perm[base + r]];
+        const float* xr = X + src * dim;
+        float* cr = C_new + (int64_t)c * dim;
+        for (int f = 0; f < dim; ++f) cr[f] = xr[f];
+        cn2[c] = npy_sumsq(xr, dim);
+      }
+      base += total;
+    }
+    __syncthreads();
+    for (int c = t; c < k; c += blockDim.x)
+      if (counts[c] < thr) counts[c] = cmin;
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 44);
+  mt_store(&ms, mt_mid);
+  if (rn.rows) {
+    __syncthreads();
+    mt_randint_block(&ms, 0, rn.n, rn.bs, rn.rows);
+    GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 45);
+    mt_store(&ms, rn.out);
+  }
+  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 46);
+}
+
+}  // namespace
+
+int mb_rng_launch(const DevMT* in, DevMT* out, int64_t n, int64_t bs, int64_t* rows, hipStream_t s) {
+  GDD_REQUIRE(n > 0 && n - 1 <= 0xffffffffll, "mb_rng: n out of range");
+  k_mb_rng<<<1, 1024, 0, s>>>(in, out, n, bs, rows);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const float* X,
+                       const int64_t* rows, float* C_new, float* counts, void* step_ws,
+                       size_t step_ws_bytes, const DevMT* mt_in, DevMT* mt_mid, const RngNext& rn,
+                       void* state, hipStream_t s) {
+  GDD_REQUIRE(2 * (int64_t)k <= bs, "mb_reassign: needs k <= batch/2");
+  StepWs w = carve_step(step_ws, step_ws_bytes, bs, k);
+  const size_t lds = sizeof(int) * (size_t)((bs + 1) & ~1ll) + sizeof(int64_t) * (size_t)k;
+  GDD_REQUIRE(lds <= 150 * 1024, "mb_reassign: batch too large for the LDS swap table");
+  if (lds > 65536)
+    GDD_HIP(hipFuncSetAttribute((const void*)k_mb_reassign, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+  const int32_t* stop = &static_cast<MBState*>(state)->stop_at;
+  k_mb_reassign<<<1, 1024, lds, s>>>(step, bs, dim, k, ratio, X, rows, C_new, counts, w.cn2, mt_in,
+                                     mt_mid, rn, stop);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+}  // namespace gdd

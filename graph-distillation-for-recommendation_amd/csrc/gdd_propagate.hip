@@ -20,6 +20,8 @@
 // fit one segment write p and update target in the epilogue; split rows write partials that a
 // second kernel folds in order.
 #include <algorithm>
+#include <cstdlib>
+#include <type_traits>
 
 #include "gdd_common.hpp"
 
@@ -58,6 +60,34 @@ __device__ __forceinline__ void vload(const float* p, float (&r)[V]) {
     r[0] = t.x; r[1] = t.y;
   } else {
     r[0] = *p;
+  }
+}
+// streamed (once-touched) rows: non-temporal, so they do not push the gathered x rows out of the
+// caches between their reuses
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+template <int V>
+__device__ __forceinline__ void vload_nt(const float* p, float (&r)[V]) {
+  if constexpr (V == 4) {
+    f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    r[0] = t.x; r[1] = t.y; r[2] = t.z; r[3] = t.w;
+  } else if constexpr (V == 2) {
+    f32x2 t = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(p));
+    r[0] = t.x; r[1] = t.y;
+  } else {
+    r[0] = __builtin_nontemporal_load(p);
+  }
+}
+template <int V>
+__device__ __forceinline__ void vstore_nt(float* p, const float (&r)[V]) {
+  if constexpr (V == 4) {
+    f32x4 t = {r[0], r[1], r[2], r[3]};
+    __builtin_nontemporal_store(t, reinterpret_cast<f32x4*>(p));
+  } else if constexpr (V == 2) {
+    f32x2 t = {r[0], r[1]};
+    __builtin_nontemporal_store(t, reinterpret_cast<f32x2*>(p));
+  } else {
+    __builtin_nontemporal_store(r[0], p);
   }
 }
 template <int V>
@@ -106,7 +136,11 @@ __global__ void k_make_items(int64_t n, const int32_t* __restrict__ rowptr,
 }
 
 // ---- one hop -----------------------------------------------------------------------------------
-template <int V, int G>
+// XCD-aware slicing (S > 0): the grid is 1-D and consecutive blocks land on consecutive XCDs, so
+// block b runs on XCD b % 8. That XCD always gets feature slice (b % 8) % S of the rows, i.e. its L2
+// only ever caches 1/S of every gathered row, and the 8/S XCDs sharing a slice split the items.
+// S = 0: grid (items, d chunks), no XCD mapping.
+template <int V, int G, int S>
 __global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
                                              const int32_t* __restrict__ counts,
                                              const int32_t* __restrict__ col,
@@ -115,10 +149,20 @@ __global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
                                              float* __restrict__ acc_out, float acc_scale,
                                              float* __restrict__ partials) {
   const int lane = threadIdx.x & (G - 1);
-  const int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  int64_t ib;  // item block
+  int chunk;   // feature chunk of G*V
+  if constexpr (S > 0) {
+    const int xcd = blockIdx.x & 7;
+    chunk = xcd % S;
+    ib = (int64_t)(blockIdx.x >> 3) * (8 / S) + xcd / S;
+  } else {
+    chunk = blockIdx.y;
+    ib = blockIdx.x;
+  }
+  const int64_t g = (ib * blockDim.x + threadIdx.x) / G;
   if (g >= counts[0]) return;
   const Item it = items[g];
-  const int f = (blockIdx.y * G + lane) * V;
+  const int f = (chunk * G + lane) * V;
   const bool fa = f < d;
   float acc[V];
 #pragma unroll
@@ -127,8 +171,8 @@ __global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
   for (int32_t c0 = it.begin; c0 < it.end; c0 += G) {
     const int32_t p = c0 + lane;
     const bool in = p < it.end;
-    const int32_t cj = in ? col[p] : 0;
-    const float vj = in ? scale * val[p] : 0.f;  // fp32(alpha) * v, rounded (agent :64)
+    const int32_t cj = in ? __builtin_nontemporal_load(col + p) : 0;
+    const float vj = in ? scale * __builtin_nontemporal_load(val + p) : 0.f;  // fp32(alpha)*v (agent :64)
     const int cnt = min(G, it.end - c0);
     for (int t = 0; t < cnt; t += kUnroll) {
       float xv[kUnroll][V];
@@ -157,13 +201,13 @@ __global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
   if (!fa) return;
   if (it.pslot < 0) {
     const int64_t o = (int64_t)it.row * d + f;
-    vstore<V>(y + o, acc);
+    vstore<V>(y + o, acc);  // gathered by the next hop: default policy
     if (acc_out) {
       float t[V];
-      vload<V>(acc_out + o, t);
+      vload_nt<V>(acc_out + o, t);
 #pragma unroll
       for (int v = 0; v < V; ++v) t[v] = t[v] + acc_scale * acc[v];  // two roundings (agent :65)
-      vstore<V>(acc_out + o, t);
+      vstore_nt<V>(acc_out + o, t);
     }
   } else {
     vstore<V>(partials + (int64_t)it.pslot * d + f, acc);
@@ -259,15 +303,46 @@ template <int V, int G>
 void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float scale, int d,
                    const float* x, float* y, float* acc, float acc_scale, hipStream_t s) {
   constexpr int kGroups = 256 / G;
-  dim3 grid((unsigned)((pl.max_items + kGroups - 1) / kGroups), (unsigned)((d + G * V - 1) / (G * V)));
-  k_hop<V, G><<<grid, 256, 0, s>>>(pl.items, pl.counts, col, val, scale, d, x, y, acc, acc_scale,
-                                   pl.partials);
+  const int64_t iblocks = (pl.max_items + kGroups - 1) / kGroups;
+  const int chunks = (d + G * V - 1) / (G * V);
+  auto xcd_launch = [&](auto S_) {
+    constexpr int S = decltype(S_)::value;
+    const int64_t groups = (iblocks + (8 / S) - 1) / (8 / S);
+    k_hop<V, G, S><<<(unsigned)(groups * 8), 256, 0, s>>>(pl.items, pl.counts, col, val, scale, d,
+                                                          x, y, acc, acc_scale, pl.partials);
+  };
+  if (chunks == 8)
+    xcd_launch(std::integral_constant<int, 8>());
+  else if (chunks == 4)
+    xcd_launch(std::integral_constant<int, 4>());
+  else if (chunks == 2)
+    xcd_launch(std::integral_constant<int, 2>());
+  else if (chunks == 1)
+    xcd_launch(std::integral_constant<int, 1>());
+  else
+    k_hop<V, G, 0><<<dim3((unsigned)iblocks, (unsigned)chunks), 256, 0, s>>>(
+        pl.items, pl.counts, col, val, scale, d, x, y, acc, acc_scale, pl.partials);
+}
+
+// lanes per item: the whole row up to 64 lanes, or (GDD_HOP_LANES=8/16/32, V = 4) narrower groups
+// that split the row into XCD slices
+int hop_lanes_override() {
+  static int v = [] {
+    const char* e = getenv("GDD_HOP_LANES");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 template <int V>
 void launch_hop_v(const Plan& pl, const int32_t* col, const float* val, float scale, int d,
                   const float* x, float* y, float* acc, float acc_scale, hipStream_t s) {
   const int lanes = (d + V - 1) / V;
+  const int ov = hop_lanes_override();
+  if (ov == 8)
+    return launch_hop_vg<V, 8>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+  if (ov == 16)
+    return launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
   if (lanes <= 16)
     launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
   else if (lanes <= 32)

@@ -100,6 +100,27 @@ class _Ops:
         return centers, idx
 
 
+_SIDE_STREAMS = {}
+
+
+def _side_inertia(sq: torch.Tensor):
+    """gdd_inertia(sq) on a per-device side stream, ordered after the caller's stream; returns the
+    device scalar and the event that marks it ready."""
+    dev = sq.device
+    side = _SIDE_STREAMS.get(dev)
+    if side is None:
+        side = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    out = torch.empty(1, dtype=torch.float32, device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    lib = _lib.device_lib()
+    _lib.check(lib.gdd_inertia(sq.shape[0], sq.data_ptr(), None, out.data_ptr(), side.cuda_stream))
+    sq.record_stream(side)
+    out.record_stream(side)
+    ev = torch.cuda.Event()
+    ev.record(side)
+    return out, ev
+
+
 class _BaseKMeans:
     def __init__(self, n_clusters=8, *, init="k-means++", n_init="auto", max_iter=300, tol=1e-4,
                  verbose=0, random_state=None, device="cuda"):
@@ -121,6 +142,43 @@ class _BaseKMeans:
 
     def fit_predict(self, X, y=None, sample_weight=None):
         return self.fit(X, sample_weight=sample_weight).labels_
+
+    # fitted attributes as scikit-learn exposes them (host numpy / Python float), copied from the
+    # device tensors on first access so the fit itself never waits on a device-to-host copy
+    @property
+    def cluster_centers_(self):
+        if getattr(self, "_centers_np", None) is None:
+            self._centers_np = self.cluster_centers_device_.cpu().numpy()
+        return self._centers_np
+
+    @cluster_centers_.setter
+    def cluster_centers_(self, value):
+        self._centers_np = np.asarray(value)
+
+    @property
+    def labels_(self):
+        if getattr(self, "_labels_np", None) is None:
+            self._labels_np = self.labels_device_.cpu().numpy()
+        return self._labels_np
+
+    @labels_.setter
+    def labels_(self, value):
+        self._labels_np = np.asarray(value)
+
+    @property
+    def inertia_(self):
+        pending = getattr(self, "_inertia_async", None)
+        if pending is not None:
+            out, ev = pending
+            ev.synchronize()
+            self._inertia_value = float(out.item())
+            self._inertia_async = None
+        return self._inertia_value
+
+    @inertia_.setter
+    def inertia_(self, value):
+        self._inertia_async = None
+        self._inertia_value = value
 
     def predict(self, X):
         Xd = _as_device_f32(X, self.device)
@@ -177,27 +235,30 @@ class MiniBatchKMeans(_BaseKMeans):
         st = _lib.MTState.from_random_state(rs)
         ws = _lib.workspace(lib.gdd_minibatch_kmeans_fit_ws_bytes(n, dim, k, bs, isz), dev)
         centers = torch.empty((k, dim), dtype=torch.float32, device=dev)
-        labels = torch.empty(n, dtype=torch.int32, device=dev) if self.compute_labels else None
-        inertia = torch.empty(1, dtype=torch.float32, device=dev)
         n_steps, ewa = ctypes.c_int64(0), ctypes.c_double(0.0)
         max_ni = -1 if self.max_no_improvement is None else int(self.max_no_improvement)
+        # the final labels pass is enqueued below, so that its inertia can run off the main stream
         _lib.check(lib.gdd_minibatch_kmeans_fit(
             n, dim, Xd.data_ptr(), k, bs, int(self.max_iter), max_ni, float(self.reassignment_ratio),
-            isz, self._n_init(3), int(bool(self.compute_labels)), ctypes.addressof(st),
+            isz, self._n_init(3), 0, ctypes.addressof(st),
             ctypes.cast(_lib.argsort_callback, ctypes.c_void_p).value, centers.data_ptr(),
-            _lib.ptr(labels), inertia.data_ptr(), ctypes.addressof(n_steps), ctypes.addressof(ewa),
+            None, None, ctypes.addressof(n_steps), ctypes.addressof(ewa),
             ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev)))
+        del ws
         st.to_random_state(rs)  # leave the generator where sklearn leaves it
         self.n_steps_ = int(n_steps.value)
         self.n_iter_ = int(np.ceil((self.n_steps_ * bs) / n))
         self.cluster_centers_device_ = centers
-        self.cluster_centers_ = centers.cpu().numpy()
         if self.compute_labels:
+            # full labels pass (:2191-2197): labels on the caller's stream; the inertia (a sequential
+            # fp32 fold bound by its add chain) on a side stream, read on first access of inertia_
+            labels = torch.empty(n, dtype=torch.int32, device=dev)
+            sq = torch.empty(n, dtype=torch.float32, device=dev)
+            _Ops(dev, n, k, dim).assign(Xd, centers, labels=labels, sq=sq)
             self.labels_device_ = labels
-            self.labels_ = labels.cpu().numpy()
-            self.inertia_ = float(inertia.item())
+            self._inertia_async = _side_inertia(sq)
         else:
-            self.inertia_ = ewa.value * n
+            self._inertia_value = ewa.value * n
         return self
 
     def _fit_host_loop(self, Xd, rs):

@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Propagation timing at the arxiv shape (device events): whole gdd_propagate and per hop."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "graph-distillation-for-recommendation_amd"))
+import torch  # noqa: E402
+
+import gdd  # noqa: E402
+from gdd import synth  # noqa: E402
+
+
+def main(cfg_name="arxiv", reps=10):
+    cfg = synth.CONFIGS[cfg_name]
+    A = synth.chung_lu(cfg.n, cfg.avg_degree, cfg.seed)
+    X = torch.from_numpy(synth.features(cfg.n, cfg.d, cfg.seed)).cuda()
+    gn = gdd.normalize_adj(gdd.to_csr(A))
+    for _ in range(2):
+        gdd.propagate(gn, X, cfg.T, cfg.alpha)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        gdd.propagate(gn, X, cfg.T, cfg.alpha)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    n, d, nnz, hops = cfg.n, cfg.d, gn.nnz, cfg.T - 1
+    bytes_hop = 4 * (n + 1) + 8 * nnz + 16 * n * d
+    print(f"{cfg_name}: propagate {ms:.3f} ms, {ms / hops * 1e3:.1f} us/hop incl. plan+init, "
+          f"algorithmic {bytes_hop * hops / ms / 1e6:.0f} GB/s", flush=True)
+
+
+if __name__ == "__main__":
+    main(*(sys.argv[1:2] or ["arxiv"]))

@@ -48,6 +48,7 @@ def main():
         show("assign_small", a, [0, 2, 3, 5, 13, 14, 15, 16], 0)
         show("update block0", a, list(range(20, 26)), 20)
         show("update tail", a, list(range(30, 33)), 30)
+        show("mb_reassign", a, list(range(40, 47)), 40)
         bank = 10 * ((cfg.k - 2) & 1)  # round k-2 is the last complete tail
         show("kpp_tail", p, [bank + i for i in range(7)], bank)
         show("kpp_dist", p, list(range(20, 24)), 20)
