@@ -124,13 +124,29 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max = float(t.item())
 
-    # roofline of the dominant device kernel: the propagation SpMM hop (HBM-bound)
-    prop_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1, _ in prop_ev]))
-    nnz = prop_ev[0][2]
+    # roofline of the dominant HBM kernel: one propagation hop (k_hop + its split-row fix-up), timed
+    # per launch with HIP events on the stream it runs on, against a plan built once (the same
+    # plan gdd_propagate builds per call)
+    gn = gdd.normalize_adj(graph)
     n, d, hops = cfg.n, cfg.d, cfg.T - 1
+    nnz = gn.nnz
+    plan = gdd.graph.SpMMPlan(gn, d)
+    bufs = [X.clone(), torch.empty_like(X)]
+    acc = torch.zeros_like(X)
+    w32 = float(np.float32(1.0 - cfg.alpha))
+    for h in range(3):
+        plan.hop(bufs[h % 2], bufs[(h + 1) % 2], cfg.alpha, acc, w32)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for h in range(hops):
+        plan.hop(bufs[h % 2], bufs[(h + 1) % 2], cfg.alpha, acc, w32)
+    ev[1].record()
+    torch.cuda.synchronize()
+    hop_ms = ev[0].elapsed_time(ev[1]) / hops
+    prop_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1, _ in prop_ev]))
     bytes_hop = 4 * (n + 1) + 8 * nnz + 16 * n * d  # rowptr, col, val, p_in, p_out, target r/w
-    bytes_total = hops * bytes_hop + 8 * n * d     # + target = (1-a) X
-    achieved = bytes_total / (prop_ms * 1e-3) / 1e9
+    achieved = bytes_hop / (hop_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic()
 
     out = {
         "metric": "distill wallclock (SpMM+k-means) & test-acc parity, ogbn-arxiv r=0.5% @1-8 GPU",
@@ -152,10 +168,11 @@ def main():
                    "nodes": cfg.n, "nnz_in": nnz_in, "nnz_norm": nnz, "feat_dim": d,
                    "k": cfg.k, "parallelism": f"replicas x{world} (one graph per GPU)",
                    "kmeans_steps": n_steps_km},
-        "roofline": {"bound": "hbm", "kernel": "propagate (17 x k_hop + fixup)",
+        "roofline": {"bound": "hbm", "kernel": "k_hop (+ k_fixup): one propagation hop",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "algorithmic_bytes": bytes_total, "avg_ms": prop_ms},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "algorithmic_bytes_per_launch": bytes_hop, "avg_launch_ms": hop_ms,
+                     "traffic_source": traffic_src, "propagate_call_ms": prop_ms},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -165,6 +182,19 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def pmc_traffic():
+    """HBM-side bytes per k_hop launch from the newest committed rocprofv3 PMC summary
+    (profiles/<round>_khop_traffic.json, written by tools/pmc_summary.py from FETCH_SIZE and
+    WRITE_SIZE passes of this same bench command), or (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_khop_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        rec = json.load(f)
+    return rec.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(cfg, A, X_h, cpu_steps, gpu_km_steps):

@@ -269,12 +269,10 @@ size_t plan_ws_bytes(int64_t n, int64_t nnz, int d) {
   return b + 4096;
 }
 
-int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv, Plan& pl,
-               hipStream_t s) {
-  int32_t* nseg = cv.take<int32_t>(n);
-  int32_t* npart = cv.take<int32_t>(n);
-  int32_t* item_off = cv.take<int32_t>(n);
-  int32_t* part_off = cv.take<int32_t>(n);
+// carve the plan's buffers (same layout for build_plan and a later planned hop)
+int carve_plan(int64_t n, int64_t nnz, int d, Carver& cv, Plan& pl, int32_t** tmp, void** scan_ws,
+               size_t* scan_bytes) {
+  for (int q = 0; q < 4; ++q) tmp[q] = cv.take<int32_t>(n);
   pl.max_items = max_items_for(n, nnz);
   pl.max_long = nnz / kSeg + 1;
   pl.items = cv.take<Item>(pl.max_items);
@@ -282,9 +280,20 @@ int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv,
   pl.long_rows = cv.take<int32_t>(pl.max_long);
   pl.long_off = cv.take<int32_t>(pl.max_long);
   pl.partials = cv.take<float>(max_parts_for(nnz) * (size_t)d);
-  size_t sb = scan_i32_ws_bytes(n);
-  void* scan_ws = cv.take<char>(sb);
+  *scan_bytes = scan_i32_ws_bytes(n);
+  *scan_ws = cv.take<char>(*scan_bytes);
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "propagate: workspace too small");
+  return GDD_OK;
+}
+
+int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv, Plan& pl,
+               hipStream_t s) {
+  int32_t* tmp[4];
+  void* scan_ws;
+  size_t sb;
+  int rc0 = carve_plan(n, nnz, d, cv, pl, tmp, &scan_ws, &sb);
+  if (rc0) return rc0;
+  int32_t *nseg = tmp[0], *npart = tmp[1], *item_off = tmp[2], *part_off = tmp[3];
   const unsigned gb = (unsigned)((n + 255) / 256);
   GDD_HIP(hipMemsetAsync(pl.counts, 0, sizeof(int32_t) * 4, s));
   k_seg_counts<<<gb, 256, 0, s>>>(n, rowptr, nseg, npart);
@@ -402,6 +411,32 @@ extern "C" int gdd_spmm(int64_t n, int64_t nnz, const int32_t* rowptr, const int
   rc = build_plan(n, nnz, d, rowptr, cv, pl, s);
   if (rc) return rc;
   return run_hop(pl, rowptr, col, val, scale, d, x, y, acc, acc_scale, s);
+}
+
+extern "C" int gdd_spmm_plan(int64_t n, int64_t nnz, const int32_t* rowptr, int d, void* ws,
+                             size_t ws_bytes, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && n < INT32_MAX && nnz >= 0 && nnz < INT32_MAX && d > 0 && rowptr && ws,
+              "spmm_plan: bad arguments");
+  Carver cv(ws, ws_bytes);
+  Plan pl;
+  return build_plan(n, nnz, d, rowptr, cv, pl, to_hip(stream));
+}
+
+extern "C" int gdd_spmm_planned(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
+                                const float* val, int d, float scale, const float* x, float* y,
+                                float* acc, float acc_scale, const void* ws, size_t ws_bytes,
+                                gdd_stream_t stream) {
+  int rc = check_csr_args(n, nnz, rowptr, col, val, d);
+  if (rc) return rc;
+  GDD_REQUIRE(x && y && ws, "spmm_planned: null pointer");
+  Carver cv(const_cast<void*>(ws), ws_bytes);
+  Plan pl;
+  int32_t* tmp[4];
+  void* scan_ws;
+  size_t sb;
+  rc = carve_plan(n, nnz, d, cv, pl, tmp, &scan_ws, &sb);
+  if (rc) return rc;
+  return run_hop(pl, rowptr, col, val, scale, d, x, y, acc, acc_scale, to_hip(stream));
 }
 
 extern "C" int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,

@@ -38,6 +38,9 @@ SIGNATURES = {
                                _vp, _vp, _vp, _c_size, _vp]),
     "gdd_spmm": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _c_int, _c_f32, _vp, _vp, _vp, _c_f32,
                           _vp, _c_size, _vp]),
+    "gdd_spmm_plan": (_c_int, [_c_i64, _c_i64, _vp, _c_int, _vp, _c_size, _vp]),
+    "gdd_spmm_planned": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _c_int, _c_f32, _vp, _vp, _vp,
+                                  _c_f32, _vp, _c_size, _vp]),
     "gdd_row_norms": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp]),
     "gdd_kmeans_assign_ws_bytes": (_c_size, [_c_i64]),
     "gdd_kmeans_assign": (_c_int, [_c_i64, _c_int, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _vp,

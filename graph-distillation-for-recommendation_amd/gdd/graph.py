@@ -172,3 +172,25 @@ def spmm(adj: CSRGraph, x: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
                             y.data_ptr(), None, 0.0, ws.data_ptr(), ws.numel(),
                             _lib.stream_ptr(x.device)))
     return y
+
+
+class SpMMPlan:
+    """A CSR structure's row-segment work list, built once (gdd_spmm_plan); each :meth:`hop`
+    is then one planned SpMM launch pair (gdd_spmm_planned) with the canonical summation order."""
+
+    def __init__(self, adj: CSRGraph, d: int):
+        self.adj, self.d = adj, d
+        self.lib, self.ws = _ws_propagate(adj, d)
+        _lib.check(self.lib.gdd_spmm_plan(adj.n, adj.nnz, adj.rowptr.data_ptr(), d,
+                                          self.ws.data_ptr(), self.ws.numel(),
+                                          _lib.stream_ptr(adj.device)))
+
+    def hop(self, x: torch.Tensor, y: torch.Tensor, scale: float = 1.0, acc: torch.Tensor = None,
+            acc_scale: float = 0.0) -> torch.Tensor:
+        """y = (scale·A) @ x; with acc also acc = acc + acc_scale * y (two fp32 roundings)."""
+        a = self.adj
+        _lib.check(self.lib.gdd_spmm_planned(
+            a.n, a.nnz, a.rowptr.data_ptr(), _lib.ptr(a.col), _lib.ptr(a.values()), self.d,
+            float(scale), x.data_ptr(), y.data_ptr(), _lib.ptr(acc), float(acc_scale),
+            self.ws.data_ptr(), self.ws.numel(), _lib.stream_ptr(x.device)))
+        return y

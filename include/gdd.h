@@ -79,6 +79,14 @@ int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* 
 int gdd_spmm(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* val,
              int d, float scale, const float* x, float* y, float* acc, float acc_scale, void* ws,
              size_t ws_bytes, gdd_stream_t stream);
+/* The same hop split in two: gdd_spmm_plan builds the row-segment work list of a CSR structure in  */
+/* ws (gdd_propagate_ws_bytes(n, nnz, d)); gdd_spmm_planned then runs hops against it without      */
+/* rebuilding it (one k_hop + one fix-up launch per call) — the unit the bench times per launch.     */
+int gdd_spmm_plan(int64_t n, int64_t nnz, const int32_t* rowptr, int d, void* ws, size_t ws_bytes,
+                  gdd_stream_t stream);
+int gdd_spmm_planned(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
+                     const float* val, int d, float scale, const float* x, float* y, float* acc,
+                     float acc_scale, const void* ws, size_t ws_bytes, gdd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* (a5/a6/a8) k-means building blocks (scikit-learn 1.7.2 semantics, fp32 data)                      */

@@ -101,3 +101,29 @@ def test_spmm_matches_oracle():
     g = gdd.normalize_adj(gdd.to_csr(A))
     y = gdd.spmm(g, torch.from_numpy(x).cuda(), 0.7)
     assert np.array_equal(y.cpu().numpy().view(np.uint32), y_ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("d", [128, 40, 7])
+def test_planned_hop_matches_oracle_and_accumulates(d):
+    # gdd_spmm_plan once, then gdd_spmm_planned hops (the unit bench.py times): bit-exact with the
+    # oracle's canonical order, including a hub row split into several segments
+    n = 3000
+    A = _graph(n, 12.0, 21)
+    A = A.tolil()
+    A[5, :] = 1.0  # a hub row of n entries (> GDD_PROP_SEG): the split-row fix-up path
+    A = A.tocsr()
+    rp, col, _ = _csr_host(A)
+    ro, co, vo = O.normalize_csr(rp, col, None, -1)
+    x = synth.features(n, d, 2)
+    acc0 = synth.features(n, d, 3)
+    y_ref = O.spmm(ro, co, vo, x, scale=0.91)
+    acc_ref = (acc0 + np.float32(0.09) * y_ref).astype(np.float32)
+    g = gdd.normalize_adj(gdd.to_csr(A))
+    plan = gdd.graph.SpMMPlan(g, d)
+    xd = torch.from_numpy(x).cuda()
+    for _ in range(2):  # the plan is reusable
+        y = torch.empty_like(xd)
+        acc = torch.from_numpy(acc0).cuda()
+        plan.hop(xd, y, 0.91, acc, 0.09)
+        assert np.array_equal(y.cpu().numpy().view(np.uint32), y_ref.view(np.uint32))
+        assert np.array_equal(acc.cpu().numpy().view(np.uint32), acc_ref.view(np.uint32))
