@@ -80,6 +80,33 @@ __device__ float sdot_skx_finish(float a, float rx, float ry, int64_t n, float* 
   return r;
 }
 
+// sdot_skx_finish with the fold done by cross-lane shuffles instead of lane 0 over LDS (same
+// operations, same order); every lane returns the dot.
+__device__ float sdot_skx_finish_shfl(float a, float rx, float ry, int64_t n) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n1 = n & ~31ll;
+  const int64_t n64 = n1 & ~63ll;
+  // acc[u][l] = a[16u + l] + a[16u + l + 8], held by lane 16u + l (l < 8)
+  float acc = a + __shfl_down(a, 8);
+  if (n64 < n1) {  // the 32-wide block: acc[u][l] = fma(x[n64 + 8u + l], y[n64 + 8u + l], acc[u][l])
+    const int src = ((lane >> 4) << 3) + (lane & 7);
+    acc = __builtin_fmaf(__shfl(rx, src), __shfl(ry, src), acc);
+  }
+  // s[l] = ((acc[0][l] + acc[1][l]) + acc[2][l]) + acc[3][l]  (lanes 0..7)
+  const float a1 = __shfl(acc, (lane + 16) & 63), a2 = __shfl(acc, (lane + 32) & 63),
+              a3 = __shfl(acc, (lane + 48) & 63);
+  const float sl = ((acc + a1) + a2) + a3;
+  const float h = sl + __shfl(sl, (lane + 4) & 63);  // h[l] = s[l] + s[l+4]  (lanes 0..3)
+  const float h0 = __shfl(h, 0), h1 = __shfl(h, 1), h2 = __shfl(h, 2), h3 = __shfl(h, 3);
+  double dot = n1 ? (double)((h0 + h1) + (h2 + h3)) : 0.0;
+  for (int64_t t = n1; t < n; ++t) {
+    const int L = (int)(t - n64);
+    const float p = __shfl(ry, L) * __shfl(rx, L);
+    dot = dot + (double)p;
+  }
+  return (float)dot;
+}
+
 // the whole dot by one wave (used once, for the first centre's potential)
 __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restrict__ y, int64_t n,
                                float* scratch /* 192 floats of LDS owned by this wave */) {
@@ -349,6 +376,103 @@ __global__ __launch_bounds__(kTailThreads) void k_kpp_tail(
   GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 6 + 10 * (c & 1));
 }
 
+// Rounds c >= 1 when every thread's share of a distance row fits in registers (chunk <= kR) and
+// T <= kTT. Everything the round needs is requested up front: the lane accumulators and
+// remainders for the potentials and every trial's slice of its distance row, so the cumulative
+// potential of the winning trial starts as soon as the argmin is known; the binary searches are
+// replaced by counts (cum is non-decreasing: searchsorted_left(cum, r) = #{i : cum[i] < r}).
+template <int kTT, int kR>
+__global__ __launch_bounds__(kTailThreads) void k_kpp_tail_fast(
+    int64_t n, int dim, const float* __restrict__ X, const float* __restrict__ w,
+    const float* __restrict__ dist, const float* __restrict__ acc, int T, int c, int k,
+    const double* __restrict__ uniforms, float* __restrict__ centers,
+    int64_t* __restrict__ indices, KppState* __restrict__ st) {
+  __shared__ float s_pot[kMaxTrials];
+  __shared__ double s_r[kMaxTrials];
+  __shared__ double s_part[kTailThreads / 64];
+  __shared__ int s_cnt[kMaxTrials][kTailThreads / 64];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 0 + 10 * (c & 1));
+  const bool more = c + 1 < k;
+  const double u_mine = (tid < T && more) ? uniforms[(int64_t)c * T + tid] : 0.0;
+  const int64_t chunk = (n + kTailThreads - 1) / kTailThreads;
+  const int64_t lo = min<int64_t>(n, tid * chunk), hi = min<int64_t>(n, lo + chunk);
+  float wv[kR];
+#pragma unroll
+  for (int u = 0; u < kR; ++u) wv[u] = (w && lo + u < hi) ? w[lo + u] : 1.0f;
+  // potentials of the T trials
+  if (wave < T) {
+    const int64_t ri = (n & ~63ll) + lane;
+    const float rx = ri < n ? dist[(int64_t)wave * n + ri] : 0.f;
+    const float ry = ri < n ? (w ? w[ri] : 1.0f) : 0.f;
+    const float p = sdot_skx_finish_shfl(acc[wave * 64 + lane], rx, ry, n);
+    if (lane == 0) s_pot[wave] = p;
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 1 + 10 * (c & 1));
+  int b = 0;  // np.argmin: first minimum; a NaN is returned as soon as it is met
+  for (int t = 1; t < T; ++t) {
+    const float pb = s_pot[b], pt = s_pot[t];
+    if (pb == pb && (pt < pb || pt != pt)) b = t;
+  }
+  const float pot = s_pot[b];
+  const int64_t src = st->cand[b];
+  if (tid == 0) {
+    st->best = b;
+    st->pot = pot;
+    indices[c] = src;
+  }
+  if (tid < T) s_r[tid] = u_mine * (double)pot;
+  for (int j = tid; j < dim; j += kTailThreads) centers[(int64_t)c * dim + j] = X[src * dim + j];
+  if (!more) return;
+  // cumulative potential of the winning trial (fp64 of the fp32 products w_i * closest_i)
+  float pr[kR];
+  const float* row = dist + (int64_t)b * n;
+#pragma unroll
+  for (int u = 0; u < kR; ++u) pr[u] = (lo + u < hi) ? wv[u] * row[lo + u] : 0.f;
+  double run = 0.0;
+#pragma unroll
+  for (int u = 0; u < kR; ++u)
+    if (lo + u < hi) run = run + (double)pr[u];
+  double incl = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) s_part[wave] = incl;
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 4 + 10 * (c & 1));
+  double base = incl - run;
+  for (int q = 0; q < wave; ++q) base += s_part[q];
+  // counts of cum[i] < r_t over the wave's entries (one ballot per entry slot and trial)
+  double cu[kR];
+#pragma unroll
+  for (int u = 0; u < kR; ++u) {
+    base = base + (double)pr[u];
+    cu[u] = base;
+  }
+#pragma unroll
+  for (int t = 0; t < kTT; ++t) {
+    if (t < T) {
+      const double r = s_r[t];
+      int cw = 0;
+#pragma unroll
+      for (int u = 0; u < kR; ++u) cw += __popcll(__ballot(lo + u < hi && cu[u] < r));
+      if (lane == 0) s_cnt[t][wave] = cw;
+    }
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 5 + 10 * (c & 1));
+  if (tid < T) {
+    int64_t a = 0;
+    for (int q = 0; q < kTailThreads / 64; ++q) a += s_cnt[tid][q];
+    if (a > n - 1) a = n - 1;
+    st->cand[tid] = a;
+  }
+  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 6 + 10 * (c & 1));
+}
+
 __global__ void k_ones(int64_t n, float* p) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = 1.0f;
@@ -409,6 +533,8 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   if (lds > 65536)
     GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dist<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  constexpr int kFastT = 12, kFastR = 4;
+  const bool fast_tail = n_trials <= kFastT && (n + kTailThreads - 1) / kTailThreads <= kFastR;
   for (int c = 1; c < k; ++c) {
     const float* prev = dist[(c - 1) & 1];
     float* cur = dist[c & 1];
@@ -419,8 +545,12 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       k_kpp_dist<false><<<dim3(G, n_trials), 256, lds, s>>>(n, dim, X, w, xsq, closest0, prev, st,
                                                             cur, acc, L);
     GDD_LAUNCHED();
-    k_kpp_tail<<<1, kTailThreads, 0, s>>>(n, dim, X, w, closest0, cur, acc, n_trials, c, k,
-                                          first_id, uniforms, xsq, cum, centers, indices, st);
+    if (fast_tail)
+      k_kpp_tail_fast<kFastT, kFastR><<<1, kTailThreads, 0, s>>>(n, dim, X, w, cur, acc, n_trials, c,
+                                                                 k, uniforms, centers, indices, st);
+    else
+      k_kpp_tail<<<1, kTailThreads, 0, s>>>(n, dim, X, w, closest0, cur, acc, n_trials, c, k,
+                                            first_id, uniforms, xsq, cum, centers, indices, st);
     GDD_LAUNCHED();
   }
   return GDD_OK;

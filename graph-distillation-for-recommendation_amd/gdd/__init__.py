@@ -6,15 +6,17 @@ the reference file:line each entry point replaces):
 * :func:`gdd.graph.to_csr`, :func:`gdd.graph.normalize_adj_tensor`, :func:`gdd.graph.propagate`
 * :class:`gdd.kmeans.KMeans`, :class:`gdd.kmeans.MiniBatchKMeans`
 * :func:`gdd.cluster.cluster_mean`, :func:`gdd.cluster.argmax_rows`
-* :func:`gdd.pipeline.pretrained_clustering_hot_path` — normalise → propagate → k-means on the
-  logits → cluster means → argmax labels, as ClustGDD.pretrained_clustering does it.
+* :class:`gdd.sharded.ShardedKMeans` — Lloyd over range-partitioned rows on several ranks, one
+  fixed-point all-reduce per iteration (rank-count invariant)
 """
 from . import _lib  # noqa: F401  (imports torch first, see _lib docstring)
 from .cluster import argmax_rows, cluster_mean, group_by_label
 from .graph import CSRGraph, normalize_adj, normalize_adj_tensor, propagate, spmm, to_csr
 from .kmeans import KMeans, MiniBatchKMeans
+from .sharded import ShardedKMeans, shard_rows
 
 __all__ = [
     "CSRGraph", "to_csr", "normalize_adj", "normalize_adj_tensor", "propagate", "spmm",
-    "KMeans", "MiniBatchKMeans", "cluster_mean", "argmax_rows", "group_by_label",
+    "KMeans", "MiniBatchKMeans", "ShardedKMeans", "shard_rows", "cluster_mean", "argmax_rows",
+    "group_by_label",
 ]
