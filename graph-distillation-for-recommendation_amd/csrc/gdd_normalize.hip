@@ -132,6 +132,7 @@ __global__ void k_rows_emit(int64_t n, const int32_t* __restrict__ rowptr,
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kGroup;
   if (i >= n) return;  // whole group exits together
   const int add = *flag;
+  if (!val && add) return;  // binary with I added: the entry-parallel kernels own this case
   const int32_t s = rowptr[i], e = rowptr[i + 1];
   int32_t base = kFill ? rowptr_out[i] : 0;
   int32_t written = 0;
@@ -182,6 +183,101 @@ __global__ void k_rows_emit(int64_t n, const int32_t* __restrict__ rowptr,
   if (!kFill && lane == 0) cnt[i] = written;
 }
 
+// ---- binary adjacency with I added (the reference's case: normalize_adj_tensor on 0/1 data) ----
+// Every degree is >= 1, so every r_i > 0 and every scaled value is > 0: nothing is dropped, and a
+// row's output is its input with the diagonal merged in. Work is then entry-parallel — one lane
+// per stored entry — instead of row-parallel, so hub rows (12k entries in the arxiv-shaped graph)
+// no longer serialise one lane group. The kernels are no-ops when the probe chose the other path.
+__device__ __forceinline__ bool fast_path(const int32_t* flag) { return *flag == 1; }
+
+// per row: output count and where the diagonal sits (lower bound of i in the row's columns)
+__global__ void k_fast_count(int64_t n, const int32_t* __restrict__ rowptr,
+                             const int32_t* __restrict__ col, const int32_t* __restrict__ flag,
+                             int32_t* __restrict__ cnt, int32_t* __restrict__ dpos) {
+  if (!fast_path(flag)) return;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t s = rowptr[i], e = rowptr[i + 1];
+  int32_t a = s, b = e;
+  while (a < b) {
+    const int32_t m = (a + b) >> 1;
+    if (col[m] < (int32_t)i)
+      a = m + 1;
+    else
+      b = m;
+  }
+  const bool has = a < e && col[a] == (int32_t)i;
+  cnt[i] = (e - s) + (has ? 0 : 1);
+  dpos[i] = has ? -(a - s) - 1 : (a - s);  // < 0: stored at -(v+1); >= 0: inserted at v
+}
+
+// one lane per stored entry; the block's row range is found once, each lane then searches it
+__global__ __launch_bounds__(256) void k_fast_fill(int64_t n, int64_t nnz,
+                                                   const int32_t* __restrict__ rowptr,
+                                                   const int32_t* __restrict__ col,
+                                                   const int32_t* __restrict__ flag,
+                                                   const double* __restrict__ r64,
+                                                   const int32_t* __restrict__ dpos,
+                                                   const int32_t* __restrict__ rowptr_out,
+                                                   int32_t* __restrict__ col_out,
+                                                   float* __restrict__ val_out) {
+  if (!fast_path(flag)) return;
+  __shared__ int32_t s_rows[2];
+  const int64_t p0 = (int64_t)blockIdx.x * blockDim.x;
+  if (p0 >= nnz) return;
+  const int64_t p1 = min<int64_t>(nnz, p0 + blockDim.x) - 1;
+  if (threadIdx.x < 2) {  // last row whose start <= target
+    const int64_t target = threadIdx.x == 0 ? p0 : p1;
+    int64_t a = 0, b = n;  // rowptr[a] <= target < rowptr[b]
+    while (b - a > 1) {
+      const int64_t m = (a + b) >> 1;
+      if (rowptr[m] <= target)
+        a = m;
+      else
+        b = m;
+    }
+    s_rows[threadIdx.x] = (int32_t)a;
+  }
+  __syncthreads();
+  const int64_t p = p0 + threadIdx.x;
+  if (p >= nnz) return;
+  int64_t a = s_rows[0], b = (int64_t)s_rows[1] + 1;
+  while (b - a > 1) {
+    const int64_t m = (a + b) >> 1;
+    if (rowptr[m] <= p)
+      a = m;
+    else
+      b = m;
+  }
+  const int32_t i = (int32_t)a;
+  const int32_t off = (int32_t)(p - rowptr[i]);
+  const int32_t dp = dpos[i];
+  const int32_t j = col[p];
+  // binary a_ij = 1, plus I on the diagonal; fp64 scaling as in scaled_value()
+  const double v = (j == i) ? 2.0 : 1.0;
+  const double t = r64[i] * v;
+  const double u = t * r64[j];
+  const int32_t pos = rowptr_out[i] + off + ((dp >= 0 && off >= dp) ? 1 : 0);
+  col_out[pos] = j;
+  val_out[pos] = (float)u;
+}
+
+// the diagonals that (A + I) adds to rows without a stored one
+__global__ void k_fast_diag(int64_t n, const int32_t* __restrict__ flag,
+                            const double* __restrict__ r64, const int32_t* __restrict__ dpos,
+                            const int32_t* __restrict__ rowptr_out, int32_t* __restrict__ col_out,
+                            float* __restrict__ val_out) {
+  if (!fast_path(flag)) return;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t dp = dpos[i];
+  if (dp < 0) return;
+  const double t = r64[i] * 1.0;
+  const int32_t pos = rowptr_out[i] + dp;
+  col_out[pos] = (int32_t)i;
+  val_out[pos] = (float)(t * r64[i]);
+}
+
 __global__ void k_set_last(int64_t n, const int32_t* __restrict__ cnt, int32_t* rowptr_out) {
   // rowptr_out holds the exclusive scan of cnt; close it with the total
   if (threadIdx.x == 0 && blockIdx.x == 0) rowptr_out[n] = rowptr_out[n - 1] + cnt[n - 1];
@@ -198,6 +294,7 @@ extern "C" size_t gdd_normalize_ws_bytes(int64_t n, int64_t nnz) {
   b += align256(sizeof(double) * (size_t)n);    // r64
   b += align256(sizeof(float) * (size_t)n);     // r32
   b += align256(sizeof(int32_t) * (size_t)n);   // cnt
+  b += align256(sizeof(int32_t) * (size_t)n);   // dpos
   b += scan_i32_ws_bytes(n) + 256;
   return b;
 }
@@ -218,6 +315,7 @@ extern "C" int gdd_normalize_csr(int64_t n, int64_t nnz, const int32_t* rowptr,
   double* r64 = cv.take<double>(n);
   float* r32 = cv.take<float>(n);
   int32_t* cnt = cv.take<int32_t>(n);
+  int32_t* dpos = cv.take<int32_t>(n);
   size_t scan_bytes = scan_i32_ws_bytes(n);
   void* scan_ws = cv.take<char>(scan_bytes);
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "normalize: workspace %zu too small", ws_bytes);
@@ -227,6 +325,13 @@ extern "C" int gdd_normalize_csr(int64_t n, int64_t nnz, const int32_t* rowptr,
   k_row_scale<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(n, rowptr, col, val, flag, r64, r32);
   GDD_LAUNCHED();
   const unsigned grid = (unsigned)((n * kGroup + 255) / 256);
+  const unsigned rgrid = (unsigned)((n + 255) / 256);
+  // binary input: the probe's flag picks the entry-parallel kernels (I added) or the general
+  // row-group kernels (no I); each set returns at once when the other applies
+  if (!val) {
+    k_fast_count<<<rgrid, 256, 0, s>>>(n, rowptr, col, flag, cnt, dpos);
+    GDD_LAUNCHED();
+  }
   k_rows_emit<false><<<grid, 256, 0, s>>>(n, rowptr, col, val, flag, r64, r32, cnt, nullptr,
                                           nullptr, nullptr);
   GDD_LAUNCHED();
@@ -234,6 +339,15 @@ extern "C" int gdd_normalize_csr(int64_t n, int64_t nnz, const int32_t* rowptr,
   if (rc) return rc;
   k_set_last<<<1, 64, 0, s>>>(n, cnt, rowptr_out);
   GDD_LAUNCHED();
+  if (!val) {
+    if (nnz > 0) {
+      k_fast_fill<<<(unsigned)((nnz + 255) / 256), 256, 0, s>>>(n, nnz, rowptr, col, flag, r64,
+                                                               dpos, rowptr_out, col_out, val_out);
+      GDD_LAUNCHED();
+    }
+    k_fast_diag<<<rgrid, 256, 0, s>>>(n, flag, r64, dpos, rowptr_out, col_out, val_out);
+    GDD_LAUNCHED();
+  }
   k_rows_emit<true><<<grid, 256, 0, s>>>(n, rowptr, col, val, flag, r64, r32, cnt, rowptr_out,
                                          col_out, val_out);
   GDD_LAUNCHED();
