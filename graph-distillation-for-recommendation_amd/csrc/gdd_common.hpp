@@ -82,6 +82,9 @@ int minibatch_step_dev(int64_t b, int dim, const float* X, const int64_t* rows, 
                        const float* C_old, float* C_new, float* weight_sums, int32_t* labels,
                        int step_i, int64_t n_samples, int max_no_improvement, int flags,
                        void* state, void* ws, size_t ws_bytes, const RngNext& rn, hipStream_t s);
+int mb_loop_begin(int64_t b, int k, void* ws, size_t ws_bytes, hipStream_t s);
+int mb_loop_end(int64_t b, int k, int last_step, int64_t n_samples, int max_no_improvement,
+                void* state, void* ws, size_t ws_bytes, hipStream_t s);
 int mb_rng_launch(const DevMT* in, DevMT* out, int64_t n, int64_t bs, int64_t* rows, hipStream_t s);
 int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const float* X,
                        const int64_t* rows, float* C_new, float* counts, void* step_ws,

@@ -13,7 +13,8 @@
 //   shuffle    RandomState.permutation(n) (legacy _shuffle_raw + random_interval): one lane walks
 //              the tempered words to get j_i for i = n-1..1; the first m entries of the permuted
 //              arange are then traced backwards through the swaps, one lane per entry
-// Requirements: blockDim.x is a multiple of 64 and >= 256; every thread of the block calls in.
+// Requirements: blockDim.x is a multiple of 64 and >= 256 (the twist's widest phase is 227 words;
+// randint walks the key block in windows of blockDim.x words); every thread of the block calls in.
 #pragma once
 
 #include <cstdint>
@@ -127,7 +128,7 @@ __device__ inline void mt_randint_block(MTScratch* s, int64_t low, int64_t high,
       __syncthreads();
     }
     const int pos = s->pos;
-    const int avail = 624 - pos;
+    const int avail = min(624 - pos, (int)blockDim.x);  // this pass's window of words
     uint32_t v = 0;
     bool ok = false;
     if (t < avail) {
@@ -144,7 +145,7 @@ __device__ inline void mt_randint_block(MTScratch* s, int64_t low, int64_t high,
       if (t == 0) s->pos = pos + s->last + 1;
       produced = count;
     } else {
-      if (t == 0) s->pos = 624;
+      if (t == 0) s->pos = pos + avail;
       produced += total;
     }
     __syncthreads();
@@ -155,10 +156,11 @@ __device__ inline void mt_randint_block(MTScratch* s, int64_t low, int64_t high,
 __device__ inline void mt_permutation_prefix_block(MTScratch* s, int64_t n, int m, int* J,
                                             int64_t* __restrict__ perm) {
   const int t = threadIdx.x;
-  // wave 0 walks the words 64 at a time; the block regenerates the key block when it runs dry.
-  // In a window of 64 words with i - 64 >= 1 and one mask for all of [i-64, i], word u is accepted
-  // iff v_u <= i - (accepted before u): v_u <= i - 63 is surely accepted, v_u > i surely rejected,
-  // and the few words in between are settled in order. Other windows go word by word on lane 0.
+  // wave 0 walks the words up to 64 at a time; the block regenerates the key block when it runs
+  // dry. In a window of wn words that cannot take i below the smallest value with the current
+  // mask, word u is accepted iff v_u <= i - (accepted before u): v_u <= i - (wn-1) is surely
+  // accepted, v_u > i surely rejected, and the few words in between are settled in order. At the
+  // bottom of a mask range (i a power of two) words go one by one until the first acceptance.
   if (t == 0) s->last = (int)n - 1;  // the next i to draw for
   __syncthreads();
   const int lane = t & 63;
@@ -172,13 +174,17 @@ __device__ inline void mt_permutation_prefix_block(MTScratch* s, int64_t n, int 
     if (t < 64) {
       int i = s->last, pos = s->pos;
       while (i >= 1 && pos < 624) {
-        const int navail = min(64, 624 - pos);
         const uint32_t mk = mask32((uint32_t)i);
-        const bool fast = navail == 64 && i - 64 >= 1 && mask32((uint32_t)(i - 64)) == mk;
-        if (fast) {
-          const uint32_t v = mt_temper(s->key[pos + lane]) & mk;
-          const unsigned long long sure = __ballot(v + 63u <= (uint32_t)i);
-          unsigned long long maybe = __ballot(v + 63u > (uint32_t)i && v <= (uint32_t)i);
+        const int m_lo = (int)((mk >> 1) + 1);  // smallest i drawn with this mask
+        // a window of wn words cannot accept more than wn, so i stays >= m_lo and the mask fixed
+        const int wn = min(64, min(624 - pos, i - m_lo));
+        if (wn >= 1) {
+          const bool valid = lane < wn;
+          const uint32_t v = valid ? (mt_temper(s->key[pos + lane]) & mk) : 0xffffffffu;
+          // lane u draws for i_u in [i - u, i]: v <= i - (wn - 1) accepts for sure, v > i never
+          const unsigned long long sure = __ballot(valid && v + (uint32_t)(wn - 1) <= (uint32_t)i);
+          unsigned long long maybe =
+              __ballot(valid && v + (uint32_t)(wn - 1) > (uint32_t)i && v <= (uint32_t)i);
           unsigned long long acc = sure;
           while (maybe) {
             const int u = __ffsll((long long)maybe) - 1;
@@ -189,18 +195,17 @@ __device__ inline void mt_permutation_prefix_block(MTScratch* s, int64_t n, int 
           }
           if ((acc >> lane) & 1ull) J[i - __popcll(acc & ((1ull << lane) - 1ull))] = (int)v;
           i -= __popcll(acc);
-          pos += 64;
+          pos += wn;
         } else {
+          // i == m_lo: word by word until one is accepted (the mask shrinks after it)
           int i0 = i, p0 = pos;
           if (lane == 0) {
-            uint32_t m0 = mk;
-            const int end = pos + navail;
-            while (i0 >= 1 && p0 < end) {
-              const uint32_t v = mt_temper(s->key[p0++]) & m0;
+            while (p0 < 624) {
+              const uint32_t v = mt_temper(s->key[p0++]) & mk;
               if (v <= (uint32_t)i0) {
                 J[i0] = (int)v;
                 --i0;
-                m0 = mask32((uint32_t)(i0 > 0 ? i0 : 1));
+                break;
               }
             }
           }

@@ -105,9 +105,9 @@ size_t fit_ws(void* base, size_t cap, int64_t n, int dim, int k, int64_t bs, int
 int local_trials(int k) { return 2 + (int)std::log((double)k); }
 
 // The step loop with every draw and decision on the device (see the dev_loop comment in the fit).
-// Per step s: the assignment launch (plus, unless s reassigns, a workgroup drawing batch s+1), the
-// update launch (with the batch inertia and the convergence test), and at scheduled reassignment
-// steps the reassignment launch (which then draws batch s+1). Chunks of kDevChunk steps are
+// Per step s: the assignment launch (plus a workgroup finishing step s-1 — its batch inertia and
+// convergence test — and, unless s reassigns, a workgroup drawing batch s+1), the update launch,
+// and at scheduled reassignment steps the reassignment launch (which then draws batch s+1). Chunks of kDevChunk steps are
 // enqueued back to back; the host reads the stop word of chunk c while chunk c+1 runs.
 constexpr int kDevChunk = 16;
 
@@ -122,6 +122,8 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n
   h_mt->pad = 0;
   GDD_HIP(hipMemcpyAsync(w.mtb + 2, h_mt, sizeof(DevMT), hipMemcpyHostToDevice, s));
   int rc = mb_rng_launch(w.mtb + 2, w.mtb + 0, n, bs, w.rows_d, s);
+  if (rc) return rc;
+  rc = mb_loop_begin(bs, k, w.step_ws, w.step_bytes, s);
   if (rc) return rc;
   const bool reassign = reassignment_ratio > 0.f;
   hipEvent_t ev[2];
@@ -166,6 +168,10 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n
         rc = mb_reassign_launch((int)st, bs, dim, k, reassignment_ratio, X, rows_cur, c_new, w.counts,
                                 w.step_ws, w.step_bytes, mt_cur, mt_cur, has_next ? next : none,
                                 w.state, s);
+        if (rc) return rc;
+      }
+      if (!has_next) {  // the last step's inertia and convergence test (otherwise in step st+1)
+        rc = mb_loop_end(bs, k, (int)st, n, max_no_improvement, w.state, w.step_ws, w.step_bytes, s);
         if (rc) return rc;
       }
     }

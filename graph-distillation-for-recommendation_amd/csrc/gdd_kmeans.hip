@@ -15,6 +15,7 @@
 // Loop control, RNG draws and rare branches (reassignment, relocation) live in the host layer.
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "gdd_common.hpp"
 #include "gdd_devrng.hpp"
@@ -528,14 +529,14 @@ __device__ void mb_converge(int step_i, int64_t bs, int64_t n, int max_no_improv
     __hip_atomic_store(&st->stop_at, step_i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// sequential fp32 inertia of one batch by a 64-lane block (staged in LDS 2048 at a time; lane 0
+// sequential fp32 inertia of one batch by one workgroup (staged in LDS 2048 at a time; lane 0
 // folds them in order reading 16 bytes per LDS access)
 __device__ float mb_batch_inertia(int64_t b, const float* __restrict__ sq, float* stage) {
   float acc = 0.f;
   for (int64_t base = 0; base < b; base += 2048) {
     const int m = (int)min<int64_t>(2048, b - base);
 #pragma unroll 8
-    for (int t = threadIdx.x; t < m; t += 64) stage[t] = sq[base + t] * 1.0f;
+    for (int t = threadIdx.x; t < m; t += blockDim.x) stage[t] = sq[base + t] * 1.0f;
     __syncthreads();
     if (threadIdx.x == 0) acc = fold_seq_lds(stage, m, acc);
     __syncthreads();
@@ -549,43 +550,170 @@ __global__ void k_mb_converge(int step_i, int64_t bs, int64_t n, int max_no_impr
   mb_converge(step_i, bs, n, max_no_improvement, batch_inertia[0], st);
 }
 
+// the end of a step: its batch inertia (sequential fp32 over the per-sample distances the update
+// left) and, with `converge`, the early-stopping test. Runs as its own launch (public step API)
+// or as an extra workgroup of the NEXT step's assignment launch (device loop), where it overlaps
+// that assignment: the next update is the first kernel that must see its stop decision.
+struct MbTail {
+  const float* sq;
+  float* inertia;
+  MBState* st;
+  int64_t b;
+  int64_t n_samples;
+  int max_ni;
+  int step;
+  int converge;
+  int active;
+};
+
+__device__ void mb_tail_block(const MbTail& tl, float* stage) {
+  const float inertia = mb_batch_inertia(tl.b, tl.sq, stage);
+  if (threadIdx.x == 0) {
+    tl.inertia[0] = inertia;
+    if (tl.converge) mb_converge(tl.step, tl.b, tl.n_samples, tl.max_ni, inertia, tl.st);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mb_tail(MbTail tl, const int32_t* __restrict__ stop) {
+  if (stopped(stop, tl.step)) return;
+  __shared__ __attribute__((aligned(16))) float stage[2048];
+  mb_tail_block(tl, stage);
+}
+
 // ---------------------------------------------------------------------------------------------
-// MiniBatchKMeans update (one wave per cluster; block k, when launched, is the step's tail:
-// batch inertia + convergence test). The member list and the members' source rows live in LDS
-// (dynamic: 12*b bytes). cn2_out (nullable) receives the numpy-order norm of the new centre,
-// i.e. the ||C||^2 the next step's assignment needs.
+// MiniBatchKMeans assignment spread over the chip: block (pb, g) takes batch points
+// [32pb, 32pb + 32) against centre tiles g*W .. g*W + W-1 (one 32-centre tile per wave), so every
+// CU runs about one MFMA chain per SIMD instead of one CU running all k/32 of them. The per-wave
+// minima merge in LDS and then across the G blocks of a point group with a 64-bit atomicMin on
+// the (distance, index) key (a plain store when G == 1); the update kernel reads the labels out of
+// the keys. Extra workgroups past the P*G assignment blocks run, in this order: the previous
+// step's tail (inertia + convergence, `tl.active`) and the next step's batch draw (`rn.rows`).
+// ---------------------------------------------------------------------------------------------
+__host__ __device__ inline size_t mb_assign_lds(int waves, int dim) {
+  const int dimp = (dim + 1) & ~1, S = dimp + 1;
+  return sizeof(float) * ((size_t)(32 + 32 * waves) * S + 32 * waves) + 16 +
+         sizeof(unsigned long long) * 32 * waves;
+}
+
+template <int W, bool VEC>
+__global__ __launch_bounds__(64 * W) void k_mb_assign(
+    int64_t n, int dim, int dimp, const float* __restrict__ X, const int64_t* __restrict__ rows,
+    int k, const float* __restrict__ C, const float* __restrict__ cn2,
+    unsigned long long* __restrict__ keys, int G, int P, const int32_t* __restrict__ stop,
+    int step_i, MbTail tl, RngNext rn) {
+  if (stopped(stop, step_i)) return;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int blk = blockIdx.x;
+  if (blk >= P * G) {
+    const int e = blk - P * G;
+    if (tl.active && e == 0) {
+      mb_tail_block(tl, lds);
+    } else if (rn.rows) {
+      MTScratch* ms = reinterpret_cast<MTScratch*>(lds);
+      mt_load(rn.in, ms);
+      mt_randint_block(ms, 0, rn.n, rn.bs, rn.rows);
+      mt_store(ms, rn.out);
+    }
+    return;
+  }
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 0);
+  const int pb = blk / G, g = blk - pb * G;
+  const int S = dimp + 1;
+  float* Pl = lds;                              // 32 points x S
+  float* Cl = Pl + 32 * S;                      // W centre tiles x 32 x S
+  float* Nl = Cl + (size_t)W * 32 * S;          // W x 32 norms
+  unsigned long long* Kl =
+      reinterpret_cast<unsigned long long*>(((uintptr_t)(Nl + 32 * W) + 15) & ~uintptr_t(15));
+  __shared__ int64_t s_rows[32];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t p0 = (int64_t)pb * 32;
+  const int np = (int)min<int64_t>(32, n - p0);
+  const int cb = (g * W + wave) * 32;  // this wave's tile
+  // trip 1: row indices and the centre tile, requested together
+  int64_t my_row = 0;
+  if (tid < 32 && tid < np) my_row = rows ? rows[p0 + tid] : p0 + tid;
+  float* Cw = Cl + (size_t)wave * 32 * S;
+  float* Nw = Nl + wave * 32;
+  if (cb < k) {
+    const float* Cb = C + (int64_t)cb * dim;
+    stage_rows32<VEC>(Cw, S, [&](int r) { return Cb + (int64_t)r * dim; }, k - cb, dim, dimp, lane,
+                      64);
+    if (cn2 && lane < 32) Nw[lane] = (cb + lane < k) ? cn2[cb + lane] : 0.f;
+  }
+  if (tid < 32) s_rows[tid] = my_row;
+  __syncthreads();
+  // trip 2: the point rows
+  stage_rows32<VEC, 4>(Pl, S, [&](int r) { return X + s_rows[r] * dim; }, np, dim, dimp, tid,
+                       64 * W);
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 3);
+  unsigned long long best = ~0ull;
+  if (cb < k) {
+    const int kh = lane >> 5;
+    if (!cn2 && lane < 32) Nw[lane] = (cb + lane < k) ? npy_sumsq(Cw + lane * S, dim) : 0.f;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const floatx16 acc = mfma_chain<16>(Cw + (lane & 31) * S + kh, Pl + (lane & 31) * S + kh, dimp);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ci = (r & 3) + 8 * (r >> 2) + 4 * kh;
+      if (cb + ci < k) {
+        const unsigned long long key = pack_key(__builtin_fmaf(-2.f, acc[r], Nw[ci]), cb + ci);
+        best = key < best ? key : best;
+      }
+    }
+  }
+  const unsigned long long other = __shfl_xor(best, 32);
+  best = other < best ? other : best;
+  if (lane < 32) Kl[wave * 32 + lane] = best;
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 13);
+  if (wave == 0 && lane < np) {
+    unsigned long long b = Kl[lane];
+#pragma unroll
+    for (int q = 1; q < W; ++q) {
+      const unsigned long long o = Kl[q * 32 + lane];
+      b = o < b ? o : b;
+    }
+    if (G == 1)
+      keys[p0 + lane] = b;
+    else
+      atomicMin(keys + p0 + lane, b);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// MiniBatchKMeans update, one wave per cluster. Membership comes from `labels` or, in the fused
+// step, from the assignment's 64-bit keys (label = low word), then:
+//   * labels_out (nullable): the batch labels; sq_out (nullable): each member's distance to its
+//     old centre in the _euclidean_dense_dense order (the step's inertia terms, _k_means_common.pyx
+//     :26-48 / :92-121) — computed here, where the member rows are gathered anyway;
+//   * keys_reset (nullable): the other key buffer is cleared for the next step's assignment.
+// The member list and the members' source rows live in LDS (dynamic: 12*b bytes). cn2_out
+// (nullable) receives the numpy-order norm of the new centre for the next step's assignment.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, const float* __restrict__ X,
                                                         const int64_t* __restrict__ rows,
                                                         const float* __restrict__ w,
-                                                        const int32_t* __restrict__ labels, int k,
-                                                        const float* __restrict__ C_old,
+                                                        const int32_t* __restrict__ labels,
+                                                        const unsigned long long* __restrict__ keys,
+                                                        int k, const float* __restrict__ C_old,
                                                         float* __restrict__ C_new,
                                                         float* __restrict__ Wsum,
                                                         float* __restrict__ cn2_out,
                                                         const int32_t* __restrict__ stop, int step_i,
-                                                        const float* __restrict__ sq,
-                                                        float* __restrict__ inertia_out,
-                                                        MBState* __restrict__ st, int converge,
-                                                        int64_t n_samples, int max_no_improvement) {
+                                                        int32_t* __restrict__ labels_out,
+                                                        float* __restrict__ sq_out,
+                                                        unsigned long long* __restrict__ keys_reset) {
   if (stopped(stop, step_i)) return;
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 20);
-  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0 && (int)blockIdx.x == k, 30);
   extern __shared__ __attribute__((aligned(16))) float mb_lds[];
   const int c = blockIdx.x;
   const int lane = threadIdx.x;
-  if (c == k) {
-    // tail block (launched only by the fused step): batch inertia, then the convergence test
-    const float inertia = mb_batch_inertia(b, sq, mb_lds);
-    GDD_STAMP_WHEN(g_stamps_kmeans, lane == 0, 31);
-    if (lane == 0) {
-      inertia_out[0] = inertia;
-      if (converge) mb_converge(step_i, b, n_samples, max_no_improvement, inertia, st);
-    }
-    GDD_STAMP_WHEN(g_stamps_kmeans, lane == 0, 32);
-    return;
-  }
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 21);
+  if (keys_reset)
+    for (int64_t i = (int64_t)c * 64 + lane; i < b; i += (int64_t)gridDim.x * 64) keys_reset[i] = ~0ull;
   int64_t* src = reinterpret_cast<int64_t*>(mb_lds);      // b source rows
   int32_t* mem = reinterpret_cast<int32_t*>(src + b);     // b member positions
   int count = 0;
@@ -595,7 +723,7 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int64_t i = base + u * 64 + lane;
-      lab[u] = i < b ? labels[i] : -1;
+      lab[u] = i < b ? (keys ? (int32_t)(unsigned)(keys[i] & 0xffffffffull) : labels[i]) : -1;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -611,6 +739,13 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
   for (int t = lane; t < count; t += 64) src[t] = rows ? rows[mem[t]] : (int64_t)mem[t];
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 23);
+  if (labels_out || sq_out) {  // per member: its label and its distance to the old centre
+    const float* crow = C_old + (int64_t)c * dim;
+    for (int t = lane; t < count; t += 64) {
+      if (labels_out) labels_out[mem[t]] = c;
+      if (sq_out) sq_out[mem[t]] = skl_sqdist(X + src[t] * dim, crow, dim);
+    }
+  }
   // wsum: sequential fp32 in batch order (update_center_dense :78-83); unit weights sum exactly
   float wsum = 0.f;
   if (w) {
@@ -976,26 +1111,67 @@ namespace {
 constexpr int64_t kMaxBatch = 13312;  // 12*b bytes of LDS per update block (<= 156 KiB)
 
 size_t update_lds(int64_t b) {
-  // src rows (8b) + member positions (4b) + the new centre row (<= 512 floats); the tail block
-  // reuses the region as its 2048-float inertia stage
-  return std::max<size_t>(12 * (size_t)b + 512 * sizeof(float), 2048 * sizeof(float));
+  // src rows (8b) + member positions (4b) + the new centre row (<= 512 floats)
+  return 12 * (size_t)b + 512 * sizeof(float);
 }
 
-int launch_update(int grid, int64_t b, int dim, const float* X, const int64_t* rows, const float* w,
-                  const int32_t* labels, int k, const float* C_old, float* C_new, float* Wsum,
-                  float* cn2_out, const int32_t* stop, int step_i, const float* sq, float* inertia,
-                  MBState* st, int converge, int64_t n_samples, int max_ni, hipStream_t s) {
+int launch_update(int64_t b, int dim, const float* X, const int64_t* rows, const float* w,
+                  const int32_t* labels, const unsigned long long* keys, int k, const float* C_old,
+                  float* C_new, float* Wsum, float* cn2_out, const int32_t* stop, int step_i,
+                  int32_t* labels_out, float* sq_out, unsigned long long* keys_reset,
+                  hipStream_t s) {
   GDD_REQUIRE(b <= kMaxBatch, "minibatch: batch %lld exceeds %lld", (long long)b,
               (long long)kMaxBatch);
   const size_t lds = update_lds(b);
   if (lds > 65536)
     GDD_HIP(hipFuncSetAttribute((const void*)k_minibatch_update,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  k_minibatch_update<<<grid, 64, lds, s>>>(b, dim, X, rows, w, labels, k, C_old, C_new, Wsum,
-                                           cn2_out, stop, step_i, sq, inertia, st, converge,
-                                           n_samples, max_ni);
+  k_minibatch_update<<<k, 64, lds, s>>>(b, dim, X, rows, w, labels, keys, k, C_old, C_new, Wsum,
+                                        cn2_out, stop, step_i, labels_out, sq_out, keys_reset);
   GDD_LAUNCHED();
   return GDD_OK;
+}
+
+template <int W, bool VEC>
+int launch_mb_assign_t(int64_t b, int dim, const float* X, const int64_t* rows, int k,
+                       const float* C, const float* cn2, unsigned long long* keys,
+                       const int32_t* stop, int step_i, const MbTail& tl, const RngNext& rn,
+                       hipStream_t s) {
+  const int dimp = (dim + 1) & ~1;
+  const int tiles = (k + 31) / 32;
+  const int G = (tiles + W - 1) / W;
+  const int P = (int)((b + 31) / 32);
+  const size_t lds = std::max({mb_assign_lds(W, dim), sizeof(float) * 2048 + 16,
+                               sizeof(MTScratch) + 64});
+  if (lds > 65536)
+    GDD_HIP(hipFuncSetAttribute((const void*)k_mb_assign<W, VEC>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const unsigned grid = (unsigned)(P * G) + (tl.active ? 1u : 0u) + (rn.rows ? 1u : 0u);
+  k_mb_assign<W, VEC><<<grid, 64 * W, lds, s>>>(b, dim, dimp, X, rows, k, C, cn2, keys, G, P, stop,
+                                                step_i, tl, rn);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+template <bool VEC>
+int launch_mb_assign_v(int64_t b, int dim, const float* X, const int64_t* rows, int k,
+                       const float* C, const float* cn2, unsigned long long* keys,
+                       const int32_t* stop, int step_i, const MbTail& tl, const RngNext& rn,
+                       hipStream_t s) {
+  if (mb_assign_lds(4, dim) <= 96 * 1024)
+    return launch_mb_assign_t<4, VEC>(b, dim, X, rows, k, C, cn2, keys, stop, step_i, tl, rn, s);
+  if (mb_assign_lds(2, dim) <= kLdsCap)
+    return launch_mb_assign_t<2, VEC>(b, dim, X, rows, k, C, cn2, keys, stop, step_i, tl, rn, s);
+  return launch_mb_assign_t<1, VEC>(b, dim, X, rows, k, C, cn2, keys, stop, step_i, tl, rn, s);
+}
+
+int launch_mb_assign(int64_t b, int dim, const float* X, const int64_t* rows, int k, const float* C,
+                     const float* cn2, unsigned long long* keys, const int32_t* stop, int step_i,
+                     const MbTail& tl, const RngNext& rn, hipStream_t s) {
+  const bool vec = (dim % 4 == 0) &&
+                   ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(C)) & 15) == 0;
+  return vec ? launch_mb_assign_v<true>(b, dim, X, rows, k, C, cn2, keys, stop, step_i, tl, rn, s)
+             : launch_mb_assign_v<false>(b, dim, X, rows, k, C, cn2, keys, stop, step_i, tl, rn, s);
 }
 }  // namespace
 
@@ -1008,24 +1184,28 @@ extern "C" int gdd_minibatch_update(int64_t b, int dim, const float* X, const in
   GDD_REQUIRE(C_old != C_new, "minibatch_update: C_old and C_new must differ");
   (void)ws;
   (void)ws_bytes;
-  return launch_update(k, b, dim, X, rows, w, labels, k, C_old, C_new, weight_sums, nullptr,
-                       nullptr, 0, nullptr, nullptr, nullptr, 0, 1, -1, to_hip(stream));
+  return launch_update(b, dim, X, rows, w, labels, nullptr, k, C_old, C_new, weight_sums, nullptr,
+                       nullptr, 0, nullptr, nullptr, nullptr, to_hip(stream));
 }
 
 // ---- fused MiniBatchKMeans step (_mini_batch_step + _mini_batch_convergence) ------------------
+// Step s uses key buffer and distance buffer s % 2: the assignment writes keys[s%2], the update
+// reads them (and clears keys[(s+1)%2] for step s+1) and writes sq[s%2], the tail folds sq[s%2].
 namespace {
 struct StepWs {
-  unsigned long long* keys;
+  unsigned long long* keys[2];
   float* cn2;
-  float* sq;
+  float* sq[2];
   float* inertia;
 };
 StepWs carve_step(void* ws, size_t ws_bytes, int64_t b, int k) {
   Carver cv(ws, ws_bytes);
   StepWs w;
-  w.keys = cv.take<unsigned long long>(b);
+  w.keys[0] = cv.take<unsigned long long>(b);
+  w.keys[1] = cv.take<unsigned long long>(b);
   w.cn2 = cv.take<float>(k);
-  w.sq = cv.take<float>(b);
+  w.sq[0] = cv.take<float>(b);
+  w.sq[1] = cv.take<float>(b);
   w.inertia = cv.take<float>(1);
   return w;
 }
@@ -1034,8 +1214,9 @@ StepWs carve_step(void* ws, size_t ws_bytes, int64_t b, int k) {
 extern "C" size_t gdd_minibatch_state_bytes(void) { return sizeof(MBState); }
 
 extern "C" size_t gdd_minibatch_step_ws_bytes(int64_t b, int k) {
-  return gdd_kmeans_assign_ws_bytes(b) + align256(sizeof(float) * (size_t)std::max(k, 1)) +
-         align256(sizeof(float) * (size_t)std::max<int64_t>(b, 1)) + align256(sizeof(float)) + 1024;
+  const size_t bb = (size_t)std::max<int64_t>(b, 1);
+  return 2 * align256(sizeof(unsigned long long) * bb) + align256(sizeof(float) * (size_t)std::max(k, 1)) +
+         2 * align256(sizeof(float) * bb) + align256(sizeof(float)) + 1024;
 }
 
 extern "C" int gdd_minibatch_step(int64_t b, int dim, const float* X, const int64_t* rows, int k,
@@ -1043,11 +1224,36 @@ extern "C" int gdd_minibatch_step(int64_t b, int dim, const float* X, const int6
                                   int32_t* labels, int step_i, int64_t n_samples,
                                   int max_no_improvement, int flags, void* state, void* ws,
                                   size_t ws_bytes, gdd_stream_t stream) {
-  return gdd::minibatch_step_dev(b, dim, X, rows, k, C_old, C_new, weight_sums, labels, step_i,
-                                 n_samples, max_no_improvement, flags, state, ws, ws_bytes,
-                                 RngNext{nullptr, nullptr, nullptr, 0, 0}, to_hip(stream));
+  GDD_REQUIRE(b > 0 && dim > 0 && dim <= 512 && k > 0 && n_samples > 0, "minibatch_step: bad shape");
+  GDD_REQUIRE(X && rows && C_old && C_new && weight_sums && labels && state && ws,
+              "minibatch_step: null pointer");
+  GDD_REQUIRE(C_old != C_new, "minibatch_step: C_old and C_new must differ");
+  if (ws_bytes < gdd_minibatch_step_ws_bytes(b, k))
+    return fail(GDD_E_WORKSPACE, "minibatch_step: workspace too small");
+  hipStream_t s = to_hip(stream);
+  MBState* st = static_cast<MBState*>(state);
+  const int32_t* stop = &st->stop_at;
+  StepWs w = carve_step(ws, ws_bytes, b, k);
+  const int cur = step_i & 1;
+  k_fill_u64<<<blocks_for(b), 256, 0, s>>>(b, w.keys[cur], ~0ull, stop, step_i);
+  GDD_LAUNCHED();
+  const float* cn2 = (flags & GDD_STEP_NORMS_VALID) ? w.cn2 : nullptr;
+  const MbTail none{nullptr, nullptr, nullptr, 0, 0, 0, 0, 0, 0};
+  int rc = launch_mb_assign(b, dim, X, rows, k, C_old, cn2, w.keys[cur], stop, step_i, none,
+                            RngNext{nullptr, nullptr, nullptr, 0, 0}, s);
+  if (rc) return rc;
+  rc = launch_update(b, dim, X, rows, nullptr, nullptr, w.keys[cur], k, C_old, C_new, weight_sums,
+                     w.cn2, stop, step_i, labels, w.sq[cur], nullptr, s);
+  if (rc) return rc;
+  const MbTail tl{w.sq[cur], w.inertia, st, b, n_samples, max_no_improvement, step_i,
+                  (flags & GDD_STEP_CONVERGE) ? 1 : 0, 1};
+  k_mb_tail<<<1, 256, 0, s>>>(tl, stop);
+  GDD_LAUNCHED();
+  return GDD_OK;
 }
 
+// device loop, step s: the assignment launch also folds step s-1's inertia and runs its
+// convergence test (tail) and, with rn, draws batch s+1; the update clears the other key buffer
 int gdd::minibatch_step_dev(int64_t b, int dim, const float* X, const int64_t* rows, int k,
                             const float* C_old, float* C_new, float* weight_sums, int32_t* labels,
                             int step_i, int64_t n_samples, int max_no_improvement, int flags,
@@ -1062,22 +1268,35 @@ int gdd::minibatch_step_dev(int64_t b, int dim, const float* X, const int64_t* r
   MBState* st = static_cast<MBState*>(state);
   const int32_t* stop = &st->stop_at;
   StepWs w = carve_step(ws, ws_bytes, b, k);
-  const bool norms_valid = (flags & GDD_STEP_NORMS_VALID) != 0;
-  const float* cn2 = w.cn2;
-  if (!norms_valid) {
-    if (use_small_assign(b, dim)) {
-      cn2 = nullptr;  // the fused kernel computes them from its LDS tiles
-    } else {
-      k_row_norms<<<blocks_for(k), 256, 0, s>>>(k, dim, C_old, w.cn2, stop, step_i);
-      GDD_LAUNCHED();
-    }
-  }
-  int rc = launch_assign(b, dim, X, rows, k, C_old, cn2, labels, w.sq, w.keys, stop, step_i, s, rn);
+  const int cur = step_i & 1, prev = cur ^ 1;
+  const float* cn2 = (flags & GDD_STEP_NORMS_VALID) ? w.cn2 : nullptr;
+  const MbTail tl{w.sq[prev], w.inertia, st, b, n_samples, max_no_improvement, step_i - 1,
+                  (flags & GDD_STEP_CONVERGE) ? 1 : 0, step_i > 0 ? 1 : 0};
+  int rc = launch_mb_assign(b, dim, X, rows, k, C_old, cn2, w.keys[cur], stop, step_i, tl, rn, s);
   if (rc) return rc;
-  // k update blocks (+ ||C_new||^2 for the next step) and one tail block (inertia, convergence)
-  return launch_update(k + 1, b, dim, X, rows, nullptr, labels, k, C_old, C_new, weight_sums, w.cn2,
-                       stop, step_i, w.sq, w.inertia, st, flags & GDD_STEP_CONVERGE, n_samples,
-                       max_no_improvement, s);
+  return launch_update(b, dim, X, rows, nullptr, nullptr, w.keys[cur], k, C_old, C_new,
+                       weight_sums, w.cn2, stop, step_i, labels, w.sq[cur], w.keys[prev], s);
+}
+
+// device loop: clear both key buffers before step 0; after the last step, its tail
+int gdd::mb_loop_begin(int64_t b, int k, void* ws, size_t ws_bytes, hipStream_t s) {
+  StepWs w = carve_step(ws, ws_bytes, b, k);
+  for (int q = 0; q < 2; ++q) {
+    k_fill_u64<<<blocks_for(b), 256, 0, s>>>(b, w.keys[q], ~0ull, nullptr, 0);
+    GDD_LAUNCHED();
+  }
+  return GDD_OK;
+}
+
+int gdd::mb_loop_end(int64_t b, int k, int last_step, int64_t n_samples, int max_no_improvement,
+                     void* state, void* ws, size_t ws_bytes, hipStream_t s) {
+  StepWs w = carve_step(ws, ws_bytes, b, k);
+  MBState* st = static_cast<MBState*>(state);
+  const MbTail tl{w.sq[last_step & 1], w.inertia, st, b, n_samples, max_no_improvement, last_step,
+                  1, 1};
+  k_mb_tail<<<1, 256, 0, s>>>(tl, &st->stop_at);
+  GDD_LAUNCHED();
+  return GDD_OK;
 }
 
 extern "C" int gdd_minibatch_converge(int64_t b, int k, int step_i, int64_t n_samples,
