@@ -12,6 +12,7 @@
 // tail(0) seeds the loop from the first centre (random_state.choice on the host). `closest` is
 // never copied: round c reads dist[(c-1)&1][best_{c-1}].
 #include <algorithm>
+#include <cstdlib>
 
 #include "gdd_common.hpp"
 
@@ -473,6 +474,216 @@ __global__ __launch_bounds__(kTailThreads) void k_kpp_tail_fast(
   GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 6 + 10 * (c & 1));
 }
 
+// ---- all rounds in one launch ------------------------------------------------------------------
+// The same two phases per round, inside one persistent launch of G*T workgroups (<= 256, one per
+// CU, so all are resident): every workgroup runs its slice of the distance phase, releases its
+// writes and arrives on a counter; the last arriver runs the tail (potentials, argmin, cumulative
+// potential, next candidates) and publishes the next round number; the others wait for it. This
+// removes two launch ramps and a dependent kernel boundary per round, but each round then pays two
+// agent-scope fences per workgroup; see the launcher for the measurement. Every wait is bounded:
+// a workgroup that waits too long sets `err` and leaves.
+struct KppSync {
+  unsigned int arrive;  // arrivals so far (NB per round)
+  unsigned int round;   // candidates published for this round
+  unsigned int err;
+  unsigned int pad;
+};
+
+__device__ __forceinline__ bool kpp_wait_round(KppSync* sy, unsigned c) {
+  unsigned long long spins = 0;
+  while (__hip_atomic_load(&sy->round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1ull << 22)) return false;
+  }
+  return true;
+}
+
+// distance phase of workgroup (g, t): as k_kpp_dist with the chain distances in LDS
+__device__ void kpp_dist_phase(int64_t n, int dim, const float* __restrict__ X,
+                               const float* __restrict__ w, const double* __restrict__ xsq,
+                               const float* __restrict__ closest0, const float* __restrict__ dist_prev,
+                               const KppState* __restrict__ st, float* __restrict__ dist,
+                               float* __restrict__ acc, int L, int t, int g, double* s_c) {
+  const int tid = threadIdx.x;
+  const int64_t J = n >> 6, n64 = J << 6;
+  const int64_t nloc = (int64_t)L * J;
+  const int64_t ntot = nloc + (g == 0 ? n - n64 : 0);
+  const int best = st->best;
+  const int64_t ct = st->cand[t];
+  const double cn = xsq[ct];
+  const float* closest = best < 0 ? closest0 : dist_prev + (int64_t)best * n;
+  for (int j = tid; j < dim; j += blockDim.x) s_c[j] = (double)X[ct * dim + j];
+  __syncthreads();
+  float* sd = reinterpret_cast<float*>(s_c + dim);
+  float* drow = dist + (int64_t)t * n;
+  for (int64_t q = tid; q < ntot; q += blockDim.x) {
+    int64_t i;
+    if (q < nloc) {
+      const int64_t j = q / L;
+      i = (int64_t)g * L + (q - j * L) + 64 * j;
+    } else {
+      i = n64 + (q - nloc);
+    }
+    const float* xi = X + i * dim;
+    const double xs = xsq[i];
+    const float cl = closest[i];
+    double dot = 0.0;
+    int j = 0;
+    for (; j + 8 <= dim; j += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = xi[j + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) dot = __builtin_fma(s_c[j + u], (double)v[u], dot);
+    }
+    for (; j < dim; ++j) dot = __builtin_fma(s_c[j], (double)xi[j], dot);
+    const double d = ((-2.0 * dot) + cn) + xs;
+    float f = (float)d;
+    f = f < 0.f ? 0.f : f;
+    f = np_minimum(cl, f);
+    drow[i] = f;
+    if (q < nloc) sd[q] = f;
+  }
+  __syncthreads();
+  if (tid < L) {
+    const int l = g * L + tid;
+    float a = 0.f;
+    int64_t j = 0;
+    for (; j + 8 <= J; j += 8) {
+      float xv[8], yv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        xv[u] = sd[(j + u) * L + tid];
+        yv[u] = w ? w[l + 64 * (j + u)] : 1.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a = __builtin_fmaf(xv[u], yv[u], a);
+    }
+    for (; j < J; ++j) a = __builtin_fmaf(sd[j * L + tid], w ? w[l + 64 * j] : 1.0f, a);
+    acc[t * 64 + l] = a;
+  }
+}
+
+// tail phase by one 256-thread workgroup (each thread owns <= kR consecutive points of a row)
+template <int kR>
+__device__ void kpp_tail_phase(int64_t n, int dim, const float* __restrict__ X,
+                               const float* __restrict__ w, const float* __restrict__ dist,
+                               const float* __restrict__ acc, int T, int c, int k,
+                               const double* __restrict__ uniforms, float* __restrict__ centers,
+                               int64_t* __restrict__ indices, KppState* __restrict__ st,
+                               float* s_pot, double* s_r, double* s_part, int* s_cnt) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6;
+  const bool more = c + 1 < k;
+  const double u_mine = (tid < T && more) ? uniforms[(int64_t)c * T + tid] : 0.0;
+  for (int tr = wave; tr < T; tr += nw) {
+    const int64_t ri = (n & ~63ll) + lane;
+    const float rx = ri < n ? dist[(int64_t)tr * n + ri] : 0.f;
+    const float ry = ri < n ? (w ? w[ri] : 1.0f) : 0.f;
+    const float p = sdot_skx_finish_shfl(acc[tr * 64 + lane], rx, ry, n);
+    if (lane == 0) s_pot[tr] = p;
+  }
+  __syncthreads();
+  int b = 0;  // np.argmin: first minimum; a NaN is returned as soon as it is met
+  for (int t = 1; t < T; ++t) {
+    const float pb = s_pot[b], pt = s_pot[t];
+    if (pb == pb && (pt < pb || pt != pt)) b = t;
+  }
+  const float pot = s_pot[b];
+  const int64_t src = st->cand[b];
+  for (int j = tid; j < dim; j += blockDim.x) centers[(int64_t)c * dim + j] = X[src * dim + j];
+  if (tid == 0) indices[c] = src;
+  if (!more) return;
+  if (tid < T) s_r[tid] = u_mine * (double)pot;
+  const int64_t chunk = (n + blockDim.x - 1) / blockDim.x;
+  const int64_t lo = min<int64_t>(n, tid * chunk), hi = min<int64_t>(n, lo + chunk);
+  const float* row = dist + (int64_t)b * n;
+  float pr[kR];
+#pragma unroll
+  for (int u = 0; u < kR; ++u) pr[u] = (lo + u < hi) ? (w ? w[lo + u] : 1.0f) * row[lo + u] : 0.f;
+  double run = 0.0;
+#pragma unroll
+  for (int u = 0; u < kR; ++u)
+    if (lo + u < hi) run = run + (double)pr[u];
+  double incl = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) s_part[wave] = incl;
+  __syncthreads();  // s_part, s_r; also every thread has read st->cand[b]
+  double base = incl - run;
+  for (int q = 0; q < wave; ++q) base += s_part[q];
+  double cu[kR];
+#pragma unroll
+  for (int u = 0; u < kR; ++u) {
+    base = base + (double)pr[u];
+    cu[u] = base;
+  }
+  for (int t = 0; t < T; ++t) {
+    const double r = s_r[t];
+    int cw = 0;
+#pragma unroll
+    for (int u = 0; u < kR; ++u) cw += __popcll(__ballot(lo + u < hi && cu[u] < r));
+    if (lane == 0) s_cnt[t * 4 + wave] = cw;
+  }
+  __syncthreads();
+  if (tid < T) {
+    int64_t a = 0;
+    for (int q = 0; q < nw; ++q) a += s_cnt[tid * 4 + q];
+    if (a > n - 1) a = n - 1;
+    st->cand[tid] = a;
+  }
+  if (tid == 0) {
+    st->best = b;
+    st->pot = pot;
+  }
+}
+
+template <int kR>
+__global__ __launch_bounds__(256) void k_kpp_rounds(
+    int64_t n, int dim, const float* __restrict__ X, const float* __restrict__ w,
+    const double* __restrict__ xsq, const float* __restrict__ closest0, float* __restrict__ dist0,
+    float* __restrict__ dist1, float* __restrict__ acc, int L, int G, int T, int k,
+    const double* __restrict__ uniforms, float* __restrict__ centers, int64_t* __restrict__ indices,
+    KppState* __restrict__ st, KppSync* __restrict__ sy) {
+  extern __shared__ double s_c[];
+  __shared__ float s_pot[kMaxTrials];
+  __shared__ double s_r[kMaxTrials];
+  __shared__ double s_part[4];
+  __shared__ int s_cnt[kMaxTrials * 4];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x;
+  const int t = blockIdx.x / G, g = blockIdx.x - t * G;
+  const unsigned NB = gridDim.x;
+  for (int c = 1; c < k; ++c) {
+    if (c > 1) {
+      if (tid == 0) s_flag = kpp_wait_round(sy, (unsigned)c) ? 1 : 0;
+      __syncthreads();
+      if (!s_flag) {
+        if (tid == 0) atomicOr(&sy->err, 1u);
+        return;
+      }
+      __threadfence();  // acquire: the published candidates and the previous distance rows
+    }
+    const float* prev = ((c - 1) & 1) ? dist1 : dist0;
+    float* cur = (c & 1) ? dist1 : dist0;
+    kpp_dist_phase(n, dim, X, w, xsq, closest0, prev, st, cur, acc, L, t, g, s_c);
+    __threadfence();  // release this workgroup's distances and chain accumulators
+    __syncthreads();
+    if (tid == 0) s_flag = (atomicAdd(&sy->arrive, 1u) == (unsigned)c * NB - 1u) ? 1 : 0;
+    __syncthreads();
+    if (!s_flag) continue;
+    __threadfence();  // acquire every workgroup's writes of this round
+    kpp_tail_phase<kR>(n, dim, X, w, cur, acc, T, c, k, uniforms, centers, indices, st, s_pot, s_r,
+                       s_part, s_cnt);
+    __threadfence();  // release the next round's candidates
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(&sy->round, (unsigned)(c + 1), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __global__ void k_ones(int64_t n, float* p) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = 1.0f;
@@ -491,6 +702,7 @@ extern "C" size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int n_trials) {
   b += 2 * align256(sizeof(float) * n * (size_t)std::max(n_trials, 1));     // dist ping-pong
   b += align256(sizeof(double) * n);                                        // cum
   b += align256(sizeof(float) * 64 * (size_t)std::max(n_trials, 1));       // lane accumulators
+  b += align256(sizeof(KppSync));
   return b + 2048;
 }
 
@@ -513,6 +725,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   float* dist[2] = {cv.take<float>(n * (size_t)n_trials), cv.take<float>(n * (size_t)n_trials)};
   double* cum = cv.take<double>(n);
   float* acc = cv.take<float>(64 * (size_t)n_trials);
+  KppSync* sy = cv.take<KppSync>(1);
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans++: workspace too small");
   const unsigned nb = (unsigned)((n + 255) / 256);
   // w == nullptr: unit sample weights, handled in the kernels
@@ -533,6 +746,22 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   if (lds > 65536)
     GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dist<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  // all rounds in one persistent launch (opt-in, GDD_KPP_PERSISTENT=1): measured 31 us per round
+  // at the arxiv shape against 13 us for the two launches below — the agent-scope fences each
+  // workgroup needs per round (L2 write-back + invalidate on gfx950) cost more than the launch
+  // boundaries they replace. Kept for the handoff work that would make it pay (sc1 granules).
+  const int NB = G * n_trials;
+  if (k > 1 && NB <= 256 && chain_in_lds && (n + 255) / 256 <= 16 &&
+      getenv("GDD_KPP_PERSISTENT") != nullptr) {
+    GDD_HIP(hipMemsetAsync(sy, 0, sizeof(KppSync), s));
+    if (lds > 65536)
+      GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_rounds<16>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    k_kpp_rounds<16><<<NB, 256, lds, s>>>(n, dim, X, w, xsq, closest0, dist[0], dist[1], acc, L, G,
+                                          n_trials, k, uniforms, centers, indices, st, sy);
+    GDD_LAUNCHED();
+    return GDD_OK;
+  }
   constexpr int kFastT = 12, kFastR = 4;
   const bool fast_tail = n_trials <= kFastT && (n + kTailThreads - 1) / kTailThreads <= kFastR;
   for (int c = 1; c < k; ++c) {
