@@ -6,10 +6,13 @@ the reference file:line each entry point replaces):
 * :func:`gdd.graph.to_csr`, :func:`gdd.graph.normalize_adj_tensor`, :func:`gdd.graph.propagate`
 * :class:`gdd.kmeans.KMeans`, :class:`gdd.kmeans.MiniBatchKMeans`
 * :func:`gdd.cluster.cluster_mean`, :func:`gdd.cluster.argmax_rows`
+* :mod:`gdd.pipeline` — ``pretrained_clustering_hot_path`` (the ClustGDD stage end to end),
+  ``kmeans_cluster`` / ``teacher_means`` / ``standard_scaler`` (distill_recsys)
 * :class:`gdd.sharded.ShardedKMeans` — Lloyd over range-partitioned rows on several ranks, one
   fixed-point all-reduce per iteration (rank-count invariant)
 """
 from . import _lib  # noqa: F401  (imports torch first, see _lib docstring)
+from . import pipeline  # noqa: F401
 from .cluster import argmax_rows, cluster_mean, group_by_label
 from .graph import CSRGraph, normalize_adj, normalize_adj_tensor, propagate, spmm, to_csr
 from .kmeans import KMeans, MiniBatchKMeans

@@ -75,6 +75,7 @@ SIGNATURES = {
     "gdd_kmeans_plusplus_ws_bytes": (_c_size, [_c_i64, _c_int]),
     "gdd_kmeans_plusplus": (_c_int, [_c_i64, _c_int, _vp, _vp, _c_int, _c_int, _c_i64, _vp, _vp,
                                      _vp, _vp, _c_size, _vp]),
+    "gdd_standard_scaler": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "gdd_cluster_mean": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _c_int, _c_int, _vp, _vp, _vp]),
     "gdd_argmax_rows": (_c_int, [_c_int, _c_int, _vp, _vp, _vp]),
 }

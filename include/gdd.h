@@ -230,6 +230,16 @@ int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const float* w, int 
                         void* ws, size_t ws_bytes, gdd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------- */
+/* (a8) StandardScaler(with_mean=True, with_std=True).fit_transform(X) on fp32 X                    */
+/* Replaces the scaling step of distill_recsys.kmeans_cluster (distill_recsys.py:172), scikit-learn  */
+/* 1.7.2 semantics (preprocessing/_data.py partial_fit/transform, utils/extmath.py                  */
+/* _incremental_mean_and_var): fp64 column sums in row order, corrected two-pass variance,          */
+/* near-constant columns scaled by 1, X_out = fp32(fp32(x - mean) / scale). mean/scale: dim doubles. */
+/* ---------------------------------------------------------------------------------------------- */
+int gdd_standard_scaler(int64_t n, int dim, const float* X, float* X_out, double* mean,
+                        double* scale, gdd_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------- */
 /* (a7) cluster-feature mean. Replaces clustgdd_agent_transduct.py:116-127 (induct :143-154) and the  */
 /* teacher index_add_/bincount means of distill_recsys.py:623-636.                                   */
 /* feat_syn[c,:] = fp32( (sequential fp64 sum over members of c in sample order) / count_c );         */

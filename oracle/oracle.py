@@ -398,3 +398,30 @@ def cluster_features(target_feat, logits, n_syn: int, dataset: str, seed: int,
     feat_syn, _ = cluster_mean(target_feat, labels, n_syn)
     labels_syn = np.argmax(res["cluster_centers_"], axis=-1)
     return feat_syn, labels_syn, labels.astype(np.int32), res
+
+
+# ------------------------------------------------------------------------------------------------
+# StandardScaler().fit_transform (sklearn/preprocessing/_data.py, utils/extmath.py
+# _incremental_mean_and_var, first call): distill_recsys.py:172
+# ------------------------------------------------------------------------------------------------
+def standard_scaler(X):
+    """(X_scaled fp32, mean fp64, scale fp64) with fp64 column sums accumulated row by row."""
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    n = X.shape[0]
+    s = np.zeros(X.shape[1], np.float64)
+    for i in range(n):
+        s = s + X[i].astype(np.float64)
+    mean = s / n
+    corr = np.zeros_like(s)
+    ssq = np.zeros_like(s)
+    for i in range(n):
+        t = X[i].astype(np.float64) - mean
+        corr = corr + t
+        ssq = ssq + t * t
+    var = (ssq - (corr * corr) / n) / n
+    eps = np.finfo(np.float64).eps
+    constant = var <= (n * eps) * var + ((n * mean) * eps) ** 2
+    scale = np.where(constant, 1.0, np.sqrt(var))
+    c = (X.astype(np.float64) - mean).astype(np.float32)
+    out = (c.astype(np.float64) / scale).astype(np.float32)
+    return out, mean, scale

@@ -103,3 +103,23 @@ def test_pretrained_clustering_vs_reference(tag):
     np.testing.assert_allclose(feat_syn.cpu().numpy(), z["feat_syn"], rtol=MEAN_RTOL, atol=MEAN_ATOL)
     labels_syn = gdd.argmax_rows(km.cluster_centers_device_)
     assert np.array_equal(labels_syn.cpu().numpy(), z["labels_syn"])
+
+
+def test_recsys_kmeans_cluster_device_scaler():
+    # distill_recsys.kmeans_cluster end to end on the device (StandardScaler included)
+    from gdd import pipeline
+    z = load("golden_kmeans.npz")
+    lab, cen = pipeline.kmeans_cluster(z["rs_X"], n_clusters=200, seed=42, minibatch=False)
+    assert np.array_equal(lab, z["rs_labels"])
+    assert np.array_equal(bits(cen), bits(z["rs_centers"]))
+
+
+def test_standard_scaler_vs_oracle():
+    from oracle import oracle as O
+    from gdd import pipeline
+    X = (np.random.default_rng(6).standard_normal((17730, 64)) * 2 - 1).astype(np.float32)
+    X[:, 5] = 3.0  # a constant column: scale 1
+    out, mean, scale = pipeline.standard_scaler(X)
+    ref, m_ref, s_ref = O.standard_scaler(X)
+    assert np.array_equal(bits(out.cpu().numpy()), bits(ref))
+    assert np.array_equal(mean.cpu().numpy(), m_ref) and np.array_equal(scale.cpu().numpy(), s_ref)

@@ -101,3 +101,16 @@ def test_pretrained_clustering_vs_reference(tag):
     feat_syn, _ = O.cluster_mean(z["target_feat"], res["labels_"], k)
     np.testing.assert_allclose(feat_syn, z["feat_syn"], rtol=MEAN_RTOL, atol=MEAN_ATOL)
     assert np.array_equal(np.argmax(res["cluster_centers_"], axis=-1), z["labels_syn"])
+
+
+def test_standard_scaler_vs_sklearn():
+    # the oracle's row-ordered fp64 restatement equals scikit-learn's StandardScaler bit for bit
+    # on the recsys fixture and on wider synthetic inputs (parity of the device scaler rests on it)
+    from sklearn.preprocessing import StandardScaler
+    z = load("golden_kmeans.npz")
+    rng = np.random.default_rng(4)
+    for X in (z["rs_X"], (rng.standard_normal((17730, 64)) * 3 + 1).astype(np.float32)):
+        sk = StandardScaler().fit(X)
+        out, mean, scale = O.standard_scaler(X)
+        assert np.array_equal(out.view(np.uint32), sk.transform(X).view(np.uint32))
+        assert np.array_equal(mean, sk.mean_) and np.array_equal(scale, sk.scale_)
