@@ -474,6 +474,404 @@ __global__ __launch_bounds__(kTailThreads) void k_kpp_tail_fast(
   GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 6 + 10 * (c & 1));
 }
 
+// ---- speculative candidate draws -----------------------------------------------------------------
+// Round c's tail used to be serial: potentials -> argmin -> the winning trial's cumulative potential
+// -> the next candidates. But every trial t already has its own row dist[t] (the closest distances
+// if t wins), so the next round's candidates can be drawn for EVERY possible winner, in parallel,
+// one workgroup per trial: next[t][j] = searchsorted(cumsum(w * dist[t]), u[c][j] * pot[t]). The
+// next distance launch then reads the T potentials, takes the argmin b (first minimum, NaN first as
+// np.argmin) and uses next[b][*] — the argmin and its dependent row read leave the critical path.
+struct KppSpec {
+  float pot[2][kMaxTrials];                   // by round parity: potentials of that round's trials
+  int64_t cand[2][kMaxTrials];                // by round parity: that round's candidates
+  int64_t next[2][kMaxTrials][kMaxTrials];    // next[p][t][j]: round c+1's trial j if t wins round c
+};
+
+__device__ __forceinline__ int kpp_argmin(const float* pot, int T) {
+  int b = 0;
+  for (int t = 1; t < T; ++t) {
+    const float pb = pot[b], pt = pot[t];
+    if (pb == pb && (pt < pb || pt != pt)) b = t;
+  }
+  return b;
+}
+
+// round 0 (the tail of the first centre, from KppState) seeds round 1: one "trial" that always wins
+__global__ void k_kpp_spec_seed(const KppState* __restrict__ st, int T, KppSpec* __restrict__ sp) {
+  const int j = threadIdx.x;
+  if (j < kMaxTrials) {
+    sp->pot[0][j] = j == 0 ? st->pot : __builtin_inff();
+    if (j < T) sp->next[0][0][j] = st->cand[j];
+  }
+}
+
+// round c >= 1, workgroup (g, t): the winner of round c-1, this trial's candidate, then the
+// distance phase (kpp_dist_phase's work) with the candidate passed in
+__global__ __launch_bounds__(256) void k_kpp_dist_spec(
+    int64_t n, int dim, const float* __restrict__ X, const float* __restrict__ w,
+    const double* __restrict__ xsq, const float* __restrict__ closest0,
+    const float* __restrict__ dist_prev, KppSpec* __restrict__ sp, float* __restrict__ dist,
+    float* __restrict__ acc, int L, int T, int c, float* __restrict__ centers,
+    int64_t* __restrict__ indices) {
+  extern __shared__ double s_c[];
+  const int t = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
+  const int pp = (c - 1) & 1;
+  const int b = kpp_argmin(sp->pot[pp], T);
+  const int64_t ct = sp->next[pp][b][t];
+  if (g == 0 && tid == 0) sp->cand[c & 1][t] = ct;
+  if (c >= 2 && g == 0 && t == 0) {  // round c-1's centre (round 0's is written by its tail)
+    const int64_t src = sp->cand[pp][b];
+    if (tid == 0) indices[c - 1] = src;
+    for (int j = tid; j < dim; j += blockDim.x) centers[(int64_t)(c - 1) * dim + j] = X[src * dim + j];
+  }
+  const int64_t J = n >> 6, n64 = J << 6;
+  const int64_t nloc = (int64_t)L * J;
+  const int64_t ntot = nloc + (g == 0 ? n - n64 : 0);
+  const double cn = xsq[ct];
+  const float* closest = c == 1 ? closest0 : dist_prev + (int64_t)b * n;
+  for (int j = tid; j < dim; j += blockDim.x) s_c[j] = (double)X[ct * dim + j];
+  __syncthreads();
+  float* sd = reinterpret_cast<float*>(s_c + dim);
+  float* drow = dist + (int64_t)t * n;
+  for (int64_t q = tid; q < ntot; q += blockDim.x) {
+    int64_t i;
+    if (q < nloc) {
+      const int64_t j = q / L;
+      i = (int64_t)g * L + (q - j * L) + 64 * j;
+    } else {
+      i = n64 + (q - nloc);
+    }
+    const float* xi = X + i * dim;
+    const double xs = xsq[i];
+    const float cl = closest[i];
+    double dot = 0.0;
+    int j = 0;
+    for (; j + 8 <= dim; j += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = xi[j + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) dot = __builtin_fma(s_c[j + u], (double)v[u], dot);
+    }
+    for (; j < dim; ++j) dot = __builtin_fma(s_c[j], (double)xi[j], dot);
+    const double d = ((-2.0 * dot) + cn) + xs;
+    float f = (float)d;
+    f = f < 0.f ? 0.f : f;
+    f = np_minimum(cl, f);
+    drow[i] = f;
+    if (q < nloc) sd[q] = f;
+  }
+  __syncthreads();
+  if (tid < L) {
+    const int l = g * L + tid;
+    float a = 0.f;
+    int64_t j = 0;
+    for (; j + 8 <= J; j += 8) {
+      float xv[8], yv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        xv[u] = sd[(j + u) * L + tid];
+        yv[u] = w ? w[l + 64 * (j + u)] : 1.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a = __builtin_fmaf(xv[u], yv[u], a);
+    }
+    for (; j < J; ++j) a = __builtin_fmaf(sd[j * L + tid], w ? w[l + 64 * j] : 1.0f, a);
+    acc[t * 64 + l] = a;
+  }
+}
+
+// round c, workgroup t: this trial's potential and, unless c is the last round, the next round's
+// candidates should t win (counts over this trial's cumulative potential, as k_kpp_tail_fast)
+template <int kR>
+__global__ __launch_bounds__(kTailThreads) void k_kpp_trial_tail(
+    int64_t n, const float* __restrict__ w, const float* __restrict__ dist,
+    const float* __restrict__ acc, int T, int c, int k, const double* __restrict__ uniforms,
+    KppSpec* __restrict__ sp) {
+  __shared__ float s_pot;
+  __shared__ double s_r[kMaxTrials];
+  __shared__ double s_part[kTailThreads / 64];
+  __shared__ int s_cnt[kMaxTrials][kTailThreads / 64];
+  const int t = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int p = c & 1;
+  const bool more = c + 1 < k;
+  const double u_mine = (tid < T && more) ? uniforms[(int64_t)c * T + tid] : 0.0;
+  const int64_t chunk = (n + kTailThreads - 1) / kTailThreads;
+  const int64_t lo = min<int64_t>(n, tid * chunk), hi = min<int64_t>(n, lo + chunk);
+  const float* row = dist + (int64_t)t * n;
+  float pr[kR];
+#pragma unroll
+  for (int u = 0; u < kR; ++u)
+    pr[u] = (more && lo + u < hi) ? (w ? w[lo + u] : 1.0f) * row[lo + u] : 0.f;
+  if (wave == 0) {
+    const int64_t ri = (n & ~63ll) + lane;
+    const float rx = ri < n ? row[ri] : 0.f;
+    const float ry = ri < n ? (w ? w[ri] : 1.0f) : 0.f;
+    const float pt = sdot_skx_finish_shfl(acc[t * 64 + lane], rx, ry, n);
+    if (lane == 0) {
+      s_pot = pt;
+      sp->pot[p][t] = pt;
+    }
+  }
+  if (!more) return;
+  double run = 0.0;
+#pragma unroll
+  for (int u = 0; u < kR; ++u)
+    if (lo + u < hi) run = run + (double)pr[u];
+  double incl = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) s_part[wave] = incl;
+  __syncthreads();  // s_pot, s_part
+  if (tid < T) s_r[tid] = u_mine * (double)s_pot;
+  // exclusive prefix of the wave totals: lanes 0..15 scan them, every lane takes its wave's entry
+  double wp = lane < kTailThreads / 64 ? s_part[lane] : 0.0;
+  double wincl = wp;
+#pragma unroll
+  for (int o = 1; o < kTailThreads / 64; o <<= 1) {
+    const double v = __shfl_up(wincl, o);
+    if (lane >= o) wincl += v;
+  }
+  double base = (incl - run) + (wave > 0 ? __shfl(wincl, wave - 1) : 0.0);
+  double cu[kR];
+#pragma unroll
+  for (int u = 0; u < kR; ++u) {
+    base = base + (double)pr[u];
+    cu[u] = base;
+  }
+  __syncthreads();  // s_r
+  for (int j = 0; j < T; ++j) {
+    const double r = s_r[j];
+    int cw = 0;
+#pragma unroll
+    for (int u = 0; u < kR; ++u) cw += __popcll(__ballot(lo + u < hi && cu[u] < r));
+    if (lane == 0) s_cnt[j][wave] = cw;
+  }
+  __syncthreads();
+  if (tid < T) {
+    int64_t a = 0;
+    for (int q = 0; q < kTailThreads / 64; ++q) a += s_cnt[tid][q];
+    if (a > n - 1) a = n - 1;
+    sp->next[p][t][tid] = a;
+  }
+}
+
+// after the last round: its winner is the last centre
+__global__ void k_kpp_spec_finish(int dim, const float* __restrict__ X, const KppSpec* __restrict__ sp,
+                                  int T, int c, float* __restrict__ centers,
+                                  int64_t* __restrict__ indices) {
+  const int p = c & 1;
+  const int b = kpp_argmin(sp->pot[p], T);
+  const int64_t src = sp->cand[p][b];
+  if (threadIdx.x == 0) indices[c] = src;
+  for (int j = threadIdx.x; j < dim; j += blockDim.x) centers[(int64_t)c * dim + j] = X[src * dim + j];
+}
+
+// ---- one launch per round ---------------------------------------------------------------------
+// Round c's launch also finishes round c-1: every workgroup folds the previous round's lane
+// accumulators into the T potentials (redundantly, from 2 KB), takes the argmin b, scans the
+// winner's row dist_prev[b] into the fp64 cumulative potential and draws ITS trial's candidate by
+// counting (searchsorted_left), then runs the distance phase for that candidate. One launch and
+// three dependent memory trips per round (accumulators, winner's row, candidate row) instead of two
+// launches with a single-workgroup tail between them. Workgroup (0, 0) writes round c-1's centre.
+// Needs chunk = ceil(n / 256) <= kR (each thread scans <= kR consecutive entries of the row).
+template <int kR, int kPre>
+__global__ __launch_bounds__(256) void k_kpp_round(
+    int64_t n, int dim, const float* __restrict__ X, const float* __restrict__ w,
+    const double* __restrict__ xsq, const float* __restrict__ closest0,
+    const float* __restrict__ dist_prev, float* __restrict__ dist_cur,
+    const float* __restrict__ acc_prev, float* __restrict__ acc_cur, int L, int T, int c,
+    const double* __restrict__ uniforms, const KppState* __restrict__ st,
+    const int64_t* __restrict__ cand_prev, int64_t* __restrict__ cand_cur,
+    float* __restrict__ centers, int64_t* __restrict__ indices) {
+  extern __shared__ double s_c[];  // dim doubles, then the chain distances (fp32)
+  __shared__ float s_pot[kMaxTrials];
+  __shared__ double s_part[4];
+  __shared__ int s_cnt[4];
+  const int t = blockIdx.y, g = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int nw = blockDim.x >> 6;
+  const double u = uniforms[(int64_t)(c - 1) * T + t];
+  // this workgroup's points (strided lanes, see k_kpp_dist) and, with kPre, their rows requested now
+  const int64_t J = n >> 6, n64 = J << 6;
+  const int64_t nloc = (int64_t)L * J;
+  const int64_t ntot = nloc + (g == 0 ? n - n64 : 0);
+  auto point_of = [&](int64_t q) -> int64_t {
+    if (q < nloc) {
+      const int64_t j = q / L;
+      return (int64_t)g * L + (q - j * L) + 64 * j;
+    }
+    return n64 + (q - nloc);
+  };
+  float xr[kPre > 0 ? kPre : 1];
+  double xs0 = 0.0;
+  const int64_t i0 = tid < ntot ? point_of(tid) : 0;
+  auto prefetch_rows = [&]() {  // dim % 4 == 0 (host-checked): float4 loads
+    if (kPre > 0 && tid < ntot) {
+      const float4* xi = reinterpret_cast<const float4*>(X + i0 * dim);
+#pragma unroll
+      for (int j = 0; j < (kPre > 0 ? kPre : 4) / 4; ++j) {
+        const float4 v = 4 * j < dim ? xi[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        xr[4 * j] = v.x;
+        xr[4 * j + 1] = v.y;
+        xr[4 * j + 2] = v.z;
+        xr[4 * j + 3] = v.w;
+      }
+      xs0 = xsq[i0];
+    }
+  };
+  // ---- previous round's potentials and winner (round 0: the first centre's potential)
+  if (c == 1) {
+    if (tid == 0) s_pot[0] = st->pot;
+    prefetch_rows();
+  } else {
+    // the potentials' inputs are requested before the point rows, so they land first
+    float a_in[kMaxTrials / 4], rx_in[kMaxTrials / 4];
+    const int64_t ri = (n & ~63ll) + lane;
+    const float ry = ri < n ? (w ? w[ri] : 1.0f) : 0.f;
+#pragma unroll
+    for (int q = 0; q < kMaxTrials / 4; ++q) {
+      const int tr = wave + q * 4;
+      a_in[q] = tr < T ? acc_prev[tr * 64 + lane] : 0.f;
+      rx_in[q] = (tr < T && ri < n) ? dist_prev[(int64_t)tr * n + ri] : 0.f;
+    }
+    prefetch_rows();
+#pragma unroll
+    for (int q = 0; q < kMaxTrials / 4; ++q) {
+      const int tr = wave + q * 4;
+      if (tr < T) {
+        const float p = sdot_skx_finish_shfl(a_in[q], rx_in[q], ry, n);
+        if (lane == 0) s_pot[tr] = p;
+      }
+    }
+  }
+  __syncthreads();
+  const int b = c == 1 ? 0 : kpp_argmin(s_pot, T);
+  const double r = u * (double)s_pot[b];
+  const float* row = c == 1 ? closest0 : dist_prev + (int64_t)b * n;
+  const float cl0 = (kPre > 0 && tid < ntot) ? row[i0] : 0.f;
+  // ---- the winner's cumulative potential, scanned in place; this trial's candidate by counting
+  const int64_t chunk = (n + blockDim.x - 1) / blockDim.x;
+  const int64_t lo = min<int64_t>(n, tid * chunk), hi = min<int64_t>(n, lo + chunk);
+  float pr[kR];
+#pragma unroll
+  for (int q = 0; q < kR; ++q) pr[q] = (lo + q < hi) ? (w ? w[lo + q] : 1.0f) * row[lo + q] : 0.f;
+  double run = 0.0;
+#pragma unroll
+  for (int q = 0; q < kR; ++q)
+    if (lo + q < hi) run = run + (double)pr[q];
+  double incl = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) s_part[wave] = incl;
+  __syncthreads();
+  double base = incl - run;
+  for (int q = 0; q < wave; ++q) base += s_part[q];
+  int cw = 0;
+#pragma unroll
+  for (int q = 0; q < kR; ++q) {
+    base = base + (double)pr[q];
+    cw += __popcll(__ballot(lo + q < hi && base < r));
+  }
+  if (lane == 0) s_cnt[wave] = cw;
+  __syncthreads();
+  int64_t ct = 0;
+  for (int q = 0; q < nw; ++q) ct += s_cnt[q];
+  if (ct > n - 1) ct = n - 1;
+  if (g == 0 && tid == 0) cand_cur[t] = ct;
+  if (c >= 2 && g == 0 && t == 0) {  // round c-1's centre (round 0's is written by its tail)
+    const int64_t src = cand_prev[b];
+    if (tid == 0) indices[c - 1] = src;
+    for (int j = tid; j < dim; j += blockDim.x) centers[(int64_t)(c - 1) * dim + j] = X[src * dim + j];
+  }
+  // ---- distances to this trial's candidate, np.minimum with the winner's row, lane chains
+  const double cn = xsq[ct];
+  for (int j = tid; j < dim; j += blockDim.x) s_c[j] = (double)X[ct * dim + j];
+  __syncthreads();
+  float* sd = reinterpret_cast<float*>(s_c + dim);
+  float* drow = dist_cur + (int64_t)t * n;
+  if (kPre > 0) {  // one point per thread, row already in registers
+    if (tid < ntot) {
+      double dot = 0.0;
+#pragma unroll
+      for (int j = 0; j < (kPre > 0 ? kPre : 1); ++j)
+        if (j < dim) dot = __builtin_fma(s_c[j], (double)xr[j], dot);
+      const double d = ((-2.0 * dot) + cn) + xs0;
+      float f = (float)d;
+      f = f < 0.f ? 0.f : f;
+      f = np_minimum(cl0, f);
+      drow[i0] = f;
+      if (tid < nloc) sd[tid] = f;
+    }
+  } else
+  for (int64_t q = tid; q < ntot; q += blockDim.x) {
+    const int64_t i = point_of(q);
+    const float* xi = X + i * dim;
+    const double xs = xsq[i];
+    const float cl = row[i];
+    double dot = 0.0;
+    int j = 0;
+    for (; j + 8 <= dim; j += 8) {
+      float v[8];
+#pragma unroll
+      for (int uu = 0; uu < 8; ++uu) v[uu] = xi[j + uu];
+#pragma unroll
+      for (int uu = 0; uu < 8; ++uu) dot = __builtin_fma(s_c[j + uu], (double)v[uu], dot);
+    }
+    for (; j < dim; ++j) dot = __builtin_fma(s_c[j], (double)xi[j], dot);
+    const double d = ((-2.0 * dot) + cn) + xs;
+    float f = (float)d;
+    f = f < 0.f ? 0.f : f;
+    f = np_minimum(cl, f);
+    drow[i] = f;
+    if (q < nloc) sd[q] = f;
+  }
+  __syncthreads();
+  if (tid < L) {
+    const int l = g * L + tid;
+    float a = 0.f;
+    int64_t j = 0;
+    for (; j + 8 <= J; j += 8) {
+      float xv[8], yv[8];
+#pragma unroll
+      for (int uu = 0; uu < 8; ++uu) {
+        xv[uu] = sd[(j + uu) * L + tid];
+        yv[uu] = w ? w[l + 64 * (j + uu)] : 1.0f;
+      }
+#pragma unroll
+      for (int uu = 0; uu < 8; ++uu) a = __builtin_fmaf(xv[uu], yv[uu], a);
+    }
+    for (; j < J; ++j) a = __builtin_fmaf(sd[j * L + tid], w ? w[l + 64 * j] : 1.0f, a);
+    acc_cur[t * 64 + l] = a;
+  }
+}
+
+// after the last round: its potentials, winner and centre
+__global__ __launch_bounds__(256) void k_kpp_round_final(
+    int64_t n, int dim, const float* __restrict__ X, const float* __restrict__ w,
+    const float* __restrict__ dist, const float* __restrict__ acc, int T, int c,
+    const int64_t* __restrict__ cand, float* __restrict__ centers, int64_t* __restrict__ indices) {
+  __shared__ float s_pot[kMaxTrials];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6;
+  for (int tr = wave; tr < T; tr += nw) {
+    const int64_t ri = (n & ~63ll) + lane;
+    const float rx = ri < n ? dist[(int64_t)tr * n + ri] : 0.f;
+    const float ry = ri < n ? (w ? w[ri] : 1.0f) : 0.f;
+    const float p = sdot_skx_finish_shfl(acc[tr * 64 + lane], rx, ry, n);
+    if (lane == 0) s_pot[tr] = p;
+  }
+  __syncthreads();
+  const int b = kpp_argmin(s_pot, T);
+  const int64_t src = cand[b];
+  if (tid == 0) indices[c] = src;
+  for (int j = tid; j < dim; j += blockDim.x) centers[(int64_t)c * dim + j] = X[src * dim + j];
+}
+
 // ---- all rounds in one launch ------------------------------------------------------------------
 // The same two phases per round, inside one persistent launch of G*T workgroups (<= 256, one per
 // CU, so all are resident): every workgroup runs its slice of the distance phase, releases its
@@ -701,8 +1099,10 @@ extern "C" size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int n_trials) {
   b += align256(sizeof(float) * n);                                         // closest0
   b += 2 * align256(sizeof(float) * n * (size_t)std::max(n_trials, 1));     // dist ping-pong
   b += align256(sizeof(double) * n);                                        // cum
-  b += align256(sizeof(float) * 64 * (size_t)std::max(n_trials, 1));       // lane accumulators
+  b += 2 * align256(sizeof(float) * 64 * (size_t)std::max(n_trials, 1));   // lane accumulators
+  b += 2 * align256(sizeof(int64_t) * kMaxTrials);                          // round candidates
   b += align256(sizeof(KppSync));
+  b += align256(sizeof(KppSpec));
   return b + 2048;
 }
 
@@ -725,7 +1125,10 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   float* dist[2] = {cv.take<float>(n * (size_t)n_trials), cv.take<float>(n * (size_t)n_trials)};
   double* cum = cv.take<double>(n);
   float* acc = cv.take<float>(64 * (size_t)n_trials);
+  float* acc2 = cv.take<float>(64 * (size_t)n_trials);
+  int64_t* candb[2] = {cv.take<int64_t>(kMaxTrials), cv.take<int64_t>(kMaxTrials)};
   KppSync* sy = cv.take<KppSync>(1);
+  KppSpec* sp = cv.take<KppSpec>(1);
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans++: workspace too small");
   const unsigned nb = (unsigned)((n + 255) / 256);
   // w == nullptr: unit sample weights, handled in the kernels
@@ -759,6 +1162,54 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     k_kpp_rounds<16><<<NB, 256, lds, s>>>(n, dim, X, w, xsq, closest0, dist[0], dist[1], acc, L, G,
                                           n_trials, k, uniforms, centers, indices, st, sy);
+    GDD_LAUNCHED();
+    return GDD_OK;
+  }
+  // one launch per round (k_kpp_round) when a 256-thread workgroup scans the winner's row in
+  // <= 16 entries per thread
+  if (k > 1 && chain_in_lds && (n + 255) / 256 <= 16 && getenv("GDD_KPP_SPEC") == nullptr) {
+    float* accb[2] = {acc, acc2};
+    // opt-in (GDD_KPP_PREFETCH=1): the point rows requested into registers at the start of the
+    // round. Measured slower at the arxiv shape (13.7 vs 12.6 ms per fit): the extra in-flight
+    // loads delay the critical potential/winner-row requests more than they hide.
+    const bool pre = (int64_t)L * J + (n - (J << 6)) <= 256 && dim <= 64 && dim % 4 == 0 &&
+                     (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
+                     getenv("GDD_KPP_PREFETCH") != nullptr;
+    auto kern = pre ? k_kpp_round<16, 64> : k_kpp_round<16, 0>;
+    if (lds > 65536)
+      GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+    for (int c = 1; c < k; ++c) {
+      kern<<<dim3(G, n_trials), 256, lds, s>>>(
+          n, dim, X, w, xsq, closest0, dist[(c - 1) & 1], dist[c & 1], accb[(c - 1) & 1],
+          accb[c & 1], L, n_trials, c, uniforms, st, candb[(c - 1) & 1], candb[c & 1], centers,
+          indices);
+      GDD_LAUNCHED();
+    }
+    k_kpp_round_final<<<1, 256, 0, s>>>(n, dim, X, w, dist[(k - 1) & 1], accb[(k - 1) & 1],
+                                        n_trials, k - 1, candb[(k - 1) & 1], centers, indices);
+    GDD_LAUNCHED();
+    return GDD_OK;
+  }
+  // speculative draws: per round one distance launch and one per-trial tail launch (T workgroups)
+  constexpr int kSpecR = 8;
+  if (k > 1 && chain_in_lds && (n + kTailThreads - 1) / kTailThreads <= kSpecR) {
+    k_kpp_spec_seed<<<1, 64, 0, s>>>(st, n_trials, sp);
+    GDD_LAUNCHED();
+    if (lds > 65536)
+      GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dist_spec,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    for (int c = 1; c < k; ++c) {
+      const float* prev = dist[(c - 1) & 1];
+      float* cur = dist[c & 1];
+      k_kpp_dist_spec<<<dim3(G, n_trials), 256, lds, s>>>(n, dim, X, w, xsq, closest0, prev, sp, cur,
+                                                          acc, L, n_trials, c, centers, indices);
+      GDD_LAUNCHED();
+      k_kpp_trial_tail<kSpecR><<<n_trials, kTailThreads, 0, s>>>(n, w, cur, acc, n_trials, c, k,
+                                                                 uniforms, sp);
+      GDD_LAUNCHED();
+    }
+    k_kpp_spec_finish<<<1, 256, 0, s>>>(dim, X, sp, n_trials, k - 1, centers, indices);
     GDD_LAUNCHED();
     return GDD_OK;
   }
