@@ -88,14 +88,62 @@ __device__ __forceinline__ float skl_sqdist(const float* __restrict__ a, const f
   return r;
 }
 
+// skl_sqdist with a 16-byte-aligned global `a`, dim % 4 == 0: the row is fetched as float4, eight
+// at a time ahead of the ordered group sums (same arithmetic, same order)
+__device__ __forceinline__ float skl_sqdist_v4(const float* __restrict__ a, const float* __restrict__ b,
+                                               int dim) {
+  const float4* a4 = reinterpret_cast<const float4*>(a);
+  const int q = dim >> 2;
+  float r = 0.f;
+  for (int j0 = 0; j0 < q; j0 += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = j0 + u < q ? a4[j0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (j0 + u < q) {
+        const float* bb = b + 4 * (j0 + u);
+        const float d0 = v[u].x - bb[0], d1 = v[u].y - bb[1], d2 = v[u].z - bb[2], d3 = v[u].w - bb[3];
+        r = r + (((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
+      }
+    }
+  }
+  return r;
+}
+
 // ---------------------------------------------------------------------------------------------
 // assignment: MFMA distance tiles + lexicographic (distance, index) argmin
 // ---------------------------------------------------------------------------------------------
 // (d, c) packed so that unsigned 64-bit order == lexicographic order on (d as float, c)
 __device__ __forceinline__ unsigned long long pack_key(float d, int c) {
-  unsigned u = __float_as_uint(d);
+  // -0.0 + 0.0 = +0.0: both zeros get one key, so they tie on the index as sklearn's `<` does
+  unsigned u = __float_as_uint(d + 0.0f);
   u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
   return ((unsigned long long)u << 32) | (unsigned)c;
+}
+
+// lexicographic (distance, index) minimum of one lane's 16 tile entries against its running best:
+// lane l holds centres cb + (r&3) + 8(r>>2) + 4(l>>5), increasing with r, so a strict float `<`
+// keeps the lowest index among equal distances; the result is packed once
+__device__ __forceinline__ unsigned long long tile_best(const floatx16& acc, const float* Nw, int cb,
+                                                       int kh, int k, unsigned long long best) {
+  float nv[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) nv[r] = Nw[(r & 3) + 8 * (r >> 2) + 4 * kh];
+  float bd = 0.f;
+  int bi = -1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int ci = cb + (r & 3) + 8 * (r >> 2) + 4 * kh;
+    const float d = __builtin_fmaf(-2.f, acc[r], nv[r]);
+    if (ci < k && (bi < 0 || d < bd)) {
+      bd = d;
+      bi = ci;
+    }
+  }
+  if (bi < 0) return best;
+  const unsigned long long key = pack_key(bd, bi);
+  return key < best ? key : best;
 }
 
 __global__ void k_fill_u64(int64_t n, unsigned long long* p, unsigned long long v,
@@ -363,14 +411,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_assign_small(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const floatx16 acc = mfma_chain<WAVES == 16 ? 10 : 16>(ap, bp, dimp);
     GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 5);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int ci = (r & 3) + 8 * (r >> 2) + 4 * kh;
-      if (cb + ci < k) {
-        const unsigned long long key = pack_key(__builtin_fmaf(-2.f, acc[r], Nw[ci]), cb + ci);
-        best = key < best ? key : best;
-      }
-    }
+    best = tile_best(acc, Nw, cb, kh, k, best);
   }
   const unsigned long long other = __shfl_xor(best, 32);
   best = other < best ? other : best;
@@ -654,16 +695,12 @@ __global__ __launch_bounds__(64 * W) void k_mb_assign(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 4);
     const floatx16 acc = mfma_chain<16>(Cw + (lane & 31) * S + kh, Pl + (lane & 31) * S + kh, dimp);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int ci = (r & 3) + 8 * (r >> 2) + 4 * kh;
-      if (cb + ci < k) {
-        const unsigned long long key = pack_key(__builtin_fmaf(-2.f, acc[r], Nw[ci]), cb + ci);
-        best = key < best ? key : best;
-      }
-    }
+    GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0 && acc[0] != 12345.f), 5);
+    best = tile_best(acc, Nw, cb, kh, k, best);
   }
+  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0 && best != 0ull), 6);
   const unsigned long long other = __shfl_xor(best, 32);
   best = other < best ? other : best;
   if (lane < 32) Kl[wave * 32 + lane] = best;
@@ -714,19 +751,24 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 21);
   if (keys_reset)
     for (int64_t i = (int64_t)c * 64 + lane; i < b; i += (int64_t)gridDim.x * 64) keys_reset[i] = ~0ull;
+  if (sq_out) {  // the old centre row, for the member distances (after the new row in LDS)
+    float* crow = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(reinterpret_cast<int64_t*>(mb_lds) + b) + b) + dim;
+    for (int f = lane; f < dim; f += 64) crow[f] = C_old[(int64_t)c * dim + f];
+  }
   int64_t* src = reinterpret_cast<int64_t*>(mb_lds);      // b source rows
   int32_t* mem = reinterpret_cast<int32_t*>(src + b);     // b member positions
   int count = 0;
-  for (int64_t base = 0; base < b; base += 64 * 8) {
-    // eight independent label loads in flight per lane, then the ordered ballot compaction
-    int32_t lab[8];
+  for (int64_t base = 0; base < b; base += 64 * 16) {
+    // sixteen independent label loads in flight per lane (a 1024-sample batch in one trip), then
+    // the ordered ballot compaction
+    int32_t lab[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const int64_t i = base + u * 64 + lane;
       lab[u] = i < b ? (keys ? (int32_t)(unsigned)(keys[i] & 0xffffffffull) : labels[i]) : -1;
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const bool is = lab[u] == c;
       const unsigned long long m = __ballot(is);
       const int before = __popcll(m & ((1ull << lane) - 1ull));
@@ -740,10 +782,13 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 23);
   if (labels_out || sq_out) {  // per member: its label and its distance to the old centre
-    const float* crow = C_old + (int64_t)c * dim;
+    const float* crow = reinterpret_cast<float*>(mem + b) + dim;  // staged at the start
+    const bool v4 = (dim & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
     for (int t = lane; t < count; t += 64) {
       if (labels_out) labels_out[mem[t]] = c;
-      if (sq_out) sq_out[mem[t]] = skl_sqdist(X + src[t] * dim, crow, dim);
+      if (sq_out)
+        sq_out[mem[t]] = v4 ? skl_sqdist_v4(X + src[t] * dim, crow, dim)
+                            : skl_sqdist(X + src[t] * dim, crow, dim);
     }
   }
   // wsum: sequential fp32 in batch order (update_center_dense :78-83); unit weights sum exactly
@@ -1111,8 +1156,8 @@ namespace {
 constexpr int64_t kMaxBatch = 13312;  // 12*b bytes of LDS per update block (<= 156 KiB)
 
 size_t update_lds(int64_t b) {
-  // src rows (8b) + member positions (4b) + the new centre row (<= 512 floats)
-  return 12 * (size_t)b + 512 * sizeof(float);
+  // src rows (8b) + member positions (4b) + the new and the old centre rows (<= 2 x 512 floats)
+  return 12 * (size_t)b + 2 * 512 * sizeof(float);
 }
 
 int launch_update(int64_t b, int dim, const float* X, const int64_t* rows, const float* w,
