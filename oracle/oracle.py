@@ -73,6 +73,12 @@ def lib():
         L.oracle_sdot_skx.argtypes = [f32p, f32p, i64]
         L.oracle_kmeans_plusplus.argtypes = [i64, ci, f32p, vp, ci, ci, i64, f64p, f32p, i64p]
         L.oracle_labels_sqdist.argtypes = [i64, ci, f32p, f32p, i32p, f32p]
+        L.oracle_sgemv_t_row.restype = cf
+        L.oracle_sgemv_t_row.argtypes = [f32p, f32p, i64, ci, ci]
+        L.oracle_skl_sqdist_upcast.argtypes = [ci, f32p, i64, ci, f32p, f32p]
+        L.oracle_skl_batch_size.restype = i64
+        L.oracle_skl_batch_size.argtypes = [i64, i64, ci]
+        L.oracle_skl_dot_mode.argtypes = [ci, i64, ci, ci, i64, ctypes.POINTER(ci)]
         L.oracle_cr_rsqrt.restype = ctypes.c_double
         L.oracle_cr_rsqrt.argtypes = [ctypes.c_double]
         _lib = L
@@ -180,6 +186,15 @@ def _check_random_state(seed):
     if isinstance(seed, np.random.RandomState):
         return seed
     raise ValueError(f"{seed!r} cannot be used to seed a RandomState")
+
+
+def skl_sqdist_upcast(Cx, X):
+    """sklearn _euclidean_distances(Cx, X, Y_norm_squared=fp32 norms, squared=True), fp32 inputs
+    (pairwise.py _euclidean_distances_upcast with OpenBLAS 0.3.29 SkylakeX summation orders)."""
+    Cx, X = _c(np.atleast_2d(Cx), np.float32), _c(X, np.float32)
+    out = np.empty((Cx.shape[0], X.shape[0]), np.float32)
+    lib().oracle_skl_sqdist_upcast(Cx.shape[0], Cx, X.shape[0], X.shape[1], X, out)
+    return out
 
 
 def kmeans_plusplus(X, k: int, rs: np.random.RandomState, n_local_trials=None):

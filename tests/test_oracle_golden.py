@@ -114,3 +114,22 @@ def test_standard_scaler_vs_sklearn():
         out, mean, scale = O.standard_scaler(X)
         assert np.array_equal(out.view(np.uint32), sk.transform(X).view(np.uint32))
         assert np.array_equal(mean, sk.mean_) and np.array_equal(scale, sk.scale_)
+
+
+@pytest.mark.parametrize("n,dim,k,seed", [(50, 4, 50, 3), (537, 10, 60, 1), (611, 17, 80, 2),
+                                          (300, 33, 300, 5)])
+def test_kmeans_plusplus_vs_sklearn_duplicates(n, dim, k, seed):
+    # duplicated rows drive the potential to ~0: the candidates then hinge on the last bits of
+    # -2<x,c> + |c|^2 + |x|^2, i.e. on numpy's fp64 einsum order for the norms (row_norms of the
+    # upcast chunk); the oracle restates it and must pick scikit-learn's indices exactly
+    from sklearn.cluster import _kmeans as K
+    from sklearn.utils.extmath import row_norms
+    X = np.random.default_rng(seed).standard_normal((n, dim)).astype(np.float32) * 2
+    X[1::7] = X[0]
+    X[2::11] = X[5]
+    X = X - X.mean(axis=0)
+    ci, ii = K._kmeans_plusplus(X, k, row_norms(X, squared=True), np.ones(n, np.float32),
+                                np.random.RandomState(seed))
+    co, io = O.kmeans_plusplus(X, k, np.random.RandomState(seed))
+    assert np.array_equal(ii, io)
+    assert np.array_equal(bits(ci), bits(co))
