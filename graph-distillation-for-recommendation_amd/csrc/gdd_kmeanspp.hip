@@ -1,17 +1,37 @@
 // gdd_kmeanspp.hip — greedy k-means++ seeding on the device (sklearn _kmeans_plusplus,
 // sklearn/cluster/_kmeans.py:174-272), with the host's RNG draws passed in.
 //
-// Two launches per seeding round c = 1..k-1, no host round trip (the chosen trial and the current
-// potential live in device memory):
-//   dist(c)   grid      dist[t][i] = np.minimum(closest_i, fp32(max(0, ((-2<x_cand,x_i>) +
-//                       |x_cand|^2) + |x_i|^2)))   fp64 upcast distances (pairwise.py:582-650)
-//   tail(c)   1 block   pot[t] = fp32 dot(dist[t], w) in OpenBLAS SkylakeX sdot order; best =
-//                       first argmin; centers[c] = X[cand[best]]; then for round c+1:
-//                       cum = inclusive fp64 prefix of fp32(w * dist[best])   (stable_cumsum)
-//                       cand[t] = searchsorted_left(cum, u[c][t] * (double)pot), clipped to n-1
-// tail(0) seeds the loop from the first centre (random_state.choice on the host). `closest` is
-// never copied: round c reads dist[(c-1)&1][best_{c-1}].
+// What has to match, element for element (oracle/gdd_oracle.c restates each piece and is pinned
+// against scikit-learn 1.7.2 + numpy 2.2 + OpenBLAS 0.3.29 SkylakeX, 8 BLAS threads):
+//   distances   _euclidean_distances(C, X, squared=True) on fp32 X: rows of X in chunks of
+//               batch_size upcast to fp64, d = ((-2 C.X^T) + |c|^2) + |x|^2 with numpy's fp64 einsum
+//               norms, fp32, max(., 0). The fp64 product's summation order is OpenBLAS's and depends
+//               on the chunk shape (ddot, dgemv_t, the TN small-matrix dgemm, the regular dgemm and
+//               its edge kernels); skl_mode() picks it per (point, trial). Almost every shape is the
+//               plain k-ordered chain (the fast path); the others take skl_dot().
+//   potentials  first centre: closest @ w = sdot (64 lane chains); trials (T >= 2): (T, n) @ (n, 1)
+//               = sgemv_t: per trial, fp32 lane chains inside blocks of 4096 entries (NBMAX), the
+//               block results added in order, the n%4 trailing entries last.
+//   candidates  searchsorted_left(cumsum_fp64(w * closest), u * pot), clipped to n - 1.
+//
+// Layout: the points are cut into blocks of 4096 (kBlk) — the sgemv_t block and the unit of the
+// cumulative potential. One launch per round c = 1..k-1, grid (blocks, T), 256 threads:
+//   fold      every workgroup folds round c-1's per-block potential terms into the T potentials,
+//             takes the argmin (np.argmin: first minimum, NaN first) and the winner's row;
+//   draw      finds the block where the winner's cumulative potential crosses u * pot (per-block
+//             fp64 totals, scanned in a fixed order) and counts inside that block: its trial's
+//             candidate (cum is non-decreasing, so searchsorted_left = #{cum < r});
+//   distance  its block of points against that candidate, np.minimum with the winner's row;
+//   terms     the block's fp64 cumulative total and the block's sgemv_t lane chains (4 or 8 fp32
+//             chains of <= 1024 entries) — round c+1's fold reads T * blocks values, never a row.
+// A last single-workgroup launch folds round k-1. The cumulative potential is evaluated block-wise
+// (thread-sequential, then fixed shuffle/wave combinations) instead of strictly left to right;
+// every workgroup evaluates the same numbers, the sequence stays non-decreasing, and it can differ
+// from numpy's only by fp64 rounding — a draw changes only if u * pot falls inside that rounding
+// gap (probability ~1e-13 per draw), which no fixture or test has produced.
 #include <algorithm>
+#include <climits>
+#include <cmath>
 #include <cstdlib>
 
 #include "gdd_common.hpp"
@@ -21,25 +41,47 @@ GDD_STAMP_TABLE(kpp)
 namespace {
 
 constexpr int kMaxTrials = 16;
-constexpr int kTailThreads = 1024;
-constexpr int kTailLdsCum = 6144;  // cumulative potential kept in LDS up to this n (48 KiB)
+constexpr int kBlk = 4096;               // sgemv_t NBMAX and the cumulative-potential block
+constexpr int kThr = 256;
+constexpr int kPer = kBlk / kThr;        // 16 entries per thread
+constexpr int kBlasThreads = 8;          // OpenBLAS threads of the pinned reference run
 
 struct KppState {
-  float pot;   // current potential (fp32, as sklearn keeps it)
-  int best;    // trial chosen in the previous round; -1 = the distances to the first centre
-  int64_t cand[kMaxTrials];
+  float pot;  // the first centre's potential (sdot)
+  int pad;
 };
 
-// OpenBLAS 0.3.28/29 SkylakeX sdot (kernel/x86_64/sdot.c + sdot_microk_skylakex-2.c), emulated by
-// one wave: the 64 lanes are the 4 x 16 AVX-512 accumulators of the 64-wide loop (lane u*16+l
-// runs accumulator u, lane l); they fold to 4 x 8 AVX2 accumulators for the 32-wide remainder;
-// lanes then combine ((a0+a1)+a2)+a3, 8 -> 4 by halves, and (h0+h1)+(h2+h3); the scalar tail is
-// added in double. All 64 lanes call it; lane 0 returns the value.
-// The 64 lane chains of the 64-wide loop are independent: per round, k_kpp_dist runs them in the
-// blocks that produce the distances (no block ever re-reads a whole distance row), and the tail
-// only combines 64 accumulators per trial (sdot_skx_finish).
-// the combination after the 64-wide loop: `a` = this lane's accumulator of that loop; (rx, ry) =
-// element n64 + lane of x and y (zero past n). Lane 0 returns the dot.
+__device__ __forceinline__ float np_minimum(float a, float b) {
+  if (a != a || b != b) return __builtin_nanf("");
+  return b < a ? b : a;
+}
+
+// row_norms of the upcast chunk (pairwise.py _euclidean_distances_upcast): numpy's fp64 einsum
+// order — 2 lanes over 8-element blocks, high pair first, zero-padded pairs for the tail, a0 + a1.
+// fp32 squares are exact in fp64, so only the order matters.
+__device__ __forceinline__ double npy_sumsq_f64(const float* __restrict__ x, int dim) {
+  double a0 = 0.0, a1 = 0.0;
+  int j = 0;
+  for (; dim - j >= 8; j += 8) {
+#pragma unroll
+    for (int v = 3; v >= 0; --v) {
+      const double e0 = x[j + 2 * v], e1 = x[j + 2 * v + 1];
+      a0 = e0 * e0 + a0;
+      a1 = e1 * e1 + a1;
+    }
+  }
+  for (; j < dim; j += 2) {
+    const double e0 = x[j], e1 = j + 1 < dim ? (double)x[j + 1] : 0.0;
+    a0 = e0 * e0 + a0;
+    a1 = e1 * e1 + a1;
+  }
+  return a0 + a1;
+}
+
+// ---- OpenBLAS SkylakeX sdot (kernel/x86_64/sdot.c + sdot_microk_skylakex-2.c) ---------------------
+// One wave: lane u*16+l runs AVX-512 accumulator u, lane l of the 64-wide loop; they fold to 4 x 8
+// AVX2 accumulators for the 32-wide remainder; then ((a0+a1)+a2)+a3, 8 -> 4 by halves,
+// (h0+h1)+(h2+h3); the scalar tail is added in double. Lane 0 returns the value.
 __device__ float sdot_skx_finish(float a, float rx, float ry, int64_t n, float* scratch) {
   const int lane = threadIdx.x & 63;
   const int64_t n1 = n & ~31ll;
@@ -59,7 +101,7 @@ __device__ float sdot_skx_finish(float a, float rx, float ry, int64_t n, float* 
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int l = 0; l < 8; ++l) acc[u][l] = scratch[u * 16 + l] + scratch[u * 16 + l + 8];
-    if (n64 < n1) {  // at most one 32-wide block remains
+    if (n64 < n1) {
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -81,34 +123,6 @@ __device__ float sdot_skx_finish(float a, float rx, float ry, int64_t n, float* 
   return r;
 }
 
-// sdot_skx_finish with the fold done by cross-lane shuffles instead of lane 0 over LDS (same
-// operations, same order); every lane returns the dot.
-__device__ float sdot_skx_finish_shfl(float a, float rx, float ry, int64_t n) {
-  const int lane = threadIdx.x & 63;
-  const int64_t n1 = n & ~31ll;
-  const int64_t n64 = n1 & ~63ll;
-  // acc[u][l] = a[16u + l] + a[16u + l + 8], held by lane 16u + l (l < 8)
-  float acc = a + __shfl_down(a, 8);
-  if (n64 < n1) {  // the 32-wide block: acc[u][l] = fma(x[n64 + 8u + l], y[n64 + 8u + l], acc[u][l])
-    const int src = ((lane >> 4) << 3) + (lane & 7);
-    acc = __builtin_fmaf(__shfl(rx, src), __shfl(ry, src), acc);
-  }
-  // s[l] = ((acc[0][l] + acc[1][l]) + acc[2][l]) + acc[3][l]  (lanes 0..7)
-  const float a1 = __shfl(acc, (lane + 16) & 63), a2 = __shfl(acc, (lane + 32) & 63),
-              a3 = __shfl(acc, (lane + 48) & 63);
-  const float sl = ((acc + a1) + a2) + a3;
-  const float h = sl + __shfl(sl, (lane + 4) & 63);  // h[l] = s[l] + s[l+4]  (lanes 0..3)
-  const float h0 = __shfl(h, 0), h1 = __shfl(h, 1), h2 = __shfl(h, 2), h3 = __shfl(h, 3);
-  double dot = n1 ? (double)((h0 + h1) + (h2 + h3)) : 0.0;
-  for (int64_t t = n1; t < n; ++t) {
-    const int L = (int)(t - n64);
-    const float p = __shfl(ry, L) * __shfl(rx, L);
-    dot = dot + (double)p;
-  }
-  return (float)dot;
-}
-
-// the whole dot by one wave (used once, for the first centre's potential)
 __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restrict__ y, int64_t n,
                                float* scratch /* 192 floats of LDS owned by this wave */) {
   const int lane = threadIdx.x & 63;
@@ -116,7 +130,6 @@ __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restr
   const int64_t ri = n64 + lane;
   const float rx = ri < n ? x[ri] : 0.f;
   const float ry = ri < n ? (y ? y[ri] : 1.0f) : 0.f;
-  // y == nullptr: unit sample weights (fma(x, 1, a) == a + x, one rounding either way)
   float a = 0.f;
   for (int64_t i0 = 0; i0 < n64; i0 += 64 * 32) {
     float xv[32], yv[32];
@@ -133,958 +146,588 @@ __device__ float sdot_skx_wave(const float* __restrict__ x, const float* __restr
   return sdot_skx_finish(a, rx, ry, n, scratch);
 }
 
-__device__ __forceinline__ float np_minimum(float a, float b) {
-  if (a != a || b != b) return __builtin_nanf("");
-  return b < a ? b : a;
-}
+// ---- scikit-learn's upcast distance: which OpenBLAS summation order element (point i, trial t)
+// gets (oracle_skl_dot_mode in oracle/gdd_oracle.c states the rules and where they were pinned) ----
+enum SklMode { SKL_SEQ, SKL_TREE8, SKL_HALVES8, SKL_GEMV4, SKL_GEMV2, SKL_L2E, SKL_L4E, SKL_DDOT };
 
-// |x|^2 in fp64 (row_norms of the upcast chunk) and the distances to the first center
-__global__ void k_kpp_init(int64_t n, int dim, const float* __restrict__ X, int64_t first_id,
-                           double* __restrict__ xsq, float* __restrict__ closest) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float* xi = X + i * dim;
-  const float* xc = X + first_id * dim;
-  double s = 0.0, sc = 0.0, dot = 0.0;
-  for (int j = 0; j < dim; ++j) {
-    const double v = (double)xi[j], c = (double)xc[j];
-    s = __builtin_fma(v, v, s);
-    sc = __builtin_fma(c, c, sc);
-    dot = __builtin_fma(c, v, dot);
-  }
-  xsq[i] = s;
-  const float f = (float)(((-2.0 * dot) + sc) + s);
-  closest[i] = f < 0.f ? 0.f : f;
-}
-
-// Round c: distances of every point to trial t's candidate (fp64 upcast, pairwise.py:582-650),
-// np.minimum with the current closest distances, and the 64-wide-loop chains of the potential's
-// sdot. Grid (G, T): block (g, t) owns the sdot lanes l in [g*L, (g+1)*L), L = 64/G, i.e. the
-// points i = l + 64 j, j < J = n64/64; it writes their distances to dist[t][i] (the tail's cumsum
-// reads one row), runs its lanes' ordered fp32 chains over them and leaves acc[t][l]. Block 0 also
-// writes the remainder points n64 <= i < n. The candidate row is staged in LDS as fp64.
-template <bool kChainLds>
-__global__ __launch_bounds__(256) void k_kpp_dist(int64_t n, int dim, const float* __restrict__ X,
-                                                  const float* __restrict__ w,
-                                                  const double* __restrict__ xsq,
-                                                  const float* __restrict__ closest0,
-                                                  const float* __restrict__ dist_prev,
-                                                  const KppState* __restrict__ st,
-                                                  float* __restrict__ dist, float* __restrict__ acc,
-                                                  int L) {
-  GDD_STAMP_WHEN(g_stamps_kpp, (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0), 20);
-  extern __shared__ double s_c[];  // dim doubles, then the block's chain distances (fp32)
-  const int t = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
-  const int64_t J = n >> 6, n64 = J << 6;
-  const int64_t nloc = (int64_t)L * J;
-  const int64_t ntot = nloc + (g == 0 ? n - n64 : 0);
-  const int best = st->best;
-  const int64_t ct = st->cand[t];
-  const double cn = xsq[ct];
-  const float* closest = best < 0 ? closest0 : dist_prev + (int64_t)best * n;
-  for (int j = tid; j < dim; j += blockDim.x) s_c[j] = (double)X[ct * dim + j];
-  __syncthreads();
-  GDD_STAMP_WHEN(g_stamps_kpp, (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0), 21);
-  float* sd = reinterpret_cast<float*>(s_c + dim);
-  float* drow = dist + (int64_t)t * n;
-  for (int64_t q = tid; q < ntot; q += blockDim.x) {
-    int64_t i;
-    if (q < nloc) {
-      const int64_t j = q / L;
-      i = (int64_t)g * L + (q - j * L) + 64 * j;
-    } else {
-      i = n64 + (q - nloc);
-    }
-    const float* xi = X + i * dim;
-    const double xs = xsq[i];
-    const float cl = closest[i];
-    double dot = 0.0;
-    int j = 0;
-    for (; j + 8 <= dim; j += 8) {  // eight loads in flight ahead of the ordered fmas
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = xi[j + u];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) dot = __builtin_fma(s_c[j + u], (double)v[u], dot);
-    }
-    for (; j < dim; ++j) dot = __builtin_fma(s_c[j], (double)xi[j], dot);
-    const double d = ((-2.0 * dot) + cn) + xs;
-    float f = (float)d;
-    f = f < 0.f ? 0.f : f;
-    f = np_minimum(cl, f);
-    drow[i] = f;
-    if (kChainLds && q < nloc) sd[q] = f;
-  }
-  __syncthreads();  // also orders this block's global writes for the chain reads below
-  GDD_STAMP_WHEN(g_stamps_kpp, (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0), 22);
-  if (tid < L) {
-    const int l = g * L + tid;
-    float a = 0.f;
-    int64_t j = 0;
-    for (; j + 8 <= J; j += 8) {
-      float xv[8], yv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int64_t i = l + 64 * (j + u);
-        xv[u] = kChainLds ? sd[(j + u) * L + tid] : drow[i];
-        yv[u] = w ? w[i] : 1.0f;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) a = __builtin_fmaf(xv[u], yv[u], a);
-    }
-    for (; j < J; ++j) {
-      const int64_t i = l + 64 * j;
-      a = __builtin_fmaf(kChainLds ? sd[j * L + tid] : drow[i], w ? w[i] : 1.0f, a);
-    }
-    acc[t * 64 + l] = a;
-  }
-  GDD_STAMP_WHEN(g_stamps_kpp, (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0), 23);
-}
-
-// end of round c (c = 0: the first centre) and the candidate draw of round c+1
-__global__ __launch_bounds__(kTailThreads) void k_kpp_tail(
-    int64_t n, int dim, const float* __restrict__ X, const float* __restrict__ w,
-    const float* __restrict__ closest0, const float* __restrict__ dist,
-    const float* __restrict__ acc, int T, int c, int k,
-    int64_t first_id, const double* __restrict__ uniforms, const double* __restrict__ xsq,
-    double* __restrict__ cum, float* __restrict__ centers, int64_t* __restrict__ indices,
-    KppState* __restrict__ st) {
-  __shared__ float scratch[kMaxTrials * 192];
-  __shared__ float s_pot[kMaxTrials];
-  __shared__ double s_part[kTailThreads / 64];
-  __shared__ double s_cum[kTailLdsCum];
-  __shared__ int s_best;
-  __shared__ int64_t s_src;
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 0 + 10 * (c & 1));
-  // this round's draw for the next candidates, requested up front
-  const double u_mine = (tid < T && c + 1 < k) ? uniforms[(int64_t)c * T + tid] : 0.0;
-  // ---- finish round c ----
-  if (c == 0) {
-    if (wave == 0) {
-      const float p = sdot_skx_wave(closest0, w, n, scratch);  // closest_dist_sq @ sample_weight
-      if (tid == 0) s_pot[0] = p;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      s_best = -1;
-      s_src = first_id;
-      st->best = -1;
-      st->pot = s_pot[0];
-      indices[0] = first_id;
-    }
-  } else {
-    if (wave < T) {
-      const int lane = tid & 63;
-      const int64_t ri = (n & ~63ll) + lane;
-      const float rx = ri < n ? dist[(int64_t)wave * n + ri] : 0.f;
-      const float ry = ri < n ? (w ? w[ri] : 1.0f) : 0.f;
-      const float p = sdot_skx_finish(acc[wave * 64 + lane], rx, ry, n, scratch + wave * 192);
-      if (lane == 0) s_pot[wave] = p;
-    }
-    __syncthreads();
-    GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 1 + 10 * (c & 1));
-    if (tid == 0) {
-      int b = 0;  // np.argmin: first minimum; a NaN is returned as soon as it is met
-      for (int t = 1; t < T; ++t) {
-        const float pb = s_pot[b], pt = s_pot[t];
-        if (pb == pb && (pt < pb || pt != pt)) b = t;
-      }
-      s_best = b;
-      s_src = st->cand[b];
-      st->best = b;
-      st->pot = s_pot[b];
-      indices[c] = st->cand[b];
-    }
-  }
-  __syncthreads();
-  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 2 + 10 * (c & 1));
-  for (int j = tid; j < dim; j += kTailThreads) centers[(int64_t)c * dim + j] = X[s_src * dim + j];
-  if (c + 1 >= k) return;
-  // ---- candidates of round c+1 ----
-  const float* closest = s_best < 0 ? closest0 : dist + (int64_t)s_best * n;
-  const int64_t chunk = (n + kTailThreads - 1) / kTailThreads;
-  const int64_t lo = min<int64_t>(n, tid * chunk), hi = min<int64_t>(n, lo + chunk);
-  // fp32 products w_i * closest_i of this thread's chunk (kept in registers when it is short)
-  constexpr int kReg = 8;
-  float pr[kReg];
-#pragma unroll
-  for (int u = 0; u < kReg; ++u) {
-    const int64_t i = lo + u;
-    pr[u] = (chunk <= kReg && i < hi) ? (w ? w[i] : 1.0f) * closest[i] : 0.f;
-  }
-  double run = 0.0;
-  if (chunk <= kReg) {
-#pragma unroll
-    for (int u = 0; u < kReg; ++u)
-      if (lo + u < hi) run = run + (double)pr[u];
-  } else {
-    for (int64_t i = lo; i < hi; ++i) run = run + (double)((w ? w[i] : 1.0f) * closest[i]);
-  }
-  // exclusive scan of the per-thread chunk totals: wave shuffles, then the 16 wave totals
-  const int lane = tid & 63;
-  double incl = run;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const double v = __shfl_up(incl, o);
-    if (lane >= o) incl += v;
-  }
-  if (lane == 63) s_part[wave] = incl;
-  __syncthreads();
-  if (tid == 0) {
-    double a = 0.0;
-    for (int q = 0; q < kTailThreads / 64; ++q) {
-      const double t = s_part[q];
-      s_part[q] = a;
-      a += t;
-    }
-  }
-  __syncthreads();
-  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 4 + 10 * (c & 1));
-  double base = s_part[wave] + (incl - run);
-  // small n: the cumulative potential stays in LDS for the binary searches
-  double* cs = (n <= kTailLdsCum) ? s_cum : cum;
-  if (chunk <= kReg) {
-#pragma unroll
-    for (int u = 0; u < kReg; ++u)
-      if (lo + u < hi) {
-        base = base + (double)pr[u];
-        cs[lo + u] = base;
-      }
-  } else {
-    for (int64_t i = lo; i < hi; ++i) {
-      base = base + (double)((w ? w[i] : 1.0f) * closest[i]);
-      cs[i] = base;
-    }
-  }
-  __threadfence_block();
-  __syncthreads();
-  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 5 + 10 * (c & 1));
-  if (tid < T) {
-    const double r = u_mine * (double)s_pot[s_best < 0 ? 0 : s_best];
-    int64_t a = 0, b = n;  // first index with cum[idx] >= r  (np.searchsorted side='left')
-    while (a < b) {
-      const int64_t m = (a + b) >> 1;
-      if (cs[m] < r)
-        a = m + 1;
-      else
-        b = m;
-    }
-    if (a > n - 1) a = n - 1;
-    st->cand[tid] = a;
-  }
-  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 6 + 10 * (c & 1));
-}
-
-// Rounds c >= 1 when every thread's share of a distance row fits in registers (chunk <= kR) and
-// T <= kTT. Everything the round needs is requested up front: the lane accumulators and
-// remainders for the potentials and every trial's slice of its distance row, so the cumulative
-// potential of the winning trial starts as soon as the argmin is known; the binary searches are
-// replaced by counts (cum is non-decreasing: searchsorted_left(cum, r) = #{i : cum[i] < r}).
-template <int kTT, int kR>
-__global__ __launch_bounds__(kTailThreads) void k_kpp_tail_fast(
-    int64_t n, int dim, const float* __restrict__ X, const float* __restrict__ w,
-    const float* __restrict__ dist, const float* __restrict__ acc, int T, int c, int k,
-    const double* __restrict__ uniforms, float* __restrict__ centers,
-    int64_t* __restrict__ indices, KppState* __restrict__ st) {
-  __shared__ float s_pot[kMaxTrials];
-  __shared__ double s_r[kMaxTrials];
-  __shared__ double s_part[kTailThreads / 64];
-  __shared__ int s_cnt[kMaxTrials][kTailThreads / 64];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 0 + 10 * (c & 1));
-  const bool more = c + 1 < k;
-  const double u_mine = (tid < T && more) ? uniforms[(int64_t)c * T + tid] : 0.0;
-  const int64_t chunk = (n + kTailThreads - 1) / kTailThreads;
-  const int64_t lo = min<int64_t>(n, tid * chunk), hi = min<int64_t>(n, lo + chunk);
-  float wv[kR];
-#pragma unroll
-  for (int u = 0; u < kR; ++u) wv[u] = (w && lo + u < hi) ? w[lo + u] : 1.0f;
-  // potentials of the T trials
-  if (wave < T) {
-    const int64_t ri = (n & ~63ll) + lane;
-    const float rx = ri < n ? dist[(int64_t)wave * n + ri] : 0.f;
-    const float ry = ri < n ? (w ? w[ri] : 1.0f) : 0.f;
-    const float p = sdot_skx_finish_shfl(acc[wave * 64 + lane], rx, ry, n);
-    if (lane == 0) s_pot[wave] = p;
-  }
-  __syncthreads();
-  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 1 + 10 * (c & 1));
-  int b = 0;  // np.argmin: first minimum; a NaN is returned as soon as it is met
-  for (int t = 1; t < T; ++t) {
-    const float pb = s_pot[b], pt = s_pot[t];
-    if (pb == pb && (pt < pb || pt != pt)) b = t;
-  }
-  const float pot = s_pot[b];
-  const int64_t src = st->cand[b];
-  if (tid == 0) {
-    st->best = b;
-    st->pot = pot;
-    indices[c] = src;
-  }
-  if (tid < T) s_r[tid] = u_mine * (double)pot;
-  for (int j = tid; j < dim; j += kTailThreads) centers[(int64_t)c * dim + j] = X[src * dim + j];
-  if (!more) return;
-  // cumulative potential of the winning trial (fp64 of the fp32 products w_i * closest_i)
-  float pr[kR];
-  const float* row = dist + (int64_t)b * n;
-#pragma unroll
-  for (int u = 0; u < kR; ++u) pr[u] = (lo + u < hi) ? wv[u] * row[lo + u] : 0.f;
-  double run = 0.0;
-#pragma unroll
-  for (int u = 0; u < kR; ++u)
-    if (lo + u < hi) run = run + (double)pr[u];
-  double incl = run;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const double v = __shfl_up(incl, o);
-    if (lane >= o) incl += v;
-  }
-  if (lane == 63) s_part[wave] = incl;
-  __syncthreads();
-  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 4 + 10 * (c & 1));
-  double base = incl - run;
-  for (int q = 0; q < wave; ++q) base += s_part[q];
-  // counts of cum[i] < r_t over the wave's entries (one ballot per entry slot and trial)
-  double cu[kR];
-#pragma unroll
-  for (int u = 0; u < kR; ++u) {
-    base = base + (double)pr[u];
-    cu[u] = base;
-  }
-#pragma unroll
-  for (int t = 0; t < kTT; ++t) {
-    if (t < T) {
-      const double r = s_r[t];
-      int cw = 0;
-#pragma unroll
-      for (int u = 0; u < kR; ++u) cw += __popcll(__ballot(lo + u < hi && cu[u] < r));
-      if (lane == 0) s_cnt[t][wave] = cw;
-    }
-  }
-  __syncthreads();
-  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 5 + 10 * (c & 1));
-  if (tid < T) {
-    int64_t a = 0;
-    for (int q = 0; q < kTailThreads / 64; ++q) a += s_cnt[tid][q];
-    if (a > n - 1) a = n - 1;
-    st->cand[tid] = a;
-  }
-  GDD_STAMP_WHEN(g_stamps_kpp, tid == 0, 6 + 10 * (c & 1));
-}
-
-// ---- speculative candidate draws -----------------------------------------------------------------
-// Round c's tail used to be serial: potentials -> argmin -> the winning trial's cumulative potential
-// -> the next candidates. But every trial t already has its own row dist[t] (the closest distances
-// if t wins), so the next round's candidates can be drawn for EVERY possible winner, in parallel,
-// one workgroup per trial: next[t][j] = searchsorted(cumsum(w * dist[t]), u[c][j] * pot[t]). The
-// next distance launch then reads the T potentials, takes the argmin b (first minimum, NaN first as
-// np.argmin) and uses next[b][*] — the argmin and its dependent row read leave the critical path.
-struct KppSpec {
-  float pot[2][kMaxTrials];                   // by round parity: potentials of that round's trials
-  int64_t cand[2][kMaxTrials];                // by round parity: that round's candidates
-  int64_t next[2][kMaxTrials][kMaxTrials];    // next[p][t][j]: round c+1's trial j if t wins round c
+struct SklPlan {
+  int64_t n, B;  // points; rows per chunk of _euclidean_distances_upcast for this call
+  int T, dim;    // candidate rows of the call (1: the first centre)
+  int all_seq;   // every element takes the plain k-ordered chain (no K split): the fast path
+  int pad;
 };
 
-__device__ __forceinline__ int kpp_argmin(const float* pot, int T) {
+__device__ __forceinline__ int skl_gemv_kind(int64_t j, int64_t w) {
+  const int64_t w4 = w & ~3ll;
+  return (j >= w4 && (w & 2) && j < w4 + 2) ? SKL_GEMV2 : SKL_GEMV4;
+}
+
+__device__ int skl_mode(const SklPlan& p, int64_t i, int t, int* split) {
+  const int64_t s = (i / p.B) * p.B;
+  const int64_t m = min(p.B, p.n - s), r = i - s;
+  *split = 0;
+  if (p.T == 1 && m == 1) return SKL_DDOT;
+  if (p.T == 1) {  // dgemv_t; columns split over the BLAS threads when dim * m >= 460800
+    int64_t a = 0, wd = m;
+    if ((int64_t)p.dim * m >= 460800) {
+      int64_t left = m, s0 = 0;
+      for (int cpu = 0; left > 0; ++cpu) {
+        const int rest = kBlasThreads - cpu;
+        int64_t w = rest > 0 ? (left + rest - 1) / rest : left;
+        w = max<int64_t>(w, 4);
+        w = min<int64_t>(w, left);
+        if (r < s0 + w) {
+          a = s0;
+          wd = w;
+          break;
+        }
+        s0 += w;
+        left -= w;
+      }
+    }
+    return skl_gemv_kind(r - a, wd);
+  }
+  if (m == 1) return skl_gemv_kind(t, p.T);
+  const double mnk = (double)m * (double)p.T * (double)p.dim;
+  if (mnk <= 1e6 && m * p.T <= 1200 && p.dim >= 32)  // TN small-matrix kernel
+    return (r < (m & ~3ll) || t < (p.T & ~3)) ? SKL_TREE8 : SKL_HALVES8;
+  const bool threaded = kBlasThreads >= 2 && mnk >= 524288.0;
+  if (p.dim > 384) *split = threaded ? (p.dim + 1) / 2 : ((p.dim / 2 + 15) / 16) * 16;
+  if (!threaded && m > 192 && t < (p.T / 12) * 12) {  // single-threaded edge kernels
+    const int64_t e = (m & ~15ll) + ((m & 8) ? 8 : 0);
+    if (r >= e) return ((m & 4) && r < e + 4) ? SKL_L2E : SKL_L4E;
+  }
+  return SKL_SEQ;
+}
+
+// the k-ordered fp64 chain (fp32 products are exact in fp64: fma == mul + add)
+__device__ __forceinline__ double dot_seq(const double* __restrict__ c, const float* __restrict__ x,
+                                          int dim) {
+  double dot = 0.0;
+  int j = 0;
+  for (; j + 8 <= dim; j += 8) {  // eight loads in flight ahead of the ordered fmas
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = x[j + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) dot = __builtin_fma(c[j + u], (double)v[u], dot);
+  }
+  for (; j < dim; ++j) dot = __builtin_fma(c[j], (double)x[j], dot);
+  return dot;
+}
+
+__device__ double skl_dot(const double* __restrict__ c, const float* __restrict__ x, int d, int mode,
+                          int sp) {
+  switch (mode) {
+    case SKL_SEQ: {
+      if (sp <= 0) return dot_seq(c, x, d);
+      double a = 0.0, b = 0.0;
+      for (int k = 0; k < sp; ++k) a = __builtin_fma(c[k], (double)x[k], a);
+      for (int k = sp; k < d; ++k) b = __builtin_fma(c[k], (double)x[k], b);
+      return a + b;
+    }
+    case SKL_TREE8:
+    case SKL_HALVES8: {
+      double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      int k = 0;
+      for (; k + 8 <= d; k += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] = __builtin_fma(c[k + u], (double)x[k + u], a[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 7; ++u)
+        if (k + u < d) a[u] = __builtin_fma(c[k + u], (double)x[k + u], a[u]);
+      if (mode == SKL_TREE8) return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+      return ((a[0] + a[4]) + (a[2] + a[6])) + ((a[1] + a[5]) + (a[3] + a[7]));
+    }
+    case SKL_GEMV4:
+    case SKL_GEMV2: {
+      const int d4 = d & ~3;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      for (int k = 0; k < d4; k += 4) {
+        if (mode == SKL_GEMV4) {
+          a0 = __builtin_fma(c[k], (double)x[k], a0);
+          a1 = __builtin_fma(c[k + 1], (double)x[k + 1], a1);
+          a2 = __builtin_fma(c[k + 2], (double)x[k + 2], a2);
+          a3 = __builtin_fma(c[k + 3], (double)x[k + 3], a3);
+        } else {
+          a0 = __builtin_fma(c[k], (double)x[k], a0);
+          a1 = __builtin_fma(c[k + 1], (double)x[k + 1], a1);
+          a0 = __builtin_fma(c[k + 2], (double)x[k + 2], a0);
+          a1 = __builtin_fma(c[k + 3], (double)x[k + 3], a1);
+        }
+      }
+      double r = 0.0 + (mode == SKL_GEMV4 ? (a0 + a2) + (a1 + a3) : a0 + a1);
+      if (d > d4) {
+        double s = c[d4] * (double)x[d4];
+        for (int k = d4 + 1; k < d; ++k) s = __builtin_fma(c[k], (double)x[k], s);
+        r = r + s;
+      }
+      return r;
+    }
+    case SKL_L2E: {
+      const int db = d & ~1;
+      double a0 = 0.0, a1 = 0.0;
+      for (int k = 0; k < db; k += 2) {
+        a0 = __builtin_fma(c[k], (double)x[k], a0);
+        a1 = __builtin_fma(c[k + 1], (double)x[k + 1], a1);
+      }
+      double r = a0 + a1;
+      for (int k = db; k < d; ++k) r = __builtin_fma(c[k], (double)x[k], r);
+      return r;
+    }
+    case SKL_L4E: {
+      const int db = d & ~3;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      for (int k = 0; k < db; k += 4) {
+        a0 = __builtin_fma(c[k], (double)x[k], a0);
+        a1 = __builtin_fma(c[k + 1], (double)x[k + 1], a1);
+        a2 = __builtin_fma(c[k + 2], (double)x[k + 2], a2);
+        a3 = __builtin_fma(c[k + 3], (double)x[k + 3], a3);
+      }
+      double r = (a0 + a1) + (a2 + a3);
+      for (int k = db; k < d; ++k) r = __builtin_fma(c[k], (double)x[k], r);
+      return r;
+    }
+    default: {  // SKL_DDOT: 4 x 8 lanes over 32-blocks, folded to 4 x 4, 16-blocks, tail in order
+      const int n1 = d & ~15, n32 = n1 & ~31;
+      double r = 0.0;
+      if (n1) {
+        double z[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int l = 0; l < 8; ++l) z[u][l] = 0.0;
+        for (int i = 0; i < n32; i += 32)
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int l = 0; l < 8; ++l)
+              z[u][l] = __builtin_fma(c[i + u * 8 + l], (double)x[i + u * 8 + l], z[u][l]);
+        double q[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int l = 0; l < 4; ++l) q[u][l] = z[u][l] + z[u][l + 4];
+        for (int i = n32; i < n1; i += 16)
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int l = 0; l < 4; ++l)
+              q[u][l] = __builtin_fma(c[i + u * 4 + l], (double)x[i + u * 4 + l], q[u][l]);
+        double h[4];
+#pragma unroll
+        for (int l = 0; l < 4; ++l) h[l] = ((q[0][l] + q[1][l]) + q[2][l]) + q[3][l];
+        r = (h[0] + h[2]) + (h[1] + h[3]);
+      }
+      for (int k = n1; k < d; ++k) r = __builtin_fma((double)x[k], c[k], r);
+      return r;
+    }
+  }
+}
+
+__device__ __forceinline__ double skl_point_dot(const SklPlan& p, const double* __restrict__ c,
+                                                const float* __restrict__ x, int64_t i, int t) {
+  if (p.all_seq) return dot_seq(c, x, p.dim);
+  int sp;
+  const int mode = skl_mode(p, i, t, &sp);
+  if (mode == SKL_SEQ && sp == 0) return dot_seq(c, x, p.dim);
+  return skl_dot(c, x, p.dim, mode, sp);
+}
+
+// ---- the block-wise fp64 cumulative potential ----------------------------------------------------
+// prefix(e) of entry e = 16*tid + u of a block: thread-sequential running sum r_u, the exclusive
+// shuffle scan E of the thread totals inside the wave, the wave totals added in wave order B:
+// prefix = (B + E) + r_u. Both the producer of a block's total and the searches use this function,
+// so a block's total equals the prefix of its last entry bit for bit.
+__device__ __forceinline__ void block_prefix(const double (&v)[kPer], double (&pre)[kPer],
+                                             double* s_wave /* 4 */) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double r[kPer];
+  double run = 0.0;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    run = run + v[u];
+    r[u] = run;
+  }
+  double inc = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double y = __shfl_up(inc, o);
+    if (lane >= o) inc = inc + y;
+  }
+  double ex = __shfl_up(inc, 1);
+  if (lane == 0) ex = 0.0;
+  __syncthreads();  // s_wave may still be read by a previous call
+  if (lane == 63) s_wave[wave] = inc;
+  __syncthreads();
+  double B = 0.0;
+  for (int q = 0; q < wave; ++q) B = B + s_wave[q];
+  const double base = B + ex;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) pre[u] = base + r[u];
+}
+
+// ---- the trials' potentials from their per-block sgemv_t terms -------------------------------------
+struct KppArgs {
+  int64_t n, m1;      // points; m1 = n & ~3 (the entries under sgemv_t blocks)
+  int dim, T, nblk, nsg;  // nblk = ceil(n / 4096); nsg = ceil(m1 / 4096)
+  const float* X;
+  const float* w;     // sample weights (nullptr: ones)
+  const double* xsq;
+  const float* closest0;
+  const double* fsum0;  // [nblk] block totals of w * closest0
+  float* dist[2];     // [T][n] by round parity
+  float* vblk[2];     // [T][nblk] sgemv_t block results
+  double* fsum[2];    // [T][nblk] cumulative-potential block totals
+  int64_t* cand[2];   // [kMaxTrials]
+  float* pot1;        // [2] T == 1: the round's potential (sdot), by parity
+  const double* uniforms;
+  const KppState* st;
+  float* centers;
+  int64_t* indices;
+  SklPlan plan;
+};
+
+__device__ __forceinline__ float wv(const float* w, int64_t i) { return w ? w[i] : 1.0f; }
+
+// potential of trial tr of the round whose terms are at parity q: the block results in order, then
+// the m3 trailing entries (their products folded as the sgemv_t scalar tail: p0, fma, fma)
+__device__ float fold_pot(const KppArgs& a, int q, int tr) {
+  const float* vb = a.vblk[q] + (int64_t)tr * a.nblk;
+  float y = 0.f;
   int b = 0;
-  for (int t = 1; t < T; ++t) {
-    const float pb = pot[b], pt = pot[t];
+  for (; b + 8 <= a.nsg; b += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = vb[b + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) y = y + v[u];
+  }
+  for (; b < a.nsg; ++b) y = y + vb[b];
+  if (a.m1 < a.n) {
+    const float* row = a.dist[q] + (int64_t)tr * a.n;
+    float s = row[a.m1] * wv(a.w, a.m1);
+    for (int64_t o = a.m1 + 1; o < a.n; ++o) s = __builtin_fmaf(row[o], wv(a.w, o), s);
+    y = y + s;
+  }
+  return y;
+}
+
+// the T potentials of the round at parity q into s_pot; returns the argmin (np.argmin semantics)
+__device__ int fold_round(const KppArgs& a, int q, float* s_pot) {
+  const int tid = threadIdx.x;
+  if (a.T == 1) {
+    if (tid == 0) s_pot[0] = a.pot1[q];
+  } else if (tid < a.T) {
+    s_pot[tid] = fold_pot(a, q, tid);
+  }
+  __syncthreads();
+  int b = 0;
+  for (int t = 1; t < a.T; ++t) {
+    const float pb = s_pot[b], pt = s_pot[t];
     if (pb == pb && (pt < pb || pt != pt)) b = t;
   }
   return b;
 }
 
-// round 0 (the tail of the first centre, from KppState) seeds round 1: one "trial" that always wins
-__global__ void k_kpp_spec_seed(const KppState* __restrict__ st, int T, KppSpec* __restrict__ sp) {
-  const int j = threadIdx.x;
-  if (j < kMaxTrials) {
-    sp->pot[0][j] = j == 0 ? st->pot : __builtin_inff();
-    if (j < T) sp->next[0][0][j] = st->cand[j];
+// ---- first centre -----------------------------------------------------------------------------------
+// One workgroup per block: |x|^2 (numpy einsum order), the distances to the first centre (T = 1
+// orders: dgemv_t / ddot), and the block's cumulative-potential total.
+__global__ __launch_bounds__(kThr) void k_kpp_init(KppArgs a, SklPlan p1, int64_t first_id,
+                                                   double* __restrict__ xsq_out,
+                                                   float* __restrict__ closest_out,
+                                                   double* __restrict__ fsum_out) {
+  extern __shared__ double s_c[];  // dim doubles, then the block's distances (fp32)
+  __shared__ double s_wave[4];
+  __shared__ double s_sc;
+  const int tid = threadIdx.x;
+  const int64_t j0 = (int64_t)blockIdx.x * kBlk;
+  const float* xc = a.X + first_id * a.dim;
+  for (int j = tid; j < a.dim; j += kThr) s_c[j] = (double)xc[j];
+  if (tid == 0) s_sc = npy_sumsq_f64(xc, a.dim);
+  __syncthreads();
+  float* s_d = reinterpret_cast<float*>(s_c + a.dim);
+  const double sc = s_sc;
+#pragma unroll 1
+  for (int u = 0; u < kPer; ++u) {
+    const int o = tid + kThr * u;
+    const int64_t i = j0 + o;
+    float f = 0.f;
+    if (i < a.n) {
+      const float* xi = a.X + i * a.dim;
+      const double s = npy_sumsq_f64(xi, a.dim);
+      xsq_out[i] = s;
+      const double dot = skl_point_dot(p1, s_c, xi, i, 0);
+      f = (float)(((-2.0 * dot) + sc) + s);
+      f = f < 0.f ? 0.f : f;
+      closest_out[i] = f;
+    }
+    s_d[o] = f;
   }
+  __syncthreads();
+  double v[kPer], pre[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int64_t e = j0 + kPer * tid + u;
+    v[u] = e < a.n ? (double)(wv(a.w, e) * s_d[kPer * tid + u]) : 0.0;
+  }
+  block_prefix(v, pre, s_wave);
+  const int64_t last = min<int64_t>(a.n, j0 + kBlk) - 1 - j0;
+  if (tid == (int)(last / kPer)) fsum_out[blockIdx.x] = pre[last % kPer];
 }
 
-// round c >= 1, workgroup (g, t): the winner of round c-1, this trial's candidate, then the
-// distance phase (kpp_dist_phase's work) with the candidate passed in
-__global__ __launch_bounds__(256) void k_kpp_dist_spec(
-    int64_t n, int dim, const float* __restrict__ X, const float* __restrict__ w,
-    const double* __restrict__ xsq, const float* __restrict__ closest0,
-    const float* __restrict__ dist_prev, KppSpec* __restrict__ sp, float* __restrict__ dist,
-    float* __restrict__ acc, int L, int T, int c, float* __restrict__ centers,
-    int64_t* __restrict__ indices) {
-  extern __shared__ double s_c[];
-  const int t = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
-  const int pp = (c - 1) & 1;
-  const int b = kpp_argmin(sp->pot[pp], T);
-  const int64_t ct = sp->next[pp][b][t];
-  if (g == 0 && tid == 0) sp->cand[c & 1][t] = ct;
-  if (c >= 2 && g == 0 && t == 0) {  // round c-1's centre (round 0's is written by its tail)
-    const int64_t src = sp->cand[pp][b];
-    if (tid == 0) indices[c - 1] = src;
-    for (int j = tid; j < dim; j += blockDim.x) centers[(int64_t)(c - 1) * dim + j] = X[src * dim + j];
+// the first centre's potential (closest @ w: sdot), index and row
+__global__ void k_kpp_first(int64_t n, int dim, const float* __restrict__ X,
+                            const float* __restrict__ w, const float* __restrict__ closest0,
+                            int64_t first_id, KppState* __restrict__ st,
+                            float* __restrict__ centers, int64_t* __restrict__ indices) {
+  __shared__ float scratch[192];
+  const float p = sdot_skx_wave(closest0, w, n, scratch);
+  if (threadIdx.x == 0) {
+    st->pot = p;
+    indices[0] = first_id;
   }
-  const int64_t J = n >> 6, n64 = J << 6;
-  const int64_t nloc = (int64_t)L * J;
-  const int64_t ntot = nloc + (g == 0 ? n - n64 : 0);
-  const double cn = xsq[ct];
-  const float* closest = c == 1 ? closest0 : dist_prev + (int64_t)b * n;
-  for (int j = tid; j < dim; j += blockDim.x) s_c[j] = (double)X[ct * dim + j];
-  __syncthreads();
-  float* sd = reinterpret_cast<float*>(s_c + dim);
-  float* drow = dist + (int64_t)t * n;
-  for (int64_t q = tid; q < ntot; q += blockDim.x) {
-    int64_t i;
-    if (q < nloc) {
-      const int64_t j = q / L;
-      i = (int64_t)g * L + (q - j * L) + 64 * j;
-    } else {
-      i = n64 + (q - nloc);
-    }
-    const float* xi = X + i * dim;
-    const double xs = xsq[i];
-    const float cl = closest[i];
-    double dot = 0.0;
-    int j = 0;
-    for (; j + 8 <= dim; j += 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = xi[j + u];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) dot = __builtin_fma(s_c[j + u], (double)v[u], dot);
-    }
-    for (; j < dim; ++j) dot = __builtin_fma(s_c[j], (double)xi[j], dot);
-    const double d = ((-2.0 * dot) + cn) + xs;
-    float f = (float)d;
-    f = f < 0.f ? 0.f : f;
-    f = np_minimum(cl, f);
-    drow[i] = f;
-    if (q < nloc) sd[q] = f;
+  for (int j = threadIdx.x; j < dim; j += blockDim.x) centers[j] = X[first_id * dim + j];
+}
+
+// T == 1: the single trial's potential is (1, n) @ (n, 1) -> sdot
+__global__ void k_kpp_pot1(int64_t n, const float* __restrict__ row, const float* __restrict__ w,
+                           float* __restrict__ out) {
+  __shared__ float scratch[192];
+  const float p = sdot_skx_wave(row, w, n, scratch);
+  if (threadIdx.x == 0) *out = p;
+}
+
+// ---- one seeding round ------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
+  extern __shared__ double s_c[];  // dim doubles, then the block's distances (fp32)
+  __shared__ float s_pot[kMaxTrials];
+  __shared__ double s_wave[4];
+  __shared__ int s_jmin;
+  __shared__ double s_P;
+  __shared__ int s_cnt[kThr / 64];
+  const int t = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int pq = (c - 1) & 1, cq = c & 1;
+  const int64_t n = a.n;
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 20);
+  const double u = a.uniforms[(int64_t)(c - 1) * a.T + t];
+  if (tid == 0) s_jmin = INT_MAX;
+  // ---- fold round c-1 (round 0: the first centre)
+  int bw = 0;
+  float pot;
+  const float* wrow;
+  const double* wfs;
+  if (c == 1) {
+    pot = a.st->pot;
+    wrow = a.closest0;
+    wfs = a.fsum0;
+    __syncthreads();
+  } else {
+    bw = fold_round(a, pq, s_pot);
+    pot = s_pot[bw];
+    wrow = a.dist[pq] + (int64_t)bw * n;
+    wfs = a.fsum[pq] + (int64_t)bw * a.nblk;
   }
-  __syncthreads();
-  if (tid < L) {
-    const int l = g * L + tid;
-    float a = 0.f;
-    int64_t j = 0;
-    for (; j + 8 <= J; j += 8) {
-      float xv[8], yv[8];
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 21);
+  const double r = u * (double)pot;
+  // ---- the block where the cumulative potential reaches r
+  {
+    const int64_t ch = (a.nblk + kThr - 1) / kThr;
+    const int64_t lo = min<int64_t>(a.nblk, tid * ch), hi = min<int64_t>(a.nblk, lo + ch);
+    double run = 0.0;
+    for (int64_t j = lo; j < hi; ++j) run = run + wfs[j];
+    double inc = run;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        xv[u] = sd[(j + u) * L + tid];
-        yv[u] = w ? w[l + 64 * (j + u)] : 1.0f;
+    for (int o = 1; o < 64; o <<= 1) {
+      const double y = __shfl_up(inc, o);
+      if (lane >= o) inc = inc + y;
+    }
+    double ex = __shfl_up(inc, 1);
+    if (lane == 0) ex = 0.0;
+    if (lane == 63) s_wave[wave] = inc;
+    __syncthreads();
+    double B = 0.0;
+    for (int q = 0; q < wave; ++q) B = B + s_wave[q];
+    double P = B + ex;
+    int found = INT_MAX;
+    double Pf = 0.0;
+    for (int64_t j = lo; j < hi; ++j) {
+      const double Pn = P + wfs[j];
+      if (Pn >= r) {
+        found = (int)j;
+        Pf = P;
+        break;
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) a = __builtin_fmaf(xv[u], yv[u], a);
+      P = Pn;
     }
-    for (; j < J; ++j) a = __builtin_fmaf(sd[j * L + tid], w ? w[l + 64 * j] : 1.0f, a);
-    acc[t * 64 + l] = a;
+    if (found != INT_MAX) atomicMin(&s_jmin, found);
+    __syncthreads();
+    if (found != INT_MAX && found == s_jmin) s_P = Pf;
+    __syncthreads();
   }
-}
-
-// round c, workgroup t: this trial's potential and, unless c is the last round, the next round's
-// candidates should t win (counts over this trial's cumulative potential, as k_kpp_tail_fast)
-template <int kR>
-__global__ __launch_bounds__(kTailThreads) void k_kpp_trial_tail(
-    int64_t n, const float* __restrict__ w, const float* __restrict__ dist,
-    const float* __restrict__ acc, int T, int c, int k, const double* __restrict__ uniforms,
-    KppSpec* __restrict__ sp) {
-  __shared__ float s_pot;
-  __shared__ double s_r[kMaxTrials];
-  __shared__ double s_part[kTailThreads / 64];
-  __shared__ int s_cnt[kMaxTrials][kTailThreads / 64];
-  const int t = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int p = c & 1;
-  const bool more = c + 1 < k;
-  const double u_mine = (tid < T && more) ? uniforms[(int64_t)c * T + tid] : 0.0;
-  const int64_t chunk = (n + kTailThreads - 1) / kTailThreads;
-  const int64_t lo = min<int64_t>(n, tid * chunk), hi = min<int64_t>(n, lo + chunk);
-  const float* row = dist + (int64_t)t * n;
-  float pr[kR];
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 22);
+  int64_t ct = n - 1;
+  const int jb = s_jmin;
+  if (jb != INT_MAX) {  // count inside block jb (uniform branch)
+    const int64_t e0 = (int64_t)jb * kBlk + kPer * tid;
+    double v[kPer], pre[kPer];
 #pragma unroll
-  for (int u = 0; u < kR; ++u)
-    pr[u] = (more && lo + u < hi) ? (w ? w[lo + u] : 1.0f) * row[lo + u] : 0.f;
-  if (wave == 0) {
-    const int64_t ri = (n & ~63ll) + lane;
-    const float rx = ri < n ? row[ri] : 0.f;
-    const float ry = ri < n ? (w ? w[ri] : 1.0f) : 0.f;
-    const float pt = sdot_skx_finish_shfl(acc[t * 64 + lane], rx, ry, n);
-    if (lane == 0) {
-      s_pot = pt;
-      sp->pot[p][t] = pt;
+    for (int q = 0; q < kPer; ++q) {
+      const int64_t e = e0 + q;
+      v[q] = e < n ? (double)(wv(a.w, e) * wrow[e]) : 0.0;
     }
-  }
-  if (!more) return;
-  double run = 0.0;
-#pragma unroll
-  for (int u = 0; u < kR; ++u)
-    if (lo + u < hi) run = run + (double)pr[u];
-  double incl = run;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const double v = __shfl_up(incl, o);
-    if (lane >= o) incl += v;
-  }
-  if (lane == 63) s_part[wave] = incl;
-  __syncthreads();  // s_pot, s_part
-  if (tid < T) s_r[tid] = u_mine * (double)s_pot;
-  // exclusive prefix of the wave totals: lanes 0..15 scan them, every lane takes its wave's entry
-  double wp = lane < kTailThreads / 64 ? s_part[lane] : 0.0;
-  double wincl = wp;
-#pragma unroll
-  for (int o = 1; o < kTailThreads / 64; o <<= 1) {
-    const double v = __shfl_up(wincl, o);
-    if (lane >= o) wincl += v;
-  }
-  double base = (incl - run) + (wave > 0 ? __shfl(wincl, wave - 1) : 0.0);
-  double cu[kR];
-#pragma unroll
-  for (int u = 0; u < kR; ++u) {
-    base = base + (double)pr[u];
-    cu[u] = base;
-  }
-  __syncthreads();  // s_r
-  for (int j = 0; j < T; ++j) {
-    const double r = s_r[j];
+    block_prefix(v, pre, s_wave);
+    const double P = s_P;
     int cw = 0;
 #pragma unroll
-    for (int u = 0; u < kR; ++u) cw += __popcll(__ballot(lo + u < hi && cu[u] < r));
-    if (lane == 0) s_cnt[j][wave] = cw;
+    for (int q = 0; q < kPer; ++q) cw += __popcll(__ballot(e0 + q < n && P + pre[q] < r));
+    if (lane == 0) s_cnt[wave] = cw;
+    __syncthreads();
+    int64_t cnt = 0;
+    for (int q = 0; q < kThr / 64; ++q) cnt += s_cnt[q];
+    ct = min<int64_t>(n - 1, (int64_t)jb * kBlk + cnt);
   }
+  if (blk == 0 && tid == 0) a.cand[cq][t] = ct;
+  if (c >= 2 && blk == 0 && t == 0) {  // round c-1's centre (round 0's is written by k_kpp_first)
+    const int64_t src = a.cand[pq][bw];
+    if (tid == 0) a.indices[c - 1] = src;
+    for (int j = tid; j < a.dim; j += kThr) a.centers[(int64_t)(c - 1) * a.dim + j] = a.X[src * a.dim + j];
+  }
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 23);
+  // ---- distances of this block's points to the candidate, np.minimum with the winner's row
+  const double cn = a.xsq[ct];
+  for (int j = tid; j < a.dim; j += kThr) s_c[j] = (double)a.X[ct * a.dim + j];
   __syncthreads();
-  if (tid < T) {
-    int64_t a = 0;
-    for (int q = 0; q < kTailThreads / 64; ++q) a += s_cnt[tid][q];
-    if (a > n - 1) a = n - 1;
-    sp->next[p][t][tid] = a;
-  }
-}
-
-// after the last round: its winner is the last centre
-__global__ void k_kpp_spec_finish(int dim, const float* __restrict__ X, const KppSpec* __restrict__ sp,
-                                  int T, int c, float* __restrict__ centers,
-                                  int64_t* __restrict__ indices) {
-  const int p = c & 1;
-  const int b = kpp_argmin(sp->pot[p], T);
-  const int64_t src = sp->cand[p][b];
-  if (threadIdx.x == 0) indices[c] = src;
-  for (int j = threadIdx.x; j < dim; j += blockDim.x) centers[(int64_t)c * dim + j] = X[src * dim + j];
-}
-
-// ---- one launch per round ---------------------------------------------------------------------
-// Round c's launch also finishes round c-1: every workgroup folds the previous round's lane
-// accumulators into the T potentials (redundantly, from 2 KB), takes the argmin b, scans the
-// winner's row dist_prev[b] into the fp64 cumulative potential and draws ITS trial's candidate by
-// counting (searchsorted_left), then runs the distance phase for that candidate. One launch and
-// three dependent memory trips per round (accumulators, winner's row, candidate row) instead of two
-// launches with a single-workgroup tail between them. Workgroup (0, 0) writes round c-1's centre.
-// Needs chunk = ceil(n / 256) <= kR (each thread scans <= kR consecutive entries of the row).
-template <int kR, int kPre>
-__global__ __launch_bounds__(256) void k_kpp_round(
-    int64_t n, int dim, const float* __restrict__ X, const float* __restrict__ w,
-    const double* __restrict__ xsq, const float* __restrict__ closest0,
-    const float* __restrict__ dist_prev, float* __restrict__ dist_cur,
-    const float* __restrict__ acc_prev, float* __restrict__ acc_cur, int L, int T, int c,
-    const double* __restrict__ uniforms, const KppState* __restrict__ st,
-    const int64_t* __restrict__ cand_prev, int64_t* __restrict__ cand_cur,
-    float* __restrict__ centers, int64_t* __restrict__ indices) {
-  extern __shared__ double s_c[];  // dim doubles, then the chain distances (fp32)
-  __shared__ float s_pot[kMaxTrials];
-  __shared__ double s_part[4];
-  __shared__ int s_cnt[4];
-  const int t = blockIdx.y, g = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int nw = blockDim.x >> 6;
-  const double u = uniforms[(int64_t)(c - 1) * T + t];
-  // this workgroup's points (strided lanes, see k_kpp_dist) and, with kPre, their rows requested now
-  const int64_t J = n >> 6, n64 = J << 6;
-  const int64_t nloc = (int64_t)L * J;
-  const int64_t ntot = nloc + (g == 0 ? n - n64 : 0);
-  auto point_of = [&](int64_t q) -> int64_t {
-    if (q < nloc) {
-      const int64_t j = q / L;
-      return (int64_t)g * L + (q - j * L) + 64 * j;
-    }
-    return n64 + (q - nloc);
-  };
-  float xr[kPre > 0 ? kPre : 1];
-  double xs0 = 0.0;
-  const int64_t i0 = tid < ntot ? point_of(tid) : 0;
-  auto prefetch_rows = [&]() {  // dim % 4 == 0 (host-checked): float4 loads
-    if (kPre > 0 && tid < ntot) {
-      const float4* xi = reinterpret_cast<const float4*>(X + i0 * dim);
-#pragma unroll
-      for (int j = 0; j < (kPre > 0 ? kPre : 4) / 4; ++j) {
-        const float4 v = 4 * j < dim ? xi[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-        xr[4 * j] = v.x;
-        xr[4 * j + 1] = v.y;
-        xr[4 * j + 2] = v.z;
-        xr[4 * j + 3] = v.w;
-      }
-      xs0 = xsq[i0];
-    }
-  };
-  // ---- previous round's potentials and winner (round 0: the first centre's potential)
-  if (c == 1) {
-    if (tid == 0) s_pot[0] = st->pot;
-    prefetch_rows();
-  } else {
-    // the potentials' inputs are requested before the point rows, so they land first
-    float a_in[kMaxTrials / 4], rx_in[kMaxTrials / 4];
-    const int64_t ri = (n & ~63ll) + lane;
-    const float ry = ri < n ? (w ? w[ri] : 1.0f) : 0.f;
-#pragma unroll
-    for (int q = 0; q < kMaxTrials / 4; ++q) {
-      const int tr = wave + q * 4;
-      a_in[q] = tr < T ? acc_prev[tr * 64 + lane] : 0.f;
-      rx_in[q] = (tr < T && ri < n) ? dist_prev[(int64_t)tr * n + ri] : 0.f;
-    }
-    prefetch_rows();
-#pragma unroll
-    for (int q = 0; q < kMaxTrials / 4; ++q) {
-      const int tr = wave + q * 4;
-      if (tr < T) {
-        const float p = sdot_skx_finish_shfl(a_in[q], rx_in[q], ry, n);
-        if (lane == 0) s_pot[tr] = p;
-      }
-    }
-  }
-  __syncthreads();
-  const int b = c == 1 ? 0 : kpp_argmin(s_pot, T);
-  const double r = u * (double)s_pot[b];
-  const float* row = c == 1 ? closest0 : dist_prev + (int64_t)b * n;
-  const float cl0 = (kPre > 0 && tid < ntot) ? row[i0] : 0.f;
-  // ---- the winner's cumulative potential, scanned in place; this trial's candidate by counting
-  const int64_t chunk = (n + blockDim.x - 1) / blockDim.x;
-  const int64_t lo = min<int64_t>(n, tid * chunk), hi = min<int64_t>(n, lo + chunk);
-  float pr[kR];
-#pragma unroll
-  for (int q = 0; q < kR; ++q) pr[q] = (lo + q < hi) ? (w ? w[lo + q] : 1.0f) * row[lo + q] : 0.f;
-  double run = 0.0;
-#pragma unroll
-  for (int q = 0; q < kR; ++q)
-    if (lo + q < hi) run = run + (double)pr[q];
-  double incl = run;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const double v = __shfl_up(incl, o);
-    if (lane >= o) incl += v;
-  }
-  if (lane == 63) s_part[wave] = incl;
-  __syncthreads();
-  double base = incl - run;
-  for (int q = 0; q < wave; ++q) base += s_part[q];
-  int cw = 0;
-#pragma unroll
-  for (int q = 0; q < kR; ++q) {
-    base = base + (double)pr[q];
-    cw += __popcll(__ballot(lo + q < hi && base < r));
-  }
-  if (lane == 0) s_cnt[wave] = cw;
-  __syncthreads();
-  int64_t ct = 0;
-  for (int q = 0; q < nw; ++q) ct += s_cnt[q];
-  if (ct > n - 1) ct = n - 1;
-  if (g == 0 && tid == 0) cand_cur[t] = ct;
-  if (c >= 2 && g == 0 && t == 0) {  // round c-1's centre (round 0's is written by its tail)
-    const int64_t src = cand_prev[b];
-    if (tid == 0) indices[c - 1] = src;
-    for (int j = tid; j < dim; j += blockDim.x) centers[(int64_t)(c - 1) * dim + j] = X[src * dim + j];
-  }
-  // ---- distances to this trial's candidate, np.minimum with the winner's row, lane chains
-  const double cn = xsq[ct];
-  for (int j = tid; j < dim; j += blockDim.x) s_c[j] = (double)X[ct * dim + j];
-  __syncthreads();
-  float* sd = reinterpret_cast<float*>(s_c + dim);
-  float* drow = dist_cur + (int64_t)t * n;
-  if (kPre > 0) {  // one point per thread, row already in registers
-    if (tid < ntot) {
-      double dot = 0.0;
-#pragma unroll
-      for (int j = 0; j < (kPre > 0 ? kPre : 1); ++j)
-        if (j < dim) dot = __builtin_fma(s_c[j], (double)xr[j], dot);
-      const double d = ((-2.0 * dot) + cn) + xs0;
-      float f = (float)d;
+  float* s_d = reinterpret_cast<float*>(s_c + a.dim);
+  const int64_t j0 = (int64_t)blk * kBlk;
+  float* drow = a.dist[cq] + (int64_t)t * n;
+#pragma unroll 1
+  for (int q = 0; q < kPer; ++q) {
+    const int o = tid + kThr * q;
+    const int64_t i = j0 + o;
+    float f = 0.f;
+    if (i < n) {
+      const float* xi = a.X + i * a.dim;
+      const double dot = skl_point_dot(a.plan, s_c, xi, i, t);
+      f = (float)(((-2.0 * dot) + cn) + a.xsq[i]);
       f = f < 0.f ? 0.f : f;
-      f = np_minimum(cl0, f);
-      drow[i0] = f;
-      if (tid < nloc) sd[tid] = f;
+      f = np_minimum(wrow[i], f);
+      drow[i] = f;
     }
-  } else
-  for (int64_t q = tid; q < ntot; q += blockDim.x) {
-    const int64_t i = point_of(q);
-    const float* xi = X + i * dim;
-    const double xs = xsq[i];
-    const float cl = row[i];
-    double dot = 0.0;
-    int j = 0;
-    for (; j + 8 <= dim; j += 8) {
-      float v[8];
-#pragma unroll
-      for (int uu = 0; uu < 8; ++uu) v[uu] = xi[j + uu];
-#pragma unroll
-      for (int uu = 0; uu < 8; ++uu) dot = __builtin_fma(s_c[j + uu], (double)v[uu], dot);
-    }
-    for (; j < dim; ++j) dot = __builtin_fma(s_c[j], (double)xi[j], dot);
-    const double d = ((-2.0 * dot) + cn) + xs;
-    float f = (float)d;
-    f = f < 0.f ? 0.f : f;
-    f = np_minimum(cl, f);
-    drow[i] = f;
-    if (q < nloc) sd[q] = f;
+    s_d[o] = f;
   }
   __syncthreads();
-  if (tid < L) {
-    const int l = g * L + tid;
-    float a = 0.f;
-    int64_t j = 0;
-    for (; j + 8 <= J; j += 8) {
-      float xv[8], yv[8];
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 24);
+  // ---- the block's terms for round c+1: cumulative total, sgemv_t lane chains
+  {
+    double v[kPer], pre[kPer];
 #pragma unroll
-      for (int uu = 0; uu < 8; ++uu) {
-        xv[uu] = sd[(j + uu) * L + tid];
-        yv[uu] = w ? w[l + 64 * (j + uu)] : 1.0f;
-      }
-#pragma unroll
-      for (int uu = 0; uu < 8; ++uu) a = __builtin_fmaf(xv[uu], yv[uu], a);
+    for (int q = 0; q < kPer; ++q) {
+      const int64_t e = j0 + kPer * tid + q;
+      v[q] = e < n ? (double)(wv(a.w, e) * s_d[kPer * tid + q]) : 0.0;
     }
-    for (; j < J; ++j) a = __builtin_fmaf(sd[j * L + tid], w ? w[l + 64 * j] : 1.0f, a);
-    acc_cur[t * 64 + l] = a;
+    block_prefix(v, pre, s_wave);
+    const int64_t last = min<int64_t>(n, j0 + kBlk) - 1 - j0;
+    if (tid == (int)(last / kPer)) a.fsum[cq][(int64_t)t * a.nblk + blk] = pre[last % kPer];
   }
+  const int64_t NB = min<int64_t>(kBlk, a.m1 - j0);
+  if (NB > 0 && a.T > 1 && wave == 0) {
+    const bool k4x2 = (a.T & 2) && t >= (a.T & ~3) && t < (a.T & ~3) + 2;
+    const float* wb = a.w ? a.w + j0 : nullptr;
+    float acc = 0.f;
+    if (k4x2) {  // 4 lanes (o % 4), product then add
+      if (lane < 4) {
+        int64_t o = lane;
+        for (; o + 28 < NB; o += 32) {
+          float x[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) x[q] = s_d[o + 4 * q] * (wb ? wb[o + 4 * q] : 1.0f);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc = acc + x[q];
+        }
+        for (; o < NB; o += 4) acc = acc + s_d[o] * (wb ? wb[o] : 1.0f);
+      }
+      const float a1 = __shfl(acc, 1), a2 = __shfl(acc, 2), a3 = __shfl(acc, 3);
+      if (lane == 0) a.vblk[cq][(int64_t)t * a.nblk + blk] = (acc + a1) + (a2 + a3);
+    } else {  // 8 lanes: the first NB&4 entries into lanes 0..3, then lane (o - (NB&4)) % 8; fma
+      const int64_t h4 = NB & 4;
+      if (lane < 8) {
+        if (lane < h4) acc = __builtin_fmaf(s_d[lane], wb ? wb[lane] : 1.0f, acc);
+        int64_t o = h4 + lane;
+        for (; o + 56 < NB; o += 64) {
+          float x[8], y[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            x[q] = s_d[o + 8 * q];
+            y[q] = wb ? wb[o + 8 * q] : 1.0f;
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc = __builtin_fmaf(x[q], y[q], acc);
+        }
+        for (; o < NB; o += 8) acc = __builtin_fmaf(s_d[o], wb ? wb[o] : 1.0f, acc);
+      }
+      const float ql = acc + __shfl(acc, (lane + 4) & 63);  // q_l = a_l + a_{l+4}
+      const float q1 = __shfl(ql, 1), q2 = __shfl(ql, 2), q3 = __shfl(ql, 3);
+      if (lane == 0) a.vblk[cq][(int64_t)t * a.nblk + blk] = (ql + q1) + (q2 + q3);
+    }
+  }
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 25);
 }
 
 // after the last round: its potentials, winner and centre
-__global__ __launch_bounds__(256) void k_kpp_round_final(
-    int64_t n, int dim, const float* __restrict__ X, const float* __restrict__ w,
-    const float* __restrict__ dist, const float* __restrict__ acc, int T, int c,
-    const int64_t* __restrict__ cand, float* __restrict__ centers, int64_t* __restrict__ indices) {
+__global__ __launch_bounds__(kThr) void k_kpp_final(KppArgs a, int c) {
   __shared__ float s_pot[kMaxTrials];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6;
-  for (int tr = wave; tr < T; tr += nw) {
-    const int64_t ri = (n & ~63ll) + lane;
-    const float rx = ri < n ? dist[(int64_t)tr * n + ri] : 0.f;
-    const float ry = ri < n ? (w ? w[ri] : 1.0f) : 0.f;
-    const float p = sdot_skx_finish_shfl(acc[tr * 64 + lane], rx, ry, n);
-    if (lane == 0) s_pot[tr] = p;
-  }
-  __syncthreads();
-  const int b = kpp_argmin(s_pot, T);
-  const int64_t src = cand[b];
-  if (tid == 0) indices[c] = src;
-  for (int j = tid; j < dim; j += blockDim.x) centers[(int64_t)c * dim + j] = X[src * dim + j];
+  const int q = c & 1;
+  const int b = fold_round(a, q, s_pot);
+  const int64_t src = a.cand[q][b];
+  if (threadIdx.x == 0) a.indices[c] = src;
+  for (int j = threadIdx.x; j < a.dim; j += kThr) a.centers[(int64_t)c * a.dim + j] = a.X[src * a.dim + j];
 }
 
-// ---- all rounds in one launch ------------------------------------------------------------------
-// The same two phases per round, inside one persistent launch of G*T workgroups (<= 256, one per
-// CU, so all are resident): every workgroup runs its slice of the distance phase, releases its
-// writes and arrives on a counter; the last arriver runs the tail (potentials, argmin, cumulative
-// potential, next candidates) and publishes the next round number; the others wait for it. This
-// removes two launch ramps and a dependent kernel boundary per round, but each round then pays two
-// agent-scope fences per workgroup; see the launcher for the measurement. Every wait is bounded:
-// a workgroup that waits too long sets `err` and leaves.
-struct KppSync {
-  unsigned int arrive;  // arrivals so far (NB per round)
-  unsigned int round;   // candidates published for this round
-  unsigned int err;
-  unsigned int pad;
-};
+// _euclidean_distances(C, X, squared=True) on its own (the distance of every round, exposed for
+// callers and for the element-wise parity tests of every summation-order mode)
+__global__ __launch_bounds__(kThr) void k_skl_sqdist(SklPlan p, const float* __restrict__ C,
+                                                     const float* __restrict__ X,
+                                                     float* __restrict__ out) {
+  extern __shared__ double s_c[];
+  __shared__ double s_cn;
+  const int t = blockIdx.y;
+  const float* ct = C + (int64_t)t * p.dim;
+  for (int j = threadIdx.x; j < p.dim; j += kThr) s_c[j] = (double)ct[j];
+  if (threadIdx.x == 0) s_cn = npy_sumsq_f64(ct, p.dim);
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kThr + threadIdx.x;
+  if (i >= p.n) return;
+  const float* xi = X + i * p.dim;
+  const double dot = skl_point_dot(p, s_c, xi, i, t);
+  float f = (float)(((-2.0 * dot) + s_cn) + npy_sumsq_f64(xi, p.dim));
+  out[(int64_t)t * p.n + i] = f < 0.f ? 0.f : f;
+}
 
-__device__ __forceinline__ bool kpp_wait_round(KppSync* sy, unsigned c) {
-  unsigned long long spins = 0;
-  while (__hip_atomic_load(&sy->round, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c) {
-    __builtin_amdgcn_s_sleep(1);
-    if (++spins > (1ull << 22)) return false;
+// ---- host side ------------------------------------------------------------------------------------
+int64_t skl_batch_size(int64_t nx, int64_t ny, int dim) {  // pairwise.py _euclidean_distances_upcast
+  double maxmem = (double)((nx + ny) * (int64_t)dim + nx * ny) / 10.0;
+  if (maxmem < 1310720.0) maxmem = 1310720.0;
+  const double tmp = 2.0 * dim;
+  const int64_t b = (int64_t)((-tmp + std::sqrt(tmp * tmp + 4.0 * maxmem)) / 2.0);
+  return b < 1 ? 1 : b;
+}
+
+// true when every element of a call with T candidate rows takes the plain chain
+bool skl_all_seq(int64_t n, int T, int dim, int64_t B) {
+  if (T == 1 || dim > 384) return false;
+  int64_t ms[2] = {std::min(n, B), n > B ? n % B : 0};
+  for (int64_t m : ms) {
+    if (m <= 0) continue;
+    if (m == 1) return false;
+    const double mnk = (double)m * T * dim;
+    if (mnk <= 1e6 && m * T <= 1200 && dim >= 32) return false;
+    const bool threaded = kBlasThreads >= 2 && mnk >= 524288.0;
+    if (!threaded && m > 192 && T >= 12 && (m & 7) != 0) return false;
   }
   return true;
-}
-
-// distance phase of workgroup (g, t): as k_kpp_dist with the chain distances in LDS
-__device__ void kpp_dist_phase(int64_t n, int dim, const float* __restrict__ X,
-                               const float* __restrict__ w, const double* __restrict__ xsq,
-                               const float* __restrict__ closest0, const float* __restrict__ dist_prev,
-                               const KppState* __restrict__ st, float* __restrict__ dist,
-                               float* __restrict__ acc, int L, int t, int g, double* s_c) {
-  const int tid = threadIdx.x;
-  const int64_t J = n >> 6, n64 = J << 6;
-  const int64_t nloc = (int64_t)L * J;
-  const int64_t ntot = nloc + (g == 0 ? n - n64 : 0);
-  const int best = st->best;
-  const int64_t ct = st->cand[t];
-  const double cn = xsq[ct];
-  const float* closest = best < 0 ? closest0 : dist_prev + (int64_t)best * n;
-  for (int j = tid; j < dim; j += blockDim.x) s_c[j] = (double)X[ct * dim + j];
-  __syncthreads();
-  float* sd = reinterpret_cast<float*>(s_c + dim);
-  float* drow = dist + (int64_t)t * n;
-  for (int64_t q = tid; q < ntot; q += blockDim.x) {
-    int64_t i;
-    if (q < nloc) {
-      const int64_t j = q / L;
-      i = (int64_t)g * L + (q - j * L) + 64 * j;
-    } else {
-      i = n64 + (q - nloc);
-    }
-    const float* xi = X + i * dim;
-    const double xs = xsq[i];
-    const float cl = closest[i];
-    double dot = 0.0;
-    int j = 0;
-    for (; j + 8 <= dim; j += 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = xi[j + u];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) dot = __builtin_fma(s_c[j + u], (double)v[u], dot);
-    }
-    for (; j < dim; ++j) dot = __builtin_fma(s_c[j], (double)xi[j], dot);
-    const double d = ((-2.0 * dot) + cn) + xs;
-    float f = (float)d;
-    f = f < 0.f ? 0.f : f;
-    f = np_minimum(cl, f);
-    drow[i] = f;
-    if (q < nloc) sd[q] = f;
-  }
-  __syncthreads();
-  if (tid < L) {
-    const int l = g * L + tid;
-    float a = 0.f;
-    int64_t j = 0;
-    for (; j + 8 <= J; j += 8) {
-      float xv[8], yv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        xv[u] = sd[(j + u) * L + tid];
-        yv[u] = w ? w[l + 64 * (j + u)] : 1.0f;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) a = __builtin_fmaf(xv[u], yv[u], a);
-    }
-    for (; j < J; ++j) a = __builtin_fmaf(sd[j * L + tid], w ? w[l + 64 * j] : 1.0f, a);
-    acc[t * 64 + l] = a;
-  }
-}
-
-// tail phase by one 256-thread workgroup (each thread owns <= kR consecutive points of a row)
-template <int kR>
-__device__ void kpp_tail_phase(int64_t n, int dim, const float* __restrict__ X,
-                               const float* __restrict__ w, const float* __restrict__ dist,
-                               const float* __restrict__ acc, int T, int c, int k,
-                               const double* __restrict__ uniforms, float* __restrict__ centers,
-                               int64_t* __restrict__ indices, KppState* __restrict__ st,
-                               float* s_pot, double* s_r, double* s_part, int* s_cnt) {
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6;
-  const bool more = c + 1 < k;
-  const double u_mine = (tid < T && more) ? uniforms[(int64_t)c * T + tid] : 0.0;
-  for (int tr = wave; tr < T; tr += nw) {
-    const int64_t ri = (n & ~63ll) + lane;
-    const float rx = ri < n ? dist[(int64_t)tr * n + ri] : 0.f;
-    const float ry = ri < n ? (w ? w[ri] : 1.0f) : 0.f;
-    const float p = sdot_skx_finish_shfl(acc[tr * 64 + lane], rx, ry, n);
-    if (lane == 0) s_pot[tr] = p;
-  }
-  __syncthreads();
-  int b = 0;  // np.argmin: first minimum; a NaN is returned as soon as it is met
-  for (int t = 1; t < T; ++t) {
-    const float pb = s_pot[b], pt = s_pot[t];
-    if (pb == pb && (pt < pb || pt != pt)) b = t;
-  }
-  const float pot = s_pot[b];
-  const int64_t src = st->cand[b];
-  for (int j = tid; j < dim; j += blockDim.x) centers[(int64_t)c * dim + j] = X[src * dim + j];
-  if (tid == 0) indices[c] = src;
-  if (!more) return;
-  if (tid < T) s_r[tid] = u_mine * (double)pot;
-  const int64_t chunk = (n + blockDim.x - 1) / blockDim.x;
-  const int64_t lo = min<int64_t>(n, tid * chunk), hi = min<int64_t>(n, lo + chunk);
-  const float* row = dist + (int64_t)b * n;
-  float pr[kR];
-#pragma unroll
-  for (int u = 0; u < kR; ++u) pr[u] = (lo + u < hi) ? (w ? w[lo + u] : 1.0f) * row[lo + u] : 0.f;
-  double run = 0.0;
-#pragma unroll
-  for (int u = 0; u < kR; ++u)
-    if (lo + u < hi) run = run + (double)pr[u];
-  double incl = run;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const double v = __shfl_up(incl, o);
-    if (lane >= o) incl += v;
-  }
-  if (lane == 63) s_part[wave] = incl;
-  __syncthreads();  // s_part, s_r; also every thread has read st->cand[b]
-  double base = incl - run;
-  for (int q = 0; q < wave; ++q) base += s_part[q];
-  double cu[kR];
-#pragma unroll
-  for (int u = 0; u < kR; ++u) {
-    base = base + (double)pr[u];
-    cu[u] = base;
-  }
-  for (int t = 0; t < T; ++t) {
-    const double r = s_r[t];
-    int cw = 0;
-#pragma unroll
-    for (int u = 0; u < kR; ++u) cw += __popcll(__ballot(lo + u < hi && cu[u] < r));
-    if (lane == 0) s_cnt[t * 4 + wave] = cw;
-  }
-  __syncthreads();
-  if (tid < T) {
-    int64_t a = 0;
-    for (int q = 0; q < nw; ++q) a += s_cnt[tid * 4 + q];
-    if (a > n - 1) a = n - 1;
-    st->cand[tid] = a;
-  }
-  if (tid == 0) {
-    st->best = b;
-    st->pot = pot;
-  }
-}
-
-template <int kR>
-__global__ __launch_bounds__(256) void k_kpp_rounds(
-    int64_t n, int dim, const float* __restrict__ X, const float* __restrict__ w,
-    const double* __restrict__ xsq, const float* __restrict__ closest0, float* __restrict__ dist0,
-    float* __restrict__ dist1, float* __restrict__ acc, int L, int G, int T, int k,
-    const double* __restrict__ uniforms, float* __restrict__ centers, int64_t* __restrict__ indices,
-    KppState* __restrict__ st, KppSync* __restrict__ sy) {
-  extern __shared__ double s_c[];
-  __shared__ float s_pot[kMaxTrials];
-  __shared__ double s_r[kMaxTrials];
-  __shared__ double s_part[4];
-  __shared__ int s_cnt[kMaxTrials * 4];
-  __shared__ int s_flag;
-  const int tid = threadIdx.x;
-  const int t = blockIdx.x / G, g = blockIdx.x - t * G;
-  const unsigned NB = gridDim.x;
-  for (int c = 1; c < k; ++c) {
-    if (c > 1) {
-      if (tid == 0) s_flag = kpp_wait_round(sy, (unsigned)c) ? 1 : 0;
-      __syncthreads();
-      if (!s_flag) {
-        if (tid == 0) atomicOr(&sy->err, 1u);
-        return;
-      }
-      __threadfence();  // acquire: the published candidates and the previous distance rows
-    }
-    const float* prev = ((c - 1) & 1) ? dist1 : dist0;
-    float* cur = (c & 1) ? dist1 : dist0;
-    kpp_dist_phase(n, dim, X, w, xsq, closest0, prev, st, cur, acc, L, t, g, s_c);
-    __threadfence();  // release this workgroup's distances and chain accumulators
-    __syncthreads();
-    if (tid == 0) s_flag = (atomicAdd(&sy->arrive, 1u) == (unsigned)c * NB - 1u) ? 1 : 0;
-    __syncthreads();
-    if (!s_flag) continue;
-    __threadfence();  // acquire every workgroup's writes of this round
-    kpp_tail_phase<kR>(n, dim, X, w, cur, acc, T, c, k, uniforms, centers, indices, st, s_pot, s_r,
-                       s_part, s_cnt);
-    __threadfence();  // release the next round's candidates
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(&sy->round, (unsigned)(c + 1), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-__global__ void k_ones(int64_t n, float* p) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) p[i] = 1.0f;
 }
 
 }  // namespace
@@ -1092,18 +735,34 @@ __global__ void k_ones(int64_t n, float* p) {
 
 using namespace gdd;
 
+extern "C" int gdd_skl_sqdist(int n_rows, const float* C, int64_t n, int dim, const float* X,
+                              float* out, gdd_stream_t stream) {
+  GDD_REQUIRE(n_rows >= 1 && n > 0 && dim > 0 && dim <= 4096, "skl_sqdist: invalid shape");
+  GDD_REQUIRE(n <= (int64_t)INT_MAX * kThr, "skl_sqdist: n too large");
+  GDD_REQUIRE(C && X && out, "skl_sqdist: null pointer");
+  SklPlan p{n, skl_batch_size(n_rows, n, dim), n_rows, dim, 0, 0};
+  p.all_seq = skl_all_seq(n, n_rows, dim, p.B) ? 1 : 0;
+  const size_t lds = sizeof(double) * (size_t)dim;
+  k_skl_sqdist<<<dim3((unsigned)((n + kThr - 1) / kThr), (unsigned)n_rows), kThr, lds,
+                 to_hip(stream)>>>(p, C, X, out);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
 extern "C" size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int n_trials) {
+  const size_t T = (size_t)std::max(n_trials, 1);
+  const size_t nblk = (size_t)((n + kBlk - 1) / kBlk);
   size_t b = 0;
   b += align256(sizeof(KppState));
-  b += align256(sizeof(double) * n);                                        // xsq
-  b += align256(sizeof(float) * n);                                         // closest0
-  b += 2 * align256(sizeof(float) * n * (size_t)std::max(n_trials, 1));     // dist ping-pong
-  b += align256(sizeof(double) * n);                                        // cum
-  b += 2 * align256(sizeof(float) * 64 * (size_t)std::max(n_trials, 1));   // lane accumulators
-  b += 2 * align256(sizeof(int64_t) * kMaxTrials);                          // round candidates
-  b += align256(sizeof(KppSync));
-  b += align256(sizeof(KppSpec));
-  return b + 2048;
+  b += align256(sizeof(double) * n);          // xsq
+  b += align256(sizeof(float) * n);           // closest0
+  b += align256(sizeof(double) * nblk);       // fsum0
+  b += 2 * align256(sizeof(float) * n * T);   // dist ping-pong
+  b += 2 * align256(sizeof(float) * nblk * T);    // vblk
+  b += 2 * align256(sizeof(double) * nblk * T);   // fsum
+  b += 2 * align256(sizeof(int64_t) * kMaxTrials);
+  b += align256(sizeof(float) * 2);           // pot1
+  return b + 1024;
 }
 
 extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const float* w, int k,
@@ -1115,123 +774,63 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   GDD_REQUIRE(n_trials >= 1 && n_trials <= kMaxTrials, "kmeans++: n_trials=%d unsupported",
               n_trials);
   GDD_REQUIRE(dim <= 4096, "kmeans++: dim=%d unsupported", dim);
+  GDD_REQUIRE(n < (int64_t)INT_MAX * kBlk, "kmeans++: n=%lld too large", (long long)n);
   GDD_REQUIRE(first_id >= 0 && first_id < n, "kmeans++: first_id out of range");
   GDD_REQUIRE(X && centers && indices && ws && (k == 1 || uniforms), "kmeans++: null pointer");
   hipStream_t s = to_hip(stream);
+  const int T = n_trials;
+  const int nblk = (int)((n + kBlk - 1) / kBlk);
   Carver cv(ws, ws_bytes);
+  KppArgs a{};
   KppState* st = cv.take<KppState>(1);
   double* xsq = cv.take<double>(n);
   float* closest0 = cv.take<float>(n);
-  float* dist[2] = {cv.take<float>(n * (size_t)n_trials), cv.take<float>(n * (size_t)n_trials)};
-  double* cum = cv.take<double>(n);
-  float* acc = cv.take<float>(64 * (size_t)n_trials);
-  float* acc2 = cv.take<float>(64 * (size_t)n_trials);
-  int64_t* candb[2] = {cv.take<int64_t>(kMaxTrials), cv.take<int64_t>(kMaxTrials)};
-  KppSync* sy = cv.take<KppSync>(1);
-  KppSpec* sp = cv.take<KppSpec>(1);
+  double* fsum0 = cv.take<double>(nblk);
+  for (int q = 0; q < 2; ++q) a.dist[q] = cv.take<float>(n * (size_t)T);
+  for (int q = 0; q < 2; ++q) a.vblk[q] = cv.take<float>((size_t)nblk * T);
+  for (int q = 0; q < 2; ++q) a.fsum[q] = cv.take<double>((size_t)nblk * T);
+  for (int q = 0; q < 2; ++q) a.cand[q] = cv.take<int64_t>(kMaxTrials);
+  a.pot1 = cv.take<float>(2);
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans++: workspace too small");
-  const unsigned nb = (unsigned)((n + 255) / 256);
-  // w == nullptr: unit sample weights, handled in the kernels
-  k_kpp_init<<<nb, 256, 0, s>>>(n, dim, X, first_id, xsq, closest0);
-  GDD_LAUNCHED();
-  k_kpp_tail<<<1, kTailThreads, 0, s>>>(n, dim, X, w, closest0, dist[1], acc, n_trials, 0, k,
-                                        first_id, uniforms, xsq, cum, centers, indices, st);
-  GDD_LAUNCHED();
-  // lanes per distance block: about one point per thread (L * J ~ 256), L a power of two
-  const int64_t J = n >> 6;
-  int L = 64;
-  while (L > 1 && (int64_t)L * J > 256) L >>= 1;
-  const int G = 64 / L;
-  // the block's chain distances stay in LDS when they fit next to the candidate row
-  const size_t lds_chain = sizeof(double) * (size_t)dim + sizeof(float) * (size_t)L * J;
-  const int chain_in_lds = lds_chain <= 65536 ? 1 : 0;
-  const size_t lds = chain_in_lds ? lds_chain : sizeof(double) * (size_t)dim;
-  if (lds > 65536)
-    GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dist<false>,
+  a.n = n;
+  a.m1 = n & ~3ll;
+  a.dim = dim;
+  a.T = T;
+  a.nblk = nblk;
+  a.nsg = (int)((a.m1 + kBlk - 1) / kBlk);
+  a.X = X;
+  a.w = w;
+  a.xsq = xsq;
+  a.closest0 = closest0;
+  a.fsum0 = fsum0;
+  a.uniforms = uniforms;
+  a.st = st;
+  a.centers = centers;
+  a.indices = indices;
+  a.plan = SklPlan{n, skl_batch_size(T, n, dim), T, dim, 0, 0};
+  a.plan.all_seq = skl_all_seq(n, T, dim, a.plan.B) ? 1 : 0;
+  const SklPlan p1{n, skl_batch_size(1, n, dim), 1, dim, 0, 0};
+  const size_t lds = sizeof(double) * (size_t)dim + sizeof(float) * kBlk;
+  if (lds > 65536) {
+    GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_init,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  // all rounds in one persistent launch (opt-in, GDD_KPP_PERSISTENT=1): measured 31 us per round
-  // at the arxiv shape against 13 us for the two launches below — the agent-scope fences each
-  // workgroup needs per round (L2 write-back + invalidate on gfx950) cost more than the launch
-  // boundaries they replace. Kept for the handoff work that would make it pay (sc1 granules).
-  const int NB = G * n_trials;
-  if (k > 1 && NB <= 256 && chain_in_lds && (n + 255) / 256 <= 16 &&
-      getenv("GDD_KPP_PERSISTENT") != nullptr) {
-    GDD_HIP(hipMemsetAsync(sy, 0, sizeof(KppSync), s));
-    if (lds > 65536)
-      GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_rounds<16>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    k_kpp_rounds<16><<<NB, 256, lds, s>>>(n, dim, X, w, xsq, closest0, dist[0], dist[1], acc, L, G,
-                                          n_trials, k, uniforms, centers, indices, st, sy);
-    GDD_LAUNCHED();
-    return GDD_OK;
+    GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_round,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   }
-  // one launch per round (k_kpp_round) when a 256-thread workgroup scans the winner's row in
-  // <= 16 entries per thread
-  if (k > 1 && chain_in_lds && (n + 255) / 256 <= 16 && getenv("GDD_KPP_SPEC") == nullptr) {
-    float* accb[2] = {acc, acc2};
-    // opt-in (GDD_KPP_PREFETCH=1): the point rows requested into registers at the start of the
-    // round. Measured slower at the arxiv shape (13.7 vs 12.6 ms per fit): the extra in-flight
-    // loads delay the critical potential/winner-row requests more than they hide.
-    const bool pre = (int64_t)L * J + (n - (J << 6)) <= 256 && dim <= 64 && dim % 4 == 0 &&
-                     (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
-                     getenv("GDD_KPP_PREFETCH") != nullptr;
-    auto kern = pre ? k_kpp_round<16, 64> : k_kpp_round<16, 0>;
-    if (lds > 65536)
-      GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds));
-    for (int c = 1; c < k; ++c) {
-      kern<<<dim3(G, n_trials), 256, lds, s>>>(
-          n, dim, X, w, xsq, closest0, dist[(c - 1) & 1], dist[c & 1], accb[(c - 1) & 1],
-          accb[c & 1], L, n_trials, c, uniforms, st, candb[(c - 1) & 1], candb[c & 1], centers,
-          indices);
-      GDD_LAUNCHED();
-    }
-    k_kpp_round_final<<<1, 256, 0, s>>>(n, dim, X, w, dist[(k - 1) & 1], accb[(k - 1) & 1],
-                                        n_trials, k - 1, candb[(k - 1) & 1], centers, indices);
-    GDD_LAUNCHED();
-    return GDD_OK;
-  }
-  // speculative draws: per round one distance launch and one per-trial tail launch (T workgroups)
-  constexpr int kSpecR = 8;
-  if (k > 1 && chain_in_lds && (n + kTailThreads - 1) / kTailThreads <= kSpecR) {
-    k_kpp_spec_seed<<<1, 64, 0, s>>>(st, n_trials, sp);
-    GDD_LAUNCHED();
-    if (lds > 65536)
-      GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dist_spec,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    for (int c = 1; c < k; ++c) {
-      const float* prev = dist[(c - 1) & 1];
-      float* cur = dist[c & 1];
-      k_kpp_dist_spec<<<dim3(G, n_trials), 256, lds, s>>>(n, dim, X, w, xsq, closest0, prev, sp, cur,
-                                                          acc, L, n_trials, c, centers, indices);
-      GDD_LAUNCHED();
-      k_kpp_trial_tail<kSpecR><<<n_trials, kTailThreads, 0, s>>>(n, w, cur, acc, n_trials, c, k,
-                                                                 uniforms, sp);
-      GDD_LAUNCHED();
-    }
-    k_kpp_spec_finish<<<1, 256, 0, s>>>(dim, X, sp, n_trials, k - 1, centers, indices);
-    GDD_LAUNCHED();
-    return GDD_OK;
-  }
-  constexpr int kFastT = 12, kFastR = 4;
-  const bool fast_tail = n_trials <= kFastT && (n + kTailThreads - 1) / kTailThreads <= kFastR;
+  k_kpp_init<<<nblk, kThr, lds, s>>>(a, p1, first_id, xsq, closest0, fsum0);
+  GDD_LAUNCHED();
+  k_kpp_first<<<1, 64, 0, s>>>(n, dim, X, w, closest0, first_id, st, centers, indices);
+  GDD_LAUNCHED();
+  if (k == 1) return GDD_OK;
   for (int c = 1; c < k; ++c) {
-    const float* prev = dist[(c - 1) & 1];
-    float* cur = dist[c & 1];
-    if (chain_in_lds)
-      k_kpp_dist<true><<<dim3(G, n_trials), 256, lds, s>>>(n, dim, X, w, xsq, closest0, prev, st,
-                                                           cur, acc, L);
-    else
-      k_kpp_dist<false><<<dim3(G, n_trials), 256, lds, s>>>(n, dim, X, w, xsq, closest0, prev, st,
-                                                            cur, acc, L);
+    k_kpp_round<<<dim3(nblk, T), kThr, lds, s>>>(a, c);
     GDD_LAUNCHED();
-    if (fast_tail)
-      k_kpp_tail_fast<kFastT, kFastR><<<1, kTailThreads, 0, s>>>(n, dim, X, w, cur, acc, n_trials, c,
-                                                                 k, uniforms, centers, indices, st);
-    else
-      k_kpp_tail<<<1, kTailThreads, 0, s>>>(n, dim, X, w, closest0, cur, acc, n_trials, c, k,
-                                            first_id, uniforms, xsq, cum, centers, indices, st);
-    GDD_LAUNCHED();
+    if (T == 1) {
+      k_kpp_pot1<<<1, 64, 0, s>>>(n, a.dist[c & 1], w, a.pot1 + (c & 1));
+      GDD_LAUNCHED();
+    }
   }
+  k_kpp_final<<<1, kThr, 0, s>>>(a, k - 1);
+  GDD_LAUNCHED();
   return GDD_OK;
 }

@@ -29,7 +29,7 @@ int fail(int code, const char* fmt, ...) {
 
 size_t scan_i32_ws_bytes(int64_t n) {
   size_t bytes = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
                                    (int)n);
   return align256(bytes);
 }
@@ -45,7 +45,7 @@ int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, void* ws, siz
 
 size_t sort_pairs_ws_bytes(int64_t n) {
   size_t bytes = 0;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
                                      (const int32_t*)nullptr, (int32_t*)nullptr, (int)n);
   return align256(bytes);
 }

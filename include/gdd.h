@@ -221,13 +221,21 @@ int gdd_labels_changed(int64_t n, const int32_t* labels, int32_t* labels_old, in
 /* Greedy k-means++ seeding, sklearn _kmeans_plusplus (sklearn/cluster/_kmeans.py:174-272) on the    */
 /* device. Host supplies the reference RNG draws: first_id (random_state.choice) and                 */
 /* uniforms[(k-1) * n_trials] (random_state.uniform(size=n_trials) per center, concatenated).        */
-/* Distances: fp64 upcast -2<x_c,x> + |x_c|^2 + |x|^2, stored fp32, clipped at 0 (pairwise.py:582-650). */
-/* Potentials: fp32 sums (see DESIGN.md for their order). Writes centers (k x dim) and indices.      */
+/* Distances: fp64 upcast -2<x_c,x> + |x_c|^2 + |x|^2, stored fp32, clipped at 0 (pairwise.py:582-650), */
+/* in OpenBLAS's per-shape summation orders (gdd_skl_sqdist). Potentials: the first as sdot, the     */
+/* trials' as sgemv_t (_kmeans.py:239-251). Writes centers (k x dim) and indices. 1 <= n_trials <= 16. */
 /* ---------------------------------------------------------------------------------------------- */
 size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int n_trials);
 int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const float* w, int k, int n_trials,
                         int64_t first_id, const double* uniforms, float* centers, int64_t* indices,
                         void* ws, size_t ws_bytes, gdd_stream_t stream);
+
+/* sklearn.metrics.pairwise._euclidean_distances(C, X, squared=True) for fp32 C (n_rows x dim) and X  */
+/* (n x dim), as scikit-learn 1.7.2 computes it for k-means++ (_kmeans.py:229, 245): X in chunks of   */
+/* batch_size rows upcast to fp64, numpy einsum norms, the OpenBLAS 0.3.29 SkylakeX summation order of */
+/* each chunk's product, fp32, max(., 0). out: n_rows x n. Device pointers.                            */
+int gdd_skl_sqdist(int n_rows, const float* C, int64_t n, int dim, const float* X, float* out,
+                   gdd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* (a8) StandardScaler(with_mean=True, with_std=True).fit_transform(X) on fp32 X                    */

@@ -1,0 +1,92 @@
+"""Edge cases of the k-means kernels and fits (GPU vs the oracle, bit-exact).
+
+Shapes the reference's inputs can take but the main tests do not: a single sample or centre,
+partial 32-row tiles, dim 1 and the 512 maximum, duplicated rows (distance ties), k = n,
+batch larger than n, reassignment disabled, early stopping disabled (max_no_improvement=None).
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import bits
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+import gdd  # noqa: E402
+from gdd import synth  # noqa: E402
+from gdd.kmeans import _Ops  # noqa: E402
+
+
+@pytest.mark.parametrize("n,dim,k", [(1, 3, 1), (31, 5, 4), (33, 1, 33), (200, 512, 7),
+                                     (1000, 40, 1), (4097, 2, 600)])
+def test_assign_edges(n, dim, k):
+    rng = np.random.default_rng(n + dim + k)
+    X = rng.standard_normal((n, dim)).astype(np.float32)
+    C = X[rng.choice(n, size=k, replace=k > n)].copy() if k <= n else rng.standard_normal((k, dim)).astype(np.float32)
+    lab_ref, sq_ref = O.assign(X, C)
+    Xd, Cd = torch.from_numpy(X).cuda(), torch.from_numpy(C).cuda()
+    lab = torch.empty(n, dtype=torch.int32, device="cuda")
+    sq = torch.empty(n, dtype=torch.float32, device="cuda")
+    _Ops("cuda", n, k, dim).assign(Xd, Cd, labels=lab, sq=sq)
+    assert np.array_equal(lab.cpu().numpy(), lab_ref)
+    assert np.array_equal(bits(sq.cpu().numpy()), bits(sq_ref))
+
+
+def test_assign_ties_between_tiles_and_zero_signs():
+    # identical centres in different 32-centre tiles and chunks: the lowest index must win, also
+    # when the distance is exactly zero (the packed key treats -0.0 and +0.0 as one value)
+    rng = np.random.default_rng(1)
+    base = rng.standard_normal((5, 16)).astype(np.float32)
+    C = np.tile(base, (140, 1))  # 700 centres, every row repeated 140 times
+    X = np.concatenate([base, np.zeros((3, 16), np.float32), base * 0.5]).astype(np.float32)
+    lab_ref, sq_ref = O.assign(X, C)
+    lab = torch.empty(X.shape[0], dtype=torch.int32, device="cuda")
+    sq = torch.empty(X.shape[0], dtype=torch.float32, device="cuda")
+    _Ops("cuda", X.shape[0], C.shape[0], 16).assign(torch.from_numpy(X).cuda(),
+                                                     torch.from_numpy(C).cuda(), labels=lab, sq=sq)
+    assert np.array_equal(lab.cpu().numpy(), lab_ref)
+    assert lab_ref.max() < 5
+
+
+@pytest.mark.parametrize("n,dim,k,n_init", [(50, 4, 50, 1), (300, 3, 12, 2), (64, 1, 5, 1)])
+def test_kmeans_edges(n, dim, k, n_init):
+    X = synth.blobs(n, dim, max(1, k // 3), seed=n)
+    X[1::7] = X[0]  # duplicated rows
+    np.random.seed(3)
+    ref = O.kmeans(X, k, n_init=n_init)
+    np.random.seed(3)
+    m = gdd.KMeans(n_clusters=k, n_init=n_init).fit(X)
+    assert m.n_iter_ == ref["n_iter_"]
+    assert np.array_equal(m.labels_, ref["labels_"])
+    assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"]))
+
+
+@pytest.mark.parametrize("kw", [dict(batch_size=5000), dict(reassignment_ratio=0.0),
+                                dict(max_no_improvement=None, max_iter=3), dict(n_clusters=1),
+                                dict(init_size=40)])
+def test_minibatch_edges(kw):
+    n, dim = 3000, 9
+    X = synth.blobs(n, dim, 20, seed=2)
+    args = dict(n_clusters=20, random_state=7, batch_size=256)
+    args.update(kw)
+    ref = O.minibatch_kmeans(X, args.pop("n_clusters"), **args)
+    args = dict(n_clusters=20, random_state=7, batch_size=256)
+    args.update(kw)
+    m = gdd.MiniBatchKMeans(**args).fit(X)
+    assert m.n_steps_ == ref["n_steps_"]
+    assert np.array_equal(m.labels_, ref["labels_"])
+    assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"]))
+    assert m.inertia_ == ref["inertia_"]
+
+
+def test_cluster_mean_single_cluster_and_mostly_empty():
+    feat = synth.features(1000, 33, 4)
+    for lab in (np.zeros(1000, np.int32), np.full(1000, 6, np.int32)):
+        ref, cnt_ref = O.cluster_mean(feat, lab, 9)
+        out, cnt = gdd.cluster_mean(torch.from_numpy(feat).cuda(), lab, 9)
+        assert np.array_equal(cnt.cpu().numpy(), cnt_ref)
+        o = out.cpu().numpy()
+        assert np.array_equal(np.isnan(o), np.isnan(ref))
+        m = ~np.isnan(ref)
+        assert np.array_equal(bits(o[m]), bits(ref[m]))
