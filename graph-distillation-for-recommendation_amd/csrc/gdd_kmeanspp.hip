@@ -42,8 +42,9 @@ namespace {
 
 constexpr int kMaxTrials = 16;
 constexpr int kBlk = 4096;               // sgemv_t NBMAX and the cumulative-potential block
-constexpr int kThr = 256;
-constexpr int kPer = kBlk / kThr;        // 16 entries per thread
+constexpr int kThr = 1024;               // 16 waves: one workgroup per (block, trial)
+constexpr int kWaves = kThr / 64;
+constexpr int kPer = kBlk / kThr;        // 4 entries per thread
 constexpr int kBlasThreads = 8;          // OpenBLAS threads of the pinned reference run
 
 struct KppState {
@@ -335,13 +336,88 @@ __device__ __forceinline__ double skl_point_dot(const SklPlan& p, const double* 
   return skl_dot(c, x, p.dim, mode, sp);
 }
 
+// the plain k-ordered fp64 chains of the kPer points tid + kThr * q of the block at j0 against the
+// staged candidate s_c (all_seq plans): the points' chains are interleaved and each step's loads for
+// all of them are in flight together (float4 when rows are 16-byte aligned)
+__device__ __forceinline__ void seq_dots(const float* __restrict__ X, int dim, int64_t n, int64_t j0,
+                                         const double* __restrict__ s_c, double (&dot)[kPer]) {
+  const int tid = threadIdx.x;
+  const float* xr[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int64_t i = j0 + tid + kThr * q;
+    xr[q] = X + (i < n ? i : j0) * (int64_t)dim;
+    dot[q] = 0.0;
+  }
+  int j = 0;
+  if ((dim & 3) == 0 && ((uintptr_t)X & 15) == 0) {
+    for (; j + 8 <= dim; j += 8) {
+      float4 u0[kPer], u1[kPer];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        u0[q] = *reinterpret_cast<const float4*>(xr[q] + j);
+        u1[q] = *reinterpret_cast<const float4*>(xr[q] + j + 4);
+      }
+      const double c0 = s_c[j], c1 = s_c[j + 1], c2 = s_c[j + 2], c3 = s_c[j + 3];
+      const double c4 = s_c[j + 4], c5 = s_c[j + 5], c6 = s_c[j + 6], c7 = s_c[j + 7];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        double d = dot[q];
+        d = __builtin_fma(c0, (double)u0[q].x, d);
+        d = __builtin_fma(c1, (double)u0[q].y, d);
+        d = __builtin_fma(c2, (double)u0[q].z, d);
+        d = __builtin_fma(c3, (double)u0[q].w, d);
+        d = __builtin_fma(c4, (double)u1[q].x, d);
+        d = __builtin_fma(c5, (double)u1[q].y, d);
+        d = __builtin_fma(c6, (double)u1[q].z, d);
+        d = __builtin_fma(c7, (double)u1[q].w, d);
+        dot[q] = d;
+      }
+    }
+    if (j + 4 <= dim) {
+      float4 u0[kPer];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) u0[q] = *reinterpret_cast<const float4*>(xr[q] + j);
+      const double c0 = s_c[j], c1 = s_c[j + 1], c2 = s_c[j + 2], c3 = s_c[j + 3];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        double d = dot[q];
+        d = __builtin_fma(c0, (double)u0[q].x, d);
+        d = __builtin_fma(c1, (double)u0[q].y, d);
+        d = __builtin_fma(c2, (double)u0[q].z, d);
+        d = __builtin_fma(c3, (double)u0[q].w, d);
+        dot[q] = d;
+      }
+      j += 4;
+    }
+  }
+  for (; j + 4 <= dim; j += 4) {
+    float u[kPer][4];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) u[q][v] = xr[q][j + v];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const double cv = s_c[j + v];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) dot[q] = __builtin_fma(cv, (double)u[q][v], dot[q]);
+    }
+  }
+  for (; j < dim; ++j) {
+    const double cv = s_c[j];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) dot[q] = __builtin_fma(cv, (double)xr[q][j], dot[q]);
+  }
+}
+
 // ---- the block-wise fp64 cumulative potential ----------------------------------------------------
 // prefix(e) of entry e = 16*tid + u of a block: thread-sequential running sum r_u, the exclusive
 // shuffle scan E of the thread totals inside the wave, the wave totals added in wave order B:
 // prefix = (B + E) + r_u. Both the producer of a block's total and the searches use this function,
 // so a block's total equals the prefix of its last entry bit for bit.
 __device__ __forceinline__ void block_prefix(const double (&v)[kPer], double (&pre)[kPer],
-                                             double* s_wave /* 4 */) {
+                                             double* s_wave /* kWaves */) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double r[kPer];
   double run = 0.0;
@@ -439,7 +515,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_init(KppArgs a, SklPlan p1, int64_
                                                    float* __restrict__ closest_out,
                                                    double* __restrict__ fsum_out) {
   extern __shared__ double s_c[];  // dim doubles, then the block's distances (fp32)
-  __shared__ double s_wave[4];
+  __shared__ double s_wave[kWaves];
   __shared__ double s_sc;
   const int tid = threadIdx.x;
   const int64_t j0 = (int64_t)blockIdx.x * kBlk;
@@ -499,14 +575,112 @@ __global__ void k_kpp_pot1(int64_t n, const float* __restrict__ row, const float
   if (threadIdx.x == 0) *out = p;
 }
 
+// ---- distances of one block's points to the staged candidate s_c (|c|^2 = cn), np.minimum with
+// the winner's row; written to drow (global) and s_d (LDS, block order)
+template <bool SEQ>
+__device__ __forceinline__ void block_dists(const KppArgs& a, int t, int64_t j0, double cn,
+                                            const double* __restrict__ s_c,
+                                            const float* __restrict__ wrow, float* __restrict__ drow,
+                                            float* __restrict__ s_d) {
+  const int tid = threadIdx.x;
+  const int64_t n = a.n;
+  if constexpr (SEQ) {
+    double dot[kPer];
+    seq_dots(a.X, a.dim, n, j0, s_c, dot);
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int o = tid + kThr * q;
+      const int64_t i = j0 + o;
+      float f = 0.f;
+      if (i < n) {
+        f = (float)(((-2.0 * dot[q]) + cn) + a.xsq[i]);
+        f = f < 0.f ? 0.f : f;
+        f = np_minimum(wrow[i], f);
+        drow[i] = f;
+      }
+      s_d[o] = f;
+    }
+  } else {
+#pragma unroll 1
+    for (int q = 0; q < kPer; ++q) {
+      const int o = tid + kThr * q;
+      const int64_t i = j0 + o;
+      float f = 0.f;
+      if (i < n) {
+        const float* xi = a.X + i * a.dim;
+        const double dot = skl_point_dot(a.plan, s_c, xi, i, t);
+        f = (float)(((-2.0 * dot) + cn) + a.xsq[i]);
+        f = f < 0.f ? 0.f : f;
+        f = np_minimum(wrow[i], f);
+        drow[i] = f;
+      }
+      s_d[o] = f;
+    }
+  }
+}
+
+// sgemv_t block result of trial t over the NB (> 0) entries of s_d (weights wb, nullptr: ones), run by
+// one wave; lane 0 returns it
+__device__ float sgemv_block_wave(const float* __restrict__ s_d, const float* __restrict__ wb,
+                                  int64_t NB, int t, int T) {
+  const int lane = threadIdx.x & 63;
+  const bool k4x2 = (T & 2) && t >= (T & ~3) && t < (T & ~3) + 2;
+  float acc = 0.f;
+  if (k4x2) {  // 4 lanes (o % 4), product then add
+    if (lane < 4) {
+      int64_t o = lane;
+      for (; o + 28 < NB; o += 32) {
+        float x[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] = s_d[o + 4 * q] * (wb ? wb[o + 4 * q] : 1.0f);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc = acc + x[q];
+      }
+      for (; o < NB; o += 4) acc = acc + s_d[o] * (wb ? wb[o] : 1.0f);
+    }
+    const float a1 = __shfl(acc, 1), a2 = __shfl(acc, 2), a3 = __shfl(acc, 3);
+    return (acc + a1) + (a2 + a3);
+  }
+  // 8 lanes: the first NB&4 entries into lanes 0..3, then lane (o - (NB&4)) % 8; fma
+  const int64_t h4 = NB & 4;
+  if (lane < 8) {
+    if (lane < h4) acc = __builtin_fmaf(s_d[lane], wb ? wb[lane] : 1.0f, acc);
+    int64_t o = h4 + lane;
+    if (!wb) {  // unit weights: fma(x, 1, acc) == acc + x; 32 LDS reads ahead of the chain
+      for (; o + 8 * 31 < NB; o += 256) {
+        float x[32];
+#pragma unroll
+        for (int q = 0; q < 32; ++q) x[q] = s_d[o + 8 * q];
+#pragma unroll
+        for (int q = 0; q < 32; ++q) acc = acc + x[q];
+      }
+    }
+    for (; o + 56 < NB; o += 64) {
+      float x[8], y[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        x[q] = s_d[o + 8 * q];
+        y[q] = wb ? wb[o + 8 * q] : 1.0f;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc = __builtin_fmaf(x[q], y[q], acc);
+    }
+    for (; o < NB; o += 8) acc = __builtin_fmaf(s_d[o], wb ? wb[o] : 1.0f, acc);
+  }
+  const float ql = acc + __shfl(acc, (lane + 4) & 63);  // q_l = a_l + a_{l+4}
+  const float q1 = __shfl(ql, 1), q2 = __shfl(ql, 2), q3 = __shfl(ql, 3);
+  return (ql + q1) + (q2 + q3);
+}
+
 // ---- one seeding round ------------------------------------------------------------------------------
+template <bool SEQ>
 __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   extern __shared__ double s_c[];  // dim doubles, then the block's distances (fp32)
   __shared__ float s_pot[kMaxTrials];
-  __shared__ double s_wave[4];
+  __shared__ double s_wave[kWaves];
   __shared__ int s_jmin;
   __shared__ double s_P;
-  __shared__ int s_cnt[kThr / 64];
+  __shared__ int s_cnt[kWaves];
   const int t = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int pq = (c - 1) & 1, cq = c & 1;
@@ -586,7 +760,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     if (lane == 0) s_cnt[wave] = cw;
     __syncthreads();
     int64_t cnt = 0;
-    for (int q = 0; q < kThr / 64; ++q) cnt += s_cnt[q];
+    for (int q = 0; q < kWaves; ++q) cnt += s_cnt[q];
     ct = min<int64_t>(n - 1, (int64_t)jb * kBlk + cnt);
   }
   if (blk == 0 && tid == 0) a.cand[cq][t] = ct;
@@ -603,21 +777,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   float* s_d = reinterpret_cast<float*>(s_c + a.dim);
   const int64_t j0 = (int64_t)blk * kBlk;
   float* drow = a.dist[cq] + (int64_t)t * n;
-#pragma unroll 1
-  for (int q = 0; q < kPer; ++q) {
-    const int o = tid + kThr * q;
-    const int64_t i = j0 + o;
-    float f = 0.f;
-    if (i < n) {
-      const float* xi = a.X + i * a.dim;
-      const double dot = skl_point_dot(a.plan, s_c, xi, i, t);
-      f = (float)(((-2.0 * dot) + cn) + a.xsq[i]);
-      f = f < 0.f ? 0.f : f;
-      f = np_minimum(wrow[i], f);
-      drow[i] = f;
-    }
-    s_d[o] = f;
-  }
+  block_dists<SEQ>(a, t, j0, cn, s_c, wrow, drow, s_d);
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 24);
   // ---- the block's terms for round c+1: cumulative total, sgemv_t lane chains
@@ -634,46 +794,11 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   }
   const int64_t NB = min<int64_t>(kBlk, a.m1 - j0);
   if (NB > 0 && a.T > 1 && wave == 0) {
-    const bool k4x2 = (a.T & 2) && t >= (a.T & ~3) && t < (a.T & ~3) + 2;
-    const float* wb = a.w ? a.w + j0 : nullptr;
-    float acc = 0.f;
-    if (k4x2) {  // 4 lanes (o % 4), product then add
-      if (lane < 4) {
-        int64_t o = lane;
-        for (; o + 28 < NB; o += 32) {
-          float x[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) x[q] = s_d[o + 4 * q] * (wb ? wb[o + 4 * q] : 1.0f);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) acc = acc + x[q];
-        }
-        for (; o < NB; o += 4) acc = acc + s_d[o] * (wb ? wb[o] : 1.0f);
-      }
-      const float a1 = __shfl(acc, 1), a2 = __shfl(acc, 2), a3 = __shfl(acc, 3);
-      if (lane == 0) a.vblk[cq][(int64_t)t * a.nblk + blk] = (acc + a1) + (a2 + a3);
-    } else {  // 8 lanes: the first NB&4 entries into lanes 0..3, then lane (o - (NB&4)) % 8; fma
-      const int64_t h4 = NB & 4;
-      if (lane < 8) {
-        if (lane < h4) acc = __builtin_fmaf(s_d[lane], wb ? wb[lane] : 1.0f, acc);
-        int64_t o = h4 + lane;
-        for (; o + 56 < NB; o += 64) {
-          float x[8], y[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            x[q] = s_d[o + 8 * q];
-            y[q] = wb ? wb[o + 8 * q] : 1.0f;
-          }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) acc = __builtin_fmaf(x[q], y[q], acc);
-        }
-        for (; o < NB; o += 8) acc = __builtin_fmaf(s_d[o], wb ? wb[o] : 1.0f, acc);
-      }
-      const float ql = acc + __shfl(acc, (lane + 4) & 63);  // q_l = a_l + a_{l+4}
-      const float q1 = __shfl(ql, 1), q2 = __shfl(ql, 2), q3 = __shfl(ql, 3);
-      if (lane == 0) a.vblk[cq][(int64_t)t * a.nblk + blk] = (ql + q1) + (q2 + q3);
-    }
+    const float v = sgemv_block_wave(s_d, a.w ? a.w + j0 : nullptr, NB, t, a.T);
+    if (lane == 0) a.vblk[cq][(int64_t)t * a.nblk + blk] = v;
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 25);
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0 && c < 128), 128 + c);
 }
 
 // after the last round: its potentials, winner and centre
@@ -684,6 +809,298 @@ __global__ __launch_bounds__(kThr) void k_kpp_final(KppArgs a, int c) {
   const int64_t src = a.cand[q][b];
   if (threadIdx.x == 0) a.indices[c] = src;
   for (int j = threadIdx.x; j < a.dim; j += kThr) a.centers[(int64_t)c * a.dim + j] = a.X[src * a.dim + j];
+}
+
+// ---- single-block rounds (n <= 4096, T >= 2: MiniBatchKMeans' init subset, small KMeans) ---------
+// Two launches per round, each moving little data through any one CU (a CU pulls only ~35-70 GB/s
+// from L2/Infinity Cache, so staging T rows in one workgroup costs microseconds):
+//   k_kpp1_dist (round c)  points x trial-groups over many workgroups: reads round c-1's T
+//       potentials and the T x T table of "candidates if trial t wins", takes np.argmin, and computes
+//       its 64 points' distances to this round's T candidates, np.minimum with the winner's row.
+//   k_kpp1_pick (round c)  one workgroup per trial: stages the trial's row, runs its sgemv_t lane
+//       chains (the exact potential), its fp64 cumulative potential, and counts the candidates every
+//       trial would draw in round c+1 if this trial wins (the uniforms are known in advance).
+// Round 0 (the first centre) is a pick over closest0 with the sdot potential. After round k-1,
+// k_kpp1_final takes the last argmin.
+constexpr int kTg = 2;       // trials per thread in the distance phase
+constexpr int kPts = 64;     // points per distance workgroup (one per lane; waves = trial groups)
+
+struct Kpp1Args {
+  int64_t n, m1;
+  int dim, T, k, pad;
+  const float* X;
+  const float* XT;     // X^T (dim x n) for plain-chain plans
+  const float* w;
+  const double* xsq;
+  const float* closest0;
+  const KppState* st;
+  const double* uniforms;
+  float* dist[2];      // [T][n]
+  float* potv[2];      // [T]
+  int64_t* candw[2];   // [T][T]
+  int64_t* candself[2];  // [T]
+  float* centers;
+  int64_t* indices;
+  SklPlan plan;
+};
+
+__device__ __forceinline__ int kpp1_argmin(const float* __restrict__ pot, int T) {
+  int b = 0;
+  for (int q = 1; q < T; ++q) {
+    const float pb = pot[b], pt = pot[q];
+    if (pb == pb && (pt < pb || pt != pt)) b = q;
+  }
+  return b;
+}
+
+template <bool SEQ>
+__global__ __launch_bounds__(256) void k_kpp1_dist(Kpp1Args a, int c) {
+  extern __shared__ double s_cr[];  // T * dim candidate rows (fp64)
+  __shared__ int64_t s_cand[kMaxTrials];
+  __shared__ double s_cn[kMaxTrials];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int pq = (c - 1) & 1, cq = c & 1, T = a.T, dim = a.dim;
+  const int Tp = c == 1 ? 1 : T;  // trials of round c-1 (round 0: the first centre)
+  const int n = (int)a.n;
+  const int i = blockIdx.x * kPts + lane;
+  const int ic = min(i, n - 1);  // clamped: every load below is unconditional (no branches
+                                 // around loads, so they all stay in flight together)
+  const int t0 = (blockIdx.y * 4 + wave) * kTg;
+  const bool live = i < n && t0 < T;
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && c == a.k - 2), 60);
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && c == a.k - 1), 65);
+  // the point's row does not depend on round c-1: request it first
+  constexpr int kX = SEQ ? 48 : 1;
+  float x[kX];
+  if (SEQ && dim <= kX) {
+#pragma unroll
+    for (int v = 0; v < kX; ++v) x[v] = a.XT[(int64_t)min(v, dim - 1) * n + ic];
+  }
+  const double xs = a.xsq[ic];
+  // round c-1: potentials -> np.argmin (every thread), then its winner's row and candidates
+  float pv[kMaxTrials];
+#pragma unroll
+  for (int q = 0; q < kMaxTrials; ++q) pv[q] = a.potv[pq][min(q, Tp - 1)];
+  int bw = 0;  // np.argmin: first minimum, a NaN wins at once
+  float best = pv[0];
+#pragma unroll
+  for (int q = 1; q < kMaxTrials; ++q) {
+    const float pt = pv[q];
+    if (q < Tp && best == best && (pt < best || pt != pt)) {
+      bw = q;
+      best = pt;
+    }
+  }
+  const float wi = c == 1 ? a.closest0[ic] : a.dist[pq][(int64_t)bw * n + ic];
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && c == a.k - 2), 61);
+  if (tid < T) {
+    const int64_t ct = a.candw[pq][(int64_t)bw * T + tid];
+    s_cand[tid] = ct;
+    s_cn[tid] = a.xsq[ct];
+  }
+  __syncthreads();
+  for (int e = tid; e < T * dim; e += 256) {
+    const int t = e / dim, j = e - t * dim;
+    s_cr[e] = (double)a.X[s_cand[t] * dim + j];
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0) {
+    if (tid < T) a.candself[cq][tid] = s_cand[tid];
+    if (c >= 2) {  // round c-1's centre
+      const int64_t src = a.candself[pq][bw];
+      if (tid == 0) a.indices[c - 1] = src;
+      for (int j = tid; j < dim; j += 256) a.centers[(int64_t)(c - 1) * dim + j] = a.X[src * dim + j];
+    }
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && c == a.k - 2), 62);
+  if (!live) return;
+  double dot[kTg];
+  const int t1 = min(t0 + 1, T - 1);
+  if constexpr (SEQ) {
+    dot[0] = 0.0;
+    dot[1] = 0.0;
+    const double* c0 = s_cr + (size_t)t0 * dim;
+    const double* c1 = s_cr + (size_t)t1 * dim;
+    if (dim <= kX) {
+#pragma unroll
+      for (int v = 0; v < kX; ++v) {
+        if (v < dim) {
+          const double xv = (double)x[v];
+          dot[0] = __builtin_fma(c0[v], xv, dot[0]);
+          dot[1] = __builtin_fma(c1[v], xv, dot[1]);
+        }
+      }
+    } else {
+      for (int j = 0; j < dim; j += 16) {
+        float y[16];
+#pragma unroll
+        for (int v = 0; v < 16; ++v) y[v] = a.XT[(int64_t)min(j + v, dim - 1) * n + i];
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          if (j + v < dim) {
+            dot[0] = __builtin_fma(c0[j + v], (double)y[v], dot[0]);
+            dot[1] = __builtin_fma(c1[j + v], (double)y[v], dot[1]);
+          }
+        }
+      }
+    }
+  } else {
+    dot[0] = skl_point_dot(a.plan, s_cr + (size_t)t0 * dim, a.X + (int64_t)i * dim, i, t0);
+    dot[1] = skl_point_dot(a.plan, s_cr + (size_t)t1 * dim, a.X + (int64_t)i * dim, i, t1);
+  }
+#pragma unroll
+  for (int u = 0; u < kTg; ++u) {
+    const int t = t0 + u;
+    if (t < T) {
+      float f = (float)(((-2.0 * dot[u]) + s_cn[t]) + xs);
+      f = f < 0.f ? 0.f : f;
+      a.dist[cq][(int64_t)t * n + i] = np_minimum(wi, f);
+    }
+  }
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && c == a.k - 2), 63);
+}
+
+// one sgemv_t lane chain over L entries stored contiguously in LDS (chain-major layout):
+// acc = acc + x in order, float4 reads issued 8 ahead of the dependent adds
+__device__ __forceinline__ float chain_add(const float* __restrict__ p, int L, float acc) {
+  int m = 0;
+  for (; m + 32 <= L; m += 32) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + m + 4 * u);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      acc = acc + v[u].x;
+      acc = acc + v[u].y;
+      acc = acc + v[u].z;
+      acc = acc + v[u].w;
+    }
+  }
+  for (; m < L; ++m) acc = acc + p[m];
+  return acc;
+}
+
+constexpr int kChainLd = kBlk / 4 + 68;  // chain-major LDS stride (floats): 4 (mod 64), >= 1024 + 4
+
+// round c's trial t (c == 0: the first centre over closest0, potential = the sdot): potential,
+// cumulative potential, and round c+1's candidates if this trial wins
+__global__ __launch_bounds__(kThr) void k_kpp1_pick(Kpp1Args a, int c) {
+  __shared__ float s_d[kBlk];
+  __shared__ float s_ch[8 * kChainLd];  // unit weights: chain l's entries contiguous
+  __shared__ double s_wave[kWaves];
+  __shared__ int s_cnt[kMaxTrials][kWaves];
+  __shared__ float s_pot;
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cq = c & 1, T = a.T;
+  const int n = (int)a.n, m1 = (int)a.m1;
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 70);
+  // this round's uniforms for the next round's draws: requested up front
+  double u[kMaxTrials];
+  const int un = c + 1 < a.k ? T : 1;
+#pragma unroll
+  for (int q = 0; q < kMaxTrials; ++q) u[q] = a.uniforms[(int64_t)c * T + min(q, un - 1)];
+  const float* row = c == 0 ? a.closest0 : a.dist[cq] + (int64_t)t * n;
+  const bool k4x2 = c > 0 && (T & 2) && t >= (T & ~3) && t < (T & ~3) + 2;
+  const int nl = k4x2 ? 4 : 8;                 // chain lanes
+  const int h4 = k4x2 ? 0 : (m1 & 4);          // 8-lane kernel: first m1 & 4 entries go to lanes 0..3
+  const bool perm = c > 0 && a.w == nullptr;
+  float r[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) r[q] = row[min(tid + kThr * q, n - 1)];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int e = tid + kThr * q;
+    if (e < n) {
+      s_d[e] = r[q];
+      if (perm && e >= h4 && e < m1) {
+        const int o = e - h4;
+        s_ch[(o % nl) * kChainLd + o / nl] = r[q];
+      }
+    }
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 71);
+  double v[kPer], pre[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int e = kPer * tid + q;
+    v[q] = e < n ? (double)(wv(a.w, e) * s_d[kPer * tid + q]) : 0.0;
+  }
+  block_prefix(v, pre, s_wave);
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 72);
+  if (wave == 0) {
+    float y = 0.f;
+    if (c == 0) {
+      y = a.st->pot;
+    } else if (m1 > 0) {  // sgemv_t: the block's lane chains, then the n % 4 trailing entries
+      if (perm) {
+        float acc = 0.f;
+        if (lane < nl) {
+          if (lane < h4) acc = acc + s_d[lane];
+          const int o0 = lane;  // chain lane's entries o = h4 + lane + nl * m
+          const int L = (m1 - h4 - o0 + nl - 1) / nl;
+          acc = chain_add(s_ch + lane * kChainLd, max(L, 0), acc);
+        }
+        if (k4x2) {
+          const float a1 = __shfl(acc, 1), a2 = __shfl(acc, 2), a3 = __shfl(acc, 3);
+          y = (acc + a1) + (a2 + a3);
+        } else {
+          const float ql = acc + __shfl(acc, (lane + 4) & 63);
+          const float q1 = __shfl(ql, 1), q2 = __shfl(ql, 2), q3 = __shfl(ql, 3);
+          y = (ql + q1) + (q2 + q3);
+        }
+      } else {
+        y = sgemv_block_wave(s_d, a.w, m1, t, T);
+      }
+    }
+    if (c > 0 && m1 < n && lane == 0) {
+      float sx = s_d[m1] * wv(a.w, m1);
+      for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_d[o], wv(a.w, o), sx);
+      y = y + sx;
+    }
+    if (lane == 0) {
+      s_pot = y;
+      a.potv[cq][t] = y;
+    }
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 73);
+  if (c + 1 >= a.k) return;
+  const double pot = (double)s_pot;
+#pragma unroll
+  for (int t2 = 0; t2 < kMaxTrials; ++t2) {
+    if (t2 < T) {
+      const double rr = u[t2] * pot;
+      int cw = 0;
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) cw += __popcll(__ballot(kPer * tid + q < n && pre[q] < rr));
+      if (lane == 0) s_cnt[t2][wave] = cw;
+    }
+  }
+  __syncthreads();
+  if (tid < T) {
+    int64_t cnt = 0;
+    for (int q = 0; q < kWaves; ++q) cnt += s_cnt[tid][q];
+    a.candw[cq][(int64_t)t * T + tid] = min<int64_t>(n - 1, cnt);
+  }
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 74);
+}
+
+// after round k-1: its winner and centre
+__global__ __launch_bounds__(64) void k_kpp1_final(Kpp1Args a, int c) {
+  const int q = c & 1;
+  const int b = kpp1_argmin(a.potv[q], a.T);
+  const int64_t src = a.candself[q][b];
+  if (threadIdx.x == 0) a.indices[c] = src;
+  for (int j = threadIdx.x; j < a.dim; j += 64) a.centers[(int64_t)c * a.dim + j] = a.X[src * a.dim + j];
+}
+
+// X^T (dim x n) for the single-block distance phase: coalesced loads
+__global__ void k_kpp_xt(int n, int dim, const float* __restrict__ X, float* __restrict__ XT) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * dim) return;
+  const int j = e / n, i = e - j * n;
+  XT[e] = X[(int64_t)i * dim + j];
 }
 
 // _euclidean_distances(C, X, squared=True) on its own (the distance of every round, exposed for
@@ -749,7 +1166,7 @@ extern "C" int gdd_skl_sqdist(int n_rows, const float* C, int64_t n, int dim, co
   return GDD_OK;
 }
 
-extern "C" size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int n_trials) {
+extern "C" size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int dim, int n_trials) {
   const size_t T = (size_t)std::max(n_trials, 1);
   const size_t nblk = (size_t)((n + kBlk - 1) / kBlk);
   size_t b = 0;
@@ -762,6 +1179,10 @@ extern "C" size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int n_trials) {
   b += 2 * align256(sizeof(double) * nblk * T);   // fsum
   b += 2 * align256(sizeof(int64_t) * kMaxTrials);
   b += align256(sizeof(float) * 2);           // pot1
+  b += 2 * align256(sizeof(float) * T);       // potv
+  b += 2 * align256(sizeof(int64_t) * T * T); // candw
+  b += 2 * align256(sizeof(int64_t) * T);     // candself
+  if (n <= kBlk) b += align256(sizeof(float) * n * (size_t)std::max(dim, 1));  // XT
   return b + 1024;
 }
 
@@ -791,6 +1212,11 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   for (int q = 0; q < 2; ++q) a.fsum[q] = cv.take<double>((size_t)nblk * T);
   for (int q = 0; q < 2; ++q) a.cand[q] = cv.take<int64_t>(kMaxTrials);
   a.pot1 = cv.take<float>(2);
+  Kpp1Args b1{};
+  for (int q = 0; q < 2; ++q) b1.potv[q] = cv.take<float>(T);
+  for (int q = 0; q < 2; ++q) b1.candw[q] = cv.take<int64_t>((size_t)T * T);
+  for (int q = 0; q < 2; ++q) b1.candself[q] = cv.take<int64_t>(T);
+  float* XT = n <= kBlk ? cv.take<float>((size_t)n * dim) : nullptr;
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans++: workspace too small");
   a.n = n;
   a.m1 = n & ~3ll;
@@ -811,19 +1237,65 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   a.plan.all_seq = skl_all_seq(n, T, dim, a.plan.B) ? 1 : 0;
   const SklPlan p1{n, skl_batch_size(1, n, dim), 1, dim, 0, 0};
   const size_t lds = sizeof(double) * (size_t)dim + sizeof(float) * kBlk;
+  const bool seq = a.plan.all_seq != 0;
+  const bool single = nblk == 1 && T >= 2 && (!seq || XT);
   if (lds > 65536) {
-    GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_init,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_round,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const void* fns[] = {(const void*)k_kpp_init, (const void*)k_kpp_round<true>,
+                         (const void*)k_kpp_round<false>};
+    for (const void* f : fns)
+      GDD_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   }
   k_kpp_init<<<nblk, kThr, lds, s>>>(a, p1, first_id, xsq, closest0, fsum0);
   GDD_LAUNCHED();
   k_kpp_first<<<1, 64, 0, s>>>(n, dim, X, w, closest0, first_id, st, centers, indices);
   GDD_LAUNCHED();
   if (k == 1) return GDD_OK;
+  if (single) {
+    b1.n = n;
+    b1.m1 = a.m1;
+    b1.dim = dim;
+    b1.T = T;
+    b1.k = k;
+    b1.X = X;
+    b1.XT = XT;
+    b1.w = w;
+    b1.xsq = xsq;
+    b1.closest0 = closest0;
+    b1.st = st;
+    b1.uniforms = uniforms;
+    for (int q = 0; q < 2; ++q) b1.dist[q] = a.dist[q];
+    b1.centers = centers;
+    b1.indices = indices;
+    b1.plan = a.plan;
+    if (seq) {
+      k_kpp_xt<<<(unsigned)((n * dim + 255) / 256), 256, 0, s>>>((int)n, dim, X, XT);
+      GDD_LAUNCHED();
+    }
+    const size_t lds1 = sizeof(double) * (size_t)T * dim;
+    if (lds1 > 65536)
+      for (const void* f : {(const void*)k_kpp1_dist<true>, (const void*)k_kpp1_dist<false>})
+        GDD_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
+    const dim3 g1((unsigned)((n + kPts - 1) / kPts), (unsigned)(((T + kTg - 1) / kTg + 3) / 4));
+    k_kpp1_pick<<<1, kThr, 0, s>>>(b1, 0);
+    GDD_LAUNCHED();
+    for (int c = 1; c < k; ++c) {
+      if (seq)
+        k_kpp1_dist<true><<<g1, 256, lds1, s>>>(b1, c);
+      else
+        k_kpp1_dist<false><<<g1, 256, lds1, s>>>(b1, c);
+      GDD_LAUNCHED();
+      k_kpp1_pick<<<T, kThr, 0, s>>>(b1, c);
+      GDD_LAUNCHED();
+    }
+    k_kpp1_final<<<1, 64, 0, s>>>(b1, k - 1);
+    GDD_LAUNCHED();
+    return GDD_OK;
+  }
   for (int c = 1; c < k; ++c) {
-    k_kpp_round<<<dim3(nblk, T), kThr, lds, s>>>(a, c);
+    if (seq)
+      k_kpp_round<true><<<dim3(nblk, T), kThr, lds, s>>>(a, c);
+    else
+      k_kpp_round<false><<<dim3(nblk, T), kThr, lds, s>>>(a, c);
     GDD_LAUNCHED();
     if (T == 1) {
       k_kpp_pot1<<<1, 64, 0, s>>>(n, a.dist[c & 1], w, a.pot1 + (c & 1));

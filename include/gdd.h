@@ -225,7 +225,7 @@ int gdd_labels_changed(int64_t n, const int32_t* labels, int32_t* labels_old, in
 /* in OpenBLAS's per-shape summation orders (gdd_skl_sqdist). Potentials: the first as sdot, the     */
 /* trials' as sgemv_t (_kmeans.py:239-251). Writes centers (k x dim) and indices. 1 <= n_trials <= 16. */
 /* ---------------------------------------------------------------------------------------------- */
-size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int n_trials);
+size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int dim, int n_trials);
 int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const float* w, int k, int n_trials,
                         int64_t first_id, const double* uniforms, float* centers, int64_t* indices,
                         void* ws, size_t ws_bytes, gdd_stream_t stream);

@@ -49,9 +49,11 @@ def main():
         show("update block0", a, list(range(20, 26)), 20)
         show("update tail", a, list(range(30, 33)), 30)
         show("mb_reassign", a, list(range(40, 47)), 40)
-        bank = 10 * ((cfg.k - 2) & 1)  # round k-2 is the last complete tail
-        show("kpp_tail", p, [bank + i for i in range(7)], bank)
-        show("kpp_dist", p, list(range(20, 24)), 20)
+        t0 = p[60]
+        lab = {60: "dist start", 66: "XT loaded", 67: "potv[0]", 68: "potv[1]", 61: "argmin", 62: "cand rows", 63: "dist end", 70: "pick start",
+               71: "staged", 72: "prefix", 73: "chain", 74: "pick end", 65: "next dist start"}
+        print("kpp single-block round k-2 (us): " + ", ".join(
+            f"{lab[q]} {(p[q] - t0) / 100:.2f}" for q in [60, 66, 67, 68, 61, 62, 63, 70, 71, 72, 73, 74, 65]))
 
 
 if __name__ == "__main__":
