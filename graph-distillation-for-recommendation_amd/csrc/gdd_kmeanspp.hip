@@ -856,7 +856,7 @@ __device__ __forceinline__ int kpp1_argmin(const float* __restrict__ pot, int T)
 template <bool SEQ>
 __global__ __launch_bounds__(256) void k_kpp1_dist(Kpp1Args a, int c) {
   extern __shared__ double s_cr[];  // T * dim candidate rows (fp64)
-  __shared__ int64_t s_cand[kMaxTrials];
+  __shared__ int64_t s_cw[kMaxTrials * kMaxTrials];
   __shared__ double s_cn[kMaxTrials];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int pq = (c - 1) & 1, cq = c & 1, T = a.T, dim = a.dim;
@@ -869,7 +869,7 @@ __global__ __launch_bounds__(256) void k_kpp1_dist(Kpp1Args a, int c) {
   const bool live = i < n && t0 < T;
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && c == a.k - 2), 60);
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && c == a.k - 1), 65);
-  // the point's row does not depend on round c-1: request it first
+  // round trip 1: the point's row, round c-1's potentials and its whole candidate table
   constexpr int kX = SEQ ? 48 : 1;
   float x[kX];
   if (SEQ && dim <= kX) {
@@ -877,10 +877,10 @@ __global__ __launch_bounds__(256) void k_kpp1_dist(Kpp1Args a, int c) {
     for (int v = 0; v < kX; ++v) x[v] = a.XT[(int64_t)min(v, dim - 1) * n + ic];
   }
   const double xs = a.xsq[ic];
-  // round c-1: potentials -> np.argmin (every thread), then its winner's row and candidates
   float pv[kMaxTrials];
 #pragma unroll
   for (int q = 0; q < kMaxTrials; ++q) pv[q] = a.potv[pq][min(q, Tp - 1)];
+  if (tid < Tp * T) s_cw[tid] = a.candw[pq][tid];
   int bw = 0;  // np.argmin: first minimum, a NaN wins at once
   float best = pv[0];
 #pragma unroll
@@ -891,20 +891,21 @@ __global__ __launch_bounds__(256) void k_kpp1_dist(Kpp1Args a, int c) {
       best = pt;
     }
   }
-  const float wi = c == 1 ? a.closest0[ic] : a.dist[pq][(int64_t)bw * n + ic];
-  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && c == a.k - 2), 61);
-  if (tid < T) {
-    const int64_t ct = a.candw[pq][(int64_t)bw * T + tid];
-    s_cand[tid] = ct;
-    s_cn[tid] = a.xsq[ct];
-  }
   __syncthreads();
-  for (int e = tid; e < T * dim; e += 256) {
-    const int t = e / dim, j = e - t * dim;
-    s_cr[e] = (double)a.X[s_cand[t] * dim + j];
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && c == a.k - 2), 61);
+  // round trip 2: the winner's row, this round's candidate rows and norms
+  const float wi = c == 1 ? a.closest0[ic] : a.dist[pq][(int64_t)bw * n + ic];
+  const int64_t* cand = s_cw + bw * T;
+  if (tid < T) s_cn[tid] = a.xsq[cand[tid]];
+  // candidate rows in fp64; short rows (plain chains) padded with zeros to kX, so the chain below
+  // runs a fixed trip count without branches (dot + 0 * x == dot)
+  const int cs = (SEQ && dim <= kX) ? kX : dim;
+  for (int e = tid; e < T * cs; e += 256) {
+    const int t = e / cs, j = e - t * cs;
+    s_cr[e] = j < dim ? (double)a.X[cand[t] * dim + min(j, dim - 1)] : 0.0;
   }
   if (blockIdx.x == 0 && blockIdx.y == 0) {
-    if (tid < T) a.candself[cq][tid] = s_cand[tid];
+    if (tid < T) a.candself[cq][tid] = cand[tid];
     if (c >= 2) {  // round c-1's centre
       const int64_t src = a.candself[pq][bw];
       if (tid == 0) a.indices[c - 1] = src;
@@ -919,16 +920,14 @@ __global__ __launch_bounds__(256) void k_kpp1_dist(Kpp1Args a, int c) {
   if constexpr (SEQ) {
     dot[0] = 0.0;
     dot[1] = 0.0;
-    const double* c0 = s_cr + (size_t)t0 * dim;
-    const double* c1 = s_cr + (size_t)t1 * dim;
+    const double* c0 = s_cr + (size_t)t0 * cs;
+    const double* c1 = s_cr + (size_t)t1 * cs;
     if (dim <= kX) {
 #pragma unroll
       for (int v = 0; v < kX; ++v) {
-        if (v < dim) {
-          const double xv = (double)x[v];
-          dot[0] = __builtin_fma(c0[v], xv, dot[0]);
-          dot[1] = __builtin_fma(c1[v], xv, dot[1]);
-        }
+        const double xv = (double)x[v];
+        dot[0] = __builtin_fma(c0[v], xv, dot[0]);
+        dot[1] = __builtin_fma(c1[v], xv, dot[1]);
       }
     } else {
       for (int j = 0; j < dim; j += 16) {
@@ -1271,7 +1270,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       k_kpp_xt<<<(unsigned)((n * dim + 255) / 256), 256, 0, s>>>((int)n, dim, X, XT);
       GDD_LAUNCHED();
     }
-    const size_t lds1 = sizeof(double) * (size_t)T * dim;
+    const size_t lds1 = sizeof(double) * (size_t)T * std::max(dim, 48);
     if (lds1 > 65536)
       for (const void* f : {(const void*)k_kpp1_dist<true>, (const void*)k_kpp1_dist<false>})
         GDD_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
