@@ -43,9 +43,6 @@ constexpr int kChunkCap = 64;
 
 struct Pinned {
   void* p = nullptr;
-  ~Pinned() {
-    if (p) (void)hipHostFree(p);
-  }
 };
 
 struct FitWs {
@@ -209,12 +206,26 @@ extern "C" size_t gdd_minibatch_kmeans_fit_ws_bytes(int64_t n, int dim, int k, i
   return fit_ws(nullptr, 0, n, dim, k, bs, init_size, local_trials(k), nullptr);
 }
 
+// pinned host bytes of one fit: a chunk of batch indices, the k-means++ uniforms, read-backs
+size_t fit_host_ws(int k, int64_t bs, int64_t isz, int T) {
+  return sizeof(int64_t) * (size_t)kChunkCap * bs + sizeof(double) * (size_t)std::max(k - 1, 1) * T +
+         sizeof(int64_t) * 2 * (size_t)isz + sizeof(float) * (size_t)k * 2 + 256 + sizeof(DevMT) +
+         sizeof(int64_t) * 2 * (size_t)k;
+}
+
+extern "C" size_t gdd_minibatch_kmeans_fit_host_ws_bytes(int64_t n, int k, int64_t batch_size,
+                                                         int64_t init_size) {
+  const int64_t bs = std::min<int64_t>(batch_size, n);
+  return fit_host_ws(k, bs, init_size, local_trials(k));
+}
+
 extern "C" int gdd_minibatch_kmeans_fit(
     int64_t n, int dim, const float* X, int k, int64_t batch_size, int max_iter,
     int max_no_improvement, float reassignment_ratio, int64_t init_size, int n_init,
     int compute_labels, void* rng_state, void (*argsort_cb)(const float*, int64_t, int64_t*),
     float* centers_out, int32_t* labels_out, float* inertia_out, int64_t* n_steps_out,
-    double* ewa_out, void* ws, size_t ws_bytes, gdd_stream_t stream) {
+    double* ewa_out, void* ws, size_t ws_bytes, void* host_ws, size_t host_ws_bytes,
+    gdd_stream_t stream) {
   GDD_REQUIRE(n > 0 && dim > 0 && dim <= 512 && k > 0 && k <= n, "mbk_fit: bad shape");
   GDD_REQUIRE(batch_size > 0 && max_iter >= 0 && n_init >= 1 && init_size >= k && init_size <= n,
               "mbk_fit: bad parameters");
@@ -230,13 +241,11 @@ extern "C" int gdd_minibatch_kmeans_fit(
     return fail(GDD_E_WORKSPACE, "mbk_fit: workspace too small");
   LegacyRNG rng(static_cast<MTState*>(rng_state));
 
-  // pinned staging: batch indices of one chunk, k-means++ uniforms, small read-backs
-  const size_t pin_bytes = sizeof(int64_t) * (size_t)kChunkCap * bs +
-                           sizeof(double) * (size_t)std::max(k - 1, 1) * T +
-                           sizeof(int64_t) * 2 * (size_t)isz + sizeof(float) * (size_t)k * 2 + 256 +
-                           sizeof(DevMT) + sizeof(int64_t) * 2 * (size_t)k;
+  // pinned staging (caller-owned): batch indices of one chunk, k-means++ uniforms, small read-backs
+  const size_t pin_bytes = fit_host_ws(k, bs, isz, T);
+  GDD_REQUIRE(host_ws && host_ws_bytes >= pin_bytes, "mbk_fit: pinned host workspace too small");
   Pinned pin;
-  GDD_HIP(hipHostMalloc(&pin.p, pin_bytes, hipHostMallocDefault));
+  pin.p = host_ws;
   char* pp = static_cast<char*>(pin.p);
   int64_t* h_rows = reinterpret_cast<int64_t*>(pp);
   pp += sizeof(int64_t) * (size_t)kChunkCap * bs;
@@ -425,19 +434,23 @@ extern "C" int gdd_minibatch_kmeans_fit(
   *n_steps_out = last + 1;
   const float* C = w.C[(last + 1) % 2];
   GDD_HIP(hipMemcpyAsync(centers_out, C, sizeof(float) * (size_t)k * dim, hipMemcpyDeviceToDevice, s));
-  if (ewa_out) {
-    GDD_HIP(hipMemcpyAsync(h_counts, w.state, sizeof(double), hipMemcpyDeviceToHost, s));
-    GDD_HIP(hipStreamSynchronize(s));
-    std::memcpy(ewa_out, h_counts, sizeof(double));
-  }
   if (compute_labels) {  // final labels pass + inertia (:2191-2197)
     int rc = gdd_row_norms(k, dim, C, reinterpret_cast<float*>(w.pairs), stream);
     if (rc) return rc;
     rc = gdd_kmeans_assign(n, dim, X, nullptr, k, C, reinterpret_cast<float*>(w.pairs), labels_out,
                            w.sq, w.assign_ws, w.assign_bytes, stream);
     if (rc) return rc;
-    rc = gdd_inertia(n, w.sq, nullptr, inertia_out, stream);
-    if (rc) return rc;
+    if (compute_labels == 2) {  // per-sample squared distances for the caller's own inertia fold
+      GDD_HIP(hipMemcpyAsync(inertia_out, w.sq, sizeof(float) * (size_t)n, hipMemcpyDeviceToDevice, s));
+    } else {
+      rc = gdd_inertia(n, w.sq, nullptr, inertia_out, stream);
+      if (rc) return rc;
+    }
+  }
+  if (ewa_out) {  // after the labels pass is enqueued, so the device never idles on this read
+    GDD_HIP(hipMemcpyAsync(h_counts, w.state, sizeof(double), hipMemcpyDeviceToHost, s));
+    GDD_HIP(hipStreamSynchronize(s));
+    std::memcpy(ewa_out, h_counts, sizeof(double));
   }
   return GDD_OK;
 }

@@ -58,7 +58,8 @@ SIGNATURES = {
     "gdd_minibatch_kmeans_fit_ws_bytes": (_c_size, [_c_i64, _c_int, _c_int, _c_i64, _c_i64]),
     "gdd_minibatch_kmeans_fit": (_c_int, [_c_i64, _c_int, _vp, _c_int, _c_i64, _c_int, _c_int,
                                           _c_f32, _c_i64, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp,
-                                          _vp, _vp, _vp, _c_size, _vp]),
+                                          _vp, _vp, _vp, _c_size, _vp, _c_size, _vp]),
+    "gdd_minibatch_kmeans_fit_host_ws_bytes": (_c_size, [_c_i64, _c_int, _c_i64, _c_i64]),
     "gdd_rng_randint": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp]),
     "gdd_rng_random_sample": (_c_int, [_vp, _c_i64, _vp]),
     "gdd_rng_permutation": (_c_int, [_vp, _c_i64, _vp]),
@@ -138,6 +139,11 @@ def ptr(t) -> int | None:
 
 def workspace(nbytes: int, device) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+def pinned_workspace(nbytes: int) -> torch.Tensor:
+    """Page-locked host staging from PyTorch's pinned caching allocator (no per-call hipHostMalloc)."""
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, pin_memory=True)
 
 
 class MTState(ctypes.Structure):

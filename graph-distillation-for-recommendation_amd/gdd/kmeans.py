@@ -234,27 +234,29 @@ class MiniBatchKMeans(_BaseKMeans):
         dev = Xd.device
         st = _lib.MTState.from_random_state(rs)
         ws = _lib.workspace(lib.gdd_minibatch_kmeans_fit_ws_bytes(n, dim, k, bs, isz), dev)
+        hws = _lib.pinned_workspace(lib.gdd_minibatch_kmeans_fit_host_ws_bytes(n, k, bs, isz))
         centers = torch.empty((k, dim), dtype=torch.float32, device=dev)
         n_steps, ewa = ctypes.c_int64(0), ctypes.c_double(0.0)
         max_ni = -1 if self.max_no_improvement is None else int(self.max_no_improvement)
-        # the final labels pass is enqueued below, so that its inertia can run off the main stream
+        # compute_labels: the native fit enqueues the full labels pass (:2191-2197) as soon as the
+        # loop stops and leaves the per-sample distances in `sq`; their inertia (a sequential fp32
+        # fold bound by its add chain) runs on a side stream, read on first access of inertia_
+        labels = sq = None
+        if self.compute_labels:
+            labels = torch.empty(n, dtype=torch.int32, device=dev)
+            sq = torch.empty(n, dtype=torch.float32, device=dev)
         _lib.check(lib.gdd_minibatch_kmeans_fit(
             n, dim, Xd.data_ptr(), k, bs, int(self.max_iter), max_ni, float(self.reassignment_ratio),
-            isz, self._n_init(3), 0, ctypes.addressof(st),
+            isz, self._n_init(3), 2 if self.compute_labels else 0, ctypes.addressof(st),
             ctypes.cast(_lib.argsort_callback, ctypes.c_void_p).value, centers.data_ptr(),
-            None, None, ctypes.addressof(n_steps), ctypes.addressof(ewa),
-            ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev)))
-        del ws
+            labels.data_ptr() if labels is not None else None, sq.data_ptr() if sq is not None else None,
+            ctypes.addressof(n_steps), None if self.compute_labels else ctypes.addressof(ewa),
+            ws.data_ptr(), ws.numel(), hws.data_ptr(), hws.numel(), _lib.stream_ptr(dev)))
         st.to_random_state(rs)  # leave the generator where sklearn leaves it
         self.n_steps_ = int(n_steps.value)
         self.n_iter_ = int(np.ceil((self.n_steps_ * bs) / n))
         self.cluster_centers_device_ = centers
         if self.compute_labels:
-            # full labels pass (:2191-2197): labels on the caller's stream; the inertia (a sequential
-            # fp32 fold bound by its add chain) on a side stream, read on first access of inertia_
-            labels = torch.empty(n, dtype=torch.int32, device=dev)
-            sq = torch.empty(n, dtype=torch.float32, device=dev)
-            _Ops(dev, n, k, dim).assign(Xd, centers, labels=labels, sq=sq)
             self.labels_device_ = labels
             self._inertia_async = _side_inertia(sq)
         else:

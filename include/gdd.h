@@ -161,7 +161,9 @@ typedef struct gdd_mt_state {
 /* exactly as scikit-learn advances it. argsort_cb must reproduce np.argsort(weight_sums); it is    */
 /* only called when more than batch/2 centres are due for reassignment (possible only if k > b/2).   */
 /* Host syncs: one per reassignment step and one at the end. centers_out k x dim, labels_out n,      */
-/* inertia_out 1 float (device); n_steps_out, ewa_out (nullable) host.                              */
+/* inertia_out (device): compute_labels 1 -> 1 float, the inertia; compute_labels 2 -> n floats, the  */
+/* per-sample squared distances (the caller folds them, e.g. on a side stream); n_steps_out, ewa_out  */
+/* (nullable) host.                                                                                  */
 size_t gdd_minibatch_kmeans_fit_ws_bytes(int64_t n, int dim, int k, int64_t batch_size,
                                          int64_t init_size);
 int gdd_minibatch_kmeans_fit(int64_t n, int dim, const float* X, int k, int64_t batch_size,
@@ -169,7 +171,10 @@ int gdd_minibatch_kmeans_fit(int64_t n, int dim, const float* X, int k, int64_t 
                              int64_t init_size, int n_init, int compute_labels, void* rng,
                              void (*argsort_cb)(const float*, int64_t, int64_t*), float* centers_out,
                              int32_t* labels_out, float* inertia_out, int64_t* n_steps_out,
-                             double* ewa_out, void* ws, size_t ws_bytes, gdd_stream_t stream);
+                             double* ewa_out, void* ws, size_t ws_bytes, void* host_ws,
+                             size_t host_ws_bytes, gdd_stream_t stream);
+/* pinned host staging the fit needs (host_ws: page-locked, caller-owned, e.g. a pinned torch tensor) */
+size_t gdd_minibatch_kmeans_fit_host_ws_bytes(int64_t n, int k, int64_t batch_size, int64_t init_size);
 
 /* Host-only numpy-legacy draws used by the native loops (exposed for parity tests):                */
 /* randint(low, high, count) (int64), random_sample(count), permutation(n), and                      */
