@@ -80,6 +80,21 @@ SIGNATURES = {
     "gdd_standard_scaler": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "gdd_cluster_mean": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _c_int, _c_int, _vp, _vp, _vp]),
     "gdd_argmax_rows": (_c_int, [_c_int, _c_int, _vp, _vp, _vp]),
+    "gdd_coo_rows": (_c_int, [_c_i64, _vp, _vp, _vp]),
+    "gdd_er_ws_bytes": (_c_size, [_c_i64, _c_int]),
+    "gdd_attaw_er": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp,
+                              _c_size, _vp]),
+    "gdd_vanilla_er": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
+    "gdd_softmax_rows": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp]),
+    "gdd_topk_ws_bytes": (_c_size, [_c_i64, _c_int]),
+    "gdd_class_topk": (_c_int, [_c_i64, _vp, _vp, _vp, _c_int, _vp, _c_i64, _vp, _vp, _c_size,
+                                _vp]),
+    "gdd_compress_ws_bytes": (_c_size, [_c_int]),
+    "gdd_graph_compress": (_c_int, [_c_i64, _vp, _c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    _c_size, _vp]),
+    "gdd_select_csr_ws_bytes": (_c_size, [_c_i64]),
+    "gdd_select_csr": (_c_int, [_c_i64, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_size,
+                                _vp]),
 }
 
 _lib = None

@@ -265,6 +265,46 @@ int gdd_cluster_mean(int64_t n, int d, const float* feat, const int32_t* perm, c
 /* labels_syn[c] = argmax_j centers[c,j] (first max wins, torch.argmax; transduct:126).              */
 int gdd_argmax_rows(int k, int dim, const float* centers, int64_t* out, gdd_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------------- */
+/* (f1/f2) graph condensation: ClustGDD.graph_sparse + ClustGDD.graph_compress                      */
+/* (clustgdd_agent_transduct.py:131-250, induct:156-274) and the effective-resistance estimators    */
+/* of utils_clustgdd.py:149-182. Edges are the entries of a canonical CSR; rows[e] is each entry's */
+/* row (gdd_coo_rows). Orders restated bit for bit by oracle/condense.py.                           */
+/* ---------------------------------------------------------------------------------------------- */
+int gdd_coo_rows(int64_t n, const int32_t* rowptr, int32_t* rows, gdd_stream_t stream);
+size_t gdd_er_ws_bytes(int64_t n, int C);
+/* attaw_ER_estimator (utils_clustgdd.py:162-182): rew[e] = val[e] * cos(ebd[src], ebd[dst])         */
+/* (ebd: n x C logits), deg = row sums of rew (CSR order), er[e] = rew/deg[src] + rew/deg[dst].     */
+int gdd_attaw_er(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* rows,
+                 const int32_t* col, const float* val, int C, const float* ebd, float* rew, float* er,
+                 void* ws, size_t ws_bytes, gdd_stream_t stream);
+/* ER_estimator (utils_clustgdd.py:149-159): the same bound on val (NULL = binary).                 */
+int gdd_vanilla_er(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* rows,
+                   const int32_t* col, const float* val, float* er, void* ws, size_t ws_bytes,
+                   gdd_stream_t stream);
+/* F.softmax(x, dim=-1) on n x C rows (e = fp32(exp(double(x - max))), sequential sum, e / sum).     */
+int gdd_softmax_rows(int64_t n, int C, const float* x, float* p, gdd_stream_t stream);
+size_t gdd_topk_ws_bytes(int64_t nnz, int nsets);
+/* torch.topk(weight, m) per set, as the ascending edge ids of the m largest (NaN largest, ties to   */
+/* the lower id): probs (n x nsets) given -> set i weighs edge e by (probs[src,i]*probs[dst,i])*er  */
+/* (graph_sparse 'attaw', :154-182); probs NULL -> one set weighed by er ('vanilla'/'single').      */
+/* sel: nsets x m int32.                                                                             */
+int gdd_class_topk(int64_t nnz, const int32_t* rows, const int32_t* col, const float* er, int nsets,
+                   const float* probs, int64_t m, int32_t* sel, void* ws, size_t ws_bytes,
+                   gdd_stream_t stream);
+size_t gdd_compress_ws_bytes(int kk);
+/* graph_compress (:234-250) for one edge set (all m edges, or the m edge ids in sel):               */
+/* out (kk x kk) = P^T A P with P = onehot(labels)/cluster sizes, diagonal removed; an empty        */
+/* cluster gives a NaN row and column (the reference's 0/0 column of P). kk = max label + 1.        */
+int gdd_graph_compress(int64_t n, const int32_t* labels, int kk, int64_t m, const int32_t* rows,
+                       const int32_t* col, const float* val, const int32_t* sel, float* out, void* ws,
+                       size_t ws_bytes, gdd_stream_t stream);
+size_t gdd_select_csr_ws_bytes(int64_t n);
+/* the selected edges (ascending ids, so already in CSR order) as a CSR: rowptr_out n+1, col/val m. */
+int gdd_select_csr(int64_t n, const int32_t* rows, const int32_t* col, const float* val, int64_t m,
+                   const int32_t* sel, int32_t* rowptr_out, int32_t* col_out, float* val_out, void* ws,
+                   size_t ws_bytes, gdd_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -14,7 +14,10 @@ setting in which its Lloyd M-step merge order is deterministic.
   G3b golden_kmeans_arxiv.json  MiniBatchKMeans on a 169,343 x 40 input (hashes of the outputs)
   G4/G5 golden_clustgdd_*.npz  ClustGDD.pretrained_clustering end to end (CPU), with the exact
                            k-means input and numpy RNG state captured at the sklearn call
-Usage: python tools/make_golden.py
+  G6 golden_condense.npz   ClustGDD.graph_sparse(sp_type='attaw'/'vanilla'/'single') and
+                           ClustGDD.graph_compress (clustgdd_agent_transduct.py:131-250), with the
+                           effective-resistance intermediates of utils_clustgdd.attaw_ER_estimator
+Usage: python tools/make_golden.py [G1 G2 ...]   (default: all)
 """
 import hashlib
 import json
@@ -234,6 +237,46 @@ def g5_clustgdd(agent, dataset):
     np.savez_compressed(os.path.join(OUT, f"golden_clustgdd_{tag}.npz"), **out)
 
 
+def g6_condense(du, agent):
+    """graph_sparse + graph_compress on a 500-node graph (C=5 classes, k=40 clusters), two label
+    sets: every cluster populated, and cluster 17 empty (the reference's NaN row/column)."""
+    import torch
+    import utils_clustgdd as uc
+    n, C, k, ratio = 500, 5, 40, 0.4
+    A = synth.chung_lu(n, 8.0, 61)
+    rp, ci, vi = csr_arrays(A)
+    adj_norm = du.normalize_adj_tensor(du.sparse_mx_to_torch_sparse_tensor(sp.csr_matrix(A)),
+                                       sparse=True)
+    rng = np.random.default_rng(62)
+    ebd = torch.from_numpy((rng.standard_normal((n, C)) * 2.0).astype(np.float32))
+    r, c, v = coo_sorted(adj_norm)
+    out = {"rowptr": rp, "col": ci, "val": vi, "norm_row": r, "norm_col": c, "norm_val": v,
+           "ebd": ebd.numpy(), "ratio": np.float64(ratio), "k": np.int64(k)}
+    a = adj_norm.coalesce()
+    src, dst = a._indices()[0], a._indices()[1]
+    er, rew = uc.attaw_ER_estimator(adj_norm, ebd, src, dst)
+    out["er_attaw"] = er.numpy()
+    out["reweighted_val"] = rew.coalesce()._values().numpy()
+    out["er_vanilla"] = uc.ER_estimator(adj_norm, src, dst).numpy()
+    for sp_type in ("attaw", "vanilla", "single"):
+        gl = agent.ClustGDD.graph_sparse(None, adj_norm, ratio, ebd=ebd, sp_type=sp_type)
+        out[f"{sp_type}_count"] = np.int64(len(gl))
+        for q, g in enumerate(gl):
+            gr, gc, gv = coo_sorted(g)
+            out.update({f"{sp_type}{q}_row": gr, f"{sp_type}{q}_col": gc, f"{sp_type}{q}_val": gv})
+    sparsed = agent.ClustGDD.graph_sparse(None, adj_norm, ratio, ebd=ebd, sp_type="attaw")
+    lab_full = rng.permutation(np.arange(n) % k)
+    lab_gap = lab_full.copy()
+    lab_gap[lab_gap == 17] = 18
+    for tag, lab in (("full", lab_full), ("gap", lab_gap)):
+        cl, adj_syn = agent.ClustGDD.graph_compress(None, torch.from_numpy(lab), adj_norm, sparsed)
+        out[f"{tag}_labels"] = lab.astype(np.int32)
+        out[f"{tag}_adj_syn"] = adj_syn.to_dense().numpy()
+        for q, g in enumerate(cl):
+            out[f"{tag}_compressed{q}"] = g.to_dense().numpy()
+    np.savez_compressed(os.path.join(OUT, "golden_condense.npz"), **out)
+
+
 def main():
     from threadpoolctl import threadpool_limits
     import sklearn
@@ -241,13 +284,21 @@ def main():
     import torch
     os.makedirs(OUT, exist_ok=True)
     du, agent, recsys = import_reference()
+    which = set(sys.argv[1:]) or {"G1", "G2", "G3", "G3b", "G5", "G6"}
     with threadpool_limits(limits=1):
-        g1_normalize(du)
-        g2_propagate(du)
-        g3_kmeans(recsys)
-        g3b_arxiv()
-        g5_clustgdd(agent, "cora")
-        g5_clustgdd(agent, "ogbn-arxiv")
+        if "G1" in which:
+            g1_normalize(du)
+        if "G2" in which:
+            g2_propagate(du)
+        if "G3" in which:
+            g3_kmeans(recsys)
+        if "G3b" in which:
+            g3b_arxiv()
+        if "G5" in which:
+            g5_clustgdd(agent, "cora")
+            g5_clustgdd(agent, "ogbn-arxiv")
+        if "G6" in which:
+            g6_condense(du, agent)
     with open(os.path.join(OUT, "VERSIONS.json"), "w") as f:
         json.dump({"scikit-learn": sklearn.__version__, "numpy": np.__version__,
                    "scipy": scipy.__version__, "torch": torch.__version__,
