@@ -58,17 +58,46 @@ __global__ void k_edge_cos(int64_t nnz, int C, const int32_t* __restrict__ rows,
   const float* a = xu + (int64_t)rows[e] * C;
   const float* b = xu + (int64_t)col[e] * C;
   float s = 0.f;
-  for (int j = 0; j < C; ++j) s = s + a[j] * b[j];
+  int j = 0;
+  if ((C & 3) == 0) {  // rows 16-byte aligned: 8 float4 pairs in flight ahead of the ordered sum
+    for (; j + 32 <= C; j += 32) {
+      float4 x[8], y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        x[u] = *reinterpret_cast<const float4*>(a + j + 4 * u);
+        y[u] = *reinterpret_cast<const float4*>(b + j + 4 * u);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s = s + x[u].x * y[u].x;
+        s = s + x[u].y * y[u].y;
+        s = s + x[u].z * y[u].z;
+        s = s + x[u].w * y[u].w;
+      }
+    }
+    for (; j + 4 <= C; j += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(a + j);
+      const float4 y = *reinterpret_cast<const float4*>(b + j);
+      s = s + x.x * y.x;
+      s = s + x.y * y.y;
+      s = s + x.z * y.z;
+      s = s + x.w * y.w;
+    }
+  }
+  for (; j < C; ++j) s = s + a[j] * b[j];
   rew[e] = (val ? val[e] : 1.0f) * s;
 }
 
-// sequential fp32 row sums in CSR order
+constexpr int kLongRow = 512;  // rows at least this long are summed by a whole workgroup
+
+// sequential fp32 row sums in CSR order (rows shorter than kLongRow: one thread each)
 __global__ void k_row_sums(int64_t n, const int32_t* __restrict__ rowptr, const float* __restrict__ v,
                            float* __restrict__ deg) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
   const int32_t e1 = rowptr[r + 1];
   int32_t e = rowptr[r];
+  if (e1 - e >= kLongRow) return;
   float s = 0.f;
   for (; e + 8 <= e1; e += 8) {
     float t[8];
@@ -79,6 +108,47 @@ __global__ void k_row_sums(int64_t n, const int32_t* __restrict__ rowptr, const 
   }
   for (; e < e1; ++e) s = s + (v ? v[e] : 1.0f);
   deg[r] = s;
+}
+
+// rows of kLongRow+ entries: the workgroup of 64 rows walks its long rows; per row, all threads stage
+// chunks of 4096 values into LDS (coalesced) and thread 0 folds them in order (float4 LDS reads
+// eight ahead of the dependent adds), double-buffered so the next chunk loads under the fold
+__global__ __launch_bounds__(kThreads) void k_row_sums_long(int64_t n, const int32_t* __restrict__ rowptr,
+                                                            const float* __restrict__ v,
+                                                            float* __restrict__ deg) {
+  __shared__ __attribute__((aligned(16))) float buf[2][4096];
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  for (int64_t r = r0; r < min<int64_t>(n, r0 + 64); ++r) {
+    const int32_t b = rowptr[r], e1 = rowptr[r + 1];
+    if (e1 - b < kLongRow) continue;  // uniform across the workgroup
+    float acc = 0.f;
+    int cur = 0;
+    for (int32_t c = b; c < e1; c += 4096) {
+      const int m = min(4096, e1 - c);
+      for (int t = threadIdx.x; t < m; t += kThreads) buf[cur][t] = v ? v[c + t] : 1.0f;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const float4* b4 = reinterpret_cast<const float4*>(buf[cur]);
+        int t = 0;
+        for (; t + 32 <= m; t += 32) {
+          float4 x[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) x[u] = b4[t / 4 + u];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            acc = acc + x[u].x;
+            acc = acc + x[u].y;
+            acc = acc + x[u].z;
+            acc = acc + x[u].w;
+          }
+        }
+        for (; t < m; ++t) acc = acc + buf[cur][t];
+      }
+      cur ^= 1;
+    }
+    if (threadIdx.x == 0) deg[r] = acc;
+    __syncthreads();
+  }
 }
 
 __global__ void k_er(int64_t nnz, const int32_t* __restrict__ rows, const int32_t* __restrict__ col,
@@ -117,7 +187,18 @@ __global__ void k_class_keys(int64_t nnz, int nsets, const int32_t* __restrict__
   }
   const float* pa = probs + (int64_t)rows[e] * nsets;
   const float* pb = probs + (int64_t)col[e] * nsets;
-  for (int i = 0; i < nsets; ++i) keys[(int64_t)i * nnz + e] = okey((pa[i] * pb[i]) * x);
+  int i = 0;
+  if ((nsets & 3) == 0) {
+    for (; i + 4 <= nsets; i += 4) {
+      const float4 u = *reinterpret_cast<const float4*>(pa + i);
+      const float4 v = *reinterpret_cast<const float4*>(pb + i);
+      keys[(int64_t)i * nnz + e] = okey((u.x * v.x) * x);
+      keys[(int64_t)(i + 1) * nnz + e] = okey((u.y * v.y) * x);
+      keys[(int64_t)(i + 2) * nnz + e] = okey((u.z * v.z) * x);
+      keys[(int64_t)(i + 3) * nnz + e] = okey((u.w * v.w) * x);
+    }
+  }
+  for (; i < nsets; ++i) keys[(int64_t)i * nnz + e] = okey((pa[i] * pb[i]) * x);
 }
 
 // ---- radix select of the m-th largest key per set (4 passes of 8 bits, top byte first) ----
@@ -305,12 +386,19 @@ struct FixState {
   int shift;
 };
 
-__global__ void k_label_sizes(int64_t n, const int32_t* __restrict__ labels, int kk,
-                              unsigned long long* __restrict__ size) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  const int a = labels[r];
-  if (a >= 0 && a < kk) atomicAdd(&size[a], 1ull);
+// cluster sizes: per-workgroup LDS histograms (kk <= 16384), merged with one global add per bin
+__global__ __launch_bounds__(kThreads) void k_label_sizes(int64_t n, const int32_t* __restrict__ labels,
+                                                          int kk, unsigned long long* __restrict__ size) {
+  extern __shared__ unsigned int h[];
+  for (int b = threadIdx.x; b < kk; b += kThreads) h[b] = 0u;
+  __syncthreads();
+  for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < n; r += (int64_t)gridDim.x * kThreads) {
+    const int a = labels[r];
+    if (a >= 0 && a < kk) atomicAdd(&h[a], 1u);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kk; b += kThreads)
+    if (h[b]) atomicAdd(&size[b], (unsigned long long)h[b]);
 }
 
 __global__ void k_fix_maxabs(int64_t m, const int32_t* __restrict__ sel, const float* __restrict__ val,
@@ -425,6 +513,8 @@ extern "C" int gdd_attaw_er(int64_t n, int64_t nnz, const int32_t* rowptr, const
   GDD_LAUNCHED();
   k_row_sums<<<grid1(n), kThreads, 0, s>>>(n, rowptr, rew, deg);
   GDD_LAUNCHED();
+  k_row_sums_long<<<grid1(n, 64), kThreads, 0, s>>>(n, rowptr, rew, deg);
+  GDD_LAUNCHED();
   k_er<<<grid1(nnz), kThreads, 0, s>>>(nnz, rows, col, rew, deg, er);
   GDD_LAUNCHED();
   return GDD_OK;
@@ -441,6 +531,8 @@ extern "C" int gdd_vanilla_er(int64_t n, int64_t nnz, const int32_t* rowptr, con
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "vanilla_er: workspace too small");
   if (nnz == 0) return GDD_OK;
   k_row_sums<<<grid1(n), kThreads, 0, s>>>(n, rowptr, val, deg);
+  GDD_LAUNCHED();
+  k_row_sums_long<<<grid1(n, 64), kThreads, 0, s>>>(n, rowptr, val, deg);
   GDD_LAUNCHED();
   k_er<<<grid1(nnz), kThreads, 0, s>>>(nnz, rows, col, val, deg, er);
   GDD_LAUNCHED();
@@ -520,7 +612,9 @@ extern "C" int gdd_graph_compress(int64_t n, const int32_t* labels, int kk, int6
   GDD_HIP(hipMemsetAsync(acc, 0, sizeof(unsigned long long) * (size_t)kk * kk, s));
   GDD_HIP(hipMemsetAsync(size, 0, sizeof(unsigned long long) * (size_t)kk, s));
   GDD_HIP(hipMemsetAsync(fs, 0, sizeof(FixState), s));
-  k_label_sizes<<<grid1(n), kThreads, 0, s>>>(n, labels, kk, size);
+  GDD_REQUIRE(kk <= 16384, "graph_compress: at most 16384 clusters");
+  k_label_sizes<<<(unsigned)std::min<int64_t>(grid1(n), 256), kThreads, sizeof(unsigned) * kk, s>>>(
+      n, labels, kk, size);
   GDD_LAUNCHED();
   if (m > 0) {
     k_fix_maxabs<<<(unsigned)std::min<int64_t>(grid1(m), 1024), kThreads, 0, s>>>(m, sel, val, fs);

@@ -173,14 +173,31 @@ def compress_dense(labels: torch.Tensor, adj: CSRGraph, kk: int) -> torch.Tensor
     return out
 
 
-def graph_compress(cluster_labels, adj_norm, adj_list: Sequence):
+def _stack_to_sparse(stack: torch.Tensor):
+    """[G, kk, kk] dense -> G coalesced sparse COO tensors (what ``.to_sparse()`` gives each),
+    with two host round trips for all G instead of one per matrix."""
+    G, kk = stack.shape[0], stack.shape[1]
+    idx = stack.nonzero()  # row-major: graph, row, col (NaN counts as nonzero, as in to_sparse)
+    vals = stack[idx[:, 0], idx[:, 1], idx[:, 2]]
+    counts = torch.bincount(idx[:, 0], minlength=G).cpu().tolist()
+    out, o = [], 0
+    for c in counts:
+        ij = idx[o:o + c, 1:].t().contiguous()
+        out.append(torch.sparse_coo_tensor(ij, vals[o:o + c], (kk, kk), is_coalesced=True))
+        o += c
+    return out
+
+
+def graph_compress(cluster_labels, adj_norm, adj_list: Sequence, dense: bool = False):
     """ClustGDD.graph_compress (clustgdd_agent_transduct.py:234-250) -> (compressed_graph_list,
     adj_syn), each ``(P^T A P - diag).to_sparse()`` with P the size-normalised one-hot cluster
-    matrix of ``cluster_num = max(label) + 1`` columns."""
+    matrix of ``cluster_num = max(label) + 1`` columns. ``dense=True`` returns the dense matrices
+    (what graph_refusion consumes via ``.to_dense()``, :276) and skips the sparse conversion."""
     adj_norm = _csr(adj_norm)
     dev = adj_norm.device
     labels = _labels_device(cluster_labels, dev)
     kk = int(labels.max().item()) + 1
-    compressed = [compress_dense(labels, _csr(a, dev), kk).to_sparse() for a in adj_list]
-    adj_syn = compress_dense(labels, adj_norm, kk).to_sparse()
-    return compressed, adj_syn
+    graphs = [_csr(a, dev) for a in adj_list] + [adj_norm]
+    stack = torch.stack([compress_dense(labels, g, kk) for g in graphs])
+    mats = list(stack.unbind(0)) if dense else _stack_to_sparse(stack)
+    return mats[:-1], mats[-1]
