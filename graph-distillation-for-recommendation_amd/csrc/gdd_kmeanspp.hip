@@ -839,6 +839,10 @@ struct Kpp1Args {
   float* potv[2];      // [T]
   int64_t* candw[2];   // [T][T]
   int64_t* candself[2];  // [T]
+  int64_t* candr[2];   // fused rounds: the round's T candidates (written by the previous fold)
+  double* candn[2];    // fused rounds: their squared norms
+  int* win;            // fused rounds: [2] the winning trial, by round parity
+  unsigned* counter;   // fused rounds: [k] arrivals per round (zeroed per fit)
   float* centers;
   int64_t* indices;
   SklPlan plan;
@@ -1085,6 +1089,295 @@ __global__ __launch_bounds__(kThr) void k_kpp1_pick(Kpp1Args a, int c) {
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 74);
 }
 
+__device__ __forceinline__ int kpp1_ld(int64_t n) {  // LDS row stride: 8 (mod 64) floats
+  return (int)(((n + 63) & ~63ll) + 8);
+}
+
+// the T potentials of the staged rows (sgemv_t lane chains, n % 4 tail) into s_pot
+struct Kpp1FoldView {
+  int64_t n, m1;
+  int T;
+  const float* w;
+};
+
+__device__ void kpp1_fold(const Kpp1FoldView& a, const float* __restrict__ s_rows, int ld,
+                          float* __restrict__ s_pot) {
+  const int tid = threadIdx.x, T = a.T;
+  const int64_t NB = a.m1;
+  if (tid >= 8 * ((T + 7) & ~7)) return;  // whole waves only (the shuffles below)
+  const int t = tid >> 3, l = tid & 7;
+  const bool act = t < T;
+  const float* row = s_rows + (size_t)(act ? t : 0) * ld;
+  const float* w = a.w;
+  const bool k4x2 = (T & 2) && t >= (T & ~3) && t < (T & ~3) + 2;
+  float acc = 0.f;
+  if (act && NB > 0) {
+    if (k4x2) {  // 4 lanes (o % 4), product then add
+      if (l < 4) {
+        int64_t o = l;
+        if (!w) {
+          for (; o + 4 * 31 < NB; o += 128) {
+            float x[32];
+#pragma unroll
+            for (int q = 0; q < 32; ++q) x[q] = row[o + 4 * q];
+#pragma unroll
+            for (int q = 0; q < 32; ++q) acc = acc + x[q];
+          }
+        }
+        for (; o < NB; o += 4) acc = acc + row[o] * (w ? w[o] : 1.0f);
+      }
+    } else {  // 8 lanes: the first NB&4 entries into lanes 0..3, then lane (o - (NB&4)) % 8; fma
+      const int64_t h4 = NB & 4;
+      if (l < h4) acc = __builtin_fmaf(row[l], w ? w[l] : 1.0f, acc);
+      int64_t o = h4 + l;
+      if (!w) {  // unit weights: fma(x, 1, acc) == acc + x
+        for (; o + 8 * 31 < NB; o += 256) {
+          float x[32];
+#pragma unroll
+          for (int q = 0; q < 32; ++q) x[q] = row[o + 8 * q];
+#pragma unroll
+          for (int q = 0; q < 32; ++q) acc = acc + x[q];
+        }
+      }
+      for (; o < NB; o += 8) acc = __builtin_fmaf(row[o], w ? w[o] : 1.0f, acc);
+    }
+  }
+  // group of 8 lanes at t * 8
+  const int lane = tid & 63, g0 = lane & ~7;
+  const float a0 = __shfl(acc, g0), a1 = __shfl(acc, g0 + 1), a2 = __shfl(acc, g0 + 2),
+              a3 = __shfl(acc, g0 + 3), a4 = __shfl(acc, g0 + 4), a5 = __shfl(acc, g0 + 5),
+              a6 = __shfl(acc, g0 + 6), a7 = __shfl(acc, g0 + 7);
+  if (act && l == 0) {
+    float y = 0.f;
+    if (NB > 0) {
+      if (k4x2) {
+        y = (a0 + a1) + (a2 + a3);
+      } else {
+        const float q0 = a0 + a4, q1 = a1 + a5, q2 = a2 + a6, q3 = a3 + a7;
+        y = (q0 + q1) + (q2 + q3);
+      }
+    }
+    if (a.m1 < a.n) {
+      float sx = row[a.m1] * wv(w, a.m1);
+      for (int64_t o = a.m1 + 1; o < a.n; ++o) sx = __builtin_fmaf(row[o], wv(w, o), sx);
+      y = y + sx;
+    }
+    s_pot[t] = y;
+  }
+}
+
+constexpr int kMaxDimF = 512;  // fused rounds: candidate rows up to this many features
+
+// ---- single-block rounds in ONE launch. Grid (point blocks of 256, T trials): workgroup (b, t)
+// computes trial t's distances for its 256 points; the last workgroup of trial t to finish folds
+// trial t (the pick work: its exact sgemv_t potential, its cumulative potential, and the candidates
+// every trial would draw in round c+1 if t wins). Hand-off without fences, in the first form of
+// MI355X_MICROARCH.md's table: every distance store sc1 (write-through), every storing wave drained
+// (vmcnt(0)), a workgroup barrier, one lane's agent-scope add to the trial's counter for the round;
+// the workgroup whose add returns G-1 reads the row back with sc1 loads. Nothing spins.
+constexpr int kFPts = 256;   // points per distance workgroup
+constexpr int kFPW = 22;     // prefix entries per thread of waves 1..3 in the fold (192 x 22 >= 4096)
+
+template <bool SEQ>
+__global__ __launch_bounds__(256) void k_kpp1_fused(Kpp1Args a, int c) {
+  __shared__ double s_c[kMaxDimF];              // this trial's candidate row (fp64, zero-padded)
+  __shared__ float s_d[kBlk];                   // fold: the row, natural order
+  __shared__ float s_ch[8 * kChainLd];          // fold: chain-major copy (unit weights)
+  __shared__ double s_cum[kBlk];               // fold: the winner-if row's cumulative potential
+  __shared__ double s_wave[4];
+  __shared__ float s_pot;
+  __shared__ double s_cn;
+  __shared__ int s_last;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int t = blockIdx.y, pq = (c - 1) & 1, cq = c & 1, T = a.T, dim = a.dim;
+  const int Tp = c == 1 ? 1 : T;  // trials of round c-1 (round 0: the first centre)
+  const int n = (int)a.n;
+  const int i = blockIdx.x * kFPts + tid;
+  const int ic = min(i, n - 1);
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && t == 0 && c == a.k - 2), 60);
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && t == 0 && c == a.k - 1), 65);
+  // round trip 1: the point's column, round c-1's potentials and this trial's column of its table
+  constexpr int kX = SEQ ? 48 : 1;
+  float x[kX];
+  if (SEQ && dim <= kX) {
+#pragma unroll
+    for (int v = 0; v < kX; ++v) x[v] = a.XT[(int64_t)min(v, dim - 1) * n + ic];
+  }
+  const double xs = a.xsq[ic];
+  float pv[kMaxTrials];
+  int64_t cw[kMaxTrials];
+#pragma unroll
+  for (int q = 0; q < kMaxTrials; ++q) {
+    pv[q] = a.potv[pq][min(q, Tp - 1)];
+    cw[q] = a.candw[pq][(int64_t)min(q, Tp - 1) * T + t];
+  }
+  int bw = 0;  // np.argmin: first minimum, a NaN wins at once
+  float best = pv[0];
+  int64_t ct = cw[0];
+#pragma unroll
+  for (int q = 1; q < kMaxTrials; ++q) {
+    const float pt = pv[q];
+    if (q < Tp && best == best && (pt < best || pt != pt)) {
+      bw = q;
+      best = pt;
+      ct = cw[q];
+    }
+  }
+  // round trip 2: the winner's row, this trial's candidate row
+  const float wi = c == 1 ? a.closest0[ic] : a.dist[pq][(int64_t)bw * n + ic];
+  const int cs = (SEQ && dim <= kX) ? kX : dim;
+  for (int j = tid; j < cs; j += 256) s_c[j] = j < dim ? (double)a.X[ct * dim + min(j, dim - 1)] : 0.0;
+  if (tid == 0) s_cn = a.xsq[ct];
+  if (blockIdx.x == 0 && tid == 0) {
+    a.candself[cq][t] = ct;
+    if (c >= 2 && t == 0) a.indices[c - 1] = a.candself[pq][bw];  // rows gathered after the rounds
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && t == 0 && c == a.k - 2), 61);
+  if (i < n) {
+    double dot = 0.0;
+    if constexpr (SEQ) {
+      if (dim <= kX) {
+#pragma unroll
+        for (int v = 0; v < kX; ++v) dot = __builtin_fma(s_c[v], (double)x[v], dot);
+      } else {
+        for (int j = 0; j < dim; j += 16) {
+          float y[16];
+#pragma unroll
+          for (int v = 0; v < 16; ++v) y[v] = a.XT[(int64_t)min(j + v, dim - 1) * n + i];
+#pragma unroll
+          for (int v = 0; v < 16; ++v)
+            if (j + v < dim) dot = __builtin_fma(s_c[j + v], (double)y[v], dot);
+        }
+      }
+    } else {
+      dot = skl_point_dot(a.plan, s_c, a.X + (int64_t)i * dim, i, t);
+    }
+    float f = (float)(((-2.0 * dot) + s_cn) + xs);
+    f = f < 0.f ? 0.f : f;
+    __hip_atomic_store(a.dist[cq] + (int64_t)t * n + i, np_minimum(wi, f), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);  // sc1: write-through
+  }
+  // hand-off: every storing wave drained, barrier, one agent-scope add per workgroup
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    s_last = __hip_atomic_fetch_add(a.counter + (int64_t)c * T + t, 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 62);
+  // ---- fold trial t (its last workgroup): the row back with sc1 loads
+  const double ut = (c + 1 < a.k && tid < T) ? a.uniforms[(int64_t)c * T + tid] : 0.0;
+  const int m1 = (int)a.m1;
+  const bool k4x2 = (T & 2) && t >= (T & ~3) && t < (T & ~3) + 2;
+  const int h4 = k4x2 ? 0 : (m1 & 4);
+  const bool perm = a.w == nullptr;
+  {
+    const float* row = a.dist[cq] + (int64_t)t * n;
+    float r[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      r[q] = __hip_atomic_load(row + min(tid + 256 * q, n - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = tid + 256 * q;
+      if (e < n) {
+        s_d[e] = r[q];
+        if (perm && e >= h4 && e < m1) {
+          const int o = e - h4;
+          if (k4x2)
+            s_ch[(o & 3) * kChainLd + (o >> 2)] = r[q];
+          else
+            s_ch[(o & 7) * kChainLd + (o >> 3)] = r[q];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 63);
+  const int jp = tid - 64;  // prefix thread of waves 1..3
+  double pre[kFPW];
+  if (wave == 0) {  // sgemv_t: the lane chains, then the n % 4 trailing entries
+    float y = 0.f;
+    if (m1 > 0) {
+      if (perm) {
+        const int nl = k4x2 ? 4 : 8;
+        float acc = 0.f;
+        if (lane < nl) {
+          if (lane < h4) acc = acc + s_d[lane];
+          const int L = (m1 - h4 - lane + nl - 1) / nl;
+          acc = chain_add(s_ch + lane * kChainLd, max(L, 0), acc);
+        }
+        if (k4x2) {
+          const float a1 = __shfl(acc, 1), a2 = __shfl(acc, 2), a3 = __shfl(acc, 3);
+          y = (acc + a1) + (a2 + a3);
+        } else {
+          const float ql = acc + __shfl(acc, (lane + 4) & 63);
+          const float q1 = __shfl(ql, 1), q2 = __shfl(ql, 2), q3 = __shfl(ql, 3);
+          y = (ql + q1) + (q2 + q3);
+        }
+      } else {
+        y = sgemv_block_wave(s_d, a.w, m1, t, T);
+      }
+    }
+    if (m1 < n && lane == 0) {
+      float sx = s_d[m1] * wv(a.w, m1);
+      for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_d[o], wv(a.w, o), sx);
+      y = y + sx;
+    }
+    if (lane == 0) {
+      s_pot = y;
+      a.potv[cq][t] = y;
+    }
+  } else {  // the cumulative potential: thread runs and the wave's inclusive scan
+    double run = 0.0;
+#pragma unroll
+    for (int q = 0; q < kFPW; ++q) {
+      const int e = kFPW * jp + q;
+      run = run + (e < n ? (double)(wv(a.w, e) * s_d[min(e, n - 1)]) : 0.0);
+      pre[q] = run;
+    }
+    double inc = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double y = __shfl_up(inc, o);
+      if (lane >= o) inc = inc + y;
+    }
+    double ex = __shfl_up(inc, 1);
+    if (lane == 0) ex = 0.0;
+    if (lane == 63) s_wave[wave - 1] = inc;
+#pragma unroll
+    for (int q = 0; q < kFPW; ++q) pre[q] = ex + pre[q];
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 70);
+  if (c + 1 < a.k) {
+    if (wave > 0) {
+      double B = 0.0;
+      for (int q = 0; q < wave - 1; ++q) B = B + s_wave[q];
+      const double pot = (double)s_pot;
+#pragma unroll
+      for (int q = 0; q < kFPW; ++q) {
+        const int e = kFPW * jp + q;
+        if (e < n) s_cum[e] = B + pre[q];
+      }
+      (void)pot;
+    }
+    __syncthreads();
+    if (tid < T) {  // searchsorted_left(cum, u * pot) over the LDS cumulative potential
+      const double rr = ut * (double)s_pot;
+      int lo = 0, hi = n;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_cum[mid] < rr) lo = mid + 1; else hi = mid;
+      }
+      a.candw[cq][(int64_t)t * T + tid] = min(n - 1, lo);
+    }
+  }
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 74);
+}
+
 // after round k-1: its winner and centre
 __global__ __launch_bounds__(64) void k_kpp1_final(Kpp1Args a, int c) {
   const int q = c & 1;
@@ -1092,6 +1385,15 @@ __global__ __launch_bounds__(64) void k_kpp1_final(Kpp1Args a, int c) {
   const int64_t src = a.candself[q][b];
   if (threadIdx.x == 0) a.indices[c] = src;
   for (int j = threadIdx.x; j < a.dim; j += 64) a.centers[(int64_t)c * a.dim + j] = a.X[src * a.dim + j];
+}
+
+// centres from their indices (fused rounds record only the index of each round's winner)
+__global__ void k_kpp_gather_centres(int k, int dim, const float* __restrict__ X,
+                                     const int64_t* __restrict__ indices, float* __restrict__ centers) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)k * dim) return;
+  const int64_t c = e / dim, j = e - c * dim;
+  centers[e] = X[indices[c] * dim + j];
 }
 
 // X^T (dim x n) for the single-block distance phase: coalesced loads
@@ -1165,7 +1467,14 @@ extern "C" int gdd_skl_sqdist(int n_rows, const float* C, int64_t n, int dim, co
   return GDD_OK;
 }
 
+size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k);
+
 extern "C" size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int dim, int n_trials) {
+  return kpp_ws_bytes(n, dim, n_trials, (int)std::min<int64_t>(n, INT_MAX));
+}
+
+// k (centres) only sizes the fused rounds' arrival counters; the query bounds it by n
+size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k) {
   const size_t T = (size_t)std::max(n_trials, 1);
   const size_t nblk = (size_t)((n + kBlk - 1) / kBlk);
   size_t b = 0;
@@ -1181,6 +1490,8 @@ extern "C" size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int dim, int n_trials)
   b += 2 * align256(sizeof(float) * T);       // potv
   b += 2 * align256(sizeof(int64_t) * T * T); // candw
   b += 2 * align256(sizeof(int64_t) * T);     // candself
+  b += 2 * align256(sizeof(int64_t) * T) + 2 * align256(sizeof(double) * T);  // candr, candn
+  b += align256(sizeof(int) * 2) + align256(sizeof(unsigned) * (size_t)std::max(k, 1) * T);  // counters
   if (n <= kBlk) b += align256(sizeof(float) * n * (size_t)std::max(dim, 1));  // XT
   return b + 1024;
 }
@@ -1215,6 +1526,10 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   for (int q = 0; q < 2; ++q) b1.potv[q] = cv.take<float>(T);
   for (int q = 0; q < 2; ++q) b1.candw[q] = cv.take<int64_t>((size_t)T * T);
   for (int q = 0; q < 2; ++q) b1.candself[q] = cv.take<int64_t>(T);
+  for (int q = 0; q < 2; ++q) b1.candr[q] = cv.take<int64_t>(T);
+  for (int q = 0; q < 2; ++q) b1.candn[q] = cv.take<double>(T);
+  b1.win = cv.take<int>(2);
+  b1.counter = cv.take<unsigned>((size_t)std::min<int64_t>(n, INT_MAX) * T);
   float* XT = n <= kBlk ? cv.take<float>((size_t)n * dim) : nullptr;
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans++: workspace too small");
   a.n = n;
@@ -1277,6 +1592,26 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     const dim3 g1((unsigned)((n + kPts - 1) / kPts), (unsigned)(((T + kTg - 1) / kTg + 3) / 4));
     k_kpp1_pick<<<1, kThr, 0, s>>>(b1, 0);
     GDD_LAUNCHED();
+    const dim3 gf((unsigned)((n + kFPts - 1) / kFPts), (unsigned)T);
+    if (dim <= kMaxDimF && gf.x * gf.y <= 256 && getenv("GDD_KPP_TWO_LAUNCH") == nullptr) {
+      // one launch per round: distances, then each trial's last workgroup folds it (no fences)
+      GDD_HIP(hipMemsetAsync(b1.counter, 0, sizeof(unsigned) * (size_t)k * T, s));
+      for (int c = 1; c < k; ++c) {
+        if (seq)
+          k_kpp1_fused<true><<<gf, 256, 0, s>>>(b1, c);
+        else
+          k_kpp1_fused<false><<<gf, 256, 0, s>>>(b1, c);
+        GDD_LAUNCHED();
+      }
+      k_kpp1_final<<<1, 64, 0, s>>>(b1, k - 1);
+      GDD_LAUNCHED();
+      if (k > 2) {  // rounds 1..k-2 recorded indices only (round 0's and k-1's rows are written)
+        k_kpp_gather_centres<<<(unsigned)(((int64_t)k * dim + 255) / 256), 256, 0, s>>>(k, dim, X, indices,
+                                                                                         centers);
+        GDD_LAUNCHED();
+      }
+      return GDD_OK;
+    }
     for (int c = 1; c < k; ++c) {
       if (seq)
         k_kpp1_dist<true><<<g1, 256, lds1, s>>>(b1, c);

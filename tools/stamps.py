@@ -50,10 +50,10 @@ def main():
         show("update tail", a, list(range(30, 33)), 30)
         show("mb_reassign", a, list(range(40, 47)), 40)
         t0 = p[60]
-        lab = {60: "dist start", 66: "XT loaded", 67: "potv[0]", 68: "potv[1]", 61: "argmin", 62: "cand rows", 63: "dist end", 70: "pick start",
-               71: "staged", 72: "prefix", 73: "chain", 74: "pick end", 65: "next dist start"}
-        print("kpp single-block round k-2 (us): " + ", ".join(
-            f"{lab[q]} {(p[q] - t0) / 100:.2f}" for q in [60, 61, 62, 63, 70, 71, 72, 73, 74, 65]))
+        lab = {60: "start", 61: "cand row", 62: "last arrived", 63: "row staged", 70: "chain+prefix",
+               74: "end", 65: "next start"}
+        print("kpp fused round k-2 (us): " + ", ".join(
+            f"{lab[q]} {(p[q] - t0) / 100:.2f}" for q in [60, 61, 62, 63, 70, 74, 65]))
 
 
 if __name__ == "__main__":
