@@ -470,27 +470,45 @@ __global__ __launch_bounds__(64 * WAVES) void k_assign_small(
 // eight float4 reads are issued before the current 32 dependent adds, so the add chain (not the
 // LDS latency) bounds it. b must be 16-byte aligned.
 __device__ __forceinline__ float fold_seq_lds(const float* __restrict__ b, int m, float acc) {
+  // two register buffers of 8 float4, used alternately (no copies): each loads while the other's
+  // 32 terms are added
   const float4* b4 = reinterpret_cast<const float4*>(b);
   const int g = m >> 5;
+  int q = 0;
   if (g > 0) {
-    float4 cur[8];
+    float4 A[8], B[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) cur[u] = b4[u];
-    for (int q = 0; q < g; ++q) {
-      float4 nxt[8];
-      if (q + 1 < g) {
+    for (int u = 0; u < 8; ++u) A[u] = b4[u];
+    for (; q + 2 <= g; q += 2) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) nxt[u] = b4[(q + 1) * 8 + u];
+      for (int u = 0; u < 8; ++u) B[u] = b4[(q + 1) * 8 + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc = acc + A[u].x;
+        acc = acc + A[u].y;
+        acc = acc + A[u].z;
+        acc = acc + A[u].w;
+      }
+      if (q + 2 < g) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) A[u] = b4[(q + 2) * 8 + u];
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        acc = acc + cur[u].x;
-        acc = acc + cur[u].y;
-        acc = acc + cur[u].z;
-        acc = acc + cur[u].w;
+        acc = acc + B[u].x;
+        acc = acc + B[u].y;
+        acc = acc + B[u].z;
+        acc = acc + B[u].w;
       }
+    }
+    if (q < g) {  // one group left, in A
 #pragma unroll
-      for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
+      for (int u = 0; u < 8; ++u) {
+        acc = acc + A[u].x;
+        acc = acc + A[u].y;
+        acc = acc + A[u].z;
+        acc = acc + A[u].w;
+      }
     }
   }
   for (int t = g << 5; t < m; ++t) acc = acc + b[t];
