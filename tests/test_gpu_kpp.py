@@ -68,6 +68,11 @@ KPP_CASES = [
     (1500, 1, 25, None, None),
     (1000, 12, 30, None, 1),    # one trial: sdot potentials
     (3000, 40, 120, None, None),
+    (3000, 48, 60, None, None),   # fused rounds: the 48-feature register chain, and one past it
+    (3000, 49, 60, None, None),
+    (700, 600, 30, None, None),   # rows wider than the fused kernel's 512: two launches per round
+    (10, 3, 2, None, None),       # k = 2: a single round, no centre gather
+    (2708, 7, 70, None, None),    # Cora shape: T = 6, two trials on the 4-lane sgemv_t kernel
 ]
 
 
@@ -81,5 +86,17 @@ def test_kmeans_plusplus_orders(n, dim, k, dup, trials):
     ops = _Ops("cuda", n, k, dim)
     c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(5),
                                  n_local_trials=trials)
+    assert np.array_equal(idx.cpu().numpy(), idx_ref)
+    assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref))
+
+
+def test_kmeans_plusplus_two_launch_path(monkeypatch):
+    """The two-launch rounds (GDD_KPP_TWO_LAUNCH) give the same seeding as the fused ones."""
+    n, dim, k = 3000, 40, 90
+    X = np.ascontiguousarray(synth.blobs(n, dim, 20, seed=9), np.float32)
+    c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(3))
+    monkeypatch.setenv("GDD_KPP_TWO_LAUNCH", "1")
+    ops = _Ops("cuda", n, k, dim)
+    c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(3))
     assert np.array_equal(idx.cpu().numpy(), idx_ref)
     assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref))
