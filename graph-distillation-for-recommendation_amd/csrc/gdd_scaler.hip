@@ -89,3 +89,14 @@ extern "C" int gdd_standard_scaler(int64_t n, int dim, const float* X, float* X_
   GDD_LAUNCHED();
   return GDD_OK;
 }
+
+extern "C" int gdd_standard_scaler_transform(int64_t n, int dim, const float* X, const double* mean,
+                                             const double* scale, float* X_out, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && dim > 0 && X && X_out && mean && scale, "standard_scaler_transform: bad arguments");
+  hipStream_t s = to_hip(stream);
+  const int64_t total = n * (int64_t)dim;
+  k_scale_rows<<<(unsigned)std::min<int64_t>((total + 255) / 256, 8192), 256, 0, s>>>(
+      total, dim, X, mean, scale, X_out);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}

@@ -17,12 +17,13 @@ from . import _lib  # noqa: F401  (imports torch first, see _lib docstring)
 from . import pipeline  # noqa: F401
 from .cluster import argmax_rows, cluster_mean, group_by_label
 from .condense import ER_estimator, attaw_ER_estimator, graph_compress, graph_sparse
-from .graph import CSRGraph, normalize_adj, normalize_adj_tensor, propagate, spmm, to_csr
+from .graph import (CSRGraph, induced_subgraph, normalize_adj, normalize_adj_tensor, propagate, spmm,
+                    to_csr)
 from .kmeans import KMeans, MiniBatchKMeans
 from .sharded import ShardedKMeans, shard_rows
 
 __all__ = [
     "CSRGraph", "to_csr", "normalize_adj", "normalize_adj_tensor", "propagate", "spmm",
     "KMeans", "MiniBatchKMeans", "ShardedKMeans", "shard_rows", "cluster_mean", "argmax_rows",
-    "group_by_label", "graph_sparse", "graph_compress", "ER_estimator", "attaw_ER_estimator",
+    "induced_subgraph", "group_by_label", "graph_sparse", "graph_compress", "ER_estimator", "attaw_ER_estimator",
 ]

@@ -78,6 +78,7 @@ SIGNATURES = {
     "gdd_kmeans_plusplus": (_c_int, [_c_i64, _c_int, _vp, _vp, _c_int, _c_int, _c_i64, _vp, _vp,
                                      _vp, _vp, _c_size, _vp]),
     "gdd_standard_scaler": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "gdd_standard_scaler_transform": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "gdd_cluster_mean": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _c_int, _c_int, _vp, _vp, _vp]),
     "gdd_argmax_rows": (_c_int, [_c_int, _c_int, _vp, _vp, _vp]),
     "gdd_coo_rows": (_c_int, [_c_i64, _vp, _vp, _vp]),
@@ -92,6 +93,10 @@ SIGNATURES = {
     "gdd_compress_ws_bytes": (_c_size, [_c_int]),
     "gdd_graph_compress": (_c_int, [_c_i64, _vp, _c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                     _c_size, _vp]),
+    "gdd_subgraph_ws_bytes": (_c_size, [_c_i64, _c_i64]),
+    "gdd_subgraph_count": (_c_int, [_c_i64, _vp, _vp, _c_i64, _vp, _vp, _vp, _c_size, _vp]),
+    "gdd_subgraph_fill": (_c_int, [_c_i64, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _c_size, _vp]),
     "gdd_select_csr_ws_bytes": (_c_size, [_c_i64]),
     "gdd_select_csr": (_c_int, [_c_i64, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_size,
                                 _vp]),

@@ -120,6 +120,44 @@ def normalize_adj(adj: CSRGraph, self_loops: int = -1) -> CSRGraph:
     return CSRGraph(rowptr_out, col_out[:nnz_out], val_out[:nnz_out], n)
 
 
+def induced_subgraph(adj: CSRGraph, idx) -> CSRGraph:
+    """``adj[np.ix_(idx, idx)]`` on the device, canonical CSR (utils_graphsaint.py:34-36: the
+    inductive agent's ``adj_train/val/test``, clustgdd_agent_induct.py:38-94).
+
+    ``idx`` (host array or device tensor of node ids) must be strictly increasing, as GraphSAINT's
+    role lists are; the kernels flag any other order and this raises ValueError. Values are kept
+    (a binary graph stays binary).
+    """
+    lib = _lib.device_lib()
+    dev = adj.device
+    if isinstance(idx, torch.Tensor):
+        ix = idx.to(device=dev, dtype=torch.int32).contiguous()
+    else:
+        h = np.asarray(idx, dtype=np.int64)
+        if h.size and (h.min() < 0 or h.max() >= adj.n or np.any(np.diff(h) <= 0)):
+            raise ValueError("induced_subgraph: idx must be strictly increasing node ids in [0, n)")
+        ix = torch.from_numpy(np.ascontiguousarray(h.astype(np.int32))).to(dev)
+    m = int(ix.numel())
+    if m == 0:
+        raise ValueError("induced_subgraph: empty node set")
+    rowptr = torch.empty(m + 1, dtype=torch.int32, device=dev)
+    ws = _lib.workspace(lib.gdd_subgraph_ws_bytes(adj.n, m), dev)
+    st = _lib.stream_ptr(dev)
+    _lib.check(lib.gdd_subgraph_count(adj.n, adj.rowptr.data_ptr(), _lib.ptr(adj.col), m,
+                                      ix.data_ptr(), rowptr.data_ptr(), ws.data_ptr(), ws.numel(), st))
+    nnz = int(rowptr[m].item())
+    col = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    val = None if adj.val is None else torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+    bad = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.check(lib.gdd_subgraph_fill(adj.n, adj.rowptr.data_ptr(), _lib.ptr(adj.col),
+                                     _lib.ptr(adj.val), m, ix.data_ptr(), rowptr.data_ptr(),
+                                     col.data_ptr(), _lib.ptr(val), bad.data_ptr(), ws.data_ptr(),
+                                     ws.numel(), st))
+    if int(bad.item()):
+        raise ValueError("induced_subgraph: idx must be strictly increasing node ids in [0, n)")
+    return CSRGraph(rowptr, col[:nnz], None if val is None else val[:nnz], m)
+
+
 def normalize_adj_tensor(adj, sparse: bool = True, device=None) -> CSRGraph:
     """Drop-in for deep_robust_utils.normalize_adj_tensor(adj, sparse=True) (:245-256)."""
     if not sparse:

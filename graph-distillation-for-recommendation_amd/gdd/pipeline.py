@@ -5,6 +5,10 @@
   logits (MiniBatchKMeans for ogbn-arxiv, KMeans otherwise), per-cluster feature means and argmax
   labels. The MLP that produces the logits (models/gcn.py:626-653) is the caller's: pass the
   logits, or a callable that maps ``target_feat`` to them.
+* :func:`pretrained_clustering_induct_hot_path` — the inductive agent's path
+  (clustgdd_agent_induct.py:37-155): the same stages per role sub-graph (train/val/test), k-means on
+  the train logits (MiniBatchKMeans for reddit, KMeans otherwise); :func:`graphsaint_split` builds
+  its inputs as ``utils_graphsaint.DataGraphSAINT`` does (induced sub-graphs, train-fitted scaler).
 * :func:`kmeans_cluster` — ``distill_recsys.kmeans_cluster`` (distill_recsys.py:158-181):
   StandardScaler on the device (``gdd_standard_scaler``), then MiniBatchKMeans when
   ``minibatch and n > 20000`` else KMeans, ``n_init="auto"``; returns (labels int64, centres fp32).
@@ -18,7 +22,7 @@ import torch
 
 from . import _lib
 from .cluster import argmax_rows, cluster_mean
-from .graph import normalize_adj, propagate, to_csr
+from .graph import CSRGraph, induced_subgraph, normalize_adj, propagate, to_csr
 from .kmeans import KMeans, MiniBatchKMeans
 
 
@@ -34,6 +38,45 @@ def standard_scaler(X, device="cuda"):
     _lib.check(lib.gdd_standard_scaler(n, dim, Xd.data_ptr(), out.data_ptr(), mean.data_ptr(),
                                        scale.data_ptr(), _lib.stream_ptr(Xd.device)))
     return out, mean, scale
+
+
+def standard_scaler_transform(X, mean: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    """StandardScaler.transform with a fitted (mean_, scale_) (fp64 device vectors)."""
+    lib = _lib.device_lib()
+    Xd = X.to(dtype=torch.float32).contiguous()
+    out = torch.empty_like(Xd)
+    _lib.check(lib.gdd_standard_scaler_transform(Xd.shape[0], Xd.shape[1], Xd.data_ptr(),
+                                                 mean.data_ptr(), scale.data_ptr(), out.data_ptr(),
+                                                 _lib.stream_ptr(Xd.device)))
+    return out
+
+
+def graphsaint_split(adj_full, feat, idx_train, idx_val, idx_test, device="cuda"):
+    """The preparation of ``utils_graphsaint.DataGraphSAINT`` (utils_graphsaint.py:17-50) on the
+    device, from the already-loaded ``adj_full`` and raw ``feats``: the three induced sub-graphs
+    ``adj_full[np.ix_(idx, idx)]`` and the features standardised with a StandardScaler fitted on
+    the train rows (then ``feat[idx]`` per role). Role lists must be strictly increasing (the
+    GraphSAINT role.json lists are). Returns a namespace with the reference's attribute names
+    (adj_full, feat_full, feat_train/val/test, adj_train/val/test, idx_train/val/test); graphs are
+    :class:`CSRGraph`, features device fp32. (The ogbn-arxiv symmetrisation at :19-21 is a
+    file-format fix-up of one dataset and is left to the loader.)
+    """
+    from types import SimpleNamespace
+    g = adj_full if isinstance(adj_full, CSRGraph) else to_csr(adj_full, device=device)
+    X = feat if isinstance(feat, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(feat, np.float32))
+    X = X.to(device=g.device, dtype=torch.float32).contiguous()
+    ids = {}
+    for name, idx in (("train", idx_train), ("val", idx_val), ("test", idx_test)):
+        t = idx if isinstance(idx, torch.Tensor) else torch.from_numpy(np.asarray(idx, np.int64))
+        ids[name] = t.to(device=g.device, dtype=torch.int64)
+    _, mean, scale = standard_scaler(X.index_select(0, ids["train"]), device=g.device)  # :40-42
+    feat_full = standard_scaler_transform(X, mean, scale)                                # :43
+    ns = SimpleNamespace(adj_full=g, feat_full=feat_full, scaler_mean=mean, scaler_scale=scale)
+    for name, t in ids.items():
+        setattr(ns, "idx_" + name, t)
+        setattr(ns, "feat_" + name, feat_full.index_select(0, t))                         # :46-48
+        setattr(ns, "adj_" + name, induced_subgraph(g, t))                                 # :34-36
+    return ns
 
 
 def kmeans_cluster(X, n_clusters: int, seed: int, minibatch: bool = True, batch_size: int = 2048,
@@ -85,3 +128,38 @@ def pretrained_clustering_hot_path(features, adj, T: int, alpha: float, logits, 
     feat_syn, _ = cluster_mean(target_feat, km.labels_device_, nnodes_syn)  # transduct:121-125
     labels_syn = argmax_rows(km.cluster_centers_device_)                    # transduct:126
     return feat_syn, labels_syn, km.labels_device_.to(torch.int32), adj_norm, target_feat, prop_feat
+
+
+def pretrained_clustering_induct_hot_path(data, T: int, alpha: float, logits_train, nnodes_syn: int,
+                                          dataset: str = "", seed: int = 15,
+                                          cluster_minibatch: int = 1000, device="cuda"):
+    """The hot path of the inductive ClustGDD.pretrained_clustering (clustgdd_agent_induct.py:37-155).
+
+    ``data`` carries ``adj_train/adj_val/adj_test`` (CSRGraph or anything :func:`to_csr` takes) and
+    ``feat_train/feat_val/feat_test`` (e.g. :func:`graphsaint_split`'s result). ``logits_train``: the
+    MLP's train-node output (n_train x C), or a callable ``f(target_train, target_val) -> logits``
+    (the MLP is fitted on both, :103-109). Each role graph is normalised and propagated on its own
+    (:56-94); k-means runs on the train logits — MiniBatchKMeans(random_state=seed) for 'reddit',
+    KMeans on the global numpy RNG otherwise (:129-134) — and the cluster means are taken over the
+    train targets (:143-154). Returns (cluster_feat_centers, cluster_center_labels, cluster_labels
+    int32, target_feat_train, adj_train_norm, target_feat_val, target_feat_test).
+    """
+    targets, norms = {}, {}
+    for name in ("train", "val", "test"):
+        adj = getattr(data, "adj_" + name)
+        g = adj if isinstance(adj, CSRGraph) else to_csr(adj, device=device)
+        norms[name] = normalize_adj(g)                                              # :56-64
+        X = getattr(data, "feat_" + name)
+        X = X if isinstance(X, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(X, np.float32))
+        X = X.to(device=g.device, dtype=torch.float32).contiguous()
+        targets[name], _ = propagate(norms[name], X, T, alpha)                      # :67-94
+    out = logits_train(targets["train"], targets["val"]) if callable(logits_train) else logits_train
+    if dataset == "reddit":                                                         # :129-134
+        km = MiniBatchKMeans(n_clusters=nnodes_syn, random_state=seed, batch_size=cluster_minibatch,
+                             device=device).fit(out)
+    else:
+        km = KMeans(n_clusters=nnodes_syn, device=device).fit(out)
+    feat_syn, _ = cluster_mean(targets["train"], km.labels_device_, nnodes_syn)     # :143-151
+    labels_syn = argmax_rows(km.cluster_centers_device_)                            # :152
+    return (feat_syn, labels_syn, km.labels_device_.to(torch.int32), targets["train"], norms["train"],
+            targets["val"], targets["test"])

@@ -251,6 +251,10 @@ int gdd_skl_sqdist(int n_rows, const float* C, int64_t n, int dim, const float* 
 /* ---------------------------------------------------------------------------------------------- */
 int gdd_standard_scaler(int64_t n, int dim, const float* X, float* X_out, double* mean,
                         double* scale, gdd_stream_t stream);
+/* StandardScaler.transform with a fitted mean/scale (utils_graphsaint.py:41-44 fits on the train   */
+/* rows and transforms every row): X_out = fp32(fp32(x - mean) / scale).                            */
+int gdd_standard_scaler_transform(int64_t n, int dim, const float* X, const double* mean,
+                                  const double* scale, float* X_out, gdd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* (a7) cluster-feature mean. Replaces clustgdd_agent_transduct.py:116-127 (induct :143-154) and the  */
@@ -304,6 +308,22 @@ size_t gdd_select_csr_ws_bytes(int64_t n);
 int gdd_select_csr(int64_t n, const int32_t* rows, const int32_t* col, const float* val, int64_t m,
                    const int32_t* sel, int32_t* rowptr_out, int32_t* col_out, float* val_out, void* ws,
                    size_t ws_bytes, gdd_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* induced sub-graph adj_full[np.ix_(idx, idx)] as canonical CSR (utils_graphsaint.py:34-36; the   */
+/* inductive agent's train/val/test graphs, clustgdd_agent_induct.py:38-94). idx: m strictly        */
+/* increasing node ids. Two calls: _count writes rowptr_out (m+1; nnz_out = rowptr_out[m], read by  */
+/* the caller to size col/val), _fill writes col_out / val_out (val_out NULL: binary) and copies a  */
+/* flag (nonzero if idx was not strictly increasing or out of range) to bad_out (device, nullable). */
+/* Both calls share one workspace (gdd_subgraph_ws_bytes), which _count fills and _fill reads.      */
+/* ---------------------------------------------------------------------------------------------- */
+size_t gdd_subgraph_ws_bytes(int64_t n, int64_t m);
+int gdd_subgraph_count(int64_t n, const int32_t* rowptr, const int32_t* col, int64_t m,
+                       const int32_t* idx, int32_t* rowptr_out, void* ws, size_t ws_bytes,
+                       gdd_stream_t stream);
+int gdd_subgraph_fill(int64_t n, const int32_t* rowptr, const int32_t* col, const float* val, int64_t m,
+                      const int32_t* idx, const int32_t* rowptr_out, int32_t* col_out, float* val_out,
+                      int32_t* bad_out, void* ws, size_t ws_bytes, gdd_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -440,3 +440,38 @@ def standard_scaler(X):
     c = (X.astype(np.float64) - mean).astype(np.float32)
     out = (c.astype(np.float64) / scale).astype(np.float32)
     return out, mean, scale
+
+
+# ------------------------------------------------------------------------------------------------
+# GraphSAINT preparation (utils_graphsaint.py:34-48): induced sub-graphs adj_full[np.ix_(idx, idx)]
+# and a StandardScaler fitted on the train rows, applied to every row
+# ------------------------------------------------------------------------------------------------
+def induced_subgraph(rowptr, col, val, idx):
+    """CSR (rowptr, col, val) of A[idx][:, idx] for strictly increasing idx; val None = binary."""
+    rowptr = np.asarray(rowptr, np.int64)
+    col = np.asarray(col, np.int64)
+    idx = np.asarray(idx, np.int64)
+    n = len(rowptr) - 1
+    if len(idx) and (np.any(np.diff(idx) <= 0) or idx[0] < 0 or idx[-1] >= n):
+        raise ValueError("idx must be strictly increasing node ids")
+    pos = np.full(n, -1, np.int64)
+    pos[idx] = np.arange(len(idx))
+    out_rp = [0]
+    out_c, out_v = [], []
+    for r in idx:
+        cs = col[rowptr[r]:rowptr[r + 1]]
+        q = pos[cs]
+        keep = q >= 0
+        out_c.append(q[keep])
+        if val is not None:
+            out_v.append(np.asarray(val, np.float32)[rowptr[r]:rowptr[r + 1]][keep])
+        out_rp.append(out_rp[-1] + int(keep.sum()))
+    c = np.concatenate(out_c).astype(np.int32) if out_c else np.zeros(0, np.int32)
+    v = None if val is None else (np.concatenate(out_v) if out_v else np.zeros(0, np.float32))
+    return np.asarray(out_rp, np.int32), c, v
+
+
+def scaler_transform(X, mean, scale):
+    """StandardScaler.transform on fp32 X: fp32(fp32(x - mean) / scale) (two fp64 ufuncs, fp32 out)."""
+    c = (np.asarray(X, np.float32).astype(np.float64) - mean).astype(np.float32)
+    return (c.astype(np.float64) / scale).astype(np.float32)

@@ -123,3 +123,33 @@ def test_standard_scaler_vs_oracle():
     ref, m_ref, s_ref = O.standard_scaler(X)
     assert np.array_equal(bits(out.cpu().numpy()), bits(ref))
     assert np.array_equal(mean.cpu().numpy(), m_ref) and np.array_equal(scale.cpu().numpy(), s_ref)
+
+
+@pytest.mark.parametrize("tag", ["flickr", "reddit"])
+def test_pretrained_clustering_induct_vs_reference(tag):
+    """DataGraphSAINT's preparation + the inductive pretrained_clustering on the device (G7)."""
+    from gdd import pipeline
+    z = load(f"golden_clustgdd_induct_{tag}.npz")
+    data = pipeline.graphsaint_split(_graph(z["rowptr"], z["col"]), z["feat_raw"], z["idx_train"],
+                                     z["idx_val"], z["idx_test"])
+    assert np.array_equal(bits(data.feat_full.cpu().numpy()), bits(z["feat_full"]))
+    for name in ("train", "val", "test"):
+        g = getattr(data, "adj_" + name)
+        assert g.val is None  # binary stays binary
+        assert np.array_equal(g.rowptr.cpu().numpy(), z[f"sub_{name}_rowptr"])
+        assert np.array_equal(g.col.cpu().numpy(), z[f"sub_{name}_col"])
+    k = int(z["n_syn"])
+    np.random.set_state(rng_from_fixture(z).get_state())  # KMeans(random_state=None): global RNG
+    feat_syn, labels_syn, cl, tgt, gn, tv, tt = pipeline.pretrained_clustering_induct_hot_path(
+        data, int(z["T"]), float(z["alpha"]), z["kmeans_X"], k, dataset=tag, seed=15,
+        cluster_minibatch=100)
+    r, c, v = csr_to_sorted_coo(gn.rowptr.cpu().numpy(), gn.col.cpu().numpy(), gn.val.cpu().numpy())
+    assert np.array_equal(r, z["norm_train_row"]) and np.array_equal(c, z["norm_train_col"])
+    assert np.array_equal(bits(v), bits(z["norm_train_val"]))
+    np.testing.assert_allclose(tgt.cpu().numpy(), z["target_train"], rtol=PROP_RTOL, atol=PROP_ATOL)
+    np.testing.assert_allclose(tv.cpu().numpy(), z["target_val"], rtol=PROP_RTOL, atol=PROP_ATOL)
+    assert tt.shape == (len(z["idx_test"]), z["feat_raw"].shape[1])
+    assert np.array_equal(cl.cpu().numpy(), z["cluster_labels"])
+    np.testing.assert_allclose(feat_syn.cpu().numpy(), z["feat_syn"], rtol=MEAN_RTOL, atol=MEAN_ATOL,
+                               equal_nan=True)
+    assert np.array_equal(labels_syn.cpu().numpy(), z["labels_syn"])

@@ -133,3 +133,41 @@ def test_kmeans_plusplus_vs_sklearn_duplicates(n, dim, k, seed):
     co, io = O.kmeans_plusplus(X, k, np.random.RandomState(seed))
     assert np.array_equal(ii, io)
     assert np.array_equal(bits(ci), bits(co))
+
+
+@pytest.mark.parametrize("tag", ["flickr", "reddit"])
+def test_pretrained_clustering_induct_vs_reference(tag):
+    """utils_graphsaint.DataGraphSAINT + the inductive ClustGDD.pretrained_clustering (G7)."""
+    z = load(f"golden_clustgdd_induct_{tag}.npz")
+    _, mean, scale = O.standard_scaler(z["feat_raw"][z["idx_train"]])
+    feat_full = O.scaler_transform(z["feat_raw"], mean, scale)
+    assert np.array_equal(bits(feat_full), bits(z["feat_full"]))
+    subs = {}
+    for name in ("train", "val", "test"):
+        rp, c, v = O.induced_subgraph(z["rowptr"], z["col"], None, z["idx_" + name])
+        assert np.array_equal(rp, z[f"sub_{name}_rowptr"]) and np.array_equal(c, z[f"sub_{name}_col"])
+        subs[name] = (rp, c)
+    ro, co, vo = O.normalize_csr(*subs["train"], None, -1)
+    r, c, v = csr_to_sorted_coo(ro, co, vo)
+    assert np.array_equal(r, z["norm_train_row"]) and np.array_equal(c, z["norm_train_col"])
+    assert np.array_equal(bits(v), bits(z["norm_train_val"]))
+    T, alpha = int(z["T"]), float(z["alpha"])
+    target, _ = O.propagate(ro, co, vo, feat_full[z["idx_train"]], T, alpha)
+    np.testing.assert_allclose(target, z["target_train"], rtol=PROP_RTOL, atol=PROP_ATOL)
+    rv, cv, vv = O.normalize_csr(*subs["val"], None, -1)
+    tv, _ = O.propagate(rv, cv, vv, feat_full[z["idx_val"]], T, alpha)
+    np.testing.assert_allclose(tv, z["target_val"], rtol=PROP_RTOL, atol=PROP_ATOL)
+    k = int(z["n_syn"])
+    if tag == "reddit":
+        res = O.minibatch_kmeans(z["kmeans_X"], k, random_state=15, batch_size=100)
+    else:
+        res = O.kmeans(z["kmeans_X"], k, random_state=rng_from_fixture(z))
+    assert np.array_equal(res["labels_"], z["cluster_labels"])
+    feat_syn, _ = O.cluster_mean(z["target_train"], res["labels_"], k)
+    np.testing.assert_allclose(feat_syn, z["feat_syn"], rtol=MEAN_RTOL, atol=MEAN_ATOL, equal_nan=True)
+    assert np.array_equal(np.argmax(res["cluster_centers_"], axis=-1), z["labels_syn"])
+
+
+def test_induced_subgraph_rejects_unsorted():
+    with pytest.raises(ValueError):
+        O.induced_subgraph(np.array([0, 1, 2, 3]), np.array([1, 0, 2]), None, [2, 1])

@@ -17,6 +17,11 @@ setting in which its Lloyd M-step merge order is deterministic.
   G6 golden_condense.npz   ClustGDD.graph_sparse(sp_type='attaw'/'vanilla'/'single') and
                            ClustGDD.graph_compress (clustgdd_agent_transduct.py:131-250), with the
                            effective-resistance intermediates of utils_clustgdd.attaw_ER_estimator
+  G7 golden_clustgdd_induct_*.npz  the inductive pipeline: utils_graphsaint.DataGraphSAINT on files
+                           written to a temp dir (StandardScaler on the train rows, the three
+                           adj_full[np.ix_(idx, idx)] sub-graphs), then clustgdd_agent_induct
+                           .ClustGDD.pretrained_clustering ('flickr': KMeans, 'reddit':
+                           MiniBatchKMeans), with the k-means input and RNG state captured
 Usage: python tools/make_golden.py [G1 G2 ...]   (default: all)
 """
 import hashlib
@@ -277,6 +282,99 @@ def g6_condense(du, agent):
     np.savez_compressed(os.path.join(OUT, "golden_condense.npz"), **out)
 
 
+def g7_induct(dataset):
+    """utils_graphsaint.DataGraphSAINT + clustgdd_agent_induct.ClustGDD.pretrained_clustering on a
+    small synthetic GraphSAINT-format dataset (device='cpu')."""
+    import random
+    import tempfile
+    import torch
+    sys.path.insert(0, REF)
+    import clustgdd_agent_induct as induct
+    import utils_graphsaint as saint
+    n, d, C = 900, 40, 5
+    rng = np.random.default_rng(77 if dataset == "reddit" else 71)
+    labels = rng.integers(0, C, n)
+    mu = rng.standard_normal((C, d)) * 1.5
+    feat = (mu[labels] + rng.standard_normal((n, d)) * 1.2 + 3.0).astype(np.float32)
+    src = rng.integers(0, n, 5000)
+    same = rng.random(5000) < 0.8
+    dst = np.where(same, [rng.choice(np.where(labels == labels[s])[0]) for s in src],
+                   rng.integers(0, n, 5000))
+    keep = src != dst
+    A = sp.coo_matrix((np.ones(keep.sum(), np.float32), (src[keep], dst[keep])), shape=(n, n))
+    A = sp.csr_matrix(A + A.T)
+    A.data[:] = 1.0
+    A.sort_indices()
+    role_of = rng.choice(3, n, p=[0.5, 0.2, 0.3])  # interleaved ascending role lists
+    role = {"tr": np.where(role_of == 0)[0].tolist(), "va": np.where(role_of == 1)[0].tolist(),
+            "te": np.where(role_of == 2)[0].tolist()}
+    with tempfile.TemporaryDirectory() as tmp:
+        base = os.path.join(tmp, "data", dataset)
+        os.makedirs(base)
+        sp.save_npz(os.path.join(base, "adj_full.npz"), A)
+        np.save(os.path.join(base, "feats.npy"), feat)
+        with open(os.path.join(base, "role.json"), "w") as f:
+            json.dump(role, f)
+        with open(os.path.join(base, "class_map.json"), "w") as f:
+            json.dump({str(i): int(labels[i]) for i in range(n)}, f)
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            data = saint.DataGraphSAINT(dataset)
+        finally:
+            os.chdir(cwd)
+    args = _Args()
+    args.reduction_rate, args.prop_num, args.alpha = 0.2, 4, 0.8
+    args.hidden, args.predropout, args.prewd, args.prenlayers = 64, 0.5, 5e-4, 2
+    args.prelr, args.preep, args.dataset, args.seed, args.cluster_minibatch = 0.01, 30, dataset, 15, 100
+
+    captured = {}
+    real_km, real_mb = induct.KMeans, induct.MiniBatchKMeans
+
+    def capture(cls):
+        class Wrapped(cls):
+            def fit(self, X, *a, **kw):
+                captured["X"] = np.array(X, copy=True)
+                captured["rng_state"] = np.random.get_state()
+                captured["params"] = {k: v for k, v in self.get_params().items()
+                                      if k in ("n_clusters", "random_state", "batch_size", "n_init")}
+                return super().fit(X, *a, **kw)
+        return Wrapped
+
+    induct.KMeans, induct.MiniBatchKMeans = capture(real_km), capture(real_mb)
+    try:
+        random.seed(15)
+        np.random.seed(15)
+        torch.manual_seed(15)
+        a = induct.ClustGDD(data, args, device="cpu")
+        res = a.pretrained_clustering(data)
+    finally:
+        induct.KMeans, induct.MiniBatchKMeans = real_km, real_mb
+    feat_syn, labels_syn, cluster_labels, target_train, adj_train_norm = res[:5]
+    target_val = res[6]
+    st = captured["rng_state"]
+    out = {"T": np.int64(args.prop_num), "alpha": np.float64(args.alpha),
+           "feat_raw": feat, "labels": labels.astype(np.int64),
+           "idx_train": data.idx_train.astype(np.int64), "idx_val": data.idx_val.astype(np.int64),
+           "idx_test": data.idx_test.astype(np.int64),
+           "feat_full": np.asarray(data.feat_full), "target_train": target_train.numpy(),
+           "target_val": target_val.numpy(), "kmeans_X": captured["X"],
+           "rng_key": st[1], "rng_pos": np.int64(st[2]), "rng_has_gauss": np.int64(st[3]),
+           "rng_cached_gauss": np.float64(st[4]),
+           "n_syn": np.int64(a.nnodes_syn), "feat_syn": feat_syn.numpy(),
+           "labels_syn": labels_syn.numpy(), "cluster_labels": cluster_labels.numpy(),
+           "kmeans_params": json.dumps({k: (v if not isinstance(v, np.integer) else int(v))
+                                        for k, v in captured["params"].items()})}
+    rp, ci, vi = csr_arrays(A)
+    out.update(rowptr=rp, col=ci, val=vi)
+    for name in ("train", "val", "test"):
+        sub = getattr(data, "adj_" + name).tocsr()
+        out[f"sub_{name}_rowptr"], out[f"sub_{name}_col"], out[f"sub_{name}_val"] = csr_arrays(sub)
+    r, c, v = coo_sorted(adj_train_norm)
+    out.update(norm_train_row=r, norm_train_col=c, norm_train_val=v)
+    np.savez_compressed(os.path.join(OUT, f"golden_clustgdd_induct_{dataset}.npz"), **out)
+
+
 def main():
     from threadpoolctl import threadpool_limits
     import sklearn
@@ -284,7 +382,7 @@ def main():
     import torch
     os.makedirs(OUT, exist_ok=True)
     du, agent, recsys = import_reference()
-    which = set(sys.argv[1:]) or {"G1", "G2", "G3", "G3b", "G5", "G6"}
+    which = set(sys.argv[1:]) or {"G1", "G2", "G3", "G3b", "G5", "G6", "G7"}
     with threadpool_limits(limits=1):
         if "G1" in which:
             g1_normalize(du)
@@ -299,6 +397,9 @@ def main():
             g5_clustgdd(agent, "ogbn-arxiv")
         if "G6" in which:
             g6_condense(du, agent)
+        if "G7" in which:
+            g7_induct("flickr")
+            g7_induct("reddit")
     with open(os.path.join(OUT, "VERSIONS.json"), "w") as f:
         json.dump({"scikit-learn": sklearn.__version__, "numpy": np.__version__,
                    "scipy": scipy.__version__, "torch": torch.__version__,
