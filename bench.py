@@ -147,6 +147,7 @@ def main():
     bytes_hop = 4 * (n + 1) + 8 * nnz + 16 * n * d  # rowptr, col, val, p_in, p_out, target r/w
     achieved = bytes_hop / (hop_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic()
+    copy_gbs = copy_peak(dev)
 
     out = {
         "metric": "distill wallclock (SpMM+k-means) & test-acc parity, ogbn-arxiv r=0.5% @1-8 GPU",
@@ -172,7 +173,8 @@ def main():
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": bytes_hop, "avg_launch_ms": hop_ms,
-                     "traffic_source": traffic_src, "propagate_call_ms": prop_ms},
+                     "traffic_source": traffic_src, "propagate_call_ms": prop_ms,
+                     "copy_peak_measured": copy_gbs, "frac_of_copy_peak": achieved / copy_gbs},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -182,6 +184,29 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def copy_peak(dev, nbytes=1 << 30, reps=10):
+    """Achievable HBM bandwidth on this box: libgdd's streaming copy of 1 GiB (read + write bytes
+    per copy), timed with HIP events on the stream it runs on."""
+    from gdd import _lib
+    lib = _lib.device_lib()
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).uniform_()
+    dst = torch.empty_like(src)
+    st = _lib.stream_ptr(dev)
+    for _ in range(3):
+        _lib.check(lib.gdd_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, st))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(reps):
+        _lib.check(lib.gdd_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, st))
+    ev[1].record()
+    torch.cuda.synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    if not torch.equal(src[:1024], dst[:1024]) or not torch.equal(src[-1024:], dst[-1024:]):
+        raise RuntimeError("stream copy mismatch")
+    del src, dst
+    return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
 def pmc_traffic():

@@ -40,24 +40,59 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
   return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
 }
 
-// regenerate the 624-word key block in LDS (mt19937_gen)
+// regenerate the 624-word key block in LDS (mt19937_gen). Word kk >= 227 depends on the NEW word
+// kk - 227, so thread t < 227 carries the chain t -> 227 + t -> 454 + t in registers: every read
+// is of an old word, all reads precede all writes, and word 623 (which needs new words 0 and 396)
+// follows. Three barriers.
 __device__ inline void mt_twist_block(uint32_t* key) {
   const int t = threadIdx.x;
-  uint32_t v = 0;
-  if (t < 227) v = mt_mix(key[t], key[t + 1], key[t + 397]);
+  uint32_t n0 = 0, n1 = 0, n2 = 0, o623 = 0;
+  if (t < 227) {
+    n0 = mt_mix(key[t], key[t + 1], key[t + 397]);
+    n1 = mt_mix(key[227 + t], key[228 + t], n0);
+    if (t < 169) n2 = mt_mix(key[454 + t], key[455 + t], n1);
+    if (t == 0) o623 = key[623];
+  }
   __syncthreads();
-  if (t < 227) key[t] = v;
+  if (t < 227) {
+    key[t] = n0;
+    key[227 + t] = n1;
+    if (t < 169) key[454 + t] = n2;
+  }
   __syncthreads();
-  if (t < 227) v = mt_mix(key[227 + t], key[228 + t], key[t]);
+  if (t == 0) key[623] = mt_mix(o623, key[0], key[396]);
   __syncthreads();
-  if (t < 227) key[227 + t] = v;
-  __syncthreads();
-  if (t < 169) v = mt_mix(key[454 + t], key[455 + t], key[227 + t]);
-  __syncthreads();
-  if (t < 169) key[454 + t] = v;
-  __syncthreads();
-  if (t == 0) key[623] = mt_mix(key[623], key[0], key[396]);
-  __syncthreads();
+}
+
+// the same with ONE wave (no block barriers): lane l carries the chains of t = l, l+64, l+128,
+// l+192 (< 227); all old words are read before any write (a wave's LDS operations execute in
+// order; the empty asm keeps the compiler from moving reads past writes it cannot relate).
+__device__ inline void mt_twist_wave(uint32_t* key) {
+  const int lane = threadIdx.x & 63;
+  uint32_t n0[4], n1[4], n2[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int t = lane + 64 * g;
+    const int tc = t < 227 ? t : 0;
+    n0[g] = mt_mix(key[tc], key[tc + 1], key[tc + 397]);
+    n1[g] = mt_mix(key[227 + tc], key[228 + tc], n0[g]);
+    const int t3 = tc < 169 ? tc : 0;
+    n2[g] = mt_mix(key[454 + t3], key[455 + t3], n1[g]);
+  }
+  const uint32_t o623 = key[623];
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int t = lane + 64 * g;
+    if (t < 227) {
+      key[t] = n0[g];
+      key[227 + t] = n1[g];
+      if (t < 169) key[454 + t] = n2[g];
+    }
+  }
+  asm volatile("" ::: "memory");
+  if (lane == 0) key[623] = mt_mix(o623, key[0], key[396]);
+  asm volatile("" ::: "memory");
 }
 
 // exclusive prefix count of `flag` over the block; returns the prefix, *total = block count.
@@ -245,6 +280,109 @@ __device__ inline void mt_permutation_prefix_block(MTScratch* s, int64_t n, int 
     perm[p] = q;
   }
   __syncthreads();
+}
+
+// out[0..count) = randint(low, high, count) by ONE wave (no block barriers; the other waves are
+// free meanwhile). Same words, same acceptance as mt_randint_block. Writes s->pos from lane 0.
+__device__ inline void mt_randint_wave(MTScratch* s, int64_t low, int64_t high, int64_t count,
+                                       int64_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t rng = (uint32_t)(high - 1 - low);
+  if (rng == 0) {
+    for (int64_t i = lane; i < count; i += 64) out[i] = low;
+    return;
+  }
+  const uint32_t mask = mask32(rng);
+  int pos = __builtin_amdgcn_readfirstlane(s->pos);
+  int64_t produced = 0;
+  while (produced < count) {
+    if (pos >= 624) {
+      mt_twist_wave(s->key);
+      pos = 0;
+    }
+    const int wn = min(64, 624 - pos);
+    uint32_t v = 0;
+    bool ok = false;
+    if (lane < wn) {
+      v = mt_temper(s->key[pos + lane]) & mask;
+      ok = v <= rng;
+    }
+    const unsigned long long b = __ballot(ok);
+    const int before = __popcll(b & ((1ull << lane) - 1ull));
+    const int64_t need = count - produced;
+    if (ok && before < need) out[produced + before] = low + (int64_t)v;
+    const int tot = __popcll(b);
+    if (tot >= need) {
+      pos += __ffsll((long long)__ballot(ok && before == need - 1));  // through the last word used
+      produced = count;
+    } else {
+      pos += wn;
+      produced += tot;
+    }
+    asm volatile("" ::: "memory");
+  }
+  if (lane == 0) s->pos = pos;
+}
+
+// J[i] = random_interval(i) for i = n-1 .. 1: the draws of the legacy shuffle behind
+// RandomState.permutation(n), by ONE wave (twists included), 64 words per window. Word u of a
+// window is accepted iff (w_u & mask32(i_u)) <= i_u with i_u = i - (#accepted before u), a
+// sequential recurrence. Solved as a fixed point: guess the acceptances, recount the prefix, repeat
+// until nothing changes. Each pass settles at least one more leading word, so the loop ends within
+// 64 passes and its fixed point is the sequential answer; a window usually settles in a few passes
+// (only words within a few of the threshold ever flip). Words after i reaches 0 are not consumed.
+// Writes s->pos from lane 0.
+__device__ inline void mt_shuffle_draws_wave(MTScratch* s, int n, int* J) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int i = n - 1;
+  int pos = __builtin_amdgcn_readfirstlane(s->pos);
+  while (i >= 1) {
+    if (pos >= 624) {
+      mt_twist_wave(s->key);
+      pos = 0;
+    }
+    const int wn = min(64, 624 - pos);
+    const uint32_t word = lane < wn ? mt_temper(s->key[pos + lane]) : 0u;
+    unsigned long long acc = 0;
+    int iu = i;
+    bool live = lane < wn;
+    while (true) {
+      live = lane < wn && iu >= 1;
+      const uint32_t mu = 0xffffffffu >> __builtin_clz((uint32_t)(iu > 1 ? iu : 1));
+      const unsigned long long nacc = __ballot(live && (word & mu) <= (uint32_t)iu);
+      if (nacc == acc) break;
+      acc = nacc;
+      iu = i - __popcll(acc & below);
+    }
+    if ((acc >> lane) & 1ull) J[iu] = (int)(word & (0xffffffffu >> __builtin_clz((uint32_t)iu)));
+    const unsigned long long lv = __ballot(live);  // a prefix of the window
+    i -= __popcll(acc);
+    pos += __popcll(lv);
+    asm volatile("" ::: "memory");
+  }
+  if (lane == 0) s->pos = pos;
+}
+
+// RandomState.permutation(n)[p] from the shuffle's draws J (J[0] must be 0), for one p by one
+// wave: tracing position p back through the swaps (applied for i = n-1 .. 1), the swaps below p
+// never touch it, swap p sends it to J[p], and after that it moves (to i) only at a swap i whose
+// partner J[i] is its current position. The wave scans J 64 entries at a time.
+__device__ inline int shuffle_trace_wave(const int* J, int n, int p) {
+  const int lane = threadIdx.x & 63;
+  int q = J[p];
+  int i0 = p + 1;
+  while (i0 < n) {
+    const int i = i0 + lane;
+    const unsigned long long b = __ballot(i < n && J[i < n ? i : 0] == q);
+    if (b) {
+      q = i0 + __ffsll((long long)b) - 1;
+      i0 = q + 1;
+    } else {
+      i0 += 64;
+    }
+  }
+  return q;
 }
 
 // "draw the next batch in this launch": an extra workgroup of the assignment kernel runs

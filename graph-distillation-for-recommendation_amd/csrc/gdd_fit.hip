@@ -159,7 +159,7 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n
       const int flags = GDD_STEP_CONVERGE | (st > 0 ? GDD_STEP_NORMS_VALID : 0);
       rc = minibatch_step_dev(bs, dim, X, rows_cur, k, c_old, c_new, w.counts, w.labels_b, (int)st, n,
                               max_no_improvement, flags, w.state, w.step_ws, w.step_bytes,
-                              (!do_rr && has_next) ? next : none, s);
+                              has_next ? next : none, s);  // at reassignment steps: speculative
       if (rc) return rc;
       if (do_rr) {
         rc = mb_reassign_launch((int)st, bs, dim, k, reassignment_ratio, X, rows_cur, c_new, w.counts,

@@ -1506,6 +1506,8 @@ __global__ __launch_bounds__(1024) void k_mb_rng(const DevMT* __restrict__ in, D
 //   counts[to] = min(counts[~to]).
 // `mid` receives the MT state after the permutation draws (the state sklearn leaves if this is
 // the last step); with rn.rows the workgroup then draws the next step's batch.
+// Wave 0 does the serial parts without block barriers (the count statistics, then the shuffle's
+// draws); all waves then trace permutation(b)[r] for r < m (one wave per r) and copy the rows.
 // Requires m <= b/2 (true whenever k <= b/2; the host keeps other shapes on its own loop).
 __global__ __launch_bounds__(1024) void k_mb_reassign(
     int step, int64_t bs, int dim, int k, float ratio, const float* __restrict__ X,
@@ -1513,96 +1515,111 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
     float* __restrict__ cn2, const DevMT* __restrict__ mt_in, DevMT* __restrict__ mt_mid,
     RngNext rn, const int32_t* __restrict__ stop) {
   if (stopped(stop, step)) return;
+#ifdef GDD_STAMPS
+  unsigned long long tl[7] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0};
+#define RS_STAMP(q) tl[(q) - 40] = __builtin_amdgcn_s_memrealtime()
+#else
+#define RS_STAMP(q) do {} while (0)
+#endif
   GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 40);
-  extern __shared__ int J[];  // bs swap partners, then the permutation prefix (int64)
+  extern __shared__ int J[];  // bs shuffle draws, then the reassigned clusters in order (k ints)
   __shared__ MTScratch ms;
-  __shared__ float s_f[32];
-  __shared__ int s_i[2];
-  __shared__ int s_cw[16];
+  __shared__ float s_thr, s_min;
+  __shared__ int s_m;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = blockDim.x >> 6;
-  // max(counts)
-  float mx = -__builtin_inff();
-  for (int c = t; c < k; c += blockDim.x) mx = fmaxf(mx, counts[c]);
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  if (lane == 0) s_f[wave] = mx;
-  __syncthreads();
-  if (t == 0) {
-    float m = s_f[0];
-    for (int w = 1; w < nw; ++w) m = fmaxf(m, s_f[w]);
-    s_f[31] = m;
-  }
-  __syncthreads();
-  const float thr = ratio * s_f[31];  // NEP 50: fp32(ratio) * fp32 max, rounded to fp32
-  // |to| and min(counts[~to])
-  int cnt = 0;
-  float mn = __builtin_inff();
-  for (int c = t; c < k; c += blockDim.x) {
-    const float v = counts[c];
-    if (v < thr)
-      ++cnt;
-    else
-      mn = fminf(mn, v);
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    cnt += __shfl_xor(cnt, o);
-    mn = fminf(mn, __shfl_xor(mn, o));
-  }
-  __syncthreads();
-  if (lane == 0) {
-    s_f[wave] = mn;
-    s_cw[wave] = cnt;
-  }
-  __syncthreads();
-  if (t == 0) {
-    int c2 = 0;
-    float m2 = __builtin_inff();
-    for (int w = 0; w < nw; ++w) {
-      c2 += s_cw[w];
-      m2 = fminf(m2, s_f[w]);
-    }
-    s_i[0] = c2;
-    s_f[30] = m2;
-  }
-  __syncthreads();
-  const int m = s_i[0];
-  const float cmin = s_f[30];
-  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 41);
-  mt_load(mt_in, &ms);
-  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 42);
-  if (m > 0) {
-    int64_t* perm = reinterpret_cast<int64_t*>(J + ((bs + 1) & ~1ll));
-    mt_permutation_prefix_block(&ms, bs, m, J, perm);
-    GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 43);
-    // rank of each reassigned cluster in cluster order -> its new row
+  int* s_list = J + ((bs + 1) & ~1ll);
+  // the key block's loads go out with wave 0's loads of the counts
+  const uint32_t kreg = t < 624 ? mt_in->key[t] : 0u;
+  const int preg = mt_in->pos;
+  if (wave == 0) {
+    // up to 1024 counts in registers, every load in flight at once (a loop of dependent loads
+    // would pay one memory round trip per 64 clusters)
+    constexpr int kReg = 16;
+    float cv[kReg];
+#pragma unroll
+    for (int q = 0; q < kReg; ++q) cv[q] = counts[min(lane + 64 * q, k - 1)];
+    float mx = -__builtin_inff();
+#pragma unroll
+    for (int q = 0; q < kReg; ++q)
+      if (lane + 64 * q < k) mx = fmaxf(mx, cv[q]);
+    for (int c = 64 * kReg + lane; c < k; c += 64) mx = fmaxf(mx, counts[c]);
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    const float thr = ratio * mx;  // NEP 50: fp32(ratio) * fp32 max, rounded to fp32
+    float mn = __builtin_inff();
     int base = 0;
-    for (int c0 = 0; c0 < k; c0 += blockDim.x) {
-      const int c = c0 + t;
-      const bool to = c < k && counts[c] < thr;
-      int total;
-      const int r = block_prefix_count(to, ms.cnt, &total);
-      if (to) {
-        const int64_t src = rows[perm[base + r]];
-        const float* xr = X + src * dim;
-        float* cr = C_new + (int64_t)c * dim;
-        for (int f = 0; f < dim; ++f) cr[f] = xr[f];
-        cn2[c] = npy_sumsq(xr, dim);
-      }
-      base += total;
+    for (int c0 = 0; c0 < k; c0 += 64) {
+      const int c = c0 + lane;
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < kReg; ++q)
+        if (c0 == 64 * q) v = cv[q];
+      if (c0 >= 64 * kReg) v = c < k ? counts[c] : 0.f;
+      const bool to = c < k && v < thr;
+      if (c < k && !to) mn = fminf(mn, v);
+      const unsigned long long b = __ballot(to);
+      if (to) s_list[base + __popcll(b & ((1ull << lane) - 1ull))] = c;
+      base += __popcll(b);
+    }
+    for (int o = 32; o > 0; o >>= 1) mn = fminf(mn, __shfl_xor(mn, o));
+    if (lane == 0) {
+      s_thr = thr;
+      s_min = mn;
+      s_m = base;
+    }
+  }
+  if (t < 624) ms.key[t] = kreg;
+  if (t == 0) ms.pos = preg;
+  __syncthreads();
+  const int m = s_m;
+  const float thr = s_thr, cmin = s_min;
+  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 41);
+  RS_STAMP(41);
+  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 42);
+  RS_STAMP(42);
+  if (m > 0) {
+    if (wave == 0) {
+      if (lane == 0) J[0] = 0;  // swap 0 <-> 0: lets position 0 trace like the others
+      mt_shuffle_draws_wave(&ms, (int)bs, J);
     }
     __syncthreads();
+    GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 43);
+    RS_STAMP(43);
+    mt_store(&ms, mt_mid);
+    for (int r = wave; r < m; r += nw) {
+      const int c = s_list[r];
+      const int64_t src = rows[shuffle_trace_wave(J, (int)bs, r)];
+      const float* xr = X + src * dim;
+      float* cr = C_new + (int64_t)c * dim;
+      for (int f = lane; f < dim; f += 64) cr[f] = xr[f];
+      if (lane == 0) cn2[c] = npy_sumsq(xr, dim);
+    }
     for (int c = t; c < k; c += blockDim.x)
       if (counts[c] < thr) counts[c] = cmin;
-  }
-  __syncthreads();
-  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 44);
-  mt_store(&ms, mt_mid);
-  if (rn.rows) {
-    __syncthreads();
-    mt_randint_block(&ms, 0, rn.n, rn.bs, rn.rows);
-    GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 45);
-    mt_store(&ms, rn.out);
+    GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 44);
+    RS_STAMP(44);
+    if (rn.rows) {  // the next batch after the permutation (replaces the speculative one)
+      __syncthreads();  // every read of the key block done before the draws twist it
+      mt_randint_block(&ms, 0, rn.n, rn.bs, rn.rows);
+      GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 45);
+      RS_STAMP(45);
+      mt_store(&ms, rn.out);
+    }
+  } else {
+    // nothing drawn: the state stays, and the step's own launch already drew the next batch
+    // from it (the host passes that speculative draw at every reassignment step)
+    GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 44);
+    RS_STAMP(44);
+    if (mt_mid != mt_in) mt_store(&ms, mt_mid);
   }
   GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 46);
+  RS_STAMP(46);
+#ifdef GDD_STAMPS
+  if (threadIdx.x == 0 && m > 0) {
+    for (int q = 0; q < 7; ++q) g_stamps_kmeans[50 + q] = tl[q];
+    g_stamps_kmeans[57] = (unsigned long long)m;
+  }
+#endif
+#undef RS_STAMP
 }
 
 }  // namespace
@@ -1620,7 +1637,7 @@ int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const 
                        void* state, hipStream_t s) {
   GDD_REQUIRE(2 * (int64_t)k <= bs, "mb_reassign: needs k <= batch/2");
   StepWs w = carve_step(step_ws, step_ws_bytes, bs, k);
-  const size_t lds = sizeof(int) * (size_t)((bs + 1) & ~1ll) + sizeof(int64_t) * (size_t)k;
+  const size_t lds = sizeof(int) * (size_t)((bs + 1) & ~1ll) + sizeof(int) * (size_t)k;
   GDD_REQUIRE(lds <= 150 * 1024, "mb_reassign: batch too large for the LDS swap table");
   if (lds > 65536)
     GDD_HIP(hipFuncSetAttribute((const void*)k_mb_reassign, hipFuncAttributeMaxDynamicSharedMemorySize,

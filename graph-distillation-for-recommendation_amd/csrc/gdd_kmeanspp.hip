@@ -1204,16 +1204,21 @@ __global__ __launch_bounds__(256) void k_kpp1_fused(Kpp1Args a, int c) {
     for (int v = 0; v < kX; ++v) x[v] = a.XT[(int64_t)min(v, dim - 1) * n + ic];
   }
   const double xs = a.xsq[ic];
-  float pv[kMaxTrials];
+  float pv[kMaxTrials], dv[kMaxTrials];
   int64_t cw[kMaxTrials];
+  // every trial's distance for this point too (the winner is not known yet): the winner's row
+  // then costs no dependent round trip of its own
+  const float* dprev = c == 1 ? a.closest0 : a.dist[pq];
 #pragma unroll
   for (int q = 0; q < kMaxTrials; ++q) {
     pv[q] = a.potv[pq][min(q, Tp - 1)];
     cw[q] = a.candw[pq][(int64_t)min(q, Tp - 1) * T + t];
+    dv[q] = dprev[(int64_t)min(q, Tp - 1) * n + ic];
   }
   int bw = 0;  // np.argmin: first minimum, a NaN wins at once
   float best = pv[0];
   int64_t ct = cw[0];
+  float wi = dv[0];
 #pragma unroll
   for (int q = 1; q < kMaxTrials; ++q) {
     const float pt = pv[q];
@@ -1221,10 +1226,10 @@ __global__ __launch_bounds__(256) void k_kpp1_fused(Kpp1Args a, int c) {
       bw = q;
       best = pt;
       ct = cw[q];
+      wi = dv[q];
     }
   }
-  // round trip 2: the winner's row, this trial's candidate row
-  const float wi = c == 1 ? a.closest0[ic] : a.dist[pq][(int64_t)bw * n + ic];
+  // round trip 2: this trial's candidate row
   const int cs = (SEQ && dim <= kX) ? kX : dim;
   for (int j = tid; j < cs; j += 256) s_c[j] = j < dim ? (double)a.X[ct * dim + min(j, dim - 1)] : 0.0;
   if (tid == 0) s_cn = a.xsq[ct];

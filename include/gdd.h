@@ -40,6 +40,9 @@ const char* gdd_last_error(void);
 int gdd_abi_version(void); /* bumps on any signature change */
 /* 1 if the current HIP device is gfx950 and the embedded code objects can run on it. */
 int gdd_device_ok(void);
+/* Streaming device copy (16-byte aligned, bytes % 16 == 0): the bench's measured HBM copy peak     */
+/* (SURVEY §8(d) roofline: "measure the achievable peak on the box with a copy kernel").           */
+int gdd_stream_copy(const void* src, void* dst, size_t bytes, gdd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* (a2) normalisation:  Â = D^-1/2 (A + I) D^-1/2                                                   */

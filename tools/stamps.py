@@ -49,6 +49,7 @@ def main():
         show("update block0", a, list(range(20, 26)), 20)
         show("update tail", a, list(range(30, 33)), 30)
         show("mb_reassign", a, list(range(40, 47)), 40)
+        show(f"reassign m={a[57]}", a, list(range(50, 57)), 50)
         t0 = p[60]
         lab = {60: "start", 61: "cand row", 62: "last arrived", 63: "row staged", 70: "chain+prefix",
                74: "end", 65: "next start"}
