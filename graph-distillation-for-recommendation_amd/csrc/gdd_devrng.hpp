@@ -145,6 +145,122 @@ __device__ inline void mt_store(const MTScratch* s, DevMT* __restrict__ dst) {
   }
 }
 
+// key block `nw` = the twist of block `old` (both LDS, distinct): thread t < 227 carries the chain
+// t -> 227 + t -> 454 + t in registers; word 623 follows once new words 0 and 396 are in. Two
+// barriers; needs blockDim.x >= 227.
+__device__ inline void mt_twist_into(const uint32_t* __restrict__ old, uint32_t* __restrict__ nw) {
+  const int t = threadIdx.x;
+  if (t < 227) {
+    const uint32_t n0 = mt_mix(old[t], old[t + 1], old[t + 397]);
+    const uint32_t n1 = mt_mix(old[227 + t], old[228 + t], n0);
+    nw[t] = n0;
+    nw[227 + t] = n1;
+    if (t < 169) nw[454 + t] = mt_mix(old[454 + t], old[455 + t], n1);
+  }
+  __syncthreads();
+  if (t == 0) nw[623] = mt_mix(old[623], nw[0], nw[396]);
+  __syncthreads();
+}
+
+// LDS of mt_randint_ring: five key blocks (block b of the stream in slot b % 5) + scratch
+constexpr int kMtRing = 5;
+constexpr size_t kMtRingBytes = sizeof(uint32_t) * (kMtRing * 624 + 64);
+
+// out[0..count) = randint(low, high, count) with every thread busy: each pass takes the next
+// 2048 words (2048 / blockDim.x consecutive words per thread), the key blocks they span twisted
+// ahead into the ring, acceptance flags, one block prefix of the per-thread counts, ordered
+// stores. `ring` slot 0 holds the current key block and `pos` its position (numpy's pos: 624 =
+// exhausted). The final state goes to `state_out`. blockDim.x: a power of two in [256, 1024].
+__device__ inline void mt_randint_ring(uint32_t* ring, int pos, int64_t low, int64_t high,
+                                       int64_t count, int64_t* __restrict__ out,
+                                       DevMT* __restrict__ state_out) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nwv = blockDim.x >> 6;
+  int* scr = reinterpret_cast<int*>(ring + kMtRing * 624);  // 16 wave totals, the last word
+  const uint32_t rng = (uint32_t)(high - 1 - low);
+  int last_block = 0, last_pos = pos;
+  if (rng == 0) {
+    for (int64_t i = t; i < count; i += blockDim.x) out[i] = low;
+  } else {
+    const uint32_t mask = mask32(rng);
+    const int wpt = 2048 / (int)blockDim.x;  // 2, 4 or 8
+    int base = 0, ready = 0;
+    int64_t produced = 0;
+    while (produced < count) {
+      const int hib = base + (pos + 2047) / 624;
+      while (ready < hib) {
+        mt_twist_into(ring + (ready % kMtRing) * 624, ring + ((ready + 1) % kMtRing) * 624);
+        ++ready;
+      }
+      const int r0 = pos + wpt * t;  // this thread's first word, relative to block `base`
+      uint32_t v[8];
+      unsigned okb = 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[u] = 0;
+        if (u < wpt) {
+          const int r = r0 + u, b = base + r / 624;
+          v[u] = mt_temper(ring[(b % kMtRing) * 624 + (r - (r / 624) * 624)]) & mask;
+          okb |= (v[u] <= rng ? 1u : 0u) << u;
+        }
+      }
+      const int cnt = __popc(okb);
+      // exclusive prefix of cnt over the block: wave scan, then the wave totals
+      int inc = cnt;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+      }
+      if (lane == 63) scr[wave] = inc;
+      __syncthreads();
+      int wb = 0, tot = 0;
+      for (int w = 0; w < nwv; ++w) {
+        const int c = scr[w];
+        wb += w < wave ? c : 0;
+        tot += c;
+      }
+      int rank = wb + inc - cnt;
+      const int64_t need = count - produced;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if ((okb >> u) & 1u) {
+          if (rank < need) out[produced + rank] = low + (int64_t)v[u];
+          if (rank == need - 1) scr[32] = r0 + u;
+          ++rank;
+        }
+      }
+      __syncthreads();
+      if (tot >= need) {
+        const int wl = scr[32];  // the last word consumed, relative to block `base`
+        last_block = base + wl / 624;
+        last_pos = wl - (wl / 624) * 624 + 1;
+        produced = count;
+      } else {
+        produced += tot;
+        const int nx = pos + 2048;
+        base += nx / 624;
+        pos = nx - (nx / 624) * 624;
+      }
+    }
+  }
+  const uint32_t* kb = ring + (last_block % kMtRing) * 624;
+  for (int i = t; i < 624; i += blockDim.x) state_out->key[i] = kb[i];
+  if (t == 0) {
+    state_out->pos = last_pos;
+    state_out->pad = 0;
+  }
+}
+
+// the next batch in its own workgroup: load the state into the ring, draw, store the new state
+__device__ inline void mt_randint_from(const DevMT* __restrict__ in, uint32_t* ring, int64_t low,
+                                       int64_t high, int64_t count, int64_t* __restrict__ out,
+                                       DevMT* __restrict__ state_out) {
+  for (int i = threadIdx.x; i < 624; i += blockDim.x) ring[i] = in->key[i];
+  const int pos = in->pos;
+  __syncthreads();
+  mt_randint_ring(ring, pos, low, high, count, out, state_out);
+}
+
 // out[0..count) = randint(low, high, count) (high - low - 1 < 2^32)
 __device__ inline void mt_randint_block(MTScratch* s, int64_t low, int64_t high, int64_t count,
                                  int64_t* __restrict__ out) {

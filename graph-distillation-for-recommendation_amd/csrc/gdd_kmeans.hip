@@ -350,10 +350,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_assign_small(
   if (rn.rows && blockIdx.x == gridDim.x - 1) {
     // extra workgroup: the next step's batch indices (randint(0, n, b)) from the device MT state,
     // concurrently with this step's assignment
-    MTScratch* ms = reinterpret_cast<MTScratch*>(lds);
-    mt_load(rn.in, ms);
-    mt_randint_block(ms, 0, rn.n, rn.bs, rn.rows);
-    mt_store(ms, rn.out);
+    mt_randint_from(rn.in, reinterpret_cast<uint32_t*>(lds), 0, rn.n, rn.bs, rn.rows, rn.out);
     return;
   }
   const int S = dimp + 1;
@@ -668,10 +665,7 @@ __global__ __launch_bounds__(64 * W) void k_mb_assign(
     if (tl.active && e == 0) {
       mb_tail_block(tl, lds);
     } else if (rn.rows) {
-      MTScratch* ms = reinterpret_cast<MTScratch*>(lds);
-      mt_load(rn.in, ms);
-      mt_randint_block(ms, 0, rn.n, rn.bs, rn.rows);
-      mt_store(ms, rn.out);
+      mt_randint_from(rn.in, reinterpret_cast<uint32_t*>(lds), 0, rn.n, rn.bs, rn.rows, rn.out);
     }
     return;
   }
@@ -1054,7 +1048,7 @@ int launch_assign_small_t(int64_t n, int dim, const float* X, const int64_t* row
                           const float* C, const float* cn2, int32_t* labels, float* sq_dist,
                           const int32_t* stop, int step_i, const RngNext& rn, hipStream_t s) {
   const int dimp = (dim + 1) & ~1;
-  const size_t lds = std::max(assign_small_lds(W, dim), sizeof(MTScratch) + 64);
+  const size_t lds = std::max(assign_small_lds(W, dim), kMtRingBytes + 64);
   if (lds > 65536)
     GDD_HIP(hipFuncSetAttribute((const void*)k_assign_small<W, VEC>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1205,7 +1199,7 @@ int launch_mb_assign_t(int64_t b, int dim, const float* X, const int64_t* rows, 
   const int G = (tiles + W - 1) / W;
   const int P = (int)((b + 31) / 32);
   const size_t lds = std::max({mb_assign_lds(W, dim), sizeof(float) * 2048 + 16,
-                               sizeof(MTScratch) + 64});
+                               kMtRingBytes + 64});
   if (lds > 65536)
     GDD_HIP(hipFuncSetAttribute((const void*)k_mb_assign<W, VEC>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1492,10 +1486,8 @@ namespace {
 // randint(0, n, b) for one step from the device MT state (single workgroup)
 __global__ __launch_bounds__(1024) void k_mb_rng(const DevMT* __restrict__ in, DevMT* __restrict__ out,
                                                  int64_t n, int64_t bs, int64_t* __restrict__ rows) {
-  __shared__ MTScratch ms;
-  mt_load(in, &ms);
-  mt_randint_block(&ms, 0, n, bs, rows);
-  mt_store(&ms, out);
+  __shared__ uint32_t ring[kMtRingBytes / sizeof(uint32_t)];
+  mt_randint_from(in, ring, 0, n, bs, rows, out);
 }
 
 // The reassignment branch of _mini_batch_step (sklearn/cluster/_kmeans.py:1640-1667) at a step
@@ -1598,11 +1590,12 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
     GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 44);
     RS_STAMP(44);
     if (rn.rows) {  // the next batch after the permutation (replaces the speculative one)
-      __syncthreads();  // every read of the key block done before the draws twist it
-      mt_randint_block(&ms, 0, rn.n, rn.bs, rn.rows);
+      uint32_t* ring = reinterpret_cast<uint32_t*>(s_list + k);
+      for (int i = t; i < 624; i += blockDim.x) ring[i] = ms.key[i];
+      __syncthreads();
+      mt_randint_ring(ring, ms.pos, 0, rn.n, rn.bs, rn.rows, rn.out);
       GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 45);
       RS_STAMP(45);
-      mt_store(&ms, rn.out);
     }
   } else {
     // nothing drawn: the state stays, and the step's own launch already drew the next batch
@@ -1637,7 +1630,7 @@ int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const 
                        void* state, hipStream_t s) {
   GDD_REQUIRE(2 * (int64_t)k <= bs, "mb_reassign: needs k <= batch/2");
   StepWs w = carve_step(step_ws, step_ws_bytes, bs, k);
-  const size_t lds = sizeof(int) * (size_t)((bs + 1) & ~1ll) + sizeof(int) * (size_t)k;
+  const size_t lds = sizeof(int) * (size_t)((bs + 1) & ~1ll) + sizeof(int) * (size_t)k + kMtRingBytes;
   GDD_REQUIRE(lds <= 150 * 1024, "mb_reassign: batch too large for the LDS swap table");
   if (lds > 65536)
     GDD_HIP(hipFuncSetAttribute((const void*)k_mb_reassign, hipFuncAttributeMaxDynamicSharedMemorySize,

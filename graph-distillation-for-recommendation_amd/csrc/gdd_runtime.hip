@@ -64,25 +64,23 @@ int sort_pairs_i32(const int32_t* keys_in, int32_t* keys_out, const int32_t* val
 }
 
 // streaming copy used to measure the achievable HBM bandwidth on the box (report the
-// measured copy peak beside the 8 TB/s spec). Each workgroup streams one contiguous chunk: 4 x 16 B
-// per thread in flight, nontemporal so the copy does not thrash L2 / MALL.
+// measured copy peak beside the 8 TB/s spec). Grid-stride over 16-byte words, 4 in flight per lane,
+// nontemporal: the fastest of the shapes tools/probe/copy_probe.hip compares (~6.1 TB/s on 1 GiB).
 typedef float v4f __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void k_stream_copy(const v4f* __restrict__ src,
-                                                     v4f* __restrict__ dst, int64_t n16,
-                                                     int64_t per_block) {
-  const int64_t b0 = (int64_t)blockIdx.x * per_block;
-  const int64_t b1 = b0 + per_block < n16 ? b0 + per_block : n16;
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += 4 * 256) {
+                                                     v4f* __restrict__ dst, int64_t n16) {
+  const int64_t step = (int64_t)gridDim.x * 1024;
+  for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += step) {
     v4f v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t j = i + u * 256;
-      if (j < b1) v[u] = __builtin_nontemporal_load(src + j);
+      if (j < n16) v[u] = __builtin_nontemporal_load(src + j);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t j = i + u * 256;
-      if (j < b1) __builtin_nontemporal_store(v[u], dst + j);
+      if (j < n16) __builtin_nontemporal_store(v[u], dst + j);
     }
   }
 }
@@ -96,12 +94,10 @@ int gdd_stream_copy(const void* src, void* dst, size_t bytes, gdd_stream_t strea
   GDD_REQUIRE(((uintptr_t)src | (uintptr_t)dst) % 16 == 0, "stream_copy: 16-byte aligned buffers");
   const int64_t n16 = (int64_t)(bytes / 16);
   if (n16 == 0) return GDD_OK;
-  const int64_t blocks = 4096;  // 16 per CU
-  int64_t per = (n16 + blocks - 1) / blocks;
-  per = (per + 1023) / 1024 * 1024;
-  const unsigned g = (unsigned)((n16 + per - 1) / per);
+  const int64_t want = (n16 + 1023) / 1024;
+  const unsigned g = (unsigned)(want < 8192 ? want : 8192);
   gdd::k_stream_copy<<<g, 256, 0, gdd::to_hip(stream)>>>(static_cast<const gdd::v4f*>(src),
-                                                        static_cast<gdd::v4f*>(dst), n16, per);
+                                                        static_cast<gdd::v4f*>(dst), n16);
   GDD_LAUNCHED();
   return GDD_OK;
 }

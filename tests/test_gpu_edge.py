@@ -90,3 +90,16 @@ def test_cluster_mean_single_cluster_and_mostly_empty():
         assert np.array_equal(np.isnan(o), np.isnan(ref))
         m = ~np.isnan(ref)
         assert np.array_equal(bits(o[m]), bits(ref[m]))
+
+
+@pytest.mark.parametrize("nbytes", [16, 4096 + 48, 1 << 20, (1 << 24) + 16 * 1023])
+def test_stream_copy_exact(nbytes):
+    # the bench's copy-peak kernel: every byte copied, nothing past the end touched
+    from gdd import _lib
+    lib = _lib.device_lib()
+    src = torch.randint(-2**31, 2**31 - 1, (nbytes // 4 + 4,), dtype=torch.int32, device="cuda")
+    dst = torch.zeros_like(src)
+    _lib.check(lib.gdd_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, _lib.stream_ptr("cuda")))
+    torch.cuda.synchronize()
+    m = nbytes // 4
+    assert torch.equal(src[:m], dst[:m]) and int(dst[m:].abs().sum()) == 0
