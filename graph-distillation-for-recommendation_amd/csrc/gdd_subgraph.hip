@@ -134,3 +134,78 @@ extern "C" int gdd_subgraph_fill(int64_t n, const int32_t* rowptr, const int32_t
   if (bad_out) GDD_HIP(hipMemcpyAsync(bad_out, bad, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
   return GDD_OK;
 }
+
+// ---- CSR transpose: Aᵀ as canonical CSR (the backward of the GCN evaluator's SpMM, models/gcn.py
+// :36-51: d(A @ S)/dS = Aᵀ @ grad). Stable radix sort of (column, entry) pairs, so each transposed
+// row lists its entries by ascending original row; counts by integer atomics, one scan.
+namespace gdd {
+namespace {
+
+__global__ void k_entry_rows(int64_t n, const int32_t* __restrict__ rowptr, int32_t* __restrict__ rows,
+                             int32_t* __restrict__ iota) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  for (int32_t p = rowptr[r]; p < rowptr[r + 1]; ++p) {
+    rows[p] = (int32_t)r;
+    iota[p] = p;
+  }
+}
+
+__global__ void k_col_counts(int64_t nnz, const int32_t* __restrict__ col, int32_t* __restrict__ cnt) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < nnz) atomicAdd(cnt + col[p], 1);
+}
+
+__global__ void k_transpose_fill(int64_t nnz, const int32_t* __restrict__ perm,
+                                 const int32_t* __restrict__ rows, const float* __restrict__ val,
+                                 int32_t* __restrict__ col_t, float* __restrict__ val_t) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nnz) return;
+  const int32_t e = perm[p];
+  col_t[p] = rows[e];
+  if (val_t) val_t[p] = val ? val[e] : 1.0f;
+}
+
+int bits_for(int64_t n) {
+  int b = 1;
+  while (b < 31 && (int64_t(1) << b) < n) ++b;
+  return b;
+}
+
+}  // namespace
+}  // namespace gdd
+
+extern "C" size_t gdd_csr_transpose_ws_bytes(int64_t n, int64_t nnz) {
+  return align256(sizeof(int32_t) * (size_t)nnz) * 4 + align256(sizeof(int32_t) * (size_t)(n + 1)) +
+         sort_pairs_ws_bytes(nnz) + scan_i32_ws_bytes(n + 1) + 1024;
+}
+
+extern "C" int gdd_csr_transpose(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
+                                 const float* val, int32_t* rowptr_t, int32_t* col_t, float* val_t,
+                                 void* ws, size_t ws_bytes, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && n < INT_MAX && nnz >= 0 && nnz < INT_MAX, "csr_transpose: bad shape");
+  GDD_REQUIRE(rowptr && rowptr_t && ws && (nnz == 0 || (col && col_t)), "csr_transpose: null pointer");
+  hipStream_t s = to_hip(stream);
+  Carver cv(ws, ws_bytes);
+  int32_t* rows = cv.take<int32_t>(nnz);
+  int32_t* iota = cv.take<int32_t>(nnz);
+  int32_t* keys = cv.take<int32_t>(nnz);
+  int32_t* perm = cv.take<int32_t>(nnz);
+  int32_t* cnt = cv.take<int32_t>(n + 1);
+  const size_t sb = sort_pairs_ws_bytes(nnz), cb = scan_i32_ws_bytes(n + 1);
+  char* sort_ws = cv.take<char>(sb);
+  char* scan_ws = cv.take<char>(cb);
+  if (!cv.ok()) return fail(GDD_E_WORKSPACE, "csr_transpose: workspace too small");
+  GDD_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (size_t)(n + 1), s));
+  if (nnz > 0) {
+    k_entry_rows<<<grid1(n), kThreads, 0, s>>>(n, rowptr, rows, iota);
+    GDD_LAUNCHED();
+    k_col_counts<<<grid1(nnz), kThreads, 0, s>>>(nnz, col, cnt);
+    GDD_LAUNCHED();
+    int rc = sort_pairs_i32(col, keys, iota, perm, nnz, bits_for(n), sort_ws, sb, s);
+    if (rc) return rc;
+    k_transpose_fill<<<grid1(nnz), kThreads, 0, s>>>(nnz, perm, rows, val, col_t, val_t);
+    GDD_LAUNCHED();
+  }
+  return exclusive_scan_i32(cnt, rowptr_t, n + 1, scan_ws, cb, s);
+}

@@ -328,6 +328,17 @@ int gdd_subgraph_fill(int64_t n, const int32_t* rowptr, const int32_t* col, cons
                       const int32_t* idx, const int32_t* rowptr_out, int32_t* col_out, float* val_out,
                       int32_t* bad_out, void* ws, size_t ws_bytes, gdd_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------------- */
+/* CSR transpose Aᵀ (square n x n, canonical output: each row's entries by ascending column). The   */
+/* backward of the GCN evaluator's SpMM (models/gcn.py:36-51, d(A @ S)/dS = Aᵀ @ grad) and of any   */
+/* caller that needs Aᵀ of a non-symmetric graph. val may be NULL (binary: val_t gets 1.0f) and     */
+/* val_t may be NULL (structure only).                                                              */
+/* ---------------------------------------------------------------------------------------------- */
+size_t gdd_csr_transpose_ws_bytes(int64_t n, int64_t nnz);
+int gdd_csr_transpose(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* val,
+                      int32_t* rowptr_t, int32_t* col_t, float* val_t, void* ws, size_t ws_bytes,
+                      gdd_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
