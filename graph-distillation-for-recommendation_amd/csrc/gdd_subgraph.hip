@@ -175,15 +175,18 @@ int bits_for(int64_t n) {
 }  // namespace
 }  // namespace gdd
 
-extern "C" size_t gdd_csr_transpose_ws_bytes(int64_t n, int64_t nnz) {
-  return align256(sizeof(int32_t) * (size_t)nnz) * 4 + align256(sizeof(int32_t) * (size_t)(n + 1)) +
-         sort_pairs_ws_bytes(nnz) + scan_i32_ws_bytes(n + 1) + 1024;
+extern "C" size_t gdd_csr_transpose_ws_bytes(int64_t n, int64_t n_cols, int64_t nnz) {
+  const int64_t m = n > n_cols ? n : n_cols;
+  return align256(sizeof(int32_t) * (size_t)nnz) * 4 + align256(sizeof(int32_t) * (size_t)(m + 1)) +
+         sort_pairs_ws_bytes(nnz) + scan_i32_ws_bytes(m + 1) + 1024;
 }
 
-extern "C" int gdd_csr_transpose(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
-                                 const float* val, int32_t* rowptr_t, int32_t* col_t, float* val_t,
-                                 void* ws, size_t ws_bytes, gdd_stream_t stream) {
-  GDD_REQUIRE(n > 0 && n < INT_MAX && nnz >= 0 && nnz < INT_MAX, "csr_transpose: bad shape");
+extern "C" int gdd_csr_transpose(int64_t n, int64_t n_cols, int64_t nnz, const int32_t* rowptr,
+                                 const int32_t* col, const float* val, int32_t* rowptr_t, int32_t* col_t,
+                                 float* val_t, int32_t* perm_out, void* ws, size_t ws_bytes,
+                                 gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && n < INT_MAX && n_cols > 0 && n_cols < INT_MAX && nnz >= 0 && nnz < INT_MAX,
+              "csr_transpose: bad shape");
   GDD_REQUIRE(rowptr && rowptr_t && ws && (nnz == 0 || (col && col_t)), "csr_transpose: null pointer");
   hipStream_t s = to_hip(stream);
   Carver cv(ws, ws_bytes);
@@ -191,21 +194,23 @@ extern "C" int gdd_csr_transpose(int64_t n, int64_t nnz, const int32_t* rowptr, 
   int32_t* iota = cv.take<int32_t>(nnz);
   int32_t* keys = cv.take<int32_t>(nnz);
   int32_t* perm = cv.take<int32_t>(nnz);
-  int32_t* cnt = cv.take<int32_t>(n + 1);
-  const size_t sb = sort_pairs_ws_bytes(nnz), cb = scan_i32_ws_bytes(n + 1);
+  int32_t* cnt = cv.take<int32_t>(n_cols + 1);
+  const size_t sb = sort_pairs_ws_bytes(nnz), cb = scan_i32_ws_bytes(n_cols + 1);
   char* sort_ws = cv.take<char>(sb);
   char* scan_ws = cv.take<char>(cb);
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "csr_transpose: workspace too small");
-  GDD_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (size_t)(n + 1), s));
+  GDD_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (size_t)(n_cols + 1), s));
   if (nnz > 0) {
     k_entry_rows<<<grid1(n), kThreads, 0, s>>>(n, rowptr, rows, iota);
     GDD_LAUNCHED();
     k_col_counts<<<grid1(nnz), kThreads, 0, s>>>(nnz, col, cnt);
     GDD_LAUNCHED();
-    int rc = sort_pairs_i32(col, keys, iota, perm, nnz, bits_for(n), sort_ws, sb, s);
+    int rc = sort_pairs_i32(col, keys, iota, perm, nnz, bits_for(n_cols), sort_ws, sb, s);
     if (rc) return rc;
     k_transpose_fill<<<grid1(nnz), kThreads, 0, s>>>(nnz, perm, rows, val, col_t, val_t);
     GDD_LAUNCHED();
+    if (perm_out)
+      GDD_HIP(hipMemcpyAsync(perm_out, perm, sizeof(int32_t) * (size_t)nnz, hipMemcpyDeviceToDevice, s));
   }
-  return exclusive_scan_i32(cnt, rowptr_t, n + 1, scan_ws, cb, s);
+  return exclusive_scan_i32(cnt, rowptr_t, n_cols + 1, scan_ws, cb, s);
 }

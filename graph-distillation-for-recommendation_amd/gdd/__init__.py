@@ -14,7 +14,7 @@ the reference file:line each entry point replaces):
   fixed-point all-reduce per iteration (rank-count invariant)
 """
 from . import _lib  # noqa: F401  (imports torch first, see _lib docstring)
-from . import gcn, pipeline  # noqa: F401
+from . import gcn, pipeline, recsys  # noqa: F401
 from .cluster import argmax_rows, cluster_mean, group_by_label
 from .condense import ER_estimator, attaw_ER_estimator, graph_compress, graph_sparse
 from .graph import (CSRGraph, induced_subgraph, normalize_adj, normalize_adj_tensor, propagate, spmm,

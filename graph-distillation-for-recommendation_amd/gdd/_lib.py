@@ -94,8 +94,13 @@ SIGNATURES = {
     "gdd_graph_compress": (_c_int, [_c_i64, _vp, _c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                     _c_size, _vp]),
     "gdd_stream_copy": (_c_int, [_vp, _vp, _c_size, _vp]),
-    "gdd_csr_transpose_ws_bytes": (_c_size, [_c_i64, _c_i64]),
-    "gdd_csr_transpose": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
+    "gdd_csr_transpose_ws_bytes": (_c_size, [_c_i64, _c_i64, _c_i64]),
+    "gdd_csr_transpose": (_c_int, [_c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _c_size, _vp]),
+    "gdd_bipartite_condense_ws_bytes": (_c_size, [_c_i64, _c_int]),
+    "gdd_bipartite_condense": (_c_int, [_c_i64, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _vp,
+                                        _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
+    "gdd_edge_dots": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gdd_subgraph_ws_bytes": (_c_size, [_c_i64, _c_i64]),
     "gdd_subgraph_count": (_c_int, [_c_i64, _vp, _vp, _c_i64, _vp, _vp, _vp, _c_size, _vp]),
     "gdd_subgraph_fill": (_c_int, [_c_i64, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,

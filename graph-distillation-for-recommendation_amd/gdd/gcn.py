@@ -43,10 +43,11 @@ def transpose(adj: CSRGraph) -> CSRGraph:
     rowptr = torch.empty(adj.n + 1, dtype=torch.int32, device=dev)
     col = torch.empty(max(adj.nnz, 1), dtype=torch.int32, device=dev)
     val = None if adj.val is None else torch.empty(max(adj.nnz, 1), dtype=torch.float32, device=dev)
-    ws = _lib.workspace(lib.gdd_csr_transpose_ws_bytes(adj.n, adj.nnz), dev)
-    _lib.check(lib.gdd_csr_transpose(adj.n, adj.nnz, adj.rowptr.data_ptr(), _lib.ptr(adj.col),
+    ws = _lib.workspace(lib.gdd_csr_transpose_ws_bytes(adj.n, adj.n, adj.nnz), dev)
+    _lib.check(lib.gdd_csr_transpose(adj.n, adj.n, adj.nnz, adj.rowptr.data_ptr(), _lib.ptr(adj.col),
                                      _lib.ptr(adj.val), rowptr.data_ptr(), col.data_ptr(),
-                                     _lib.ptr(val), ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev)))
+                                     _lib.ptr(val), None, ws.data_ptr(), ws.numel(),
+                                     _lib.stream_ptr(dev)))
     t = CSRGraph(rowptr, col[:adj.nnz], None if val is None else val[:adj.nnz], adj.n)
     t.__dict__["_transpose"] = adj
     adj.__dict__["_transpose"] = t

@@ -79,6 +79,45 @@ def graphsaint_split(adj_full, feat, idx_train, idx_val, idx_test, device="cuda"
     return ns
 
 
+def load_graphsaint(dataset_dir: str, dataset: str = "", device="cuda"):
+    """utils_graphsaint.DataGraphSAINT(dataset) (utils_graphsaint.py:14-68) from a GraphSAINT-format
+    directory (adj_full.npz, role.json, feats.npy, class_map.json): the files are read on the host
+    with loaders that execute nothing (scipy.sparse.load_npz / numpy.load without pickles / json),
+    then :func:`graphsaint_split` prepares the role sub-graphs and the train-fitted scaling on the
+    device. Labels follow process_labels (:70-87): a list per node gives a multi-label matrix, ints a
+    vector shifted to start at 0. ogbn-arxiv is symmetrised as in :19-21."""
+    import json
+    import os
+    import scipy.sparse as sp
+    adj_full = sp.load_npz(os.path.join(dataset_dir, "adj_full.npz")).tocsr()
+    if dataset == "ogbn-arxiv":
+        adj_full = adj_full + adj_full.T
+        adj_full[adj_full > 1] = 1
+    with open(os.path.join(dataset_dir, "role.json")) as f:
+        role = json.load(f)
+    feat = np.load(os.path.join(dataset_dir, "feats.npy"), allow_pickle=False)
+    with open(os.path.join(dataset_dir, "class_map.json")) as f:
+        class_map = json.load(f)
+    n = adj_full.shape[0]
+    first = next(iter(class_map.values()))
+    if isinstance(first, list):
+        labels = np.zeros((n, len(first)))
+        for k_, v in class_map.items():
+            labels[int(k_)] = v
+        nclass = len(first)
+    else:
+        labels = np.zeros(n, dtype=np.int32)
+        for k_, v in class_map.items():
+            labels[int(k_)] = v
+        labels = labels - labels.min()
+        nclass = int(labels.max()) + 1
+    ns = graphsaint_split(adj_full, feat, role["tr"], role["va"], role["te"], device=device)
+    ns.nnodes, ns.nclass, ns.labels_full = n, nclass, labels
+    for name, key in (("train", "tr"), ("val", "va"), ("test", "te")):
+        setattr(ns, "labels_" + name, labels[np.asarray(role[key], dtype=np.int64)])
+    return ns
+
+
 def kmeans_cluster(X, n_clusters: int, seed: int, minibatch: bool = True, batch_size: int = 2048,
                    device="cuda"):
     """distill_recsys.kmeans_cluster on the device -> (labels int64 numpy, centres fp32 numpy)."""

@@ -329,15 +329,35 @@ int gdd_subgraph_fill(int64_t n, const int32_t* rowptr, const int32_t* col, cons
                       int32_t* bad_out, void* ws, size_t ws_bytes, gdd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------- */
-/* CSR transpose Aᵀ (square n x n, canonical output: each row's entries by ascending column). The   */
-/* backward of the GCN evaluator's SpMM (models/gcn.py:36-51, d(A @ S)/dS = Aᵀ @ grad) and of any   */
-/* caller that needs Aᵀ of a non-symmetric graph. val may be NULL (binary: val_t gets 1.0f) and     */
-/* val_t may be NULL (structure only).                                                              */
+/* CSR transpose Aᵀ of an n x n_cols matrix (output n_cols x n, canonical: each row's entries by    */
+/* ascending column). The backward of the GCN evaluator's SpMM (models/gcn.py:36-51, d(A @ S)/dS =  */
+/* Aᵀ @ grad) and the item side of the recommender's bipartite propagation (distill_recsys.py        */
+/* :336-346). val may be NULL (binary: val_t gets 1.0f); val_t may be NULL (structure only);         */
+/* perm_out (nullable, nnz) receives the source entry of every transposed entry, so callers whose    */
+/* values change (learned edge weights) re-gather val_t = val[perm] without re-sorting.              */
 /* ---------------------------------------------------------------------------------------------- */
-size_t gdd_csr_transpose_ws_bytes(int64_t n, int64_t nnz);
-int gdd_csr_transpose(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* val,
-                      int32_t* rowptr_t, int32_t* col_t, float* val_t, void* ws, size_t ws_bytes,
-                      gdd_stream_t stream);
+size_t gdd_csr_transpose_ws_bytes(int64_t n, int64_t n_cols, int64_t nnz);
+int gdd_csr_transpose(int64_t n, int64_t n_cols, int64_t nnz, const int32_t* rowptr, const int32_t* col,
+                      const float* val, int32_t* rowptr_t, int32_t* col_t, float* val_t, int32_t* perm_out,
+                      void* ws, size_t ws_bytes, gdd_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------- */
+/* (f4) recommender condensation. build_condensed_bipartite (distill_recsys.py:184-201): the       */
+/* interactions (train_u[e], train_i[e]) become super-node pairs (u2cu[u], i2ci[i]); the output is   */
+/* the num_cu x num_ci matrix of pair counts as canonical CSR (what scipy's coo -> sum_duplicates -> */
+/* tocsr gives): rowptr_out (num_cu+1), col_out / val_out with capacity E, the stored count written */
+/* to nnz_out (device int). bad_out (device, nullable): nonzero if an id was out of range.          */
+/* gdd_edge_dots: out[e] = sum_f a[ra[e],f] * b[rb[e],f] (fp32 fma chain, f ascending) - the edge   */
+/* gradient of the LightGCN message passing (RecsysModel.propagate, :336-346).                       */
+/* ---------------------------------------------------------------------------------------------- */
+size_t gdd_bipartite_condense_ws_bytes(int64_t E, int num_cu);
+int gdd_bipartite_condense(int64_t E, const int32_t* train_u, const int32_t* train_i, int64_t num_users,
+                           int64_t num_items, const int32_t* u2cu, const int32_t* i2ci, int num_cu,
+                           int num_ci, int32_t* rowptr_out, int32_t* col_out, float* val_out,
+                           int32_t* nnz_out, int32_t* bad_out, void* ws, size_t ws_bytes,
+                           gdd_stream_t stream);
+int gdd_edge_dots(int64_t E, int d, const int32_t* ra, const float* a, const int32_t* rb, const float* b,
+                  float* out, gdd_stream_t stream);
 
 #ifdef __cplusplus
 }

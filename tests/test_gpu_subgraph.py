@@ -89,3 +89,27 @@ def test_graphsaint_split_scaler_matches_oracle():
         sub = getattr(ns, "adj_" + name)
         assert np.array_equal(sub.rowptr.cpu().numpy(), ref.indptr)
         assert np.array_equal(sub.col.cpu().numpy(), ref.indices)
+
+
+def test_load_graphsaint_files_vs_reference(tmp_path):
+    # the G7 dataset written back in GraphSAINT's file format, read by load_graphsaint: the same
+    # scaled features and role sub-graphs DataGraphSAINT produced (bit-exact)
+    import json
+    from gdd import pipeline
+    from golden_util import load
+    z = load("golden_clustgdd_induct_flickr.npz")
+    n = len(z["rowptr"]) - 1
+    A = sp.csr_matrix((np.ones(len(z["col"]), np.float32), z["col"], z["rowptr"]), shape=(n, n))
+    sp.save_npz(tmp_path / "adj_full.npz", A)
+    np.save(tmp_path / "feats.npy", z["feat_raw"])
+    json.dump({"tr": z["idx_train"].tolist(), "va": z["idx_val"].tolist(), "te": z["idx_test"].tolist()},
+              open(tmp_path / "role.json", "w"))
+    json.dump({str(i): int(z["labels"][i]) for i in range(n)}, open(tmp_path / "class_map.json", "w"))
+    ns = pipeline.load_graphsaint(str(tmp_path), "flickr")
+    assert np.array_equal(bits(ns.feat_full.cpu().numpy()), bits(z["feat_full"]))
+    assert ns.nclass == int(z["labels"].max()) + 1
+    assert np.array_equal(ns.labels_train, z["labels"][z["idx_train"]])
+    for name in ("train", "val", "test"):
+        g = getattr(ns, "adj_" + name)
+        assert np.array_equal(g.rowptr.cpu().numpy(), z[f"sub_{name}_rowptr"])
+        assert np.array_equal(g.col.cpu().numpy(), z[f"sub_{name}_col"])

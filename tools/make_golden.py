@@ -22,6 +22,9 @@ setting in which its Lloyd M-step merge order is deterministic.
                            adj_full[np.ix_(idx, idx)] sub-graphs), then clustgdd_agent_induct
                            .ClustGDD.pretrained_clustering ('flickr': KMeans, 'reddit':
                            MiniBatchKMeans), with the k-means input and RNG state captured
+  G8 golden_recsys.npz     distill_recsys.build_condensed_bipartite on synthetic interactions (with
+                           empty super-nodes), condensed_csr_to_edge_index, and LightGCNCondensed
+                           (propagate outputs, bpr_loss and every parameter gradient) on CPU
 Usage: python tools/make_golden.py [G1 G2 ...]   (default: all)
 """
 import hashlib
@@ -375,6 +378,47 @@ def g7_induct(dataset):
     np.savez_compressed(os.path.join(OUT, f"golden_clustgdd_induct_{dataset}.npz"), **out)
 
 
+def g8_recsys(recsys):
+    """The recommender's condensation and LightGCN refinement model (device='cpu')."""
+    import torch
+    rng = np.random.default_rng(81)
+    nu, ni, E = 900, 600, 7000
+    train_u = rng.integers(0, nu, E).astype(np.int64)
+    train_i = (rng.zipf(1.6, E) % ni).astype(np.int64)  # popular items: many duplicate pairs
+    num_cu, num_ci = 90, 60
+    u2cu = rng.integers(0, num_cu - 3, nu).astype(np.int64)  # the last 3 super-users stay empty
+    i2ci = rng.integers(0, num_ci, ni).astype(np.int64)
+    C = recsys.build_condensed_bipartite(train_u, train_i, u2cu, i2ci, num_cu, num_ci)
+    edge_index, w0 = recsys.condensed_csr_to_edge_index(C, device=torch.device("cpu"))
+    torch.manual_seed(7)
+    model = recsys.LightGCNCondensed(num_cu=num_cu, num_ci=num_ci, dim=32, num_layers=3,
+                                     edge_index=edge_index, edge_weight_init=w0,
+                                     device=torch.device("cpu"))
+    with torch.no_grad():  # non-trivial deltas and edge logits
+        model.user_delta.copy_(torch.randn(num_cu, 32) * 0.05)
+        model.item_delta.copy_(torch.randn(num_ci, 32) * 0.05)
+        model.edge_logit.add_(torch.randn(edge_index.shape[1]) * 0.3)
+    params = {k: v.detach().clone().numpy() for k, v in model.named_parameters()}
+    u_out, i_out = model.propagate()
+    bu = torch.from_numpy(rng.integers(0, num_cu, 256).astype(np.int64))
+    bp = torch.from_numpy(rng.integers(0, num_ci, 256).astype(np.int64))
+    bn = torch.from_numpy(rng.integers(0, num_ci, 256).astype(np.int64))
+    loss = model.bpr_loss(bu, bp, bn, reg_lambda=1e-4)
+    loss.backward()
+    out = {"train_u": train_u, "train_i": train_i, "u2cu": u2cu, "i2ci": i2ci,
+           "num_cu": np.int64(num_cu), "num_ci": np.int64(num_ci),
+           "C_indptr": C.indptr.astype(np.int64), "C_indices": C.indices.astype(np.int64),
+           "C_data": C.data.astype(np.float32), "edge_index": edge_index.numpy(), "w0": w0.numpy(),
+           "u_out": u_out.detach().numpy(), "i_out": i_out.detach().numpy(),
+           "bpr_u": bu.numpy(), "bpr_pos": bp.numpy(), "bpr_neg": bn.numpy(),
+           "loss": np.float64(loss.item()), "dim": np.int64(32), "layers": np.int64(3)}
+    for k, v in params.items():
+        out["param_" + k.replace(".", "_")] = v
+    for k, v in model.named_parameters():
+        out["grad_" + k.replace(".", "_")] = v.grad.detach().numpy()
+    np.savez_compressed(os.path.join(OUT, "golden_recsys.npz"), **out)
+
+
 def main():
     from threadpoolctl import threadpool_limits
     import sklearn
@@ -382,7 +426,7 @@ def main():
     import torch
     os.makedirs(OUT, exist_ok=True)
     du, agent, recsys = import_reference()
-    which = set(sys.argv[1:]) or {"G1", "G2", "G3", "G3b", "G5", "G6", "G7"}
+    which = set(sys.argv[1:]) or {"G1", "G2", "G3", "G3b", "G5", "G6", "G7", "G8"}
     with threadpool_limits(limits=1):
         if "G1" in which:
             g1_normalize(du)
@@ -397,6 +441,8 @@ def main():
             g5_clustgdd(agent, "ogbn-arxiv")
         if "G6" in which:
             g6_condense(du, agent)
+        if "G8" in which:
+            g8_recsys(recsys)
         if "G7" in which:
             g7_induct("flickr")
             g7_induct("reddit")
