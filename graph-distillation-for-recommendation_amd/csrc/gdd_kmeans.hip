@@ -225,6 +225,91 @@ __global__ __launch_bounds__(64 * WAVES) void k_assign(int64_t n, int dim, int d
   }
 }
 
+// ---- bf16 distance variant (configs 2, 3 and 5 carry fp32 and bf16 distances) ----
+// Same block shape and key merge as k_assign, but the X and C tiles are rounded to bf16 (nearest
+// even) in LDS and each 32x32 tile is a chain of v_mfma_f32_32x32x16_bf16 (fp32 accumulate). The
+// distance is fma(-2, <x, c>_bf16, ||c||^2) with the fp32 numpy-order norms, the label the first
+// minimum. Not bit-compatible with sklearn (the dot products round their operands): labels agree
+// except where two centres' fp32 distances lie within the bf16 rounding of the dot products.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);  // NaN stays NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+__host__ __device__ inline size_t assign_bf16_lds(int waves, int dimp16, int cch) {
+  const int SB = dimp16 + 8;  // bf16 per LDS row: 16-byte aligned rows, shifted by 16 B per row
+  const int ncp = (cch + 31) & ~31;
+  return sizeof(uint16_t) * ((size_t)ncp * SB + (size_t)32 * waves * SB) + sizeof(float) * ncp + 16;
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_assign_bf16(int64_t n, int dim, int dimp16,
+                                                            const float* __restrict__ X,
+                                                            const int64_t* __restrict__ rows, int k,
+                                                            const float* __restrict__ C,
+                                                            const float* __restrict__ cn2, int cch,
+                                                            unsigned long long* __restrict__ keys) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
+  constexpr int kPts = 32 * WAVES;
+  const int SB = dimp16 + 8;
+  const int c0 = blockIdx.y * cch;
+  const int nc = min(k, c0 + cch) - c0;
+  const int ncp = (nc + 31) & ~31;
+  uint16_t* Cl = lds16;
+  uint16_t* Pl = Cl + (size_t)ncp * SB;
+  float* Nl = reinterpret_cast<float*>(Pl + (size_t)kPts * SB);
+  const int tid = threadIdx.x;
+  const int64_t p0 = (int64_t)blockIdx.x * kPts;
+  for (int idx = tid; idx < kPts * dimp16; idx += blockDim.x) {
+    const int r = idx / dimp16, c = idx - r * dimp16;
+    const int64_t pi = p0 + r;
+    float v = 0.f;
+    if (pi < n && c < dim) {
+      const int64_t src = rows ? rows[pi] : pi;
+      v = X[src * dim + c];
+    }
+    Pl[r * SB + c] = f32_to_bf16_rne(v);
+  }
+  for (int idx = tid; idx < ncp * dimp16; idx += blockDim.x) {
+    const int r = idx / dimp16, c = idx - r * dimp16;
+    Cl[r * SB + c] = f32_to_bf16_rne((r < nc && c < dim) ? C[(int64_t)(c0 + r) * dim + c] : 0.f);
+  }
+  for (int idx = tid; idx < ncp; idx += blockDim.x) Nl[idx] = idx < nc ? cn2[c0 + idx] : 0.f;
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63;
+  const int kh = lane >> 5;
+  const uint16_t* bp = Pl + (wave * 32 + (lane & 31)) * SB + 8 * kh;
+  unsigned long long best = ~0ull;
+  for (int ct = 0; ct < ncp; ct += 32) {
+    const uint16_t* ap = Cl + (ct + (lane & 31)) * SB + 8 * kh;
+    floatx16 acc = {};
+    for (int s16 = 0; s16 < dimp16; s16 += 16) {
+      const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(ap + s16);
+      const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(bp + s16);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ci = ct + (r & 3) + 8 * (r >> 2) + 4 * kh;
+      if (ci < nc) {
+        const float d = __builtin_fmaf(-2.f, acc[r], Nl[ci]);
+        const unsigned long long key = pack_key(d, c0 + ci);
+        best = key < best ? key : best;
+      }
+    }
+  }
+  const unsigned long long other = __shfl_xor(best, 32);
+  best = other < best ? other : best;
+  if (lane < 32) {
+    const int64_t pi = p0 + wave * 32 + lane;
+    if (pi < n && best != ~0ull) atomicMin(keys + pi, best);
+  }
+}
+
 __global__ void k_assign_finalize(int64_t n, int dim, const float* __restrict__ X,
                                   const int64_t* __restrict__ rows, const float* __restrict__ C,
                                   const unsigned long long* __restrict__ keys,
@@ -663,9 +748,13 @@ __global__ __launch_bounds__(64 * W) void k_mb_assign(
   if (blk >= P * G) {
     const int e = blk - P * G;
     if (tl.active && e == 0) {
+      GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 82);
       mb_tail_block(tl, lds);
+      GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 80);
     } else if (rn.rows) {
+      GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 83);
       mt_randint_from(rn.in, reinterpret_cast<uint32_t*>(lds), 0, rn.n, rn.bs, rn.rows, rn.out);
+      GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 81);
     }
     return;
   }
@@ -1148,6 +1237,38 @@ extern "C" int gdd_kmeans_assign(int64_t n, int dim, const float* X, const int64
     return fail(GDD_E_WORKSPACE, "assign: workspace %zu too small", ws_bytes);
   return launch_assign(n, dim, X, rows, k, C, c_norm2, labels, sq_dist,
                        static_cast<unsigned long long*>(ws), nullptr, 0, to_hip(stream));
+}
+
+extern "C" int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const int64_t* rows, int k,
+                                      const float* C, const float* c_norm2, int32_t* labels,
+                                      float* sq_dist, void* ws, size_t ws_bytes, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && dim > 0 && dim <= 512 && k > 0, "kmeans_assign_bf16: bad shape");
+  GDD_REQUIRE(X && C && c_norm2 && labels && ws, "kmeans_assign_bf16: null pointer");
+  if (ws_bytes < gdd_kmeans_assign_ws_bytes(n))
+    return fail(GDD_E_WORKSPACE, "kmeans_assign_bf16: workspace too small");
+  hipStream_t s = to_hip(stream);
+  unsigned long long* keys = static_cast<unsigned long long*>(ws);
+  const int dimp16 = (dim + 15) & ~15;
+  constexpr int kWaves = 4;
+  const int64_t gx = (n + 32 * kWaves - 1) / (32 * kWaves);
+  const int kp = (k + 31) & ~31;
+  int cch = 32;
+  while (cch + 32 <= kp && assign_bf16_lds(kWaves, dimp16, cch + 32) <= 65536) cch += 32;
+  int64_t gy = (k + cch - 1) / cch;
+  while (gx * gy < 1024 && cch > 32) {
+    cch -= 32;
+    gy = (k + cch - 1) / cch;
+  }
+  GDD_REQUIRE(gx < (1ll << 31) && gy < 65536, "kmeans_assign_bf16: grid too large");
+  const size_t lds = assign_bf16_lds(kWaves, dimp16, cch);
+  k_fill_u64<<<blocks_for(n), 256, 0, s>>>(n, keys, ~0ull, nullptr, 0);
+  GDD_LAUNCHED();
+  k_assign_bf16<kWaves><<<dim3((unsigned)gx, (unsigned)gy), 64 * kWaves, lds, s>>>(
+      n, dim, dimp16, X, rows, k, C, c_norm2, cch, keys);
+  GDD_LAUNCHED();
+  k_assign_finalize<<<blocks_for(n), 256, 0, s>>>(n, dim, X, rows, C, keys, labels, sq_dist, nullptr, 0);
+  GDD_LAUNCHED();
+  return GDD_OK;
 }
 
 extern "C" int gdd_inertia(int64_t n, const float* sq_dist, const float* w, float* out,

@@ -67,10 +67,13 @@ class _Ops:
                                           self.stream))
         return self.cn2
 
-    def assign(self, X, C, rows=None, labels=None, sq=None, n=None):
+    def assign(self, X, C, rows=None, labels=None, sq=None, n=None, precision="fp32"):
         n = (rows.shape[0] if rows is not None else X.shape[0]) if n is None else n
         cn2 = self.row_norms(C)
-        _lib.check(self.lib.gdd_kmeans_assign(
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        fn = self.lib.gdd_kmeans_assign if precision == "fp32" else self.lib.gdd_kmeans_assign_bf16
+        _lib.check(fn(
             n, self.dim, X.data_ptr(), _lib.ptr(rows), C.shape[0], C.data_ptr(), cn2.data_ptr(),
             labels.data_ptr(), _lib.ptr(sq), self.ws_assign.data_ptr(), self.ws_assign.numel(),
             self.stream))
@@ -180,12 +183,15 @@ class _BaseKMeans:
         self._inertia_async = None
         self._inertia_value = value
 
-    def predict(self, X):
+    def predict(self, X, precision: str = "fp32"):
+        """Nearest centre of each row. precision='fp32' is sklearn's predict bit for bit;
+        'bf16' rounds the dot products' operands to bf16 (MFMA bf16 path) and may
+        differ where two centres are within that rounding."""
         Xd = _as_device_f32(X, self.device)
         C = torch.from_numpy(np.ascontiguousarray(self.cluster_centers_, np.float32)).to(Xd.device)
         ops = _Ops(Xd.device, Xd.shape[0], C.shape[0], Xd.shape[1])
         labels = torch.empty(Xd.shape[0], dtype=torch.int32, device=Xd.device)
-        ops.assign(Xd, C, labels=labels)
+        ops.assign(Xd, C, labels=labels, precision=precision)
         return labels.cpu().numpy()
 
     @staticmethod

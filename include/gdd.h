@@ -115,6 +115,15 @@ size_t gdd_kmeans_assign_ws_bytes(int64_t n);
 int gdd_kmeans_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k,
                       const float* C, const float* c_norm2, int32_t* labels, float* sq_dist,
                       void* ws, size_t ws_bytes, gdd_stream_t stream);
+/* bf16 distance variant (configs 2, 3, 5 carry fp32 and bf16 distances). Same        */
+/* arguments and outputs; the X and C operands are rounded to bf16 (nearest even) and the dot       */
+/* products run as v_mfma_f32_32x32x16_bf16 chains with fp32 accumulation; distances use the fp32    */
+/* c_norm2. NOT bit-compatible with sklearn: a label may differ where two centres' distances lie     */
+/* within the bf16 rounding of the dot products (|err| <= ~2^-7 ||x|| ||c||). sq_dist is the exact   */
+/* fp32 distance to the chosen centre.                                                              */
+int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const int64_t* rows, int k,
+                           const float* C, const float* c_norm2, int32_t* labels, float* sq_dist,
+                           void* ws, size_t ws_bytes, gdd_stream_t stream);
 
 /* out[0] = sequential fp32 sum of sq_dist[i] * w[i] in sample order (w == NULL: ones); this is      */
 /* sklearn _inertia_dense with one OpenMP thread (_k_means_common.pyx:92-121).                       */

@@ -158,3 +158,35 @@ def test_minibatch_tol_path():
     # the centre-shift sum is an fp32 device reduction (numpy's pairwise order is not restated):
     # same result unless the stop test sits within rounding of the tolerance
     assert abs(m.n_steps_ - ref["n_steps_"]) <= 1
+
+
+@pytest.mark.parametrize("n,dim,k", [(50000, 40, 454), (3000, 7, 70), (20000, 64, 200), (1000, 47, 1)])
+def test_assign_bf16_within_rounding(n, dim, k):
+    # the bf16 distance variant: labels equal the exact fp32 ones except where two
+    # centres' distances lie within the bf16 rounding of the dot products (2^-7 ||x|| ||c|| each)
+    from gdd.kmeans import _Ops
+    rng = np.random.default_rng(n + k)
+    X = (rng.standard_normal((n, dim)) + rng.integers(0, 5, (n, 1))).astype(np.float32)
+    C = X[rng.choice(n, k, replace=False)] + rng.standard_normal((k, dim)).astype(np.float32) * 0.1
+    Xd, Cd = torch.from_numpy(X).cuda(), torch.from_numpy(C).cuda()
+    ops = _Ops("cuda", n, k, dim)
+    l32 = torch.empty(n, dtype=torch.int32, device="cuda")
+    l16 = torch.empty(n, dtype=torch.int32, device="cuda")
+    sq16 = torch.empty(n, dtype=torch.float32, device="cuda")
+    ops.assign(Xd, Cd, labels=l32)
+    ops.assign(Xd, Cd, labels=l16, sq=sq16, precision="bf16")
+    a, b = l32.cpu().numpy(), l16.cpu().numpy()
+    assert b.min() >= 0 and b.max() < k
+    assert (a == b).mean() >= 0.95  # near-ties are common here: centres sit among the points
+    diff = np.nonzero(a != b)[0]
+    X64, C64 = X.astype(np.float64), C.astype(np.float64)
+    xn = np.linalg.norm(X64, axis=1)
+    cn = np.linalg.norm(C64, axis=1)
+    for i in diff[:2000]:
+        di = ((X64[i] - C64) ** 2).sum(-1)
+        bound = 2 * 2.0 ** -7 * xn[i] * (cn[a[i]] + cn[b[i]]) + 1e-3 * (1 + di[a[i]])
+        assert di[b[i]] - di[a[i]] <= bound
+    # sq_dist is the exact fp32 distance to the chosen centre (the fp32 finalize path)
+    i = rng.integers(0, n, 64)
+    ref = ((X[i] - C[b[i]]) ** 2).sum(-1)
+    np.testing.assert_allclose(sq16.cpu().numpy()[i], ref, rtol=1e-5, atol=1e-5)

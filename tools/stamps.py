@@ -45,7 +45,7 @@ def main():
         a = read(lib, "kmeans")
         p = read(lib, "kpp")
         print(f"rep {rep}: steps={km.n_steps_}")
-        show("assign_small", a, [0, 2, 3, 4, 5, 6, 13, 14, 15, 16], 0)
+        show("assign_small", a, [0, 2, 3, 4, 5, 6, 13, 14, 15, 16, 82, 80, 83, 81], 0)
         show("update block0", a, list(range(20, 26)), 20)
         show("update tail", a, list(range(30, 33)), 30)
         show("mb_reassign", a, list(range(40, 47)), 40)
