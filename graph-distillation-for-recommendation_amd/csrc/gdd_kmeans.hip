@@ -153,14 +153,18 @@ __global__ void k_fill_u64(int64_t n, unsigned long long* p, unsigned long long 
   if (i < n) p[i] = v;
 }
 
-// One block = WAVES waves x 32 points; blockIdx.y = a chunk of `cch` centers. A wave computes the
-// 32x32 tile D[center][point] = sum_t C[center][t] * X[point][t] with dimp/2 chained
+// One block = WAVES waves x 32 points; blockIdx.y = a chunk of `cch` centers. A wave computes
+// 32x32 tiles D[center][point] = sum_t C[center][t] * X[point][t] with chained
 // v_mfma_f32_32x32x2_f32 (lanes 0-31 feed feature 2s, lanes 32-63 feature 2s+1 of each step, so the
 // chain visits features in order 0,1,2,...). Lane l then holds point l&31 against the 16 centers
 // (r&3)+8(r>>2)+4(l>>5), r = 0..15, and keeps a running lexicographic minimum; the two half-waves
 // merge with one xor-shuffle and the block's result enters keys[] through a 64-bit atomicMin.
-// LDS rows use an odd stride (dimp+1 floats) so the 32 rows read by one ds_read_b32 hit 32 banks.
-template <int WAVES>
+// Rows are zero-padded to dimp (a multiple of 16 features, so the step loop runs in unguarded groups
+// of 8 whose LDS operands are all read before the group's MFMAs), two centre tiles advance together
+// (two independent accumulator chains), and LDS rows use an odd stride (dimp+1 floats) so the 32 rows
+// read by one ds_read_b32 hit 32 banks. Zero features add exact zeros to the fma chain (a -0/+0
+// difference in a dot product is erased by pack_key), so the distances stay bit-exact.
+template <int WAVES, bool VEC>
 __global__ __launch_bounds__(64 * WAVES) void k_assign(int64_t n, int dim, int dimp,
                                                        const float* __restrict__ X,
                                                        const int64_t* __restrict__ rows, int k,
@@ -180,20 +184,46 @@ __global__ __launch_bounds__(64 * WAVES) void k_assign(int64_t n, int dim, int d
   float* Nl = Pl + (size_t)kPts * S;
   const int tid = threadIdx.x;
   const int64_t p0 = (int64_t)blockIdx.x * kPts;
-
-  for (int idx = tid; idx < kPts * dimp; idx += blockDim.x) {
-    const int r = idx / dimp, c = idx - r * dimp;
-    const int64_t pi = p0 + r;
-    float v = 0.f;
-    if (pi < n && c < dim) {
-      const int64_t src = rows ? rows[pi] : pi;
-      v = X[src * dim + c];
+  if (VEC) {  // float4 rows (dim % 4 == 0, 16-byte aligned X and C)
+    const int q = dim >> 2;
+    for (int idx = tid; idx < kPts * q; idx += blockDim.x) {
+      const int r = idx / q, c4 = idx - r * q;
+      const int64_t pi = p0 + r;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (pi < n) v = *reinterpret_cast<const float4*>(X + (rows ? rows[pi] : pi) * dim + 4 * c4);
+      float* d = Pl + r * S + 4 * c4;
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
     }
-    Pl[r * S + c] = v;
+    for (int idx = tid; idx < ncp * q; idx += blockDim.x) {
+      const int r = idx / q, c4 = idx - r * q;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < nc) v = *reinterpret_cast<const float4*>(C + (int64_t)(c0 + r) * dim + 4 * c4);
+      float* d = Cl + r * S + 4 * c4;
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+    }
+  } else {
+    for (int idx = tid; idx < kPts * dim; idx += blockDim.x) {
+      const int r = idx / dim, c = idx - r * dim;
+      const int64_t pi = p0 + r;
+      Pl[r * S + c] = pi < n ? X[(rows ? rows[pi] : pi) * dim + c] : 0.f;
+    }
+    for (int idx = tid; idx < ncp * dim; idx += blockDim.x) {
+      const int r = idx / dim, c = idx - r * dim;
+      Cl[r * S + c] = r < nc ? C[(int64_t)(c0 + r) * dim + c] : 0.f;
+    }
   }
-  for (int idx = tid; idx < ncp * dimp; idx += blockDim.x) {
-    const int r = idx / dimp, c = idx - r * dimp;
-    Cl[r * S + c] = (r < nc && c < dim) ? C[(int64_t)(c0 + r) * dim + c] : 0.f;
+  const int pad = dimp - dim;
+  if (pad > 0) {
+    for (int idx = tid; idx < (ncp + kPts) * pad; idx += blockDim.x) {
+      const int r = idx / pad, c = dim + (idx - r * pad);
+      Cl[r * S + c] = 0.f;  // rows ncp.. are the point rows (Pl follows Cl with the same stride)
+    }
   }
   for (int idx = tid; idx < ncp; idx += blockDim.x) Nl[idx] = idx < nc ? cn2[c0 + idx] : 0.f;
   __syncthreads();
@@ -201,18 +231,40 @@ __global__ __launch_bounds__(64 * WAVES) void k_assign(int64_t n, int dim, int d
   const int wave = tid >> 6, lane = tid & 63;
   const int kh = lane >> 5;
   const float* bp = Pl + (wave * 32 + (lane & 31)) * S + kh;
+  const int ns = dimp >> 1;  // a multiple of 8
   unsigned long long best = ~0ull;
-  for (int ct = 0; ct < ncp; ct += 32) {
-    const float* ap = Cl + (ct + (lane & 31)) * S + kh;
-    floatx16 acc = {};
-    for (int s2 = 0; s2 < dimp; s2 += 2)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[s2], bp[s2], acc, 0, 0, 0);
+  for (int ct = 0; ct < ncp; ct += 64) {
+    const bool two = ct + 32 < ncp;
+    const float* ap0 = Cl + (ct + (lane & 31)) * S + kh;
+    const float* ap1 = two ? ap0 + 32 * S : ap0;
+    floatx16 acc0 = {}, acc1 = {};
+    for (int s0 = 0; s0 < ns; s0 += 8) {
+      float a0[8], a1[8], bv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int o = 2 * (s0 + u);
+        a0[u] = ap0[o];
+        a1[u] = ap1[o];
+        bv[u] = bp[o];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], bv[u], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], bv[u], acc1, 0, 0, 0);
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int ci = ct + (r & 3) + 8 * (r >> 2) + 4 * kh;
       if (ci < nc) {
-        const float d = __builtin_fmaf(-2.f, acc[r], Nl[ci]);
+        const float d = __builtin_fmaf(-2.f, acc0[r], Nl[ci]);
         const unsigned long long key = pack_key(d, c0 + ci);
+        best = key < best ? key : best;
+      }
+      const int cj = ci + 32;
+      if (two && cj < nc) {
+        const float d = __builtin_fmaf(-2.f, acc1[r], Nl[cj]);
+        const unsigned long long key = pack_key(d, c0 + cj);
         best = key < best ? key : best;
       }
     }
@@ -222,6 +274,117 @@ __global__ __launch_bounds__(64 * WAVES) void k_assign(int64_t n, int dim, int d
   if (lane < 32) {
     const int64_t pi = p0 + wave * 32 + lane;
     if (pi < n && best != ~0ull) atomicMin(keys + pi, best);
+  }
+}
+
+// Persistent variant for dimp <= 96 (every config's k-means input): a block stages its centre
+// chunk ONCE, then walks point tiles t = blockIdx.x, +gridDim.x, ... While a tile's MFMA tiles run,
+// the next tile's rows are already in flight into registers (two threads per point row, features
+// h, h+2, ... with clamped, unconditional loads), so the staging hides behind the MFMAs instead of
+// preceding them in every block. Same tiles, order and key merge as k_assign (bit-exact); with a
+// single centre chunk (gridDim.y == 1) the keys are stored, not atomically merged.
+constexpr int kPersistMaxHalf = 48;  // ceil(96 / 2) row elements per thread
+__global__ __launch_bounds__(256) void k_assign_persist(int64_t n, int dim, int dimp,
+                                                       const float* __restrict__ X,
+                                                       const int64_t* __restrict__ rows, int k,
+                                                       const float* __restrict__ C,
+                                                       const float* __restrict__ cn2, int cch,
+                                                       unsigned long long* __restrict__ keys,
+                                                       const int32_t* __restrict__ stop, int step_i) {
+  if (stopped(stop, step_i)) return;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int kPts = 128;
+  const int S = dimp + 1;
+  const int c0 = blockIdx.y * cch;
+  const int nc = min(k, c0 + cch) - c0;
+  const int ncp = (nc + 31) & ~31;
+  float* Cl = lds;
+  float* Pl = Cl + (size_t)ncp * S;
+  float* Nl = Pl + (size_t)kPts * S;
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < ncp * dimp; idx += blockDim.x) {
+    const int r = idx / dimp, c = idx - r * dimp;
+    Cl[r * S + c] = (r < nc && c < dim) ? C[(int64_t)(c0 + r) * dim + c] : 0.f;
+  }
+  for (int idx = tid; idx < ncp; idx += blockDim.x) Nl[idx] = idx < nc ? cn2[c0 + idx] : 0.f;
+  const int64_t ntiles = (n + kPts - 1) / kPts;
+  const int pr = tid >> 1, ph = tid & 1;  // staging: point row pr, features ph, ph+2, ...
+  const int half = (dim + 1 - ph) >> 1;   // this thread's element count
+  float v[kPersistMaxHalf];
+  auto fetch = [&](int64_t t) {
+    const int64_t pi = t * kPts + pr;
+    const bool ok = pi < n;
+    const float* xr = X + (ok ? (rows ? rows[pi] : pi) : 0) * dim;
+#pragma unroll
+    for (int j = 0; j < kPersistMaxHalf; ++j) v[j] = xr[min(ph + 2 * j, dim - 1)];
+    if (!ok) {
+#pragma unroll
+      for (int j = 0; j < kPersistMaxHalf; ++j) v[j] = 0.f;
+    }
+  };
+  int64_t t = blockIdx.x;
+  if (t < ntiles) fetch(t);
+  const int wave = tid >> 6, lane = tid & 63;
+  const int kh = lane >> 5;
+  const float* bp = Pl + (wave * 32 + (lane & 31)) * S + kh;
+  const int ns = dimp >> 1;
+  for (; t < ntiles; t += gridDim.x) {
+    __syncthreads();  // the previous tile's MFMAs are done with Pl
+#pragma unroll
+    for (int j = 0; j < kPersistMaxHalf; ++j) {
+      const int c = ph + 2 * j;
+      if (c < dimp) Pl[pr * S + c] = (j < half) ? v[j] : 0.f;
+    }
+    __syncthreads();
+    if (t + gridDim.x < ntiles) fetch(t + gridDim.x);  // in flight during this tile's MFMAs
+    unsigned long long best = ~0ull;
+    for (int ct = 0; ct < ncp; ct += 64) {
+      const bool two = ct + 32 < ncp;
+      const float* ap0 = Cl + (ct + (lane & 31)) * S + kh;
+      const float* ap1 = two ? ap0 + 32 * S : ap0;
+      floatx16 acc0 = {}, acc1 = {};
+      for (int s0 = 0; s0 < ns; s0 += 8) {
+        float a0[8], a1[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int o = 2 * (s0 + u);
+          a0[u] = ap0[o];
+          a1[u] = ap1[o];
+          bv[u] = bp[o];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], bv[u], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], bv[u], acc1, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ci = ct + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        if (ci < nc) {
+          const float d = __builtin_fmaf(-2.f, acc0[r], Nl[ci]);
+          const unsigned long long key = pack_key(d, c0 + ci);
+          best = key < best ? key : best;
+        }
+        const int cj = ci + 32;
+        if (two && cj < nc) {
+          const float d = __builtin_fmaf(-2.f, acc1[r], Nl[cj]);
+          const unsigned long long key = pack_key(d, c0 + cj);
+          best = key < best ? key : best;
+        }
+      }
+    }
+    const unsigned long long other = __shfl_xor(best, 32);
+    best = other < best ? other : best;
+    if (lane < 32) {
+      const int64_t pi = t * kPts + wave * 32 + lane;
+      if (pi < n && best != ~0ull) {
+        if (gridDim.y == 1)
+          keys[pi] = best;
+        else
+          atomicMin(keys + pi, best);
+      }
+    }
   }
 }
 
@@ -1171,7 +1334,6 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
                   const float* c_norm2, int32_t* labels, float* sq_dist,
                   unsigned long long* keys, const int32_t* stop, int step_i, hipStream_t s,
                   const RngNext& rn = RngNext{nullptr, nullptr, nullptr, 0, 0}) {
-  const int dimp = (dim + 1) & ~1;
   if (use_small_assign(n, dim)) {
     const bool vec = (dim % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(C)) & 15) == 0;
     return vec ? launch_assign_small<true>(n, dim, X, rows, k, C, c_norm2, labels, sq_dist, stop,
@@ -1181,39 +1343,76 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
   }
   GDD_REQUIRE(!rn.rows, "assign: in-launch batch draws need the small-batch path");
   GDD_REQUIRE(c_norm2 && keys, "assign: large-n path needs c_norm2 and the key workspace");
-  const int waves = dimp <= 96 ? 4 : (dimp <= 224 ? 2 : 1);
+  const int dimp16 = (dim + 15) & ~15;  // zero-padded rows: unguarded groups of 8 MFMA steps
+  if (dimp16 <= 96) {
+    // persistent blocks: all centres in one chunk when they fit 2 blocks per CU, else the fewest
+    // chunks that do; about two blocks per CU walk the point tiles
+    const int kt = (k + 31) / 32;
+    int chunks = 1;
+    while (chunks < kt && assign_lds(4, dimp16, ((kt + chunks - 1) / chunks) * 32) > 78 * 1024) ++chunks;
+    const int cch = ((kt + chunks - 1) / chunks) * 32;
+    const int gy = (k + cch - 1) / cch;
+    const int64_t ntiles = (n + 127) / 128;
+    const int64_t gx = std::min<int64_t>(ntiles, std::max<int64_t>(1, 512 / gy));
+    const size_t lds = assign_lds(4, dimp16, cch);
+    if (gy > 1) {
+      k_fill_u64<<<blocks_for(n), 256, 0, s>>>(n, keys, ~0ull, stop, step_i);
+      GDD_LAUNCHED();
+    }
+    if (lds > 65536)
+      GDD_HIP(hipFuncSetAttribute((const void*)k_assign_persist, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+    k_assign_persist<<<dim3((unsigned)gx, (unsigned)gy), 256, lds, s>>>(n, dim, dimp16, X, rows, k, C,
+                                                                       c_norm2, cch, keys, stop, step_i);
+    GDD_LAUNCHED();
+    k_assign_finalize<<<blocks_for(n), 256, 0, s>>>(n, dim, X, rows, C, keys, labels, sq_dist, stop,
+                                                    step_i);
+    GDD_LAUNCHED();
+    return GDD_OK;
+  }
+  const int waves = dimp16 <= 96 ? 4 : (dimp16 <= 224 ? 2 : 1);
   const int64_t gx = (n + 32 * waves - 1) / (32 * waves);
   // centers per block: as many as fit the LDS budget (>= 32), then fewer while the grid is too
   // small to occupy 256 CUs
-  const size_t budget = dimp <= 224 ? 65536 : 160000;
+  const size_t budget = dimp16 <= 224 ? 65536 : 160000;
   const int kp = (k + 31) & ~31;
   int cch = 32;
-  while (cch + 32 <= kp && assign_lds(waves, dimp, cch + 32) <= budget) cch += 32;
+  while (cch + 32 <= kp && assign_lds(waves, dimp16, cch + 32) <= budget) cch += 32;
   int64_t gy = (k + cch - 1) / cch;
   while (gx * gy < 1024 && cch > 32) {
     cch -= 32;
     gy = (k + cch - 1) / cch;
   }
   GDD_REQUIRE(gx < (1ll << 31) && gy < 65536, "assign: grid too large");
-  const size_t lds = assign_lds(waves, dimp, cch);
+  const size_t lds = assign_lds(waves, dimp16, cch);
   k_fill_u64<<<blocks_for(n), 256, 0, s>>>(n, keys, ~0ull, stop, step_i);
   GDD_LAUNCHED();
   dim3 grid((unsigned)gx, (unsigned)gy);
-  if (lds > 65536) {
-    // gfx950 has 160 KiB of LDS per CU; opt the kernel in to more than the 64 KiB default
-    if (waves == 2)
-      GDD_HIP(hipFuncSetAttribute((const void*)k_assign<2>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    else if (waves == 1)
-      GDD_HIP(hipFuncSetAttribute((const void*)k_assign<1>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  }
+  const bool vec = (dim % 4 == 0) &&
+                   ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(C)) & 15) == 0;
+  auto go = [&](auto W_, auto V_) {
+    constexpr int W = decltype(W_)::value;
+    constexpr bool V = decltype(V_)::value;
+    if (lds > 65536)  // gfx950 has 160 KiB of LDS per CU; opt in above the 64 KiB default
+      GDD_HIP(hipFuncSetAttribute((const void*)k_assign<W, V>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+    k_assign<W, V><<<grid, 64 * W, lds, s>>>(n, dim, dimp16, X, rows, k, C, c_norm2, cch, keys, stop,
+                                             step_i);
+    return GDD_OK;
+  };
+  using T4 = std::integral_constant<int, 4>;
+  using T2 = std::integral_constant<int, 2>;
+  using T1 = std::integral_constant<int, 1>;
+  using VT = std::true_type;
+  using VF = std::false_type;
+  int rc0;
   if (waves == 4)
-    k_assign<4><<<grid, 256, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys, stop, step_i);
+    rc0 = vec ? go(T4(), VT()) : go(T4(), VF());
   else if (waves == 2)
-    k_assign<2><<<grid, 128, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys, stop, step_i);
+    rc0 = vec ? go(T2(), VT()) : go(T2(), VF());
   else
-    k_assign<1><<<grid, 64, lds, s>>>(n, dim, dimp, X, rows, k, C, c_norm2, cch, keys, stop, step_i);
+    rc0 = vec ? go(T1(), VT()) : go(T1(), VF());
+  if (rc0) return rc0;
   GDD_LAUNCHED();
   k_assign_finalize<<<blocks_for(n), 256, 0, s>>>(n, dim, X, rows, C, keys, labels, sq_dist, stop,
                                                   step_i);
