@@ -1125,24 +1125,96 @@ __global__ void k_offsets(int64_t n, const int32_t* __restrict__ skeys, int k,
 // ---------------------------------------------------------------------------------------------
 // Lloyd accumulation (sequential per cluster, sample order) and fixed-point variant
 // ---------------------------------------------------------------------------------------------
-__global__ void k_segment_sum_f32(int dim, const float* __restrict__ X, const float* __restrict__ w,
-                                  const int32_t* __restrict__ perm,
-                                  const int32_t* __restrict__ offsets, float* __restrict__ sums,
-                                  float* __restrict__ wsum) {
-  const int c = blockIdx.x;
+// One workgroup per cluster, its members (perm[offsets[c] .. offsets[c+1]), sample order) in
+// chunks of R rows staged through two LDS buffers: while thread f folds chunk i's column f as a
+// sequential fp32 chain (sum + X*w, separate mul and add), chunk i+1's rows are in flight into
+// registers, and chunk i+2's member ids too (so no chunk waits for the perm -> X round trip twice).
+// Staging map: !WIDE (dim <= 256): thread t loads feature t % dim of rows t / dim + q * rpp
+// (rpp = 256 / dim rows per pass, 48 passes); WIDE: features t and t + 256 of rows q (24 passes).
+// Weights (or unit counts) fold in the same order by a spare thread (dim < 256) or thread 0.
+constexpr int kSegLds = 12288;  // floats per LDS buffer (48 KiB)
+template <bool WIDE>
+__global__ __launch_bounds__(256) void k_segment_sum_f32(int dim, const float* __restrict__ X,
+                                                         const float* __restrict__ w,
+                                                         const int32_t* __restrict__ perm,
+                                                         const int32_t* __restrict__ offsets,
+                                                         float* __restrict__ sums,
+                                                         float* __restrict__ wsum) {
+  constexpr int P = WIDE ? 24 : 48;  // rows per thread per chunk
+  extern __shared__ __attribute__((aligned(16))) float sbuf[];
+  const int c = blockIdx.x, tid = threadIdx.x;
   const int32_t b = offsets[c], e = offsets[c + 1];
-  for (int f = threadIdx.x; f < dim; f += blockDim.x) {
-    float acc = 0.f;
-    for (int32_t t = b; t < e; ++t) {
-      const int32_t i = perm[t];
-      acc = acc + X[(int64_t)i * dim + f] * (w ? w[i] : 1.0f);
+  const int rpp = WIDE ? 1 : 256 / dim;
+  const int R = min(rpp * P, 1024);  // R * dim <= kSegLds
+  const int f0 = WIDE ? tid : tid % dim;
+  const int r0 = WIDE ? 0 : tid / dim;
+  const bool st_on = WIDE || r0 < rpp;
+  auto buf_of = [&](int slot) { return sbuf + slot * kSegLds; };
+  auto wbuf_of = [&](int slot) { return sbuf + 2 * kSegLds + slot * 1024; };
+  float v[WIDE ? 2 * P : P];
+  int32_t pa[P], pb[P];
+  auto fetch_ids = [&](int32_t m0, int32_t(&dst)[P]) {
+    const int32_t last = max(min(e - m0, R) - 1, 0);
+#pragma unroll
+    for (int q = 0; q < P; ++q) dst[q] = perm[m0 + min(r0 + q * rpp, last)];
+  };
+  auto fetch_x = [&](const int32_t(&ids)[P]) {
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const int64_t i = ids[q];
+      v[q] = X[i * dim + f0];
+      if constexpr (WIDE) v[P + q] = X[i * dim + min(f0 + 256, dim - 1)];
     }
-    sums[(int64_t)c * dim + f] = acc;
+  };
+  auto store = [&](int slot, int32_t m0) {
+    if (!st_on) return;
+    const int rows = min(e - m0, R);
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const int r = r0 + q * rpp;
+      if (r < rows) {
+        buf_of(slot)[r * dim + f0] = v[q];
+        if constexpr (WIDE)
+          if (f0 + 256 < dim) buf_of(slot)[r * dim + f0 + 256] = v[P + q];
+      }
+    }
+  };
+  float acc0 = 0.f, acc1 = 0.f, wacc = 0.f;
+  if (b < e) {
+    fetch_ids(b, pa);
+    fetch_x(pa);
+    if (b + R < e) fetch_ids(b + R, pb);
   }
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int32_t t = b; t < e; ++t) s = s + (w ? w[perm[t]] : 1.0f);
-    wsum[c] = s;
+  int slot = 0;
+  for (int32_t m0 = b; m0 < e; m0 += R) {
+    const int rows = min(R, e - m0);
+    store(slot, m0);
+    for (int r = tid; r < rows; r += 256) wbuf_of(slot)[r] = w ? w[perm[m0 + r]] : 1.0f;
+    __syncthreads();
+    if (m0 + R < e) {
+      fetch_x(pb);                                   // chunk i+1's rows (ids already here)
+      if (m0 + 2 * R < e) fetch_ids(m0 + 2 * R, pb);  // chunk i+2's ids
+    }
+    const float* B = buf_of(slot);
+    const float* W = wbuf_of(slot);
+    if (tid < dim)
+      for (int r = 0; r < rows; ++r) acc0 = acc0 + B[r * dim + tid] * W[r];
+    if (WIDE && tid + 256 < dim)
+      for (int r = 0; r < rows; ++r) acc1 = acc1 + B[r * dim + tid + 256] * W[r];
+    if (!WIDE && dim < 256 && tid == 255)  // a spare thread folds the weights
+      for (int r = 0; r < rows; ++r) wacc = wacc + W[r];
+    slot ^= 1;
+  }
+  if (tid < dim) sums[(int64_t)c * dim + tid] = acc0;
+  if (WIDE && tid + 256 < dim) sums[(int64_t)c * dim + tid + 256] = acc1;
+  if (dim >= 256) {  // no spare thread: fold the weights after
+    if (tid == 0) {
+      float s2 = 0.f;
+      for (int32_t t = b; t < e; ++t) s2 = s2 + (w ? w[perm[t]] : 1.0f);
+      wsum[c] = s2;
+    }
+  } else if (tid == 255) {
+    wsum[c] = wacc;
   }
 }
 
@@ -1722,7 +1794,17 @@ extern "C" int gdd_segment_sum_f32(int64_t n, int dim, const float* X, const flo
                                    float* wsum, gdd_stream_t stream) {
   GDD_REQUIRE(n > 0 && dim > 0 && k > 0 && X && perm && offsets && sums && wsum,
               "segment_sum_f32: bad arguments");
-  k_segment_sum_f32<<<k, 64, 0, to_hip(stream)>>>(dim, X, w, perm, offsets, sums, wsum);
+  GDD_REQUIRE(dim <= 512, "segment_sum_f32: dim=%d > 512", dim);
+  const size_t lds = sizeof(float) * (2 * kSegLds + 2048);
+  if (dim > 256) {
+    GDD_HIP(hipFuncSetAttribute((const void*)k_segment_sum_f32<true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    k_segment_sum_f32<true><<<k, 256, lds, to_hip(stream)>>>(dim, X, w, perm, offsets, sums, wsum);
+  } else {
+    GDD_HIP(hipFuncSetAttribute((const void*)k_segment_sum_f32<false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    k_segment_sum_f32<false><<<k, 256, lds, to_hip(stream)>>>(dim, X, w, perm, offsets, sums, wsum);
+  }
   GDD_LAUNCHED();
   return GDD_OK;
 }

@@ -490,13 +490,40 @@ __device__ float fold_pot(const KppArgs& a, int q, int tr) {
   return y;
 }
 
-// the T potentials of the round at parity q into s_pot; returns the argmin (np.argmin semantics)
+// the T potentials of the round at parity q into s_pot; returns the argmin (np.argmin semantics).
+// The per-block sgemv_t results are staged through LDS in chunks (every thread loads, one memory
+// round trip per chunk), then T threads fold their trial's chunk in block order: the same sequential
+// fp32 chain as fold_pot, without one dependent global load group per 8 blocks.
+constexpr int kFoldChunk = 512;
 __device__ int fold_round(const KppArgs& a, int q, float* s_pot) {
+  __shared__ float s_fold[kFoldChunk * kMaxTrials];
   const int tid = threadIdx.x;
   if (a.T == 1) {
     if (tid == 0) s_pot[0] = a.pot1[q];
-  } else if (tid < a.T) {
-    s_pot[tid] = fold_pot(a, q, tid);
+  } else {
+    float y = 0.f;
+    for (int64_t b0 = 0; b0 < a.nsg; b0 += kFoldChunk) {
+      const int m = (int)min<int64_t>(kFoldChunk, a.nsg - b0);
+      for (int e = tid; e < m * a.T; e += blockDim.x) {
+        const int tr = e / m, bb = e - tr * m;
+        s_fold[tr * kFoldChunk + bb] = a.vblk[q][(int64_t)tr * a.nblk + b0 + bb];
+      }
+      __syncthreads();
+      if (tid < a.T) {
+        const float* v = s_fold + tid * kFoldChunk;
+        for (int bb = 0; bb < m; ++bb) y = y + v[bb];
+      }
+      __syncthreads();
+    }
+    if (tid < a.T) {
+      if (a.m1 < a.n) {
+        const float* row = a.dist[q] + (int64_t)tid * a.n;
+        float sx = row[a.m1] * wv(a.w, a.m1);
+        for (int64_t o = a.m1 + 1; o < a.n; ++o) sx = __builtin_fmaf(row[o], wv(a.w, o), sx);
+        y = y + sx;
+      }
+      s_pot[tid] = y;
+    }
   }
   __syncthreads();
   int b = 0;

@@ -190,3 +190,39 @@ def test_assign_bf16_within_rounding(n, dim, k):
     i = rng.integers(0, n, 64)
     ref = ((X[i] - C[b[i]]) ** 2).sum(-1)
     np.testing.assert_allclose(sq16.cpu().numpy()[i], ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("n,dim,k,weighted", [(5000, 1, 7, False), (20000, 7, 70, True), (30000, 47, 5, False),
+                                              (3000, 256, 9, True), (2000, 300, 4, False), (1500, 512, 3, True)])
+def test_segment_sum_f32_sequential(n, dim, k, weighted):
+    # Lloyd's M-step sums (sklearn lloyd_iter_chunked_dense, one thread): per cluster, sequential fp32
+    # in sample order (sum + x*w); an empty cluster gives zeros
+    rng = np.random.default_rng(dim)
+    X = rng.standard_normal((n, dim)).astype(np.float32)
+    lab = rng.integers(0, k - 1, n).astype(np.int32)  # cluster k-1 stays empty
+    w = (rng.random(n) + 0.5).astype(np.float32) if weighted else None
+    lib = _lib.device_lib()
+    Xd, ld = torch.from_numpy(X).cuda(), torch.from_numpy(lab).cuda()
+    wd = torch.from_numpy(w).cuda() if weighted else None
+    perm = torch.empty(n, dtype=torch.int32, device="cuda")
+    offs = torch.empty(k + 1, dtype=torch.int32, device="cuda")
+    ws = _lib.workspace(lib.gdd_group_ws_bytes(n, k), "cuda")
+    st = _lib.stream_ptr("cuda")
+    _lib.check(lib.gdd_group_by_label(n, ld.data_ptr(), k, perm.data_ptr(), offs.data_ptr(), ws.data_ptr(),
+                                      ws.numel(), st))
+    sums = torch.empty(k, dim, dtype=torch.float32, device="cuda")
+    wsum = torch.empty(k, dtype=torch.float32, device="cuda")
+    _lib.check(lib.gdd_segment_sum_f32(n, dim, Xd.data_ptr(), _lib.ptr(wd), perm.data_ptr(), offs.data_ptr(), k,
+                                       sums.data_ptr(), wsum.data_ptr(), st))
+    ref = np.zeros((k, dim), np.float32)
+    wref = np.zeros(k, np.float32)
+    for c in range(k):
+        idx = np.nonzero(lab == c)[0]
+        if idx.size == 0:
+            continue
+        terms = X[idx] * (w[idx][:, None] if weighted else np.float32(1.0))
+        ref[c] = np.add.accumulate(terms.astype(np.float32), axis=0, dtype=np.float32)[-1]
+        wt = w[idx] if weighted else np.ones(idx.size, np.float32)
+        wref[c] = np.add.accumulate(wt, dtype=np.float32)[-1]
+    assert np.array_equal(sums.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(wsum.cpu().numpy().view(np.uint32), wref.view(np.uint32))
