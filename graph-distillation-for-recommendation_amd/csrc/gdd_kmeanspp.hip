@@ -327,6 +327,18 @@ __device__ double skl_dot(const double* __restrict__ c, const float* __restrict_
   }
 }
 
+// does every element of the chunk with m rows take the plain k-ordered chain? (the per-chunk form of
+// the host's skl_all_seq: a call whose last chunk is small runs edge kernels there, but its other
+// chunks stay plain)
+__device__ __forceinline__ bool skl_chunk_seq(const SklPlan& p, int64_t m) {
+  if (p.T == 1 || p.dim > 384 || m <= 1) return false;
+  const double mnk = (double)m * p.T * p.dim;
+  if (mnk <= 1e6 && m * p.T <= 1200 && p.dim >= 32) return false;
+  const bool threaded = kBlasThreads >= 2 && mnk >= 524288.0;
+  if (!threaded && m > 192 && p.T >= 12 && (m & 7) != 0) return false;
+  return true;
+}
+
 __device__ __forceinline__ double skl_point_dot(const SklPlan& p, const double* __restrict__ c,
                                                 const float* __restrict__ x, int64_t i, int t) {
   if (p.all_seq) return dot_seq(c, x, p.dim);
@@ -411,6 +423,39 @@ __device__ __forceinline__ void seq_dots(const float* __restrict__ X, int dim, i
   }
 }
 
+// seq_dots from the transpose XT (dim x n): lanes read consecutive points of one feature, so every
+// load is coalesced (a row-major read of 4096 scattered rows refetches each line per feature group)
+__device__ __forceinline__ void seq_dots_t(const float* __restrict__ XT, int dim, int64_t n, int64_t j0,
+                                           const double* __restrict__ s_c, double (&dot)[kPer]) {
+  const int tid = threadIdx.x;
+  int64_t ix[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int64_t i = j0 + tid + kThr * q;
+    ix[q] = i < n ? i : j0;
+    dot[q] = 0.0;
+  }
+  int j = 0;
+  for (; j + 8 <= dim; j += 8) {
+    float u[8][kPer];
+#pragma unroll
+    for (int v = 0; v < 8; ++v)
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) u[v][q] = XT[(int64_t)(j + v) * n + ix[q]];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const double cv = s_c[j + v];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) dot[q] = __builtin_fma(cv, (double)u[v][q], dot[q]);
+    }
+  }
+  for (; j < dim; ++j) {
+    const double cv = s_c[j];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) dot[q] = __builtin_fma(cv, (double)XT[(int64_t)j * n + ix[q]], dot[q]);
+  }
+}
+
 // ---- the block-wise fp64 cumulative potential ----------------------------------------------------
 // prefix(e) of entry e = 16*tid + u of a block: thread-sequential running sum r_u, the exclusive
 // shuffle scan E of the thread totals inside the wave, the wave totals added in wave order B:
@@ -449,6 +494,7 @@ struct KppArgs {
   int64_t n, m1;      // points; m1 = n & ~3 (the entries under sgemv_t blocks)
   int dim, T, nblk, nsg;  // nblk = ceil(n / 4096); nsg = ceil(m1 / 4096)
   const float* X;
+  const float* XT;    // dim x n transpose for the plain-chain distances (nullptr: read X rows)
   const float* w;     // sample weights (nullptr: ones)
   const double* xsq;
   const float* closest0;
@@ -613,7 +659,10 @@ __device__ __forceinline__ void block_dists(const KppArgs& a, int t, int64_t j0,
   const int64_t n = a.n;
   if constexpr (SEQ) {
     double dot[kPer];
-    seq_dots(a.X, a.dim, n, j0, s_c, dot);
+    if (a.XT)
+      seq_dots_t(a.XT, a.dim, n, j0, s_c, dot);
+    else
+      seq_dots(a.X, a.dim, n, j0, s_c, dot);
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const int o = tid + kThr * q;
@@ -628,6 +677,35 @@ __device__ __forceinline__ void block_dists(const KppArgs& a, int t, int64_t j0,
       s_d[o] = f;
     }
   } else {
+    // the block's points in chunks of _euclidean_distances_upcast that all take the plain chain:
+    // the interleaved fast path of SEQ (only a call's small last chunk runs the edge kernels)
+    bool bseq = true;
+    {
+      const int64_t B = a.plan.B;
+      const int64_t s0 = j0 / B, s1 = min(n - 1, j0 + (int64_t)kBlk - 1) / B;
+      for (int64_t sc = s0; sc <= s1; ++sc) bseq = bseq && skl_chunk_seq(a.plan, min(B, n - sc * B));
+    }
+    if (bseq) {
+      double dot[kPer];
+      if (a.XT)
+        seq_dots_t(a.XT, a.dim, n, j0, s_c, dot);
+      else
+        seq_dots(a.X, a.dim, n, j0, s_c, dot);
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        const int o = tid + kThr * q;
+        const int64_t i = j0 + o;
+        float f = 0.f;
+        if (i < n) {
+          f = (float)(((-2.0 * dot[q]) + cn) + a.xsq[i]);
+          f = f < 0.f ? 0.f : f;
+          f = np_minimum(wrow[i], f);
+          drow[i] = f;
+        }
+        s_d[o] = f;
+      }
+      return;
+    }
 #pragma unroll 1
     for (int q = 0; q < kPer; ++q) {
       const int o = tid + kThr * q;
@@ -1524,7 +1602,8 @@ size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k) {
   b += 2 * align256(sizeof(int64_t) * T);     // candself
   b += 2 * align256(sizeof(int64_t) * T) + 2 * align256(sizeof(double) * T);  // candr, candn
   b += align256(sizeof(int) * 2) + align256(sizeof(unsigned) * (size_t)std::max(k, 1) * T);  // counters
-  if (n <= kBlk) b += align256(sizeof(float) * n * (size_t)std::max(dim, 1));  // XT
+  if (n <= kBlk || (int64_t)n * std::max(dim, 1) < INT_MAX)
+    b += align256(sizeof(float) * n * (size_t)std::max(dim, 1));  // XT
   return b + 1024;
 }
 
@@ -1562,7 +1641,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   for (int q = 0; q < 2; ++q) b1.candn[q] = cv.take<double>(T);
   b1.win = cv.take<int>(2);
   b1.counter = cv.take<unsigned>((size_t)std::min<int64_t>(n, INT_MAX) * T);
-  float* XT = n <= kBlk ? cv.take<float>((size_t)n * dim) : nullptr;
+  float* XT = (n <= kBlk || n * (int64_t)dim < INT_MAX) ? cv.take<float>((size_t)n * dim) : nullptr;
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans++: workspace too small");
   a.n = n;
   a.m1 = n & ~3ll;
@@ -1571,6 +1650,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   a.nblk = nblk;
   a.nsg = (int)((a.m1 + kBlk - 1) / kBlk);
   a.X = X;
+  a.XT = n > kBlk ? XT : nullptr;  // the single-block path keeps its own copy in b1
   a.w = w;
   a.xsq = xsq;
   a.closest0 = closest0;
@@ -1590,6 +1670,10 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
                          (const void*)k_kpp_round<false>};
     for (const void* f : fns)
       GDD_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  }
+  if (a.XT) {
+    k_kpp_xt<<<(unsigned)((n * dim + 255) / 256), 256, 0, s>>>((int)n, dim, X, XT);
+    GDD_LAUNCHED();
   }
   k_kpp_init<<<nblk, kThr, lds, s>>>(a, p1, first_id, xsq, closest0, fsum0);
   GDD_LAUNCHED();
