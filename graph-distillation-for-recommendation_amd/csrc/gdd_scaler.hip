@@ -13,6 +13,7 @@
 // One lane per column runs the ordered fp64 sums (eight rows' loads in flight ahead of the adds);
 // the transform is elementwise.
 #include <algorithm>
+#include <climits>
 
 #include "gdd_common.hpp"
 
@@ -97,6 +98,236 @@ extern "C" int gdd_standard_scaler_transform(int64_t n, int dim, const float* X,
   const int64_t total = n * (int64_t)dim;
   k_scale_rows<<<(unsigned)std::min<int64_t>((total + 255) / 256, 8192), 256, 0, s>>>(
       total, dim, X, mean, scale, X_out);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+// ---- KMeans.fit's centring (sklearn/cluster/_kmeans.py:1476-1487 via _tolerance :279-288):
+// X_mean = X.mean(axis=0); X -= X_mean; tol = mean(X.var(axis=0)) * tol, in numpy's summation order.
+//  * dim > 1: numpy reduces axis 0 of a C-contiguous float32 array row by row, so each column is a
+//    sequential fp32 chain; the quotient by n is rounded to fp32 (numpy divides by an intp in fp64
+//    then casts: identical, a double-rounded quotient is the correctly rounded one). var: sequential
+//    fp32 sum of (x - mean)^2 (subtract, square, add), over n.
+//  * dim == 1: the reduced axis is contiguous, so numpy runs its pairwise sum (umath
+//    loops_utils.h.src pairwise_sum: n < 8 sequential; n <= 128 eight interleaved accumulators
+//    combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the n % 8 tail; otherwise split at n/2 rounded
+//    down to a multiple of 8) over 8192-element buffer chunks whose results add in order to 0.
+namespace gdd {
+namespace {
+
+// dim > 1. Workgroup b owns columns [256 b, 256 b + w) and folds all rows of them twice (mean, then
+// (x - mean)^2 while writing x - mean): chunks of R = kColLds / w rows are staged through two LDS
+// buffers (element e of a chunk = row e / w, column e % w, so the LDS image is the chunk's linear
+// index) with the next chunk in flight in registers while thread j < w folds column j. The n-long
+// fp32 chains bound it, not HBM.
+constexpr int kColLds = 12288;        // floats per LDS buffer
+constexpr int kColP = kColLds / 256;  // staged elements per thread per chunk
+__global__ __launch_bounds__(256) void k_col_stats(int64_t n, int dim, const float* __restrict__ X,
+                                                   float* __restrict__ X_out, float* __restrict__ mean,
+                                                   float* __restrict__ var) {
+  extern __shared__ __attribute__((aligned(16))) float sb[];
+  const int tid = threadIdx.x;
+  const int c0 = blockIdx.x * 256, w = min(256, dim - c0);
+  const int R = kColLds / w;
+  int rel[kColP];  // chunk-relative offsets of this thread's staged elements: row * dim + c0 + column
+  {
+    int r = tid / w, col = tid % w;
+    const int dr = 256 / w, dc = 256 % w;
+#pragma unroll
+    for (int q = 0; q < kColP; ++q) {
+      rel[q] = r * dim + c0 + col;
+      r += dr;
+      col += dc;
+      if (col >= w) {
+        col -= w;
+        ++r;
+      }
+    }
+  }
+  float v[kColP];
+  auto fetch = [&](int64_t row0) {
+    const int64_t lim = min((int64_t)R, n - row0) * w;  // valid elements in this chunk
+    const float* base = X + row0 * dim;
+#pragma unroll
+    for (int q = 0; q < kColP; ++q)
+      if (tid + 256 * q < lim) v[q] = base[rel[q]];
+  };
+  float m = 0.f;
+  for (int pass = 0; pass < 2; ++pass) {
+    float acc = 0.f;
+    fetch(0);
+    int slot = 0;
+    for (int64_t row0 = 0; row0 < n; row0 += R) {
+      float* B = sb + slot * kColLds;
+      const int rows = (int)min((int64_t)R, n - row0);
+#pragma unroll
+      for (int q = 0; q < kColP; ++q)
+        if (tid + 256 * q < rows * w) B[tid + 256 * q] = v[q];
+      __syncthreads();
+      if (row0 + R < n) fetch(row0 + R);
+      if (tid < w) {
+        if (pass == 0) {
+          for (int r = 0; r < rows; ++r) acc = acc + B[r * w + tid];
+        } else {
+          float* o = X_out + row0 * dim + c0 + tid;
+          for (int r = 0; r < rows; ++r) {
+            const float d = B[r * w + tid] - m;
+            o[(int64_t)r * dim] = d;
+            acc = acc + d * d;
+          }
+        }
+      }
+      slot ^= 1;
+    }
+    if (tid < w) {
+      if (pass == 0) {
+        m = (float)((double)acc / (double)n);
+        mean[c0 + tid] = m;
+      } else {
+        var[c0 + tid] = (float)((double)acc / (double)n);
+      }
+    }
+    __syncthreads();  // both buffers are reused by the next pass
+  }
+}
+
+// numpy's pairwise leaf (len <= 128) over x (pass 0) or over (x - m)^2 (pass 1, which also writes
+// x - m).
+__device__ float pw_leaf(const float* __restrict__ a, float* __restrict__ o, int len, int pass, float m) {
+  auto val = [&](int i) {
+    const float x = a[i];
+    if (pass == 0) return x;
+    const float d = x - m;
+    o[i] = d;
+    return d * d;
+  };
+  if (len < 8) {
+    float res = 0.f;
+    for (int i = 0; i < len; ++i) res = res + val(i);
+    return res;
+  }
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = val(j);
+  int i = 8;
+  for (; i < len - (len % 8); i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = r[j] + val(i + j);
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < len; ++i) res = res + val(i);
+  return res;
+}
+
+// dim == 1: one wave. Per 8192-element chunk lane 0 lists the pairwise tree's leaves (left first),
+// the lanes sum the leaves, lane 0 combines them post-order (left + right at every split).
+constexpr int kPwChunk = 8192, kPwMaxLeaves = 128;  // a split of > 128 leaves halves >= 64 long
+__global__ __launch_bounds__(64) void k_col_stats_pw(int64_t n, const float* __restrict__ X,
+                                                     float* __restrict__ X_out, float* __restrict__ mean,
+                                                     float* __restrict__ var) {
+  __shared__ int loff[kPwMaxLeaves], llen[kPwMaxLeaves];
+  __shared__ float lsum[kPwMaxLeaves];
+  __shared__ int s_nl;
+  __shared__ float s_m;
+  __shared__ int sm[32], ss[32];
+  __shared__ float sl[32];
+  const int lane = threadIdx.x;
+  float m = 0.f;
+  for (int pass = 0; pass < 2; ++pass) {
+    float tot = 0.f;
+    for (int64_t c = 0; c < n; c += kPwChunk) {
+      const int len = (int)min((int64_t)kPwChunk, n - c);
+      if (lane == 0) {
+        int sp = 0, nl = 0, off = 0;
+        sm[sp++] = len;
+        while (sp > 0) {
+          const int mm = sm[--sp];
+          if (mm <= 128) {
+            loff[nl] = off;
+            llen[nl] = mm;
+            ++nl;
+            off += mm;
+          } else {
+            const int n2 = mm / 2 - (mm / 2) % 8;
+            sm[sp++] = mm - n2;
+            sm[sp++] = n2;
+          }
+        }
+        s_nl = nl;
+      }
+      __syncthreads();
+      for (int l = lane; l < s_nl; l += 64)
+        lsum[l] = pw_leaf(X + c + loff[l], X_out + c + loff[l], llen[l], pass, m);
+      __syncthreads();
+      if (lane == 0) {
+        int sp = 1, li = 0;
+        float ret = 0.f;
+        bool have = false;
+        sm[0] = len;
+        ss[0] = 0;
+        while (sp > 0) {
+          const int t = sp - 1;
+          if (have) {
+            if (ss[t] == 1) {  // left done: keep it, descend right
+              sl[t] = ret;
+              ss[t] = 2;
+              have = false;
+              const int n2 = sm[t] / 2 - (sm[t] / 2) % 8;
+              sm[sp] = sm[t] - n2;
+              ss[sp] = 0;
+              ++sp;
+            } else {  // right done
+              ret = sl[t] + ret;
+              --sp;
+            }
+            continue;
+          }
+          const int mm = sm[t];
+          if (mm <= 128) {
+            ret = lsum[li++];
+            --sp;
+            have = true;
+            continue;
+          }
+          ss[t] = 1;
+          sm[sp] = mm / 2 - (mm / 2) % 8;
+          ss[sp] = 0;
+          ++sp;
+        }
+        tot = tot + ret;
+      }
+      __syncthreads();
+    }
+    if (lane == 0) {
+      if (pass == 0) {
+        s_m = (float)((double)tot / (double)n);
+        mean[0] = s_m;
+      } else {
+        var[0] = (float)((double)tot / (double)n);
+      }
+    }
+    __syncthreads();
+    m = s_m;
+  }
+}
+
+}  // namespace
+}  // namespace gdd
+
+extern "C" int gdd_center_columns(int64_t n, int dim, const float* X, float* X_out, float* mean,
+                                  float* var, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && dim > 0 && X && X_out && mean && var, "center_columns: bad arguments");
+  GDD_REQUIRE((int64_t)(kColLds / std::min(dim, 256) + kColLds / 256) * dim < INT_MAX,
+              "center_columns: dim=%d too wide", dim);
+  hipStream_t s = to_hip(stream);
+  if (dim == 1) {
+    k_col_stats_pw<<<1, 64, 0, s>>>(n, X, X_out, mean, var);
+  } else {
+    const size_t lds = sizeof(float) * 2 * kColLds;
+    void (*kfn)(int64_t, int, const float*, float*, float*, float*) = gdd::k_col_stats;
+    GDD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+    k_col_stats<<<(unsigned)((dim + 255) / 256), 256, lds, s>>>(n, dim, X, X_out, mean, var);
+  }
   GDD_LAUNCHED();
   return GDD_OK;
 }

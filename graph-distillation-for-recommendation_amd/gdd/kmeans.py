@@ -399,21 +399,24 @@ class KMeans(_BaseKMeans):
 
     def fit(self, X, y=None, sample_weight=None):
         self._check_weights(sample_weight)
-        # host copy for the O(d) preprocessing sklearn does with numpy (mean, var -> tol)
-        if isinstance(X, torch.Tensor):
-            Xh = X.detach().cpu().numpy().astype(np.float32)
-        else:
-            Xh = np.array(X, dtype=np.float32, order="C", copy=True)
-        n, dim = Xh.shape
+        X0 = _as_device_f32(X, self.device)
+        n, dim = X0.shape
         k = self.n_clusters
         if k > n:
             raise ValueError(f"n_samples={n} should be >= n_clusters={k}.")
         rs = check_random_state(self.random_state)
-        X_mean = Xh.mean(axis=0)
-        Xh = Xh - X_mean
-        tol_ = 0 if self.tol == 0 else np.mean(np.var(Xh, axis=0)) * self.tol
-        Xd = _as_device_f32(Xh, self.device)
-        dev = Xd.device
+        dev = X0.device
+        # sklearn's centring and _tolerance on the device (numpy's sequential column sums): X - mean,
+        # mean and var of the INPUT (sklearn/cluster/_kmeans.py:1476-1487, :279-288)
+        Xd = torch.empty_like(X0)
+        mean_d = torch.empty(dim, dtype=torch.float32, device=dev)
+        var_d = torch.empty(dim, dtype=torch.float32, device=dev)
+        _lib.check(_lib.device_lib().gdd_center_columns(n, dim, X0.data_ptr(), Xd.data_ptr(),
+                                                        mean_d.data_ptr(), var_d.data_ptr(),
+                                                        _lib.stream_ptr(dev)))
+        X_mean = mean_d.cpu().numpy()
+        tol_ = 0 if self.tol == 0 else np.mean(var_d.cpu().numpy()) * self.tol
+        del X0
         ops = _Ops(dev, n, k, dim)
         lib = ops.lib
         stream = ops.stream
@@ -444,7 +447,7 @@ class KMeans(_BaseKMeans):
                                                    wic.data_ptr(), stream))
                 wic_h = wic.cpu().numpy()
                 if (wic_h == 0).any():
-                    self._relocate(Xh, C, C_new, wic, wic_h, labels)
+                    self._relocate(Xd.cpu().numpy(), C, C_new, wic, wic_h, labels)
                 _lib.check(lib.gdd_average_centers(k, dim, C_new.data_ptr(), wic.data_ptr(),
                                                    C.data_ptr(), shift.data_ptr(), stream))
                 _lib.check(lib.gdd_labels_changed(n, labels.data_ptr(), labels_old.data_ptr(),

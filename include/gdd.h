@@ -263,6 +263,11 @@ int gdd_skl_sqdist(int n_rows, const float* C, int64_t n, int dim, const float* 
 /* ---------------------------------------------------------------------------------------------- */
 int gdd_standard_scaler(int64_t n, int dim, const float* X, float* X_out, double* mean,
                         double* scale, gdd_stream_t stream);
+/* KMeans.fit's centring (sklearn/cluster/_kmeans.py:1476-1487, _tolerance :279-288): mean = X.mean(0), */
+/* var = X.var(0) (numpy: sequential fp32 column sums over the rows, quotient by n rounded to fp32), */
+/* X_out = X - mean (fp32). mean/var: dim floats. X_out may not alias X.                           */
+int gdd_center_columns(int64_t n, int dim, const float* X, float* X_out, float* mean, float* var,
+                       gdd_stream_t stream);
 /* StandardScaler.transform with a fitted mean/scale (utils_graphsaint.py:41-44 fits on the train   */
 /* rows and transforms every row): X_out = fp32(fp32(x - mean) / scale).                            */
 int gdd_standard_scaler_transform(int64_t n, int dim, const float* X, const double* mean,

@@ -362,9 +362,9 @@ def kmeans(X, n_clusters: int, random_state=None, n_init="auto", max_iter: int =
     k = n_clusters
     rs = _check_random_state(random_state)
     n_init_ = 1 if n_init == "auto" else int(n_init)
+    tol_ = 0 if tol == 0 else np.mean(np.var(X, axis=0)) * tol  # _tolerance on the input (:279-288)
     X_mean = X.mean(axis=0)
     X -= X_mean
-    tol_ = 0 if tol == 0 else np.mean(np.var(X, axis=0)) * tol
     best = None
     for _ in range(n_init_):
         centers, _ = kmeans_plusplus(X, k, rs)

@@ -226,3 +226,21 @@ def test_segment_sum_f32_sequential(n, dim, k, weighted):
         wref[c] = np.add.accumulate(wt, dtype=np.float32)[-1]
     assert np.array_equal(sums.cpu().numpy().view(np.uint32), ref.view(np.uint32))
     assert np.array_equal(wsum.cpu().numpy().view(np.uint32), wref.view(np.uint32))
+
+
+@pytest.mark.parametrize("n,dim", [(1, 3), (1000, 7), (100000, 47), (20000, 64), (333, 5), (777, 300),
+                                   (2000, 600), (5, 1), (64, 1), (129, 1), (8192, 1), (30001, 1)])
+def test_center_columns_matches_numpy(n, dim):
+    # KMeans.fit's X.mean(axis=0), X - mean and X.var(axis=0) (sklearn _tolerance) bit for bit
+    rng = np.random.default_rng(n + dim)
+    X = (rng.standard_normal((n, dim)) * 3 + 1).astype(np.float32)
+    Xd = torch.from_numpy(X).cuda()
+    out = torch.empty_like(Xd)
+    mean = torch.empty(dim, dtype=torch.float32, device="cuda")
+    var = torch.empty(dim, dtype=torch.float32, device="cuda")
+    _lib.check(_lib.device_lib().gdd_center_columns(n, dim, Xd.data_ptr(), out.data_ptr(), mean.data_ptr(),
+                                                    var.data_ptr(), _lib.stream_ptr("cuda")))
+    m = X.mean(axis=0)
+    assert np.array_equal(mean.cpu().numpy().view(np.uint32), m.view(np.uint32))
+    assert np.array_equal(var.cpu().numpy().view(np.uint32), np.var(X, axis=0).view(np.uint32))
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), (X - m).view(np.uint32))
