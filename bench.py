@@ -40,8 +40,6 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="arxiv")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=60,
-                    help="minibatch steps the CPU baseline sample runs (extrapolated)")
     return ap.parse_args()
 
 
@@ -178,7 +176,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, A, X_h, args.cpu_steps, n_steps_km[-1])
+        out["cpu_baseline"] = cpu_baseline(cfg, A, X_h)
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
@@ -222,41 +220,91 @@ def pmc_traffic():
     return rec.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(cfg, A, X_h, cpu_steps, gpu_km_steps):
-    """The oracle (single-threaded C restatement) on a bounded sample of the same workload:
-    full normalise + propagation, k-means++ + `cpu_steps` minibatch steps (extrapolated to the
-    step count the GPU run took) + full labels pass + cluster means."""
-    sys.path.insert(0, ROOT)
-    from oracle import oracle as O
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg, A, X_h):
+    """The reference's own CPU path, whole step, no extrapolation: the library calls
+    ClustGDD.pretrained_clustering makes, on the same synthetic inputs, with every host core the
+    process may use —
+      * normalize_adj_tensor(sparse=True) (deep_robust_utils.py:180-207, 245-256): scipy, A + I only
+        if A[0,0] == 0, D^-1/2 (A+I) D^-1/2 in fp64, cast to an fp32 torch sparse COO tensor;
+      * the propagation loop (clustgdd_agent_transduct.py:59-65): torch CPU sparse `@`, T-1 hops;
+      * the logits (the MLP stand-in: one fp32 GEMM, as on the GPU);
+      * MiniBatchKMeans(n_clusters=k, random_state=seed, batch_size=1000).fit (transduct:102-103),
+        scikit-learn with its OpenMP/BLAS threads;
+      * the cluster-mean loop (transduct:116-127): target[torch.where(labels == i)[0]].mean(0) per i.
+    """
     import scipy.sparse as sp
-    from gdd import synth
-    A = sp.csr_matrix(A)
+    from sklearn.cluster import MiniBatchKMeans
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    try:
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(limits=threads)
+    except ImportError:  # pragma: no cover
+        limiter = None
+    A = sp.coo_matrix(A, dtype=np.float32)
+    n = A.shape[0]
+    # the agent's adjacency arrives as a torch sparse COO tensor (to_tensor, deep_robust_utils.py:85-113)
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.vstack((A.row, A.col)).astype(np.int64)),
+                                  torch.from_numpy(A.data), (n, n))
     t0 = time.perf_counter()
-    ro, co, vo = O.normalize_csr(A.indptr, A.indices, None, -1)
-    target, _ = O.propagate(ro, co, vo, X_h, cfg.T, cfg.alpha)
-    t_graph = time.perf_counter() - t0
-    rng = np.random.default_rng(cfg.seed + 3)
-    W = (rng.standard_normal((cfg.d, cfg.n_classes)) / np.sqrt(cfg.d)).astype(np.float32)
-    b = (rng.standard_normal(cfg.n_classes) * 0.1).astype(np.float32)
-    logits = target @ W + b
+    # normalize_adj_tensor(adj, sparse=True): to_scipy (CSR from the COO values/indices), then
+    # normalize_adj on a LIL matrix (A + I only if A[0,0] == 0; fp64 row sums; inf -> 0; two diagonal
+    # scalings), then back to an fp32 torch COO tensor (sparse_mx_to_torch_sparse_tensor)
+    vals, ind = adj._values().numpy(), adj._indices().numpy()
+    M = sp.csr_matrix((vals, ind), shape=(n, n)).tolil()
+    if M[0, 0] == 0:
+        M = M + sp.eye(n)
+    deg = np.array(M.sum(1))
+    with np.errstate(divide="ignore"):
+        r = np.power(deg, -0.5).flatten()
+    r[np.isinf(r)] = 0.0
+    D = sp.diags(r)
+    M = D.dot(M).dot(D).tocoo().astype(np.float32)
+    idx = torch.cat((torch.LongTensor(M.row).unsqueeze(1), torch.LongTensor(M.col).unsqueeze(1)), 1)
+    adj_norm = torch.sparse_coo_tensor(idx.t(), torch.FloatTensor(M.data), (n, n))
     t1 = time.perf_counter()
-    res = O.minibatch_kmeans(logits, cfg.k, random_state=cfg.seed, batch_size=cfg.batch,
-                             max_iter=max(1, (cpu_steps * cfg.batch) // cfg.n + 1),
-                             compute_labels=False)
-    t_km_sample = time.perf_counter() - t1
-    steps_done = res["n_steps_"]
+    feats = torch.from_numpy(X_h)
+    prop = feats
+    target = (1 - cfg.alpha) * prop
+    for _ in range(1, cfg.T):
+        prop = cfg.alpha * adj_norm @ prop
+        target = target + (1 - cfg.alpha) * prop
     t2 = time.perf_counter()
-    labels, _ = O.labels_inertia(logits, res["cluster_centers_"])
-    O.cluster_mean(target, labels, cfg.k)
-    t_tail = time.perf_counter() - t2
-    # extrapolate the minibatch loop to the GPU run's step count (the init is paid once)
-    t_est = t_graph + t_km_sample * max(gpu_km_steps, 1) / max(steps_done, 1) + t_tail
-    sample_s = t_graph + t_km_sample + t_tail
-    return {"value": cfg.n / t_est, "unit": "nodes/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/ C restatement, 1 thread: normalise + {cfg.T - 1} hops on the full "
-                      f"graph, k-means++ and {steps_done} of {gpu_km_steps} minibatch steps "
-                      f"(extrapolated), full labels pass + cluster means; {sample_s:.1f} s measured",
-            "est_seconds_per_step": t_est}
+    rng = np.random.default_rng(cfg.seed + 3)
+    W = torch.from_numpy((rng.standard_normal((cfg.d, cfg.n_classes)) / np.sqrt(cfg.d)).astype(np.float32))
+    b = torch.from_numpy((rng.standard_normal(cfg.n_classes) * 0.1).astype(np.float32))
+    logits = torch.addmm(b, target, W).numpy()
+    t3 = time.perf_counter()
+    km = MiniBatchKMeans(n_clusters=cfg.k, random_state=cfg.seed, batch_size=cfg.batch).fit(logits)
+    t4 = time.perf_counter()
+    lab = torch.from_numpy(km.labels_.astype(np.int64))
+    feat_syn = torch.stack([target[torch.where(lab == i)[0]].mean(dim=0) for i in range(cfg.k)])
+    labels_syn = torch.argmax(torch.from_numpy(km.cluster_centers_), dim=-1)
+    t5 = time.perf_counter()
+    del feat_syn, labels_syn
+    if limiter is not None:
+        limiter.unregister() if hasattr(limiter, "unregister") else None
+    total = t5 - t0
+    return {"value": n / total, "unit": "nodes/s", "cores": threads, "kind": "reference-library",
+            "cpu_model": _cpu_model(),
+            "sample": (f"one whole step of the reference's CPU path on the bench's graph ({n} nodes): "
+                       f"scipy normalize_adj, {cfg.T - 1} torch CPU sparse hops, logits GEMM, sklearn "
+                       f"MiniBatchKMeans(k={cfg.k}, b={cfg.batch}, seed {cfg.seed}, {km.n_steps_} steps), "
+                       f"torch where/mean loop; {threads} threads; {total:.1f} s measured"),
+            "seconds_per_step": total,
+            "stages_s": {"normalize": t1 - t0, "propagate": t2 - t1, "logits": t3 - t2,
+                         "minibatch_kmeans": t4 - t3, "cluster_mean": t5 - t4}}
 
 
 if __name__ == "__main__":

@@ -91,6 +91,43 @@ int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const 
                        size_t step_ws_bytes, const DevMT* mt_in, DevMT* mt_mid, const RngNext& rn,
                        void* state, hipStream_t s);
 
+// internal entry point of the k-means assignment (gdd_kmeans.hip), used by the Lloyd loop
+// (gdd_lloyd.hip): ||C||² into cn2, then labels of all n rows; every kernel skips once `stop`
+// says step `step_i` lies past the stopping decision (see stopped()).
+int kmeans_assign_dev(int64_t n, int dim, const float* X, int k, const float* C, float* cn2,
+                      int32_t* labels, unsigned long long* keys, const int32_t* stop, int step_i,
+                      hipStream_t s);
+
+// `stop` (nullable) points at a device stop word (0 = running, s+1 = a test fired at step s; the
+// MiniBatch MBState::stop_at, the Lloyd LloydState::stop_at). Kernels of a later step return at
+// once, so the host can enqueue steps ahead of the stopping decision. One 32-bit word read with an
+// agent-scope atomic load: the test written by a sibling block of the same launch is never seen
+// torn, and step s itself always completes.
+__device__ __forceinline__ bool stopped(const int32_t* stop, int step_i) {
+  if (!stop) return false;
+  const int v = __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return v != 0 && v - 1 < step_i;
+}
+
+// sklearn _euclidean_dense_dense(a, b, n_features, squared=True) (_k_means_common.pyx:26-48):
+// groups of 4 summed left to right, added to the running result; remainder added one by one.
+// Separate mul/add (no fma).
+__device__ __forceinline__ float skl_sqdist(const float* __restrict__ a, const float* __restrict__ b,
+                                            int dim) {
+  float r = 0.f;
+  int j = 0;
+  for (; j + 4 <= dim; j += 4) {
+    float d0 = a[j] - b[j], d1 = a[j + 1] - b[j + 1], d2 = a[j + 2] - b[j + 2],
+          d3 = a[j + 3] - b[j + 3];
+    r = r + (((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
+  }
+  for (; j < dim; ++j) {
+    float d0 = a[j] - b[j];
+    r = r + d0 * d0;
+  }
+  return r;
+}
+
 // ---------------------------------------------------------------------------------------------
 // numerics shared by kernels and documented in DESIGN.md
 // ---------------------------------------------------------------------------------------------

@@ -420,9 +420,12 @@ extern "C" int gdd_minibatch_kmeans_fit(
                              hipMemcpyDeviceToHost, s));
       GDD_HIP(hipStreamSynchronize(s));
       if (h_flag[0]) stop_step = h_flag[0] - 1;
-    } else if (!synced) {
+    } else {
+      // also after a reassignment step's sync: its H2D copies out of the caller's pinned staging
+      // (h_pairs, h_counts) are still queued, and that buffer may be reused once we return
       GDD_HIP(hipStreamSynchronize(s));
     }
+    (void)synced;
     if (stop_step >= 0 && stop_step < i + m - 1) {
       // sklearn drew batch indices only up to the stopping step: rewind the generator
       *static_cast<MTState*>(rng_state) = snapshot;

@@ -53,39 +53,11 @@ __device__ __forceinline__ float npy_sumsq(const float* __restrict__ x, int dim)
   return (a[0] + a[1]) + (a[2] + a[3]);
 }
 
-// `stop` (nullable) points at MBState::stop_at (0 = running, s+1 = the convergence test fired at
-// step s). Kernels of a later step return at once, so the host can enqueue steps ahead of the
-// stopping decision. One 32-bit word read with an agent-scope atomic load: the test written by a
-// sibling block of the same launch is never seen torn, and step s itself always completes.
-__device__ __forceinline__ bool stopped(const int32_t* stop, int step_i) {
-  if (!stop) return false;
-  const int v = __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return v != 0 && v - 1 < step_i;
-}
-
 __global__ void k_row_norms(int64_t n, int dim, const float* __restrict__ X, float* __restrict__ out,
                             const int32_t* __restrict__ stop, int step_i) {
   if (stopped(stop, step_i)) return;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = npy_sumsq(X + i * dim, dim);
-}
-
-// sklearn _euclidean_dense_dense(a, b, n_features, squared=True): groups of 4 summed left to right,
-// added to the running result; remainder added one by one. Separate mul/add (no fma).
-__device__ __forceinline__ float skl_sqdist(const float* __restrict__ a, const float* __restrict__ b,
-                                            int dim) {
-  float r = 0.f;
-  int j = 0;
-  for (; j + 4 <= dim; j += 4) {
-    float d0 = a[j] - b[j], d1 = a[j + 1] - b[j + 1], d2 = a[j + 2] - b[j + 2],
-          d3 = a[j + 3] - b[j + 3];
-    r = r + (((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
-  }
-  for (; j < dim; ++j) {
-    float d0 = a[j] - b[j];
-    r = r + d0 * d0;
-  }
-  return r;
 }
 
 // skl_sqdist with a 16-byte-aligned global `a`, dim % 4 == 0: the row is fetched as float4, eight
@@ -1105,119 +1077,8 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
 }
 
 // ---------------------------------------------------------------------------------------------
-// grouping: offsets from sorted labels
+// fixed-point per-cluster sums (the order-free sharded variant, gdd/sharded.py)
 // ---------------------------------------------------------------------------------------------
-__global__ void k_iota(int64_t n, int32_t* p) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) p[i] = (int32_t)i;
-}
-
-__global__ void k_offsets(int64_t n, const int32_t* __restrict__ skeys, int k,
-                          int32_t* __restrict__ offsets) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i > n) return;
-  // offsets[c] = first sorted position with key >= c
-  const int prev = (i == 0) ? -1 : skeys[i - 1];
-  const int cur = (i == n) ? k : skeys[i];
-  for (int c = prev + 1; c <= cur && c <= k; ++c) offsets[c] = (int32_t)i;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Lloyd accumulation (sequential per cluster, sample order) and fixed-point variant
-// ---------------------------------------------------------------------------------------------
-// One workgroup per cluster, its members (perm[offsets[c] .. offsets[c+1]), sample order) in
-// chunks of R rows staged through two LDS buffers: while thread f folds chunk i's column f as a
-// sequential fp32 chain (sum + X*w, separate mul and add), chunk i+1's rows are in flight into
-// registers, and chunk i+2's member ids too (so no chunk waits for the perm -> X round trip twice).
-// Staging map: !WIDE (dim <= 256): thread t loads feature t % dim of rows t / dim + q * rpp
-// (rpp = 256 / dim rows per pass, 48 passes); WIDE: features t and t + 256 of rows q (24 passes).
-// Weights (or unit counts) fold in the same order by a spare thread (dim < 256) or thread 0.
-constexpr int kSegLds = 12288;  // floats per LDS buffer (48 KiB)
-template <bool WIDE>
-__global__ __launch_bounds__(256) void k_segment_sum_f32(int dim, const float* __restrict__ X,
-                                                         const float* __restrict__ w,
-                                                         const int32_t* __restrict__ perm,
-                                                         const int32_t* __restrict__ offsets,
-                                                         float* __restrict__ sums,
-                                                         float* __restrict__ wsum) {
-  constexpr int P = WIDE ? 24 : 48;  // rows per thread per chunk
-  extern __shared__ __attribute__((aligned(16))) float sbuf[];
-  const int c = blockIdx.x, tid = threadIdx.x;
-  const int32_t b = offsets[c], e = offsets[c + 1];
-  const int rpp = WIDE ? 1 : 256 / dim;
-  const int R = min(rpp * P, 1024);  // R * dim <= kSegLds
-  const int f0 = WIDE ? tid : tid % dim;
-  const int r0 = WIDE ? 0 : tid / dim;
-  const bool st_on = WIDE || r0 < rpp;
-  auto buf_of = [&](int slot) { return sbuf + slot * kSegLds; };
-  auto wbuf_of = [&](int slot) { return sbuf + 2 * kSegLds + slot * 1024; };
-  float v[WIDE ? 2 * P : P];
-  int32_t pa[P], pb[P];
-  auto fetch_ids = [&](int32_t m0, int32_t(&dst)[P]) {
-    const int32_t last = max(min(e - m0, R) - 1, 0);
-#pragma unroll
-    for (int q = 0; q < P; ++q) dst[q] = perm[m0 + min(r0 + q * rpp, last)];
-  };
-  auto fetch_x = [&](const int32_t(&ids)[P]) {
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const int64_t i = ids[q];
-      v[q] = X[i * dim + f0];
-      if constexpr (WIDE) v[P + q] = X[i * dim + min(f0 + 256, dim - 1)];
-    }
-  };
-  auto store = [&](int slot, int32_t m0) {
-    if (!st_on) return;
-    const int rows = min(e - m0, R);
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const int r = r0 + q * rpp;
-      if (r < rows) {
-        buf_of(slot)[r * dim + f0] = v[q];
-        if constexpr (WIDE)
-          if (f0 + 256 < dim) buf_of(slot)[r * dim + f0 + 256] = v[P + q];
-      }
-    }
-  };
-  float acc0 = 0.f, acc1 = 0.f, wacc = 0.f;
-  if (b < e) {
-    fetch_ids(b, pa);
-    fetch_x(pa);
-    if (b + R < e) fetch_ids(b + R, pb);
-  }
-  int slot = 0;
-  for (int32_t m0 = b; m0 < e; m0 += R) {
-    const int rows = min(R, e - m0);
-    store(slot, m0);
-    for (int r = tid; r < rows; r += 256) wbuf_of(slot)[r] = w ? w[perm[m0 + r]] : 1.0f;
-    __syncthreads();
-    if (m0 + R < e) {
-      fetch_x(pb);                                   // chunk i+1's rows (ids already here)
-      if (m0 + 2 * R < e) fetch_ids(m0 + 2 * R, pb);  // chunk i+2's ids
-    }
-    const float* B = buf_of(slot);
-    const float* W = wbuf_of(slot);
-    if (tid < dim)
-      for (int r = 0; r < rows; ++r) acc0 = acc0 + B[r * dim + tid] * W[r];
-    if (WIDE && tid + 256 < dim)
-      for (int r = 0; r < rows; ++r) acc1 = acc1 + B[r * dim + tid + 256] * W[r];
-    if (!WIDE && dim < 256 && tid == 255)  // a spare thread folds the weights
-      for (int r = 0; r < rows; ++r) wacc = wacc + W[r];
-    slot ^= 1;
-  }
-  if (tid < dim) sums[(int64_t)c * dim + tid] = acc0;
-  if (WIDE && tid + 256 < dim) sums[(int64_t)c * dim + tid + 256] = acc1;
-  if (dim >= 256) {  // no spare thread: fold the weights after
-    if (tid == 0) {
-      float s2 = 0.f;
-      for (int32_t t = b; t < e; ++t) s2 = s2 + (w ? w[perm[t]] : 1.0f);
-      wsum[c] = s2;
-    }
-  } else if (tid == 255) {
-    wsum[c] = wacc;
-  }
-}
-
 __global__ void k_segment_sum_fixed(int64_t n, int dim, const float* __restrict__ X,
                                     const float* __restrict__ w, const int32_t* __restrict__ labels,
                                     int scale_exp, long long* __restrict__ sums,
@@ -1248,26 +1109,6 @@ __global__ void k_fixed_to_centers(int k, int dim, const long long* __restrict__
   }
 }
 
-// _average_centers + _center_shift, one block per cluster
-__global__ void k_average_centers(int k, int dim, float* __restrict__ C_new,
-                                  const float* __restrict__ wsum, const float* __restrict__ C_old,
-                                  float* __restrict__ shift, int argmax_w) {
-  const int c = blockIdx.x;
-  const float wc = wsum[c];
-  const int64_t cb = (int64_t)c * dim;
-  if (wc > 0.f) {
-    const float alpha = (float)(1.0 / (double)wc);  // `1.0 / weight` is a C double division
-    for (int f = threadIdx.x; f < dim; f += blockDim.x) C_new[cb + f] = C_new[cb + f] * alpha;
-  } else {
-    // sklearn copies centers[argmax_weight] (already averaged or not, by loop order); the host only
-    // takes this path after relocation left no empty cluster, so it is effectively unreachable
-    const int64_t ab = (int64_t)argmax_w * dim;
-    for (int f = threadIdx.x; f < dim; f += blockDim.x) C_new[cb + f] = C_new[ab + f];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 && shift) shift[c] = sqrtf(skl_sqdist(C_new + cb, C_old + cb, dim));
-}
-
 __global__ void k_point_center_sqdist(int64_t n, int dim, const float* __restrict__ X,
                                       const int32_t* __restrict__ labels,
                                       const float* __restrict__ C, float* __restrict__ out) {
@@ -1276,51 +1117,7 @@ __global__ void k_point_center_sqdist(int64_t n, int dim, const float* __restric
   out[i] = skl_sqdist(X + i * dim, C + (int64_t)labels[i] * dim, dim);
 }
 
-__global__ void k_labels_changed(int64_t n, const int32_t* __restrict__ labels,
-                                 int32_t* __restrict__ old, int32_t* __restrict__ changed) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int32_t a = labels[i];
-  if (a != old[i]) {
-    *changed = 1;
-    old[i] = a;
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// cluster feature mean (fp64 sequential per cluster, sample order) and row argmax
-// ---------------------------------------------------------------------------------------------
-__global__ void k_cluster_mean(int d, const float* __restrict__ feat, const int32_t* __restrict__ perm,
-                               const int32_t* __restrict__ offsets, int empty_as_zero,
-                               float* __restrict__ out, long long* __restrict__ counts) {
-  const int c = blockIdx.y;
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  const int32_t b = offsets[c], e = offsets[c + 1];
-  if (f == 0 && counts) counts[c] = e - b;
-  if (f >= d) return;
-  double acc = 0.0;
-  int32_t t = b;
-  // 4 independent gathers in flight ahead of the (ordered) fp64 adds
-  for (; t + 4 <= e; t += 4) {
-    const float v0 = feat[(int64_t)perm[t] * d + f];
-    const float v1 = feat[(int64_t)perm[t + 1] * d + f];
-    const float v2 = feat[(int64_t)perm[t + 2] * d + f];
-    const float v3 = feat[(int64_t)perm[t + 3] * d + f];
-    acc = acc + (double)v0;
-    acc = acc + (double)v1;
-    acc = acc + (double)v2;
-    acc = acc + (double)v3;
-  }
-  for (; t < e; ++t) acc = acc + (double)feat[(int64_t)perm[t] * d + f];
-  const int32_t cnt = e - b;
-  float r;
-  if (cnt == 0)
-    r = empty_as_zero ? 0.f : __builtin_nanf("");
-  else
-    r = (float)(acc / (double)cnt);
-  out[(int64_t)c * d + f] = r;
-}
-
+// row argmax (torch.argmax of the centres, transduct:126)
 __global__ void k_argmax_rows(int k, int dim, const float* __restrict__ C, int64_t* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= k) return;
@@ -1492,6 +1289,16 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
   return GDD_OK;
 }
 }  // namespace
+
+namespace gdd {
+int kmeans_assign_dev(int64_t n, int dim, const float* X, int k, const float* C, float* cn2,
+                      int32_t* labels, unsigned long long* keys, const int32_t* stop, int step_i,
+                      hipStream_t s) {
+  k_row_norms<<<blocks_for(k), 256, 0, s>>>(k, dim, C, cn2, stop, step_i);
+  GDD_LAUNCHED();
+  return launch_assign(n, dim, X, nullptr, k, C, cn2, labels, nullptr, keys, stop, step_i, s);
+}
+}  // namespace gdd
 
 extern "C" size_t gdd_kmeans_assign_ws_bytes(int64_t n) {
   return align256(sizeof(unsigned long long) * (size_t)std::max<int64_t>(n, 1));
@@ -1762,53 +1569,6 @@ extern "C" int gdd_minibatch_converge(int64_t b, int k, int step_i, int64_t n_sa
   return GDD_OK;
 }
 
-extern "C" size_t gdd_group_ws_bytes(int64_t n, int k) {
-  (void)k;
-  return align256(sizeof(int32_t) * (size_t)n) * 2 + sort_pairs_ws_bytes(n) + 1024;
-}
-
-extern "C" int gdd_group_by_label(int64_t n, const int32_t* labels, int k, int32_t* perm,
-                                  int32_t* offsets, void* ws, size_t ws_bytes,
-                                  gdd_stream_t stream) {
-  GDD_REQUIRE(n > 0 && k > 0 && labels && perm && offsets && ws, "group_by_label: bad arguments");
-  hipStream_t s = to_hip(stream);
-  Carver cv(ws, ws_bytes);
-  int32_t* iota = cv.take<int32_t>(n);
-  int32_t* skeys = cv.take<int32_t>(n);
-  size_t sb = sort_pairs_ws_bytes(n);
-  void* sws = cv.take<char>(sb);
-  if (!cv.ok()) return fail(GDD_E_WORKSPACE, "group_by_label: workspace too small");
-  int bits = 1;
-  while ((1ll << bits) < (long long)k) ++bits;
-  k_iota<<<blocks_for(n), 256, 0, s>>>(n, iota);
-  GDD_LAUNCHED();
-  int rc = sort_pairs_i32(labels, skeys, iota, perm, n, bits, sws, sb, s);
-  if (rc) return rc;
-  k_offsets<<<blocks_for(n + 1), 256, 0, s>>>(n, skeys, k, offsets);
-  GDD_LAUNCHED();
-  return GDD_OK;
-}
-
-extern "C" int gdd_segment_sum_f32(int64_t n, int dim, const float* X, const float* w,
-                                   const int32_t* perm, const int32_t* offsets, int k, float* sums,
-                                   float* wsum, gdd_stream_t stream) {
-  GDD_REQUIRE(n > 0 && dim > 0 && k > 0 && X && perm && offsets && sums && wsum,
-              "segment_sum_f32: bad arguments");
-  GDD_REQUIRE(dim <= 512, "segment_sum_f32: dim=%d > 512", dim);
-  const size_t lds = sizeof(float) * (2 * kSegLds + 2048);
-  if (dim > 256) {
-    GDD_HIP(hipFuncSetAttribute((const void*)k_segment_sum_f32<true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    k_segment_sum_f32<true><<<k, 256, lds, to_hip(stream)>>>(dim, X, w, perm, offsets, sums, wsum);
-  } else {
-    GDD_HIP(hipFuncSetAttribute((const void*)k_segment_sum_f32<false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    k_segment_sum_f32<false><<<k, 256, lds, to_hip(stream)>>>(dim, X, w, perm, offsets, sums, wsum);
-  }
-  GDD_LAUNCHED();
-  return GDD_OK;
-}
-
 extern "C" int gdd_segment_sum_fixed(int64_t n, int dim, const float* X, const float* w,
                                      const int32_t* labels, int k, int scale_exp,
                                      long long* sums_fx, long long* counts, gdd_stream_t stream) {
@@ -1834,41 +1594,10 @@ extern "C" int gdd_fixed_to_centers(int k, int dim, const long long* sums_fx,
   return GDD_OK;
 }
 
-extern "C" int gdd_average_centers(int k, int dim, float* C_new, const float* wsum,
-                                   const float* C_old, float* center_shift, gdd_stream_t stream) {
-  GDD_REQUIRE(k > 0 && dim > 0 && C_new && wsum && C_old, "average_centers: bad arguments");
-  k_average_centers<<<k, 64, 0, to_hip(stream)>>>(k, dim, C_new, wsum, C_old, center_shift, 0);
-  GDD_LAUNCHED();
-  return GDD_OK;
-}
-
 extern "C" int gdd_point_center_sqdist(int64_t n, int dim, const float* X, const int32_t* labels,
                                        const float* C, float* out, gdd_stream_t stream) {
   GDD_REQUIRE(n > 0 && dim > 0 && X && labels && C && out, "point_center_sqdist: bad arguments");
   k_point_center_sqdist<<<blocks_for(n), 256, 0, to_hip(stream)>>>(n, dim, X, labels, C, out);
-  GDD_LAUNCHED();
-  return GDD_OK;
-}
-
-extern "C" int gdd_labels_changed(int64_t n, const int32_t* labels, int32_t* labels_old,
-                                  int32_t* changed, gdd_stream_t stream) {
-  GDD_REQUIRE(n > 0 && labels && labels_old && changed, "labels_changed: bad arguments");
-  hipStream_t s = to_hip(stream);
-  GDD_HIP(hipMemsetAsync(changed, 0, sizeof(int32_t), s));
-  k_labels_changed<<<blocks_for(n), 256, 0, s>>>(n, labels, labels_old, changed);
-  GDD_LAUNCHED();
-  return GDD_OK;
-}
-
-extern "C" int gdd_cluster_mean(int64_t n, int d, const float* feat, const int32_t* perm,
-                                const int32_t* offsets, int k, int empty_as_zero, float* feat_syn,
-                                long long* counts, gdd_stream_t stream) {
-  GDD_REQUIRE(n > 0 && d > 0 && k > 0 && feat && perm && offsets && feat_syn,
-              "cluster_mean: bad arguments");
-  GDD_REQUIRE(k < 65536, "cluster_mean: k=%d too large", k);
-  dim3 grid((unsigned)((d + 127) / 128), (unsigned)k);
-  k_cluster_mean<<<grid, 128, 0, to_hip(stream)>>>(d, feat, perm, offsets, empty_as_zero, feat_syn,
-                                                   counts);
   GDD_LAUNCHED();
   return GDD_OK;
 }

@@ -1,0 +1,772 @@
+// gdd_lloyd.hip — (a6/a7/a8) grouping by label, ordered per-cluster folds, and the device-resident
+// Lloyd loop of sklearn KMeans.fit.
+//
+// What is restated:
+//   Lloyd M-step      _k_means_lloyd.pyx:111-160 with one OpenMP thread: per cluster, a sequential
+//                     fp32 chain `sum + x*w` over its members in sample order; weight sums likewise
+//   relocation input  _k_means_common.pyx:124-164 `((X - centers_old[labels])**2).sum(axis=1)`:
+//                     numpy's pairwise sum over each contiguous row (gdd_relocate_distances)
+//   average / shift   _k_means_common.pyx:215-251 `_average_centers` (empty clusters copy the FIRST
+//                     heaviest cluster's row, averaged or not by loop order) and `_center_shift`
+//   convergence       sklearn/cluster/_kmeans.py:717-734: strict label equality first, then
+//                     `(center_shift**2).sum() <= tol` (numpy pairwise fp32 sum, compared in fp64)
+//   cluster mean      clustgdd_agent_transduct.py:116-125 (`mean` of the members' rows): fp64 sum
+//                     in sample order, one division, one rounding to fp32; empty -> NaN (or 0 for
+//                     distill_recsys.py:623-636's clamp_min(1) means)
+//
+// Grouping is a stable counting sort: per wave-tile label histograms (LDS), one exclusive scan of
+// the cluster-major histogram matrix, then each wave re-reads its tile and places every label at
+// its cluster's running offset + its rank among equal labels of the same 64-label chunk (ballot
+// match over the label bits). Sample order within a cluster is therefore preserved, which is what
+// the ordered folds need.
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstddef>
+
+#include "gdd_common.hpp"
+
+namespace gdd {
+namespace {
+
+inline unsigned blocks_of(int64_t n, int t = 256) { return (unsigned)((n + t - 1) / t); }
+
+// ---------------------------------------------------------------------------------------------
+// stable counting sort of labels
+// ---------------------------------------------------------------------------------------------
+constexpr int kTileUnit = 1024;   // labels per wave per tile unit (16 per lane)
+constexpr int kCountMaxK = 32768;  // LDS: (waves per block) x k int32 counters
+
+struct GroupPlan {
+  int m;           // tile = m * 1024 labels, one wave each
+  int64_t ntiles;  // columns of the cluster-major histogram matrix
+  int waves;       // waves per 256-lane block (each has its own k counters in LDS)
+};
+
+GroupPlan group_plan(int64_t n, int k) {
+  GroupPlan p;
+  p.m = (int)std::min<int64_t>(4, std::max<int64_t>(1, (n + (1 << 20) - 1) >> 20));
+  p.ntiles = std::max<int64_t>(1, (n + (int64_t)p.m * kTileUnit - 1) / ((int64_t)p.m * kTileUnit));
+  p.waves = k <= 4096 ? 4 : 1;
+  return p;
+}
+
+template <int M>
+__device__ __forceinline__ void load_tile(int64_t n, const int32_t* __restrict__ labels, int64_t base,
+                                          int lane, int32_t (&lv)[M * 16]) {
+#pragma unroll
+  for (int q = 0; q < M * 16; ++q) {
+    const int64_t i = base + (int64_t)q * 64 + lane;
+    lv[q] = i < n ? labels[i] : -1;
+  }
+}
+
+// per-tile histogram column: ghist[c * ntiles + t] = #{i in tile t : labels[i] == c}; labels outside
+// [0, k) are not counted (they belong to no cluster, as in the reference's `labels == i` loop)
+template <int M>
+__global__ __launch_bounds__(256) void k_grp_hist(int64_t n, const int32_t* __restrict__ labels, int k,
+                                                  int64_t ntiles, int32_t* __restrict__ ghist,
+                                                  const int32_t* stop, int step_i) {
+  if (stopped(stop, step_i)) return;
+  extern __shared__ int32_t sh_cnt[];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (t >= ntiles) return;  // whole wave; no block barriers below
+  int32_t* h = sh_cnt + (size_t)wv * k;
+  for (int c = lane; c < k; c += 64) h[c] = 0;
+  int32_t lv[M * 16];
+  load_tile<M>(n, labels, t * (M * kTileUnit), lane, lv);
+#pragma unroll
+  for (int q = 0; q < M * 16; ++q)
+    if ((unsigned)lv[q] < (unsigned)k) atomicAdd(&h[lv[q]], 1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  for (int c = lane; c < k; c += 64) ghist[(int64_t)c * ntiles + t] = h[c];
+}
+
+// gscan = exclusive scan of ghist (cluster-major): gscan[c * ntiles + t] is where tile t's first
+// member of cluster c goes. Chunks of 64 labels are placed in order; within a chunk, lanes with equal
+// labels (ballot match over the label bits) take consecutive slots by lane order.
+template <int M>
+__global__ __launch_bounds__(256) void k_grp_scatter(int64_t n, const int32_t* __restrict__ labels,
+                                                     int k, int bits, int64_t ntiles,
+                                                     const int32_t* __restrict__ ghist,
+                                                     const int32_t* __restrict__ gscan,
+                                                     int32_t* __restrict__ perm,
+                                                     int32_t* __restrict__ offsets,
+                                                     const int32_t* stop, int step_i) {
+  if (stopped(stop, step_i)) return;
+  extern __shared__ int32_t sh_off[];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (t >= ntiles) return;
+  int32_t* h = sh_off + (size_t)wv * k;
+  for (int c = lane; c < k; c += 64) {
+    const int32_t o = gscan[(int64_t)c * ntiles + t];
+    h[c] = o;
+    if (t == 0) offsets[c] = o;  // cluster c starts at its tile-0 offset
+  }
+  if (t == 0 && lane == 0) {
+    const int64_t last = (int64_t)k * ntiles - 1;
+    offsets[k] = gscan[last] + ghist[last];  // members with a label in [0, k)
+  }
+  int32_t lv[M * 16];
+  const int64_t base = t * (M * kTileUnit);
+  load_tile<M>(n, labels, base, lane, lv);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int q = 0; q < M * 16; ++q) {
+    const int l = lv[q];
+    const bool ok = (unsigned)l < (unsigned)k;
+    uint64_t peers = __ballot(ok);
+    for (int b = 0; b < bits; ++b) {
+      const bool bit = (l >> b) & 1;
+      const uint64_t m = __ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    if (ok) {
+      const int32_t pos = h[l] + __popcll(peers & below);
+      perm[pos] = (int32_t)(base + (int64_t)q * 64 + lane);
+    }
+    // every lane's read of h[l] above precedes the leader's update in this wave's LDS order
+    if (ok && (peers & below) == 0) h[l] += __popcll(peers);
+  }
+}
+
+// radix fallback (k > kCountMaxK): stable sort of (label, index), then first-position offsets
+__global__ void k_iota(int64_t n, int32_t* p) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = (int32_t)i;
+}
+
+__global__ void k_offsets(int64_t n, const int32_t* __restrict__ skeys, int k,
+                          int32_t* __restrict__ offsets) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  const int prev = (i == 0) ? -1 : skeys[i - 1];
+  const int cur = (i == n) ? k : skeys[i];
+  for (int c = prev + 1; c <= cur && c <= k; ++c) offsets[c] = (int32_t)i;
+}
+
+size_t group_ws(int64_t n, int k) {
+  if (k <= kCountMaxK) {
+    const GroupPlan p = group_plan(n, k);
+    const int64_t cells = (int64_t)k * p.ntiles;
+    return 2 * align256(sizeof(int32_t) * (size_t)cells) + align256(scan_i32_ws_bytes(cells)) + 256;
+  }
+  return align256(sizeof(int32_t) * (size_t)n) * 2 + sort_pairs_ws_bytes(n) + 1024;
+}
+
+int group_dev(int64_t n, const int32_t* labels, int k, int32_t* perm, int32_t* offsets, void* ws,
+              size_t ws_bytes, const int32_t* stop, int step_i, hipStream_t s) {
+  Carver cv(ws, ws_bytes);
+  if (k <= kCountMaxK) {
+    const GroupPlan p = group_plan(n, k);
+    const int64_t cells = (int64_t)k * p.ntiles;
+    GDD_REQUIRE(cells < INT_MAX, "group_by_label: k x tiles too large");
+    int32_t* ghist = cv.take<int32_t>(cells);
+    int32_t* gscan = cv.take<int32_t>(cells);
+    const size_t sb = scan_i32_ws_bytes(cells);
+    void* sws = cv.take<char>(sb);
+    if (!cv.ok()) return fail(GDD_E_WORKSPACE, "group_by_label: workspace too small");
+    int bits = 1;
+    while ((1ll << bits) < (long long)k) ++bits;
+    const unsigned grid = (unsigned)((p.ntiles + p.waves - 1) / p.waves);
+    const size_t lds = sizeof(int32_t) * (size_t)p.waves * k;
+    auto go = [&](auto M_) -> int {
+      constexpr int M = decltype(M_)::value;
+      if (lds > 65536) {
+        GDD_HIP(hipFuncSetAttribute((const void*)k_grp_hist<M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        GDD_HIP(hipFuncSetAttribute((const void*)k_grp_scatter<M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      }
+      k_grp_hist<M><<<grid, 64 * p.waves, lds, s>>>(n, labels, k, p.ntiles, ghist, stop, step_i);
+      GDD_LAUNCHED();
+      int rc = exclusive_scan_i32(ghist, gscan, cells, sws, sb, s);
+      if (rc) return rc;
+      k_grp_scatter<M><<<grid, 64 * p.waves, lds, s>>>(n, labels, k, bits, p.ntiles, ghist, gscan, perm,
+                                                       offsets, stop, step_i);
+      GDD_LAUNCHED();
+      return GDD_OK;
+    };
+    switch (p.m) {
+      case 1: return go(std::integral_constant<int, 1>());
+      case 2: return go(std::integral_constant<int, 2>());
+      case 3: return go(std::integral_constant<int, 3>());
+      default: return go(std::integral_constant<int, 4>());
+    }
+  }
+  GDD_REQUIRE(!stop, "group_by_label: k=%d too large for the device loop", k);
+  int32_t* iota = cv.take<int32_t>(n);
+  int32_t* skeys = cv.take<int32_t>(n);
+  const size_t sb = sort_pairs_ws_bytes(n);
+  void* sws = cv.take<char>(sb);
+  if (!cv.ok()) return fail(GDD_E_WORKSPACE, "group_by_label: workspace too small");
+  int bits = 1;
+  while ((1ll << bits) < (long long)k) ++bits;
+  k_iota<<<blocks_of(n), 256, 0, s>>>(n, iota);
+  GDD_LAUNCHED();
+  int rc = sort_pairs_i32(labels, skeys, iota, perm, n, bits, sws, sb, s);
+  if (rc) return rc;
+  k_offsets<<<blocks_of(n + 1), 256, 0, s>>>(n, skeys, k, offsets);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// ordered per-cluster folds: Lloyd sums (fp32 chain of x*w) and cluster means (fp64 chain of x)
+// ---------------------------------------------------------------------------------------------
+// Grid (feature slices, clusters), 256 threads. A block walks its cluster's members (perm[offsets[c]
+// .. offsets[c+1]), sample order) in chunks of R rows x FW features staged through two LDS buffers:
+// while thread f folds column f of chunk i (16 LDS reads in flight ahead of the dependent adds, two
+// alternating register sets), chunk i+1's rows are in flight into registers, and chunk i+2's member
+// ids (a three-slot ring) are loaded after the fold. Rows past a chunk's end are staged as +0.0,
+// which leaves a sum that started at +0.0 unchanged, so the fold runs in unguarded groups of 16.
+constexpr int kFoldElems = 16384;  // floats per LDS chunk buffer (64 KiB)
+constexpr int kFoldMaxR = 1024;
+
+struct FoldArgs {
+  int dim, fw_max, R;
+  const float* X;
+  const float* w;          // Lloyd sample weights (nullable: unit weights)
+  const int32_t* perm;
+  const int32_t* offsets;
+  float* out;              // k x dim: sums (Lloyd) or means
+  float* wsum;             // Lloyd weight sums
+  long long* counts;       // mean: members per cluster (nullable)
+  int empty_as_zero;
+  const int32_t* stop;
+  int step_i;
+};
+
+template <typename ACC, bool WEIGHTED>
+__device__ __forceinline__ void fold_col(const float* __restrict__ col, int stride, int rp, ACC& acc,
+                                         const float* __restrict__ W) {
+  float A[16], B[16], WA[16], WB[16];
+  auto ld = [&](float(&v)[16], float(&wv)[16], int r0) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = col[(r0 + u) * stride];
+    if constexpr (WEIGHTED) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) wv[u] = W[r0 + u];
+    }
+  };
+  auto add = [&](const float(&v)[16], const float(&wv)[16]) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if constexpr (WEIGHTED) {
+        const float term = v[u] * wv[u];
+        acc = acc + (ACC)term;
+      } else {
+        acc = acc + (ACC)v[u];
+      }
+    }
+  };
+  ld(A, WA, 0);
+  int r0 = 0;
+  for (; r0 + 32 <= rp; r0 += 32) {
+    ld(B, WB, r0 + 16);
+    add(A, WA);
+    if (r0 + 32 < rp) ld(A, WA, r0 + 32);
+    add(B, WB);
+  }
+  if (r0 < rp) add(A, WA);
+}
+
+template <typename ACC, bool VEC, bool WEIGHTED, bool MEAN>
+__global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
+  if (stopped(a.stop, a.step_i)) return;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int U = VEC ? 4 : 1;            // floats per staged element
+  constexpr int Q = kFoldElems / (256 * U);  // staged elements per thread per chunk
+  const int R = a.R, dim = a.dim, tid = threadIdx.x;
+  float* Bbuf = smem;
+  int32_t* sid = reinterpret_cast<int32_t*>(smem + 2 * kFoldElems);  // 3 x R
+  float* Wbuf = smem + 2 * kFoldElems + 3 * R;                         // 3 x R (WEIGHTED)
+  const int c = blockIdx.y;
+  const int f0 = blockIdx.x * a.fw_max;
+  const int FW = min(a.fw_max, dim - f0);
+  const int FWu = FW / U;
+  const int32_t b = a.offsets[c], e = a.offsets[c + 1];
+  const int nm = e - b;
+  ACC acc = 0;
+  float wacc = 0.f;
+  if (nm > 0) {
+    const int nch = (nm + R - 1) / R;
+    const int dr = 256 / FWu, df = 256 % FWu;
+    const int r_init = tid / FWu, f_init = tid % FWu;
+    float xv[Q * U];
+    auto load_ids = [&](int chunk) {
+      const int slot = chunk % 3, m0 = chunk * R;
+      const int rows = min(R, nm - m0);
+      for (int r = tid; r < R; r += 256) {
+        const int32_t id = a.perm[b + m0 + min(r, rows - 1)];
+        sid[slot * R + r] = id;
+        if constexpr (WEIGHTED) Wbuf[slot * R + r] = r < rows ? a.w[id] : 0.f;
+      }
+    };
+    auto gather = [&](int chunk) {
+      const int32_t* ids = sid + (chunk % 3) * R;
+      int r = r_init, f = f_init;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int64_t id = ids[min(r, R - 1)];
+        const float* src = a.X + id * dim + f0 + f * U;
+        if constexpr (VEC) {
+          const float4 v = *reinterpret_cast<const float4*>(src);
+          xv[4 * q] = v.x;
+          xv[4 * q + 1] = v.y;
+          xv[4 * q + 2] = v.z;
+          xv[4 * q + 3] = v.w;
+        } else {
+          xv[q] = *src;
+        }
+        r += dr;
+        f += df;
+        if (f >= FWu) {
+          f -= FWu;
+          ++r;
+        }
+      }
+    };
+    auto store = [&](int chunk) {
+      float* B = Bbuf + (chunk & 1) * kFoldElems;
+      const int rows = min(R, nm - chunk * R);
+      int r = r_init, f = f_init;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        if (r < R) {
+          const bool live = r < rows;
+          if constexpr (VEC) {
+            float4 v = live ? make_float4(xv[4 * q], xv[4 * q + 1], xv[4 * q + 2], xv[4 * q + 3])
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4*>(B + r * FW + 4 * f) = v;
+          } else {
+            B[r * FW + f] = live ? xv[q] : 0.f;
+          }
+        }
+        r += dr;
+        f += df;
+        if (f >= FWu) {
+          f -= FWu;
+          ++r;
+        }
+      }
+    };
+    load_ids(0);
+    if (nch > 1) load_ids(1);
+    __syncthreads();
+    gather(0);
+    store(0);
+    __syncthreads();
+    for (int i = 0; i < nch; ++i) {
+      const int rows = min(R, nm - i * R);
+      if (i + 1 < nch) gather(i + 1);  // ids of chunk i+1 were staged before the last barrier
+      if (tid < FW) {
+        const float* col = Bbuf + (i & 1) * kFoldElems + tid;
+        fold_col<ACC, WEIGHTED>(col, FW, (rows + 15) & ~15, acc, Wbuf + (i % 3) * R);
+      }
+      if (WEIGHTED && tid == 255) {
+        const float* W = Wbuf + (i % 3) * R;
+        for (int r = 0; r < rows; ++r) wacc = wacc + W[r];
+      }
+      if (i + 1 < nch) {
+        store(i + 1);                       // buffer (i+1)&1 was last read in iteration i-1
+        if (i + 2 < nch) load_ids(i + 2);   // slot (i+2)%3 was last read in iteration i-1
+      }
+      __syncthreads();
+    }
+  }
+  const int64_t ob = (int64_t)c * dim + f0;
+  if constexpr (MEAN) {
+    if (tid < FW) {
+      float r;
+      if (nm == 0)
+        r = a.empty_as_zero ? 0.f : __builtin_nanf("");
+      else
+        r = (float)((double)acc / (double)nm);
+      a.out[ob + tid] = r;
+    }
+    if (blockIdx.x == 0 && tid == 0 && a.counts) a.counts[c] = nm;
+  } else {
+    if (tid < FW) a.out[ob + tid] = (float)acc;
+    // unit weights: a sequential fp32 count, which sticks at 2^24
+    if (blockIdx.x == 0 && tid == 255) a.wsum[c] = WEIGHTED ? wacc : fminf((float)nm, 16777216.f);
+  }
+}
+
+int fold_launch(const FoldArgs& a0, int k, bool mean, hipStream_t s) {
+  FoldArgs a = a0;
+  const bool weighted = a.w != nullptr;
+  a.fw_max = std::min(a.dim, weighted ? 192 : 256);  // weighted: thread 255 folds the weights
+  if (a.fw_max % 4 != 0 && a.fw_max < a.dim) a.fw_max &= ~3;
+  int R = std::min(kFoldMaxR, kFoldElems / a.fw_max);
+  R &= ~15;
+  a.R = std::max(R, 16);
+  const bool vec = a.dim % 4 == 0 && a.fw_max % 4 == 0 && (reinterpret_cast<uintptr_t>(a.X) & 15) == 0;
+  const unsigned nsl = (unsigned)((a.dim + a.fw_max - 1) / a.fw_max);
+  GDD_REQUIRE(k < 65536, "cluster fold: k=%d too large", k);
+  const size_t lds = sizeof(float) * (2 * (size_t)kFoldElems + 3 * (size_t)a.R * (weighted ? 2 : 1));
+  dim3 grid(nsl, (unsigned)k);
+  auto go = [&](auto kern) -> int {
+    GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    kern<<<grid, 256, lds, s>>>(a);
+    GDD_LAUNCHED();
+    return GDD_OK;
+  };
+  if (mean) return vec ? go(k_seg_fold<double, true, false, true>) : go(k_seg_fold<double, false, false, true>);
+  if (weighted)
+    return vec ? go(k_seg_fold<float, true, true, false>) : go(k_seg_fold<float, false, true, false>);
+  return vec ? go(k_seg_fold<float, true, false, false>) : go(k_seg_fold<float, false, false, false>);
+}
+
+// ---------------------------------------------------------------------------------------------
+// numpy pairwise sum (umath loops_utils.h.src): n < 8 sequential; n <= 128 eight interleaved
+// accumulators ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the n % 8 tail; otherwise split at n/2
+// rounded down to a multiple of 8, left + right.
+// ---------------------------------------------------------------------------------------------
+template <class F>
+__device__ float pw_leaf(F val, int off, int n) {
+  if (n < 8) {
+    float res = 0.f;
+    for (int i = 0; i < n; ++i) res = res + val(off + i);
+    return res;
+  }
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = val(off + j);
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = r[j] + val(off + i + j);
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res = res + val(off + i);
+  return res;
+}
+
+template <int D, class F>
+__device__ __attribute__((noinline)) float pw_sum(F val, int off, int n) {
+  if constexpr (D == 0) {
+    return pw_leaf(val, off, n);
+  } else {
+    if (n <= 128) return pw_leaf(val, off, n);
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return pw_sum<D - 1>(val, off, n2) + pw_sum<D - 1>(val, off + n2, n - n2);
+  }
+}
+constexpr int kPwDepth = 24;  // n < 128 * 2^24
+
+// ---------------------------------------------------------------------------------------------
+// _average_centers + _center_shift
+// ---------------------------------------------------------------------------------------------
+// One 64-lane block per cluster. sklearn walks j = 0..k-1: a cluster with weight scales its row
+// by fp32(1/w); an empty one copies the row of argmax(weight) (first maximum) as it stands at that
+// moment, i.e. averaged when argmax < j. Here the heaviest cluster's block writes every empty row
+// (from its raw and its averaged values) before averaging its own, so no block reads a row another
+// block is rescaling; empty blocks return at once. Shifts: sqrt(_euclidean_dense_dense).
+__global__ __launch_bounds__(64) void k_avg_centers(int k, int dim, float* __restrict__ C_new,
+                                                    const float* __restrict__ wsum,
+                                                    const float* __restrict__ C_old,
+                                                    float* __restrict__ shift, const int32_t* stop,
+                                                    int step_i) {
+  if (stopped(stop, step_i)) return;
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const float wc = wsum[c];
+  if (!(wc > 0.f)) return;
+  float bv = -1.f;
+  int bi = INT_MAX, any_empty = 0;
+  for (int j = lane; j < k; j += 64) {
+    const float v = wsum[j];
+    if (v > bv) {
+      bv = v;
+      bi = j;
+    }
+    any_empty |= !(v > 0.f);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o);
+    const int oi = __shfl_xor(bi, o);
+    if (ov > bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+    any_empty |= __shfl_xor(any_empty, o);
+  }
+  const float alpha = (float)(1.0 / (double)wc);  // `1.0 / weight` is a C double division
+  const int64_t cb = (int64_t)c * dim;
+  const bool donor = any_empty && bi == c;
+  if (donor) {
+    for (int j = 0; j < k; ++j) {
+      if (wsum[j] > 0.f) continue;
+      const int64_t jb = (int64_t)j * dim;
+      for (int f = lane; f < dim; f += 64) {
+        const float raw = C_new[cb + f];
+        C_new[jb + f] = c < j ? raw * alpha : raw;
+      }
+    }
+  }
+  for (int f = lane; f < dim; f += 64) C_new[cb + f] = C_new[cb + f] * alpha;
+  __syncthreads();
+  if (lane == 0 && shift) {
+    shift[c] = sqrtf(skl_sqdist(C_new + cb, C_old + cb, dim));
+    if (donor)
+      for (int j = 0; j < k; ++j)
+        if (!(wsum[j] > 0.f))
+          shift[j] = sqrtf(skl_sqdist(C_new + (int64_t)j * dim, C_old + (int64_t)j * dim, dim));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// the Lloyd loop's control words
+// ---------------------------------------------------------------------------------------------
+// Iteration i runs as two steps: 2i (E-step labels, grouping, sums, the empty-cluster check) and
+// 2i+1 (average + shift, labels changed, convergence). stop_at = s+1 skips every later step.
+struct LloydState {
+  int32_t stop_at;   // offset 0
+  int32_t reason;    // 0 running/max_iter, 1 strict, 2 tol, 3 needs relocation
+  int32_t iter;      // iteration the reason refers to
+  int32_t changed;   // labels changed in the current iteration
+  int32_t done;      // iterations completed (the convergence step's count)
+  int32_t pad[11];
+};
+static_assert(sizeof(LloydState) == 64, "LloydState is 64 bytes");
+
+__global__ void k_lloyd_changed(int64_t n, const int32_t* __restrict__ labels,
+                                int32_t* __restrict__ old, LloydState* st, int step_i) {
+  if (stopped(&st->stop_at, step_i)) return;
+  int any = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t a = labels[i];
+    if (a != old[i]) {
+      any = 1;
+      old[i] = a;
+    }
+  }
+  if (__any(any) && (threadIdx.x & 63) == 0) st->changed = 1;
+}
+
+__global__ __launch_bounds__(256) void k_lloyd_check_empty(int k, const float* __restrict__ wsum,
+                                                           LloydState* st, int it, int step_i) {
+  if (stopped(&st->stop_at, step_i)) return;
+  __shared__ int s_any;
+  if (threadIdx.x == 0) s_any = 0;
+  __syncthreads();
+  int any = 0;
+  for (int j = threadIdx.x; j < k; j += blockDim.x) any |= !(wsum[j] > 0.f);
+  if (any) s_any = 1;
+  __syncthreads();
+  if (threadIdx.x == 0 && s_any) {
+    st->reason = 3;
+    st->iter = it;
+    __hip_atomic_store(&st->stop_at, step_i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+constexpr int kShiftLds = 8192;
+__global__ __launch_bounds__(256) void k_lloyd_converge(int k, const float* __restrict__ shift,
+                                                        double tol, LloydState* st, int it,
+                                                        int step_i) {
+  if (stopped(&st->stop_at, step_i)) return;
+  __shared__ float sq[kShiftLds];
+  const bool in_lds = k <= kShiftLds;
+  if (in_lds)
+    for (int j = threadIdx.x; j < k; j += blockDim.x) sq[j] = shift[j] * shift[j];
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  int reason = 0;
+  if (st->changed == 0) {
+    reason = 1;  // np.array_equal(labels, labels_old)
+  } else {
+    float tot;
+    if (in_lds)
+      tot = pw_sum<kPwDepth>([&](int j) { return sq[j]; }, 0, k);
+    else
+      tot = pw_sum<kPwDepth>([&](int j) { const float v = shift[j]; return v * v; }, 0, k);
+    if ((double)tot <= tol) reason = 2;
+  }
+  st->changed = 0;
+  st->done = it + 1;
+  if (reason) {
+    st->reason = reason;
+    st->iter = it;
+    __hip_atomic_store(&st->stop_at, step_i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ((X - C[labels])**2).sum(axis=1) in numpy's order: fp32 squares, pairwise per contiguous row
+__global__ void k_relocate_distances(int64_t n, int dim, const float* __restrict__ X,
+                                     const int32_t* __restrict__ labels, const float* __restrict__ C,
+                                     float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* x = X + i * dim;
+  const float* cr = C + (int64_t)labels[i] * dim;
+  out[i] = pw_sum<kPwDepth>([&](int j) { const float d = x[j] - cr[j]; return d * d; }, 0, dim);
+}
+
+}  // namespace
+}  // namespace gdd
+
+using namespace gdd;
+
+// ---- grouping and folds (C ABI) ------------------------------------------------------------------
+extern "C" size_t gdd_group_ws_bytes(int64_t n, int k) { return group_ws(std::max<int64_t>(n, 1), std::max(k, 1)); }
+
+extern "C" int gdd_group_by_label(int64_t n, const int32_t* labels, int k, int32_t* perm,
+                                  int32_t* offsets, void* ws, size_t ws_bytes,
+                                  gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && k > 0 && labels && perm && offsets && ws, "group_by_label: bad arguments");
+  if (ws_bytes < group_ws(n, k)) return fail(GDD_E_WORKSPACE, "group_by_label: workspace too small");
+  return group_dev(n, labels, k, perm, offsets, ws, ws_bytes, nullptr, 0, to_hip(stream));
+}
+
+extern "C" int gdd_segment_sum_f32(int64_t n, int dim, const float* X, const float* w,
+                                   const int32_t* perm, const int32_t* offsets, int k, float* sums,
+                                   float* wsum, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && dim > 0 && k > 0 && X && perm && offsets && sums && wsum,
+              "segment_sum_f32: bad arguments");
+  FoldArgs a{dim, 0, 0, X, w, perm, offsets, sums, wsum, nullptr, 0, nullptr, 0};
+  return fold_launch(a, k, false, to_hip(stream));
+}
+
+extern "C" int gdd_cluster_mean(int64_t n, int d, const float* feat, const int32_t* perm,
+                                const int32_t* offsets, int k, int empty_as_zero, float* feat_syn,
+                                long long* counts, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && d > 0 && k > 0 && feat && perm && offsets && feat_syn,
+              "cluster_mean: bad arguments");
+  FoldArgs a{d, 0, 0, feat, nullptr, perm, offsets, feat_syn, nullptr, counts, empty_as_zero, nullptr, 0};
+  return fold_launch(a, k, true, to_hip(stream));
+}
+
+extern "C" int gdd_average_centers(int k, int dim, float* C_new, const float* wsum,
+                                   const float* C_old, float* center_shift, gdd_stream_t stream) {
+  GDD_REQUIRE(k > 0 && dim > 0 && C_new && wsum && C_old, "average_centers: bad arguments");
+  k_avg_centers<<<k, 64, 0, to_hip(stream)>>>(k, dim, C_new, wsum, C_old, center_shift, nullptr, 0);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" int gdd_relocate_distances(int64_t n, int dim, const float* X, const int32_t* labels,
+                                      const float* C, float* out, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && dim > 0 && X && labels && C && out, "relocate_distances: bad arguments");
+  k_relocate_distances<<<blocks_of(n), 256, 0, to_hip(stream)>>>(n, dim, X, labels, C, out);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+// ---- the device-resident Lloyd loop -----------------------------------------------------------------
+extern "C" size_t gdd_lloyd_state_bytes(void) { return sizeof(LloydState); }
+
+extern "C" size_t gdd_kmeans_lloyd_ws_bytes(int64_t n, int dim, int k) {
+  (void)dim;
+  return align256(sizeof(unsigned long long) * (size_t)n) + align256(sizeof(float) * (size_t)k) +
+         align256(sizeof(int32_t) * (size_t)n) + align256(sizeof(int32_t) * (size_t)(k + 1)) +
+         group_ws(n, k) + 1024;
+}
+
+extern "C" size_t gdd_kmeans_lloyd_host_ws_bytes(void) { return 4 * sizeof(LloydState); }
+
+extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, float* C0, float* C1,
+                                    int32_t* labels, int32_t* labels_old, float* wsum, float* shift,
+                                    int it0, int resume, int max_iter, double tol, void* state,
+                                    int32_t* out_done, int32_t* out_reason, void* ws, size_t ws_bytes,
+                                    void* host_ws, size_t host_ws_bytes, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && dim > 0 && dim <= 512 && k > 0 && k <= kCountMaxK && X && C0 && C1 && labels &&
+                  labels_old && wsum && shift && state && out_done && out_reason && ws && host_ws,
+              "kmeans_lloyd_run: bad arguments");
+  GDD_REQUIRE(it0 >= 0 && it0 <= max_iter && max_iter < (INT_MAX / 2 - 2), "kmeans_lloyd_run: bad iteration range");
+  if (ws_bytes < gdd_kmeans_lloyd_ws_bytes(n, dim, k))
+    return fail(GDD_E_WORKSPACE, "kmeans_lloyd_run: workspace too small");
+  if (host_ws_bytes < gdd_kmeans_lloyd_host_ws_bytes())
+    return fail(GDD_E_WORKSPACE, "kmeans_lloyd_run: host workspace too small");
+  hipStream_t s = to_hip(stream);
+  Carver cv(ws, ws_bytes);
+  auto* keys = cv.take<unsigned long long>(n);
+  float* cn2 = cv.take<float>(k);
+  int32_t* perm = cv.take<int32_t>(n);
+  int32_t* offsets = cv.take<int32_t>(k + 1);
+  const size_t gb = group_ws(n, k);
+  void* gws = cv.take<char>(gb);
+  if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans_lloyd_run: workspace too small");
+  LloydState* st = static_cast<LloydState*>(state);
+  LloydState* hs = static_cast<LloydState*>(host_ws);
+  // a fresh run (or a resume after the host's relocation) starts with the stop word clear; the
+  // changed flag is kept on resume (the E-step that set it already ran)
+  GDD_HIP(hipMemsetAsync(st, 0, offsetof(LloydState, changed), s));
+  if (!resume) GDD_HIP(hipMemsetAsync(&st->changed, 0, sizeof(int32_t), s));
+  FoldArgs fa{dim, 0, 0, X, nullptr, perm, offsets, nullptr, wsum, nullptr, 0, &st->stop_at, 0};
+  const unsigned cgrid = std::min<unsigned>(blocks_of(n), 2048);
+  auto enqueue = [&](int i, bool phase_a) -> int {
+    float* cin = (i & 1) ? C1 : C0;
+    float* cout = (i & 1) ? C0 : C1;
+    const int sa = 2 * i, sb = 2 * i + 1;
+    if (phase_a) {
+      int rc = kmeans_assign_dev(n, dim, X, k, cin, cn2, labels, keys, &st->stop_at, sa, s);
+      if (rc) return rc;
+      rc = group_dev(n, labels, k, perm, offsets, gws, gb, &st->stop_at, sa, s);
+      if (rc) return rc;
+      fa.out = cout;
+      fa.step_i = sa;
+      rc = fold_launch(fa, k, false, s);
+      if (rc) return rc;
+      k_lloyd_check_empty<<<1, 256, 0, s>>>(k, wsum, st, i, sa);
+      GDD_LAUNCHED();
+    }
+    k_avg_centers<<<k, 64, 0, s>>>(k, dim, cout, wsum, cin, shift, &st->stop_at, sb);
+    GDD_LAUNCHED();
+    k_lloyd_changed<<<cgrid, 256, 0, s>>>(n, labels, labels_old, st, sb);
+    GDD_LAUNCHED();
+    k_lloyd_converge<<<1, 256, 0, s>>>(k, shift, tol, st, i, sb);
+    GDD_LAUNCHED();
+    return GDD_OK;
+  };
+  // chunks of iterations enqueued ahead of the decision; the host reads the state of chunk c while
+  // chunk c+1 runs (two pinned slots, one event each)
+  hipEvent_t ev[2];
+  GDD_HIP(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+  GDD_HIP(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+  int rc = GDD_OK;
+  int i = it0, chunk = 0, pending = -1, ch = 2;
+  bool stop = false;
+  int done = it0, reason = 0;
+  auto poll = [&](int slot) -> int {
+    GDD_HIP(hipEventSynchronize(ev[slot]));
+    if (hs[slot].stop_at) {
+      stop = true;
+      reason = hs[slot].reason;
+      done = reason == 3 ? hs[slot].iter : hs[slot].done;
+    } else {
+      done = hs[slot].done;
+    }
+    return GDD_OK;
+  };
+  while (i < max_iter && !stop) {
+    const int m = std::min(ch, max_iter - i);
+    for (int j = 0; j < m && rc == GDD_OK; ++j, ++i) rc = enqueue(i, !(resume && i == it0));
+    if (rc) break;
+    const int slot = chunk & 1;
+    GDD_HIP(hipMemcpyAsync(&hs[slot], st, sizeof(LloydState), hipMemcpyDeviceToHost, s));
+    GDD_HIP(hipEventRecord(ev[slot], s));
+    if (pending >= 0) {
+      rc = poll(pending);
+      if (rc) break;
+    }
+    pending = slot;
+    ++chunk;
+    ch = std::min(ch * 2, 8);
+  }
+  if (rc == GDD_OK && pending >= 0 && !stop) rc = poll(pending);
+  if (rc == GDD_OK) {
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) rc = fail((int)e, "kmeans_lloyd_run: %s", hipGetErrorString(e));
+  }
+  (void)hipEventDestroy(ev[0]);
+  (void)hipEventDestroy(ev[1]);
+  if (rc) return rc;
+  if (!stop) done = max_iter;  // ran out of iterations (sklearn's loop end)
+  *out_done = done;
+  *out_reason = reason;
+  return GDD_OK;
+}

@@ -74,7 +74,13 @@ SIGNATURES = {
     "gdd_fixed_to_centers": (_c_int, [_c_int, _c_int, _vp, _vp, _c_int, _vp, _vp]),
     "gdd_average_centers": (_c_int, [_c_int, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "gdd_point_center_sqdist": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
-    "gdd_labels_changed": (_c_int, [_c_i64, _vp, _vp, _vp, _vp]),
+    "gdd_relocate_distances": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "gdd_lloyd_state_bytes": (_c_size, []),
+    "gdd_kmeans_lloyd_ws_bytes": (_c_size, [_c_i64, _c_int, _c_int]),
+    "gdd_kmeans_lloyd_host_ws_bytes": (_c_size, []),
+    "gdd_kmeans_lloyd_run": (_c_int, [_c_i64, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_int,
+                                      _c_int, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _c_size,
+                                      _vp, _c_size, _vp]),
     "gdd_skl_sqdist": (_c_int, [_c_int, _vp, _c_i64, _c_int, _vp, _vp, _vp]),
     "gdd_kmeans_plusplus_ws_bytes": (_c_size, [_c_i64, _c_int, _c_int]),
     "gdd_kmeans_plusplus": (_c_int, [_c_i64, _c_int, _vp, _vp, _c_int, _c_int, _c_i64, _vp, _vp,

@@ -5,8 +5,10 @@
   and the teacher ``index_add_``/``bincount`` means of distill_recsys.py:623-636
   (``empty_as_zero=True``: ``clamp_min(1)`` gives zero rows for empty clusters).
 * :func:`argmax_rows` is ``torch.argmax(cluster_centers, dim=-1)`` (transduct:126).
-One stable device sort groups the samples by label; every cluster row is then one fp64 sum over
-its members in sample order, divided by the count and rounded to fp32 once.
+A stable device counting sort groups the samples by label (no host round trip); every cluster row
+is then one fp64 sum over its members in sample order, divided by the count and rounded to fp32
+once. A label outside [0, k) belongs to no cluster, exactly as in the reference's ``labels == i``
+loop over i < k.
 """
 from __future__ import annotations
 
@@ -47,8 +49,6 @@ def cluster_mean(feat: torch.Tensor, labels, k: int, empty_as_zero: bool = False
     n, d = feat.shape
     if labels.shape[0] != n:
         raise ValueError("labels and feat disagree on the number of samples")
-    if n and (int(labels.min()) < 0 or int(labels.max()) >= k):
-        raise ValueError("labels out of range [0, k)")
     perm, offsets = group_by_label(labels, k)
     out = torch.empty((k, d), dtype=torch.float32, device=dev)
     counts = torch.empty(k, dtype=torch.int64, device=dev)

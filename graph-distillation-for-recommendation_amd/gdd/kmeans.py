@@ -420,53 +420,45 @@ class KMeans(_BaseKMeans):
         ops = _Ops(dev, n, k, dim)
         lib = ops.lib
         stream = ops.stream
-        ws_group = _lib.workspace(lib.gdd_group_ws_bytes(n, k), dev)
-        perm = torch.empty(n, dtype=torch.int32, device=dev)
-        offsets = torch.empty(k + 1, dtype=torch.int32, device=dev)
+        ws = _lib.workspace(lib.gdd_kmeans_lloyd_ws_bytes(n, dim, k), dev)
+        hws = _lib.pinned_workspace(lib.gdd_kmeans_lloyd_host_ws_bytes())
+        state = torch.zeros(lib.gdd_lloyd_state_bytes(), dtype=torch.uint8, device=dev)
         labels = torch.empty(n, dtype=torch.int32, device=dev)
         labels_old = torch.empty(n, dtype=torch.int32, device=dev)
-        changed = torch.empty(1, dtype=torch.int32, device=dev)
         wic = torch.empty(k, dtype=torch.float32, device=dev)
         shift = torch.empty(k, dtype=torch.float32, device=dev)
         sq = torch.empty(n, dtype=torch.float32, device=dev)
+        done, reason = ctypes.c_int32(0), ctypes.c_int32(0)
 
         best = None
         for _ in range(self._n_init(10)):
-            C, _ = ops.kmeans_plusplus(Xd, k, rs)
-            C_new = torch.empty_like(C)
+            C0, _ = ops.kmeans_plusplus(Xd, k, rs)
+            Cb = (C0, torch.empty_like(C0))
             labels_old.fill_(-1)
-            strict = False
-            it = 0
-            for it in range(self.max_iter):  # _kmeans_single_lloyd (:690-735)
-                ops.assign(Xd, C, labels=labels)
-                _lib.check(lib.gdd_group_by_label(n, labels.data_ptr(), k, perm.data_ptr(),
-                                                  offsets.data_ptr(), ws_group.data_ptr(),
-                                                  ws_group.numel(), stream))
-                _lib.check(lib.gdd_segment_sum_f32(n, dim, Xd.data_ptr(), None, perm.data_ptr(),
-                                                   offsets.data_ptr(), k, C_new.data_ptr(),
-                                                   wic.data_ptr(), stream))
-                wic_h = wic.cpu().numpy()
-                if (wic_h == 0).any():
-                    self._relocate(Xd.cpu().numpy(), C, C_new, wic, wic_h, labels)
-                _lib.check(lib.gdd_average_centers(k, dim, C_new.data_ptr(), wic.data_ptr(),
-                                                   C.data_ptr(), shift.data_ptr(), stream))
-                _lib.check(lib.gdd_labels_changed(n, labels.data_ptr(), labels_old.data_ptr(),
-                                                  changed.data_ptr(), stream))
-                C, C_new = C_new, C
-                if int(changed.item()) == 0:
-                    strict = True
+            it0, resume = 0, 0
+            while True:  # _kmeans_single_lloyd (:690-735), device-resident
+                _lib.check(lib.gdd_kmeans_lloyd_run(
+                    n, dim, Xd.data_ptr(), k, Cb[0].data_ptr(), Cb[1].data_ptr(), labels.data_ptr(),
+                    labels_old.data_ptr(), wic.data_ptr(), shift.data_ptr(), it0, resume,
+                    int(self.max_iter), float(tol_), state.data_ptr(), ctypes.addressof(done),
+                    ctypes.addressof(reason), ws.data_ptr(), ws.numel(), hws.data_ptr(), hws.numel(),
+                    stream))
+                if reason.value != 3:
                     break
-                sh = shift.cpu().numpy()
-                if (sh ** 2).sum() <= tol_:
-                    break
-            if not strict:
+                it = done.value  # an empty cluster at iteration `it`: relocate, then resume there
+                self._relocate(Xd, Cb[it % 2], Cb[(it + 1) % 2], wic, labels, ops)
+                it0, resume = it, 1
+            n_iter = done.value
+            strict = reason.value == 1
+            C = Cb[n_iter % 2]  # iteration i writes C[(i+1) % 2]
+            if not strict:  # the final E-step with the last centres (:736-747)
                 ops.assign(Xd, C, labels=labels)
             _lib.check(lib.gdd_point_center_sqdist(n, dim, Xd.data_ptr(), labels.data_ptr(),
                                                    C.data_ptr(), sq.data_ptr(), stream))
             inertia = float(ops.inertia(sq).item())
             lab_h = labels.cpu().numpy()
             if best is None or (inertia < best[1] and not _same_clustering(lab_h, best[0], k)):
-                best = (lab_h, inertia, C.clone(), it + 1)
+                best = (lab_h, inertia, C.clone(), n_iter)
         lab_h, inertia, C, n_iter = best
         self.labels_ = lab_h
         self.inertia_ = inertia
@@ -477,36 +469,43 @@ class KMeans(_BaseKMeans):
         return self
 
     @staticmethod
-    def _relocate(Xh, C_old, C_new, wic, wic_h, labels):
-        """_relocate_empty_clusters_dense (_k_means_common.pyx:124-164). Rare: runs the same numpy
-        expressions as sklearn on the host copy of X so the far-point ranking (argpartition) is
-        identical, then writes the few changed rows back."""
-        lab = labels.cpu().numpy()
-        co = C_old.cpu().numpy()
-        cn = C_new.cpu().numpy()
+    def _relocate(Xd, C_old, C_new, wic, labels, ops):
+        """_relocate_empty_clusters_dense (_k_means_common.pyx:124-164). Rare. The far-point distances
+        are computed on the device in numpy's order (gdd_relocate_distances), so the host's
+        np.argpartition over them ranks exactly as sklearn's; only the chosen rows and the k-sized
+        sums/weights cross to the host and back."""
+        n, dim = Xd.shape
+        wic_h = wic.cpu().numpy()
         empty = np.where(np.equal(wic_h, 0))[0].astype(np.int32)
         ne = empty.shape[0]
-        distances = ((Xh - co[lab]) ** 2).sum(axis=1)
+        if ne == 0:
+            return
+        dist = torch.empty(n, dtype=torch.float32, device=Xd.device)
+        _lib.check(ops.lib.gdd_relocate_distances(n, dim, Xd.data_ptr(), labels.data_ptr(),
+                                                  C_old.data_ptr(), dist.data_ptr(), ops.stream))
+        distances = dist.cpu().numpy()
         far = np.argpartition(distances, -ne)[:-ne - 1:-1].astype(np.int32)
         if np.max(distances) == 0:
             return
+        lab = labels.index_select(0, torch.from_numpy(far.astype(np.int64)).to(Xd.device)).cpu().numpy()
+        rows = Xd.index_select(0, torch.from_numpy(far.astype(np.int64)).to(Xd.device)).cpu().numpy()
+        cn = C_new.cpu().numpy()
         for idx in range(ne):
-            new_id, far_idx = empty[idx], far[idx]
-            old_id = lab[far_idx]
-            cn[old_id] -= Xh[far_idx]
-            cn[new_id] = Xh[far_idx]
-            wic_h[new_id] = 1.0
-            wic_h[old_id] -= 1.0
+            new_id, old_id = empty[idx], lab[idx]
+            cn[old_id] -= rows[idx] * np.float32(1.0)
+            cn[new_id] = rows[idx] * np.float32(1.0)
+            wic_h[new_id] = np.float32(1.0)
+            wic_h[old_id] -= np.float32(1.0)
         C_new.copy_(torch.from_numpy(cn))
         wic.copy_(torch.from_numpy(wic_h))
 
 
 def _same_clustering(l1, l2, k):
-    """sklearn _is_same_clustering (_k_means_common.pyx:254-266)."""
+    """sklearn _is_same_clustering (_k_means_common.pyx:254-266): the map l1 -> l2 taken at each
+    label's first occurrence must hold for every sample (vectorised; same answer as the loop)."""
+    l1 = np.asarray(l1, np.int64)
+    l2 = np.asarray(l2, np.int64)
     mapping = np.full(k, -1, np.int64)
-    for a, b in zip(l1, l2):
-        if mapping[a] == -1:
-            mapping[a] = b
-        elif mapping[a] != b:
-            return False
-    return True
+    first = np.unique(l1, return_index=True)[1]
+    mapping[l1[first]] = l2[first]
+    return bool(np.array_equal(mapping[l1], l2))

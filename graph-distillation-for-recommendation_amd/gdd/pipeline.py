@@ -119,8 +119,9 @@ def load_graphsaint(dataset_dir: str, dataset: str = "", device="cuda"):
 
 
 def kmeans_cluster(X, n_clusters: int, seed: int, minibatch: bool = True, batch_size: int = 2048,
-                   device="cuda"):
-    """distill_recsys.kmeans_cluster on the device -> (labels int64 numpy, centres fp32 numpy)."""
+                   device="cuda", n_init="auto"):
+    """distill_recsys.kmeans_cluster on the device -> (labels int64 numpy, centres fp32 numpy).
+    The reference passes ``n_init="auto"`` explicitly (distill_recsys.py:176-178), the default here."""
     if n_clusters <= 0:
         raise ValueError("n_clusters must be > 0")
     n = X.shape[0]
@@ -129,9 +130,9 @@ def kmeans_cluster(X, n_clusters: int, seed: int, minibatch: bool = True, batch_
     Xs, _, _ = standard_scaler(X, device=device)
     if minibatch and n > 20000:
         km = MiniBatchKMeans(n_clusters=n_clusters, random_state=seed, batch_size=batch_size,
-                             n_init="auto", device=device)
+                             n_init=n_init, device=device)
     else:
-        km = KMeans(n_clusters=n_clusters, random_state=seed, n_init="auto", device=device)
+        km = KMeans(n_clusters=n_clusters, random_state=seed, n_init=n_init, device=device)
     km.fit(Xs)
     return km.labels_.astype(np.int64), km.cluster_centers_.astype(np.float32)
 
@@ -144,8 +145,13 @@ def teacher_means(emb: torch.Tensor, assignment, num_clusters: int) -> torch.Ten
 
 def pretrained_clustering_hot_path(features, adj, T: int, alpha: float, logits, nnodes_syn: int,
                                    dataset: str = "", seed: int = 15, cluster_minibatch: int = 1000,
-                                   device="cuda"):
+                                   device="cuda", n_init="auto"):
     """The hot path of ClustGDD.pretrained_clustering.
+
+    ``n_init``: the estimators' default. The reference constructs them without ``n_init``
+    (transduct:103,105), so the count is the installed scikit-learn's default: 1 under >= 1.4
+    ('auto', what the fixtures were made with), 10 (KMeans) / 3 (MiniBatchKMeans) under the 1.3.2
+    that ``ClustGDD/README.md`` pins. Pass ``n_init=10`` (or 3) to reproduce 1.3.2.
 
     ``logits``: the MLP's embedding output (N x C), or a callable ``f(target_feat) -> logits``.
     Returns (cluster_feat_centers [k, d], cluster_center_labels int64 [k], cluster_labels int32 [N],
@@ -160,10 +166,10 @@ def pretrained_clustering_hot_path(features, adj, T: int, alpha: float, logits, 
     target_feat, prop_feat = propagate(adj_norm, X, T, alpha)  # transduct:59-65
     out = logits(target_feat) if callable(logits) else logits
     if dataset == "ogbn-arxiv":                                  # transduct:102-105
-        km = MiniBatchKMeans(n_clusters=nnodes_syn, random_state=seed,
+        km = MiniBatchKMeans(n_clusters=nnodes_syn, random_state=seed, n_init=n_init,
                              batch_size=cluster_minibatch, device=device).fit(out)
     else:
-        km = KMeans(n_clusters=nnodes_syn, device=device).fit(out)
+        km = KMeans(n_clusters=nnodes_syn, n_init=n_init, device=device).fit(out)
     feat_syn, _ = cluster_mean(target_feat, km.labels_device_, nnodes_syn)  # transduct:121-125
     labels_syn = argmax_rows(km.cluster_centers_device_)                    # transduct:126
     return feat_syn, labels_syn, km.labels_device_.to(torch.int32), adj_norm, target_feat, prop_feat
@@ -171,8 +177,10 @@ def pretrained_clustering_hot_path(features, adj, T: int, alpha: float, logits, 
 
 def pretrained_clustering_induct_hot_path(data, T: int, alpha: float, logits_train, nnodes_syn: int,
                                           dataset: str = "", seed: int = 15,
-                                          cluster_minibatch: int = 1000, device="cuda"):
+                                          cluster_minibatch: int = 1000, device="cuda",
+                                          n_init="auto"):
     """The hot path of the inductive ClustGDD.pretrained_clustering (clustgdd_agent_induct.py:37-155).
+    ``n_init`` as in :func:`pretrained_clustering_hot_path` (induct:131-134 passes none).
 
     ``data`` carries ``adj_train/adj_val/adj_test`` (CSRGraph or anything :func:`to_csr` takes) and
     ``feat_train/feat_val/feat_test`` (e.g. :func:`graphsaint_split`'s result). ``logits_train``: the
@@ -195,9 +203,9 @@ def pretrained_clustering_induct_hot_path(data, T: int, alpha: float, logits_tra
     out = logits_train(targets["train"], targets["val"]) if callable(logits_train) else logits_train
     if dataset == "reddit":                                                         # :129-134
         km = MiniBatchKMeans(n_clusters=nnodes_syn, random_state=seed, batch_size=cluster_minibatch,
-                             device=device).fit(out)
+                             n_init=n_init, device=device).fit(out)
     else:
-        km = KMeans(n_clusters=nnodes_syn, device=device).fit(out)
+        km = KMeans(n_clusters=nnodes_syn, n_init=n_init, device=device).fit(out)
     feat_syn, _ = cluster_mean(targets["train"], km.labels_device_, nnodes_syn)     # :143-151
     labels_syn = argmax_rows(km.cluster_centers_device_)                            # :152
     return (feat_syn, labels_syn, km.labels_device_.to(torch.int32), targets["train"], norms["train"],

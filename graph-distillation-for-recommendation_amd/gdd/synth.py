@@ -104,3 +104,14 @@ def blobs(n: int, dim: int, k: int, seed: int, spread: float = 3.0) -> np.ndarra
     centres = rng.standard_normal((k, dim)) * spread
     lab = rng.integers(0, k, n)
     return (centres[lab] + rng.standard_normal((n, dim))).astype(np.float32)
+
+
+def svd_like(n: int, dim: int, seed: int) -> np.ndarray:
+    """Stand-in for distill_recsys.compute_svd_embeddings' U * sqrt(S) (distill_recsys.py:124-155):
+    orthogonal-ish Gaussian columns scaled by the square root of a power-law singular spectrum, with
+    a heavy-tailed per-row activity (popular users/items have larger embeddings)."""
+    rng = np.random.default_rng(seed)
+    s = np.sqrt(300.0 * np.arange(1, dim + 1, dtype=np.float64) ** -0.8)
+    act = rng.pareto(2.5, n) + 0.2
+    U = rng.standard_normal((n, dim)) / np.sqrt(n) * np.sqrt(act)[:, None] * 4.0
+    return (U * s).astype(np.float32)

@@ -197,7 +197,8 @@ int gdd_rng_permutation(void* state, int64_t n, int64_t* out);
 int gdd_rng_choice_unit_weights(void* state, int64_t n, int64_t* out);
 
 /* Stable grouping of samples by label: perm[offsets[c] .. offsets[c+1]) lists the samples of        */
-/* cluster c in ascending sample order; counts[c] = offsets[c+1]-offsets[c].                         */
+/* cluster c in ascending sample order; counts[c] = offsets[c+1]-offsets[c]. Labels outside [0, k)    */
+/* belong to no cluster (offsets[k] counts the others), as in the reference's `labels == i` loop.     */
 size_t gdd_group_ws_bytes(int64_t n, int k);
 int gdd_group_by_label(int64_t n, const int32_t* labels, int k, int32_t* perm, int32_t* offsets,
                        void* ws, size_t ws_bytes, gdd_stream_t stream);
@@ -219,7 +220,8 @@ int gdd_fixed_to_centers(int k, int dim, const long long* sums_fx, const long lo
                          int scale_exp, float* centers, gdd_stream_t stream);
 
 /* sklearn _average_centers (_k_means_common.pyx:215-236): w>0: C[c,:] *= fp32(1.0/(double)w);       */
-/* w==0: C[c,:] = C[argmax_w,:]. Then center_shift[c] = sqrt(||C_new[c]-C_old[c]||^2) in the          */
+/* w==0: C[c,:] = C[argmax(w),:] (first maximum; averaged already iff argmax < c, sklearn's loop     */
+/* order). Then center_shift[c] = sqrt(||C_new[c]-C_old[c]||^2) in the          */
 /* _euclidean_dense_dense order (_center_shift :239-251).                                           */
 int gdd_average_centers(int k, int dim, float* C_new, const float* wsum, const float* C_old,
                         float* center_shift, gdd_stream_t stream);
@@ -230,9 +232,30 @@ int gdd_average_centers(int k, int dim, float* C_new, const float* wsum, const f
 int gdd_point_center_sqdist(int64_t n, int dim, const float* X, const int32_t* labels,
                             const float* C, float* out, gdd_stream_t stream);
 
-/* 1 if any labels[i] != labels_old[i] (written to *changed as int32); then labels_old = labels.     */
-int gdd_labels_changed(int64_t n, const int32_t* labels, int32_t* labels_old, int32_t* changed,
-                       gdd_stream_t stream);
+/* Relocation input of _relocate_empty_clusters_dense (_k_means_common.pyx:124-164):               */
+/* out[i] = ((X[i] - C[labels[i]])**2).sum() in numpy's pairwise order over the row (fp32).           */
+int gdd_relocate_distances(int64_t n, int dim, const float* X, const int32_t* labels,
+                           const float* C, float* out, gdd_stream_t stream);
+
+/* The device-resident Lloyd loop of sklearn _kmeans_single_lloyd (sklearn/cluster/_kmeans.py:       */
+/* 690-735), replacing the per-iteration host loop of the reference's KMeans.fit call sites          */
+/* (clustgdd_agent_transduct.py:104-105, clustgdd_agent_induct.py:133-134, distill_recsys.py:178).   */
+/* Iteration i reads centres C[i%2] (C0/C1) and writes C[(i+1)%2]: labels (MFMA assignment), the     */
+/* ordered M-step, _average_centers, _center_shift, strict convergence (labels == labels_old), then */
+/* sum(shift^2) <= tol. Runs iterations it0.. until a stop or max_iter; chunks of iterations are    */
+/* enqueued ahead of the decision (later kernels no-op through `state`). Returns *out_reason:       */
+/* 0 max_iter, 1 strict, 2 tol, 3 an empty cluster needs _relocate_empty_clusters at iteration      */
+/* *out_done (the caller relocates on C[(i+1)%2]/wsum, then calls again with it0=i, resume=1).      */
+/* Otherwise *out_done = iterations completed. labels_old starts as -1 (the caller fills it).      */
+/* state: gdd_lloyd_state_bytes() of device memory; host_ws: pinned, gdd_kmeans_lloyd_host_ws_bytes. */
+size_t gdd_lloyd_state_bytes(void);
+size_t gdd_kmeans_lloyd_ws_bytes(int64_t n, int dim, int k);
+size_t gdd_kmeans_lloyd_host_ws_bytes(void);
+int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, float* C0, float* C1,
+                         int32_t* labels, int32_t* labels_old, float* wsum, float* shift, int it0,
+                         int resume, int max_iter, double tol, void* state, int32_t* out_done,
+                         int32_t* out_reason, void* ws, size_t ws_bytes, void* host_ws,
+                         size_t host_ws_bytes, gdd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* Greedy k-means++ seeding, sklearn _kmeans_plusplus (sklearn/cluster/_kmeans.py:174-272) on the    */

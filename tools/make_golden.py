@@ -22,6 +22,10 @@ setting in which its Lloyd M-step merge order is deterministic.
                            adj_full[np.ix_(idx, idx)] sub-graphs), then clustgdd_agent_induct
                            .ClustGDD.pretrained_clustering ('flickr': KMeans, 'reddit':
                            MiniBatchKMeans), with the k-means input and RNG state captured
+  G9 golden_configs.npz / .json  config-shape k-means: KMeans(k=196)
+                           on a 200,000 x 47 products-shaped input (global RNG after np.random.seed(15),
+                           the agent's call) and distill_recsys.kmeans_cluster on ML-1M-shaped SVD
+                           embeddings (6,040 users, k=604; 3,706 items, k=371; seed 42)
   G8 golden_recsys.npz     distill_recsys.build_condensed_bipartite on synthetic interactions (with
                            empty super-nodes), condensed_csr_to_edge_index, and LightGCNCondensed
                            (propagate outputs, bpr_loss and every parameter gradient) on CPU
@@ -168,6 +172,29 @@ def g3b_arxiv():
            "labels_sha256": sha(m.labels_.astype(np.int32)),
            "centers_sha256": sha(m.cluster_centers_.astype(np.float32))}
     with open(os.path.join(OUT, "golden_kmeans_arxiv.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+
+
+def g9_configs(recsys):
+    from sklearn.cluster import KMeans
+    X = synth.blobs(200000, 47, 196, seed=5)
+    np.random.seed(15)
+    m = KMeans(n_clusters=196).fit(X)
+    rec = {"products_input": "gdd.synth.blobs(200000, 47, 196, seed=5)",
+           "products_estimator": "np.random.seed(15); KMeans(n_clusters=196) (random_state=None)",
+           "products_n_iter": int(m.n_iter_), "products_inertia": float(m.inertia_),
+           "products_labels_sha256": sha(m.labels_.astype(np.int32)),
+           "products_centers_sha256": sha(m.cluster_centers_.astype(np.float32))}
+    out = {"products_centers": m.cluster_centers_.astype(np.float32)}
+    for name, n, k in (("users", 6040, 604), ("items", 3706, 371)):
+        E = synth.svd_like(n, 64, seed=n)
+        lab, cen = recsys.kmeans_cluster(E, n_clusters=k, seed=42, minibatch=True)
+        out[f"ml1m_{name}_labels"] = lab.astype(np.int16)
+        out[f"ml1m_{name}_centers"] = cen.astype(np.float32)
+        rec[f"ml1m_{name}_input"] = f"gdd.synth.svd_like({n}, 64, seed={n})"
+    rec["ml1m_call"] = "distill_recsys.kmeans_cluster(E, n_clusters=k, seed=42, minibatch=True)"
+    np.savez_compressed(os.path.join(OUT, "golden_configs.npz"), **out)
+    with open(os.path.join(OUT, "golden_configs.json"), "w") as f:
         json.dump(rec, f, indent=1)
 
 
@@ -426,7 +453,7 @@ def main():
     import torch
     os.makedirs(OUT, exist_ok=True)
     du, agent, recsys = import_reference()
-    which = set(sys.argv[1:]) or {"G1", "G2", "G3", "G3b", "G5", "G6", "G7", "G8"}
+    which = set(sys.argv[1:]) or {"G1", "G2", "G3", "G3b", "G5", "G6", "G7", "G8", "G9"}
     with threadpool_limits(limits=1):
         if "G1" in which:
             g1_normalize(du)
@@ -443,6 +470,8 @@ def main():
             g6_condense(du, agent)
         if "G8" in which:
             g8_recsys(recsys)
+        if "G9" in which:
+            g9_configs(recsys)
         if "G7" in which:
             g7_induct("flickr")
             g7_induct("reddit")
