@@ -226,6 +226,7 @@ constexpr int kFoldMaxR = 1024;
 
 struct FoldArgs {
   int dim, fw_max, R;
+  int c0;                  // first cluster of this launch; outputs are indexed from c0 (a slice)
   const float* X;
   const float* w;          // Lloyd sample weights (nullable: unit weights)
   const int32_t* perm;
@@ -282,7 +283,7 @@ __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
   float* Bbuf = smem;
   int32_t* sid = reinterpret_cast<int32_t*>(smem + 2 * kFoldElems);  // 3 x R
   float* Wbuf = smem + 2 * kFoldElems + 3 * R;                         // 3 x R (WEIGHTED)
-  const int c = blockIdx.y;
+  const int c = a.c0 + (int)blockIdx.y;
   const int f0 = blockIdx.x * a.fw_max;
   const int FW = min(a.fw_max, dim - f0);
   const int FWu = FW / U;
@@ -376,7 +377,8 @@ __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
       __syncthreads();
     }
   }
-  const int64_t ob = (int64_t)c * dim + f0;
+  const int cs = c - a.c0;  // row of the output slice
+  const int64_t ob = (int64_t)cs * dim + f0;
   if constexpr (MEAN) {
     if (tid < FW) {
       float r;
@@ -386,15 +388,16 @@ __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
         r = (float)((double)acc / (double)nm);
       a.out[ob + tid] = r;
     }
-    if (blockIdx.x == 0 && tid == 0 && a.counts) a.counts[c] = nm;
+    if (blockIdx.x == 0 && tid == 0 && a.counts) a.counts[cs] = nm;
   } else {
     if (tid < FW) a.out[ob + tid] = (float)acc;
     // unit weights: a sequential fp32 count, which sticks at 2^24
-    if (blockIdx.x == 0 && tid == 255) a.wsum[c] = WEIGHTED ? wacc : fminf((float)nm, 16777216.f);
+    if (blockIdx.x == 0 && tid == 255) a.wsum[cs] = WEIGHTED ? wacc : fminf((float)nm, 16777216.f);
   }
 }
 
-int fold_launch(const FoldArgs& a0, int k, bool mean, hipStream_t s) {
+// clusters [a0.c0, a0.c0 + count)
+int fold_launch(const FoldArgs& a0, int count, bool mean, hipStream_t s) {
   FoldArgs a = a0;
   const bool weighted = a.w != nullptr;
   a.fw_max = std::min(a.dim, weighted ? 192 : 256);  // weighted: thread 255 folds the weights
@@ -404,9 +407,10 @@ int fold_launch(const FoldArgs& a0, int k, bool mean, hipStream_t s) {
   a.R = std::max(R, 16);
   const bool vec = a.dim % 4 == 0 && a.fw_max % 4 == 0 && (reinterpret_cast<uintptr_t>(a.X) & 15) == 0;
   const unsigned nsl = (unsigned)((a.dim + a.fw_max - 1) / a.fw_max);
-  GDD_REQUIRE(k < 65536, "cluster fold: k=%d too large", k);
+  GDD_REQUIRE(count >= 0 && count < 65536, "cluster fold: %d clusters per launch", count);
+  if (count == 0) return GDD_OK;
   const size_t lds = sizeof(float) * (2 * (size_t)kFoldElems + 3 * (size_t)a.R * (weighted ? 2 : 1));
-  dim3 grid(nsl, (unsigned)k);
+  dim3 grid(nsl, (unsigned)count);
   auto go = [&](auto kern) -> int {
     GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     kern<<<grid, 256, lds, s>>>(a);
@@ -627,8 +631,19 @@ extern "C" int gdd_segment_sum_f32(int64_t n, int dim, const float* X, const flo
                                    float* wsum, gdd_stream_t stream) {
   GDD_REQUIRE(n > 0 && dim > 0 && k > 0 && X && perm && offsets && sums && wsum,
               "segment_sum_f32: bad arguments");
-  FoldArgs a{dim, 0, 0, X, w, perm, offsets, sums, wsum, nullptr, 0, nullptr, 0};
+  FoldArgs a{dim, 0, 0, 0, X, w, perm, offsets, sums, wsum, nullptr, 0, nullptr, 0};
   return fold_launch(a, k, false, to_hip(stream));
+}
+
+extern "C" int gdd_segment_sum_f32_part(int64_t n, int dim, const float* X, const float* w,
+                                        const int32_t* perm, const int32_t* offsets, int k, int c0,
+                                        int c1, float* sums_part, float* wsum_part,
+                                        gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && dim > 0 && k > 0 && 0 <= c0 && c0 <= c1 && c1 <= k && X && perm && offsets &&
+                  (c0 == c1 || (sums_part && wsum_part)),
+              "segment_sum_f32_part: bad arguments");
+  FoldArgs a{dim, 0, 0, c0, X, w, perm, offsets, sums_part, wsum_part, nullptr, 0, nullptr, 0};
+  return fold_launch(a, c1 - c0, false, to_hip(stream));
 }
 
 extern "C" int gdd_cluster_mean(int64_t n, int d, const float* feat, const int32_t* perm,
@@ -636,8 +651,19 @@ extern "C" int gdd_cluster_mean(int64_t n, int d, const float* feat, const int32
                                 long long* counts, gdd_stream_t stream) {
   GDD_REQUIRE(n > 0 && d > 0 && k > 0 && feat && perm && offsets && feat_syn,
               "cluster_mean: bad arguments");
-  FoldArgs a{d, 0, 0, feat, nullptr, perm, offsets, feat_syn, nullptr, counts, empty_as_zero, nullptr, 0};
+  FoldArgs a{d, 0, 0, 0, feat, nullptr, perm, offsets, feat_syn, nullptr, counts, empty_as_zero, nullptr, 0};
   return fold_launch(a, k, true, to_hip(stream));
+}
+
+extern "C" int gdd_cluster_mean_part(int64_t n, int d, const float* feat, const int32_t* perm,
+                                     const int32_t* offsets, int k, int c0, int c1, int empty_as_zero,
+                                     float* feat_part, long long* counts_part, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && d > 0 && k > 0 && 0 <= c0 && c0 <= c1 && c1 <= k && feat && perm && offsets &&
+                  (c0 == c1 || feat_part),
+              "cluster_mean_part: bad arguments");
+  FoldArgs a{d, 0, 0, c0, feat, nullptr, perm, offsets, feat_part, nullptr, counts_part, empty_as_zero,
+             nullptr, 0};
+  return fold_launch(a, c1 - c0, true, to_hip(stream));
 }
 
 extern "C" int gdd_average_centers(int k, int dim, float* C_new, const float* wsum,
@@ -696,7 +722,7 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
   // changed flag is kept on resume (the E-step that set it already ran)
   GDD_HIP(hipMemsetAsync(st, 0, offsetof(LloydState, changed), s));
   if (!resume) GDD_HIP(hipMemsetAsync(&st->changed, 0, sizeof(int32_t), s));
-  FoldArgs fa{dim, 0, 0, X, nullptr, perm, offsets, nullptr, wsum, nullptr, 0, &st->stop_at, 0};
+  FoldArgs fa{dim, 0, 0, 0, X, nullptr, perm, offsets, nullptr, wsum, nullptr, 0, &st->stop_at, 0};
   const unsigned cgrid = std::min<unsigned>(blocks_of(n), 2048);
   auto enqueue = [&](int i, bool phase_a) -> int {
     float* cin = (i & 1) ? C1 : C0;

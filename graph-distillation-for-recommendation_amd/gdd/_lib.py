@@ -69,6 +69,8 @@ SIGNATURES = {
     "gdd_group_ws_bytes": (_c_size, [_c_i64, _c_int]),
     "gdd_group_by_label": (_c_int, [_c_i64, _vp, _c_int, _vp, _vp, _vp, _c_size, _vp]),
     "gdd_segment_sum_f32": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp]),
+    "gdd_segment_sum_f32_part": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
+                                          _vp, _vp, _vp]),
     "gdd_segment_sum_fixed": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _c_int, _c_int, _vp, _vp,
                                        _vp]),
     "gdd_fixed_to_centers": (_c_int, [_c_int, _c_int, _vp, _vp, _c_int, _vp, _vp]),
@@ -89,6 +91,8 @@ SIGNATURES = {
     "gdd_center_columns": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "gdd_standard_scaler_transform": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "gdd_cluster_mean": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _c_int, _c_int, _vp, _vp, _vp]),
+    "gdd_cluster_mean_part": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
+                                       _vp, _vp, _vp]),
     "gdd_argmax_rows": (_c_int, [_c_int, _c_int, _vp, _vp, _vp]),
     "gdd_coo_rows": (_c_int, [_c_i64, _vp, _vp, _vp]),
     "gdd_er_ws_bytes": (_c_size, [_c_i64, _c_int]),

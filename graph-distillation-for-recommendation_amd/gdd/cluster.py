@@ -32,11 +32,12 @@ def group_by_label(labels: torch.Tensor, k: int):
     return perm, offsets
 
 
-def cluster_mean(feat: torch.Tensor, labels, k: int, empty_as_zero: bool = False):
+def cluster_mean(feat: torch.Tensor, labels, k: int, empty_as_zero: bool = False, group=None):
     """Mean feature row of every cluster -> (feat_syn [k, d] fp32, counts [k] int64).
 
     An empty cluster gives a NaN row (the reference's mean over an empty selection) unless
-    ``empty_as_zero``.
+    ``empty_as_zero``. ``group`` (a torch.distributed group with more than one rank): the clusters
+    are partitioned over the ranks and the rows all-gathered (gdd.sharded; bit-identical).
     """
     lib = _lib.device_lib()
     feat = feat.contiguous()
@@ -49,6 +50,10 @@ def cluster_mean(feat: torch.Tensor, labels, k: int, empty_as_zero: bool = False
     n, d = feat.shape
     if labels.shape[0] != n:
         raise ValueError("labels and feat disagree on the number of samples")
+    if group is not None:
+        from .sharded import sharded_cluster_mean, world_of
+        if world_of(group)[1] > 1:
+            return sharded_cluster_mean(feat, labels, k, empty_as_zero=empty_as_zero, group=group)
     perm, offsets = group_by_label(labels, k)
     out = torch.empty((k, d), dtype=torch.float32, device=dev)
     counts = torch.empty(k, dtype=torch.int64, device=dev)

@@ -205,9 +205,12 @@ class MiniBatchKMeans(_BaseKMeans):
 
     def __init__(self, n_clusters=8, *, init="k-means++", max_iter=100, batch_size=1024, verbose=0,
                  compute_labels=True, random_state=None, tol=0.0, max_no_improvement=10,
-                 init_size=None, n_init="auto", reassignment_ratio=0.01, device="cuda"):
+                 init_size=None, n_init="auto", reassignment_ratio=0.01, device="cuda", group=None):
         super().__init__(n_clusters, init=init, n_init=n_init, max_iter=max_iter, tol=tol,
                          verbose=verbose, random_state=random_state, device=device)
+        # group: a torch.distributed group over the GPUs of a node. The steps run replicated on
+        # every rank (same RandomState); the final labels pass is partitioned by rows (gdd.sharded)
+        self.group = group
         self.batch_size = batch_size
         self.compute_labels = compute_labels
         self.max_no_improvement = max_no_improvement
@@ -247,21 +250,28 @@ class MiniBatchKMeans(_BaseKMeans):
         # compute_labels: the native fit enqueues the full labels pass (:2191-2197) as soon as the
         # loop stops and leaves the per-sample distances in `sq`; their inertia (a sequential fp32
         # fold bound by its add chain) runs on a side stream, read on first access of inertia_
+        from .sharded import world_of
+        sharded = self.compute_labels and world_of(self.group)[1] > 1
+        native_labels = self.compute_labels and not sharded
         labels = sq = None
-        if self.compute_labels:
+        if native_labels:
             labels = torch.empty(n, dtype=torch.int32, device=dev)
             sq = torch.empty(n, dtype=torch.float32, device=dev)
         _lib.check(lib.gdd_minibatch_kmeans_fit(
             n, dim, Xd.data_ptr(), k, bs, int(self.max_iter), max_ni, float(self.reassignment_ratio),
-            isz, self._n_init(3), 2 if self.compute_labels else 0, ctypes.addressof(st),
+            isz, self._n_init(3), 2 if native_labels else 0, ctypes.addressof(st),
             ctypes.cast(_lib.argsort_callback, ctypes.c_void_p).value, centers.data_ptr(),
             labels.data_ptr() if labels is not None else None, sq.data_ptr() if sq is not None else None,
-            ctypes.addressof(n_steps), None if self.compute_labels else ctypes.addressof(ewa),
+            ctypes.addressof(n_steps), None if native_labels else ctypes.addressof(ewa),
             ws.data_ptr(), ws.numel(), hws.data_ptr(), hws.numel(), _lib.stream_ptr(dev)))
         st.to_random_state(rs)  # leave the generator where sklearn leaves it
         self.n_steps_ = int(n_steps.value)
         self.n_iter_ = int(np.ceil((self.n_steps_ * bs) / n))
         self.cluster_centers_device_ = centers
+        if sharded:  # the final labels pass (:2191-2197) with the rows partitioned over the ranks
+            from .sharded import sharded_labels
+            labels, sq, _ = sharded_labels(Xd, centers, group=self.group, with_inertia=True,
+                                           fold_inertia=False)
         if self.compute_labels:
             self.labels_device_ = labels
             self._inertia_async = _side_inertia(sq)

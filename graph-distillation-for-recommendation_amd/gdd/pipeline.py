@@ -26,6 +26,15 @@ from .graph import CSRGraph, induced_subgraph, normalize_adj, propagate, to_csr
 from .kmeans import KMeans, MiniBatchKMeans
 
 
+def _lloyd(n_clusters, group, **kw):
+    """KMeans on one GPU, or gdd.sharded.ShardedKMeans (rows/clusters partitioned, bit-identical)
+    when `group` spans several ranks."""
+    from .sharded import ShardedKMeans, world_of
+    if group is not None and world_of(group)[1] > 1:
+        return ShardedKMeans(n_clusters=n_clusters, group=group, **kw)
+    return KMeans(n_clusters=n_clusters, **kw)
+
+
 def standard_scaler(X, device="cuda"):
     """StandardScaler().fit_transform(X) for fp32 X -> (X_scaled, mean_ fp64, scale_ fp64)."""
     lib = _lib.device_lib()
@@ -119,7 +128,7 @@ def load_graphsaint(dataset_dir: str, dataset: str = "", device="cuda"):
 
 
 def kmeans_cluster(X, n_clusters: int, seed: int, minibatch: bool = True, batch_size: int = 2048,
-                   device="cuda", n_init="auto"):
+                   device="cuda", n_init="auto", group=None):
     """distill_recsys.kmeans_cluster on the device -> (labels int64 numpy, centres fp32 numpy).
     The reference passes ``n_init="auto"`` explicitly (distill_recsys.py:176-178), the default here."""
     if n_clusters <= 0:
@@ -130,9 +139,9 @@ def kmeans_cluster(X, n_clusters: int, seed: int, minibatch: bool = True, batch_
     Xs, _, _ = standard_scaler(X, device=device)
     if minibatch and n > 20000:
         km = MiniBatchKMeans(n_clusters=n_clusters, random_state=seed, batch_size=batch_size,
-                             n_init=n_init, device=device)
+                             n_init=n_init, device=device, group=group)
     else:
-        km = KMeans(n_clusters=n_clusters, random_state=seed, n_init=n_init, device=device)
+        km = _lloyd(n_clusters, group, random_state=seed, n_init=n_init, device=device)
     km.fit(Xs)
     return km.labels_.astype(np.int64), km.cluster_centers_.astype(np.float32)
 
@@ -145,8 +154,12 @@ def teacher_means(emb: torch.Tensor, assignment, num_clusters: int) -> torch.Ten
 
 def pretrained_clustering_hot_path(features, adj, T: int, alpha: float, logits, nnodes_syn: int,
                                    dataset: str = "", seed: int = 15, cluster_minibatch: int = 1000,
-                                   device="cuda", n_init="auto"):
+                                   device="cuda", n_init="auto", group=None):
     """The hot path of ClustGDD.pretrained_clustering.
+
+    ``group``: a torch.distributed group over the GPUs of one node — the graph is distilled once,
+    with the k-means rows and the cluster means partitioned over the ranks (gdd.sharded), results
+    bit-identical to one GPU.
 
     ``n_init``: the estimators' default. The reference constructs them without ``n_init``
     (transduct:103,105), so the count is the installed scikit-learn's default: 1 under >= 1.4
@@ -167,10 +180,10 @@ def pretrained_clustering_hot_path(features, adj, T: int, alpha: float, logits, 
     out = logits(target_feat) if callable(logits) else logits
     if dataset == "ogbn-arxiv":                                  # transduct:102-105
         km = MiniBatchKMeans(n_clusters=nnodes_syn, random_state=seed, n_init=n_init,
-                             batch_size=cluster_minibatch, device=device).fit(out)
+                             batch_size=cluster_minibatch, device=device, group=group).fit(out)
     else:
-        km = KMeans(n_clusters=nnodes_syn, n_init=n_init, device=device).fit(out)
-    feat_syn, _ = cluster_mean(target_feat, km.labels_device_, nnodes_syn)  # transduct:121-125
+        km = _lloyd(nnodes_syn, group, n_init=n_init, device=device).fit(out)
+    feat_syn, _ = cluster_mean(target_feat, km.labels_device_, nnodes_syn, group=group)  # :121-125
     labels_syn = argmax_rows(km.cluster_centers_device_)                    # transduct:126
     return feat_syn, labels_syn, km.labels_device_.to(torch.int32), adj_norm, target_feat, prop_feat
 
@@ -178,7 +191,7 @@ def pretrained_clustering_hot_path(features, adj, T: int, alpha: float, logits, 
 def pretrained_clustering_induct_hot_path(data, T: int, alpha: float, logits_train, nnodes_syn: int,
                                           dataset: str = "", seed: int = 15,
                                           cluster_minibatch: int = 1000, device="cuda",
-                                          n_init="auto"):
+                                          n_init="auto", group=None):
     """The hot path of the inductive ClustGDD.pretrained_clustering (clustgdd_agent_induct.py:37-155).
     ``n_init`` as in :func:`pretrained_clustering_hot_path` (induct:131-134 passes none).
 
@@ -203,10 +216,10 @@ def pretrained_clustering_induct_hot_path(data, T: int, alpha: float, logits_tra
     out = logits_train(targets["train"], targets["val"]) if callable(logits_train) else logits_train
     if dataset == "reddit":                                                         # :129-134
         km = MiniBatchKMeans(n_clusters=nnodes_syn, random_state=seed, batch_size=cluster_minibatch,
-                             n_init=n_init, device=device).fit(out)
+                             n_init=n_init, device=device, group=group).fit(out)
     else:
-        km = KMeans(n_clusters=nnodes_syn, n_init=n_init, device=device).fit(out)
-    feat_syn, _ = cluster_mean(targets["train"], km.labels_device_, nnodes_syn)     # :143-151
+        km = _lloyd(nnodes_syn, group, n_init=n_init, device=device).fit(out)
+    feat_syn, _ = cluster_mean(targets["train"], km.labels_device_, nnodes_syn, group=group)     # :143-151
     labels_syn = argmax_rows(km.cluster_centers_device_)                            # :152
     return (feat_syn, labels_syn, km.labels_device_.to(torch.int32), targets["train"], norms["train"],
             targets["val"], targets["test"])

@@ -1,41 +1,85 @@
-"""Range-partitioned Lloyd k-means across ranks: one all-reduce per iteration.
+"""Multi-GPU distillation of one graph over the ranks of a node (BASELINE north star).
 
-The reference runs ``KMeans(n_clusters=k).fit(X)`` on one host (clustgdd_agent_transduct.py:104-105,
-distill_recsys.py:178). For graphs whose rows are spread over the GPUs of a node, each rank holds a
-contiguous shard of X and the centres are replicated:
+Every rank holds the whole graph, the features and the k-means input: the T-hop propagation's halo
+is the whole graph after a few hops, so normalisation and propagation run
+replicated, and so do the ~260 latency-bound MiniBatchKMeans steps (same RNG on every rank). The
+k-means work that scales with n is partitioned:
 
-* init: the shards are all-gathered once and every rank runs the same k-means++ with the same
-  RandomState (sklearn _kmeans_plusplus, ``gdd_kmeans_plusplus``), so the initial centres agree
-  bit for bit without a broadcast — the one up-front exchange;
-* iteration: local MFMA assignment (``gdd_kmeans_assign``), local per-cluster sums in int64 fixed
-  point (``gdd_segment_sum_fixed``: llrint(x·2^s), exact integer adds), ONE all-reduce of
-  [k·dim sums ‖ k counts ‖ labels-changed], then ``gdd_fixed_to_centers``. Integer sums are
-  associative, so every world size — 1, 2, 4, 8 — produces the same centres and labels;
-* stop: labels unchanged on every rank (strict convergence), or Σ‖ΔC‖² ≤ tol·mean(var(X))
-  (sklearn _kmeans.py:717-734), followed by the final E-step when the stop was not strict.
+* rows: the E-step of every Lloyd iteration and the final labels pass assign rows
+  [r·m, (r+1)·m) on rank r (m = ceil(n / R)); ONE all-gather of the int32 labels (and, for the
+  inertia, of the per-sample distances) follows;
+* clusters: the Lloyd M-step sums and the cluster means are computed for clusters
+  [r·q, (r+1)·q) (q = ceil(k / R)) over ALL their members in sample order — the single-GPU order —
+  and ONE all-gather of the k-row slices follows.
 
-Scikit-learn's single-threaded fp32 M-step sums (which ``gdd.KMeans`` reproduces bit for bit on one
-GPU) cannot be split across ranks without changing their rounding; this class instead guarantees
-rank-count invariance, with centres within fp32 rounding of the sequential ones. Empty clusters
-keep their previous centre (sklearn relocates them to far points; documented deviation).
+Each value is therefore computed by the same kernel on the same operands as on one GPU:
+labels, centres, inertia, iteration counts and cluster means are bit-identical for every world
+size, and equal scikit-learn's (fixtures G3/G9) — the reference's call sites
+``clustgdd_agent_transduct.py:102-125``, ``clustgdd_agent_induct.py:131-152`` and
+``distill_recsys.py:172-180``. Empty clusters are relocated exactly as ``_relocate_empty_clusters``
+(replicated: every rank holds X, the labels and the centres).
 
-The device primitives come from an ``ops`` object: :class:`DeviceOps` (libgdd, the product path)
-by default. Tests substitute a CPU implementation of the same five methods to exercise the
-distributed logic with the gloo backend on hosts without a GPU.
+Collectives are ``torch.distributed`` all-gathers: RCCL over xGMI for device tensors (one process
+per GPU), gloo for the CPU tests (device tensors under gloo are staged through the host). The
+primitives come from an ``ops`` object — :class:`DeviceOps` (libgdd, the product path) by default;
+tests substitute a CPU stand-in with the same methods to run the distributed logic without a GPU.
 """
 from __future__ import annotations
 
 import math
-from typing import Optional
 
 import numpy as np
 import torch
 import torch.distributed as dist
 
 from . import _lib
-from .kmeans import _Ops, check_random_state
+from .kmeans import KMeans, _Ops, _same_clustering, check_random_state
 
 
+# ------------------------------------------------------------------------------------------------
+# partitions and collectives
+# ------------------------------------------------------------------------------------------------
+def world_of(group=None):
+    """(rank, world size) of `group`, (0, 1) without an initialised process group."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group)
+    return 0, 1
+
+
+def part(n: int, rank: int, world: int):
+    """Equal-chunk partition used by the all-gathers: rank r owns [r*m, min(n, (r+1)*m)), m=ceil(n/R)."""
+    m = -(-n // world) if n else 0
+    a = min(n, rank * m)
+    return a, min(n, a + m), m
+
+
+def shard_rows(n: int, rank: int, world: int):
+    """(start, stop) of `rank` in the row partition."""
+    a, b, _ = part(n, rank, world)
+    return a, b
+
+
+def all_gather_parts(t: torch.Tensor, m: int, n: int, group=None) -> torch.Tensor:
+    """Concatenate every rank's slice (rank r's first dim holds at most m rows) into the first n rows
+    of the whole, in rank order."""
+    rank, world = world_of(group)
+    if world == 1:
+        return t[:n]
+    pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[:t.shape[0]] = t
+    if t.is_cuda and dist.get_backend(group) == "nccl":
+        out = torch.empty((world * m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, pad, group=group)
+        return out[:n]
+    host = pad.cpu()
+    parts = [torch.empty_like(host) for _ in range(world)]
+    dist.all_gather(parts, host, group=group)
+    return torch.cat(parts, 0)[:n].to(t.device)
+
+
+# ------------------------------------------------------------------------------------------------
+# the device primitives (libgdd)
+# ------------------------------------------------------------------------------------------------
 class DeviceOps:
     """libgdd primitives on one device (no CPU fallback)."""
 
@@ -43,89 +87,129 @@ class DeviceOps:
         self.device = torch.device(device)
         self.lib = _lib.device_lib()
 
+    @property
+    def stream(self):
+        return _lib.stream_ptr(self.device)
+
     def tensor(self, a, dtype=None):
-        return torch.as_tensor(a, dtype=dtype, device=self.device)
+        if isinstance(a, torch.Tensor):
+            return a.to(device=self.device, dtype=dtype or a.dtype).contiguous()
+        return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=self.device)
 
-    def assign(self, X, C, labels, sq):
-        ops = _Ops(self.device, X.shape[0], C.shape[0], X.shape[1])
-        ops.assign(X, C, labels=labels, sq=sq)
-
-    def segment_sum_fixed(self, X, labels, k, scale_exp):
+    def center(self, X):
         n, dim = X.shape
-        sums = torch.zeros((k, dim), dtype=torch.int64, device=self.device)
-        counts = torch.zeros(k, dtype=torch.int64, device=self.device)
-        _lib.check(self.lib.gdd_segment_sum_fixed(n, dim, X.data_ptr(), None, labels.data_ptr(), k,
-                                                  scale_exp, sums.data_ptr(), counts.data_ptr(),
-                                                  _lib.stream_ptr(self.device)))
-        return sums, counts
-
-    def fixed_to_centers(self, sums, counts, scale_exp, C):
-        k, dim = C.shape
-        _lib.check(self.lib.gdd_fixed_to_centers(k, dim, sums.data_ptr(), counts.data_ptr(),
-                                                 scale_exp, C.data_ptr(),
-                                                 _lib.stream_ptr(self.device)))
+        Xc = torch.empty_like(X)
+        mean = torch.empty(dim, dtype=torch.float32, device=self.device)
+        var = torch.empty(dim, dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.gdd_center_columns(n, dim, X.data_ptr(), Xc.data_ptr(), mean.data_ptr(),
+                                               var.data_ptr(), self.stream))
+        return Xc, mean.cpu().numpy(), var.cpu().numpy()
 
     def kmeans_plusplus(self, X, k, rs):
-        ops = _Ops(self.device, X.shape[0], k, X.shape[1])
-        centers, _ = ops.kmeans_plusplus(X, k, rs)
+        centers, _ = _Ops(self.device, X.shape[0], k, X.shape[1]).kmeans_plusplus(X, k, rs)
         return centers
 
+    def assign(self, X, C, r0, r1, with_sq=False):
+        n = r1 - r0
+        labels = torch.empty(n, dtype=torch.int32, device=self.device)
+        sq = torch.empty(n, dtype=torch.float32, device=self.device) if with_sq else None
+        if n:
+            _Ops(self.device, n, C.shape[0], X.shape[1]).assign(X[r0:r1], C, labels=labels, sq=sq)
+        return labels, sq
 
-def _world(group):
-    if dist.is_available() and dist.is_initialized():
-        return dist.get_rank(group), dist.get_world_size(group)
-    return 0, 1
+    def group(self, labels, k):
+        from .cluster import group_by_label
+        return group_by_label(labels, k)
+
+    def mstep(self, X, grp, k, c0, c1):
+        n, dim = X.shape
+        perm, offsets = grp
+        sums = torch.empty((c1 - c0, dim), dtype=torch.float32, device=self.device)
+        wsum = torch.empty(c1 - c0, dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.gdd_segment_sum_f32_part(n, dim, X.data_ptr(), None, perm.data_ptr(),
+                                                     offsets.data_ptr(), k, c0, c1, _lib.ptr(sums),
+                                                     _lib.ptr(wsum), self.stream))
+        return sums, wsum
+
+    def relocate(self, X, C_old, sums, wsum, labels):
+        KMeans._relocate(X, C_old, sums, wsum, labels, _Ops(self.device, 1, C_old.shape[0], X.shape[1]))
+
+    def average(self, sums, wsum, C_old):
+        k, dim = sums.shape
+        C_new = sums.clone()
+        shift = torch.empty(k, dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.gdd_average_centers(k, dim, C_new.data_ptr(), wsum.data_ptr(),
+                                                C_old.data_ptr(), shift.data_ptr(), self.stream))
+        return C_new, shift
+
+    def point_sqdist(self, X, labels, C, r0, r1):
+        out = torch.empty(r1 - r0, dtype=torch.float32, device=self.device)
+        if r1 > r0:
+            _lib.check(self.lib.gdd_point_center_sqdist(r1 - r0, X.shape[1], X[r0:r1].data_ptr(),
+                                                        labels[r0:r1].data_ptr(), C.data_ptr(),
+                                                        out.data_ptr(), self.stream))
+        return out
+
+    def inertia(self, sq):
+        out = torch.empty(1, dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.gdd_inertia(sq.shape[0], sq.data_ptr(), None, out.data_ptr(), self.stream))
+        return float(out.item())
+
+    def cluster_mean(self, feat, grp, k, c0, c1, empty_as_zero):
+        n, d = feat.shape
+        perm, offsets = grp
+        out = torch.empty((c1 - c0, d), dtype=torch.float32, device=self.device)
+        counts = torch.empty(c1 - c0, dtype=torch.int64, device=self.device)
+        _lib.check(self.lib.gdd_cluster_mean_part(n, d, feat.data_ptr(), perm.data_ptr(),
+                                                  offsets.data_ptr(), k, c0, c1, int(empty_as_zero),
+                                                  _lib.ptr(out), _lib.ptr(counts), self.stream))
+        return out, counts
 
 
-def _all_reduce(t: torch.Tensor, op, group):
-    """all_reduce that also works for device tensors under gloo (staged through the host)."""
-    if not (dist.is_available() and dist.is_initialized()):
-        return t
-    if t.is_cuda and dist.get_backend(group) != "nccl":
-        h = t.cpu()
-        dist.all_reduce(h, op=op, group=group)
-        t.copy_(h)
-    else:
-        dist.all_reduce(t, op=op, group=group)
-    return t
+# ------------------------------------------------------------------------------------------------
+# partitioned labels pass and cluster means
+# ------------------------------------------------------------------------------------------------
+def sharded_labels(X, C, group=None, ops=None, with_inertia=True, fold_inertia=True):
+    """Nearest centre of every row, rows partitioned over the ranks, labels all-gathered.
+    Returns (labels int32 [n], per-sample squared distances [n], inertia) — the inertia is the
+    sequential fp32 fold over all n in sample order (sklearn _inertia_dense, one thread);
+    ``fold_inertia=False`` leaves that fold to the caller (None)."""
+    ops = ops or DeviceOps(X.device)
+    rank, world = world_of(group)
+    n = X.shape[0]
+    r0, r1, m = part(n, rank, world)
+    lab, sq = ops.assign(X, C, r0, r1, with_sq=with_inertia)
+    labels = all_gather_parts(lab, m, n, group)
+    if not with_inertia:
+        return labels, None, None
+    sq_full = all_gather_parts(sq, m, n, group)
+    return labels, sq_full, ops.inertia(sq_full) if fold_inertia else None
 
 
-def _fixed_col_sum(V: torch.Tensor, n_total: int, group) -> torch.Tensor:
-    """Column sums of V (fp64) over every rank, via int64 fixed point (exact and order-free)."""
-    amax = torch.tensor([float(V.abs().max().item()) if V.numel() else 0.0], dtype=torch.float64,
-                        device=V.device)
-    bound = max(float(_all_reduce(amax, dist.ReduceOp.MAX, group).item()), 1e-300) * max(n_total, 1)
-    s = int(min(60, 61 - math.ceil(math.log2(bound))))
-    fx = torch.round(V * (2.0 ** s)).to(torch.int64).sum(0)
-    _all_reduce(fx, dist.ReduceOp.SUM, group)
-    return fx.to(torch.float64) * (2.0 ** -s)
+def sharded_cluster_mean(feat, labels, k: int, empty_as_zero: bool = False, group=None, ops=None):
+    """gdd.cluster_mean with clusters partitioned over the ranks (bit-identical to one GPU):
+    every rank groups the (replicated) labels, folds its clusters' members in sample order, and the
+    k-row slices are all-gathered -> (feat_syn [k, d], counts [k] int64)."""
+    ops = ops or DeviceOps(feat.device)
+    rank, world = world_of(group)
+    c0, c1, q = part(k, rank, world)
+    grp = ops.group(labels, k)
+    out, counts = ops.cluster_mean(feat, grp, k, c0, c1, empty_as_zero)
+    return all_gather_parts(out, q, k, group), all_gather_parts(counts, q, k, group)
 
 
-def _all_gather_rows(X: torch.Tensor, group) -> torch.Tensor:
-    """Concatenate every rank's rows in rank order (shards may differ in length)."""
-    rank, world = _world(group)
-    if world == 1:
-        return X
-    n_local = torch.tensor([X.shape[0]], dtype=torch.int64)
-    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(sizes, n_local, group=group)
-    sizes = [int(s.item()) for s in sizes]
-    m = max(sizes)
-    host = X.detach().cpu()
-    pad = torch.zeros((m, X.shape[1]), dtype=X.dtype)
-    pad[:host.shape[0]] = host
-    parts = [torch.zeros_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad, group=group)
-    full = torch.cat([p[:s] for p, s in zip(parts, sizes)], dim=0)
-    return full.to(X.device)
-
-
+# ------------------------------------------------------------------------------------------------
+# Lloyd KMeans over the ranks
+# ------------------------------------------------------------------------------------------------
 class ShardedKMeans:
-    """KMeans(n_clusters, max_iter, tol, random_state).fit over the rows of every rank."""
+    """sklearn KMeans(n_clusters, n_init, max_iter, tol, random_state).fit (Lloyd, _kmeans.py:
+    1427-1530 / :624-752) with the E-step partitioned by rows and the M-step by clusters. ``fit``
+    takes the whole input on every rank; every rank ends with the same fitted attributes."""
 
-    def __init__(self, n_clusters=8, *, max_iter=300, tol=1e-4, random_state=None, group=None,
-                 ops=None, device="cuda"):
+    def __init__(self, n_clusters=8, *, n_init="auto", max_iter=300, tol=1e-4, random_state=None,
+                 group=None, ops=None, device="cuda"):
         self.n_clusters = n_clusters
+        self.n_init = n_init
         self.max_iter = max_iter
         self.tol = tol
         self.random_state = random_state
@@ -133,77 +217,67 @@ class ShardedKMeans:
         self.ops = ops
         self.device = device
 
-    def fit(self, X_local):
+    def fit(self, X, y=None, sample_weight=None):
+        if sample_weight is not None and not np.all(np.asarray(sample_weight) == 1):
+            raise NotImplementedError("non-unit sample_weight is not used by the reference")
         ops = self.ops or DeviceOps(self.device)
         group = self.group
-        X = ops.tensor(np.ascontiguousarray(X_local, dtype=np.float32)
-                       if not isinstance(X_local, torch.Tensor) else X_local, dtype=torch.float32)
-        X = X.contiguous()
-        n_local, dim = X.shape
+        X = ops.tensor(X, dtype=torch.float32)
+        n, dim = X.shape
         k = self.n_clusters
-        SUM, MAX = dist.ReduceOp.SUM, dist.ReduceOp.MAX
-        nt = torch.tensor([n_local], dtype=torch.int64, device=X.device)
-        n_total = int(_all_reduce(nt, SUM, group).item())
-        if k > n_total:
-            raise ValueError(f"n_samples={n_total} should be >= n_clusters={k}.")
-        # global column mean and mean(var(X)) from fixed-point integer sums: exact, so identical
-        # for every partition of the rows (sklearn centres X by its mean, _kmeans.py:1480-1484)
-        mean = _fixed_col_sum(X.to(torch.float64), n_total, group) / n_total
-        Xc = (X.to(torch.float64) - mean).to(torch.float32).contiguous()
-        var = _fixed_col_sum(Xc.to(torch.float64) ** 2, n_total, group) / n_total
-        tol_ = float(var.mean().item()) * self.tol
-        # fixed-point scale of the M-step sums: |x| * n_total * 2^s < 2^62
-        amax = torch.tensor([float(Xc.abs().max().item()) if n_local else 0.0],
-                            dtype=torch.float64, device=X.device)
-        bound = max(float(_all_reduce(amax, MAX, group).item()), 1e-30) * n_total
-        scale_exp = int(min(60, 61 - math.ceil(math.log2(bound))))
-        # replicated k-means++ on the gathered rows (same RandomState on every rank)
+        if k > n:
+            raise ValueError(f"n_samples={n} should be >= n_clusters={k}.")
+        rank, world = world_of(group)
+        r0, r1, m = part(n, rank, world)
+        c0, c1, q = part(k, rank, world)
         rs = check_random_state(self.random_state)
-        X_full = _all_gather_rows(Xc, group)
-        C = ops.kmeans_plusplus(X_full, k, rs).contiguous()
-        del X_full
-        labels = ops.tensor(torch.zeros(n_local, dtype=torch.int32), dtype=torch.int32)
-        labels_old = ops.tensor(torch.full((n_local,), -1, dtype=torch.int32), dtype=torch.int32)
-        sq = ops.tensor(torch.zeros(n_local, dtype=torch.float32), dtype=torch.float32)
-        strict = False
-        it = 0
-        for it in range(self.max_iter):
-            ops.assign(Xc, C, labels, sq)
-            sums, counts = ops.segment_sum_fixed(Xc, labels, k, scale_exp)
-            changed = int(bool((labels != labels_old).any().item())) if n_local else 0
-            pack = torch.cat([sums.reshape(-1), counts,
-                              torch.tensor([changed], dtype=torch.int64, device=sums.device)])
-            _all_reduce(pack, SUM, group)
-            sums = pack[:k * dim].reshape(k, dim).contiguous()
-            counts = pack[k * dim:k * dim + k].contiguous()
-            any_changed = int(pack[-1].item()) > 0
-            if not any_changed:
-                strict = True  # labels identical to the previous iteration's on every rank
-                break
-            C_new = C.clone()
-            ops.fixed_to_centers(sums, counts, scale_exp, C_new)
-            shift = float(((C_new.to(torch.float64) - C.to(torch.float64)) ** 2).sum().item())
-            C = C_new
-            labels_old.copy_(labels)
-            if shift <= tol_:
-                break
-        if not strict:
-            ops.assign(Xc, C, labels, sq)  # final E-step (_kmeans.py:736-747)
-        inertia = torch.tensor([float(sq.to(torch.float64).sum().item())], dtype=torch.float64,
-                               device=X.device)
-        _all_reduce(inertia, SUM, group)
-        self.n_iter_ = it + 1
+        # centring and _tolerance on the whole (replicated) input, numpy's orders (:1476-1487, :279-288)
+        Xc, X_mean, var = ops.center(X)
+        tol_ = 0 if self.tol == 0 else np.mean(var) * self.tol
+        n_init = 1 if self.n_init == "auto" else int(self.n_init)
+        best = None
+        for _ in range(n_init):
+            C = ops.kmeans_plusplus(Xc, k, rs)  # same RandomState on every rank: same centres
+            labels_old = None
+            strict = False
+            it = 0
+            for it in range(self.max_iter):  # _kmeans_single_lloyd
+                lab, _ = ops.assign(Xc, C, r0, r1)
+                labels = all_gather_parts(lab, m, n, group)
+                grp = ops.group(labels, k)
+                sp_, wp = ops.mstep(Xc, grp, k, c0, c1)
+                sums = all_gather_parts(sp_, q, k, group).contiguous()
+                wsum = all_gather_parts(wp, q, k, group).contiguous()
+                if bool((wsum == 0).any()):
+                    ops.relocate(Xc, C, sums, wsum, labels)  # replicated, identical on every rank
+                C, shift = ops.average(sums, wsum, C)
+                if labels_old is not None and torch.equal(labels, labels_old):
+                    strict = True
+                    break
+                if (shift.cpu().numpy() ** 2).sum() <= tol_:
+                    break
+                labels_old = labels
+            if not strict:  # the final E-step with the last centres (:736-747)
+                lab, _ = ops.assign(Xc, C, r0, r1)
+                labels = all_gather_parts(lab, m, n, group)
+            sq = all_gather_parts(ops.point_sqdist(Xc, labels, C, r0, r1), m, n, group)
+            inertia = ops.inertia(sq)
+            lab_h = labels.cpu().numpy()
+            if best is None or (inertia < best[1] and not _same_clustering(lab_h, best[0], k)):
+                best = (lab_h, inertia, C.clone(), it + 1, labels)
+        lab_h, inertia, C, n_iter, labels = best
+        self.labels_ = lab_h
         self.labels_device_ = labels
-        self.cluster_centers_device_ = (C.to(torch.float64) + mean).to(torch.float32)
-        self.labels_ = labels.cpu().numpy()
-        self.cluster_centers_ = self.cluster_centers_device_.cpu().numpy()
-        self.inertia_ = float(inertia.item())
-        self.scale_exp_ = scale_exp
+        self.inertia_ = inertia
+        self.cluster_centers_ = C.cpu().numpy() + X_mean
+        self.cluster_centers_device_ = ops.tensor(self.cluster_centers_, dtype=torch.float32)
+        self.n_iter_ = n_iter
         return self
 
+    def fit_predict(self, X, y=None, sample_weight=None):
+        return self.fit(X, sample_weight=sample_weight).labels_
 
-def shard_rows(n: int, rank: int, world: int):
-    """Contiguous range partition of n rows: (start, stop) of `rank`."""
-    base, extra = divmod(n, world)
-    start = rank * base + min(rank, extra)
-    return start, start + base + (1 if rank < extra else 0)
+
+def fixed_point_scale(bound: float) -> int:
+    """Largest s with bound * 2^s < 2^61 (kept for gdd_segment_sum_fixed callers)."""
+    return int(min(60, 61 - math.ceil(math.log2(max(bound, 1e-300)))))

@@ -209,6 +209,12 @@ int gdd_group_by_label(int64_t n, const int32_t* labels, int k, int32_t* perm, i
 int gdd_segment_sum_f32(int64_t n, int dim, const float* X, const float* w, const int32_t* perm,
                         const int32_t* offsets, int k, float* sums, float* wsum, gdd_stream_t stream);
 
+/* The same sums for clusters [c0, c1) only, written as a slice (row c - c0): the cluster-partitioned */
+/* M-step of the multi-GPU Lloyd loop (gdd/sharded.py), bit-identical to the full call's rows.        */
+int gdd_segment_sum_f32_part(int64_t n, int dim, const float* X, const float* w, const int32_t* perm,
+                             const int32_t* offsets, int k, int c0, int c1, float* sums_part,
+                             float* wsum_part, gdd_stream_t stream);
+
 /* Order-independent accumulation for sharded k-means: sums_fx[c,j] += llrint(X[i,j]*w_i * 2^scale)   */
 /* (int64, exact integer adds => identical on any rank count / order), counts[c] += 1. Zero both     */
 /* outputs first. rows == NULL: rows 0..n-1.                                                        */
@@ -306,6 +312,11 @@ int gdd_standard_scaler_transform(int64_t n, int dim, const float* X, const doub
 int gdd_cluster_mean(int64_t n, int d, const float* feat, const int32_t* perm, const int32_t* offsets,
                      int k, int empty_as_zero, float* feat_syn, long long* counts,
                      gdd_stream_t stream);
+/* gdd_cluster_mean for clusters [c0, c1) only, written as a slice (row c - c0): the cluster-         */
+/* partitioned cluster mean of the multi-GPU path, bit-identical to the full call's rows.             */
+int gdd_cluster_mean_part(int64_t n, int d, const float* feat, const int32_t* perm,
+                          const int32_t* offsets, int k, int c0, int c1, int empty_as_zero,
+                          float* feat_part, long long* counts_part, gdd_stream_t stream);
 /* labels_syn[c] = argmax_j centers[c,j] (first max wins, torch.argmax; transduct:126).              */
 int gdd_argmax_rows(int k, int dim, const float* centers, int64_t* out, gdd_stream_t stream);
 

@@ -1,5 +1,5 @@
-"""Test helpers for gdd.sharded: a CPU stand-in for the device primitives (the oracle's arithmetic,
-test-only) and a gloo process-group runner."""
+"""Test helpers for gdd.sharded: a CPU stand-in for the device primitives (the oracle's arithmetic and
+numpy's, test-only) and a gloo process-group runner."""
 import os
 import socket
 
@@ -9,36 +9,68 @@ import torch
 from oracle import oracle as O
 
 
+def _np(t):
+    return t.numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+
+
 class OracleOps:
-    """The five primitives ShardedKMeans needs, computed by the oracle on the host."""
+    """The primitives gdd.sharded needs, computed on the host by the oracle (scikit-learn's orders)."""
 
     device = torch.device("cpu")
 
     def tensor(self, a, dtype=None):
-        return torch.as_tensor(a, dtype=dtype)
+        if isinstance(a, torch.Tensor):
+            return a.to(dtype=dtype or a.dtype).contiguous()
+        return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype)
 
-    def assign(self, X, C, labels, sq):
-        lab, s = O.assign(X.numpy(), C.numpy())
-        labels.copy_(torch.from_numpy(lab))
-        sq.copy_(torch.from_numpy(s))
-
-    def segment_sum_fixed(self, X, labels, k, scale_exp):
-        v = np.rint(X.numpy().astype(np.float64) * (2.0 ** scale_exp)).astype(np.int64)
-        sums = np.zeros((k, X.shape[1]), np.int64)
-        np.add.at(sums, labels.numpy(), v)
-        counts = np.bincount(labels.numpy(), minlength=k).astype(np.int64)
-        return torch.from_numpy(sums), torch.from_numpy(counts)
-
-    def fixed_to_centers(self, sums, counts, scale_exp, C):
-        s, c = sums.numpy().astype(np.float64), counts.numpy()
-        m = c > 0
-        vals = ((s * (2.0 ** -scale_exp))[m] / c[m, None]).astype(np.float32)
-        Cn = C.numpy()
-        Cn[m] = vals
+    def center(self, X):
+        x = _np(X)
+        mean = x.mean(axis=0)
+        return torch.from_numpy(x - mean), mean, np.var(x, axis=0)
 
     def kmeans_plusplus(self, X, k, rs):
-        centers, _ = O.kmeans_plusplus(X.numpy(), k, rs)
+        centers, _ = O.kmeans_plusplus(_np(X), k, rs)
         return torch.from_numpy(centers)
+
+    def assign(self, X, C, r0, r1, with_sq=False):
+        if r1 <= r0:
+            return torch.zeros(0, dtype=torch.int32), torch.zeros(0, dtype=torch.float32)
+        lab, sq = O.assign(_np(X)[r0:r1], _np(C))
+        return torch.from_numpy(lab), torch.from_numpy(sq) if with_sq else None
+
+    def group(self, labels, k):
+        return _np(labels).astype(np.int32)
+
+    def mstep(self, X, grp, k, c0, c1):
+        x = np.ascontiguousarray(_np(X), np.float32)
+        sums = np.empty((k, x.shape[1]), np.float32)
+        wic = np.empty(k, np.float32)
+        O.lib().oracle_segment_sum_f32(x.shape[0], x.shape[1], x, None, grp, k, sums, wic)
+        return torch.from_numpy(sums[c0:c1].copy()), torch.from_numpy(wic[c0:c1].copy())
+
+    def relocate(self, X, C_old, sums, wsum, labels):
+        s, w = sums.numpy(), wsum.numpy()  # views: modified in place
+        O._relocate_empty(_np(X), _np(C_old), s, w, _np(labels))
+
+    def average(self, sums, wsum, C_old):
+        cn = np.ascontiguousarray(_np(sums), np.float32).copy()
+        shift = np.empty(cn.shape[0], np.float32)
+        O.lib().oracle_average_centers(cn.shape[0], cn.shape[1], cn, _np(wsum), _np(C_old),
+                                       shift.ctypes.data_as(O.vp))
+        return torch.from_numpy(cn), torch.from_numpy(shift)
+
+    def point_sqdist(self, X, labels, C, r0, r1):
+        if r1 <= r0:
+            return torch.zeros(0, dtype=torch.float32)
+        return torch.from_numpy(O.labels_sqdist(_np(X)[r0:r1], _np(C), _np(labels)[r0:r1]))
+
+    def inertia(self, sq):
+        s = np.ascontiguousarray(_np(sq), np.float32)
+        return float(O.lib().oracle_inertia(s.shape[0], s, None))
+
+    def cluster_mean(self, feat, grp, k, c0, c1, empty_as_zero):
+        out, counts = O.cluster_mean(_np(feat), grp, k, empty_as_zero=empty_as_zero)
+        return torch.from_numpy(out[c0:c1].copy()), torch.from_numpy(counts[c0:c1].copy())
 
 
 def free_port():

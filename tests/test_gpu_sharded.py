@@ -1,5 +1,7 @@
-"""ShardedKMeans on the device primitives: equal to the oracle-backed run bit for bit, and the same
-for 1 and 2 ranks (two processes sharing cuda:0 over gloo; RCCL needs one GPU per rank)."""
+"""The multi-GPU path on the device primitives (gdd.sharded): one rank equals gdd.KMeans and the
+sklearn fixtures bit for bit; two ranks (two processes sharing cuda:0 over gloo — RCCL needs one GPU
+per rank, and this box has one) equal one rank for ShardedKMeans, the partitioned MiniBatchKMeans
+labels pass and the partitioned cluster means."""
 import os
 import sys
 
@@ -12,44 +14,69 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
+import gdd  # noqa: E402
 from gdd import synth  # noqa: E402
-from gdd.sharded import ShardedKMeans, shard_rows  # noqa: E402
-from sharded_util import OracleOps, free_port, init_gloo  # noqa: E402
+from gdd.sharded import ShardedKMeans  # noqa: E402
+from golden_util import load  # noqa: E402
+from sharded_util import free_port  # noqa: E402
 
 
 def _bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
-def test_device_ops_match_oracle_ops():
-    X = synth.blobs(4000, 24, 16, seed=4)
-    d = ShardedKMeans(n_clusters=16, random_state=9, device="cuda:0").fit(X)
-    o = ShardedKMeans(n_clusters=16, random_state=9, ops=OracleOps()).fit(X)
-    assert d.n_iter_ == o.n_iter_
-    assert np.array_equal(d.labels_, o.labels_)
-    assert np.array_equal(_bits(d.cluster_centers_), _bits(o.cluster_centers_))
+def test_one_rank_equals_kmeans_and_sklearn():
+    z = load("golden_kmeans.npz")
+    X = z["km_X"]
+    np.random.seed(15)
+    s = ShardedKMeans(n_clusters=70, n_init=10, device="cuda:0").fit(X)
+    np.random.seed(15)
+    m = gdd.KMeans(n_clusters=70, n_init=10).fit(X)
+    assert s.n_iter_ == m.n_iter_ == int(z["km10_n_iter"])
+    assert np.array_equal(s.labels_, m.labels_) and np.array_equal(s.labels_, z["km10_labels"])
+    assert np.array_equal(_bits(s.cluster_centers_), _bits(z["km10_centers"]))
+    assert s.inertia_ == m.inertia_ == float(z["km10_inertia"])
 
 
-def _worker(rank, world, port, X, out):
+def _worker(rank, world, port, X, Xm, feat, out):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE),
                                                           "graph-distillation-for-recommendation_amd"), HERE]
     import torch.distributed as dist
-    from gdd.sharded import ShardedKMeans as SK, shard_rows as sr
-    from sharded_util import init_gloo as ig
-    ig(rank, world, port)
-    a, b = sr(X.shape[0], rank, world)
-    m = SK(n_clusters=16, random_state=9, device="cuda:0").fit(X[a:b])
-    np.savez(os.path.join(out, f"r{rank}.npz"), labels=m.labels_, centers=m.cluster_centers_)
+    import gdd as G
+    from gdd.sharded import ShardedKMeans as SK
+    from sharded_util import init_gloo
+    init_gloo(rank, world, port)
+    g = dist.group.WORLD
+    np.random.seed(15)
+    m = SK(n_clusters=40, device="cuda:0", group=g).fit(X)
+    mb = G.MiniBatchKMeans(n_clusters=30, random_state=15, batch_size=500, device="cuda:0", group=g).fit(Xm)
+    fs, cnt = G.cluster_mean(torch.from_numpy(feat).cuda(), mb.labels_device_, 30, group=g)
+    np.savez(os.path.join(out, f"r{rank}.npz"), labels=m.labels_, centers=m.cluster_centers_,
+             n_iter=m.n_iter_, inertia=m.inertia_, mb_labels=mb.labels_, mb_inertia=mb.inertia_,
+             mb_centers=mb.cluster_centers_, mean=fs.cpu().numpy(), counts=cnt.cpu().numpy())
     dist.destroy_process_group()
 
 
 def test_two_ranks_match_one():
-    X = synth.blobs(4000, 24, 16, seed=4)
-    one = ShardedKMeans(n_clusters=16, random_state=9, device="cuda:0").fit(X)
+    X = synth.blobs(20000, 24, 40, seed=4)
+    X[1::9] = X[0]
+    Xm = synth.blobs(12000, 16, 30, seed=6)
+    feat = synth.features(12000, 100, 6)
+    np.random.seed(15)
+    one = gdd.KMeans(n_clusters=40).fit(X)
+    mb = gdd.MiniBatchKMeans(n_clusters=30, random_state=15, batch_size=500).fit(Xm)
+    fs, cnt = gdd.cluster_mean(torch.from_numpy(feat).cuda(), mb.labels_device_, 30)
     out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"gdd_sharded_{os.getpid()}")
     os.makedirs(out, exist_ok=True)
-    mp.spawn(_worker, args=(2, free_port(), X, out), nprocs=2, join=True)
-    parts = [np.load(os.path.join(out, f"r{r}.npz")) for r in range(2)]
-    assert np.array_equal(np.concatenate([p["labels"] for p in parts]), one.labels_)
-    for p in parts:
+    mp.spawn(_worker, args=(2, free_port(), X, Xm, feat, out), nprocs=2, join=True)
+    for r in range(2):
+        p = np.load(os.path.join(out, f"r{r}.npz"))
+        assert int(p["n_iter"]) == one.n_iter_
+        assert np.array_equal(p["labels"], one.labels_)
         assert np.array_equal(_bits(p["centers"]), _bits(one.cluster_centers_))
+        assert float(p["inertia"]) == one.inertia_
+        assert np.array_equal(p["mb_labels"], mb.labels_)
+        assert float(p["mb_inertia"]) == mb.inertia_
+        assert np.array_equal(_bits(p["mb_centers"]), _bits(mb.cluster_centers_))
+        assert np.array_equal(p["counts"], cnt.cpu().numpy())
+        assert np.array_equal(_bits(p["mean"]), _bits(fs.cpu().numpy()))

@@ -1,8 +1,10 @@
-"""ShardedKMeans across world_size 2 with the gloo backend on CPU.
+"""The multi-GPU path's distributed logic at world size 1 and 2 with the gloo backend on CPU
+(SURVEY §8(e)): rows partitioned for the E-step / labels pass, clusters for the M-step / means.
 
-The distributed logic — range partition, fixed-point all-reduce, global stop tests, replicated
-k-means++ — runs with the oracle's primitives standing in for the device ones, so the check needs
-no GPU: 1 rank and 2 ranks must give identical labels and bit-identical centres.
+The oracle's primitives stand in for the device ones (tests/sharded_util.OracleOps), so no GPU is
+needed. Every result must be bit-identical across world sizes AND equal to scikit-learn's own
+(fixture G3: KMeans with n_init 1 and 10 on the global RNG, the agents' call) — the partition only
+changes who computes a value, never how.
 """
 import os
 import sys
@@ -12,56 +14,133 @@ import pytest
 import torch.multiprocessing as mp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
 
 
-def _worker(rank, world, port, X, k, seed, out_dir):
-    sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE),
-                                                          "graph-distillation-for-recommendation_amd"), HERE]
+def _paths():
+    for p in (ROOT, os.path.join(ROOT, "graph-distillation-for-recommendation_amd"), HERE):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _worker(rank, world, port, job, out_dir):
+    _paths()
+    import torch
     import torch.distributed as dist
-    from gdd.sharded import ShardedKMeans, shard_rows
+    from gdd import sharded
     from sharded_util import OracleOps, init_gloo
+    from oracle import oracle as O
     init_gloo(rank, world, port)
-    a, b = shard_rows(X.shape[0], rank, world)
-    m = ShardedKMeans(n_clusters=k, random_state=seed, ops=OracleOps()).fit(X[a:b])
-    np.savez(os.path.join(out_dir, f"r{rank}.npz"), labels=m.labels_, centers=m.cluster_centers_,
-             n_iter=m.n_iter_, inertia=m.inertia_)
+    ops = OracleOps()
+    kind, args = job
+    res = {}
+    if kind == "kmeans":
+        X, k, n_init, seed = args
+        if seed is None:
+            np.random.seed(15)
+        m = sharded.ShardedKMeans(n_clusters=k, n_init=n_init, random_state=seed, ops=ops).fit(X)
+        res = dict(labels=m.labels_, centers=m.cluster_centers_, n_iter=m.n_iter_, inertia=m.inertia_)
+    elif kind == "labels_mean":
+        X, C, feat, k = args
+        lab, sq, inertia = sharded.sharded_labels(torch.from_numpy(X), torch.from_numpy(C), ops=ops)
+        fs, cnt = sharded.sharded_cluster_mean(torch.from_numpy(feat), lab, k, ops=ops)
+        fz, _ = sharded.sharded_cluster_mean(torch.from_numpy(feat), lab, k, empty_as_zero=True, ops=ops)
+        res = dict(labels=lab.numpy(), sq=sq.numpy(), inertia=inertia, mean=fs.numpy(),
+                   counts=cnt.numpy(), mean0=fz.numpy())
+    elif kind == "minibatch":
+        # MiniBatchKMeans as the multi-GPU path runs it: replicated steps (same RandomState on every
+        # rank), then the partitioned final labels pass
+        X, k = args
+        r = O.minibatch_kmeans(X, k, random_state=15, batch_size=500, compute_labels=False)
+        lab, sq, inertia = sharded.sharded_labels(torch.from_numpy(X),
+                                                  torch.from_numpy(r["cluster_centers_"]), ops=ops)
+        res = dict(labels=lab.numpy(), inertia=inertia, centers=r["cluster_centers_"])
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     dist.destroy_process_group()
 
 
-def _run(world, X, k, seed, tmp):
+def _run(world, job, tmp):
     from sharded_util import free_port
-    port = free_port()
     os.makedirs(tmp, exist_ok=True)
-    mp.spawn(_worker, args=(world, port, X, k, seed, str(tmp)), nprocs=world, join=True)
-    parts = [np.load(os.path.join(tmp, f"r{r}.npz")) for r in range(world)]
-    labels = np.concatenate([p["labels"] for p in parts])
-    for p in parts[1:]:
-        assert np.array_equal(p["centers"].view(np.uint32), parts[0]["centers"].view(np.uint32))
-        assert int(p["n_iter"]) == int(parts[0]["n_iter"])
-    return labels, parts[0]["centers"], int(parts[0]["n_iter"]), float(parts[0]["inertia"])
+    mp.spawn(_worker, args=(world, free_port(), job, str(tmp)), nprocs=world, join=True)
+    parts = [dict(np.load(os.path.join(tmp, f"r{r}.npz"))) for r in range(world)]
+    for p in parts[1:]:  # every rank ends with the same result
+        for key in p:
+            assert np.array_equal(np.atleast_1d(p[key]).view(np.uint8), np.atleast_1d(parts[0][key]).view(np.uint8)), key
+    return parts[0]
 
 
-@pytest.mark.parametrize("n,dim,k", [(3001, 8, 12), (1500, 40, 30)])
-def test_sharded_lloyd_rank_count_invariant(tmp_path, n, dim, k):
-    sys.path.insert(0, HERE)
-    from gdd import synth
-    X = synth.blobs(n, dim, k, seed=5)
-    l1, c1, it1, in1 = _run(1, X, k, 7, tmp_path / "w1")
-    l2, c2, it2, in2 = _run(2, X, k, 7, tmp_path / "w2")
-    assert it1 == it2
-    assert np.array_equal(l1, l2)
-    assert np.array_equal(c1.view(np.uint32), c2.view(np.uint32))
-    assert abs(in1 - in2) <= 1e-9 * max(1.0, abs(in1))
+def _same(a, b):
+    assert a.keys() == b.keys()
+    for key in a:
+        assert np.array_equal(np.atleast_1d(a[key]).view(np.uint8), np.atleast_1d(b[key]).view(np.uint8)), key
 
 
-def test_sharded_lloyd_close_to_sklearn_semantics(tmp_path):
-    # same k-means++ draws and Lloyd iterations as the single-host reference; only the M-step sum
-    # order differs (fixed point vs sequential fp32), so well-separated blobs give the same labels
-    sys.path.insert(0, HERE)
+@pytest.mark.parametrize("n_init", [1, 10])
+def test_sharded_lloyd_equals_sklearn_fixture(tmp_path, n_init):
+    _paths()
+    from golden_util import load
+    z = load("golden_kmeans.npz")
+    X = z["km_X"]
+    one = _run(1, ("kmeans", (X, 70, n_init, None)), tmp_path / "w1")
+    two = _run(2, ("kmeans", (X, 70, n_init, None)), tmp_path / "w2")
+    _same(one, two)
+    tag = f"km{n_init}"
+    assert int(two["n_iter"]) == int(z[f"{tag}_n_iter"])
+    assert np.array_equal(two["labels"], z[f"{tag}_labels"])
+    assert np.array_equal(two["centers"].view(np.uint32), z[f"{tag}_centers"].view(np.uint32))
+    assert float(two["inertia"]) == float(z[f"{tag}_inertia"])
+
+
+@pytest.mark.parametrize("n,dim,k", [(3001, 8, 12), (50, 4, 50), (300, 3, 12)])
+def test_sharded_lloyd_equals_oracle_incl_relocation(tmp_path, n, dim, k):
+    # (50, 4, 50): duplicated rows and k = n, so clusters empty out and are relocated / copied
+    _paths()
     from gdd import synth
     from oracle import oracle as O
-    X = synth.blobs(2000, 16, 10, seed=11)
-    l2, c2, _, _ = _run(2, X, 10, 3, tmp_path)
-    ref = O.kmeans(X, 10, random_state=3, n_init=1)
-    assert np.array_equal(l2, ref["labels_"])
-    np.testing.assert_allclose(c2, ref["cluster_centers_"], rtol=1e-5, atol=1e-5)
+    X = synth.blobs(n, dim, max(1, k // 3), seed=n)
+    X[1::7] = X[0]
+    ref = O.kmeans(X, k, random_state=7)
+    one = _run(1, ("kmeans", (X, k, 1, 7)), tmp_path / "w1")
+    two = _run(2, ("kmeans", (X, k, 1, 7)), tmp_path / "w2")
+    _same(one, two)
+    assert int(two["n_iter"]) == ref["n_iter_"]
+    assert np.array_equal(two["labels"], ref["labels_"])
+    assert np.array_equal(two["centers"].view(np.uint32), ref["cluster_centers_"].view(np.uint32))
+    assert float(two["inertia"]) == ref["inertia_"]
+
+
+def test_sharded_labels_pass_and_cluster_means(tmp_path):
+    _paths()
+    from gdd import synth
+    from oracle import oracle as O
+    X = synth.blobs(4001, 40, 60, seed=3)
+    C = X[:61].copy()
+    C[17] += 1e4  # a centre nobody picks: an empty cluster (NaN mean, zero with empty_as_zero)
+    feat = synth.features(4001, 33, 3)
+    one = _run(1, ("labels_mean", (X, C, feat, 61)), tmp_path / "w1")
+    two = _run(2, ("labels_mean", (X, C, feat, 61)), tmp_path / "w2")
+    _same(one, two)
+    lab, inertia = O.labels_inertia(X, C)
+    assert np.array_equal(two["labels"], lab)
+    assert float(two["inertia"]) == inertia
+    ref, cnt = O.cluster_mean(feat, lab, 61)
+    assert cnt[17] == 0
+    assert np.array_equal(two["counts"], cnt)
+    assert np.array_equal(two["mean"].view(np.uint32), ref.view(np.uint32))
+    ref0, _ = O.cluster_mean(feat, lab, 61, empty_as_zero=True)
+    assert np.array_equal(two["mean0"].view(np.uint32), ref0.view(np.uint32))
+
+
+def test_sharded_minibatch_labels_equal_sklearn_order(tmp_path):
+    _paths()
+    from gdd import synth
+    from oracle import oracle as O
+    X = synth.blobs(6000, 12, 40, seed=8)
+    ref = O.minibatch_kmeans(X, 40, random_state=15, batch_size=500)
+    one = _run(1, ("minibatch", (X, 40)), tmp_path / "w1")
+    two = _run(2, ("minibatch", (X, 40)), tmp_path / "w2")
+    _same(one, two)
+    assert np.array_equal(two["labels"], ref["labels_"])
+    assert float(two["inertia"]) == ref["inertia_"]
+    assert np.array_equal(two["centers"].view(np.uint32), ref["cluster_centers_"].view(np.uint32))
