@@ -115,79 +115,107 @@ extern "C" int gdd_standard_scaler_transform(int64_t n, int dim, const float* X,
 namespace gdd {
 namespace {
 
-// dim > 1. Workgroup b owns columns [256 b, 256 b + w) and folds all rows of them twice (mean, then
-// (x - mean)^2 while writing x - mean): chunks of R = kColLds / w rows are staged through two LDS
-// buffers (element e of a chunk = row e / w, column e % w, so the LDS image is the chunk's linear
-// index) with the next chunk in flight in registers while thread j < w folds column j. The n-long
-// fp32 chains bound it, not HBM.
-constexpr int kColLds = 12288;        // floats per LDS buffer
-constexpr int kColP = kColLds / 256;  // staged elements per thread per chunk
-__global__ __launch_bounds__(256) void k_col_stats(int64_t n, int dim, const float* __restrict__ X,
-                                                   float* __restrict__ X_out, float* __restrict__ mean,
-                                                   float* __restrict__ var) {
-  extern __shared__ __attribute__((aligned(16))) float sb[];
-  const int tid = threadIdx.x;
-  const int c0 = blockIdx.x * 256, w = min(256, dim - c0);
-  const int R = kColLds / w;
-  int rel[kColP];  // chunk-relative offsets of this thread's staged elements: row * dim + c0 + column
-  {
-    int r = tid / w, col = tid % w;
-    const int dr = 256 / w, dc = 256 % w;
+// dim > 1. Each column's sums are sequential fp32 chains over all n rows, so the kernel is bound by
+// the add chain (one dependent v_add_f32 per row) as long as rows arrive fast enough. Workgroup g
+// owns columns [8g, 8g + w): chunks of 1024 rows x 8 columns are staged through two LDS buffers (the
+// next chunk's loads in flight in registers while lane j of wave 0 folds column j with 16 LDS reads
+// ahead of its adds), then, in the second pass, every thread writes its staged elements of x - mean.
+// Only blocks with blockIdx % 8 == 0 work: they share one XCD's L2 under the observed round-robin
+// placement, so X's lines come from HBM once for all column groups (speed only, not correctness).
+constexpr int kCW = 8;                     // columns per workgroup
+constexpr int kCR = 1024;                  // rows per staged chunk
+constexpr int kCQ = kCR * kCW / 256;       // staged elements per thread per chunk
+constexpr int kColXcd = 8;
+
+__device__ __forceinline__ float col_fold(const float* __restrict__ col, int rows, int pass, float m,
+                                          float acc) {
+  // rows of this chunk, stride kCW; 16 LDS reads in flight ahead of the dependent adds
+  int r = 0;
+  for (; r + 16 <= rows; r += 16) {
+    float v[16];
 #pragma unroll
-    for (int q = 0; q < kColP; ++q) {
-      rel[q] = r * dim + c0 + col;
-      r += dr;
-      col += dc;
-      if (col >= w) {
-        col -= w;
-        ++r;
+    for (int u = 0; u < 16; ++u) v[u] = col[(r + u) * kCW];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (pass == 0) {
+        acc = acc + v[u];
+      } else {
+        const float d = v[u] - m;
+        acc = acc + d * d;
       }
     }
   }
-  float v[kColP];
-  auto fetch = [&](int64_t row0) {
-    const int64_t lim = min((int64_t)R, n - row0) * w;  // valid elements in this chunk
-    const float* base = X + row0 * dim;
+  for (; r < rows; ++r) {
+    const float x = col[r * kCW];
+    if (pass == 0) {
+      acc = acc + x;
+    } else {
+      const float d = x - m;
+      acc = acc + d * d;
+    }
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void k_col_stats(int64_t n, int dim, const float* __restrict__ X,
+                                                   float* __restrict__ X_out, float* __restrict__ mean,
+                                                   float* __restrict__ var) {
+  if (blockIdx.x % kColXcd) return;
+  __shared__ __attribute__((aligned(16))) float buf[2][kCR * kCW];
+  __shared__ float s_m[kCW];
+  const int tid = threadIdx.x;
+  const int c0 = (int)(blockIdx.x / kColXcd) * kCW, w = min(kCW, dim - c0);
+  float v[kCQ];
+  // unconditional loads at clamped addresses; rows >= n and columns >= w are never folded or written
+  auto fetch = [&](int64_t r0) {
 #pragma unroll
-    for (int q = 0; q < kColP; ++q)
-      if (tid + 256 * q < lim) v[q] = base[rel[q]];
+    for (int q = 0; q < kCQ; ++q) {
+      const int e = tid + 256 * q;
+      const int64_t row = min(r0 + (e >> 3), n - 1);
+      const int c = min(e & (kCW - 1), w - 1);
+      v[q] = X[row * dim + c0 + c];
+    }
+  };
+  auto store = [&](int slot) {
+#pragma unroll
+    for (int q = 0; q < kCQ; ++q) buf[slot][tid + 256 * q] = v[q];
   };
   float m = 0.f;
   for (int pass = 0; pass < 2; ++pass) {
     float acc = 0.f;
     fetch(0);
+    store(0);
+    __syncthreads();
+    if (kCR < n) fetch(kCR);
     int slot = 0;
-    for (int64_t row0 = 0; row0 < n; row0 += R) {
-      float* B = sb + slot * kColLds;
-      const int rows = (int)min((int64_t)R, n - row0);
+    for (int64_t r0 = 0; r0 < n; r0 += kCR) {
+      const int rows = (int)min((int64_t)kCR, n - r0);
+      if (tid < w) acc = col_fold(&buf[slot][tid], rows, pass, m, acc);
+      if (pass == 1) {  // x - mean, written from the staged chunk by every thread
 #pragma unroll
-      for (int q = 0; q < kColP; ++q)
-        if (tid + 256 * q < rows * w) B[tid + 256 * q] = v[q];
-      __syncthreads();
-      if (row0 + R < n) fetch(row0 + R);
-      if (tid < w) {
-        if (pass == 0) {
-          for (int r = 0; r < rows; ++r) acc = acc + B[r * w + tid];
-        } else {
-          float* o = X_out + row0 * dim + c0 + tid;
-          for (int r = 0; r < rows; ++r) {
-            const float d = B[r * w + tid] - m;
-            o[(int64_t)r * dim] = d;
-            acc = acc + d * d;
-          }
+        for (int q = 0; q < kCQ; ++q) {
+          const int e = tid + 256 * q;
+          const int r = e >> 3, c = e & (kCW - 1);
+          if (c < w && r < rows) X_out[(r0 + r) * dim + c0 + c] = buf[slot][e] - s_m[c];
         }
       }
+      if (r0 + kCR < n) {
+        store(slot ^ 1);                           // waits for the chunk in flight
+        if (r0 + 2 * kCR < n) fetch(r0 + 2 * kCR);  // and puts the next one in flight
+      }
+      __syncthreads();
       slot ^= 1;
     }
     if (tid < w) {
       if (pass == 0) {
         m = (float)((double)acc / (double)n);
         mean[c0 + tid] = m;
+        s_m[tid] = m;
       } else {
         var[c0 + tid] = (float)((double)acc / (double)n);
       }
     }
-    __syncthreads();  // both buffers are reused by the next pass
+    __syncthreads();
   }
 }
 
@@ -316,17 +344,12 @@ __global__ __launch_bounds__(64) void k_col_stats_pw(int64_t n, const float* __r
 extern "C" int gdd_center_columns(int64_t n, int dim, const float* X, float* X_out, float* mean,
                                   float* var, gdd_stream_t stream) {
   GDD_REQUIRE(n > 0 && dim > 0 && X && X_out && mean && var, "center_columns: bad arguments");
-  GDD_REQUIRE((int64_t)(kColLds / std::min(dim, 256) + kColLds / 256) * dim < INT_MAX,
-              "center_columns: dim=%d too wide", dim);
   hipStream_t s = to_hip(stream);
   if (dim == 1) {
     k_col_stats_pw<<<1, 64, 0, s>>>(n, X, X_out, mean, var);
   } else {
-    const size_t lds = sizeof(float) * 2 * kColLds;
-    void (*kfn)(int64_t, int, const float*, float*, float*, float*) = gdd::k_col_stats;
-    GDD_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds));
-    k_col_stats<<<(unsigned)((dim + 255) / 256), 256, lds, s>>>(n, dim, X, X_out, mean, var);
+    const unsigned groups = (unsigned)((dim + kCW - 1) / kCW);
+    k_col_stats<<<groups * kColXcd, 256, 0, s>>>(n, dim, X, X_out, mean, var);
   }
   GDD_LAUNCHED();
   return GDD_OK;
