@@ -1,0 +1,247 @@
+"""Drop-in for ``ClustGDD/clustgdd_agent_transduct.py``'s ``ClustGDD`` agent on libgdd.
+
+Same constructor (``data, args, device``), same methods and return values, same stdout lines —
+``adj_syn: (n, n) feat_syn: (n, d)``, the MLP pretrain results, ``finish clustering``,
+``Train/Test Mean Accuracy: [...]``, ``The pretraining time is …``, ``The refinement time is …``,
+``Total time is …``, ``max memory allocation: … MB`` (transduct:33, :80-94, :112, :409-429) — so a
+driver written for the reference (``gdd.train_clustgdd_transduct``) runs unchanged.
+
+What moved onto the MI355X kernels (the distillation hot path):
+* ``pretrained_clustering`` (:38-129): normalisation (``gdd_normalize_csr``), the T-hop propagation
+  (``gdd_propagate``), k-means on the MLP logits (MiniBatchKMeans for ogbn-arxiv, KMeans otherwise,
+  bit-exact with scikit-learn), the cluster means and argmax labels;
+* ``graph_sparse`` / ``graph_compress`` (:131-250): effective-resistance weights, per-class top-k
+  and the cluster-level graphs (``gdd.condense``);
+* the GCN evaluator's full-graph products (``gdd.gcn.spmm``).
+The two small torch models (the linear MLP and the GCN, ``gdd.models``) and ``graph_refusion``'s
+dense k x k products stay torch, as in the reference.
+
+``args`` may carry ``group`` (a torch.distributed group over the GPUs of a node): the k-means rows
+and the cluster means are then partitioned over the ranks (gdd.sharded), bit-identically.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import condense
+from .cluster import argmax_rows, cluster_mean
+from .graph import CSRGraph, normalize_adj, propagate, to_csr
+from .kmeans import KMeans, MiniBatchKMeans
+from .models import GCN, MLP, accuracy, normalize_dense
+
+
+class ClustGDD:
+    def __init__(self, data, args, device="cuda", **kwargs):
+        self.data = data
+        self.args = args
+        self.device = device
+        self.ori_node_num = data.feat_full.shape[0]
+        n = int(data.feat_train.shape[0] * args.reduction_rate)
+        d = data.feat_train.shape[1]
+        self.nnodes_syn = n
+        self.d = d
+        self.group = getattr(args, "group", None)
+        print("adj_syn:", (n, n), "feat_syn:", (n, d))
+
+    # -- transduct:38-129 ------------------------------------------------------------------------
+    def pretrained_clustering(self, data):
+        args, dev = self.args, self.device
+        g = data.adj_full if isinstance(data.adj_full, CSRGraph) else to_csr(data.adj_full, device=dev)
+        self.ori_edge_num = g.nnz
+        features = torch.as_tensor(np.asarray(data.feat_full), dtype=torch.float32).to(dev) \
+            if not isinstance(data.feat_full, torch.Tensor) else data.feat_full.to(dev, torch.float32)
+        labels = torch.LongTensor(np.asarray(data.labels_full)).to(dev)
+        idx_train = data.idx_train
+        adj_norm = normalize_adj(g)                                                 # :46-50
+        target_feat, _ = propagate(adj_norm, features, args.prop_num, args.alpha)   # :55-65
+        model = MLP(nfeat=target_feat.shape[-1], nhid=args.hidden, dropout=args.predropout,
+                    weight_decay=args.prewd, nlayers=args.prenlayers, lr=args.prelr,
+                    with_relu=False, with_bn=False, nclass=data.nclass, device=dev).to(dev)
+        model.fit_with_val(target_feat, adj_norm, labels[idx_train], idx_train, data,
+                           train_iters=args.preep, normalize=True, verbose=False)
+        labels_test = torch.LongTensor(data.labels_test).to(dev)
+        labels_train = torch.LongTensor(data.labels_train).to(dev)
+        output = model.predict(target_feat)
+        loss_train = F.nll_loss(output[idx_train], labels_train)
+        acc_train = accuracy(output[idx_train], labels_train)
+        print("MLP pretrain, train set results:", "loss= {:.4f}".format(loss_train.item()),
+              "accuracy= {:.4f}".format(acc_train.item()))
+        with torch.no_grad():
+            model.eval()
+            _, output = model.predict(target_feat, mode="e")
+        loss_test = F.cross_entropy(output[data.idx_test], labels_test)
+        acc_test = accuracy(output[data.idx_test], labels_test)
+        print("MLP pretrain, test set results:", "loss= {:.4f}".format(loss_test.item()),
+              "accuracy= {:.4f}".format(acc_test.item()))
+        # k-means on the logits (:100-105), on the device
+        if args.dataset == "ogbn-arxiv":
+            km = MiniBatchKMeans(n_clusters=self.nnodes_syn, random_state=args.seed,
+                                 batch_size=args.cluster_minibatch, device=dev,
+                                 group=self.group).fit(output)
+        elif self.group is not None:
+            from .pipeline import _lloyd
+            km = _lloyd(self.nnodes_syn, self.group, device=dev).fit(output)
+        else:
+            km = KMeans(n_clusters=self.nnodes_syn, device=dev).fit(output)
+        print("finish clustering")
+        cluster_labels = km.labels_device_.to(torch.int32)
+        feat_syn, _ = cluster_mean(target_feat, cluster_labels, self.nnodes_syn, group=self.group)  # :116-125
+        labels_syn = argmax_rows(km.cluster_centers_device_)                                         # :126
+        return (feat_syn, labels_syn, cluster_labels, adj_norm, features, g, labels, target_feat,
+                idx_train, data.idx_val, output)
+
+    # -- transduct:131-250 -----------------------------------------------------------------------
+    def graph_sparse(self, adj, ratio, ebd=None, sp_type="vanilla"):
+        return condense.graph_sparse(adj, ratio, ebd=ebd, sp_type=sp_type)
+
+    def graph_compress(self, cluster_labels, adj_norm, adj_list):
+        return condense.graph_compress(cluster_labels, adj_norm, adj_list)
+
+    # -- transduct:252-347 -----------------------------------------------------------------------
+    def graph_refusion(self, target_feat, idx_train, idx_val, labels_raw, feat_syn,
+                       compressed_graph_list, label_syn):
+        args, dev = self.args, self.device
+        nclass = labels_raw.max() + 1
+        alpha, frcoe, csttemp = args.alpha, args.frcoe, args.csttemp
+        feat_syn_refine = nn.Parameter(torch.zeros(feat_syn.shape[0], feat_syn.shape[1]).to(dev))
+        T = args.postprop_num
+        target_feat_syn_list = []
+        for compressed_graph in compressed_graph_list:
+            dense = compressed_graph.to_dense()
+            for t in range(T):
+                if t == 0:
+                    prop_feat_syn = feat_syn + frcoe * feat_syn_refine
+                    target_feat_syn = (1 - alpha) * prop_feat_syn
+                else:
+                    prop_feat_syn = alpha * dense @ prop_feat_syn
+                    target_feat_syn = target_feat_syn + (1 - alpha) * prop_feat_syn
+            target_feat_syn_list.append(target_feat_syn)
+        model = MLP(nfeat=feat_syn.shape[-1], nhid=args.hidden, dropout=args.predropout,
+                    weight_decay=args.prewd, nlayers=args.prenlayers, lr=args.prelr,
+                    with_relu=False, with_bn=False, nclass=int(nclass), device=dev).to(dev)
+        opt_feat = torch.optim.Adam([feat_syn_refine], lr=args.postlr_feat, weight_decay=args.postwd_feat)
+        opt_model = torch.optim.Adam(model.parameters(), lr=args.postlr_model, weight_decay=args.postwd_model)
+        best_acc_val = 0.0
+        best_feat_syn_refine = None
+        coe1 = args.predcoe
+        for i in range(args.postep):
+            opt_feat.zero_grad()
+            opt_model.zero_grad()
+            pred_list = [model(target_feat)] + [model(t) for t in target_feat_syn_list]
+            if i == args.postep // 2:
+                opt_feat = torch.optim.Adam([feat_syn_refine], lr=args.postlr_feat * 0.1,
+                                            weight_decay=args.postwd_feat)
+                opt_model = torch.optim.Adam(model.parameters(), lr=args.postlr_model * 0.1,
+                                             weight_decay=args.postwd_model)
+            loss_train = F.nll_loss(pred_list[0][idx_train], labels_raw[idx_train])
+            for j in range(1, len(pred_list)):
+                loss_train += coe1 * F.nll_loss(pred_list[j], label_syn)
+            loss_cst = self.consistency_loss(pred_list[1:], temp=csttemp)
+            loss_all = args.w1 * loss_cst + args.w2 * loss_train
+            loss_all.backward(retain_graph=True)
+            opt_model.step()
+            opt_feat.step()
+            with torch.no_grad():
+                model.eval()
+                output = model(target_feat)
+                acc_val = accuracy(output[idx_val], labels_raw[idx_val])
+                if i % 100 == 0:
+                    print("Epoch {}, training loss: {}".format(i, loss_train.item()))
+                    print("Epoch {}, acc val: {}".format(i, acc_val.item()))
+                if acc_val > best_acc_val:
+                    best_acc_val = acc_val
+                    best_feat_syn_refine = feat_syn_refine.detach()
+        if best_feat_syn_refine is None:  # the reference would fail here (never improved)
+            best_feat_syn_refine = feat_syn_refine.detach()
+        return feat_syn + frcoe * best_feat_syn_refine.detach()
+
+    # -- transduct:349-393 -----------------------------------------------------------------------
+    def test_with_val(self, runs, verbose=True):
+        res = []
+        data, device, args = self.data, self.device, self.args
+        feat_syn, adj_syn, labels_syn = self.feat_syn.detach(), self.adj_syn, self.labels_syn
+        if getattr(args, "notopo", False):
+            adj_syn = torch.eye(feat_syn.shape[0]).to(device)
+        with_bn = args.dataset in ["ogbn-arxiv"]
+        model = GCN(nfeat=feat_syn.shape[1], nhid=args.hidden, dropout=0.5, weight_decay=5e-4,
+                    nlayers=2, nclass=data.nclass, device=device).to(device)
+        if args.dataset in ["ogbn-arxiv"]:
+            model = GCN(nfeat=feat_syn.shape[1], nhid=args.hidden, dropout=0.5, weight_decay=0e-4,
+                        nlayers=2, with_bn=with_bn, nclass=data.nclass, device=device).to(device)
+        model.fit_with_val(feat_syn, adj_syn, labels_syn, data, train_iters=600, verbose=False)
+        model.eval()
+        labels_test = torch.LongTensor(data.labels_test).to(device)
+        labels_train = torch.LongTensor(data.labels_train).to(device)
+        output = model.predict(data.feat_train, data.adj_train)
+        loss_train = F.nll_loss(output, labels_train)
+        acc_train = accuracy(output, labels_train)
+        if verbose:
+            print("Train set results:", "loss= {:.4f}".format(loss_train.item()),
+                  "accuracy= {:.4f}".format(acc_train.item()))
+        res.append(acc_train.item())
+        output = model.predict(data.feat_full, data.adj_full)
+        loss_test = F.nll_loss(output[data.idx_test], labels_test)
+        acc_test = accuracy(output[data.idx_test], labels_test)
+        res.append(acc_test.item())
+        if verbose:
+            print("Test set results:", "loss= {:.4f}".format(loss_test.item()),
+                  "accuracy= {:.4f}".format(acc_test.item()))
+        return res
+
+    # -- transduct:395-429 -----------------------------------------------------------------------
+    def distill(self):
+        """pretrained_clustering -> graph_sparse -> graph_compress -> graph_refusion; sets
+        feat_syn / labels_syn / adj_syn (normalised dense) and returns the stage times."""
+        args = self.args
+        sync = torch.cuda.synchronize if torch.device(self.device).type == "cuda" else (lambda: None)
+        sync()
+        t1 = time.time()
+        (feat_syn, labels_syn, cluster_labels, adj_norm, features, adj, labels, target_feat, idx_train,
+         idx_val, ebd) = self.pretrained_clustering(self.data)
+        sync()
+        t_pc = time.time()
+        sparsed_graph_list = self.graph_sparse(adj_norm, ratio=args.sp_ratio, ebd=ebd, sp_type=args.sp_type)
+        compressed_graph_list, adj_syn = self.graph_compress(cluster_labels, adj_norm, sparsed_graph_list)
+        feat_syn = self.graph_refusion(target_feat, idx_train, idx_val, labels, feat_syn,
+                                       compressed_graph_list, labels_syn)
+        sync()
+        t2 = time.time()
+        adj_syn = adj_syn.detach().to_dense()
+        self.feat_syn = feat_syn
+        self.labels_syn = labels_syn
+        self.adj_syn = normalize_dense(adj_syn)
+        self.cluster_labels = cluster_labels
+        return t1, t_pc, t2
+
+    def train(self):
+        t1, t_pc, t2 = self.distill()
+        max_memory = torch.cuda.max_memory_allocated(self.device) \
+            if torch.device(self.device).type == "cuda" else 0
+        self.results = None
+        if not getattr(self.args, "tm_rec", False):
+            res = np.array([self.test_with_val(i) for i in range(5)])
+            self.results = res
+            print("Train/Test Mean Accuracy:", repr([res.mean(0), res.std(0)]))
+        print(f"The pretraining time is {t_pc - t1}")
+        print(f"The refinement time is {t2 - t_pc}")
+        print("Total time is {}".format(t2 - t1))
+        print(f"max memory allocation: {max_memory / (1024 ** 2):.2f} MB")
+
+    # -- transduct:449-465 -----------------------------------------------------------------------
+    def consistency_loss(self, out_list, temp=0.1):
+        ps = [torch.softmax(p, dim=1) for p in out_list]
+        sum_p = 0.0
+        for p in ps:
+            sum_p = sum_p + p
+        avg_p = sum_p / len(ps)
+        sharp_p = (torch.pow(avg_p, 1.0 / temp)
+                   / torch.sum(torch.pow(avg_p, 1.0 / temp), dim=1, keepdim=True)).detach()
+        loss = 0.0
+        for p in ps:
+            loss += torch.sum((p - sharp_p).pow(2).sum(1))
+        return temp * (loss / len(ps))
