@@ -462,6 +462,119 @@ __global__ void k_assign_finalize(int64_t n, int dim, const float* __restrict__ 
   }
 }
 
+
+// ---- persistent bf16 full pass (predict(precision="bf16")) ------------------
+// HBM-bound design: every block converts ALL centres once into v_mfma_f32_32x32x16_bf16 A-fragments
+// in LDS ([centre tile][k-step][lane] x 8 bf16, one ds_read_b128 per lane per MFMA) with the fp32
+// norms beside them (+inf past k), then each wave walks 32-point tiles: the tile's rows are one
+// contiguous span of X (float4 loads, the next tile in flight in registers while the current one
+// computes), staged in a wave-private LDS slot, turned into B-fragments (point = column, so every
+// lane owns one point's 16 centre rows per MFMA: the argmin is lane-local, then one lane^32 merge).
+// d = fma(-2, <x, c>_bf16, ||c||^2), first minimum; labels written directly (no key buffer, no
+// atomics, no finalize); sq_dist is the exact fp32 _euclidean_dense_dense to the chosen centre.
+typedef float floatx4_t __attribute__((ext_vector_type(4)));
+
+__host__ __device__ inline size_t assign_bf16p_lds(int ktiles, int nsteps, int dim) {
+  return (size_t)ktiles * nsteps * 64 * 16 + (size_t)ktiles * 32 * sizeof(float) +
+         (size_t)4 * 32 * dim * sizeof(float);
+}
+
+template <int PER>  // float4 loads per lane per 32-point tile: PER >= ceil(32 * dim / 256)
+__global__ __launch_bounds__(256) void k_assign_bf16p(int64_t n, int dim, int nsteps, int ktiles,
+                                                      const float* __restrict__ X, int k,
+                                                      const float* __restrict__ C,
+                                                      const float* __restrict__ cn2,
+                                                      int32_t* __restrict__ labels,
+                                                      float* __restrict__ sq_dist) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16x8_t* Af = reinterpret_cast<bf16x8_t*>(smem);
+  float* Cn = reinterpret_cast<float*>(smem + (size_t)ktiles * nsteps * 64 * 16);
+  float* Pt = Cn + ktiles * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, r = lane & 31;
+  for (int e = tid; e < ktiles * nsteps * 64; e += 256) {
+    const int l = e & 63, rest = e >> 6;
+    const int s = rest % nsteps, ct = rest / nsteps;
+    const int c = ct * 32 + (l & 31), f0 = 16 * s + 8 * (l >> 5);
+    bf16x8_t v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)((c < k && f0 + j < dim) ? C[(int64_t)c * dim + f0 + j] : 0.f);
+    Af[e] = v;
+  }
+  for (int c = tid; c < ktiles * 32; c += 256) Cn[c] = c < k ? cn2[c] : __builtin_inff();
+  __syncthreads();
+  float* my = Pt + wave * 32 * dim;
+  const int nf4 = 8 * dim;  // float4 per full tile (32 rows x dim floats)
+  const int64_t ntiles = (n + 31) / 32, nfull = n / 32;
+  const int64_t step = (int64_t)gridDim.x * 4;
+  int64_t t = (int64_t)blockIdx.x * 4 + wave;
+  float4 v[PER];
+  auto fetch = [&](int64_t tt) {
+    if (tt >= nfull) return;  // the partial last tile is read scalar in stage()
+    const float4* src = reinterpret_cast<const float4*>(X + tt * 32 * dim);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) v[q] = src[min(lane + 64 * q, nf4 - 1)];
+  };
+  auto stage = [&](int64_t tt) {
+    if (tt < nfull) {
+      float4* dst = reinterpret_cast<float4*>(my);
+#pragma unroll
+      for (int q = 0; q < PER; ++q)
+        if (lane + 64 * q < nf4) dst[lane + 64 * q] = v[q];
+    } else {
+      const int64_t rows = n - tt * 32;
+      for (int e = lane; e < 32 * dim; e += 64) my[e] = e < rows * dim ? X[tt * 32 * dim + e] : 0.f;
+    }
+  };
+  fetch(t);
+  for (; t < ntiles; t += step) {
+    stage(t);
+    fetch(t + step);  // in flight while this tile computes
+    bf16x8_t b[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      if (s < nsteps) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int f = 16 * s + 8 * h + j;
+          b[s][j] = (__bf16)(f < dim ? my[r * dim + f] : 0.f);
+        }
+      }
+    }
+    float bestd = __builtin_inff();
+    int bestc = 0;
+    for (int ct = 0; ct < ktiles; ++ct) {
+      floatx16 acc = {};
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        if (s < nsteps) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Af[(ct * nsteps + s) * 64 + lane], b[s], acc, 0, 0, 0);
+      const floatx4_t* cp = reinterpret_cast<const floatx4_t*>(Cn + ct * 32 + 4 * h);
+      floatx4_t cn[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) cn[g] = cp[2 * g];  // rows 8g + 4h .. +3
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const float d = __builtin_fmaf(-2.f, acc[reg], cn[reg >> 2][reg & 3]);
+        if (d < bestd) {
+          bestd = d;
+          bestc = ct * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        }
+      }
+    }
+    const float od = __shfl_xor(bestd, 32);
+    const int oc = __shfl_xor(bestc, 32);
+    if (od < bestd || (od == bestd && oc < bestc)) {
+      bestd = od;
+      bestc = oc;
+    }
+    const int64_t p = t * 32 + r;
+    if (h == 0 && p < n) {
+      labels[p] = bestc;
+      if (sq_dist) sq_dist[p] = skl_sqdist(my + r * dim, C + (int64_t)bestc * dim, dim);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // small batches (minibatch steps): one block of WAVES waves per 32 points. Wave w owns centre tiles
 // w, w+WAVES, ...; it stages its tile (and, without cached norms, their numpy-order norms) in LDS,
@@ -1327,6 +1440,31 @@ extern "C" int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const 
   hipStream_t s = to_hip(stream);
   unsigned long long* keys = static_cast<unsigned long long*>(ws);
   const int dimp16 = (dim + 15) & ~15;
+  {  // the persistent kernel: whole rows (no gathered rows), dim <= 128, centre fragments fit LDS
+    const int nsteps = dimp16 / 16, ktiles = (k + 31) / 32;
+    const size_t lds = assign_bf16p_lds(ktiles, nsteps, dim);
+    const int per_need = (8 * dim + 63) / 64;
+    const bool aligned = (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+    if (!rows && dim <= 128 && aligned && lds <= 150 * 1024) {
+      const int64_t ntiles = (n + 31) / 32;
+      const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 3) / 4, 1024));
+      auto go = [&](auto P_) -> int {
+        constexpr int P = decltype(P_)::value;
+        GDD_HIP(hipFuncSetAttribute((const void*)k_assign_bf16p<P>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+        k_assign_bf16p<P><<<grid, 256, lds, s>>>(n, dim, nsteps, ktiles, X, k, C, c_norm2, labels, sq_dist);
+        GDD_LAUNCHED();
+        return GDD_OK;
+      };
+      if (per_need <= 1) return go(std::integral_constant<int, 1>());
+      if (per_need <= 2) return go(std::integral_constant<int, 2>());
+      if (per_need <= 4) return go(std::integral_constant<int, 4>());
+      if (per_need <= 6) return go(std::integral_constant<int, 6>());
+      if (per_need <= 8) return go(std::integral_constant<int, 8>());
+      if (per_need <= 12) return go(std::integral_constant<int, 12>());
+      return go(std::integral_constant<int, 16>());
+    }
+  }
   constexpr int kWaves = 4;
   const int64_t gx = (n + 32 * kWaves - 1) / (32 * kWaves);
   const int kp = (k + 31) & ~31;

@@ -504,6 +504,7 @@ struct KppArgs {
   double* fsum[2];    // [T][nblk] cumulative-potential block totals
   int64_t* cand[2];   // [kMaxTrials]
   float* pot1;        // [2] T == 1: the round's potential (sdot), by parity
+  int* winq;          // [2] round c-1's winning trial, by the parity of c (the split-round path)
   const double* uniforms;
   const KppState* st;
   float* centers;
@@ -778,7 +779,7 @@ __device__ float sgemv_block_wave(const float* __restrict__ s_d, const float* __
 }
 
 // ---- one seeding round ------------------------------------------------------------------------------
-template <bool SEQ>
+template <bool SEQ, bool PICK = false>
 __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   extern __shared__ double s_c[];  // dim doubles, then the block's distances (fp32)
   __shared__ float s_pot[kMaxTrials];
@@ -869,12 +870,14 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     ct = min<int64_t>(n - 1, (int64_t)jb * kBlk + cnt);
   }
   if (blk == 0 && tid == 0) a.cand[cq][t] = ct;
+  if (PICK && blk == 0 && t == 0 && tid == 0) a.winq[cq] = bw;
   if (c >= 2 && blk == 0 && t == 0) {  // round c-1's centre (round 0's is written by k_kpp_first)
     const int64_t src = a.cand[pq][bw];
     if (tid == 0) a.indices[c - 1] = src;
     for (int j = tid; j < a.dim; j += kThr) a.centers[(int64_t)(c - 1) * a.dim + j] = a.X[src * a.dim + j];
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 23);
+  if constexpr (PICK) return;  // the split path: k_kpp_dists computes every trial's distances
   // ---- distances of this block's points to the candidate, np.minimum with the winner's row
   const double cn = a.xsq[ct];
   for (int j = tid; j < a.dim; j += kThr) s_c[j] = (double)a.X[ct * a.dim + j];
@@ -904,6 +907,109 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 25);
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0 && c < 128), 128 + c);
+}
+
+// ---- round c's distances for ALL trials of one point block (the split-round path, SEQ, T <= 8) ------
+// One workgroup per 4096-point block reads its points' features once (the dim x n transpose,
+// coalesced) and runs the T k-ordered fp64 chains side by side, instead of T workgroups re-reading
+// the same block (T x the X traffic); then, per trial, np.minimum with the winner's row, the
+// cumulative-potential block total (block_prefix) and the sgemv_t block term (wave t).
+constexpr int kSplitMaxT = 8;
+__global__ __launch_bounds__(kThr) void k_kpp_dists(KppArgs a, int c) {
+  extern __shared__ double s_cs[];  // T * dim doubles (candidate rows), then T * kBlk floats
+  __shared__ double s_wave[kWaves];
+  __shared__ double s_cn[kSplitMaxT];
+  const int blk = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int T = a.T, dim = a.dim;
+  const int pq = (c - 1) & 1, cq = c & 1;
+  const int64_t n = a.n, j0 = (int64_t)blk * kBlk;
+  const float* wrow = c == 1 ? a.closest0 : a.dist[pq] + (int64_t)a.winq[cq] * n;
+  for (int e = tid; e < T * dim; e += kThr) {
+    const int t = e / dim, j = e - t * dim;
+    s_cs[e] = (double)a.X[a.cand[cq][t] * dim + j];
+  }
+  if (tid < T) s_cn[tid] = a.xsq[a.cand[cq][tid]];
+  __syncthreads();
+  float* s_d = reinterpret_cast<float*>(s_cs + T * dim);
+  int64_t ix[kPer];
+  double dot[kSplitMaxT][kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int64_t i = j0 + tid + kThr * q;
+    ix[q] = i < n ? i : j0;
+#pragma unroll
+    for (int t = 0; t < kSplitMaxT; ++t) dot[t][q] = 0.0;
+  }
+  int j = 0;
+  for (; j + 4 <= dim; j += 4) {
+    float u[4][kPer];
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) u[v][q] = a.XT[(int64_t)(j + v) * n + ix[q]];
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int t = 0; t < kSplitMaxT; ++t)
+        if (t < T) {
+          const double cv = s_cs[t * dim + j + v];
+#pragma unroll
+          for (int q = 0; q < kPer; ++q) dot[t][q] = __builtin_fma(cv, (double)u[v][q], dot[t][q]);
+        }
+  }
+  for (; j < dim; ++j) {
+    float u[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) u[q] = a.XT[(int64_t)j * n + ix[q]];
+#pragma unroll
+    for (int t = 0; t < kSplitMaxT; ++t)
+      if (t < T) {
+        const double cv = s_cs[t * dim + j];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) dot[t][q] = __builtin_fma(cv, (double)u[q], dot[t][q]);
+      }
+  }
+  float wv_[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int64_t i = j0 + tid + kThr * q;
+    wv_[q] = i < n ? wrow[i] : 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < kSplitMaxT; ++t) {
+    if (t >= T) break;
+    float* drow = a.dist[cq] + (int64_t)t * n;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int o = tid + kThr * q;
+      const int64_t i = j0 + o;
+      float f = 0.f;
+      if (i < n) {
+        f = (float)(((-2.0 * dot[t][q]) + s_cn[t]) + a.xsq[i]);
+        f = f < 0.f ? 0.f : f;
+        f = np_minimum(wv_[q], f);
+        drow[i] = f;
+      }
+      s_d[t * kBlk + o] = f;
+    }
+  }
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {  // the block's cumulative-potential total, per trial
+    double v[kPer], pre[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int64_t e = j0 + kPer * tid + q;
+      v[q] = e < n ? (double)(wv(a.w, e) * s_d[t * kBlk + kPer * tid + q]) : 0.0;
+    }
+    block_prefix(v, pre, s_wave);
+    const int64_t last = min<int64_t>(n, j0 + kBlk) - 1 - j0;
+    if (tid == (int)(last / kPer)) a.fsum[cq][(int64_t)t * a.nblk + blk] = pre[last % kPer];
+  }
+  const int64_t NB = min<int64_t>(kBlk, a.m1 - j0);
+  if (NB > 0 && wave < T) {  // wave t: trial t's sgemv_t block term
+    const float v = sgemv_block_wave(s_d + wave * kBlk, a.w ? a.w + j0 : nullptr, NB, wave, T);
+    if (lane == 0) a.vblk[cq][(int64_t)wave * a.nblk + blk] = v;
+  }
 }
 
 // after the last round: its potentials, winner and centre
@@ -1597,6 +1703,7 @@ size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k) {
   b += 2 * align256(sizeof(double) * nblk * T);   // fsum
   b += 2 * align256(sizeof(int64_t) * kMaxTrials);
   b += align256(sizeof(float) * 2);           // pot1
+  b += align256(sizeof(int) * 2);             // winq
   b += 2 * align256(sizeof(float) * T);       // potv
   b += 2 * align256(sizeof(int64_t) * T * T); // candw
   b += 2 * align256(sizeof(int64_t) * T);     // candself
@@ -1633,6 +1740,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   for (int q = 0; q < 2; ++q) a.fsum[q] = cv.take<double>((size_t)nblk * T);
   for (int q = 0; q < 2; ++q) a.cand[q] = cv.take<int64_t>(kMaxTrials);
   a.pot1 = cv.take<float>(2);
+  a.winq = cv.take<int>(2);
   Kpp1Args b1{};
   for (int q = 0; q < 2; ++q) b1.potv[q] = cv.take<float>(T);
   for (int q = 0; q < 2; ++q) b1.candw[q] = cv.take<int64_t>((size_t)T * T);
@@ -1738,6 +1846,22 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       GDD_LAUNCHED();
     }
     k_kpp1_final<<<1, 64, 0, s>>>(b1, k - 1);
+    GDD_LAUNCHED();
+    return GDD_OK;
+  }
+  const size_t lds_split = sizeof(double) * (size_t)T * dim + sizeof(float) * (size_t)T * kBlk;
+  const bool split = seq && a.XT && T >= 2 && T <= kSplitMaxT && lds_split <= 150 * 1024 &&
+                     getenv("GDD_KPP_FUSED_ROUND") == nullptr;
+  if (split) {
+    GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dists, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds_split));
+    for (int c = 1; c < k; ++c) {
+      k_kpp_round<true, true><<<dim3(1, T), kThr, lds, s>>>(a, c);   // fold, winner, candidates
+      GDD_LAUNCHED();
+      k_kpp_dists<<<nblk, kThr, lds_split, s>>>(a, c);              // every trial's distances
+      GDD_LAUNCHED();
+    }
+    k_kpp_final<<<1, kThr, 0, s>>>(a, k - 1);
     GDD_LAUNCHED();
     return GDD_OK;
   }
