@@ -102,37 +102,53 @@ __device__ __forceinline__ void vstore(float* p, const float (&r)[V]) {
 }
 
 // ---- plan: per-row segment counts -> item offsets / partial offsets -> item records ----------
-__global__ void k_seg_counts(int64_t n, const int32_t* __restrict__ rowptr, int32_t* nseg,
-                             int32_t* npart) {
+// `order` (nullable): position i of the work list is row order[i] (rows scheduled longest first,
+// see build_plan); counts and offsets are indexed by position
+__global__ void k_seg_counts(int64_t n, const int32_t* __restrict__ rowptr,
+                             const int32_t* __restrict__ order, int32_t* nseg, int32_t* npart) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  int32_t len = rowptr[i + 1] - rowptr[i];
+  const int64_t r = order ? order[i] : i;
+  int32_t len = rowptr[r + 1] - rowptr[r];
   int32_t s = len <= kSeg ? 1 : (len + kSeg - 1) / kSeg;
   nseg[i] = s;
   npart[i] = s > 1 ? s : 0;
 }
 
 __global__ void k_make_items(int64_t n, const int32_t* __restrict__ rowptr,
-                             const int32_t* __restrict__ nseg, const int32_t* __restrict__ item_off,
+                             const int32_t* __restrict__ order, const int32_t* __restrict__ nseg, const int32_t* __restrict__ item_off,
                              const int32_t* __restrict__ part_off, Item* items,
                              int32_t* long_rows, int32_t* long_off, int32_t* counts) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int32_t b = rowptr[i], e = rowptr[i + 1], s = nseg[i], o = item_off[i];
+  const int32_t r = order ? order[i] : (int32_t)i;
+  const int32_t b = rowptr[r], e = rowptr[r + 1], s = nseg[i], o = item_off[i];
   if (s == 1) {
-    items[o] = Item{(int32_t)i, b, e, -1};
+    items[o] = Item{r, b, e, -1};
   } else {
     const int32_t po = part_off[i];
     for (int32_t k = 0; k < s; ++k) {
       int32_t lo = b + k * kSeg, hi = min(e, lo + kSeg);
-      items[o + k] = Item{(int32_t)i, lo, hi, po + k};
+      items[o + k] = Item{r, lo, hi, po + k};
     }
     // list of split rows for the fixup pass; list order is irrelevant (each entry is independent)
-    int32_t r = atomicAdd(&counts[1], 1);
-    long_rows[r] = (int32_t)i;
-    long_off[r] = po;
+    int32_t q = atomicAdd(&counts[1], 1);
+    long_rows[q] = r;
+    long_off[q] = po;
   }
   if (i == n - 1) counts[0] = o + s;  // number of items
+}
+
+// sort keys for the longest-first schedule: ascending key = descending row length, rows of
+// kLenKeyMax+ entries all first; ties keep row order (the radix sort is stable)
+constexpr int kLenKeyBits = 10;
+constexpr int32_t kLenKeyMax = (1 << kLenKeyBits) - 1;
+__global__ void k_len_keys(int64_t n, const int32_t* __restrict__ rowptr, int32_t* keys,
+                           int32_t* rows) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  keys[i] = kLenKeyMax - min(rowptr[i + 1] - rowptr[i], kLenKeyMax);
+  rows[i] = (int32_t)i;
 }
 
 // ---- one hop -----------------------------------------------------------------------------------
@@ -253,14 +269,29 @@ struct Plan {
   float* partials;
   int64_t max_items;
   int64_t max_long;
+  void* sort_ws;
+  size_t sort_bytes;
 };
+
+// work-list schedule: 1 = longest rows first (default), 0 = row order (GDD_HOP_SCHED overrides).
+// Items are independent (each writes its own row or partial slot), so the schedule changes only
+// timing, never a result. Longest first: the long items of a power-law graph start early instead of
+// trailing the grid (arxiv shape 220 -> 204 us per hop, products 9.7 -> 9.5 ms).
+int hop_sched() {
+  static int v = [] {
+    const char* e = getenv("GDD_HOP_SCHED");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
 
 inline int64_t max_items_for(int64_t n, int64_t nnz) { return n + nnz / kSeg + 1; }
 inline int64_t max_parts_for(int64_t nnz) { return 2 * (nnz / kSeg) + 2; }
 
 size_t plan_ws_bytes(int64_t n, int64_t nnz, int d) {
   size_t b = 0;
-  b += align256(sizeof(int32_t) * n) * 4;                // nseg, npart, item_off, part_off
+  b += align256(sizeof(int32_t) * n) * 7;  // nseg, npart, item_off, part_off, sort keys/rows x3
+  b += sort_pairs_ws_bytes(n);
   b += align256(sizeof(Item) * max_items_for(n, nnz));   // items
   b += align256(sizeof(int32_t) * 4);                    // counts
   b += align256(sizeof(int32_t) * (nnz / kSeg + 1)) * 2; // long rows
@@ -272,7 +303,7 @@ size_t plan_ws_bytes(int64_t n, int64_t nnz, int d) {
 // carve the plan's buffers (same layout for build_plan and a later planned hop)
 int carve_plan(int64_t n, int64_t nnz, int d, Carver& cv, Plan& pl, int32_t** tmp, void** scan_ws,
                size_t* scan_bytes) {
-  for (int q = 0; q < 4; ++q) tmp[q] = cv.take<int32_t>(n);
+  for (int q = 0; q < 7; ++q) tmp[q] = cv.take<int32_t>(n);
   pl.max_items = max_items_for(n, nnz);
   pl.max_long = nnz / kSeg + 1;
   pl.items = cv.take<Item>(pl.max_items);
@@ -282,13 +313,15 @@ int carve_plan(int64_t n, int64_t nnz, int d, Carver& cv, Plan& pl, int32_t** tm
   pl.partials = cv.take<float>(max_parts_for(nnz) * (size_t)d);
   *scan_bytes = scan_i32_ws_bytes(n);
   *scan_ws = cv.take<char>(*scan_bytes);
+  pl.sort_bytes = sort_pairs_ws_bytes(n);
+  pl.sort_ws = cv.take<char>(pl.sort_bytes);
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "propagate: workspace too small");
   return GDD_OK;
 }
 
 int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv, Plan& pl,
                hipStream_t s) {
-  int32_t* tmp[4];
+  int32_t* tmp[7];
   void* scan_ws;
   size_t sb;
   int rc0 = carve_plan(n, nnz, d, cv, pl, tmp, &scan_ws, &sb);
@@ -296,13 +329,22 @@ int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv,
   int32_t *nseg = tmp[0], *npart = tmp[1], *item_off = tmp[2], *part_off = tmp[3];
   const unsigned gb = (unsigned)((n + 255) / 256);
   GDD_HIP(hipMemsetAsync(pl.counts, 0, sizeof(int32_t) * 4, s));
-  k_seg_counts<<<gb, 256, 0, s>>>(n, rowptr, nseg, npart);
+  const int32_t* order = nullptr;
+  if (hop_sched() == 1) {
+    k_len_keys<<<gb, 256, 0, s>>>(n, rowptr, tmp[4], tmp[5]);
+    GDD_LAUNCHED();
+    int rc = sort_pairs_i32(tmp[4], nseg, tmp[5], tmp[6], n, kLenKeyBits, pl.sort_ws,
+                            pl.sort_bytes, s);
+    if (rc) return rc;
+    order = tmp[6];
+  }
+  k_seg_counts<<<gb, 256, 0, s>>>(n, rowptr, order, nseg, npart);
   GDD_LAUNCHED();
   int rc = exclusive_scan_i32(nseg, item_off, n, scan_ws, sb, s);
   if (rc) return rc;
   rc = exclusive_scan_i32(npart, part_off, n, scan_ws, sb, s);
   if (rc) return rc;
-  k_make_items<<<gb, 256, 0, s>>>(n, rowptr, nseg, item_off, part_off, pl.items, pl.long_rows,
+  k_make_items<<<gb, 256, 0, s>>>(n, rowptr, order, nseg, item_off, part_off, pl.items, pl.long_rows,
                                   pl.long_off, pl.counts);
   GDD_LAUNCHED();
   return GDD_OK;
@@ -352,10 +394,12 @@ void launch_hop_v(const Plan& pl, const int32_t* col, const float* val, float sc
     return launch_hop_vg<V, 8>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
   if (ov == 16)
     return launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
-  // 17..32 lanes of float4 (d in (64, 128]): two XCD slices of 16 lanes each, so an XCD's L2 caches
-  // half of every gathered row (measured at the arxiv shape, d = 128: 222.8 vs 228.5 us per hop; the
-  // gathers' L2 hit rate rises, the instruction overhead of the narrower groups stays small)
-  if (lanes <= 16 || (V == 4 && lanes <= 32 && ov != 32))
+  // 29..32 lanes of float4 (d in (112, 128]): two XCD slices of 16 lanes each, so an XCD's L2 caches
+  // half of every gathered row (measured at the arxiv shape, d = 128: 202 vs 208 us per hop; the
+  // gathers' L2 hit rate rises, the instruction overhead of the narrower groups stays small). With
+  // fewer lanes the second slice idles most of its lanes while reading the whole column/value stream
+  // again: products' d = 100 (25 lanes) runs 9.5 ms per hop in one 32-lane group vs 12.4 sliced.
+  if (lanes <= 16 || (V == 4 && lanes > 28 && lanes <= 32 && ov != 32))
     launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
   else if (lanes <= 32)
     launch_hop_vg<V, 32>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
@@ -434,7 +478,7 @@ extern "C" int gdd_spmm_planned(int64_t n, int64_t nnz, const int32_t* rowptr, c
   GDD_REQUIRE(x && y && ws, "spmm_planned: null pointer");
   Carver cv(const_cast<void*>(ws), ws_bytes);
   Plan pl;
-  int32_t* tmp[4];
+  int32_t* tmp[7];
   void* scan_ws;
   size_t sb;
   rc = carve_plan(n, nnz, d, cv, pl, tmp, &scan_ws, &sb);
