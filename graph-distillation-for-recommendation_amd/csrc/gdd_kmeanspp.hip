@@ -915,6 +915,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
 // the same block (T x the X traffic); then, per trial, np.minimum with the winner's row, the
 // cumulative-potential block total (block_prefix) and the sgemv_t block term (wave t).
 constexpr int kSplitMaxT = 8;
+constexpr int kSplitMinBlocks = 128;
 __global__ __launch_bounds__(kThr) void k_kpp_dists(KppArgs a, int c) {
   extern __shared__ double s_cs[];  // T * dim doubles (candidate rows), then T * kBlk floats
   __shared__ double s_wave[kWaves];
@@ -1850,8 +1851,11 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     return GDD_OK;
   }
   const size_t lds_split = sizeof(double) * (size_t)T * dim + sizeof(float) * (size_t)T * kBlk;
+  // the split path has one workgroup per 4096-point block: it pays only when there are enough
+  // blocks to fill the chip (products' 2.45M points: 598 blocks). With few blocks the per-(block,
+  // trial) rounds win (6,040 points: 22 vs 69 us per round; 40,000: 47 vs 84).
   const bool split = seq && a.XT && T >= 2 && T <= kSplitMaxT && lds_split <= 150 * 1024 &&
-                     getenv("GDD_KPP_FUSED_ROUND") == nullptr;
+                     nblk >= kSplitMinBlocks && getenv("GDD_KPP_FUSED_ROUND") == nullptr;
   if (split) {
     GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dists, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_split));
