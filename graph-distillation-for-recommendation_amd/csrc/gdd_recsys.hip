@@ -5,9 +5,11 @@
 //   * the per-edge dot products of the LightGCN propagation's backward (RecsysModel.propagate,
 //     :322-351: d/d norm_e of index_add_(cu, it[ci] * norm) is <grad_u[cu_e], it[ci_e]>).
 // Integer work by stable radix sorts (ci, then cu) and one scan; bit-exact.
+#include <algorithm>
 #include <climits>
 
 #include "gdd_common.hpp"
+#include "gdd_rng.hpp"
 
 namespace gdd {
 namespace {
@@ -166,6 +168,148 @@ extern "C" int gdd_edge_dots(int64_t E, int d, const int32_t* ra, const float* a
   if (E == 0) return GDD_OK;
   GDD_REQUIRE(ra && a && rb && b && out, "edge_dots: null pointer");
   k_edge_dots<<<grid1(E), kThreads, 0, to_hip(stream)>>>(E, d, ra, a, rb, b, out);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+// ---- refinement loop helpers (distill_recsys.py:217-272 sampler, :446-497 Recall@K) -------------
+namespace gdd {
+namespace {
+
+// Recall@K, pass 1: the training positives of each evaluated user scored -1e9 (:479-483)
+__global__ void k_recall_mask(int B, int64_t I, const int32_t* __restrict__ tr_ptr,
+                              const int32_t* __restrict__ tr_col, float* __restrict__ scores) {
+  const int r = blockIdx.x;
+  if (r >= B) return;
+  float* row = scores + (int64_t)r * I;
+  for (int32_t e = tr_ptr[r] + threadIdx.x; e < tr_ptr[r + 1]; e += blockDim.x) row[tr_col[e]] = -1e9f;
+}
+
+__device__ __forceinline__ uint64_t score_key(float v, int64_t j) {
+  uint32_t b = __float_as_uint(v);
+  b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);  // orderable: larger float -> larger key
+  return ((uint64_t)b << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)j);  // ties: lower index first
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t w = __shfl_xor(v, o);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
+// Recall@K, pass 2: one workgroup per evaluated user. The k largest scores (torch.topk; equal
+// scores in ascending item order) by k rounds of a block max over the row restricted to keys below
+// the previous pick, then |top-k ∩ test items| by binary search in the user's sorted, de-duplicated
+// test row; integer hits summed with one atomic per user (order-free).
+constexpr int kRecThreads = 256;
+__global__ __launch_bounds__(kRecThreads) void k_recall_topk_hits(
+    int B, int64_t I, int k, const float* __restrict__ scores, const int32_t* __restrict__ te_ptr,
+    const int32_t* __restrict__ te_col, unsigned long long* __restrict__ hits) {
+  __shared__ uint64_t s_w[kRecThreads / 64];
+  __shared__ int32_t s_pick[256];
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (r >= B) return;
+  const float* row = scores + (int64_t)r * I;
+  uint64_t prev = ~0ull;
+  for (int q = 0; q < k; ++q) {
+    uint64_t best = 0;
+    for (int64_t j = tid; j < I; j += kRecThreads) {
+      const uint64_t key = score_key(row[j], j);
+      if (key < prev && key > best) best = key;
+    }
+    best = wave_max_u64(best);
+    if (lane == 0) s_w[wave] = best;
+    __syncthreads();
+    uint64_t m = s_w[0];
+#pragma unroll
+    for (int w = 1; w < kRecThreads / 64; ++w) m = s_w[w] > m ? s_w[w] : m;
+    if (tid == 0) s_pick[q] = (int32_t)(0xFFFFFFFFu - (uint32_t)(m & 0xFFFFFFFFu));
+    prev = m;
+    __syncthreads();
+  }
+  int found = 0;
+  if (tid < k) {
+    const int32_t item = s_pick[tid];
+    int32_t lo = te_ptr[r], hi = te_ptr[r + 1];
+    while (lo < hi) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (te_col[mid] < item) lo = mid + 1; else hi = mid;
+    }
+    found = (lo < te_ptr[r + 1] && te_col[lo] == item) ? 1 : 0;
+  }
+  const unsigned long long c = __popcll(__ballot(found));
+  if (lane == 0 && c) atomicAdd(hits, c);
+}
+
+}  // namespace
+}  // namespace gdd
+
+// sample_bpr_triplets_from_condensed (distill_recsys.py:217-272) on the host, drawing from the
+// caller's numpy RandomState state exactly as the reference's Python loop does: randint(0, U, b)
+// first, then per sample the re-draws of users without a usable positive list (up to 50), the
+// positive (randint over the list), and the rejection-sampled negative (up to 50 re-draws while it
+// is a positive or equals the positive). pos lists = CSR rows (indptr int64, indices int32 in the
+// lists' own order: the positive is drawn by position); sorted (nullable: `indices` is sorted per
+// row) is the same rows sorted, for the membership test (np.isin).
+extern "C" int gdd_bpr_sample(const int64_t* indptr, const int32_t* indices, const int32_t* sorted,
+                              int64_t num_users, int64_t num_items, int64_t batch, void* state,
+                              int64_t* u_out, int64_t* pos_out, int64_t* neg_out) {
+  GDD_REQUIRE(num_users > 0 && num_items > 0 && batch >= 0, "bpr_sample: bad sizes");
+  GDD_REQUIRE(indptr && state && (batch == 0 || (u_out && pos_out && neg_out)),
+              "bpr_sample: null pointer");
+  LegacyRNG rng(static_cast<MTState*>(state));
+  auto draw = [&](int64_t hi) {
+    int64_t v;
+    rng.randint(0, hi, 1, &v);
+    return v;
+  };
+  rng.randint(0, num_users, batch, u_out);
+  for (int64_t s = 0; s < batch; ++s) {
+    int64_t uu = u_out[s];
+    auto size_of = [&](int64_t x) { return indptr[x + 1] - indptr[x]; };
+    int64_t sz = size_of(uu);
+    for (int tries = 0; tries < 50 && (sz == 0 || sz >= num_items); ++tries) {
+      uu = draw(num_users);
+      sz = size_of(uu);
+    }
+    u_out[s] = uu;
+    const int32_t* pl = indices + indptr[uu];
+    const int32_t* ps = (sorted ? sorted : indices) + indptr[uu];
+    if (sz == 0 || sz >= num_items) {  // no valid negative exists: any neg != pos
+      const int64_t p = sz == 0 ? draw(num_items) : (int64_t)pl[draw(sz)];
+      int64_t q = draw(num_items);
+      while (q == p) q = draw(num_items);
+      pos_out[s] = p;
+      neg_out[s] = q;
+      continue;
+    }
+    const int64_t p = pl[draw(sz)];
+    int64_t q = draw(num_items);
+    for (int tries = 0; tries < 50 && (std::binary_search(ps, ps + sz, (int32_t)q) || q == p); ++tries)
+      q = draw(num_items);
+    pos_out[s] = p;
+    neg_out[s] = q;
+  }
+  return GDD_OK;
+}
+
+// Recall@K over B evaluated users: scores (B x I fp32, device, overwritten by the masking),
+// tr_ptr/tr_col the users' training positives (CSR, B rows), te_ptr/te_col their de-duplicated
+// sorted test items; hits (device u64) accumulates |top-k ∩ test| over the users (not zeroed here).
+extern "C" int gdd_recall_at_k(int B, int64_t I, int k, float* scores, const int32_t* tr_ptr,
+                               const int32_t* tr_col, const int32_t* te_ptr, const int32_t* te_col,
+                               unsigned long long* hits, gdd_stream_t stream) {
+  GDD_REQUIRE(B >= 0 && I > 0 && I < INT32_MAX && k >= 1 && k <= 256 && k <= I,
+              "recall_at_k: B=%d I=%lld k=%d unsupported", B, (long long)I, k);
+  if (B == 0) return GDD_OK;
+  GDD_REQUIRE(scores && tr_ptr && te_ptr && hits, "recall_at_k: null pointer");
+  hipStream_t s = to_hip(stream);
+  k_recall_mask<<<B, 256, 0, s>>>(B, I, tr_ptr, tr_col, scores);
+  GDD_LAUNCHED();
+  k_recall_topk_hits<<<B, kRecThreads, 0, s>>>(B, I, k, scores, te_ptr, te_col, hits);
   GDD_LAUNCHED();
   return GDD_OK;
 }

@@ -13,13 +13,19 @@ Drop-ins, same names and argument meaning:
   autograd backward (the transposed products, and the edge gradient as per-edge dot products,
   ``gdd_edge_dots``). Degrees and normalisation stay the reference's torch expressions;
 * :func:`save_distilled` (:736-764) — the artefacts in the reference's formats: ``condensed_graph.npz``
-  {cu, ci, w, num_cu, num_ci}, ``u2cu.npy``, ``i2ci.npy``, ``condensed_embeddings.pt``.
+  {cu, ci, w, num_cu, num_ci}, ``u2cu.npy``, ``i2ci.npy``, ``condensed_embeddings.pt``;
+* the refinement loop's helpers (:641-733): :func:`sample_bpr_triplets_from_condensed` (:217-272) as
+  native host code drawing the same numbers from the same ``RandomState`` (``gdd_bpr_sample``), and
+  :func:`recall_at_k` (:446-497) with the masking, top-k and hit count on the device
+  (``gdd_recall_at_k``; the score GEMM is one library matmul). The driver is
+  :mod:`gdd.distill_recsys`.
 
 The message passing sums each row's edges as an fp32 fma chain in CSR order (the canonical hop order);
 the reference's ``index_add_`` (sequential on CPU, atomic on GPU) is matched to fp32 tolerance.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from dataclasses import dataclass
 from typing import Dict, Optional, Tuple
@@ -290,3 +296,125 @@ def save_distilled(out_dir: str, model: LightGCNCondensed, u2cu, i2ci, num_cu: i
                 "user_delta": model.user_delta.detach().cpu(),
                 "item_delta": model.item_delta.detach().cpu()},
                os.path.join(out_dir, "condensed_embeddings.pt"))
+
+
+# ---- refinement loop (distill_recsys.py:641-733) ---------------------------------------------------
+class PositiveLists(list):
+    """``_csr_row_to_set_list`` (distill_recsys.py:208-214): row r's column indices, as a list of
+    arrays like the reference's, also held as one CSR (``indptr`` int64, ``indices`` int32) for the
+    native sampler."""
+
+    def __init__(self, indptr, indices):
+        self.indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+        self.indices = np.ascontiguousarray(indices, dtype=np.int32)
+        super().__init__(self.indices[self.indptr[r]:self.indptr[r + 1]].astype(np.int64)
+                         for r in range(self.indptr.shape[0] - 1))
+        rows_sorted = all(np.all(np.diff(a) >= 0) for a in self)
+        self.sorted = None if rows_sorted else np.concatenate(
+            [np.sort(a) for a in self] or [np.zeros(0)]).astype(np.int32)
+
+
+def _csr_row_to_set_list(mat) -> PositiveLists:
+    if isinstance(mat, BipartiteCSR):
+        mat = mat.to_scipy()
+    mat = sp.csr_matrix(mat)
+    return PositiveLists(mat.indptr, mat.indices)
+
+
+def sample_bpr_triplets_from_condensed(pos_items_by_user, num_items: int, batch_size: int,
+                                       rng: np.random.RandomState):
+    """(u, pos_i, neg_i) int64 arrays, drawn from ``rng`` (advanced in place) in the reference's
+    order (:217-272). ``pos_items_by_user``: a :class:`PositiveLists`, a list of arrays, or a CSR."""
+    if not isinstance(pos_items_by_user, PositiveLists):
+        if sp.issparse(pos_items_by_user) or isinstance(pos_items_by_user, BipartiteCSR):
+            pos_items_by_user = _csr_row_to_set_list(pos_items_by_user)
+        else:
+            rows = [np.asarray(a, dtype=np.int64).ravel() for a in pos_items_by_user]
+            ptr = np.zeros(len(rows) + 1, np.int64)
+            np.cumsum([r.shape[0] for r in rows], out=ptr[1:])
+            pos_items_by_user = PositiveLists(ptr, np.concatenate(rows or [np.zeros(0, np.int64)]))
+    pl = pos_items_by_user
+    lib = _lib.load()
+    st = _lib.MTState.from_random_state(rng)
+    b = int(batch_size)
+    u, pos, neg = (np.empty(b, np.int64) for _ in range(3))
+    _lib.check(lib.gdd_bpr_sample(pl.indptr.ctypes.data, pl.indices.ctypes.data,
+                                  None if pl.sorted is None else pl.sorted.ctypes.data,
+                                  len(pl), int(num_items), b, ctypes.addressof(st), u.ctypes.data,
+                                  pos.ctypes.data, neg.ctypes.data))
+    st.to_random_state(rng)
+    return u, pos, neg
+
+
+def _csr_rows(ptr: np.ndarray, idx: np.ndarray, rows: np.ndarray):
+    """CSR of the selected rows (int32), in the given row order."""
+    lens = (ptr[rows + 1] - ptr[rows]).astype(np.int64)
+    out_ptr = np.zeros(rows.shape[0] + 1, np.int64)
+    np.cumsum(lens, out=out_ptr[1:])
+    gather = np.repeat(ptr[rows] - out_ptr[:-1], lens) + np.arange(out_ptr[-1])
+    return out_ptr.astype(np.int32), idx[gather].astype(np.int32)
+
+
+class RecallEvaluator:
+    """``recall_at_k`` (distill_recsys.py:446-497) with its host preparation done once: the evaluated
+    users (sorted test users, the first ``max_users``), their training positives and their
+    de-duplicated test items as device CSRs, and the denominator. Each call is one score GEMM plus
+    ``gdd_recall_at_k`` (mask, top-k, hits) and one 8-byte read."""
+
+    def __init__(self, train_R, test_u, test_i, k: int, device, max_users: int = 5000):
+        train_R = sp.csr_matrix(train_R)
+        self.device = torch.device(device)
+        test_u = np.asarray(test_u, np.int64)
+        test_i = np.asarray(test_i, np.int64)
+        users = np.unique(test_u)
+        if users.size > max_users:
+            users = users[:max_users]
+        self.users = users
+        self.num_items = int(train_R.shape[1])
+        self.k = min(int(k), self.num_items)
+        pairs = np.unique(np.stack([test_u, test_i], 1), axis=0) if test_u.size else np.zeros((0, 2), np.int64)
+        pairs = pairs[np.isin(pairs[:, 0], users)]
+        te_ptr = np.searchsorted(pairs[:, 0], np.concatenate([users, [np.iinfo(np.int64).max]]))
+        self.total = int(pairs.shape[0])
+        tr_ptr, tr_col = _csr_rows(train_R.indptr.astype(np.int64), train_R.indices, users)
+        dev = self.device
+        self.users_t = torch.from_numpy(users).to(dev)
+        self.tr_ptr, self.tr_col = torch.from_numpy(tr_ptr).to(dev), torch.from_numpy(tr_col).to(dev)
+        self.te_ptr = torch.from_numpy(te_ptr.astype(np.int32)).to(dev)
+        self.te_col = torch.from_numpy(pairs[:, 1].astype(np.int32)).to(dev)
+
+    @torch.no_grad()
+    def __call__(self, user_emb: torch.Tensor, item_emb: torch.Tensor) -> float:
+        if self.users.size == 0:
+            return 0.0
+        lib = _lib.device_lib()
+        scores = (user_emb[self.users_t] @ item_emb.t()).float().contiguous()  # [B, I] (:475-476)
+        hits = torch.zeros(1, dtype=torch.int64, device=self.device)
+        _lib.check(lib.gdd_recall_at_k(int(self.users.size), self.num_items, self.k, scores.data_ptr(),
+                                       self.tr_ptr.data_ptr(), _lib.ptr(self.tr_col),
+                                       self.te_ptr.data_ptr(), _lib.ptr(self.te_col), hits.data_ptr(),
+                                       _lib.stream_ptr(self.device)))
+        return float(int(hits.item()) / max(1, self.total))
+
+
+def recall_at_k(user_emb: torch.Tensor, item_emb: torch.Tensor, train_R, test_u, test_i, k: int,
+                device, max_users: int = 5000) -> float:
+    """Drop-in for distill_recsys.recall_at_k (:446-497); equal scores rank in ascending item order."""
+    return RecallEvaluator(train_R, test_u, test_i, k, device, max_users)(user_emb, item_emb)
+
+
+@torch.no_grad()
+def manual_adam_step(params, state: Dict[int, Dict[str, torch.Tensor]], lr: float, betas=(0.9, 0.999),
+                     eps: float = 1e-8, weight_decay: float = 0.0, step: int = 1) -> None:
+    """distill_recsys.manual_adam_step (:402-439): Adam with bias correction, the same tensor
+    expressions in the same order (so the parameter trajectory is the reference's)."""
+    b1, b2 = betas
+    for p in params:
+        if p.grad is None:
+            continue
+        g = p.grad if weight_decay == 0.0 else p.grad.add(p, alpha=weight_decay)
+        slot = state.setdefault(id(p), {"m": torch.zeros_like(p), "v": torch.zeros_like(p)})
+        m, v = slot["m"], slot["v"]
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        p.addcdiv_(m / (1 - b1 ** step), (v / (1 - b2 ** step)).sqrt().add_(eps), value=-lr)

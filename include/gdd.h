@@ -407,6 +407,24 @@ int gdd_bipartite_condense(int64_t E, const int32_t* train_u, const int32_t* tra
 int gdd_edge_dots(int64_t E, int d, const int32_t* ra, const float* a, const int32_t* rb, const float* b,
                   float* out, gdd_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------------- */
+/* (f4) the recommender's refinement loop (distill_recsys.py:641-733).                              */
+/* gdd_bpr_sample replaces sample_bpr_triplets_from_condensed (:217-272): host-only, draws from the  */
+/* caller's numpy RandomState (`state`, a gdd_mt_state, advanced in place) in the reference's order; */
+/* positive lists are CSR rows (indptr int64 [num_users+1], int32 indices in list order; `sorted`,   */
+/* nullable, the rows sorted for the membership test when `indices` is not). u/pos/neg: batch.      */
+/* gdd_recall_at_k replaces recall_at_k's masking, torch.topk and hit count (:475-497) for B users:   */
+/* scores (device, B x I, overwritten), tr_ptr/tr_col their training positives, te_ptr/te_col their   */
+/* sorted de-duplicated test items (device CSR, B rows); hits (device u64) += |top-k ∩ test|. Equal  */
+/* scores rank in ascending item order; k <= 256.                                                    */
+/* ---------------------------------------------------------------------------------------------- */
+int gdd_bpr_sample(const int64_t* indptr, const int32_t* indices, const int32_t* sorted,
+                   int64_t num_users, int64_t num_items, int64_t batch, void* state, int64_t* u_out,
+                   int64_t* pos_out, int64_t* neg_out);
+int gdd_recall_at_k(int B, int64_t I, int k, float* scores, const int32_t* tr_ptr, const int32_t* tr_col,
+                    const int32_t* te_ptr, const int32_t* te_col, unsigned long long* hits,
+                    gdd_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

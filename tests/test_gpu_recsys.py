@@ -7,6 +7,8 @@
   on CPU with the same parameters (G8): the message passing sums in CSR order instead of index_add_'s,
   so fp32 tolerances (outputs rtol 1e-5 / atol 1e-6, gradients rtol 1e-4 / atol 1e-7).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -90,3 +92,82 @@ def test_lightgcn_rejects_unsorted_edges():
                                  torch.from_numpy(z["w0"][::-1].copy()).cuda(), device=torch.device("cuda"))
     with pytest.raises(ValueError):
         m.cuda().propagate()
+
+
+# ---- the refinement loop (G11): device Recall@K and the drop-in driver ---------------------------
+def _recall_inputs(z, tag):
+    import scipy.sparse as sp
+    ue, ie = z[f"{tag}_ue"], z[f"{tag}_ie"]
+    Rtr = sp.coo_matrix((np.ones(z[f"{tag}_tr_u"].shape[0], np.float32), (z[f"{tag}_tr_u"], z[f"{tag}_tr_i"])),
+                        shape=(ue.shape[0], ie.shape[0])).tocsr()
+    return ue, ie, Rtr, z[f"{tag}_te_u"], z[f"{tag}_te_i"]
+
+
+def test_recall_at_k_device_vs_reference_and_oracle():
+    z = load("golden_refine.npz")
+    # continuous embeddings: no equal scores, the device value is the reference's
+    ue, ie, Rtr, tu, ti = _recall_inputs(z, "r0")
+    r = recsys.recall_at_k(torch.from_numpy(ue).cuda(), torch.from_numpy(ie).cuda(), Rtr, tu, ti, 20,
+                           "cuda", max_users=250)
+    assert r == float(z["r0_recall"])
+    # items sharing embeddings (as after u2cu/i2ci): equal scores at the top-k boundary. The device
+    # ranks them in ascending item order, exactly as the oracle; torch.topk's choice among them is
+    # unspecified, so the reference value is a tolerance (one boundary group).
+    ue, ie, Rtr, tu, ti = _recall_inputs(z, "r1")
+    r = recsys.recall_at_k(torch.from_numpy(ue).cuda(), torch.from_numpy(ie).cuda(), Rtr, tu, ti, 20,
+                           "cuda", max_users=250)
+    ro = R.recall(ue, ie, Rtr.indptr, Rtr.indices, tu, ti, 20, max_users=250)
+    assert r == ro
+    assert abs(r - float(z["r1_recall"])) <= 0.05
+
+
+@pytest.mark.parametrize("k,max_users", [(1, 5000), (7, 13), (64, 5000)])
+def test_recall_at_k_device_vs_oracle_shapes(k, max_users):
+    import scipy.sparse as sp
+    rng = np.random.default_rng(k)
+    nu, ni = 500, 700
+    ue = rng.standard_normal((nu, 8)).astype(np.float32)
+    ie = rng.standard_normal((ni, 8)).astype(np.float32)
+    tr = sp.random(nu, ni, density=0.05, format="csr", random_state=k, dtype=np.float32)
+    tu, ti = rng.integers(0, nu, 2000), rng.integers(0, ni, 2000)
+    r = recsys.recall_at_k(torch.from_numpy(ue).cuda(), torch.from_numpy(ie).cuda(), tr, tu, ti, k, "cuda",
+                           max_users=max_users)
+    assert r == R.recall(ue, ie, tr.indptr, tr.indices, tu, ti, k, max_users=max_users)
+
+
+def test_distill_recsys_driver_vs_reference(tmp_path, capsys):
+    """gdd.distill_recsys.run with the reference's flags on the dataset main() ran on (G11): the
+    clustering, condensed graph and sampler draws are exact; the losses follow the reference's within
+    fp32 drift (SpMM vs index_add_ order, 6 Adam steps); Recall@20 within tie resolution."""
+    from gdd import distill_recsys as D
+    z = load("golden_refine.npz")
+    lines = open(__import__("golden_util").GOLDEN + "/golden_refine_stdout.txt").read().splitlines()
+    argv = lines[0].split()
+    users, items, split = z["e2e_users"], z["e2e_items"], z["e2e_split"]
+    os.makedirs(tmp_path / "synth")
+    parts = {"train": split[0], "valid": split[1], "test": ~(split[0] | split[1])}
+    for name, m in parts.items():
+        np.savetxt(tmp_path / "synth" / f"{name}.txt", np.stack([users[m], items[m]], 1), fmt="%d")
+    args = D.parse_args(["--data_dir", str(tmp_path)] + [a if a != "cpu" else "cuda" for a in argv])
+    D.run(args, out_root=str(tmp_path / "out"), embeddings=(z["e2e_user_emb"], z["e2e_item_emb"]))
+    got = capsys.readouterr().out.splitlines()
+    ref = [l for l in lines[1:] if not l.startswith("[env]")]
+    got = [l for l in got if not l.startswith("[env]")]
+    assert len(got) == len(ref)
+    for g, r in zip(got, ref):
+        if g.startswith("[refine] ep="):
+            gl, rl = float(g.split("loss=")[1].split()[0]), float(r.split("loss=")[1].split()[0])
+            assert g.split()[1] == r.split()[1] and abs(gl - rl) <= 2e-5, (g, r)
+            assert abs(float(g.rsplit("=", 1)[1]) - float(r.rsplit("=", 1)[1])) <= 0.05, (g, r)
+        elif g.startswith("[eval]"):
+            assert abs(float(g.rsplit(" ", 1)[1]) - float(r.rsplit(" ", 1)[1])) <= 0.05, (g, r)
+        elif g.startswith("[save]"):
+            assert g.endswith("distilled_recsys/synth")
+        else:
+            assert g == r
+    out = tmp_path / "out" / "distilled_recsys" / "synth"
+    assert np.array_equal(np.load(out / "u2cu.npy"), z["e2e_u2cu"])
+    assert np.array_equal(np.load(out / "i2ci.npy"), z["e2e_i2ci"])
+    g = np.load(out / "condensed_graph.npz")
+    assert np.array_equal(g["cu"], z["e2e_cu"]) and np.array_equal(g["ci"], z["e2e_ci"])
+    np.testing.assert_allclose(g["w"], z["e2e_w"], rtol=1e-4, atol=1e-6)

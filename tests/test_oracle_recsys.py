@@ -42,3 +42,70 @@ def test_save_distilled_formats(tmp_path):
     emb = torch.load(tmp_path / "condensed_embeddings.pt", weights_only=True)
     assert sorted(emb) == ["item_delta", "item_emb", "user_delta", "user_emb"]
     assert emb["user_emb"].shape == (int(z["num_cu"]), 8)
+
+
+# ---- the refinement loop's helpers (G11: the reference's own sampler, recall_at_k and main()) ----
+def _sampler_case(z, c):
+    nu, ni, batch, seed = (int(v) for v in z[f"s{c}_meta"])
+    ptr, idx = z[f"s{c}_indptr"], z[f"s{c}_indices"]
+    rows = [idx[ptr[r]:ptr[r + 1]] for r in range(nu)]
+    return rows, ptr, idx, nu, ni, batch, seed
+
+
+def test_bpr_sampler_oracle_vs_reference():
+    z = load("golden_refine.npz")
+    for c in z["sampler_cases"]:
+        rows, _, _, nu, ni, batch, seed = _sampler_case(z, c)
+        rs = np.random.RandomState(seed)
+        u, p, n = R.bpr_triplets(rows, ni, batch, rs)
+        assert np.array_equal(u, z[f"s{c}_u"]) and np.array_equal(p, z[f"s{c}_pos"])
+        assert np.array_equal(n, z[f"s{c}_neg"])
+        st = rs.get_state(legacy=True)
+        assert np.array_equal(st[1], z[f"s{c}_key"]) and st[2] == int(z[f"s{c}_statepos"])
+
+
+def _gdd():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "graph-distillation-for-recommendation_amd"))
+    from gdd import recsys
+    return recsys
+
+
+def test_native_bpr_sampler_vs_reference():
+    # host-only native code in libgdd (gdd_bpr_sample): no device needed
+    recsys = _gdd()
+    z = load("golden_refine.npz")
+    for c in z["sampler_cases"]:
+        rows, ptr, idx, nu, ni, batch, seed = _sampler_case(z, c)
+        pl = recsys.PositiveLists(ptr, idx)
+        rs = np.random.RandomState(seed)
+        u, p, n = recsys.sample_bpr_triplets_from_condensed(pl, ni, batch, rs)
+        assert np.array_equal(u, z[f"s{c}_u"]) and np.array_equal(p, z[f"s{c}_pos"])
+        assert np.array_equal(n, z[f"s{c}_neg"])
+        st = rs.get_state(legacy=True)
+        assert np.array_equal(st[1], z[f"s{c}_key"]) and st[2] == int(z[f"s{c}_statepos"])
+        # the reference's own input form (a list of arrays) goes through the same native draws
+        u2, p2, n2 = recsys.sample_bpr_triplets_from_condensed(rows, ni, batch, np.random.RandomState(seed))
+        assert np.array_equal(u2, u) and np.array_equal(p2, p) and np.array_equal(n2, n)
+
+
+def test_native_bpr_sampler_unsorted_lists_vs_oracle():
+    recsys = _gdd()
+    rng = np.random.default_rng(5)
+    rows = [rng.permutation(50)[:rng.integers(0, 12)] for _ in range(40)]
+    rows[3] = np.arange(50)[::-1]  # a full list, descending
+    for seed in (0, 1, 2):
+        a = recsys.sample_bpr_triplets_from_condensed(rows, 50, 700, np.random.RandomState(seed))
+        b = R.bpr_triplets(rows, 50, 700, np.random.RandomState(seed))
+        assert all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+def test_recall_oracle_vs_reference_without_ties():
+    import scipy.sparse as sp
+    z = load("golden_refine.npz")
+    ue, ie = z["r0_ue"], z["r0_ie"]
+    Rtr = sp.coo_matrix((np.ones(z["r0_tr_u"].shape[0], np.float32), (z["r0_tr_u"], z["r0_tr_i"])),
+                        shape=(ue.shape[0], ie.shape[0])).tocsr()
+    r = R.recall(ue, ie, Rtr.indptr, Rtr.indices, z["r0_te_u"], z["r0_te_i"], 20, max_users=250)
+    assert r == float(z["r0_recall"])

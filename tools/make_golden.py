@@ -515,6 +515,91 @@ def g8_recsys(recsys):
     np.savez_compressed(os.path.join(OUT, "golden_recsys.npz"), **out)
 
 
+def g11_refine(recsys):
+    """The recommender's refinement loop (distill_recsys.py:217-272 sampler, :446-497 recall, :504-764
+    main on a small Rankformer-format dataset, device='cpu')."""
+    import contextlib
+    import io
+    import tempfile
+    import torch
+    out = {}
+    # (a) the BPR triplet sampler on condensed graphs with empty rows, a full row and tiny item sets
+    rng = np.random.default_rng(111)
+    cases = []
+    for ci, (nu, ni, dens, batch, seed) in enumerate([(60, 40, 0.2, 512, 42), (25, 5, 0.5, 300, 7),
+                                                       (30, 3, 0.9, 200, 3)]):
+        M = (rng.random((nu, ni)) < dens).astype(np.float32)
+        M[1] = 0.0            # a super-user without positives
+        M[2] = 1.0            # a super-user whose every item is positive
+        C = sp.csr_matrix(M)
+        pos_lists = recsys._csr_row_to_set_list(C)
+        r = np.random.RandomState(seed)
+        u, p, n = recsys.sample_bpr_triplets_from_condensed(pos_lists, ni, batch, r)
+        st = r.get_state(legacy=True)
+        out[f"s{ci}_indptr"], out[f"s{ci}_indices"] = C.indptr.astype(np.int64), C.indices.astype(np.int64)
+        out[f"s{ci}_meta"] = np.array([nu, ni, batch, seed], np.int64)
+        out[f"s{ci}_u"], out[f"s{ci}_pos"], out[f"s{ci}_neg"] = u, p, n
+        out[f"s{ci}_key"], out[f"s{ci}_statepos"] = st[1].astype(np.uint32), np.int64(st[2])
+        cases.append(ci)
+    out["sampler_cases"] = np.array(cases, np.int64)
+    # (b) recall_at_k: continuous embeddings (no ties) and cluster-shared embeddings (ties)
+    for tag, shared in (("r0", False), ("r1", True)):
+        nu, ni, d = 400, 300, 16
+        ue = rng.standard_normal((nu, d)).astype(np.float32)
+        ie = rng.standard_normal((ni, d)).astype(np.float32)
+        if shared:
+            ie = rng.standard_normal((30, d)).astype(np.float32)[rng.integers(0, 30, ni)]
+        tr_u, tr_i = rng.integers(0, nu, 3000), rng.integers(0, ni, 3000)
+        te_u, te_i = rng.integers(0, nu, 900), rng.integers(0, ni, 900)
+        Rtr = sp.coo_matrix((np.ones(3000, np.float32), (tr_u, tr_i)), shape=(nu, ni)).tocsr()
+        rec = recsys.recall_at_k(torch.from_numpy(ue), torch.from_numpy(ie), Rtr, te_u, te_i, 20,
+                                 torch.device("cpu"), max_users=250)
+        out.update({f"{tag}_ue": ue, f"{tag}_ie": ie, f"{tag}_tr_u": tr_u, f"{tag}_tr_i": tr_i,
+                    f"{tag}_te_u": te_u, f"{tag}_te_i": te_i, f"{tag}_recall": np.float64(rec)})
+    # (c) main() end to end on a small synthetic dataset (SVD embeddings captured: ARPACK's start
+    # vector is not seeded by --seed)
+    nu, ni = 600, 400
+    users = rng.integers(0, nu, 9000)
+    items = (rng.zipf(1.5, 9000) % ni)
+    perm = rng.permutation(9000)
+    tr, va, te = perm[:7000], perm[7000:8000], perm[8000:]
+    argv = ["--dataset", "synth", "--reduction_rate", "0.1", "--svd_dim", "16", "--embed_dim", "16",
+            "--lgn_layers", "2", "--refine_epochs", "6", "--batch_size", "256", "--log_every", "2",
+            "--device", "cpu", "--eval_topk", "20", "--seed", "42"]
+    with tempfile.TemporaryDirectory() as tmp:
+        os.makedirs(os.path.join(tmp, "synth"))
+        for name, idx in (("train", tr), ("valid", va), ("test", te)):
+            np.savetxt(os.path.join(tmp, "synth", f"{name}.txt"), np.stack([users[idx], items[idx]], 1), fmt="%d")
+        captured = {}
+        orig_svd = recsys.compute_svd_embeddings
+
+        def svd_capture(*a, **k):
+            captured["emb"] = orig_svd(*a, **k)
+            return captured["emb"]
+        recsys.compute_svd_embeddings = svd_capture
+        old_argv, cwd = sys.argv, os.getcwd()
+        buf = io.StringIO()
+        try:
+            sys.argv = ["distill_recsys.py", "--data_dir", tmp] + argv
+            os.chdir(tmp)
+            with contextlib.redirect_stdout(buf):
+                recsys.main()
+            art = np.load(os.path.join(tmp, "ClustGDD", "distilled_recsys", "synth", "condensed_graph.npz"))
+            out.update({"e2e_cu": art["cu"], "e2e_ci": art["ci"], "e2e_w": art["w"]})
+            out["e2e_u2cu"] = np.load(os.path.join(tmp, "ClustGDD", "distilled_recsys", "synth", "u2cu.npy"))
+            out["e2e_i2ci"] = np.load(os.path.join(tmp, "ClustGDD", "distilled_recsys", "synth", "i2ci.npy"))
+        finally:
+            sys.argv = old_argv
+            os.chdir(cwd)
+            recsys.compute_svd_embeddings = orig_svd
+    out["e2e_users"], out["e2e_items"] = users, items
+    out["e2e_split"] = np.stack([np.isin(np.arange(9000), tr), np.isin(np.arange(9000), va)], 0)
+    out["e2e_user_emb"], out["e2e_item_emb"] = captured["emb"]
+    np.savez_compressed(os.path.join(OUT, "golden_refine.npz"), **out)
+    with open(os.path.join(OUT, "golden_refine_stdout.txt"), "w") as f:
+        f.write(" ".join(argv) + "\n" + buf.getvalue())
+
+
 def main():
     from threadpoolctl import threadpool_limits
     import sklearn
@@ -541,6 +626,9 @@ def main():
             g8_recsys(recsys)
         if "G9" in which:
             g9_configs(recsys)
+        if "G11" in which:
+            torch.set_num_threads(1)
+            g11_refine(recsys)
         if "G10" in which:  # last: it patches torch.Tensor.cuda for its own run
             torch.set_num_threads(1)
             g10_agent(agent)
