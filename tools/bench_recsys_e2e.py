@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Config 4 end to end (distill_recsys.py main at the MovieLens-1M shape) on the device: the drop-in
+driver gdd.distill_recsys.run with the reference's default flags (reduction 0.1, KMeans on SVD-64
+embeddings, 500 BPR refinement epochs of batch 4096, Recall@20 every 50 epochs), on a synthetic
+Rankformer-format dataset: 6,040 users, 3,706 items, 1,000,209 unique interactions (80/10/10
+split), power-law user activity and item popularity. SVD embeddings: scipy svds on the host (timed, as in the reference).
+
+Prints the driver's own stdout and one JSON line with per-stage wall times.
+usage: bench_recsys_e2e.py [epochs]"""
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "graph-distillation-for-recommendation_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from gdd import distill_recsys as D  # noqa: E402
+
+
+def write_dataset(root, nu=6040, ni=3706, E=1000209, seed=4):
+    """Power-law user activity and item popularity (rank^-0.5 / rank^-0.8), de-duplicated and cut
+    to E unique (user, item) pairs."""
+    rng = np.random.default_rng(seed)
+    wu = np.arange(1, nu + 1, dtype=np.float64) ** -0.5
+    wi = np.arange(1, ni + 1, dtype=np.float64) ** -0.8
+    u = rng.permutation(nu)[rng.choice(nu, int(E * 1.6), p=wu / wu.sum())]
+    it = rng.permutation(ni)[rng.choice(ni, int(E * 1.6), p=wi / wi.sum())]
+    key = np.unique(u.astype(np.int64) * ni + it)
+    key = key[rng.permutation(key.shape[0])[:E]]
+    pairs = np.stack([key // ni, key % ni], 1)
+    n = pairs.shape[0]
+    a, b = int(0.8 * n), int(0.9 * n)
+    os.makedirs(os.path.join(root, "ml1m"))
+    for name, part in (("train", pairs[:a]), ("valid", pairs[a:b]), ("test", pairs[b:])):
+        np.savetxt(os.path.join(root, "ml1m", f"{name}.txt"), part, fmt="%d")
+    return n
+
+
+def main(epochs=500):
+    with tempfile.TemporaryDirectory() as tmp:
+        n = write_dataset(tmp)
+        args = D.parse_args(["--data_dir", tmp, "--dataset", "ml1m", "--refine_epochs", str(epochs)])
+        tm = {}
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        D.run(args, out_root=os.path.join(tmp, "out"), timings=tm)
+        torch.cuda.synchronize()
+        tm["total_s"] = time.perf_counter() - t0
+    tm["refine_ms_per_epoch"] = tm["refine_s"] / max(1, epochs) * 1e3
+    print(json.dumps({"workload": f"distill_recsys main, ML-1M shape: 6040 users x 3706 items, {n} unique "
+                                  f"interactions, reduction 0.1, svd 64, KMeans, {epochs} BPR epochs b=4096",
+                      **tm}), flush=True)
+
+
+if __name__ == "__main__":
+    main(*(int(a) for a in sys.argv[1:2]))
