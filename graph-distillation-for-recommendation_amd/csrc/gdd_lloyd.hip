@@ -23,6 +23,7 @@
 #include <climits>
 #include <cmath>
 #include <cstddef>
+#include <cstdlib>
 
 #include "gdd_common.hpp"
 
@@ -221,7 +222,11 @@ int group_dev(int64_t n, const int32_t* labels, int k, int32_t* perm, int32_t* o
 // alternating register sets), chunk i+1's rows are in flight into registers, and chunk i+2's member
 // ids (a three-slot ring) are loaded after the fold. Rows past a chunk's end are staged as +0.0,
 // which leaves a sum that started at +0.0 unchanged, so the fold runs in unguarded groups of 16.
-constexpr int kFoldElems = 16384;  // floats per LDS chunk buffer (64 KiB)
+constexpr int kFoldElemsMax = 16384;  // floats per LDS chunk buffer (64 KiB)
+// the cluster means use half-size chunk buffers: two workgroups fit a CU, so a launch of a few
+// hundred clusters runs in one wave instead of two (each workgroup's chunk pipeline is latency-bound;
+// arxiv bench shape, 454 clusters: 62.5 -> 50.4 us per cluster_mean call; quarter size 54.3)
+constexpr int kFoldElemsMean = 8192;
 constexpr int kFoldMaxR = 1024;
 
 struct FoldArgs {
@@ -273,7 +278,7 @@ __device__ __forceinline__ void fold_col(const float* __restrict__ col, int stri
   if (r0 < rp) add(A, WA);
 }
 
-template <typename ACC, bool VEC, bool WEIGHTED, bool MEAN>
+template <typename ACC, bool VEC, bool WEIGHTED, bool MEAN, int kFoldElems = kFoldElemsMax>
 __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
   if (stopped(a.stop, a.step_i)) return;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -402,14 +407,15 @@ int fold_launch(const FoldArgs& a0, int count, bool mean, hipStream_t s) {
   const bool weighted = a.w != nullptr;
   a.fw_max = std::min(a.dim, weighted ? 192 : 256);  // weighted: thread 255 folds the weights
   if (a.fw_max % 4 != 0 && a.fw_max < a.dim) a.fw_max &= ~3;
-  int R = std::min(kFoldMaxR, kFoldElems / a.fw_max);
+  const int elems = mean ? kFoldElemsMean : kFoldElemsMax;
+  int R = std::min(kFoldMaxR, elems / a.fw_max);
   R &= ~15;
   a.R = std::max(R, 16);
   const bool vec = a.dim % 4 == 0 && a.fw_max % 4 == 0 && (reinterpret_cast<uintptr_t>(a.X) & 15) == 0;
   const unsigned nsl = (unsigned)((a.dim + a.fw_max - 1) / a.fw_max);
   GDD_REQUIRE(count >= 0 && count < 65536, "cluster fold: %d clusters per launch", count);
   if (count == 0) return GDD_OK;
-  const size_t lds = sizeof(float) * (2 * (size_t)kFoldElems + 3 * (size_t)a.R * (weighted ? 2 : 1));
+  const size_t lds = sizeof(float) * (2 * (size_t)elems + 3 * (size_t)a.R * (weighted ? 2 : 1));
   dim3 grid(nsl, (unsigned)count);
   auto go = [&](auto kern) -> int {
     GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -417,7 +423,9 @@ int fold_launch(const FoldArgs& a0, int count, bool mean, hipStream_t s) {
     GDD_LAUNCHED();
     return GDD_OK;
   };
-  if (mean) return vec ? go(k_seg_fold<double, true, false, true>) : go(k_seg_fold<double, false, false, true>);
+  if (mean)
+    return vec ? go(k_seg_fold<double, true, false, true, kFoldElemsMean>)
+               : go(k_seg_fold<double, false, false, true, kFoldElemsMean>);
   if (weighted)
     return vec ? go(k_seg_fold<float, true, true, false>) : go(k_seg_fold<float, false, true, false>);
   return vec ? go(k_seg_fold<float, true, false, false>) : go(k_seg_fold<float, false, false, false>);
