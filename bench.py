@@ -138,6 +138,38 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max = float(t.item())
 
+    # per-phase wall times of one more (untimed) step, synchronised between phases (SURVEY §8(d):
+    # hot-path wallclock by stage and nodes clustered per second = N / k-means wallclock)
+    phases = {}
+    for _ in range(2):
+        ph = {}
+
+        def mark(name, t_prev):
+            torch.cuda.synchronize()
+            now = time.perf_counter()
+            ph[name] = (now - t_prev) * 1e3
+            return now
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        gn_p = gdd.normalize_adj(graph)
+        tp = mark("normalize", tp)
+        target_p, _ = gdd.propagate(gn_p, X, cfg.T, cfg.alpha)
+        tp = mark("propagate", tp)
+        logits_p = torch.addmm(b, target_p, W)
+        tp = mark("logits", tp)
+        if cfg.kmeans == "minibatch":
+            km_p = gdd.MiniBatchKMeans(n_clusters=cfg.k, random_state=cfg.seed, batch_size=cfg.batch,
+                                       device=dev, group=group).fit(logits_p)
+        else:
+            from gdd.pipeline import _lloyd
+            km_p = _lloyd(cfg.k, group, device=dev).fit(logits_p)
+        tp = mark("kmeans", tp)
+        gdd.cluster_mean(target_p, km_p.labels_device_, cfg.k, group=group)
+        gdd.argmax_rows(km_p.cluster_centers_device_)
+        mark("cluster_mean", tp)
+        phases = ph
+        del gn_p, target_p, logits_p, km_p
+
     # roofline of the dominant HBM kernel: one propagation hop (k_hop + its split-row fix-up), timed
     # per launch with HIP events on the stream it runs on, against a plan built once (the same
     # plan gdd_propagate builds per call)
@@ -186,6 +218,8 @@ def main():
                                    "means by clusters (RCCL all-gathers); normalise, propagation "
                                    "and minibatch steps replicated") if world > 1 else "single GPU",
                    "kmeans_steps": n_steps_km},
+        "phases_ms": phases,
+        "nodes_clustered_per_s": cfg.n / (phases["kmeans"] * 1e-3) if phases.get("kmeans") else None,
         "roofline": {"bound": "hbm", "kernel": "k_hop (+ k_fixup): one propagation hop",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
