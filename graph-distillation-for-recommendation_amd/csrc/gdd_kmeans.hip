@@ -256,6 +256,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_assign(int64_t n, int dim, int d
 // preceding them in every block. Same tiles, order and key merge as k_assign (bit-exact); with a
 // single centre chunk (gridDim.y == 1) the keys are stored, not atomically merged.
 constexpr int kPersistMaxHalf = 48;  // ceil(96 / 2) row elements per thread
+template <int NT>  // centre tiles (independent accumulator chains) per pass
 __global__ __launch_bounds__(256) void k_assign_persist(int64_t n, int dim, int dimp,
                                                        const float* __restrict__ X,
                                                        const int64_t* __restrict__ rows, int k,
@@ -310,41 +311,37 @@ __global__ __launch_bounds__(256) void k_assign_persist(int64_t n, int dim, int 
     __syncthreads();
     if (t + gridDim.x < ntiles) fetch(t + gridDim.x);  // in flight during this tile's MFMAs
     unsigned long long best = ~0ull;
-    for (int ct = 0; ct < ncp; ct += 64) {
-      const bool two = ct + 32 < ncp;
-      const float* ap0 = Cl + (ct + (lane & 31)) * S + kh;
-      const float* ap1 = two ? ap0 + 32 * S : ap0;
-      floatx16 acc0 = {}, acc1 = {};
+    for (int ct = 0; ct < ncp; ct += 32 * NT) {
+      const float* ap[NT];
+      bool live[NT];
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        live[q] = ct + 32 * q < ncp;
+        ap[q] = Cl + ((live[q] ? ct + 32 * q : ct) + (lane & 31)) * S + kh;  // dead tiles: a copy
+      }
+      floatx16 acc[NT];
+#pragma unroll
+      for (int q = 0; q < NT; ++q) acc[q] = floatx16{};
       for (int s0 = 0; s0 < ns; s0 += 8) {
-        float a0[8], a1[8], bv[8];
+        float a[NT][8], bv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int o = 2 * (s0 + u);
-          a0[u] = ap0[o];
-          a1[u] = ap1[o];
+#pragma unroll
+          for (int q = 0; q < NT; ++q) a[q][u] = ap[q][o];
           bv[u] = bp[o];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], bv[u], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], bv[u], acc1, 0, 0, 0);
-        }
-      }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ci = ct + (r & 3) + 8 * (r >> 2) + 4 * kh;
-        if (ci < nc) {
-          const float d = __builtin_fmaf(-2.f, acc0[r], Nl[ci]);
-          const unsigned long long key = pack_key(d, c0 + ci);
-          best = key < best ? key : best;
-        }
-        const int cj = ci + 32;
-        if (two && cj < nc) {
-          const float d = __builtin_fmaf(-2.f, acc1[r], Nl[cj]);
-          const unsigned long long key = pack_key(d, c0 + cj);
-          best = key < best ? key : best;
+          for (int q = 0; q < NT; ++q)
+            acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][u], bv[u], acc[q], 0, 0, 0);
         }
       }
+      // per tile: a strict float `<` scan (lowest index among equal distances), one packed key
+#pragma unroll
+      for (int q = 0; q < NT; ++q)
+        if (live[q]) best = tile_best(acc[q], Nl + ct + 32 * q, c0 + ct + 32 * q, kh, c0 + nc, best);
     }
     const unsigned long long other = __shfl_xor(best, 32);
     best = other < best ? other : best;
@@ -1341,12 +1338,18 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
       k_fill_u64<<<blocks_for(n), 256, 0, s>>>(n, keys, ~0ull, stop, step_i);
       GDD_LAUNCHED();
     }
-    if (lds > 65536)
-      GDD_HIP(hipFuncSetAttribute((const void*)k_assign_persist, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds));
-    k_assign_persist<<<dim3((unsigned)gx, (unsigned)gy), 256, lds, s>>>(n, dim, dimp16, X, rows, k, C,
-                                                                       c_norm2, cch, keys, stop, step_i);
-    GDD_LAUNCHED();
+    auto go = [&](auto kern) -> int {
+      if (lds > 65536)
+        GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      kern<<<dim3((unsigned)gx, (unsigned)gy), 256, lds, s>>>(n, dim, dimp16, X, rows, k, C, c_norm2, cch,
+                                                              keys, stop, step_i);
+      GDD_LAUNCHED();
+      return GDD_OK;
+    };
+    // two centre tiles per pass: four accumulator chains would need 292 registers, one wave per SIMD
+    // (measured 1.38 vs 0.91 ms at the products shape)
+    int rc0 = go(k_assign_persist<2>);
+    if (rc0) return rc0;
     k_assign_finalize<<<blocks_for(n), 256, 0, s>>>(n, dim, X, rows, C, keys, labels, sq_dist, stop,
                                                     step_i);
     GDD_LAUNCHED();
