@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <type_traits>
 
 #include "gdd_common.hpp"
 #include "gdd_devrng.hpp"
@@ -256,7 +257,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_assign(int64_t n, int dim, int d
 // preceding them in every block. Same tiles, order and key merge as k_assign (bit-exact); with a
 // single centre chunk (gridDim.y == 1) the keys are stored, not atomically merged.
 constexpr int kPersistMaxHalf = 48;  // ceil(96 / 2) row elements per thread
-template <int NT>  // centre tiles (independent accumulator chains) per pass
+template <int NT>  // centre tiles (independent accumulator chains) per pass; 2 (the tail pass: 1)
 __global__ __launch_bounds__(256) void k_assign_persist(int64_t n, int dim, int dimp,
                                                        const float* __restrict__ X,
                                                        const int64_t* __restrict__ rows, int k,
@@ -311,38 +312,39 @@ __global__ __launch_bounds__(256) void k_assign_persist(int64_t n, int dim, int 
     __syncthreads();
     if (t + gridDim.x < ntiles) fetch(t + gridDim.x);  // in flight during this tile's MFMAs
     unsigned long long best = ~0ull;
-    for (int ct = 0; ct < ncp; ct += 32 * NT) {
-      const float* ap[NT];
-      bool live[NT];
+    // one pass: M centre tiles from ct, M independent accumulator chains, then the per-tile scans
+    auto pass = [&](auto M_, int ct) {
+      constexpr int M = decltype(M_)::value;
+      const float* ap[M];
 #pragma unroll
-      for (int q = 0; q < NT; ++q) {
-        live[q] = ct + 32 * q < ncp;
-        ap[q] = Cl + ((live[q] ? ct + 32 * q : ct) + (lane & 31)) * S + kh;  // dead tiles: a copy
-      }
-      floatx16 acc[NT];
+      for (int q = 0; q < M; ++q) ap[q] = Cl + (ct + 32 * q + (lane & 31)) * S + kh;
+      floatx16 acc[M];
 #pragma unroll
-      for (int q = 0; q < NT; ++q) acc[q] = floatx16{};
+      for (int q = 0; q < M; ++q) acc[q] = floatx16{};
       for (int s0 = 0; s0 < ns; s0 += 8) {
-        float a[NT][8], bv[8];
+        float a[M][8], bv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int o = 2 * (s0 + u);
 #pragma unroll
-          for (int q = 0; q < NT; ++q) a[q][u] = ap[q][o];
+          for (int q = 0; q < M; ++q) a[q][u] = ap[q][o];
           bv[u] = bp[o];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
 #pragma unroll
-          for (int q = 0; q < NT; ++q)
+          for (int q = 0; q < M; ++q)
             acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][u], bv[u], acc[q], 0, 0, 0);
         }
       }
       // per tile: a strict float `<` scan (lowest index among equal distances), one packed key
 #pragma unroll
-      for (int q = 0; q < NT; ++q)
-        if (live[q]) best = tile_best(acc[q], Nl + ct + 32 * q, c0 + ct + 32 * q, kh, c0 + nc, best);
-    }
+      for (int q = 0; q < M; ++q)
+        best = tile_best(acc[q], Nl + ct + 32 * q, c0 + ct + 32 * q, kh, c0 + nc, best);
+    };
+    int ct = 0;
+    for (; ct + 32 * NT <= ncp; ct += 32 * NT) pass(std::integral_constant<int, NT>(), ct);
+    if (ct < ncp) pass(std::integral_constant<int, 1>(), ct);  // an odd last tile runs alone
     const unsigned long long other = __shfl_xor(best, 32);
     best = other < best ? other : best;
     if (lane < 32) {
