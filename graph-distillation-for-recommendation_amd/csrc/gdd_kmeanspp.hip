@@ -1378,124 +1378,24 @@ __device__ void kpp1_fold(const Kpp1FoldView& a, const float* __restrict__ s_row
   }
 }
 
-constexpr int kMaxDimF = 512;  // fused rounds: candidate rows up to this many features
-
-// ---- single-block rounds in ONE launch. Grid (point blocks of 256, T trials): workgroup (b, t)
-// computes trial t's distances for its 256 points; the last workgroup of trial t to finish folds
-// trial t (the pick work: its exact sgemv_t potential, its cumulative potential, and the candidates
-// every trial would draw in round c+1 if t wins). Hand-off without fences, in the first form of
-// MI355X_MICROARCH.md's table: every distance store sc1 (write-through), every storing wave drained
-// (vmcnt(0)), a workgroup barrier, one lane's agent-scope add to the trial's counter for the round;
-// the workgroup whose add returns G-1 reads the row back with sc1 loads. Nothing spins.
-constexpr int kFPts = 256;   // points per distance workgroup
 constexpr int kFPW = 22;     // prefix entries per thread of waves 1..3 in the fold (192 x 22 >= 4096)
 
-template <bool SEQ>
-__global__ __launch_bounds__(256) void k_kpp1_fused(Kpp1Args a, int c) {
-  __shared__ double s_c[kMaxDimF];              // this trial's candidate row (fp64, zero-padded)
-  __shared__ float s_d[kBlk];                   // fold: the row, natural order
-  __shared__ float s_ch[8 * kChainLd];          // fold: chain-major copy (unit weights)
-  __shared__ double s_cum[kBlk];               // fold: the winner-if row's cumulative potential
-  __shared__ double s_wave[4];
-  __shared__ float s_pot;
-  __shared__ double s_cn;
-  __shared__ int s_last;
+// the fold of round c's trial t by one 256-thread workgroup holding the trial's row in registers
+// (r[q] = entry tid + 256 q): the exact sgemv_t potential, the fp64 cumulative potential and the
+// candidates every trial would draw in round c+1 if t wins
+__device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t, const float (&r)[16],
+                                                double ut, float* __restrict__ s_d,
+                                                float* __restrict__ s_ch, double* __restrict__ s_cum,
+                                                double* __restrict__ s_wave, float* __restrict__ s_pot_p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int t = blockIdx.y, pq = (c - 1) & 1, cq = c & 1, T = a.T, dim = a.dim;
-  const int Tp = c == 1 ? 1 : T;  // trials of round c-1 (round 0: the first centre)
+  const int cq = c & 1, T = a.T;
   const int n = (int)a.n;
-  const int i = blockIdx.x * kFPts + tid;
-  const int ic = min(i, n - 1);
-  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && t == 0 && c == a.k - 2), 60);
-  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && t == 0 && c == a.k - 1), 65);
-  // round trip 1: the point's column, round c-1's potentials and this trial's column of its table
-  constexpr int kX = SEQ ? 48 : 1;
-  float x[kX];
-  if (SEQ && dim <= kX) {
-#pragma unroll
-    for (int v = 0; v < kX; ++v) x[v] = a.XT[(int64_t)min(v, dim - 1) * n + ic];
-  }
-  const double xs = a.xsq[ic];
-  float pv[kMaxTrials], dv[kMaxTrials];
-  int64_t cw[kMaxTrials];
-  // every trial's distance for this point too (the winner is not known yet): the winner's row
-  // then costs no dependent round trip of its own
-  const float* dprev = c == 1 ? a.closest0 : a.dist[pq];
-#pragma unroll
-  for (int q = 0; q < kMaxTrials; ++q) {
-    pv[q] = a.potv[pq][min(q, Tp - 1)];
-    cw[q] = a.candw[pq][(int64_t)min(q, Tp - 1) * T + t];
-    dv[q] = dprev[(int64_t)min(q, Tp - 1) * n + ic];
-  }
-  int bw = 0;  // np.argmin: first minimum, a NaN wins at once
-  float best = pv[0];
-  int64_t ct = cw[0];
-  float wi = dv[0];
-#pragma unroll
-  for (int q = 1; q < kMaxTrials; ++q) {
-    const float pt = pv[q];
-    if (q < Tp && best == best && (pt < best || pt != pt)) {
-      bw = q;
-      best = pt;
-      ct = cw[q];
-      wi = dv[q];
-    }
-  }
-  // round trip 2: this trial's candidate row
-  const int cs = (SEQ && dim <= kX) ? kX : dim;
-  for (int j = tid; j < cs; j += 256) s_c[j] = j < dim ? (double)a.X[ct * dim + min(j, dim - 1)] : 0.0;
-  if (tid == 0) s_cn = a.xsq[ct];
-  if (blockIdx.x == 0 && tid == 0) {
-    a.candself[cq][t] = ct;
-    if (c >= 2 && t == 0) a.indices[c - 1] = a.candself[pq][bw];  // rows gathered after the rounds
-  }
-  __syncthreads();
-  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && t == 0 && c == a.k - 2), 61);
-  if (i < n) {
-    double dot = 0.0;
-    if constexpr (SEQ) {
-      if (dim <= kX) {
-#pragma unroll
-        for (int v = 0; v < kX; ++v) dot = __builtin_fma(s_c[v], (double)x[v], dot);
-      } else {
-        for (int j = 0; j < dim; j += 16) {
-          float y[16];
-#pragma unroll
-          for (int v = 0; v < 16; ++v) y[v] = a.XT[(int64_t)min(j + v, dim - 1) * n + i];
-#pragma unroll
-          for (int v = 0; v < 16; ++v)
-            if (j + v < dim) dot = __builtin_fma(s_c[j + v], (double)y[v], dot);
-        }
-      }
-    } else {
-      dot = skl_point_dot(a.plan, s_c, a.X + (int64_t)i * dim, i, t);
-    }
-    float f = (float)(((-2.0 * dot) + s_cn) + xs);
-    f = f < 0.f ? 0.f : f;
-    __hip_atomic_store(a.dist[cq] + (int64_t)t * n + i, np_minimum(wi, f), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);  // sc1: write-through
-  }
-  // hand-off: every storing wave drained, barrier, one agent-scope add per workgroup
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0)
-    s_last = __hip_atomic_fetch_add(a.counter + (int64_t)c * T + t, 1u, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 62);
-  // ---- fold trial t (its last workgroup): the row back with sc1 loads
-  const double ut = (c + 1 < a.k && tid < T) ? a.uniforms[(int64_t)c * T + tid] : 0.0;
+  float& s_pot = *s_pot_p;
   const int m1 = (int)a.m1;
   const bool k4x2 = (T & 2) && t >= (T & ~3) && t < (T & ~3) + 2;
   const int h4 = k4x2 ? 0 : (m1 & 4);
   const bool perm = a.w == nullptr;
   {
-    const float* row = a.dist[cq] + (int64_t)t * n;
-    float r[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q)
-      r[q] = __hip_atomic_load(row + min(tid + 256 * q, n - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = tid + 256 * q;
@@ -1593,6 +1493,229 @@ __global__ __launch_bounds__(256) void k_kpp1_fused(Kpp1Args a, int c) {
     }
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 74);
+}
+
+
+constexpr int kMaxDimF = 512;  // fused rounds: candidate rows up to this many features
+
+// ---- single-block rounds in ONE launch. Grid (point blocks of 256, T trials): workgroup (b, t)
+// computes trial t's distances for its 256 points; the last workgroup of trial t to finish folds
+// trial t (the pick work: its exact sgemv_t potential, its cumulative potential, and the candidates
+// every trial would draw in round c+1 if t wins). Hand-off without fences, in the first form of
+// MI355X_MICROARCH.md's table: every distance store sc1 (write-through), every storing wave drained
+// (vmcnt(0)), a workgroup barrier, one lane's agent-scope add to the trial's counter for the round;
+// the workgroup whose add returns G-1 reads the row back with sc1 loads. Nothing spins.
+constexpr int kFPts = 256;   // points per distance workgroup
+template <bool SEQ>
+__global__ __launch_bounds__(256) void k_kpp1_fused(Kpp1Args a, int c) {
+  __shared__ double s_c[kMaxDimF];              // this trial's candidate row (fp64, zero-padded)
+  __shared__ float s_d[kBlk];                   // fold: the row, natural order
+  __shared__ float s_ch[8 * kChainLd];          // fold: chain-major copy (unit weights)
+  __shared__ double s_cum[kBlk];               // fold: the winner-if row's cumulative potential
+  __shared__ double s_wave[4];
+  __shared__ float s_pot;
+  __shared__ double s_cn;
+  __shared__ int s_last;
+  const int tid = threadIdx.x;
+  const int t = blockIdx.y, pq = (c - 1) & 1, cq = c & 1, T = a.T, dim = a.dim;
+  const int Tp = c == 1 ? 1 : T;  // trials of round c-1 (round 0: the first centre)
+  const int n = (int)a.n;
+  const int i = blockIdx.x * kFPts + tid;
+  const int ic = min(i, n - 1);
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && t == 0 && c == a.k - 2), 60);
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && t == 0 && c == a.k - 1), 65);
+  // round trip 1: the point's column, round c-1's potentials and this trial's column of its table
+  constexpr int kX = SEQ ? 48 : 1;
+  float x[kX];
+  if (SEQ && dim <= kX) {
+#pragma unroll
+    for (int v = 0; v < kX; ++v) x[v] = a.XT[(int64_t)min(v, dim - 1) * n + ic];
+  }
+  const double xs = a.xsq[ic];
+  float pv[kMaxTrials], dv[kMaxTrials];
+  int64_t cw[kMaxTrials];
+  // every trial's distance for this point too (the winner is not known yet): the winner's row
+  // then costs no dependent round trip of its own
+  const float* dprev = c == 1 ? a.closest0 : a.dist[pq];
+#pragma unroll
+  for (int q = 0; q < kMaxTrials; ++q) {
+    pv[q] = a.potv[pq][min(q, Tp - 1)];
+    cw[q] = a.candw[pq][(int64_t)min(q, Tp - 1) * T + t];
+    dv[q] = dprev[(int64_t)min(q, Tp - 1) * n + ic];
+  }
+  int bw = 0;  // np.argmin: first minimum, a NaN wins at once
+  float best = pv[0];
+  int64_t ct = cw[0];
+  float wi = dv[0];
+#pragma unroll
+  for (int q = 1; q < kMaxTrials; ++q) {
+    const float pt = pv[q];
+    if (q < Tp && best == best && (pt < best || pt != pt)) {
+      bw = q;
+      best = pt;
+      ct = cw[q];
+      wi = dv[q];
+    }
+  }
+  // round trip 2: this trial's candidate row
+  const int cs = (SEQ && dim <= kX) ? kX : dim;
+  for (int j = tid; j < cs; j += 256) s_c[j] = j < dim ? (double)a.X[ct * dim + min(j, dim - 1)] : 0.0;
+  if (tid == 0) s_cn = a.xsq[ct];
+  if (blockIdx.x == 0 && tid == 0) {
+    a.candself[cq][t] = ct;
+    if (c >= 2 && t == 0) a.indices[c - 1] = a.candself[pq][bw];  // rows gathered after the rounds
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blockIdx.x == 0 && t == 0 && c == a.k - 2), 61);
+  if (i < n) {
+    double dot = 0.0;
+    if constexpr (SEQ) {
+      if (dim <= kX) {
+#pragma unroll
+        for (int v = 0; v < kX; ++v) dot = __builtin_fma(s_c[v], (double)x[v], dot);
+      } else {
+        for (int j = 0; j < dim; j += 16) {
+          float y[16];
+#pragma unroll
+          for (int v = 0; v < 16; ++v) y[v] = a.XT[(int64_t)min(j + v, dim - 1) * n + i];
+#pragma unroll
+          for (int v = 0; v < 16; ++v)
+            if (j + v < dim) dot = __builtin_fma(s_c[j + v], (double)y[v], dot);
+        }
+      }
+    } else {
+      dot = skl_point_dot(a.plan, s_c, a.X + (int64_t)i * dim, i, t);
+    }
+    float f = (float)(((-2.0 * dot) + s_cn) + xs);
+    f = f < 0.f ? 0.f : f;
+    __hip_atomic_store(a.dist[cq] + (int64_t)t * n + i, np_minimum(wi, f), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);  // sc1: write-through
+  }
+  // hand-off: every storing wave drained, barrier, one agent-scope add per workgroup
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    s_last = __hip_atomic_fetch_add(a.counter + (int64_t)c * T + t, 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 62);
+  // ---- fold trial t (its last workgroup): the row back with sc1 loads
+  const double ut = (c + 1 < a.k && tid < T) ? a.uniforms[(int64_t)c * T + tid] : 0.0;
+  float r[16];
+  {
+    const float* row = a.dist[cq] + (int64_t)t * n;
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      r[q] = __hip_atomic_load(row + min(tid + 256 * q, n - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  kpp1_fold_trial(a, c, t, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot);
+}
+
+// ---- single-block rounds from a distance table (plain-chain plans, dim <= 48, n <= 4096). The
+// plain fp64 chain of a distance does not depend on the trial slot the candidate occupies, so every
+// distance a round can ask for is one entry of D[j][i] = the clamped fp32 upcast distance between
+// candidate point j and point i, computed once per fit by k_kpp_dmat in exactly the arithmetic of
+// the distance phase above (zero-padded 48-term fma chain, ((-2 dot) + |c|^2) + |x|^2, clamp).
+// A round is then ONE workgroup per trial: round c-1's potentials and this trial's candidate column
+// (trip 1), the winner's row = the closest distances and the candidate's D row (trip 2), the fold.
+// No distance phase, no write-through hand-off, no re-read of the row.
+constexpr int kDmX = 48;   // feature slots of the table's chain (dim <= kDmX, zero-padded)
+constexpr int kDmJ = 32;   // candidate rows per table workgroup
+constexpr int kDmMinK = 16;  // centres from which the table is built
+
+__global__ __launch_bounds__(256) void k_kpp_dmat(int n, int dim, const float* __restrict__ X,
+                                                  const float* __restrict__ XT,
+                                                  const double* __restrict__ xsq,
+                                                  float* __restrict__ D) {
+  __shared__ double s_c[kDmJ * kDmX];
+  __shared__ double s_cn[kDmJ];
+  const int tid = threadIdx.x;
+  const int i = blockIdx.x * 256 + tid, ic = min(i, n - 1);
+  const int j0 = blockIdx.y * kDmJ;
+  float x[kDmX];
+#pragma unroll
+  for (int v = 0; v < kDmX; ++v) x[v] = XT[(int64_t)min(v, dim - 1) * n + ic];
+  for (int e = tid; e < kDmJ * kDmX; e += 256) {
+    const int jj = e / kDmX, v = e - jj * kDmX;
+    const int j = min(j0 + jj, n - 1);
+    s_c[e] = v < dim ? (double)X[(int64_t)j * dim + v] : 0.0;
+  }
+  if (tid < kDmJ) s_cn[tid] = xsq[min(j0 + tid, n - 1)];
+  const double xs = xsq[ic];
+  __syncthreads();
+  for (int jj = 0; jj < kDmJ; jj += 4) {
+    double dot[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int v = 0; v < kDmX; ++v)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) dot[u] = __builtin_fma(s_c[(jj + u) * kDmX + v], (double)x[v], dot[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + jj + u;
+      float f = (float)(((-2.0 * dot[u]) + s_cn[jj + u]) + xs);
+      f = f < 0.f ? 0.f : f;
+      if (i < n && j < n) D[(int64_t)j * n + i] = f;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __restrict__ D, int c) {
+  __shared__ float s_d[kBlk];
+  __shared__ float s_ch[8 * kChainLd];
+  __shared__ double s_cum[kBlk];
+  __shared__ double s_wave[4];
+  __shared__ float s_pot;
+  const int tid = threadIdx.x;
+  const int t = blockIdx.x, pq = (c - 1) & 1, cq = c & 1, T = a.T;
+  const int Tp = c == 1 ? 1 : T;  // trials of round c-1 (round 0: the first centre)
+  const int n = (int)a.n;
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 60);
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 1), 65);
+  // trip 1: round c-1's potentials and this trial's column of its candidate table
+  float pv[kMaxTrials];
+  int64_t cw[kMaxTrials];
+#pragma unroll
+  for (int q = 0; q < kMaxTrials; ++q) {
+    pv[q] = a.potv[pq][min(q, Tp - 1)];
+    cw[q] = a.candw[pq][(int64_t)min(q, Tp - 1) * T + t];
+  }
+  const double ut = (c + 1 < a.k && tid < T) ? a.uniforms[(int64_t)c * T + tid] : 0.0;
+  int bw = 0;  // np.argmin: first minimum, a NaN wins at once
+  float best = pv[0];
+  int64_t ct = cw[0];
+#pragma unroll
+  for (int q = 1; q < kMaxTrials; ++q) {
+    const float pt = pv[q];
+    if (q < Tp && best == best && (pt < best || pt != pt)) {
+      bw = q;
+      best = pt;
+      ct = cw[q];
+    }
+  }
+  if (tid == 0) {
+    a.candself[cq][t] = ct;
+    if (c >= 2 && t == 0) a.indices[c - 1] = a.candself[pq][bw];  // rows gathered after the rounds
+  }
+  // trip 2: the closest distances (round c-1's winning row) and the candidate's table row
+  const float* wrow = c == 1 ? a.closest0 : a.dist[pq] + (int64_t)bw * n;
+  const float* drow = D + ct * n;
+  float wi[16], dd[16], r[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = min(tid + 256 * q, n - 1);
+    wi[q] = wrow[e];
+    dd[q] = drow[e];
+  }
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 61);
+  float* orow = a.dist[cq] + (int64_t)t * n;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    r[q] = np_minimum(wi[q], dd[q]);
+    if (tid + 256 * q < n) orow[tid + 256 * q] = r[q];
+  }
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 62);
+  kpp1_fold_trial(a, c, t, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot);
 }
 
 // after round k-1: its winner and centre
@@ -1712,6 +1835,7 @@ size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k) {
   b += align256(sizeof(int) * 2) + align256(sizeof(unsigned) * (size_t)std::max(k, 1) * T);  // counters
   if (n <= kBlk || (int64_t)n * std::max(dim, 1) < INT_MAX)
     b += align256(sizeof(float) * n * (size_t)std::max(dim, 1));  // XT
+  if (n <= kBlk && dim <= kDmX && T >= 2) b += align256(sizeof(float) * n * n);  // distance table
   return b + 1024;
 }
 
@@ -1751,6 +1875,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   b1.win = cv.take<int>(2);
   b1.counter = cv.take<unsigned>((size_t)std::min<int64_t>(n, INT_MAX) * T);
   float* XT = (n <= kBlk || n * (int64_t)dim < INT_MAX) ? cv.take<float>((size_t)n * dim) : nullptr;
+  float* Dm = (n <= kBlk && dim <= kDmX && T >= 2) ? cv.take<float>((size_t)n * n) : nullptr;
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans++: workspace too small");
   a.n = n;
   a.m1 = n & ~3ll;
@@ -1817,6 +1942,24 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     const dim3 g1((unsigned)((n + kPts - 1) / kPts), (unsigned)(((T + kTg - 1) / kTg + 3) / 4));
     k_kpp1_pick<<<1, kThr, 0, s>>>(b1, 0);
     GDD_LAUNCHED();
+    // the distance table pays once the rounds it saves (~3 us each) cover its one-off build
+    if (seq && Dm && k >= kDmMinK && getenv("GDD_KPP_NO_TABLE") == nullptr) {
+      k_kpp_dmat<<<dim3((unsigned)((n + 255) / 256), (unsigned)((n + kDmJ - 1) / kDmJ)), 256, 0, s>>>(
+          (int)n, dim, X, XT, xsq, Dm);
+      GDD_LAUNCHED();
+      for (int c = 1; c < k; ++c) {
+        k_kpp1_dm<<<(unsigned)T, 256, 0, s>>>(b1, Dm, c);
+        GDD_LAUNCHED();
+      }
+      k_kpp1_final<<<1, 64, 0, s>>>(b1, k - 1);
+      GDD_LAUNCHED();
+      if (k > 2) {
+        k_kpp_gather_centres<<<(unsigned)(((int64_t)k * dim + 255) / 256), 256, 0, s>>>(k, dim, X, indices,
+                                                                                         centers);
+        GDD_LAUNCHED();
+      }
+      return GDD_OK;
+    }
     const dim3 gf((unsigned)((n + kFPts - 1) / kFPts), (unsigned)T);
     if (dim <= kMaxDimF && gf.x * gf.y <= 256 && getenv("GDD_KPP_TWO_LAUNCH") == nullptr) {
       // one launch per round: distances, then each trial's last workgroup folds it (no fences)

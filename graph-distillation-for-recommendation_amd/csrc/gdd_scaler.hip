@@ -117,43 +117,50 @@ namespace {
 
 // dim > 1. Each column's sums are sequential fp32 chains over all n rows, so the kernel is bound by
 // the add chain (one dependent v_add_f32 per row) as long as rows arrive fast enough. Workgroup g
-// owns columns [8g, 8g + w): chunks of 1024 rows x 8 columns are staged through two LDS buffers (the
-// next chunk's loads in flight in registers while lane j of wave 0 folds column j with 16 LDS reads
-// ahead of its adds), then, in the second pass, every thread writes its staged elements of x - mean.
-// Only blocks with blockIdx % 8 == 0 work: they share one XCD's L2 under the observed round-robin
-// placement, so X's lines come from HBM once for all column groups (speed only, not correctness).
+// owns columns [8g, 8g + w): chunks of 1024 rows x 8 columns are staged through two LDS buffers,
+// column-major (the next chunk's loads in flight in registers meanwhile); lane j of wave 0 folds
+// column j reading 16-byte groups of 4 rows, the next 32 rows' reads issued before the current 32
+// dependent adds, so the LDS latency hides behind the chain. In the second pass every thread also
+// writes its staged elements of x - mean. Only blocks with blockIdx % 8 == 0 work: they share one
+// XCD's L2 under the observed round-robin placement, so X's lines come from HBM once for all column
+// groups (speed only, not correctness).
 constexpr int kCW = 8;                     // columns per workgroup
 constexpr int kCR = 1024;                  // rows per staged chunk
 constexpr int kCQ = kCR * kCW / 256;       // staged elements per thread per chunk
+constexpr int kCS = kCR + 8;               // column stride in LDS: (8c + r) % 64 banks, 16-B rows
 constexpr int kColXcd = 8;
 
-__device__ __forceinline__ float col_fold(const float* __restrict__ col, int rows, int pass, float m,
-                                          float acc) {
-  // rows of this chunk, stride kCW; 16 LDS reads in flight ahead of the dependent adds
+template <int PASS>
+__device__ __forceinline__ float col_add(float acc, float x, float m) {
+  if (PASS == 0) return acc + x;
+  const float d = x - m;
+  return acc + d * d;
+}
+
+template <int PASS>
+__device__ __forceinline__ float col_fold(const float* __restrict__ col, int rows, float m, float acc) {
   int r = 0;
-  for (; r + 16 <= rows; r += 16) {
-    float v[16];
+  if (rows >= 32) {
+    float4 cur[8];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = col[(r + u) * kCW];
+    for (int u = 0; u < 8; ++u) cur[u] = *reinterpret_cast<const float4*>(col + 4 * u);
+    for (; r + 32 <= rows; r += 32) {
+      // the next group's reads (past `rows` they land in the padding and are never folded)
+      float4 nxt[8];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      if (pass == 0) {
-        acc = acc + v[u];
-      } else {
-        const float d = v[u] - m;
-        acc = acc + d * d;
+      for (int u = 0; u < 8; ++u) nxt[u] = *reinterpret_cast<const float4*>(col + r + 32 + 4 * u);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc = col_add<PASS>(acc, cur[u].x, m);
+        acc = col_add<PASS>(acc, cur[u].y, m);
+        acc = col_add<PASS>(acc, cur[u].z, m);
+        acc = col_add<PASS>(acc, cur[u].w, m);
       }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
     }
   }
-  for (; r < rows; ++r) {
-    const float x = col[r * kCW];
-    if (pass == 0) {
-      acc = acc + x;
-    } else {
-      const float d = x - m;
-      acc = acc + d * d;
-    }
-  }
+  for (; r < rows; ++r) acc = col_add<PASS>(acc, col[r], m);
   return acc;
 }
 
@@ -161,7 +168,8 @@ __global__ __launch_bounds__(256) void k_col_stats(int64_t n, int dim, const flo
                                                    float* __restrict__ X_out, float* __restrict__ mean,
                                                    float* __restrict__ var) {
   if (blockIdx.x % kColXcd) return;
-  __shared__ __attribute__((aligned(16))) float buf[2][kCR * kCW];
+  // two column-major chunk buffers, plus the padding the fold's look-ahead reads may touch
+  __shared__ __attribute__((aligned(16))) float buf[2 * kCW * kCS + 32];
   __shared__ float s_m[kCW];
   const int tid = threadIdx.x;
   const int c0 = (int)(blockIdx.x / kColXcd) * kCW, w = min(kCW, dim - c0);
@@ -178,7 +186,10 @@ __global__ __launch_bounds__(256) void k_col_stats(int64_t n, int dim, const flo
   };
   auto store = [&](int slot) {
 #pragma unroll
-    for (int q = 0; q < kCQ; ++q) buf[slot][tid + 256 * q] = v[q];
+    for (int q = 0; q < kCQ; ++q) {
+      const int e = tid + 256 * q;
+      buf[slot * kCW * kCS + (e & (kCW - 1)) * kCS + (e >> 3)] = v[q];
+    }
   };
   float m = 0.f;
   for (int pass = 0; pass < 2; ++pass) {
@@ -190,13 +201,15 @@ __global__ __launch_bounds__(256) void k_col_stats(int64_t n, int dim, const flo
     int slot = 0;
     for (int64_t r0 = 0; r0 < n; r0 += kCR) {
       const int rows = (int)min((int64_t)kCR, n - r0);
-      if (tid < w) acc = col_fold(&buf[slot][tid], rows, pass, m, acc);
+      const float* sb = buf + slot * kCW * kCS;
+      if (tid < w) acc = pass == 0 ? col_fold<0>(sb + tid * kCS, rows, m, acc)
+                                   : col_fold<1>(sb + tid * kCS, rows, m, acc);
       if (pass == 1) {  // x - mean, written from the staged chunk by every thread
 #pragma unroll
         for (int q = 0; q < kCQ; ++q) {
           const int e = tid + 256 * q;
           const int r = e >> 3, c = e & (kCW - 1);
-          if (c < w && r < rows) X_out[(r0 + r) * dim + c0 + c] = buf[slot][e] - s_m[c];
+          if (c < w && r < rows) X_out[(r0 + r) * dim + c0 + c] = sb[c * kCS + r] - s_m[c];
         }
       }
       if (r0 + kCR < n) {
