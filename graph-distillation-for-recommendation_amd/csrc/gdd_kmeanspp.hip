@@ -1176,19 +1176,56 @@ __global__ __launch_bounds__(256) void k_kpp1_dist(Kpp1Args a, int c) {
 }
 
 // one sgemv_t lane chain over L entries stored contiguously in LDS (chain-major layout):
-// acc = acc + x in order, float4 reads issued 8 ahead of the dependent adds
-__device__ __forceinline__ float chain_add(const float* __restrict__ p, int L, float acc) {
+// acc = acc + x in order. Two 32-entry register groups alternate, each group's 16-byte reads issued a
+// whole group of dependent adds ahead of their use (scheduling barriers keep them there; the first
+// group goes through an empty asm so InstCombine cannot turn the loop's phi of loads into a load of
+// a phi of addresses, which would put every read right in front of its adds). Look-ahead reads run
+// at most 63 entries past L, inside the lane's kChainLd-float row.
+__device__ __forceinline__ void chain_load32(const float* __restrict__ p, float4 (&v)[8]) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + 4 * u);
+}
+
+__device__ __forceinline__ void chain_add32(const float4 (&v)[8], float& acc) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    acc = acc + v[u].x;
+    acc = acc + v[u].y;
+    acc = acc + v[u].z;
+    acc = acc + v[u].w;
+  }
+}
+
+// the plain form (reads of a group issued just before its adds), kept for A/B timing
+__device__ __forceinline__ float chain_add_plain(const float* __restrict__ p, int L, float acc) {
   int m = 0;
   for (; m + 32 <= L; m += 32) {
     float4 v[8];
+    chain_load32(p + m, v);
+    chain_add32(v, acc);
+  }
+  for (; m < L; ++m) acc = acc + p[m];
+  return acc;
+}
+
+template <bool PIPE = true>
+__device__ __forceinline__ float chain_add(const float* __restrict__ p, int L, float acc) {
+  if (!PIPE) return chain_add_plain(p, L, acc);
+  int m = 0;
+  if (L >= 64) {
+    float4 A[8], B[8];
+    chain_load32(p, A);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + m + 4 * u);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      acc = acc + v[u].x;
-      acc = acc + v[u].y;
-      acc = acc + v[u].z;
-      acc = acc + v[u].w;
+    for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(A[u].x), "+v"(A[u].y), "+v"(A[u].z), "+v"(A[u].w));
+    for (; m + 64 <= L; m += 64) {
+      chain_load32(p + m + 32, B);
+      __builtin_amdgcn_sched_barrier(0);
+      chain_add32(A, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      chain_load32(p + m + 64, A);
+      __builtin_amdgcn_sched_barrier(0);
+      chain_add32(B, acc);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   for (; m < L; ++m) acc = acc + p[m];
@@ -1383,6 +1420,7 @@ constexpr int kFPW = 22;     // prefix entries per thread of waves 1..3 in the f
 // the fold of round c's trial t by one 256-thread workgroup holding the trial's row in registers
 // (r[q] = entry tid + 256 q): the exact sgemv_t potential, the fp64 cumulative potential and the
 // candidates every trial would draw in round c+1 if t wins
+template <bool PIPE = true>
 __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t, const float (&r)[16],
                                                 double ut, float* __restrict__ s_d,
                                                 float* __restrict__ s_ch, double* __restrict__ s_cum,
@@ -1424,7 +1462,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
         if (lane < nl) {
           if (lane < h4) acc = acc + s_d[lane];
           const int L = (m1 - h4 - lane + nl - 1) / nl;
-          acc = chain_add(s_ch + lane * kChainLd, max(L, 0), acc);
+          acc = chain_add<PIPE>(s_ch + lane * kChainLd, max(L, 0), acc);
         }
         if (k4x2) {
           const float a1 = __shfl(acc, 1), a2 = __shfl(acc, 2), a3 = __shfl(acc, 3);
@@ -1660,6 +1698,7 @@ __global__ __launch_bounds__(256) void k_kpp_dmat(int n, int dim, const float* _
   }
 }
 
+template <bool PIPE>
 __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __restrict__ D, int c) {
   __shared__ float s_d[kBlk];
   __shared__ float s_ch[8 * kChainLd];
@@ -1715,7 +1754,7 @@ __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __rest
     if (tid + 256 * q < n) orow[tid + 256 * q] = r[q];
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 62);
-  kpp1_fold_trial(a, c, t, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot);
+  kpp1_fold_trial<PIPE>(a, c, t, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot);
 }
 
 // after round k-1: its winner and centre
@@ -1947,8 +1986,12 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       k_kpp_dmat<<<dim3((unsigned)((n + 255) / 256), (unsigned)((n + kDmJ - 1) / kDmJ)), 256, 0, s>>>(
           (int)n, dim, X, XT, xsq, Dm);
       GDD_LAUNCHED();
+      const bool plain = getenv("GDD_KPP_CHAIN_PLAIN") != nullptr;
       for (int c = 1; c < k; ++c) {
-        k_kpp1_dm<<<(unsigned)T, 256, 0, s>>>(b1, Dm, c);
+        if (plain)
+          k_kpp1_dm<false><<<(unsigned)T, 256, 0, s>>>(b1, Dm, c);
+        else
+          k_kpp1_dm<true><<<(unsigned)T, 256, 0, s>>>(b1, Dm, c);
         GDD_LAUNCHED();
       }
       k_kpp1_final<<<1, 64, 0, s>>>(b1, k - 1);

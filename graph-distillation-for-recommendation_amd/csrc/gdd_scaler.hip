@@ -117,50 +117,59 @@ namespace {
 
 // dim > 1. Each column's sums are sequential fp32 chains over all n rows, so the kernel is bound by
 // the add chain (one dependent v_add_f32 per row) as long as rows arrive fast enough. Workgroup g
-// owns columns [8g, 8g + w): chunks of 1024 rows x 8 columns are staged through two LDS buffers,
-// column-major (the next chunk's loads in flight in registers meanwhile); lane j of wave 0 folds
-// column j reading 16-byte groups of 4 rows, the next 32 rows' reads issued before the current 32
-// dependent adds, so the LDS latency hides behind the chain. In the second pass every thread also
-// writes its staged elements of x - mean. Only blocks with blockIdx % 8 == 0 work: they share one
-// XCD's L2 under the observed round-robin placement, so X's lines come from HBM once for all column
-// groups (speed only, not correctness).
+// owns columns [8g, 8g + w). Roles: waves 1..3 stage chunks of 768 rows x 8 columns into two
+// column-major LDS buffers (the next chunk's loads in flight in registers meanwhile; in the second
+// pass they also write x - mean from those registers); lane j of wave 0 only folds column j, its
+// 16-byte reads issued a 32-row group ahead of the dependent adds. Only blocks with blockIdx % 8 == 0
+// work: they share one XCD's L2 under the observed round-robin placement, so X's lines come from HBM
+// once for all column groups (speed only, not correctness).
 constexpr int kCW = 8;                     // columns per workgroup
-constexpr int kCR = 1024;                  // rows per staged chunk
-constexpr int kCQ = kCR * kCW / 256;       // staged elements per thread per chunk
+constexpr int kCR = 768;                   // rows per staged chunk
+constexpr int kCL = 192;                   // staging threads (waves 1..3)
+constexpr int kCQ = kCR * kCW / kCL;       // staged elements per staging thread per chunk
 constexpr int kCS = kCR + 8;               // column stride in LDS: (8c + r) % 64 banks, 16-B rows
 constexpr int kColXcd = 8;
 
-template <int PASS>
-__device__ __forceinline__ float col_add(float acc, float x, float m) {
-  if (PASS == 0) return acc + x;
-  const float d = x - m;
-  return acc + d * d;
+__device__ __forceinline__ void col_fold32(const float4 (&v)[8], float& acc) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    acc = acc + v[u].x;
+    acc = acc + v[u].y;
+    acc = acc + v[u].z;
+    acc = acc + v[u].w;
+  }
 }
 
-template <int PASS>
-__device__ __forceinline__ float col_fold(const float* __restrict__ col, int rows, float m, float acc) {
+__device__ __forceinline__ void col_load32(const float* __restrict__ p, float4 (&v)[8]) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + 4 * u);
+}
+
+// rows of one staged column, in order (x in the first pass, (x - mean)^2 in the second). Two 32-row
+// register groups alternate: each group's 16-byte reads are issued a whole group of dependent adds
+// ahead of their use (scheduling barriers keep the compiler from sinking them next to their adds;
+// the first group passes through an empty asm so InstCombine cannot fold the loop's phi of loads
+// into a load of a phi of addresses). Look-ahead reads past `rows` land in the next column or the
+// padding and are never folded.
+__device__ __forceinline__ float col_fold(const float* __restrict__ col, int rows, float acc) {
   int r = 0;
-  if (rows >= 32) {
-    float4 cur[8];
+  if (rows >= 64) {
+    float4 A[8], B[8];
+    col_load32(col, A);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) cur[u] = *reinterpret_cast<const float4*>(col + 4 * u);
-    for (; r + 32 <= rows; r += 32) {
-      // the next group's reads (past `rows` they land in the padding and are never folded)
-      float4 nxt[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) nxt[u] = *reinterpret_cast<const float4*>(col + r + 32 + 4 * u);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        acc = col_add<PASS>(acc, cur[u].x, m);
-        acc = col_add<PASS>(acc, cur[u].y, m);
-        acc = col_add<PASS>(acc, cur[u].z, m);
-        acc = col_add<PASS>(acc, cur[u].w, m);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
+    for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(A[u].x), "+v"(A[u].y), "+v"(A[u].z), "+v"(A[u].w));
+    for (; r + 64 <= rows; r += 64) {
+      col_load32(col + r + 32, B);
+      __builtin_amdgcn_sched_barrier(0);
+      col_fold32(A, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      col_load32(col + r + 64, A);
+      __builtin_amdgcn_sched_barrier(0);
+      col_fold32(B, acc);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
-  for (; r < rows; ++r) acc = col_add<PASS>(acc, col[r], m);
+  for (; r < rows; ++r) acc = acc + col[r];
   return acc;
 }
 
@@ -172,63 +181,76 @@ __global__ __launch_bounds__(256) void k_col_stats(int64_t n, int dim, const flo
   __shared__ __attribute__((aligned(16))) float buf[2 * kCW * kCS + 32];
   __shared__ float s_m[kCW];
   const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform role branch
   const int c0 = (int)(blockIdx.x / kColXcd) * kCW, w = min(kCW, dim - c0);
-  float v[kCQ];
-  // unconditional loads at clamped addresses; rows >= n and columns >= w are never folded or written
-  auto fetch = [&](int64_t r0) {
-#pragma unroll
-    for (int q = 0; q < kCQ; ++q) {
-      const int e = tid + 256 * q;
-      const int64_t row = min(r0 + (e >> 3), n - 1);
-      const int c = min(e & (kCW - 1), w - 1);
-      v[q] = X[row * dim + c0 + c];
-    }
-  };
-  auto store = [&](int slot) {
-#pragma unroll
-    for (int q = 0; q < kCQ; ++q) {
-      const int e = tid + 256 * q;
-      buf[slot * kCW * kCS + (e & (kCW - 1)) * kCS + (e >> 3)] = v[q];
-    }
-  };
-  float m = 0.f;
+  const int64_t nchunks = (n + kCR - 1) / kCR;
   for (int pass = 0; pass < 2; ++pass) {
-    float acc = 0.f;
-    fetch(0);
-    store(0);
-    __syncthreads();
-    if (kCR < n) fetch(kCR);
-    int slot = 0;
-    for (int64_t r0 = 0; r0 < n; r0 += kCR) {
-      const int rows = (int)min((int64_t)kCR, n - r0);
-      const float* sb = buf + slot * kCW * kCS;
-      if (tid < w) acc = pass == 0 ? col_fold<0>(sb + tid * kCS, rows, m, acc)
-                                   : col_fold<1>(sb + tid * kCS, rows, m, acc);
-      if (pass == 1) {  // x - mean, written from the staged chunk by every thread
-#pragma unroll
-        for (int q = 0; q < kCQ; ++q) {
-          const int e = tid + 256 * q;
-          const int r = e >> 3, c = e & (kCW - 1);
-          if (c < w && r < rows) X_out[(r0 + r) * dim + c0 + c] = sb[c * kCS + r] - s_m[c];
+    if (wave == 0) {  // ---- the fold wave
+      float acc = 0.f;
+      __syncthreads();  // chunk 0 staged
+      for (int64_t i = 0; i < nchunks; ++i) {
+        const int rows = (int)min((int64_t)kCR, n - i * kCR);
+        if (tid < w) {
+          const float* col = buf + (i & 1) * kCW * kCS + tid * kCS;
+          acc = col_fold(col, rows, acc);
+        }
+        __syncthreads();  // slot i&1 free, chunk i+1 staged
+      }
+      if (tid < w) {
+        const float q = (float)((double)acc / (double)n);
+        if (pass == 0) {
+          mean[c0 + tid] = q;
+          s_m[tid] = q;
+        } else {
+          var[c0 + tid] = q;
         }
       }
-      if (r0 + kCR < n) {
-        store(slot ^ 1);                           // waits for the chunk in flight
-        if (r0 + 2 * kCR < n) fetch(r0 + 2 * kCR);  // and puts the next one in flight
+    } else {  // ---- the staging waves
+      const int lt = tid - 64;
+      const int cc = lt & (kCW - 1);  // kCL is a multiple of kCW: every staged element is column cc
+      const float mc = pass == 1 ? s_m[min(cc, w - 1)] : 0.f;
+      float v[kCQ];
+      // unconditional loads at clamped addresses; rows >= n and columns >= w are never folded or written
+      auto fetch = [&](int64_t i) {
+#pragma unroll
+        for (int q = 0; q < kCQ; ++q) {
+          const int e = lt + kCL * q;
+          const int64_t row = min(i * kCR + (e >> 3), n - 1);
+          const int c = min(e & (kCW - 1), w - 1);
+          v[q] = X[row * dim + c0 + c];
+        }
+      };
+      auto store = [&](int64_t i) {
+        float* sb = buf + (i & 1) * kCW * kCS;
+#pragma unroll
+        for (int q = 0; q < kCQ; ++q) {  // second pass: the squared deviations, ready to add
+          const int e = lt + kCL * q;
+          const float d = v[q] - mc;
+          sb[(e & (kCW - 1)) * kCS + (e >> 3)] = pass == 0 ? v[q] : d * d;
+        }
+        if (pass == 1 && cc < w) {  // x - mean straight from the registers (column cc throughout)
+          const int64_t rows = min((int64_t)kCR, n - i * kCR);
+          float* o = X_out + (i * kCR) * dim + c0 + cc;
+#pragma unroll
+          for (int q = 0; q < kCQ; ++q) {
+            const int r = (lt + kCL * q) >> 3;
+            if (r < rows) o[(int64_t)r * dim] = v[q] - mc;
+          }
+        }
+      };
+      fetch(0);
+      store(0);
+      if (nchunks > 1) fetch(1);
+      __syncthreads();  // chunk 0 staged
+      for (int64_t i = 0; i < nchunks; ++i) {
+        if (i + 1 < nchunks) {
+          store(i + 1);                         // waits for the chunk in flight
+          if (i + 2 < nchunks) fetch(i + 2);    // and puts the next one in flight
+        }
+        __syncthreads();
       }
-      __syncthreads();
-      slot ^= 1;
     }
-    if (tid < w) {
-      if (pass == 0) {
-        m = (float)((double)acc / (double)n);
-        mean[c0 + tid] = m;
-        s_m[tid] = m;
-      } else {
-        var[c0 + tid] = (float)((double)acc / (double)n);
-      }
-    }
-    __syncthreads();
+    __syncthreads();  // the means in s_m before the second pass
   }
 }
 

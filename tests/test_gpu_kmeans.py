@@ -229,6 +229,7 @@ def test_segment_sum_f32_sequential(n, dim, k, weighted):
 
 
 @pytest.mark.parametrize("n,dim", [(1, 3), (1000, 7), (100000, 47), (20000, 64), (333, 5), (777, 300),
+                                   (768, 5), (1536, 8), (831, 9), (63, 2), (64, 3), (65, 17),
                                    (2000, 600), (5, 1), (64, 1), (129, 1), (8192, 1), (30001, 1)])
 def test_center_columns_matches_numpy(n, dim):
     # KMeans.fit's X.mean(axis=0), X - mean and X.var(axis=0) (sklearn _tolerance) bit for bit

@@ -50,6 +50,18 @@ def run(n, dim, k, reps, check=True):
           flush=True)
 
 
+def ab(n=3000, dim=40, k=454):
+    """Same-process A/B of the round variants (devices differ by up to ~10% in clock)."""
+    for var in ("", "GDD_KPP_CHAIN_PLAIN", "GDD_KPP_NO_TABLE", ""):
+        if var:
+            os.environ[var] = "1"
+        print(f"variant {var or 'default'}:", end=" ", flush=True)
+        run(n, dim, k, 5, check=False)
+        if var:
+            del os.environ[var]
+
+
 if __name__ == "__main__":
+    ab()
     for (n, dim, k) in [(3000, 40, 454), (2708, 7, 70), (6040, 64, 604), (3000, 41, 769), (17730, 64, 1773)]:
         run(n, dim, k, 3, check=n * k < 3e7)
