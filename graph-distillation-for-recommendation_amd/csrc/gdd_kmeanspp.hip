@@ -1180,7 +1180,7 @@ __global__ __launch_bounds__(256) void k_kpp1_dist(Kpp1Args a, int c) {
 // whole group of dependent adds ahead of their use (scheduling barriers keep them there; the first
 // group goes through an empty asm so InstCombine cannot turn the loop's phi of loads into a load of
 // a phi of addresses, which would put every read right in front of its adds). Look-ahead reads run
-// at most 63 entries past L, inside the lane's kChainLd-float row.
+// at most 63 entries past L, inside the lane's kChainLd-float row (L <= 1024).
 __device__ __forceinline__ void chain_load32(const float* __restrict__ p, float4 (&v)[8]) {
 #pragma unroll
   for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + 4 * u);
@@ -1212,23 +1212,40 @@ template <bool PIPE = true>
 __device__ __forceinline__ float chain_add(const float* __restrict__ p, int L, float acc) {
   if (!PIPE) return chain_add_plain(p, L, acc);
   int m = 0;
-  if (L >= 64) {
-    float4 A[8], B[8];
-    chain_load32(p, A);
+  float4 A[8];
+  chain_load32(p, A);  // past L: row padding, never added
 #pragma unroll
-    for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(A[u].x), "+v"(A[u].y), "+v"(A[u].z), "+v"(A[u].w));
-    for (; m + 64 <= L; m += 64) {
-      chain_load32(p + m + 32, B);
-      __builtin_amdgcn_sched_barrier(0);
-      chain_add32(A, acc);
-      __builtin_amdgcn_sched_barrier(0);
-      chain_load32(p + m + 64, A);
-      __builtin_amdgcn_sched_barrier(0);
-      chain_add32(B, acc);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+  for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(A[u].x), "+v"(A[u].y), "+v"(A[u].z), "+v"(A[u].w));
+  for (; m + 64 <= L; m += 64) {
+    float4 B[8];
+    chain_load32(p + m + 32, B);
+    __builtin_amdgcn_sched_barrier(0);
+    chain_add32(A, acc);
+    __builtin_amdgcn_sched_barrier(0);
+    chain_load32(p + m + 64, A);
+    __builtin_amdgcn_sched_barrier(0);
+    chain_add32(B, acc);
+    __builtin_amdgcn_sched_barrier(0);
   }
-  for (; m < L; ++m) acc = acc + p[m];
+  // A holds entries m .. m+31 (L - m < 64): the rest without single-entry LDS round trips
+  float4 B[8];
+  chain_load32(p + m + 32, B);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = m + 4 * u;
+    if (e < L) acc = acc + A[u].x;
+    if (e + 1 < L) acc = acc + A[u].y;
+    if (e + 2 < L) acc = acc + A[u].z;
+    if (e + 3 < L) acc = acc + A[u].w;
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = m + 32 + 4 * u;
+    if (e < L) acc = acc + B[u].x;
+    if (e + 1 < L) acc = acc + B[u].y;
+    if (e + 2 < L) acc = acc + B[u].z;
+    if (e + 3 < L) acc = acc + B[u].w;
+  }
   return acc;
 }
 
@@ -1736,6 +1753,7 @@ __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __rest
     a.candself[cq][t] = ct;
     if (c >= 2 && t == 0) a.indices[c - 1] = a.candself[pq][bw];  // rows gathered after the rounds
   }
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 61);
   // trip 2: the closest distances (round c-1's winning row) and the candidate's table row
   const float* wrow = c == 1 ? a.closest0 : a.dist[pq] + (int64_t)bw * n;
   const float* drow = D + ct * n;
@@ -1746,7 +1764,6 @@ __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __rest
     wi[q] = wrow[e];
     dd[q] = drow[e];
   }
-  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 61);
   float* orow = a.dist[cq] + (int64_t)t * n;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {

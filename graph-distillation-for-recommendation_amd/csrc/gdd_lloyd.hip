@@ -268,12 +268,23 @@ __device__ __forceinline__ void fold_col(const float* __restrict__ col, int stri
     }
   };
   ld(A, WA, 0);
+  // opaque first group + scheduling barriers: keeps each group's reads a group of adds ahead (the
+  // compiler otherwise folds the loop's phi of loads and re-issues every read next to its adds)
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    asm volatile("" : "+v"(A[u]));
+    if constexpr (WEIGHTED) asm volatile("" : "+v"(WA[u]));
+  }
   int r0 = 0;
   for (; r0 + 32 <= rp; r0 += 32) {
     ld(B, WB, r0 + 16);
+    __builtin_amdgcn_sched_barrier(0);
     add(A, WA);
+    __builtin_amdgcn_sched_barrier(0);
     if (r0 + 32 < rp) ld(A, WA, r0 + 32);
+    __builtin_amdgcn_sched_barrier(0);
     add(B, WB);
+    __builtin_amdgcn_sched_barrier(0);
   }
   if (r0 < rp) add(A, WA);
 }
@@ -301,14 +312,34 @@ __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
     const int dr = 256 / FWu, df = 256 % FWu;
     const int r_init = tid / FWu, f_init = tid % FWu;
     float xv[Q * U];
-    auto load_ids = [&](int chunk) {
+    // member ids of a chunk: requested into registers early (fetch_ids), written to their LDS slot
+    // later (put_ids), so the perm read overlaps a gather and a fold instead of ending an iteration
+    constexpr int kIdsPer = kFoldMaxR / 256;
+    int32_t idv[kIdsPer];
+    auto fetch_ids = [&](int chunk) {
+      const int m0 = chunk * R;
+      const int rows = min(R, nm - m0);
+#pragma unroll
+      for (int q = 0; q < kIdsPer; ++q) {
+        const int r = tid + 256 * q;
+        if (r < R) idv[q] = a.perm[b + m0 + min(r, rows - 1)];
+      }
+    };
+    auto put_ids = [&](int chunk) {
       const int slot = chunk % 3, m0 = chunk * R;
       const int rows = min(R, nm - m0);
-      for (int r = tid; r < R; r += 256) {
-        const int32_t id = a.perm[b + m0 + min(r, rows - 1)];
-        sid[slot * R + r] = id;
-        if constexpr (WEIGHTED) Wbuf[slot * R + r] = r < rows ? a.w[id] : 0.f;
+#pragma unroll
+      for (int q = 0; q < kIdsPer; ++q) {
+        const int r = tid + 256 * q;
+        if (r < R) {
+          sid[slot * R + r] = idv[q];
+          if constexpr (WEIGHTED) Wbuf[slot * R + r] = r < rows ? a.w[idv[q]] : 0.f;
+        }
       }
+    };
+    auto load_ids = [&](int chunk) {
+      fetch_ids(chunk);
+      put_ids(chunk);
     };
     auto gather = [&](int chunk) {
       const int32_t* ids = sid + (chunk % 3) * R;
@@ -366,6 +397,7 @@ __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
     __syncthreads();
     for (int i = 0; i < nch; ++i) {
       const int rows = min(R, nm - i * R);
+      if (i + 2 < nch) fetch_ids(i + 2);  // in flight through this iteration's gather and fold
       if (i + 1 < nch) gather(i + 1);  // ids of chunk i+1 were staged before the last barrier
       if (tid < FW) {
         const float* col = Bbuf + (i & 1) * kFoldElems + tid;
@@ -377,7 +409,7 @@ __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
       }
       if (i + 1 < nch) {
         store(i + 1);                       // buffer (i+1)&1 was last read in iteration i-1
-        if (i + 2 < nch) load_ids(i + 2);   // slot (i+2)%3 was last read in iteration i-1
+        if (i + 2 < nch) put_ids(i + 2);    // slot (i+2)%3 was last read in iteration i-1
       }
       __syncthreads();
     }
