@@ -441,7 +441,8 @@ class KMeans(_BaseKMeans):
         done, reason = ctypes.c_int32(0), ctypes.c_int32(0)
 
         best = None
-        for _ in range(self._n_init(10)):
+        n_inits = self._n_init(10)
+        for _ in range(n_inits):
             C0, _ = ops.kmeans_plusplus(Xd, k, rs)
             Cb = (C0, torch.empty_like(C0))
             labels_old.fill_(-1)
@@ -465,6 +466,20 @@ class KMeans(_BaseKMeans):
                 ops.assign(Xd, C, labels=labels)
             _lib.check(lib.gdd_point_center_sqdist(n, dim, Xd.data_ptr(), labels.data_ptr(),
                                                    C.data_ptr(), sq.data_ptr(), stream))
+            if n_inits == 1:
+                # one init: nothing to compare, so the fit returns without waiting on the device.
+                # The inertia (a sequential fp32 fold over n, bound by its add chain) runs on a side
+                # stream and is read on first access of inertia_; labels and centres stay on the
+                # device until their host attributes are read. cluster_centers_ = C + X_mean is the
+                # same fp32 add numpy makes.
+                self._inertia_async = _side_inertia(sq)
+                self._inertia_value = None
+                self.labels_device_ = labels
+                self._labels_np = None
+                self.cluster_centers_device_ = C + mean_d
+                self._centers_np = None
+                self.n_iter_ = n_iter
+                return self
             inertia = float(ops.inertia(sq).item())
             lab_h = labels.cpu().numpy()
             if best is None or (inertia < best[1] and not _same_clustering(lab_h, best[0], k)):
