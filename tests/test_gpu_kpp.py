@@ -103,16 +103,19 @@ def test_kmeans_plusplus_two_launch_path(monkeypatch):
     assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref))
 
 
-@pytest.mark.parametrize("n,dim,k", [(3000, 40, 454), (2708, 7, 70), (4096, 48, 40)])
-def test_kmeans_plusplus_fused_vs_table(monkeypatch, n, dim, k):
-    """The distance-table rounds (default for plain-chain plans with dim <= 48, k >= 16) and the
-    fused distance + fold rounds (GDD_KPP_NO_TABLE) give the oracle's seeding, bit for bit."""
+@pytest.mark.parametrize("n,dim,k", [(3000, 40, 454), (2708, 7, 70), (4096, 48, 40), (1999, 20, 100),
+                                     (4095, 3, 1000), (37, 5, 16)])
+def test_kmeans_plusplus_round_forms(monkeypatch, n, dim, k):
+    """Every single-block round form gives the oracle's seeding, bit for bit: one launch per round
+    over the distance table (default for plain-chain plans, dim <= 48, k >= 16), the one-workgroup
+    persistent rounds over the table (GDD_KPP_PERSIST, T <= 8), and the fused distance + fold rounds
+    (GDD_KPP_NO_TABLE)."""
     X = np.ascontiguousarray(synth.blobs(n, dim, max(2, k // 4), seed=n + dim + 1), np.float32)
     c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
-    for no_table in (False, True):
-        if no_table:
-            monkeypatch.setenv("GDD_KPP_NO_TABLE", "1")
+    for var in (None, "GDD_KPP_PERSIST", "GDD_KPP_NO_TABLE"):
+        if var:
+            monkeypatch.setenv(var, "1")
         ops = _Ops("cuda", n, k, dim)
         c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(15))
-        assert np.array_equal(idx.cpu().numpy(), idx_ref), no_table
-        assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref)), no_table
+        assert np.array_equal(idx.cpu().numpy(), idx_ref), var
+        assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref)), var
