@@ -54,6 +54,23 @@ __device__ __forceinline__ float npy_sumsq(const float* __restrict__ x, int dim)
   return (a[0] + a[1]) + (a[2] + a[3]);
 }
 
+// accumulator l of npy_sumsq (the same per-lane arithmetic): four lanes form the norm together
+__device__ __forceinline__ float npy_sumsq_acc(const float* __restrict__ x, int dim, int l) {
+  float a = 0.f;
+  int j = 0;
+  for (; dim - j >= 16; j += 16) {
+    float t = x[j + 12 + l] * x[j + 12 + l] + a;
+    t = x[j + 8 + l] * x[j + 8 + l] + t;
+    t = x[j + 4 + l] * x[j + 4 + l] + t;
+    a = x[j + l] * x[j + l] + t;
+  }
+  for (; j < dim; j += 4) {
+    const float v = (j + l < dim) ? x[j + l] : 0.f;
+    a = v * v + a;
+  }
+  return a;
+}
+
 __global__ void k_row_norms(int64_t n, int dim, const float* __restrict__ X, float* __restrict__ out,
                             const int32_t* __restrict__ stop, int step_i) {
   if (stopped(stop, step_i)) return;
@@ -1183,9 +1200,11 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
     }
   }
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 24);
-  if (cn2_out) {  // the new row is also staged in LDS: lane 0 forms its norm without HBM reads
+  if (cn2_out) {  // the new row is also staged in LDS: npy_sumsq's four accumulators on four lanes
     __syncthreads();
-    if (lane == 0) cn2_out[c] = npy_sumsq(row_out, dim);
+    const float acc = lane < 4 ? npy_sumsq_acc(row_out, dim, lane) : 0.f;
+    const float a0 = __shfl(acc, 0), a1 = __shfl(acc, 1), a2 = __shfl(acc, 2), a3 = __shfl(acc, 3);
+    if (lane == 0) cn2_out[c] = (a0 + a1) + (a2 + a3);
   }
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 25);
 }
