@@ -123,21 +123,25 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n
   rc = mb_loop_begin(bs, k, w.step_ws, w.step_bytes, s);
   if (rc) return rc;
   const bool reassign = reassignment_ratio > 0.f;
-  hipEvent_t ev[2];
-  GDD_HIP(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
-  GDD_HIP(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+  // chunks in flight before the host waits for the oldest one's stop word (GDD_MB_LOOKAHEAD, 1..3):
+  // more absorb host-side hiccups; each extra chunk can add one chunk of no-op launches after a stop
+  static const int lookahead = [] {
+    const char* e = getenv("GDD_MB_LOOKAHEAD");
+    const int v = e ? atoi(e) : 1;
+    return v < 1 ? 1 : (v > 3 ? 3 : v);
+  }();
+  hipEvent_t ev[4];
+  for (int q = 0; q < 4; ++q) GDD_HIP(hipEventCreateWithFlags(&ev[q], hipEventDisableTiming));
   struct EvGuard {
     hipEvent_t* e;
     ~EvGuard() {
-      (void)hipEventDestroy(e[0]);
-      (void)hipEventDestroy(e[1]);
+      for (int q = 0; q < 4; ++q) (void)hipEventDestroy(e[q]);
     }
   } guard{ev};
   int32_t* stop_word = reinterpret_cast<int32_t*>(static_cast<char*>(w.state) + 16);
   int64_t n_since = 0;
   int64_t i = 0;
-  int slot = 0;
-  bool pending = false;
+  int64_t chunk = 0;
   *stop_step = -1;
   while (i < n_steps) {
     const int64_t m = std::min<int64_t>(kDevChunk, n_steps - i);
@@ -173,19 +177,20 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n
       }
     }
     i += m;
-    // this chunk's stop word, read back while the next chunk runs
+    // this chunk's stop word, read back while the next chunks run
+    const int slot = (int)(chunk & 3);
     GDD_HIP(hipMemcpyAsync(h_flag + slot, stop_word, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     GDD_HIP(hipEventRecord(ev[slot], s));
-    if (pending) {
-      GDD_HIP(hipEventSynchronize(ev[slot ^ 1]));
-      if (h_flag[slot ^ 1]) break;  // the later kernels already enqueued are no-ops
+    if (chunk >= lookahead) {
+      const int old = (int)((chunk - lookahead) & 3);
+      GDD_HIP(hipEventSynchronize(ev[old]));
+      if (h_flag[old]) break;  // the later kernels already enqueued are no-ops
     }
-    pending = true;
-    slot ^= 1;
+    ++chunk;
   }
-  GDD_HIP(hipMemcpyAsync(h_flag + 2, stop_word, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  GDD_HIP(hipMemcpyAsync(h_flag + 4, stop_word, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   GDD_HIP(hipStreamSynchronize(s));
-  if (h_flag[2]) *stop_step = h_flag[2] - 1;
+  if (h_flag[4]) *stop_step = h_flag[4] - 1;
   const int64_t last = *stop_step >= 0 ? *stop_step : n_steps - 1;
   // the caller's RandomState ends where sklearn's does: after the draws of the last step
   GDD_HIP(hipMemcpyAsync(h_mt, w.mtb + last % 3, sizeof(DevMT), hipMemcpyDeviceToHost, s));
