@@ -1058,6 +1058,11 @@ struct Kpp1Args {
   float* centers;
   int64_t* indices;
   SklPlan plan;
+  // two rounds per launch (k_kpp1_dm2): round c+1's trial t given round c's winner w, at w * T + t
+  float* dist2[2];       // [T*T][n]
+  float* potv2[2];       // [T*T]
+  int64_t* candw2[2];    // [T*T][T]
+  int64_t* candself2[2];  // [T*T]
 };
 
 __device__ __forceinline__ int kpp1_argmin(const float* __restrict__ pot, int T) {
@@ -1437,13 +1442,15 @@ constexpr int kFPW = 22;     // prefix entries per thread of waves 1..3 in the f
 // the fold of round c's trial t by one 256-thread workgroup holding the trial's row in registers
 // (r[q] = entry tid + 256 q): the exact sgemv_t potential, the fp64 cumulative potential and the
 // candidates every trial would draw in round c+1 if t wins
+// pot_out (nullable) receives the potential, cand_out[0..T) the candidates (global memory or LDS)
 template <bool PIPE = true>
 __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t, const float (&r)[16],
                                                 double ut, float* __restrict__ s_d,
                                                 float* __restrict__ s_ch, double* __restrict__ s_cum,
-                                                double* __restrict__ s_wave, float* __restrict__ s_pot_p) {
+                                                double* __restrict__ s_wave, float* __restrict__ s_pot_p,
+                                                float* pot_out, int64_t* cand_out) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int cq = c & 1, T = a.T;
+  const int T = a.T;
   const int n = (int)a.n;
   float& s_pot = *s_pot_p;
   const int m1 = (int)a.m1;
@@ -1500,7 +1507,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
     }
     if (lane == 0) {
       s_pot = y;
-      a.potv[cq][t] = y;
+      if (pot_out) *pot_out = y;
     }
   } else {  // the cumulative potential: thread runs and the wave's inclusive scan
     double run = 0.0;
@@ -1544,7 +1551,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
         const int mid = (lo + hi) >> 1;
         if (s_cum[mid] < rr) lo = mid + 1; else hi = mid;
       }
-      a.candw[cq][(int64_t)t * T + tid] = min(n - 1, lo);
+      cand_out[tid] = min(n - 1, lo);
     }
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 74);
@@ -1664,7 +1671,8 @@ __global__ __launch_bounds__(256) void k_kpp1_fused(Kpp1Args a, int c) {
     for (int q = 0; q < 16; ++q)
       r[q] = __hip_atomic_load(row + min(tid + 256 * q, n - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  kpp1_fold_trial(a, c, t, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot);
+  kpp1_fold_trial(a, c, t, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv[cq] + t,
+                  a.candw[cq] + (int64_t)t * T);
 }
 
 // ---- single-block rounds from a distance table (plain-chain plans, dim <= 48, n <= 4096). The
@@ -1771,7 +1779,130 @@ __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __rest
     if (tid + 256 * q < n) orow[tid + 256 * q] = r[q];
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 62);
-  kpp1_fold_trial<PIPE>(a, c, t, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot);
+  kpp1_fold_trial<PIPE>(a, c, t, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv[cq] + t,
+                        a.candw[cq] + (int64_t)t * T);
+}
+
+// ---- two rounds per launch over the distance table (default for table plans, T <= 8). Workgroup
+// w * T + t runs round c+1's trial t on the assumption that round c's trial w wins: it forms trial w's
+// row and folds it (same operands, same slot, so bit-identical to what a round-c workgroup w would
+// compute), takes w's round-(c+1) candidate for slot t, reads that candidate's table row (a third
+// dependent trip) and folds round c+1's trial t. Workgroup w * T also publishes round c's trial w
+// (potential, candidate). The next launch resolves both winners from the potentials: T + T * T
+// floats and its column of the T * T x T candidate table in its first trip, one wave lane per entry.
+// A trailing odd round runs alone (pair == 0: T workgroups, round c only). State slots alternate by
+// launch (lq); round 1 reads the first centre's slot-0 candidates, so the first launch writes slot 1.
+// Per round this halves the launches and their two leading trips (k_kpp1_dm: 9.2 us per round).
+constexpr int kPairMaxT = 8;  // T * T <= 64: one wave lane per round-(c-1) candidate
+
+template <bool PIPE>
+__global__ __launch_bounds__(256) void k_kpp1_dm2(Kpp1Args a, const float* __restrict__ D, int c, int lq,
+                                                  int pair) {
+  __shared__ float s_d[kBlk];
+  __shared__ float s_ch[8 * kChainLd];
+  __shared__ double s_cum[kBlk];
+  __shared__ double s_wave[4];
+  __shared__ float s_pot;
+  __shared__ int64_t s_cand[kMaxTrials];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int T = a.T, pl = lq ^ 1, TT = T * T;
+  const int n = (int)a.n;
+  const int g = blockIdx.x;
+  const int w = pair ? g / T : g;        // round c's trial this workgroup forms first
+  const int t2 = pair ? g - w * T : 0;   // round c+1's trial (pair launches)
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && g == 0 && c == a.k - 3 + (a.k & 1)), 60);
+  // trip 1: the previous launch's potentials and this slot's candidates
+  const float* wrow;
+  int64_t ct;
+  if (c == 1) {
+    wrow = a.closest0;
+    ct = a.candw[0][w];  // k_kpp1_pick(.., 0): the first centre's candidates
+  } else {
+    float pv[kPairMaxT];
+#pragma unroll
+    for (int q = 0; q < kPairMaxT; ++q) pv[q] = a.potv[pl][min(q, T - 1)];
+    const float p2 = a.potv2[pl][min(lane, TT - 1)];
+    const int64_t c2 = a.candw2[pl][(int64_t)min(lane, TT - 1) * T + w];
+    int bw = 0;  // np.argmin: first minimum, a NaN wins at once
+    float best = pv[0];
+#pragma unroll
+    for (int q = 1; q < kPairMaxT; ++q) {
+      const float pt = pv[q];
+      if (q < T && best == best && (pt < best || pt != pt)) {
+        bw = q;
+        best = pt;
+      }
+    }
+    int bv = 0;
+    float best2 = __shfl(p2, bw * T);
+    for (int q = 1; q < T; ++q) {
+      const float pt = __shfl(p2, bw * T + q);
+      if (best2 == best2 && (pt < best2 || pt != pt)) {
+        bv = q;
+        best2 = pt;
+      }
+    }
+    const int j = bw * T + bv;
+    ct = __shfl(c2, j);
+    wrow = a.dist2[pl] + (int64_t)j * n;
+    if (g == 0 && tid == 0) {  // rows gathered after the rounds
+      a.indices[c - 2] = a.candself[pl][bw];
+      a.indices[c - 1] = a.candself2[pl][j];
+    }
+  }
+  const double ut = (c + 1 < a.k && tid < T) ? a.uniforms[(int64_t)c * T + tid] : 0.0;
+  const double ut2 = (pair && c + 2 < a.k && tid < T) ? a.uniforms[(int64_t)(c + 1) * T + tid] : 0.0;
+  if (tid == 0 && (!pair || t2 == 0)) a.candself[lq][w] = ct;
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && g == 0 && c == a.k - 3 + (a.k & 1)), 61);
+  // trip 2: the closest distances and the candidate's table row
+  const float* drow = D + ct * n;
+  float wi[16], dd[16], r[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = min(tid + 256 * q, n - 1);
+    wi[q] = wrow[e];
+    dd[q] = drow[e];
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) r[q] = np_minimum(wi[q], dd[q]);
+  if (!pair) {  // the last round alone: as k_kpp1_dm
+    kpp1_fold_trial<PIPE>(a, c, w, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv[lq] + w,
+                          a.candw[lq] + (int64_t)w * T);
+    return;
+  }
+  kpp1_fold_trial<PIPE>(a, c, w, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot,
+                        t2 == 0 ? a.potv[lq] + w : nullptr, s_cand);
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && g == 0 && c == a.k - 3 + (a.k & 1)), 62);
+  // trip 3: round c+1's candidate for slot t2 if w wins, and its table row
+  const int64_t c1 = s_cand[t2];
+  const int j = w * T + t2;
+  if (tid == 0) a.candself2[lq][j] = c1;
+  const float* drow2 = D + c1 * n;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) dd[q] = drow2[min(tid + 256 * q, n - 1)];
+  float* orow = a.dist2[lq] + (int64_t)j * n;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    wi[q] = np_minimum(r[q], dd[q]);
+    if (tid + 256 * q < n) orow[tid + 256 * q] = wi[q];
+  }
+  kpp1_fold_trial<PIPE>(a, c + 1, t2, wi, ut2, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv2[lq] + j,
+                        a.candw2[lq] + (int64_t)j * T);
+}
+
+// after the last launch of k_kpp1_dm2: its winner(s) and the last centre
+__global__ __launch_bounds__(64) void k_kpp1_final2(Kpp1Args a, int c, int lq, int pair) {
+  const int T = a.T;
+  const int b = kpp1_argmin(a.potv[lq], T);
+  int64_t src = a.candself[lq][b];
+  if (pair) {
+    const int v = kpp1_argmin(a.potv2[lq] + (int64_t)b * T, T);
+    if (threadIdx.x == 0) a.indices[c - 1] = src;
+    src = a.candself2[lq][(int64_t)b * T + v];
+  }
+  if (threadIdx.x == 0) a.indices[c] = src;
+  for (int j = threadIdx.x; j < a.dim; j += 64) a.centers[(int64_t)c * a.dim + j] = a.X[src * a.dim + j];
 }
 
 // ---- every single-block round in ONE workgroup (table plans, T <= 8, unit weights, n <= 4096) -----
@@ -2152,7 +2283,11 @@ size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k) {
   b += align256(sizeof(int) * 2) + align256(sizeof(unsigned) * (size_t)std::max(k, 1) * T);  // counters
   if (n <= kBlk || (int64_t)n * std::max(dim, 1) < INT_MAX)
     b += align256(sizeof(float) * n * (size_t)std::max(dim, 1));  // XT
-  if (n <= kBlk && dim <= kDmX && T >= 2) b += align256(sizeof(float) * n * n);  // distance table
+  if (n <= kBlk && dim <= kDmX && T >= 2) {
+    b += align256(sizeof(float) * n * n);  // distance table
+    b += 2 * (align256(sizeof(float) * T * T * n) + align256(sizeof(float) * T * T) +
+              align256(sizeof(int64_t) * T * T * T) + align256(sizeof(int64_t) * T * T));  // pair rounds
+  }
   return b + 1024;
 }
 
@@ -2193,6 +2328,14 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   b1.counter = cv.take<unsigned>((size_t)std::min<int64_t>(n, INT_MAX) * T);
   float* XT = (n <= kBlk || n * (int64_t)dim < INT_MAX) ? cv.take<float>((size_t)n * dim) : nullptr;
   float* Dm = (n <= kBlk && dim <= kDmX && T >= 2) ? cv.take<float>((size_t)n * n) : nullptr;
+  if (Dm) {
+    for (int q = 0; q < 2; ++q) {
+      b1.dist2[q] = cv.take<float>((size_t)T * T * n);
+      b1.potv2[q] = cv.take<float>((size_t)T * T);
+      b1.candw2[q] = cv.take<int64_t>((size_t)T * T * T);
+      b1.candself2[q] = cv.take<int64_t>((size_t)T * T);
+    }
+  }
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans++: workspace too small");
   a.n = n;
   a.m1 = n & ~3ll;
@@ -2279,6 +2422,28 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
         return GDD_OK;
       }
       const bool plain = getenv("GDD_KPP_CHAIN_PLAIN") != nullptr;
+      if (T <= kPairMaxT && getenv("GDD_KPP_SINGLE_ROUND") == nullptr) {
+        // two rounds per launch (a trailing odd round alone)
+        int lq = 1, pair = 0;
+        for (int c = 1; c < k; c += 2) {
+          lq = ((c - 1) / 2 + 1) & 1;
+          pair = c + 1 < k ? 1 : 0;
+          const unsigned grid = (unsigned)(pair ? T * T : T);
+          if (plain)
+            k_kpp1_dm2<false><<<grid, 256, 0, s>>>(b1, Dm, c, lq, pair);
+          else
+            k_kpp1_dm2<true><<<grid, 256, 0, s>>>(b1, Dm, c, lq, pair);
+          GDD_LAUNCHED();
+        }
+        k_kpp1_final2<<<1, 64, 0, s>>>(b1, k - 1, lq, pair);
+        GDD_LAUNCHED();
+        if (k > 2) {
+          k_kpp_gather_centres<<<(unsigned)(((int64_t)k * dim + 255) / 256), 256, 0, s>>>(k, dim, X, indices,
+                                                                                           centers);
+          GDD_LAUNCHED();
+        }
+        return GDD_OK;
+      }
       for (int c = 1; c < k; ++c) {
         if (plain)
           k_kpp1_dm<false><<<(unsigned)T, 256, 0, s>>>(b1, Dm, c);

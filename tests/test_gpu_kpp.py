@@ -104,15 +104,18 @@ def test_kmeans_plusplus_two_launch_path(monkeypatch):
 
 
 @pytest.mark.parametrize("n,dim,k", [(3000, 40, 454), (2708, 7, 70), (4096, 48, 40), (1999, 20, 100),
-                                     (4095, 3, 1000), (37, 5, 16)])
+                                     (4095, 3, 1000), (37, 5, 16),
+                                     # an even number of rounds: the last launch is a pair
+                                     (3000, 40, 455), (2708, 7, 71), (1999, 20, 17), (37, 5, 17),
+                                     (4095, 3, 1097)])  # T = 9: one round per launch
 def test_kmeans_plusplus_round_forms(monkeypatch, n, dim, k):
-    """Every single-block round form gives the oracle's seeding, bit for bit: one launch per round
-    over the distance table (default for plain-chain plans, dim <= 48, k >= 16), the one-workgroup
-    persistent rounds over the table (GDD_KPP_PERSIST, T <= 8), and the fused distance + fold rounds
-    (GDD_KPP_NO_TABLE)."""
+    """Every single-block round form gives the oracle's seeding, bit for bit: two rounds per launch
+    over the distance table (default for plain-chain plans, dim <= 48, k >= 16, T <= 8), one round
+    per launch over the table (GDD_KPP_SINGLE_ROUND), the one-workgroup persistent rounds over the
+    table (GDD_KPP_PERSIST, T <= 8), and the fused distance + fold rounds (GDD_KPP_NO_TABLE)."""
     X = np.ascontiguousarray(synth.blobs(n, dim, max(2, k // 4), seed=n + dim + 1), np.float32)
     c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
-    for var in (None, "GDD_KPP_PERSIST", "GDD_KPP_NO_TABLE"):
+    for var in (None, "GDD_KPP_SINGLE_ROUND", "GDD_KPP_PERSIST", "GDD_KPP_NO_TABLE"):
         if var:
             monkeypatch.setenv(var, "1")
         ops = _Ops("cuda", n, k, dim)

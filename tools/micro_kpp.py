@@ -52,7 +52,7 @@ def run(n, dim, k, reps, check=True):
 
 def ab(n=3000, dim=40, k=454):
     """Same-process A/B of the round variants (devices differ by up to ~10% in clock)."""
-    for var in ("", "GDD_KPP_PERSIST", "GDD_KPP_NO_TABLE", ""):
+    for var in ("", "GDD_KPP_SINGLE_ROUND", "GDD_KPP_PERSIST", "GDD_KPP_NO_TABLE", ""):
         if var:
             os.environ[var] = "1"
         print(f"variant {var or 'default'}:", end=" ", flush=True)
