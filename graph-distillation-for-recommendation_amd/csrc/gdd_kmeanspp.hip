@@ -1811,6 +1811,7 @@ __global__ __launch_bounds__(256) void k_kpp1_dm2(Kpp1Args a, const float* __res
   const int w = pair ? g / T : g;        // round c's trial this workgroup forms first
   const int t2 = pair ? g - w * T : 0;   // round c+1's trial (pair launches)
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && g == 0 && c == a.k - 3 + (a.k & 1)), 60);
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && g == 0 && c == a.k - 1 + (a.k & 1)), 65);
   // trip 1: the previous launch's potentials and this slot's candidates
   const float* wrow;
   int64_t ct;

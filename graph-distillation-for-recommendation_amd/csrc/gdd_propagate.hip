@@ -230,22 +230,36 @@ __global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
   }
 }
 
-// fold the partials of split rows left to right, then the same epilogue
+// fold the partials of split rows left to right, then the same epilogue. A bounded grid walks the
+// split rows (their count is only known on the device; launching one block per possible split row,
+// nnz/256 + 1, dispatched ~10k mostly idle blocks at the arxiv shape for 430 split rows); partials
+// are requested eight at a time ahead of the ordered adds.
+constexpr int kFixupBlocks = 1024;
 __global__ void k_fixup(const int32_t* __restrict__ counts, const int32_t* __restrict__ long_rows,
                         const int32_t* __restrict__ long_off, const int32_t* __restrict__ rowptr,
                         int d, const float* __restrict__ partials, float* __restrict__ y,
                         float* __restrict__ acc_out, float acc_scale) {
-  const int r = blockIdx.x;
-  if (r >= counts[1]) return;
-  const int32_t row = long_rows[r], po = long_off[r];
-  const int32_t len = rowptr[row + 1] - rowptr[row];
-  const int32_t s = (len + kSeg - 1) / kSeg;
-  for (int f = threadIdx.x; f < d; f += blockDim.x) {
-    float sum = partials[(int64_t)po * d + f];
-    for (int32_t k = 1; k < s; ++k) sum = sum + partials[(int64_t)(po + k) * d + f];
-    const int64_t o = (int64_t)row * d + f;
-    y[o] = sum;
-    if (acc_out) acc_out[o] = acc_out[o] + acc_scale * sum;
+  const int nl = counts[1];
+  for (int r = blockIdx.x; r < nl; r += gridDim.x) {
+    const int32_t row = long_rows[r], po = long_off[r];
+    const int32_t len = rowptr[row + 1] - rowptr[row];
+    const int32_t s = (len + kSeg - 1) / kSeg;
+    for (int f = threadIdx.x; f < d; f += blockDim.x) {
+      const float* pp = partials + (int64_t)po * d + f;
+      float sum = pp[0];
+      int32_t k = 1;
+      for (; k + 8 <= s; k += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = pp[(int64_t)(k + u) * d];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sum = sum + v[u];
+      }
+      for (; k < s; ++k) sum = sum + pp[(int64_t)k * d];
+      const int64_t o = (int64_t)row * d + f;
+      y[o] = sum;
+      if (acc_out) acc_out[o] = acc_out[o] + acc_scale * sum;
+    }
   }
 }
 
@@ -422,8 +436,9 @@ int run_hop(const Plan& pl, const int32_t* rowptr, const int32_t* col, const flo
   else
     launch_hop_v<1>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
   GDD_LAUNCHED();
-  k_fixup<<<(unsigned)pl.max_long, 256, 0, s>>>(pl.counts, pl.long_rows, pl.long_off, rowptr, d,
-                                                pl.partials, y, acc, acc_scale);
+  const unsigned fixup_grid = (unsigned)std::min<int64_t>(pl.max_long, kFixupBlocks);
+  k_fixup<<<fixup_grid, 256, 0, s>>>(pl.counts, pl.long_rows, pl.long_off, rowptr, d, pl.partials, y,
+                                     acc, acc_scale);
   GDD_LAUNCHED();
   return GDD_OK;
 }

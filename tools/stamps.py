@@ -51,9 +51,9 @@ def main():
         show("mb_reassign", a, list(range(40, 47)), 40)
         show(f"reassign m={a[57]}", a, list(range(50, 57)), 50)
         t0 = p[60]
-        lab = {60: "start", 61: "rows loaded", 62: "rows staged", 63: "row in LDS",
+        lab = {60: "start", 61: "winners resolved", 62: "level-1 fold done", 63: "level-2 row in LDS",
                70: "chains+prefix", 74: "search+table", 65: "next start"}
-        print("kpp table round k-2 (us): " + ", ".join(
+        print("kpp pair launch (rounds k-3, k-2) (us): " + ", ".join(
             f"{lab[q]} {(p[q] - t0) / 100:.2f}" for q in [60, 61, 62, 63, 70, 74, 65]))
 
 
