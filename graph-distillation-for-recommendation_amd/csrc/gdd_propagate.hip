@@ -163,6 +163,7 @@ __global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
                                              const float* __restrict__ val, float scale, int d,
                                              const float* __restrict__ x, float* __restrict__ y,
                                              float* __restrict__ acc_out, float acc_scale,
+                                             const float* __restrict__ acc_init,
                                              float* __restrict__ partials) {
   const int lane = threadIdx.x & (G - 1);
   int64_t ib;  // item block
@@ -220,7 +221,13 @@ __global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
     vstore<V>(y + o, acc);  // gathered by the next hop: default policy
     if (acc_out) {
       float t[V];
-      vload_nt<V>(acc_out + o, t);
+      if (acc_init) {  // first hop: the initial target fp32(1-alpha) * X (agent :59), one rounding
+        vload_nt<V>(acc_init + o, t);
+#pragma unroll
+        for (int v = 0; v < V; ++v) t[v] = acc_scale * t[v];
+      } else {
+        vload_nt<V>(acc_out + o, t);
+      }
 #pragma unroll
       for (int v = 0; v < V; ++v) t[v] = t[v] + acc_scale * acc[v];  // two roundings (agent :65)
       vstore_nt<V>(acc_out + o, t);
@@ -238,7 +245,8 @@ constexpr int kFixupBlocks = 1024;
 __global__ void k_fixup(const int32_t* __restrict__ counts, const int32_t* __restrict__ long_rows,
                         const int32_t* __restrict__ long_off, const int32_t* __restrict__ rowptr,
                         int d, const float* __restrict__ partials, float* __restrict__ y,
-                        float* __restrict__ acc_out, float acc_scale) {
+                        float* __restrict__ acc_out, float acc_scale,
+                        const float* __restrict__ acc_init) {
   const int nl = counts[1];
   for (int r = blockIdx.x; r < nl; r += gridDim.x) {
     const int32_t row = long_rows[r], po = long_off[r];
@@ -258,7 +266,7 @@ __global__ void k_fixup(const int32_t* __restrict__ counts, const int32_t* __res
       for (; k < s; ++k) sum = sum + pp[(int64_t)k * d];
       const int64_t o = (int64_t)row * d + f;
       y[o] = sum;
-      if (acc_out) acc_out[o] = acc_out[o] + acc_scale * sum;
+      if (acc_out) acc_out[o] = (acc_init ? acc_scale * acc_init[o] : acc_out[o]) + acc_scale * sum;
     }
   }
 }
@@ -302,10 +310,17 @@ int hop_sched() {
 inline int64_t max_items_for(int64_t n, int64_t nnz) { return n + nnz / kSeg + 1; }
 inline int64_t max_parts_for(int64_t nnz) { return 2 * (nnz / kSeg) + 2; }
 
+// the schedule's stable counting sort over the length keys (gdd_group_by_label: per-wave LDS
+// histograms, one scan, ranked placement; ~2.5x faster here than a radix sort of the pairs)
+constexpr int kLenKeys = kLenKeyMax + 1;
+size_t sched_ws_bytes(int64_t n) {
+  return align256(sizeof(int32_t) * (kLenKeys + 1)) + align256(gdd_group_ws_bytes(n, kLenKeys));
+}
+
 size_t plan_ws_bytes(int64_t n, int64_t nnz, int d) {
   size_t b = 0;
   b += align256(sizeof(int32_t) * n) * 7;  // nseg, npart, item_off, part_off, sort keys/rows x3
-  b += sort_pairs_ws_bytes(n);
+  b += sched_ws_bytes(n);
   b += align256(sizeof(Item) * max_items_for(n, nnz));   // items
   b += align256(sizeof(int32_t) * 4);                    // counts
   b += align256(sizeof(int32_t) * (nnz / kSeg + 1)) * 2; // long rows
@@ -327,7 +342,7 @@ int carve_plan(int64_t n, int64_t nnz, int d, Carver& cv, Plan& pl, int32_t** tm
   pl.partials = cv.take<float>(max_parts_for(nnz) * (size_t)d);
   *scan_bytes = scan_i32_ws_bytes(n);
   *scan_ws = cv.take<char>(*scan_bytes);
-  pl.sort_bytes = sort_pairs_ws_bytes(n);
+  pl.sort_bytes = sched_ws_bytes(n);
   pl.sort_ws = cv.take<char>(pl.sort_bytes);
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "propagate: workspace too small");
   return GDD_OK;
@@ -347,8 +362,14 @@ int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv,
   if (hop_sched() == 1) {
     k_len_keys<<<gb, 256, 0, s>>>(n, rowptr, tmp[4], tmp[5]);
     GDD_LAUNCHED();
-    int rc = sort_pairs_i32(tmp[4], nseg, tmp[5], tmp[6], n, kLenKeyBits, pl.sort_ws,
-                            pl.sort_bytes, s);
+    // rows grouped by key, stable: the same order as a stable sort of (key, row) pairs
+    Carver sc(pl.sort_ws, pl.sort_bytes);
+    int32_t* key_off = sc.take<int32_t>(kLenKeys + 1);
+    const size_t gws = gdd_group_ws_bytes(n, kLenKeys);
+    void* gw = sc.take<char>(gws);
+    if (!sc.ok()) return fail(GDD_E_WORKSPACE, "propagate: schedule workspace too small");
+    int rc = gdd_group_by_label(n, tmp[4], kLenKeys, tmp[6], key_off, gw, gws,
+                                reinterpret_cast<gdd_stream_t>(s));
     if (rc) return rc;
     order = tmp[6];
   }
@@ -366,7 +387,7 @@ int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv,
 
 template <int V, int G>
 void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float scale, int d,
-                   const float* x, float* y, float* acc, float acc_scale, hipStream_t s) {
+                   const float* x, float* y, float* acc, float acc_scale, const float* acc_init, hipStream_t s) {
   constexpr int kGroups = 256 / G;
   const int64_t iblocks = (pl.max_items + kGroups - 1) / kGroups;
   const int chunks = (d + G * V - 1) / (G * V);
@@ -374,7 +395,7 @@ void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float s
     constexpr int S = decltype(S_)::value;
     const int64_t groups = (iblocks + (8 / S) - 1) / (8 / S);
     k_hop<V, G, S><<<(unsigned)(groups * 8), 256, 0, s>>>(pl.items, pl.counts, col, val, scale, d,
-                                                          x, y, acc, acc_scale, pl.partials);
+                                                          x, y, acc, acc_scale, acc_init, pl.partials);
   };
   if (chunks == 8)
     xcd_launch(std::integral_constant<int, 8>());
@@ -386,7 +407,7 @@ void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float s
     xcd_launch(std::integral_constant<int, 1>());
   else
     k_hop<V, G, 0><<<dim3((unsigned)iblocks, (unsigned)chunks), 256, 0, s>>>(
-        pl.items, pl.counts, col, val, scale, d, x, y, acc, acc_scale, pl.partials);
+        pl.items, pl.counts, col, val, scale, d, x, y, acc, acc_scale, acc_init, pl.partials);
 }
 
 // lanes per item: the whole row up to 64 lanes, or (GDD_HOP_LANES=8/16/32, V = 4) narrower groups
@@ -401,44 +422,47 @@ int hop_lanes_override() {
 
 template <int V>
 void launch_hop_v(const Plan& pl, const int32_t* col, const float* val, float scale, int d,
-                  const float* x, float* y, float* acc, float acc_scale, hipStream_t s) {
+                  const float* x, float* y, float* acc, float acc_scale, const float* acc_init, hipStream_t s) {
   const int lanes = (d + V - 1) / V;
   const int ov = hop_lanes_override();
   if (ov == 8)
-    return launch_hop_vg<V, 8>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+    return launch_hop_vg<V, 8>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
   if (ov == 16)
-    return launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+    return launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
   // 29..32 lanes of float4 (d in (112, 128]): two XCD slices of 16 lanes each, so an XCD's L2 caches
   // half of every gathered row (measured at the arxiv shape, d = 128: 202 vs 208 us per hop; the
   // gathers' L2 hit rate rises, the instruction overhead of the narrower groups stays small). With
   // fewer lanes the second slice idles most of its lanes while reading the whole column/value stream
   // again: products' d = 100 (25 lanes) runs 9.5 ms per hop in one 32-lane group vs 12.4 sliced.
   if (lanes <= 16 || (V == 4 && lanes > 28 && lanes <= 32 && ov != 32))
-    launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+    launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
   else if (lanes <= 32)
-    launch_hop_vg<V, 32>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+    launch_hop_vg<V, 32>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
   else
-    launch_hop_vg<V, 64>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+    launch_hop_vg<V, 64>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
 }
 
+// acc_init (nullable): the accumulator's previous value is acc_scale * acc_init instead of acc (the
+// first hop folds the initial target = fp32(1-alpha) * X, agent :59, into its epilogue)
 int run_hop(const Plan& pl, const int32_t* rowptr, const int32_t* col, const float* val,
             float scale, int d, const float* x, float* y, float* acc, float acc_scale,
-            hipStream_t s) {
+            hipStream_t s, const float* acc_init = nullptr) {
   // float4 rows need 16-byte aligned row starts: d % 4 == 0 and 16-byte aligned bases
   auto aligned = [](const void* p, int a) { return ((uintptr_t)p % a) == 0; };
   const bool a16 = aligned(x, 16) && aligned(y, 16) && (!acc || aligned(acc, 16)) &&
-                   aligned(pl.partials, 16);
-  const bool a8 = aligned(x, 8) && aligned(y, 8) && (!acc || aligned(acc, 8));
+                   (!acc_init || aligned(acc_init, 16)) && aligned(pl.partials, 16);
+  const bool a8 = aligned(x, 8) && aligned(y, 8) && (!acc || aligned(acc, 8)) &&
+                  (!acc_init || aligned(acc_init, 8));
   if (d % 4 == 0 && a16)
-    launch_hop_v<4>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+    launch_hop_v<4>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
   else if (d % 2 == 0 && a8)
-    launch_hop_v<2>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+    launch_hop_v<2>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
   else
-    launch_hop_v<1>(pl, col, val, scale, d, x, y, acc, acc_scale, s);
+    launch_hop_v<1>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
   GDD_LAUNCHED();
   const unsigned fixup_grid = (unsigned)std::min<int64_t>(pl.max_long, kFixupBlocks);
   k_fixup<<<fixup_grid, 256, 0, s>>>(pl.counts, pl.long_rows, pl.long_off, rowptr, d, pl.partials, y,
-                                     acc, acc_scale);
+                                     acc, acc_scale, acc_init);
   GDD_LAUNCHED();
   return GDD_OK;
 }
@@ -515,9 +539,11 @@ extern "C" int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, cons
   const float w32 = (float)(1.0 - (double)alpha);
   const int64_t total = n * (int64_t)d;
   const unsigned eb = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
-  k_scale_copy<<<eb, 256, 0, s>>>(total, X, w32, target, T == 1 ? p_last : nullptr);
-  GDD_LAUNCHED();
-  if (T == 1) return GDD_OK;
+  if (T == 1) {
+    k_scale_copy<<<eb, 256, 0, s>>>(total, X, w32, target, p_last);
+    GDD_LAUNCHED();
+    return GDD_OK;
+  }
   Carver cv(ws, ws_bytes);
   Plan pl;
   rc = build_plan(n, nnz, d, rowptr, cv, pl, s);
@@ -528,7 +554,7 @@ extern "C" int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, cons
   const float* in = X;
   for (int h = 0; h < hops; ++h) {
     float* out = bufs[h % 2];
-    rc = run_hop(pl, rowptr, col, val, a32, d, in, out, target, w32, s);
+    rc = run_hop(pl, rowptr, col, val, a32, d, in, out, target, w32, s, h == 0 ? X : nullptr);
     if (rc) return rc;
     in = out;
   }
