@@ -190,14 +190,20 @@ __global__ void k_rows_emit(int64_t n, const int32_t* __restrict__ rowptr,
 // no longer serialise one lane group. The kernels are no-ops when the probe chose the other path.
 __device__ __forceinline__ bool fast_path(const int32_t* flag) { return *flag == 1; }
 
-// per row: output count and where the diagonal sits (lower bound of i in the row's columns)
+constexpr int kFillBlk = 256;     // entries per k_fast_fill block
+constexpr int kFillRowsLds = 512;  // row starts a block stages in LDS for its lanes' searches
+
+// per row: output count and where the diagonal sits (lower bound of i in the row's columns); also
+// the row holding each fill block's first entry (blk_row[b] = the row of entry b * kFillBlk)
 __global__ void k_fast_count(int64_t n, const int32_t* __restrict__ rowptr,
                              const int32_t* __restrict__ col, const int32_t* __restrict__ flag,
-                             int32_t* __restrict__ cnt, int32_t* __restrict__ dpos) {
+                             int32_t* __restrict__ cnt, int32_t* __restrict__ dpos,
+                             int32_t* __restrict__ blk_row) {
   if (!fast_path(flag)) return;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int32_t s = rowptr[i], e = rowptr[i + 1];
+  for (int64_t b = ((int64_t)s + kFillBlk - 1) / kFillBlk; b * kFillBlk < e; ++b) blk_row[b] = (int32_t)i;
   int32_t a = s, b = e;
   while (a < b) {
     const int32_t m = (a + b) >> 1;
@@ -211,43 +217,50 @@ __global__ void k_fast_count(int64_t n, const int32_t* __restrict__ rowptr,
   dpos[i] = has ? -(a - s) - 1 : (a - s);  // < 0: stored at -(v+1); >= 0: inserted at v
 }
 
-// one lane per stored entry; the block's row range is found once, each lane then searches it
-__global__ __launch_bounds__(256) void k_fast_fill(int64_t n, int64_t nnz,
-                                                   const int32_t* __restrict__ rowptr,
-                                                   const int32_t* __restrict__ col,
-                                                   const int32_t* __restrict__ flag,
-                                                   const double* __restrict__ r64,
-                                                   const int32_t* __restrict__ dpos,
-                                                   const int32_t* __restrict__ rowptr_out,
-                                                   int32_t* __restrict__ col_out,
-                                                   float* __restrict__ val_out) {
+// one lane per stored entry. The block's row range comes from k_fast_count's blk_row (its first
+// entry's row, and the next block's first row as an upper bound); the range's row starts are staged
+// in LDS for the lanes' searches (a global search when the range holds many empty rows)
+__global__ __launch_bounds__(kFillBlk) void k_fast_fill(int64_t n, int64_t nnz,
+                                                        const int32_t* __restrict__ rowptr,
+                                                        const int32_t* __restrict__ col,
+                                                        const int32_t* __restrict__ flag,
+                                                        const double* __restrict__ r64,
+                                                        const int32_t* __restrict__ dpos,
+                                                        const int32_t* __restrict__ blk_row,
+                                                        const int32_t* __restrict__ rowptr_out,
+                                                        int32_t* __restrict__ col_out,
+                                                        float* __restrict__ val_out) {
   if (!fast_path(flag)) return;
-  __shared__ int32_t s_rows[2];
-  const int64_t p0 = (int64_t)blockIdx.x * blockDim.x;
+  __shared__ int32_t s_rp[kFillRowsLds + 1];
+  const int64_t p0 = (int64_t)blockIdx.x * kFillBlk;
   if (p0 >= nnz) return;
-  const int64_t p1 = min<int64_t>(nnz, p0 + blockDim.x) - 1;
-  if (threadIdx.x < 2) {  // last row whose start <= target
-    const int64_t target = threadIdx.x == 0 ? p0 : p1;
-    int64_t a = 0, b = n;  // rowptr[a] <= target < rowptr[b]
+  const int64_t nblk = (nnz + kFillBlk - 1) / kFillBlk;
+  // rowptr[lo] <= p0 and every p of the block < rowptr[hi]
+  const int64_t lo = blk_row[blockIdx.x];
+  const int64_t hi = blockIdx.x + 1 < nblk ? (int64_t)blk_row[blockIdx.x + 1] + 1 : n;
+  const bool in_lds = hi - lo <= kFillRowsLds;
+  if (in_lds)
+    for (int64_t q = threadIdx.x; q <= hi - lo; q += kFillBlk) s_rp[q] = rowptr[lo + q];
+  __syncthreads();
+  const int64_t p = p0 + threadIdx.x;
+  if (p >= nnz) return;
+  int64_t a = lo, b = hi;  // rowptr[a] <= p < rowptr[b]: the last row whose start <= p
+  if (in_lds) {
     while (b - a > 1) {
       const int64_t m = (a + b) >> 1;
-      if (rowptr[m] <= target)
+      if (s_rp[m - lo] <= p)
         a = m;
       else
         b = m;
     }
-    s_rows[threadIdx.x] = (int32_t)a;
-  }
-  __syncthreads();
-  const int64_t p = p0 + threadIdx.x;
-  if (p >= nnz) return;
-  int64_t a = s_rows[0], b = (int64_t)s_rows[1] + 1;
-  while (b - a > 1) {
-    const int64_t m = (a + b) >> 1;
-    if (rowptr[m] <= p)
-      a = m;
-    else
-      b = m;
+  } else {
+    while (b - a > 1) {
+      const int64_t m = (a + b) >> 1;
+      if (rowptr[m] <= p)
+        a = m;
+      else
+        b = m;
+    }
   }
   const int32_t i = (int32_t)a;
   const int32_t off = (int32_t)(p - rowptr[i]);
@@ -289,12 +302,12 @@ __global__ void k_set_last(int64_t n, const int32_t* __restrict__ cnt, int32_t* 
 using namespace gdd;
 
 extern "C" size_t gdd_normalize_ws_bytes(int64_t n, int64_t nnz) {
-  (void)nnz;
   size_t b = 256;                               // flag
   b += align256(sizeof(double) * (size_t)n);    // r64
   b += align256(sizeof(float) * (size_t)n);     // r32
   b += align256(sizeof(int32_t) * (size_t)n);   // cnt
   b += align256(sizeof(int32_t) * (size_t)n);   // dpos
+  b += align256(sizeof(int32_t) * (size_t)(std::max<int64_t>(nnz, 0) / kFillBlk + 1));  // blk_row
   b += scan_i32_ws_bytes(n) + 256;
   return b;
 }
@@ -316,6 +329,7 @@ extern "C" int gdd_normalize_csr(int64_t n, int64_t nnz, const int32_t* rowptr,
   float* r32 = cv.take<float>(n);
   int32_t* cnt = cv.take<int32_t>(n);
   int32_t* dpos = cv.take<int32_t>(n);
+  int32_t* blk_row = cv.take<int32_t>(nnz / kFillBlk + 1);
   size_t scan_bytes = scan_i32_ws_bytes(n);
   void* scan_ws = cv.take<char>(scan_bytes);
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "normalize: workspace %zu too small", ws_bytes);
@@ -329,7 +343,7 @@ extern "C" int gdd_normalize_csr(int64_t n, int64_t nnz, const int32_t* rowptr,
   // binary input: the probe's flag picks the entry-parallel kernels (I added) or the general
   // row-group kernels (no I); each set returns at once when the other applies
   if (!val) {
-    k_fast_count<<<rgrid, 256, 0, s>>>(n, rowptr, col, flag, cnt, dpos);
+    k_fast_count<<<rgrid, 256, 0, s>>>(n, rowptr, col, flag, cnt, dpos, blk_row);
     GDD_LAUNCHED();
   }
   k_rows_emit<false><<<grid, 256, 0, s>>>(n, rowptr, col, val, flag, r64, r32, cnt, nullptr,
@@ -341,8 +355,8 @@ extern "C" int gdd_normalize_csr(int64_t n, int64_t nnz, const int32_t* rowptr,
   GDD_LAUNCHED();
   if (!val) {
     if (nnz > 0) {
-      k_fast_fill<<<(unsigned)((nnz + 255) / 256), 256, 0, s>>>(n, nnz, rowptr, col, flag, r64,
-                                                               dpos, rowptr_out, col_out, val_out);
+      k_fast_fill<<<(unsigned)((nnz + kFillBlk - 1) / kFillBlk), kFillBlk, 0, s>>>(
+          n, nnz, rowptr, col, flag, r64, dpos, blk_row, rowptr_out, col_out, val_out);
       GDD_LAUNCHED();
     }
     k_fast_diag<<<rgrid, 256, 0, s>>>(n, flag, r64, dpos, rowptr_out, col_out, val_out);
