@@ -25,10 +25,10 @@
 //   terms     the block's fp64 cumulative total and the block's sgemv_t lane chains (4 or 8 fp32
 //             chains of <= 1024 entries) — round c+1's fold reads T * blocks values, never a row.
 // A last single-workgroup launch folds round k-1. The cumulative potential is evaluated block-wise
-// (thread-sequential, then fixed shuffle/wave combinations) instead of strictly left to right;
-// every workgroup evaluates the same numbers, the sequence stays non-decreasing, and it can differ
-// from numpy's only by fp64 rounding — a draw changes only if u * pot falls inside that rounding
-// gap (probability ~1e-13 per draw), which no fixture or test has produced.
+// (thread-sequential, then fixed shuffle/wave combinations) instead of strictly left to right; every
+// workgroup evaluates the same numbers. It can differ from numpy's by fp64 rounding only, and every
+// search checks whether that rounding could decide its draw (cum_tol): if so, one thread replays
+// numpy's left-to-right sum (np_cumsum_search), so every draw is numpy's.
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -489,6 +489,34 @@ __device__ __forceinline__ void block_prefix(const double (&v)[kPer], double (&p
   for (int u = 0; u < kPer; ++u) pre[u] = base + r[u];
 }
 
+// ---- numpy's left-to-right cumsum, exactly --------------------------------------------------------
+// Every prefix in this file is a blocked evaluation of np.cumsum(w * closest, dtype=float64)
+// (sklearn/utils/extmath.py stable_cumsum). Any summation order of m non-negative terms lies within
+// gamma_{m-1} = (m-1)u / (1 - (m-1)u), u = 2^-53, relative of the exact sum S (Higham, "Accuracy and
+// Stability of Numerical Algorithms", 2nd ed., eq. 4.4), so a blocked prefix c and numpy's sequential
+// prefix s of the same entry differ by at most 2 gamma S. A decision `c < r` can come out differently
+// from numpy's `s < r` only if c and s straddle r, which needs |c - r| <= 2 gamma S with S <= r / (1 -
+// gamma): tol = 2.25 n u r bounds that for every n < 2^31. Each search below checks the prefixes
+// that decide its draw against tol (the two neighbours of a binary search's answer; every counted
+// entry of a ballot count; the block boundaries of the multi-block scan) and, when one is that close,
+// one thread replays numpy's sum strictly left to right. For a draw the check passes, the blocked
+// answer IS numpy's; the replay runs with probability ~5 n u per draw.
+//   exact = 1: that rule; 0: never replay (test only: shows a case is adversarial); 2: always replay.
+__device__ __forceinline__ double cum_tol(int exact, int64_t n, double r) {
+  return exact == 2 ? __builtin_inf() : exact == 0 ? -1.0 : 2.25 * (double)n * 0x1p-53 * r;
+}
+
+// searchsorted_left(np.cumsum(w * row, dtype=float64), r): the products in fp32, the running sum in
+// fp64, entry by entry (row and w may be LDS or global)
+__device__ __noinline__ int64_t np_cumsum_search(const float* row, const float* w, int64_t n, double r) {
+  double run = 0.0;
+  for (int64_t e = 0; e < n; ++e) {
+    run = run + (double)((w ? w[e] : 1.0f) * row[e]);
+    if (!(run < r)) return e;
+  }
+  return n;
+}
+
 // ---- the trials' potentials from their per-block sgemv_t terms -------------------------------------
 struct KppArgs {
   int64_t n, m1;      // points; m1 = n & ~3 (the entries under sgemv_t blocks)
@@ -510,6 +538,7 @@ struct KppArgs {
   float* centers;
   int64_t* indices;
   SklPlan plan;
+  int exact;          // cum_tol's mode
 };
 
 __device__ __forceinline__ float wv(const float* w, int64_t i) { return w ? w[i] : 1.0f; }
@@ -785,8 +814,9 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   __shared__ float s_pot[kMaxTrials];
   __shared__ double s_wave[kWaves];
   __shared__ int s_jmin;
-  __shared__ double s_P;
-  __shared__ int s_cnt[kWaves];
+  __shared__ double s_P, s_tot;
+  __shared__ int s_cnt[kWaves], s_amb[kWaves];
+  __shared__ int64_t s_ct;
   const int t = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int pq = (c - 1) & 1, cq = c & 1;
@@ -845,11 +875,18 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     if (found != INT_MAX) atomicMin(&s_jmin, found);
     __syncthreads();
     if (found != INT_MAX && found == s_jmin) s_P = Pf;
+    if (tid == 0) {  // the whole cumulative potential (the no-crossing case's boundary)
+      double tot = 0.0;
+      for (int q = 0; q < kWaves; ++q) tot = tot + s_wave[q];
+      s_tot = tot;
+    }
     __syncthreads();
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 22);
   int64_t ct = n - 1;
   const int jb = s_jmin;
+  const double tol = cum_tol(a.exact, n, r);
+  bool amb;  // a deciding prefix within tol of r (uniform across the workgroup)
   if (jb != INT_MAX) {  // count inside block jb (uniform branch)
     const int64_t e0 = (int64_t)jb * kBlk + kPer * tid;
     double v[kPer], pre[kPer];
@@ -861,13 +898,32 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     block_prefix(v, pre, s_wave);
     const double P = s_P;
     int cw = 0;
+    bool aw = false;
 #pragma unroll
-    for (int q = 0; q < kPer; ++q) cw += __popcll(__ballot(e0 + q < n && P + pre[q] < r));
-    if (lane == 0) s_cnt[wave] = cw;
+    for (int q = 0; q < kPer; ++q) {
+      const double pv = P + pre[q];
+      cw += __popcll(__ballot(e0 + q < n && pv < r));
+      aw = aw || __ballot(e0 + q < n && fabs(pv - r) <= tol) != 0ull;
+    }
+    if (lane == 0) {
+      s_cnt[wave] = cw;
+      s_amb[wave] = aw;
+    }
     __syncthreads();
     int64_t cnt = 0;
-    for (int q = 0; q < kWaves; ++q) cnt += s_cnt[q];
+    amb = fabs(P - r) <= tol;  // the boundary before block jb (entries of earlier blocks)
+    for (int q = 0; q < kWaves; ++q) {
+      cnt += s_cnt[q];
+      amb = amb || s_amb[q];
+    }
     ct = min<int64_t>(n - 1, (int64_t)jb * kBlk + cnt);
+  } else {
+    amb = fabs(s_tot - r) <= tol;
+  }
+  if (amb) {  // numpy's sequential cumsum decides this draw
+    if (tid == 0) s_ct = min<int64_t>(n - 1, np_cumsum_search(wrow, a.w, n, r));
+    __syncthreads();
+    ct = s_ct;
   }
   if (blk == 0 && tid == 0) a.cand[cq][t] = ct;
   if (PICK && blk == 0 && t == 0 && tid == 0) a.winq[cq] = bw;
@@ -1063,6 +1119,7 @@ struct Kpp1Args {
   float* potv2[2];       // [T*T]
   int64_t* candw2[2];    // [T*T][T]
   int64_t* candself2[2];  // [T*T]
+  int exact;             // cum_tol's mode
 };
 
 __device__ __forceinline__ int kpp1_argmin(const float* __restrict__ pot, int T) {
@@ -1262,7 +1319,7 @@ __global__ __launch_bounds__(kThr) void k_kpp1_pick(Kpp1Args a, int c) {
   __shared__ float s_d[kBlk];
   __shared__ float s_ch[8 * kChainLd];  // unit weights: chain l's entries contiguous
   __shared__ double s_wave[kWaves];
-  __shared__ int s_cnt[kMaxTrials][kWaves];
+  __shared__ int s_cnt[kMaxTrials][kWaves], s_amb[kMaxTrials][kWaves];
   __shared__ float s_pot;
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cq = c & 1, T = a.T;
@@ -1345,96 +1402,33 @@ __global__ __launch_bounds__(kThr) void k_kpp1_pick(Kpp1Args a, int c) {
   for (int t2 = 0; t2 < kMaxTrials; ++t2) {
     if (t2 < T) {
       const double rr = u[t2] * pot;
+      const double tol = cum_tol(a.exact, n, rr);
       int cw = 0;
+      bool aw = false;
 #pragma unroll
-      for (int q = 0; q < kPer; ++q) cw += __popcll(__ballot(kPer * tid + q < n && pre[q] < rr));
-      if (lane == 0) s_cnt[t2][wave] = cw;
+      for (int q = 0; q < kPer; ++q) {
+        const bool live = kPer * tid + q < n;
+        cw += __popcll(__ballot(live && pre[q] < rr));
+        aw = aw || __ballot(live && fabs(pre[q] - rr) <= tol) != 0ull;
+      }
+      if (lane == 0) {
+        s_cnt[t2][wave] = cw;
+        s_amb[t2][wave] = aw;
+      }
     }
   }
   __syncthreads();
   if (tid < T) {
     int64_t cnt = 0;
-    for (int q = 0; q < kWaves; ++q) cnt += s_cnt[tid][q];
+    bool amb = false;
+    for (int q = 0; q < kWaves; ++q) {
+      cnt += s_cnt[tid][q];
+      amb = amb || s_amb[tid][q];
+    }
+    if (amb) cnt = np_cumsum_search(s_d, a.w, n, a.uniforms[(int64_t)c * T + tid] * pot);
     a.candw[cq][(int64_t)t * T + tid] = min<int64_t>(n - 1, cnt);
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 74);
-}
-
-__device__ __forceinline__ int kpp1_ld(int64_t n) {  // LDS row stride: 8 (mod 64) floats
-  return (int)(((n + 63) & ~63ll) + 8);
-}
-
-// the T potentials of the staged rows (sgemv_t lane chains, n % 4 tail) into s_pot
-struct Kpp1FoldView {
-  int64_t n, m1;
-  int T;
-  const float* w;
-};
-
-__device__ void kpp1_fold(const Kpp1FoldView& a, const float* __restrict__ s_rows, int ld,
-                          float* __restrict__ s_pot) {
-  const int tid = threadIdx.x, T = a.T;
-  const int64_t NB = a.m1;
-  if (tid >= 8 * ((T + 7) & ~7)) return;  // whole waves only (the shuffles below)
-  const int t = tid >> 3, l = tid & 7;
-  const bool act = t < T;
-  const float* row = s_rows + (size_t)(act ? t : 0) * ld;
-  const float* w = a.w;
-  const bool k4x2 = (T & 2) && t >= (T & ~3) && t < (T & ~3) + 2;
-  float acc = 0.f;
-  if (act && NB > 0) {
-    if (k4x2) {  // 4 lanes (o % 4), product then add
-      if (l < 4) {
-        int64_t o = l;
-        if (!w) {
-          for (; o + 4 * 31 < NB; o += 128) {
-            float x[32];
-#pragma unroll
-            for (int q = 0; q < 32; ++q) x[q] = row[o + 4 * q];
-#pragma unroll
-            for (int q = 0; q < 32; ++q) acc = acc + x[q];
-          }
-        }
-        for (; o < NB; o += 4) acc = acc + row[o] * (w ? w[o] : 1.0f);
-      }
-    } else {  // 8 lanes: the first NB&4 entries into lanes 0..3, then lane (o - (NB&4)) % 8; fma
-      const int64_t h4 = NB & 4;
-      if (l < h4) acc = __builtin_fmaf(row[l], w ? w[l] : 1.0f, acc);
-      int64_t o = h4 + l;
-      if (!w) {  // unit weights: fma(x, 1, acc) == acc + x
-        for (; o + 8 * 31 < NB; o += 256) {
-          float x[32];
-#pragma unroll
-          for (int q = 0; q < 32; ++q) x[q] = row[o + 8 * q];
-#pragma unroll
-          for (int q = 0; q < 32; ++q) acc = acc + x[q];
-        }
-      }
-      for (; o < NB; o += 8) acc = __builtin_fmaf(row[o], w ? w[o] : 1.0f, acc);
-    }
-  }
-  // group of 8 lanes at t * 8
-  const int lane = tid & 63, g0 = lane & ~7;
-  const float a0 = __shfl(acc, g0), a1 = __shfl(acc, g0 + 1), a2 = __shfl(acc, g0 + 2),
-              a3 = __shfl(acc, g0 + 3), a4 = __shfl(acc, g0 + 4), a5 = __shfl(acc, g0 + 5),
-              a6 = __shfl(acc, g0 + 6), a7 = __shfl(acc, g0 + 7);
-  if (act && l == 0) {
-    float y = 0.f;
-    if (NB > 0) {
-      if (k4x2) {
-        y = (a0 + a1) + (a2 + a3);
-      } else {
-        const float q0 = a0 + a4, q1 = a1 + a5, q2 = a2 + a6, q3 = a3 + a7;
-        y = (q0 + q1) + (q2 + q3);
-      }
-    }
-    if (a.m1 < a.n) {
-      float sx = row[a.m1] * wv(w, a.m1);
-      for (int64_t o = a.m1 + 1; o < a.n; ++o) sx = __builtin_fmaf(row[o], wv(w, o), sx);
-      y = y + sx;
-    }
-    s_pot[t] = y;
-  }
 }
 
 constexpr int kFPW = 22;     // prefix entries per thread of waves 1..3 in the fold (192 x 22 >= 4096)
@@ -1551,6 +1545,10 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
         const int mid = (lo + hi) >> 1;
         if (s_cum[mid] < rr) lo = mid + 1; else hi = mid;
       }
+      // the answer's two neighbours decide it (cum_tol): replay numpy's sum when either is close
+      const double tol = cum_tol(a.exact, n, rr);
+      if ((lo > 0 && fabs(s_cum[lo - 1] - rr) <= tol) || (lo < n && fabs(s_cum[lo] - rr) <= tol))
+        lo = (int)np_cumsum_search(s_d, a.w, n, rr);
       cand_out[tid] = min(n - 1, lo);
     }
   }
@@ -1906,265 +1904,6 @@ __global__ __launch_bounds__(64) void k_kpp1_final2(Kpp1Args a, int c, int lq, i
   for (int j = threadIdx.x; j < a.dim; j += 64) a.centers[(int64_t)c * a.dim + j] = a.X[src * a.dim + j];
 }
 
-// ---- every single-block round in ONE workgroup (table plans, T <= 8, unit weights, n <= 4096) -----
-// Opt-in (GDD_KPP_PERSIST=1), kept as the measured answer to VERDICT r1's suggestion: 20-23 us per
-// round against 9.2-9.4 for one launch per round (tools/micro_kpp.py), because one CU then carries
-// every trial's fold. VERDICT r1's persistent single-workgroup form, made possible by the distance
-// table: a round needs
-// only T rows of D (one memory trip) and everything else is in the workgroup's LDS, so the rounds
-// run back to back with workgroup barriers only — no launches, no cross-workgroup hand-offs.
-//   [A] round c-1's winner from the LDS potentials, this round's candidates from its table row;
-//   [B] row t = np.minimum(closest, D[cand_t]) for every trial (closest = the winner's row, in LDS);
-//   [C] wave 0: all T trials' sgemv_t lane chains at once (lanes 8t..8t+7, strided LDS reads);
-//       waves 1..7: the fp64 cumulative potentials, in the fold's exact blocking (per trial 3 wave
-//       tasks of 64 threads x kFPW entries, Hillis-Steele within the wave, wave totals in order);
-//   [D] per trial and threshold u * pot: the first thread whose last cumulative value is >= the
-//       threshold re-runs its kFPW-entry run and counts — searchsorted_left without an fp64 LDS copy;
-//   [E] the candidate table for round c+1.
-constexpr int kPsThr = 512;      // 8 waves: 256 VGPRs each, nothing spills
-constexpr int kPsTrials = 8;
-constexpr int kPsTasks = 3;    // prefix wave tasks per trial
-constexpr int kPsPer = kBlk / kPsThr;      // entries per thread in [B]
-constexpr int kPsWaves = kPsThr / 64 - 1;  // prefix / search waves
-constexpr int kPsRuns = (kPsTrials * kPsTasks + kPsWaves - 1) / kPsWaves;  // tasks per wave
-constexpr int kPsPad = 512;    // LDS floats past the rows: the chains' look-ahead reads
-
-// acc + p[0] + p[stride] + ... (L entries), reads a 16-entry group ahead of the dependent adds
-__device__ __forceinline__ float chain_strided(const float* __restrict__ p, int stride, int L, float acc) {
-  float A[16], B[16];
-#pragma unroll
-  for (int u = 0; u < 16; ++u) A[u] = p[u * stride];
-#pragma unroll
-  for (int u = 0; u < 16; ++u) asm volatile("" : "+v"(A[u]));
-  int m = 0;
-  for (; m + 32 <= L; m += 32) {
-#pragma unroll
-    for (int u = 0; u < 16; ++u) B[u] = p[(m + 16 + u) * stride];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < 16; ++u) acc = acc + A[u];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < 16; ++u) A[u] = p[(m + 32 + u) * stride];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < 16; ++u) acc = acc + B[u];
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  // A holds entries m .. m+15 (L - m < 32)
-#pragma unroll
-  for (int u = 0; u < 16; ++u) B[u] = p[(m + 16 + u) * stride];
-#pragma unroll
-  for (int u = 0; u < 16; ++u)
-    if (m + u < L) acc = acc + A[u];
-#pragma unroll
-  for (int u = 0; u < 16; ++u)
-    if (m + 16 + u < L) acc = acc + B[u];
-  return acc;
-}
-
-__global__ __launch_bounds__(kPsThr) void k_kpp1_persist(Kpp1Args a, const float* __restrict__ D) {
-  extern __shared__ __attribute__((aligned(16))) float s_d[];  // T rows of ld floats (+ padding)
-  __shared__ float s_pot[kPsTrials];
-  __shared__ int64_t s_cw[kPsTrials][kPsTrials];  // [trial that wins][trial]: the next candidate
-  __shared__ int64_t s_cand[kPsTrials];           // each trial's candidate in the current round
-  __shared__ double s_u[kPsTrials];
-  __shared__ double s_wtot[kPsTrials][kPsTasks];
-  __shared__ int s_res[kPsTrials][kPsTrials][kPsTasks];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int T = a.T, n = (int)a.n, k = a.k, m1 = (int)a.m1;
-  const int ld = kpp1_ld(n);
-  // round 0 (the first centre): k_kpp1_pick left its potential and candidate column
-  if (tid == 0) s_pot[0] = a.potv[0][0];
-  if (tid < T) s_cw[0][tid] = a.candw[0][tid];
-  for (int i = tid; i < n; i += kPsThr) s_d[i] = a.closest0[i];
-  __syncthreads();
-  for (int c = 1; c < k; ++c) {
-    const int Tp = c == 1 ? 1 : T;
-    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && c == k - 2), 60);
-    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && c == k - 1), 65);
-    // [A]
-    int bw = 0;
-    float best = s_pot[0];
-    for (int q = 1; q < Tp; ++q) {
-      const float pt = s_pot[q];
-      if (best == best && (pt < best || pt != pt)) {
-        bw = q;
-        best = pt;
-      }
-    }
-    if (tid == 0 && c >= 2) a.indices[c - 1] = s_cand[bw];  // rows gathered after the rounds
-    bw = __builtin_amdgcn_readfirstlane(bw);  // uniform: scalar row bases below
-    int64_t ct[kPsTrials];
-#pragma unroll
-    for (int t = 0; t < kPsTrials; ++t) {
-      const int64_t v = s_cw[bw][min(t, T - 1)];
-      ct[t] = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
-                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v));
-    }
-    const double un = (tid < T && c + 1 < k) ? a.uniforms[(int64_t)c * T + tid] : 0.0;
-    // [B] one trip: every trial's table row for this thread's entries
-    float dd[kPsTrials][kPsPer], cl[kPsPer];
-#pragma unroll
-    for (int q = 0; q < kPsPer; ++q) {
-      const int i = min(tid + kPsThr * q, n - 1);
-      cl[q] = s_d[bw * ld + i];
-#pragma unroll
-      for (int t = 0; t < kPsTrials; ++t) dd[t][q] = (D + ct[t] * n)[i];
-    }
-    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && c == k - 2), 61);
-#pragma unroll
-    for (int q = 0; q < kPsPer; ++q) {
-      const int i = tid + kPsThr * q;
-      if (i < n) {
-#pragma unroll
-        for (int t = 0; t < kPsTrials; ++t)
-          if (t < T) s_d[t * ld + i] = np_minimum(cl[q], dd[t][q]);
-      }
-    }
-    __syncthreads();
-    if (tid < T) {
-      s_cand[tid] = ct[tid];
-      s_u[tid] = un;
-    }
-    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && c == k - 2), 62);
-    // [C]
-    double pex[kPsRuns], prun[kPsRuns];  // this thread's (ex, run) per prefix task
-    if (wave == 0) {
-      const int t = lane >> 3, l = lane & 7, g0 = lane & ~7;
-      const bool k4x2 = (T & 2) && t >= (T & ~3) && t < (T & ~3) + 2;
-      const int nl = k4x2 ? 4 : 8, h4 = k4x2 ? 0 : (m1 & 4);
-      const float* row = s_d + min(t, T - 1) * ld;
-      float acc = 0.f;
-      if (t < T && m1 > 0 && l < nl) {
-        if (l < h4) acc = acc + row[l];
-        const int L = max((m1 - h4 - l + nl - 1) / nl, 0);
-        acc = chain_strided(row + h4 + l, nl, L, acc);
-      }
-      const float ql = acc + __shfl(acc, g0 + ((l + 4) & 7));
-      const float q0 = __shfl(ql, g0), q1 = __shfl(ql, g0 + 1), q2 = __shfl(ql, g0 + 2), q3 = __shfl(ql, g0 + 3);
-      const float a0 = __shfl(acc, g0), a1 = __shfl(acc, g0 + 1), a2 = __shfl(acc, g0 + 2), a3 = __shfl(acc, g0 + 3);
-      if (t < T && l == 0) {
-        float y = 0.f;
-        if (m1 > 0) y = k4x2 ? (a0 + a1) + (a2 + a3) : (q0 + q1) + (q2 + q3);
-        if (m1 < n) {
-          float sx = row[m1] * 1.0f;
-          for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(row[o], 1.0f, sx);
-          y = y + sx;
-        }
-        s_pot[t] = y;
-      }
-    } else if (c + 1 < k) {
-#pragma unroll
-      for (int h = 0; h < kPsRuns; ++h) {
-        const int task = wave - 1 + kPsWaves * h;
-        if (task < T * kPsTasks) {
-          const int t = task / kPsTasks, p = task - t * kPsTasks;
-          const int e0 = kFPW * (p * 64 + lane);
-          const float* row = s_d + t * ld;
-          float v[kFPW];  // every read issued before the dependent fp64 adds (no branches around them)
-#pragma unroll
-          for (int q = 0; q < kFPW; ++q) v[q] = row[min(e0 + q, n - 1)];
-          double run = 0.0;
-#pragma unroll
-          for (int q = 0; q < kFPW; ++q) run = run + (e0 + q < n ? (double)(1.0f * v[q]) : 0.0);
-          double inc = run;
-#pragma unroll
-          for (int o = 1; o < 64; o <<= 1) {
-            const double y = __shfl_up(inc, o);
-            if (lane >= o) inc = inc + y;
-          }
-          double ex = __shfl_up(inc, 1);
-          if (lane == 0) ex = 0.0;
-          if (lane == 63) s_wtot[t][p] = inc;
-          pex[h] = ex;
-          prun[h] = run;
-        }
-      }
-    }
-    __syncthreads();
-    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && c == k - 2), 63);
-    if (c + 1 >= k) break;
-    // [D]
-    if (wave > 0) {
-      double su[kPsTrials];  // this round's uniforms, once per thread
-#pragma unroll
-      for (int t2 = 0; t2 < kPsTrials; ++t2) su[t2] = s_u[min(t2, T - 1)];
-#pragma unroll
-      for (int h = 0; h < kPsRuns; ++h) {
-        const int task = wave - 1 + kPsWaves * h;
-        if (task < T * kPsTasks) {
-          const int t = task / kPsTasks, p = task - t * kPsTasks;
-          const int e0 = kFPW * (p * 64 + lane);
-          const float* row = s_d + t * ld;
-          double B = 0.0;
-          for (int q = 0; q < p; ++q) B = B + s_wtot[t][q];
-          const double last = B + (pex[h] + prun[h]);
-          const bool empty = e0 >= n;
-          const double pot = (double)s_pot[t];
-          unsigned mine = 0;  // thresholds whose first non-full thread is this one
-          for (int t2 = 0; t2 < T; ++t2) {
-            const double rr = su[t2] * pot;
-            const bool full = empty || last < rr;
-            const unsigned long long m = __ballot(!full);
-            if (m == 0ull) {
-              if (lane == 0) s_res[t][t2][p] = -1;
-            } else if (lane == __builtin_ctzll(m)) {
-              mine |= 1u << t2;
-            }
-          }
-          if (mine) {  // re-run this thread's entries: searchsorted_left inside them
-            float v[kFPW];
-#pragma unroll
-            for (int q = 0; q < kFPW; ++q) v[q] = row[min(e0 + q, n - 1)];
-            for (int t2 = 0; t2 < T; ++t2) {
-              if (!((mine >> t2) & 1u)) continue;
-              const double rr = su[t2] * pot;
-              double run = 0.0;
-              int cnt = 0;
-#pragma unroll
-              for (int q = 0; q < kFPW; ++q) {
-                run = run + (e0 + q < n ? (double)(1.0f * v[q]) : 0.0);
-                cnt += (B + (pex[h] + run)) < rr ? 1 : 0;
-              }
-              s_res[t][t2][p] = e0 + cnt;
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // [E]
-    if (tid < T * T) {
-      const int t = tid / T, t2 = tid - t * T;
-      int res = n;
-      for (int p = 0; p < kPsTasks; ++p) {
-        const int r = s_res[t][t2][p];
-        if (r >= 0) {
-          res = r;
-          break;
-        }
-      }
-      s_cw[t][t2] = min(n - 1, res);
-    }
-    __syncthreads();
-    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && c == k - 2), 74);
-  }
-  if (tid == 0) {  // round k-1's winner
-    int bw = 0;
-    float best = s_pot[0];
-    for (int q = 1; q < T; ++q) {
-      const float pt = s_pot[q];
-      if (best == best && (pt < best || pt != pt)) {
-        bw = q;
-        best = pt;
-      }
-    }
-    a.indices[k - 1] = s_cand[bw];
-  }
-}
-
 // after round k-1: its winner and centre
 __global__ __launch_bounds__(64) void k_kpp1_final(Kpp1Args a, int c) {
   const int q = c & 1;
@@ -2212,7 +1951,6 @@ __global__ __launch_bounds__(kThr) void k_skl_sqdist(SklPlan p, const float* __r
 }
 
 // ---- host side ------------------------------------------------------------------------------------
-inline int kpp_ld_host(int64_t n) { return (int)(((n + 63) & ~63ll) + 8); }  // = kpp1_ld
 
 int64_t skl_batch_size(int64_t nx, int64_t ny, int dim) {  // pairwise.py _euclidean_distances_upcast
   double maxmem = (double)((nx + ny) * (int64_t)dim + nx * ny) / 10.0;
@@ -2356,6 +2094,10 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   a.indices = indices;
   a.plan = SklPlan{n, skl_batch_size(T, n, dim), T, dim, 0, 0};
   a.plan.all_seq = skl_all_seq(n, T, dim, a.plan.B) ? 1 : 0;
+  {  // cum_tol's mode: GDD_KPP_EXACT=0 (never replay; tests only) / 2 (always replay)
+    const char* ex = getenv("GDD_KPP_EXACT");
+    a.exact = ex ? atoi(ex) : 1;
+  }
   const SklPlan p1{n, skl_batch_size(1, n, dim), 1, dim, 0, 0};
   const size_t lds = sizeof(double) * (size_t)dim + sizeof(float) * kBlk;
   const bool seq = a.plan.all_seq != 0;
@@ -2392,6 +2134,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     b1.centers = centers;
     b1.indices = indices;
     b1.plan = a.plan;
+    b1.exact = a.exact;
     if (seq) {
       k_kpp_xt<<<(unsigned)((n * dim + 255) / 256), 256, 0, s>>>((int)n, dim, X, XT);
       GDD_LAUNCHED();
@@ -2408,20 +2151,6 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       k_kpp_dmat<<<dim3((unsigned)((n + 255) / 256), (unsigned)((n + kDmJ - 1) / kDmJ)), 256, 0, s>>>(
           (int)n, dim, X, XT, xsq, Dm);
       GDD_LAUNCHED();
-      const size_t lds_ps = sizeof(float) * ((size_t)T * kpp_ld_host(n) + kPsPad);
-      if (w == nullptr && T <= kPsTrials && n >= 2 && getenv("GDD_KPP_PERSIST") != nullptr) {
-        // all rounds in one workgroup (opt-in: measured 20-23 us per round at 3000 x 40, k = 454,
-        // against 9.2-9.4 for one launch per round — one CU's LDS and fp64 issue carry all T trials'
-        // chains, prefixes and searches, which T workgroups otherwise run side by side)
-        GDD_HIP(hipFuncSetAttribute((const void*)k_kpp1_persist, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds_ps));
-        k_kpp1_persist<<<1, kPsThr, lds_ps, s>>>(b1, Dm);
-        GDD_LAUNCHED();
-        k_kpp_gather_centres<<<(unsigned)(((int64_t)k * dim + 255) / 256), 256, 0, s>>>(k, dim, X, indices,
-                                                                                         centers);
-        GDD_LAUNCHED();
-        return GDD_OK;
-      }
       const bool plain = getenv("GDD_KPP_CHAIN_PLAIN") != nullptr;
       if (T <= kPairMaxT && getenv("GDD_KPP_SINGLE_ROUND") == nullptr) {
         // two rounds per launch (a trailing odd round alone)

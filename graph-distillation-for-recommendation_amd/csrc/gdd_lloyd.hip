@@ -196,7 +196,8 @@ int group_dev(int64_t n, const int32_t* labels, int k, int32_t* perm, int32_t* o
       default: return go(std::integral_constant<int, 4>());
     }
   }
-  GDD_REQUIRE(!stop, "group_by_label: k=%d too large for the device loop", k);
+  // the radix path does not read the stop word: after a stop it regroups the (unchanged) labels
+  // into the workspace, which nothing reads any more
   int32_t* iota = cv.take<int32_t>(n);
   int32_t* skeys = cv.take<int32_t>(n);
   const size_t sb = sort_pairs_ws_bytes(n);
@@ -433,8 +434,25 @@ __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
   }
 }
 
-// clusters [a0.c0, a0.c0 + count)
+// clusters [a0.c0, a0.c0 + count): launches of at most kFoldMaxGridY clusters (grid.y), each
+// writing its slice of the outputs
+constexpr int kFoldMaxGridY = 65535;
+int fold_launch_one(const FoldArgs& a0, int count, bool mean, hipStream_t s);
 int fold_launch(const FoldArgs& a0, int count, bool mean, hipStream_t s) {
+  GDD_REQUIRE(count >= 0, "cluster fold: %d clusters", count);
+  for (int off = 0; off < count; off += kFoldMaxGridY) {
+    FoldArgs a = a0;
+    a.c0 = a0.c0 + off;
+    a.out = a0.out + (int64_t)off * a0.dim;
+    if (a0.wsum) a.wsum = a0.wsum + off;
+    if (a0.counts) a.counts = a0.counts + off;
+    const int rc = fold_launch_one(a, std::min(kFoldMaxGridY, count - off), mean, s);
+    if (rc) return rc;
+  }
+  return GDD_OK;
+}
+
+int fold_launch_one(const FoldArgs& a0, int count, bool mean, hipStream_t s) {
   FoldArgs a = a0;
   const bool weighted = a.w != nullptr;
   a.fw_max = std::min(a.dim, weighted ? 192 : 256);  // weighted: thread 255 folds the weights
@@ -445,7 +463,6 @@ int fold_launch(const FoldArgs& a0, int count, bool mean, hipStream_t s) {
   a.R = std::max(R, 16);
   const bool vec = a.dim % 4 == 0 && a.fw_max % 4 == 0 && (reinterpret_cast<uintptr_t>(a.X) & 15) == 0;
   const unsigned nsl = (unsigned)((a.dim + a.fw_max - 1) / a.fw_max);
-  GDD_REQUIRE(count >= 0 && count < 65536, "cluster fold: %d clusters per launch", count);
   if (count == 0) return GDD_OK;
   const size_t lds = sizeof(float) * (2 * (size_t)elems + 3 * (size_t)a.R * (weighted ? 2 : 1));
   dim3 grid(nsl, (unsigned)count);
@@ -739,7 +756,7 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
                                     int it0, int resume, int max_iter, double tol, void* state,
                                     int32_t* out_done, int32_t* out_reason, void* ws, size_t ws_bytes,
                                     void* host_ws, size_t host_ws_bytes, gdd_stream_t stream) {
-  GDD_REQUIRE(n > 0 && dim > 0 && dim <= 512 && k > 0 && k <= kCountMaxK && X && C0 && C1 && labels &&
+  GDD_REQUIRE(n > 0 && dim > 0 && dim <= 512 && k > 0 && X && C0 && C1 && labels &&
                   labels_old && wsum && shift && state && out_done && out_reason && ws && host_ws,
               "kmeans_lloyd_run: bad arguments");
   GDD_REQUIRE(it0 >= 0 && it0 <= max_iter && max_iter < (INT_MAX / 2 - 2), "kmeans_lloyd_run: bad iteration range");
@@ -790,7 +807,14 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
   };
   // chunks of iterations enqueued ahead of the decision; the host reads the state of chunk c while
   // chunk c+1 runs (two pinned slots, one event each)
-  hipEvent_t ev[2];
+  struct EvPair {  // destroyed on every return, including the GDD_HIP early ones below
+    hipEvent_t e[2] = {nullptr, nullptr};
+    ~EvPair() {
+      for (hipEvent_t x : e)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } evs;
+  hipEvent_t* ev = evs.e;
   GDD_HIP(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
   GDD_HIP(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
   int rc = GDD_OK;
@@ -828,8 +852,6 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
     const hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess) rc = fail((int)e, "kmeans_lloyd_run: %s", hipGetErrorString(e));
   }
-  (void)hipEventDestroy(ev[0]);
-  (void)hipEventDestroy(ev[1]);
   if (rc) return rc;
   if (!stop) done = max_iter;  // ran out of iterations (sklearn's loop end)
   *out_done = done;

@@ -7,8 +7,7 @@ Drop-in for (same names, argument meaning and return structure):
 * ``utils_clustgdd.attaw_ER_estimator(adj, ebd, src, dst)`` (:162-182) — :func:`attaw_ER_estimator`;
 * ``ClustGDD.graph_sparse(adj, ratio, ebd, sp_type)`` (clustgdd_agent_transduct.py:131-232,
   clustgdd_agent_induct.py:156-256) — :func:`graph_sparse`, sp_type 'vanilla', 'attaw', 'single'
-  and 'no_sp' ('rand' draws from torch's global generator through ``torch.randperm`` on the host;
-  it is not on the distillation path and raises);
+  'no_sp' and 'rand' (uniform edge samples from torch's global CPU generator, as the reference);
 * ``ClustGDD.graph_compress(cluster_labels, adj_norm, adj_list)`` (:234-250, induct :258-274) —
   :func:`graph_compress`, returning torch sparse COO tensors like the reference's ``.to_sparse()``.
 
@@ -135,10 +134,20 @@ def graph_sparse(adj, ratio: float, ebd: Optional[torch.Tensor] = None,
     adj = _csr(adj)
     if sp_type == "no_sp":
         return [adj]
-    if sp_type == "rand":
-        raise NotImplementedError("sp_type='rand' draws torch.randperm on the host generator; "
-                                  "it is not part of the distillation path")
     m = int(adj.nnz * ratio)
+    if sp_type == "rand":
+        # per class a uniform edge sample: torch.randperm on torch's global CPU generator (the
+        # reference's call, on whatever device it runs), the first m edges carrying their
+        # ER_estimator weight ("tried version", :208-222); the edge set is rebuilt in CSR order
+        if ebd is None:
+            raise ValueError("sp_type='rand' needs the embeddings (one graph per class)")
+        er = ER_estimator(adj)
+        out = []
+        for _ in range(int(ebd.shape[-1])):
+            pick = torch.randperm(adj.nnz)[:m]
+            sel = torch.sort(pick).values.to(device=adj.device, dtype=torch.int32)
+            out.append(select_graph(adj, sel, er))
+        return out
     if sp_type == "vanilla":
         er = ER_estimator(adj)
         return [select_graph(adj, topk_edges(adj, er, m)[0], adj.values())]

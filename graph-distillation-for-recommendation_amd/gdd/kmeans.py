@@ -251,7 +251,9 @@ class MiniBatchKMeans(_BaseKMeans):
         # loop stops and leaves the per-sample distances in `sq`; their inertia (a sequential fp32
         # fold bound by its add chain) runs on a side stream, read on first access of inertia_
         from .sharded import world_of
-        sharded = self.compute_labels and world_of(self.group)[1] > 1
+        # only an explicit group shards: with group=None a process in some other job's default
+        # group (e.g. a DDP run clustering per rank) fits on its own data
+        sharded = self.compute_labels and self.group is not None and world_of(self.group)[1] > 1
         native_labels = self.compute_labels and not sharded
         labels = sq = None
         if native_labels:

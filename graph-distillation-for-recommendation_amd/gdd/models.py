@@ -281,3 +281,25 @@ class MLP(_Trainable):
         if features is not None:
             self.features = features
         return self.forward(self.features, mode)
+
+
+class MLP_Induct(MLP):
+    """models/gcn.py MLP_Induct (:705-861): the inductive agent's MLP — trained on the train role's
+    features and labels, validated on the val role's (its own sub-graph), no per-100-epoch print."""
+
+    def fit_with_val(self, feat_train, labels_train, feat_val, labels_val, train_iters=200,
+                     initialize=True, **kwargs):
+        if initialize:
+            self.initialize()
+        feat_train = _feat(feat_train, self.device)
+        feat_val = _feat(feat_val, self.device)
+        labels_train = self._set_labels(labels_train.to(self.device))
+        labels_val = labels_val.to(self.device)
+        labels_val = labels_val.float() if self.multi_label else labels_val
+        self._best_val_loop(lambda: self.loss(self.forward(feat_train), labels_train),
+                            lambda: self.forward(feat_val), labels_val, None, train_iters)
+
+    @torch.no_grad()
+    def predict(self, feat_test, mode="t"):
+        self.eval()
+        return self.forward(feat_test, mode)

@@ -389,12 +389,37 @@ class RecallEvaluator:
             return 0.0
         lib = _lib.device_lib()
         scores = (user_emb[self.users_t] @ item_emb.t()).float().contiguous()  # [B, I] (:475-476)
+        if self.k > _RECALL_KERNEL_MAX_K:
+            return self._sorted_hits(scores)
         hits = torch.zeros(1, dtype=torch.int64, device=self.device)
         _lib.check(lib.gdd_recall_at_k(int(self.users.size), self.num_items, self.k, scores.data_ptr(),
                                        self.tr_ptr.data_ptr(), _lib.ptr(self.tr_col),
                                        self.te_ptr.data_ptr(), _lib.ptr(self.te_col), hits.data_ptr(),
                                        _lib.stream_ptr(self.device)))
         return float(int(hits.item()) / max(1, self.total))
+
+    def _sorted_hits(self, scores: torch.Tensor, chunk: int = 1024) -> float:
+        """k above gdd_recall_at_k's one-pick-per-thread limit: the same mask, then a stable
+        descending sort per user (equal scores keep ascending item order, the kernel's rule) and the
+        hits among the first k, in chunks of users."""
+        B, I = scores.shape
+        tr_row = torch.repeat_interleave(torch.arange(B, device=self.device),
+                                         (self.tr_ptr[1:] - self.tr_ptr[:-1]).long())
+        scores[tr_row, self.tr_col.long()] = -1e9
+        te_row = torch.repeat_interleave(torch.arange(B, device=self.device),
+                                         (self.te_ptr[1:] - self.te_ptr[:-1]).long())
+        hits = torch.zeros((), dtype=torch.int64, device=self.device)
+        for b0 in range(0, B, chunk):
+            b1 = min(B, b0 + chunk)
+            top = torch.sort(scores[b0:b1], dim=1, descending=True, stable=True).indices[:, :self.k]
+            truth = torch.zeros((b1 - b0, I), dtype=torch.bool, device=self.device)
+            sel = (te_row >= b0) & (te_row < b1)
+            truth[te_row[sel] - b0, self.te_col[sel].long()] = True
+            hits += truth.gather(1, top).sum()
+        return float(int(hits.item()) / max(1, self.total))
+
+
+_RECALL_KERNEL_MAX_K = 256  # gdd_recall_at_k: one pick per thread of a 256-thread workgroup
 
 
 def recall_at_k(user_emb: torch.Tensor, item_emb: torch.Tensor, train_R, test_u, test_i, k: int,

@@ -211,6 +211,19 @@ def kmeans_plusplus(X, k: int, rs: np.random.RandomState, n_local_trials=None):
     return centers, idx
 
 
+def kmeans_plusplus_draws(X, k: int, T: int, first: int, u, w=None):
+    """_kmeans_plusplus with the draws given: the first centre's index and the (k-1)*T uniforms
+    (sklearn/cluster/_kmeans.py:226-268; cumsum strictly left to right, as np.cumsum)."""
+    X = _c(X, np.float32)
+    n, dim = X.shape
+    wp = None if w is None else _c(w, np.float32)
+    centers = np.empty((k, dim), np.float32)
+    idx = np.empty(k, np.int64)
+    lib().oracle_kmeans_plusplus(n, dim, X, None if wp is None else wp.ctypes.data, k, T, int(first),
+                                 _c(u, np.float64), centers, idx)
+    return centers, idx
+
+
 # ------------------------------------------------------------------------------------------------
 # MiniBatchKMeans.fit (sklearn/cluster/_kmeans.py:2046-2200), one OpenMP thread
 # ------------------------------------------------------------------------------------------------

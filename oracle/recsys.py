@@ -72,3 +72,45 @@ def recall(user_emb: np.ndarray, item_emb: np.ndarray, tr_indptr, tr_indices, te
         hit += len(truth & set(top.tolist()))
         total += len(truth)
     return hit / max(1, total)
+
+
+def recall_bounds(user_emb: np.ndarray, item_emb: np.ndarray, tr_indptr, tr_indices, test_u, test_i,
+                  k: int, max_users: int = 5000, scores=None, rel_tie: float = 0.0):
+    """[min, max] of recall_at_k (:446-497) over every order torch.topk could give equal scores.
+
+    Per user the top k are every item scored above the k-th score s_k plus m of the items scored
+    s_k (the boundary group, g items of which h are test items): a tie order can place between
+    max(0, m - (g - h)) and min(m, h) test items in those m slots. rel_tie > 0 widens the group to
+    scores within rel_tie * |s_k| of s_k, for embeddings that drifted from the reference's by fp32
+    rounding (two distinct scores that close can swap between the runs). Returns (lo, hi, groups):
+    groups = the number of users whose boundary group holds more than m items (0: the value is
+    unique, lo == hi)."""
+    test_u, test_i = np.asarray(test_u, np.int64), np.asarray(test_i, np.int64)
+    users = np.unique(test_u)[:max_users]
+    if users.size == 0:
+        return 0.0, 0.0, 0
+    S = (user_emb[users] @ item_emb.T).astype(np.float32) if scores is None else scores.copy()
+    n_items = S.shape[1]
+    lo = hi = total = groups = 0
+    for r, uu in enumerate(users):
+        S[r, tr_indices[tr_indptr[uu]:tr_indptr[uu + 1]]] = np.float32(-1e9)
+        truth = np.zeros(n_items, bool)
+        tl = test_i[test_u == uu]
+        truth[tl] = True
+        total += len(set(tl.tolist()))
+        if k >= n_items:
+            lo += int(truth.sum())
+            hi += int(truth.sum())
+            continue
+        s = S[r].astype(np.float64)
+        sk = np.sort(s)[::-1][k - 1]
+        tol = rel_tie * abs(sk)
+        above = s > sk + tol
+        grp = np.abs(s - sk) <= tol
+        m = k - int(above.sum())
+        g, h = int(grp.sum()), int((grp & truth).sum())
+        ha = int((above & truth).sum())
+        lo += ha + max(0, m - (g - h))
+        hi += ha + min(m, h)
+        groups += g > m
+    return lo / max(1, total), hi / max(1, total), groups

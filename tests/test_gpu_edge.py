@@ -103,3 +103,53 @@ def test_stream_copy_exact(nbytes):
     torch.cuda.synchronize()
     m = nbytes // 4
     assert torch.equal(src[:m], dst[:m]) and int(dst[m:].abs().sum()) == 0
+
+
+def test_cluster_mean_more_clusters_than_one_launch():
+    # k above the 65,535 clusters one fold launch's grid.y holds: the launches are chunked, each
+    # writing its slice of the means and counts
+    n, d, k = 200_000, 4, 70_001
+    feat = synth.features(n, d, 8)
+    lab = np.random.default_rng(3).integers(0, k, n).astype(np.int32)
+    lab[:5] = k - 1
+    ref, cnt_ref = O.cluster_mean(feat, lab, k)
+    out, cnt = gdd.cluster_mean(torch.from_numpy(feat).cuda(), lab, k)
+    assert np.array_equal(cnt.cpu().numpy(), cnt_ref)
+    o = out.cpu().numpy()
+    assert np.array_equal(np.isnan(o), np.isnan(ref))
+    m = ~np.isnan(ref)
+    assert np.array_equal(bits(o[m]), bits(ref[m]))
+
+
+def test_lloyd_run_k_above_counting_sort():
+    # k > 32,768: the device Lloyd loop groups the labels with the radix path (no LDS counters).
+    # One iteration from given centres (distinct data points, so no cluster is empty) against the
+    # oracle's _lloyd_iter: labels, new centres, weights and shifts bit for bit.
+    from gdd import _lib
+    import ctypes
+    n, dim, k = 34_000, 2, 33_000
+    X = np.random.default_rng(11).standard_normal((n, dim)).astype(np.float32)
+    C0 = X[:k].copy()
+    lab_ref, c_ref, wic_ref, shift_ref = O._lloyd_iter(X, C0)
+    lib = _lib.device_lib()
+    dev = torch.device("cuda")
+    Xd = torch.from_numpy(X).to(dev)
+    Cb = (torch.from_numpy(C0).to(dev), torch.empty((k, dim), dtype=torch.float32, device=dev))
+    labels = torch.empty(n, dtype=torch.int32, device=dev)
+    labels_old = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    wic = torch.empty(k, dtype=torch.float32, device=dev)
+    shift = torch.empty(k, dtype=torch.float32, device=dev)
+    ws = _lib.workspace(lib.gdd_kmeans_lloyd_ws_bytes(n, dim, k), dev)
+    hws = _lib.pinned_workspace(lib.gdd_kmeans_lloyd_host_ws_bytes())
+    state = torch.zeros(lib.gdd_lloyd_state_bytes(), dtype=torch.uint8, device=dev)
+    done, reason = ctypes.c_int32(0), ctypes.c_int32(0)
+    _lib.check(lib.gdd_kmeans_lloyd_run(n, dim, Xd.data_ptr(), k, Cb[0].data_ptr(), Cb[1].data_ptr(),
+                                        labels.data_ptr(), labels_old.data_ptr(), wic.data_ptr(),
+                                        shift.data_ptr(), 0, 0, 1, 0.0, state.data_ptr(),
+                                        ctypes.addressof(done), ctypes.addressof(reason), ws.data_ptr(),
+                                        ws.numel(), hws.data_ptr(), hws.numel(), _lib.stream_ptr(dev)))
+    assert done.value == 1 and reason.value == 0
+    assert np.array_equal(labels.cpu().numpy(), lab_ref)
+    assert np.array_equal(bits(wic.cpu().numpy()), bits(wic_ref))
+    assert np.array_equal(bits(Cb[1].cpu().numpy()), bits(c_ref))
+    assert np.array_equal(bits(shift.cpu().numpy()), bits(shift_ref))

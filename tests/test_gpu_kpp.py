@@ -111,14 +111,113 @@ def test_kmeans_plusplus_two_launch_path(monkeypatch):
 def test_kmeans_plusplus_round_forms(monkeypatch, n, dim, k):
     """Every single-block round form gives the oracle's seeding, bit for bit: two rounds per launch
     over the distance table (default for plain-chain plans, dim <= 48, k >= 16, T <= 8), one round
-    per launch over the table (GDD_KPP_SINGLE_ROUND), the one-workgroup persistent rounds over the
-    table (GDD_KPP_PERSIST, T <= 8), and the fused distance + fold rounds (GDD_KPP_NO_TABLE)."""
+    per launch over the table (GDD_KPP_SINGLE_ROUND), and the fused distance + fold rounds
+    (GDD_KPP_NO_TABLE)."""
     X = np.ascontiguousarray(synth.blobs(n, dim, max(2, k // 4), seed=n + dim + 1), np.float32)
     c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
-    for var in (None, "GDD_KPP_SINGLE_ROUND", "GDD_KPP_PERSIST", "GDD_KPP_NO_TABLE"):
+    for var in (None, "GDD_KPP_SINGLE_ROUND", "GDD_KPP_NO_TABLE"):
         if var:
             monkeypatch.setenv(var, "1")
         ops = _Ops("cuda", n, k, dim)
         c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(15))
         assert np.array_equal(idx.cpu().numpy(), idx_ref), var
         assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref)), var
+
+
+# ---- the cumulative potential: numpy's left-to-right fp64 cumsum, exactly ---------------------------
+def adversarial_points(n):
+    """1-D points whose distances to the first centre (x = 0, index 0) are [0, 1, s, ..., s, 1, 1]
+    with s = 2^-58: numpy's sequential fp64 cumsum absorbs every s into the leading 1, while any
+    blocked evaluation adds the s's together first and climbs past 1 + 2^-52 (kernel prefix trees)."""
+    X = np.full((n, 1), 2.0 ** -29, np.float32)
+    X[0], X[1], X[n - 2], X[n - 1] = 0.0, -1.0, -1.0, 1.0
+    return X
+
+
+def adversarial_uniforms(k, T, rnd):
+    """Round `rnd`'s trial 0 draws r = u * pot = 1 + 2^-48 (pot = 3 in round 1; 2 in round 2 once
+    the point +1 is a centre): numpy's index is the second -1 point (n - 2); a blocked prefix says
+    an s entry. The other draws are ordinary (round 1's near 1: the +1 point)."""
+    u = np.random.RandomState(k + T).uniform(size=(k - 1, T))
+    u[0, :] = 0.9999
+    u[rnd - 1, 0] = (1.0 + 2.0 ** -48) / (3.0 if rnd == 1 else 2.0)
+    return u.ravel()
+
+
+def _kpp_dev(X, k, T, first, u, w=None):
+    lib = _lib.device_lib()
+    n, dim = X.shape
+    Xd = torch.from_numpy(X).cuda()
+    ud = torch.from_numpy(np.ascontiguousarray(u, np.float64)).cuda()
+    wd = None if w is None else torch.from_numpy(w).cuda()
+    centers = torch.empty((k, dim), dtype=torch.float32, device="cuda")
+    idx = torch.empty(k, dtype=torch.int64, device="cuda")
+    ws = _lib.workspace(lib.gdd_kmeans_plusplus_ws_bytes(n, dim, T), Xd.device)
+    _lib.check(lib.gdd_kmeans_plusplus(n, dim, Xd.data_ptr(), _lib.ptr(wd), k, T, first, ud.data_ptr(),
+                                       centers.data_ptr(), idx.data_ptr(), ws.data_ptr(), ws.numel(),
+                                       _lib.stream_ptr(Xd.device)))
+    torch.cuda.synchronize()
+    return centers.cpu().numpy(), idx.cpu().numpy()
+
+
+# (n, env): every search form — the pick count (round 0 of the single-block paths and the two-launch
+# rounds), the fold's binary search (table pair / single rounds, fused rounds), the multi-block
+# round (per-(block, trial) and the split pick launch)
+CUMSUM_FORMS = [
+    (1000, ()), (4096, ()), (1000, ("GDD_KPP_SINGLE_ROUND",)), (1000, ("GDD_KPP_NO_TABLE",)),
+    (1000, ("GDD_KPP_NO_TABLE", "GDD_KPP_TWO_LAUNCH")), (9000, ()), (530000, ()),
+]
+
+
+@pytest.mark.parametrize("rnd", [1, 2])
+@pytest.mark.parametrize("n,env", CUMSUM_FORMS)
+def test_kpp_cumsum_adversarial(monkeypatch, n, env, rnd):
+    """A draw that lands between numpy's sequential cumulative potential and the kernels' blocked
+    one. With the rounding check (default) and with the replay forced on every draw the seeding is
+    numpy's; with the check disabled (GDD_KPP_EXACT=0) it is not — so the case is adversarial for
+    that form and the check is what makes it exact."""
+    k, T = 16, 4
+    X = adversarial_points(n)
+    u = adversarial_uniforms(k, T, rnd)
+    c_ref, idx_ref = O.kmeans_plusplus_draws(X, k, T, 0, u)
+    assert idx_ref[rnd] == n - 2
+    for var in env:
+        monkeypatch.setenv(var, "1")
+    for mode in ("1", "2"):
+        monkeypatch.setenv("GDD_KPP_EXACT", mode)
+        c, idx = _kpp_dev(X, k, T, 0, u)
+        assert np.array_equal(idx, idx_ref), (mode, idx[:4], idx_ref[:4])
+        assert np.array_equal(bits(c), bits(c_ref)), mode
+    monkeypatch.setenv("GDD_KPP_EXACT", "0")
+    _, idx = _kpp_dev(X, k, T, 0, u)
+    assert idx[rnd] != idx_ref[rnd], "the blocked prefix did not cross the threshold"
+
+
+@pytest.mark.parametrize("n", [1000, 9000])
+def test_kpp_cumsum_adversarial_weighted(monkeypatch, n):
+    """The same with sample weights (w * closest in fp32, then the fp64 sum)."""
+    k, T = 16, 4
+    X = adversarial_points(n)
+    w = np.ones(n, np.float32)
+    w[1] = 0.5
+    w[n - 2] = 2.0
+    u = adversarial_uniforms(k, T, 1)
+    u[0] = (0.5 + 2.0 ** -49) / 3.5  # w * closest = [0, 0.5, s, ..., s, 2, 1]
+    c_ref, idx_ref = O.kmeans_plusplus_draws(X, k, T, 0, u, w=w)
+    assert idx_ref[1] == n - 2
+    monkeypatch.setenv("GDD_KPP_EXACT", "1")
+    c, idx = _kpp_dev(X, k, T, 0, u, w=w)
+    assert np.array_equal(idx, idx_ref)
+    assert np.array_equal(bits(c), bits(c_ref))
+
+
+@pytest.mark.parametrize("n,dim,k", [(3000, 40, 454), (9000, 8, 60), (2708, 7, 70)])
+def test_kpp_replay_every_draw(monkeypatch, n, dim, k):
+    """GDD_KPP_EXACT=2 replays numpy's cumsum for every draw: the seeding must not change."""
+    X = np.ascontiguousarray(synth.blobs(n, dim, max(2, k // 4), seed=n + dim + 5), np.float32)
+    c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
+    monkeypatch.setenv("GDD_KPP_EXACT", "2")
+    c, idx = _Ops("cuda", n, k, dim).kmeans_plusplus(torch.from_numpy(X).cuda(), k,
+                                                     np.random.RandomState(15))
+    assert np.array_equal(idx.cpu().numpy(), idx_ref)
+    assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref))

@@ -118,10 +118,16 @@ def test_recall_at_k_device_vs_reference_and_oracle():
                            "cuda", max_users=250)
     ro = R.recall(ue, ie, Rtr.indptr, Rtr.indices, tu, ti, 20, max_users=250)
     assert r == ro
-    assert abs(r - float(z["r1_recall"])) <= 0.05
+    # the reference's value is one of the tie orders: inside the exact [min, max] over all of them
+    lo, hi, groups = R.recall_bounds(ue, ie, Rtr.indptr, Rtr.indices, tu, ti, 20, max_users=250)
+    assert groups > 0 and lo <= float(z["r1_recall"]) <= hi and lo <= r <= hi
+    ue, ie, Rtr, tu, ti = _recall_inputs(z, "r0")
+    lo, hi, groups = R.recall_bounds(ue, ie, Rtr.indptr, Rtr.indices, tu, ti, 20, max_users=250)
+    assert groups == 0 and lo == hi == float(z["r0_recall"])
 
 
-@pytest.mark.parametrize("k,max_users", [(1, 5000), (7, 13), (64, 5000)])
+@pytest.mark.parametrize("k,max_users", [(1, 5000), (7, 13), (64, 5000), (256, 5000), (300, 77), (699, 9),
+                                         (2000, 50)])
 def test_recall_at_k_device_vs_oracle_shapes(k, max_users):
     import scipy.sparse as sp
     rng = np.random.default_rng(k)
@@ -135,11 +141,41 @@ def test_recall_at_k_device_vs_oracle_shapes(k, max_users):
     assert r == R.recall(ue, ie, tr.indptr, tr.indices, tu, ti, k, max_users=max_users)
 
 
-def test_distill_recsys_driver_vs_reference(tmp_path, capsys):
+# scores within this relative distance of a user's k-th score count as tied when bounding the
+# reference's Recall from this run's embeddings: they follow the reference's within fp32 drift (losses
+# agree to 2e-5 after 6 Adam steps), so two distinct scores that close may swap between the runs
+RECALL_REL_TIE = 1e-4
+
+
+def _recording_evaluator(monkeypatch):
+    """Wraps RecallEvaluator.__call__ to keep each evaluation's inputs (users' and items' embeddings)
+    and the oracle's tie bounds for them."""
+    seen = []
+    orig = recsys.RecallEvaluator.__call__
+
+    def call(self, ue, ie):
+        v = orig(self, ue, ie)
+        u, i = ue.detach().cpu().numpy(), ie.detach().cpu().numpy()
+        tr = __import__("scipy.sparse").sparse.csr_matrix(
+            (np.ones(self.tr_col.numel(), np.float32), self.tr_col.cpu().numpy(), self.tr_ptr.cpu().numpy()),
+            shape=(self.users.size, self.num_items))
+        te_ptr, te_col = self.te_ptr.cpu().numpy(), self.te_col.cpu().numpy()
+        tu = np.repeat(self.users, np.diff(te_ptr))
+        ue_rows = u[self.users]  # the evaluated users, in order: rows 0.. of tr
+        seen.append((v, R.recall_bounds(ue_rows, i, tr.indptr, tr.indices, np.searchsorted(self.users, tu),
+                                        te_col, self.k, rel_tie=RECALL_REL_TIE)))
+        return v
+    monkeypatch.setattr(recsys.RecallEvaluator, "__call__", call)
+    return seen
+
+
+def test_distill_recsys_driver_vs_reference(tmp_path, capsys, monkeypatch):
     """gdd.distill_recsys.run with the reference's flags on the dataset main() ran on (G11): the
     clustering, condensed graph and sampler draws are exact; the losses follow the reference's within
-    fp32 drift (SpMM vs index_add_ order, 6 Adam steps); Recall@20 within tie resolution."""
+    fp32 drift (SpMM vs index_add_ order, 6 Adam steps); every Recall@20 the reference printed lies in
+    the oracle's [min, max] over the tie orders of this run's scores (RECALL_REL_TIE)."""
     from gdd import distill_recsys as D
+    seen = _recording_evaluator(monkeypatch)
     z = load("golden_refine.npz")
     lines = open(__import__("golden_util").GOLDEN + "/golden_refine_stdout.txt").read().splitlines()
     argv = lines[0].split()
@@ -154,13 +190,19 @@ def test_distill_recsys_driver_vs_reference(tmp_path, capsys):
     ref = [l for l in lines[1:] if not l.startswith("[env]")]
     got = [l for l in got if not l.startswith("[env]")]
     assert len(got) == len(ref)
+    evals = iter(seen)
+
+    def in_bounds(gv, rv):  # printed with 6 decimals
+        v, (lo, hi, _) = next(evals)
+        assert abs(gv - v) <= 5e-7 and lo - 5e-7 <= v <= hi + 5e-7
+        assert lo - 5e-7 <= rv <= hi + 5e-7, (rv, lo, hi)
     for g, r in zip(got, ref):
         if g.startswith("[refine] ep="):
             gl, rl = float(g.split("loss=")[1].split()[0]), float(r.split("loss=")[1].split()[0])
             assert g.split()[1] == r.split()[1] and abs(gl - rl) <= 2e-5, (g, r)
-            assert abs(float(g.rsplit("=", 1)[1]) - float(r.rsplit("=", 1)[1])) <= 0.05, (g, r)
+            in_bounds(float(g.rsplit("=", 1)[1]), float(r.rsplit("=", 1)[1]))
         elif g.startswith("[eval]"):
-            assert abs(float(g.rsplit(" ", 1)[1]) - float(r.rsplit(" ", 1)[1])) <= 0.05, (g, r)
+            in_bounds(float(g.rsplit(" ", 1)[1]), float(r.rsplit(" ", 1)[1]))
         elif g.startswith("[save]"):
             assert g.endswith("distilled_recsys/synth")
         else:

@@ -171,3 +171,41 @@ def test_pretrained_clustering_induct_vs_reference(tag):
 def test_induced_subgraph_rejects_unsorted():
     with pytest.raises(ValueError):
         O.induced_subgraph(np.array([0, 1, 2, 3]), np.array([1, 0, 2]), None, [2, 1])
+
+
+class _InjectedDraws(np.random.RandomState):
+    """A RandomState whose `choice` returns a fixed first centre and whose `uniform` hands out given
+    rows: scikit-learn's _kmeans_plusplus then runs on chosen draws."""
+
+    def __init__(self, first, u_rows):
+        super().__init__(0)
+        self._first, self._rows = first, list(u_rows)
+
+    def choice(self, *a, **kw):
+        return self._first
+
+    def uniform(self, *a, **kw):
+        return self._rows.pop(0)
+
+
+@pytest.mark.parametrize("rnd", [1, 2])
+@pytest.mark.parametrize("n", [1000, 9000])
+def test_kmeans_plusplus_cumsum_adversarial_vs_sklearn(n, rnd):
+    # 1-D points with distances [0, 1, s, ..., s, 1, 1] (s = 2^-58) to the first centre: numpy's
+    # sequential fp64 cumsum absorbs every s, a blocked one would not. The draw r = 1 + 2^-48 in
+    # round `rnd` sits between the two (tests/test_gpu_kpp.py runs the device on the same draws);
+    # scikit-learn picks the second -1 point (index n - 2), and so must the oracle.
+    from sklearn.cluster import _kmeans as K
+    from sklearn.utils.extmath import row_norms
+    k, T = 16, 4
+    X = np.full((n, 1), 2.0 ** -29, np.float32)
+    X[0], X[1], X[n - 2], X[n - 1] = 0.0, -1.0, -1.0, 1.0
+    u = np.random.RandomState(k + T).uniform(size=(k - 1, T))
+    u[0, :] = 0.9999
+    u[rnd - 1, 0] = (1.0 + 2.0 ** -48) / (3.0 if rnd == 1 else 2.0)
+    ci, ii = K._kmeans_plusplus(X, k, row_norms(X, squared=True), np.ones(n, np.float32),
+                                _InjectedDraws(0, u), n_local_trials=T)
+    co, io = O.kmeans_plusplus_draws(X, k, T, 0, u.ravel())
+    assert ii[rnd] == n - 2
+    assert np.array_equal(ii, io)
+    assert np.array_equal(bits(ci), bits(co))

@@ -34,6 +34,11 @@ setting in which its Lloyd M-step merge order is deterministic.
                            distilled graph, the torch RNG state before the GCN runs and the five
                            [train, test] accuracies. The agents call .cuda() in test_with_val; the
                            generator maps Tensor.cuda to the CPU for this run (no arithmetic change)
+  G12 golden_agent_induct_{flickr,reddit}.npz  the reference inductive agent end to end on the CPU
+                           (clustgdd_agent_induct.ClustGDD.train on DataGraphSAINT files: KMeans /
+                           MiniBatchKMeans, graph_sparse('attaw'), graph_compress, the reweighted
+                           graph_refusion, 5 x test_with_val), with the refusion inputs and both
+                           torch RNG states captured, and stdout
   G8 golden_recsys.npz     distill_recsys.build_condensed_bipartite on synthetic interactions (with
                            empty super-nodes), condensed_csr_to_edge_index, and LightGCNCondensed
                            (propagate outputs, bpr_loss and every parameter gradient) on CPU
@@ -474,6 +479,137 @@ def g7_induct(dataset):
     np.savez_compressed(os.path.join(OUT, f"golden_clustgdd_induct_{dataset}.npz"), **out)
 
 
+def _saint_files(tmp, dataset, n, d, C, seed):
+    """A small GraphSAINT-format dataset (adj_full.npz, feats.npy, role.json, class_map.json) under
+    tmp/data/<dataset>; returns the raw arrays."""
+    rng = np.random.default_rng(seed)
+    labels = rng.integers(0, C, n)
+    mu = rng.standard_normal((C, d)) * 0.4  # overlapping classes: accuracies well below 1
+    feat = (mu[labels] + rng.standard_normal((n, d)) * 1.2 + 3.0).astype(np.float32)
+    src = rng.integers(0, n, 6 * n)
+    same = rng.random(6 * n) < 0.8
+    dst = np.where(same, [rng.choice(np.where(labels == labels[s_])[0]) for s_ in src],
+                   rng.integers(0, n, 6 * n))
+    keep = src != dst
+    A = sp.coo_matrix((np.ones(keep.sum(), np.float32), (src[keep], dst[keep])), shape=(n, n))
+    A = sp.csr_matrix(A + A.T)
+    A.data[:] = 1.0
+    A.sort_indices()
+    role_of = rng.choice(3, n, p=[0.5, 0.2, 0.3])
+    role = {"tr": np.where(role_of == 0)[0].tolist(), "va": np.where(role_of == 1)[0].tolist(),
+            "te": np.where(role_of == 2)[0].tolist()}
+    base = os.path.join(tmp, "data", dataset)
+    os.makedirs(base)
+    sp.save_npz(os.path.join(base, "adj_full.npz"), A)
+    np.save(os.path.join(base, "feats.npy"), feat)
+    with open(os.path.join(base, "role.json"), "w") as f:
+        json.dump(role, f)
+    with open(os.path.join(base, "class_map.json"), "w") as f:
+        json.dump({str(i): int(labels[i]) for i in range(n)}, f)
+    return A, feat, labels, role
+
+
+def g12_agent_induct(dataset):
+    """The reference inductive agent (clustgdd_agent_induct.ClustGDD.train) end to end on the CPU on a
+    small GraphSAINT-format dataset, with the flags of main_induct.sh's flickr lines (epochs cut):
+    the k-means input and RNG state, the pre-refusion outputs, graph_refusion's inputs (dense
+    compressed graphs) and torch RNG state, the refined features, the distilled graph, the torch RNG
+    state before the GCN runs, the five [train, test] accuracies and stdout."""
+    import contextlib
+    import io
+    import random
+    import tempfile
+    import torch
+    sys.path.insert(0, REF)
+    import clustgdd_agent_induct as induct
+    import utils_graphsaint as saint
+    from gdd.train_clustgdd_induct import parser
+    argv = ["--dataset", dataset, "--reduction_rate", "0.05", "--prop_num", "2", "--postprop_num", "2",
+            "--alpha", "0.8", "--predropout", "0.6", "--sp_ratio", "0.5", "--preep", "100", "--postep",
+            "200", "--frcoe", "0.2", "--predcoe", "0.8", "--w1", "0.8", "--hidden", "64"]
+    args = parser().parse_args(argv)
+    with tempfile.TemporaryDirectory() as tmp:
+        A, feat, labels, role = _saint_files(tmp, dataset, 900, 40, 5, 121 if dataset == "flickr" else 122)
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            data = saint.DataGraphSAINT(dataset)
+        finally:
+            os.chdir(cwd)
+    cap = {}
+    orig = {name: getattr(induct.ClustGDD, name) for name in
+            ("pretrained_clustering", "graph_refusion", "test_with_val")}
+    real_km, real_mb = induct.KMeans, induct.MiniBatchKMeans
+
+    def capture(cls):
+        class Wrapped(cls):
+            def fit(self, X, *a, **kw):
+                cap["kmeans_X"] = np.array(X, np.float32, copy=True)
+                st = np.random.get_state()
+                cap.update(rng_key=st[1], rng_pos=np.int64(st[2]), rng_has_gauss=np.int64(st[3]),
+                           rng_cached_gauss=np.float64(st[4]))
+                return super().fit(X, *a, **kw)
+        return Wrapped
+
+    def pc(self, data_):
+        out = orig["pretrained_clustering"](self, data_)
+        cap.update(feat_syn_pre=out[0].detach().numpy(), labels_syn=out[1].numpy(),
+                   cluster_labels=out[2].numpy(), target_train=out[3].numpy(), target_val=out[6].numpy(),
+                   logits_train=out[8].numpy())
+        r, c, v = coo_sorted(out[4])
+        cap.update(norm_train_row=r, norm_train_col=c, norm_train_val=v)
+        return out
+
+    def gr(self, ttrain, tval, ltrain, lval, feat_syn, graphs, label_syn):
+        cap["refusion_rng_state"] = torch.get_rng_state().numpy().copy()
+        cap["compressed_count"] = np.int64(len(graphs))
+        for q, g in enumerate(graphs):
+            cap[f"compressed{q}"] = g.to_dense().numpy()
+        out = orig["graph_refusion"](self, ttrain, tval, ltrain, lval, feat_syn, graphs, label_syn)
+        cap["feat_syn_refined"] = out.detach().numpy()
+        return out
+
+    runs = []
+
+    def tv(self, i, verbose=True):
+        if not runs:
+            cap["torch_rng_state"] = torch.get_rng_state().numpy().copy()
+        r = orig["test_with_val"](self, i, verbose)
+        runs.append(r)
+        return r
+
+    induct.KMeans, induct.MiniBatchKMeans = capture(real_km), capture(real_mb)
+    induct.ClustGDD.pretrained_clustering = pc
+    induct.ClustGDD.graph_refusion = gr
+    induct.ClustGDD.test_with_val = tv
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    torch.cuda.max_memory_allocated = lambda *a, **k: 0
+    buf = io.StringIO()
+    try:
+        random.seed(args.seed)
+        np.random.seed(args.seed)
+        torch.manual_seed(args.seed)
+        with contextlib.redirect_stdout(buf):
+            agent = induct.ClustGDD(data, args, device="cpu")
+            ret = agent.train()
+    finally:
+        induct.KMeans, induct.MiniBatchKMeans = real_km, real_mb
+        for name, f in orig.items():
+            setattr(induct.ClustGDD, name, f)
+    out = dict(cap)
+    rp, ci, vi = csr_arrays(A)
+    out.update(rowptr=rp, col=ci, val=vi, feat_raw=feat, labels=labels.astype(np.int64),
+               idx_train=np.asarray(role["tr"], np.int64), idx_val=np.asarray(role["va"], np.int64),
+               idx_test=np.asarray(role["te"], np.int64), feat_full=np.asarray(data.feat_full),
+               n_syn=np.int64(agent.nnodes_syn), feat_syn=agent.feat_syn.detach().numpy(),
+               adj_syn=agent.adj_syn.numpy(), labels_syn_final=agent.labels_syn.numpy(),
+               adj_syn_raw=ret[1].to_dense().numpy(), runs=np.asarray(runs, np.float64),
+               argv=json.dumps(argv))
+    np.savez_compressed(os.path.join(OUT, f"golden_agent_induct_{dataset}.npz"), **out)
+    with open(os.path.join(OUT, f"golden_agent_induct_{dataset}_stdout.txt"), "w") as f:
+        f.write(buf.getvalue())
+
+
 def g8_recsys(recsys):
     """The recommender's condensation and LightGCN refinement model (device='cpu')."""
     import torch
@@ -635,6 +771,10 @@ def main():
         if "G7" in which:
             g7_induct("flickr")
             g7_induct("reddit")
+        if "G12" in which:  # patches torch.Tensor.cuda for its own run
+            torch.set_num_threads(1)
+            g12_agent_induct("flickr")
+            g12_agent_induct("reddit")
     with open(os.path.join(OUT, "VERSIONS.json"), "w") as f:
         json.dump({"scikit-learn": sklearn.__version__, "numpy": np.__version__,
                    "scipy": scipy.__version__, "torch": torch.__version__,
