@@ -10,14 +10,19 @@ One *step* = one pass of the hot path of ``ClustGDD.pretrained_clustering``
 
 Synthetic data of the arxiv shape (N=169,343, d=128, ~2.4M nnz Chung-Lu power-law graph, C=40),
 because the dataset cannot be downloaded here. ``value`` = nodes distilled per second over the
-whole job (N x steps / max-over-ranks wall time); ``ms_per_step`` is the distill
-wallclock. Multi-GPU (north star): one process per GPU, all ranks distil the SAME
-graph — normalisation, propagation and the minibatch steps run replicated (the T-hop halo is the
-whole graph; the steps are latency-bound and sequential), the final labels pass is partitioned by
-rows and the cluster means by clusters, each followed by one RCCL all-gather (gdd.sharded); results
-are bit-identical to one GPU. ``value`` counts that one graph (strong scaling).
+whole job (graphs x N x steps / max-over-ranks wall time); ``ms_per_step`` is the distill
+wallclock.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config arxiv] [--no-cpu-baseline]
+Multi-GPU, one process per GPU. The arxiv step does not shard: its T-hop halo is the
+whole graph and MiniBatchKMeans is ~260 latency-bound sequential steps, so ``--mode replicas``
+(default) runs N independent distillations, one graph per GPU (seed + rank), with no collective in
+the data path ("scaling": "weak"). ``--mode one-graph`` distils ONE graph over all ranks as the north
+star partitions it (gdd.sharded: labels pass by rows, cluster means by clusters, RCCL all-gathers,
+bit-identical to one GPU; "scaling": "strong"); at N > 1 the replicas line also carries that mode's
+time for the same graph under ``one_graph``.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config arxiv] [--mode replicas|one-graph]
+                       [--no-cpu-baseline]
 """
 from __future__ import annotations
 
@@ -42,6 +47,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="arxiv")
+    ap.add_argument("--mode", choices=("replicas", "one-graph"), default="replicas")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -80,10 +86,11 @@ def main():
     from gdd import synth
 
     cfg = synth.CONFIGS[args.config]
-    seed = cfg.seed  # every rank holds the same graph
+    one_graph = args.mode == "one-graph"
+    seed = cfg.seed + (0 if one_graph else rank)  # replicas: an independent graph per rank
     dev = torch.device("cuda", local)
     group = None
-    if world > 1:
+    if world > 1 and one_graph:
         import torch.distributed as dist
         group = dist.group.WORLD
     A = synth.chung_lu(cfg.n, cfg.avg_degree, seed)
@@ -98,7 +105,7 @@ def main():
 
     prop_ev = []
 
-    def step(record=False):
+    def step(record=False, group=group):
         gn = gdd.normalize_adj(graph)
         if record:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -132,11 +139,33 @@ def main():
     barrier(world)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    t_max = max_over_ranks(elapsed, world, dev)
+    one_graph_rec = None
+    if world > 1 and not one_graph:
+        # the same graph (rank 0's) distilled over all ranks, for the strong-scaling comparison
         import torch.distributed as dist
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    t_max = float(t.item())
+        if rank != 0:
+            A1 = synth.chung_lu(cfg.n, cfg.avg_degree, cfg.seed)
+            graph_1, X_1 = gdd.to_csr(A1, device=dev), torch.from_numpy(synth.features(cfg.n, cfg.d, cfg.seed)).to(dev)
+            graph, X = graph_1, X_1
+        g_all = dist.group.WORLD
+        for _ in range(args.warmup):
+            step(group=g_all)
+        torch.cuda.synchronize()
+        barrier(world)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step(group=g_all)
+        torch.cuda.synchronize()
+        barrier(world)
+        torch.cuda.synchronize()
+        t1_max = max_over_ranks(time.perf_counter() - t1, world, dev)
+        one_graph_rec = {"ms_per_step": 1e3 * t1_max / args.steps, "value": cfg.n * args.steps / t1_max,
+                         "unit": "nodes/s", "scaling": "strong",
+                         "parallelism": f"one graph over {world} ranks (gdd.sharded)"}
+        if rank != 0:
+            graph, X = gdd.to_csr(A, device=dev), torch.from_numpy(X_h).to(dev)
 
     # per-phase wall times of one more (untimed) step, synchronised between phases (SURVEY §8(d):
     # hot-path wallclock by stage and nodes clustered per second = N / k-means wallclock)
@@ -197,14 +226,14 @@ def main():
 
     out = {
         "metric": "distill wallclock (SpMM+k-means) & test-acc parity, ogbn-arxiv r=0.5% @1-8 GPU",
-        "value": cfg.n * args.steps / t_max,
+        "value": cfg.n * args.steps * (1 if one_graph else world) / t_max,
         "unit": "nodes/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1e3 * t_max / args.steps,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "strong" if one_graph else "weak",
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (Chung-Lu power-law graph + N(0,1) features of the ogbn-arxiv shape; "
@@ -214,9 +243,11 @@ def main():
                                "cluster means",
                    "nodes": cfg.n, "nnz_in": nnz_in, "nnz_norm": nnz, "feat_dim": d,
                    "k": cfg.k,
-                   "parallelism": (f"nodes range-partitioned x{world}: labels pass by rows, cluster "
-                                   "means by clusters (RCCL all-gathers); normalise, propagation "
-                                   "and minibatch steps replicated") if world > 1 else "single GPU",
+                   "parallelism": ("single GPU" if world == 1 else
+                                   (f"one graph over {world} ranks: labels pass by rows, cluster "
+                                    "means by clusters (RCCL all-gathers); normalise, propagation "
+                                    "and minibatch steps replicated") if one_graph else
+                                   f"replicas x{world}: one graph per GPU, no data-path collective"),
                    "kmeans_steps": n_steps_km},
         "phases_ms": phases,
         "nodes_clustered_per_s": cfg.n / (phases["kmeans"] * 1e-3) if phases.get("kmeans") else None,
@@ -229,6 +260,8 @@ def main():
         "cpu_baseline": None,
         "test_acc": test_acc_evidence(),
     }
+    if one_graph_rec is not None:
+        out["one_graph"] = one_graph_rec
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, A, X_h)
     if rank == 0:
@@ -236,6 +269,14 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def max_over_ranks(seconds, world, dev):
+    t = torch.tensor([seconds], dtype=torch.float64, device=dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def copy_peak(dev, nbytes=1 << 30, reps=10):
@@ -316,7 +357,11 @@ def cpu_baseline(cfg, A, X_h):
     """
     import scipy.sparse as sp
     from sklearn.cluster import MiniBatchKMeans
-    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    # the cores this process may run on (affinity mask; os.cpu_count() ignores it) and the OpenMP
+    # share the box sets: the baseline runs min of the two threads (= all the lease's cores)
+    affinity = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS") or 0)
+    threads = min(affinity, omp) if omp else affinity
     torch.set_num_threads(threads)
     try:
         from threadpoolctl import threadpool_limits
@@ -368,7 +413,7 @@ def cpu_baseline(cfg, A, X_h):
         limiter.unregister() if hasattr(limiter, "unregister") else None
     total = t5 - t0
     return {"value": n / total, "unit": "nodes/s", "cores": threads, "kind": "reference-library",
-            "cpu_model": _cpu_model(),
+            "affinity_cpus": affinity, "omp_num_threads": omp or None, "cpu_model": _cpu_model(),
             "sample": (f"one whole step of the reference's CPU path on the bench's graph ({n} nodes): "
                        f"scipy normalize_adj, {cfg.T - 1} torch CPU sparse hops, logits GEMM, sklearn "
                        f"MiniBatchKMeans(k={cfg.k}, b={cfg.batch}, seed {cfg.seed}, {km.n_steps_} steps), "

@@ -1209,39 +1209,6 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 25);
 }
 
-// ---------------------------------------------------------------------------------------------
-// fixed-point per-cluster sums (the order-free sharded variant, gdd/sharded.py)
-// ---------------------------------------------------------------------------------------------
-__global__ void k_segment_sum_fixed(int64_t n, int dim, const float* __restrict__ X,
-                                    const float* __restrict__ w, const int32_t* __restrict__ labels,
-                                    int scale_exp, long long* __restrict__ sums,
-                                    long long* __restrict__ counts) {
-  const int64_t total = n * dim;
-  const double sc = ldexp(1.0, scale_exp);
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = t / dim;
-    const int f = (int)(t - i * dim);
-    const int c = labels[i];
-    const double v = (double)X[t] * (double)(w ? w[i] : 1.0f) * sc;
-    atomicAdd((unsigned long long*)(sums + (int64_t)c * dim + f),
-              (unsigned long long)(long long)__builtin_rint(v));
-    if (f == 0) atomicAdd((unsigned long long*)(counts + c), 1ull);
-  }
-}
-
-__global__ void k_fixed_to_centers(int k, int dim, const long long* __restrict__ sums,
-                                   const long long* __restrict__ counts, int scale_exp,
-                                   float* __restrict__ C) {
-  const int64_t total = (int64_t)k * dim;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(t / dim);
-    const long long cnt = counts[c];
-    if (cnt > 0) C[t] = (float)(ldexp((double)sums[t], -scale_exp) / (double)cnt);
-  }
-}
-
 __global__ void k_point_center_sqdist(int64_t n, int dim, const float* __restrict__ X,
                                       const int32_t* __restrict__ labels,
                                       const float* __restrict__ C, float* __restrict__ out) {
@@ -1729,31 +1696,6 @@ extern "C" int gdd_minibatch_converge(int64_t b, int k, int step_i, int64_t n_sa
   StepWs w = carve_step(ws, ws_bytes, b, k);
   k_mb_converge<<<1, 64, 0, to_hip(stream)>>>(step_i, b, n_samples, max_no_improvement, w.inertia,
                                               static_cast<MBState*>(state));
-  GDD_LAUNCHED();
-  return GDD_OK;
-}
-
-extern "C" int gdd_segment_sum_fixed(int64_t n, int dim, const float* X, const float* w,
-                                     const int32_t* labels, int k, int scale_exp,
-                                     long long* sums_fx, long long* counts, gdd_stream_t stream) {
-  GDD_REQUIRE(n >= 0 && dim > 0 && k > 0 && sums_fx && counts, "segment_sum_fixed: bad arguments");
-  if (n == 0) return GDD_OK;
-  GDD_REQUIRE(X && labels, "segment_sum_fixed: null pointer");
-  const int64_t total = n * dim;
-  const unsigned g = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
-  k_segment_sum_fixed<<<g, 256, 0, to_hip(stream)>>>(n, dim, X, w, labels, scale_exp, sums_fx,
-                                                     counts);
-  GDD_LAUNCHED();
-  return GDD_OK;
-}
-
-extern "C" int gdd_fixed_to_centers(int k, int dim, const long long* sums_fx,
-                                    const long long* counts, int scale_exp, float* centers,
-                                    gdd_stream_t stream) {
-  GDD_REQUIRE(k > 0 && dim > 0 && sums_fx && counts && centers, "fixed_to_centers: bad arguments");
-  const int64_t total = (int64_t)k * dim;
-  k_fixed_to_centers<<<blocks_for(total), 256, 0, to_hip(stream)>>>(k, dim, sums_fx, counts,
-                                                                    scale_exp, centers);
   GDD_LAUNCHED();
   return GDD_OK;
 }

@@ -10,8 +10,11 @@ the reference file:line each entry point replaces):
   ``kmeans_cluster`` / ``teacher_means`` / ``standard_scaler`` (distill_recsys)
 * :mod:`gdd.condense` — ``graph_sparse`` / ``graph_compress`` / ``ER_estimator`` /
   ``attaw_ER_estimator`` (ClustGDD's sparsification and cluster-level graph)
-* :class:`gdd.sharded.ShardedKMeans` — Lloyd over range-partitioned rows on several ranks, one
-  fixed-point all-reduce per iteration (rank-count invariant)
+* :class:`gdd.sharded.ShardedKMeans` — Lloyd on several ranks: the E-step partitioned by rows, the
+  M-step by clusters, all-gathers of the labels and the cluster slices (bit-identical to one GPU)
+* :mod:`gdd.agent` / :mod:`gdd.agent_induct` — the transductive and inductive ClustGDD agents;
+  :mod:`gdd.train_clustgdd_transduct` / :mod:`gdd.train_clustgdd_induct` /
+  :mod:`gdd.distill_recsys` — the drop-in command lines
 """
 from . import _lib  # noqa: F401  (imports torch first, see _lib docstring)
 from . import gcn, pipeline, recsys  # noqa: F401

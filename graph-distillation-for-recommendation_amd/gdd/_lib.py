@@ -71,9 +71,6 @@ SIGNATURES = {
     "gdd_segment_sum_f32": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp]),
     "gdd_segment_sum_f32_part": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
                                           _vp, _vp, _vp]),
-    "gdd_segment_sum_fixed": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _c_int, _c_int, _vp, _vp,
-                                       _vp]),
-    "gdd_fixed_to_centers": (_c_int, [_c_int, _c_int, _vp, _vp, _c_int, _vp, _vp]),
     "gdd_average_centers": (_c_int, [_c_int, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "gdd_point_center_sqdist": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "gdd_relocate_distances": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),

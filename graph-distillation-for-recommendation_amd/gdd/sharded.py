@@ -26,8 +26,6 @@ tests substitute a CPU stand-in with the same methods to run the distributed log
 """
 from __future__ import annotations
 
-import math
-
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -201,6 +199,16 @@ def sharded_cluster_mean(feat, labels, k: int, empty_as_zero: bool = False, grou
 # ------------------------------------------------------------------------------------------------
 # Lloyd KMeans over the ranks
 # ------------------------------------------------------------------------------------------------
+def _iteration_status(wsum, labels, labels_old, shift):
+    """(any empty cluster, labels changed since the last iteration, center shifts as numpy) with
+    one device-to-host copy per iteration."""
+    changed = (torch.ones(1, device=labels.device) if labels_old is None
+               else (labels != labels_old).any().float().reshape(1))
+    h = torch.cat([(wsum == 0).any().float().reshape(1).to(changed.device), changed,
+                   shift.float().reshape(-1).to(changed.device)]).cpu().numpy()
+    return bool(h[0]), bool(h[1]), h[2:].astype(np.float32)
+
+
 class ShardedKMeans:
     """sklearn KMeans(n_clusters, n_init, max_iter, tol, random_state).fit (Lloyd, _kmeans.py:
     1427-1530 / :624-752) with the E-step partitioned by rows and the M-step by clusters. ``fit``
@@ -248,13 +256,19 @@ class ShardedKMeans:
                 sp_, wp = ops.mstep(Xc, grp, k, c0, c1)
                 sums = all_gather_parts(sp_, q, k, group).contiguous()
                 wsum = all_gather_parts(wp, q, k, group).contiguous()
-                if bool((wsum == 0).any()):
+                # average as if no cluster emptied, then ONE host read of (empty cluster?, labels
+                # changed?, the k shifts); on an empty cluster (rare) relocate and average again
+                C_new, shift = ops.average(sums, wsum, C)
+                empty, changed, shift_h = _iteration_status(wsum, labels, labels_old, shift)
+                if empty:
                     ops.relocate(Xc, C, sums, wsum, labels)  # replicated, identical on every rank
-                C, shift = ops.average(sums, wsum, C)
-                if labels_old is not None and torch.equal(labels, labels_old):
+                    C_new, shift = ops.average(sums, wsum, C)
+                    shift_h = shift.cpu().numpy()
+                C = C_new
+                if labels_old is not None and not changed:
                     strict = True
                     break
-                if (shift.cpu().numpy() ** 2).sum() <= tol_:
+                if (shift_h ** 2).sum() <= tol_:  # numpy's fp32 sum, as sklearn (:724-726)
                     break
                 labels_old = labels
             if not strict:  # the final E-step with the last centres (:736-747)
@@ -277,7 +291,3 @@ class ShardedKMeans:
     def fit_predict(self, X, y=None, sample_weight=None):
         return self.fit(X, sample_weight=sample_weight).labels_
 
-
-def fixed_point_scale(bound: float) -> int:
-    """Largest s with bound * 2^s < 2^61 (kept for gdd_segment_sum_fixed callers)."""
-    return int(min(60, 61 - math.ceil(math.log2(max(bound, 1e-300)))))

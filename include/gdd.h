@@ -215,16 +215,6 @@ int gdd_segment_sum_f32_part(int64_t n, int dim, const float* X, const float* w,
                              const int32_t* offsets, int k, int c0, int c1, float* sums_part,
                              float* wsum_part, gdd_stream_t stream);
 
-/* Order-independent accumulation for sharded k-means: sums_fx[c,j] += llrint(X[i,j]*w_i * 2^scale)   */
-/* (int64, exact integer adds => identical on any rank count / order), counts[c] += 1. Zero both     */
-/* outputs first. rows == NULL: rows 0..n-1.                                                        */
-int gdd_segment_sum_fixed(int64_t n, int dim, const float* X, const float* w, const int32_t* labels,
-                          int k, int scale_exp, long long* sums_fx, long long* counts,
-                          gdd_stream_t stream);
-/* centers[c,j] = fp32( (double)sums_fx[c,j] * 2^-scale / counts[c] ); counts[c]==0 -> leaves row.   */
-int gdd_fixed_to_centers(int k, int dim, const long long* sums_fx, const long long* counts,
-                         int scale_exp, float* centers, gdd_stream_t stream);
-
 /* sklearn _average_centers (_k_means_common.pyx:215-236): w>0: C[c,:] *= fp32(1.0/(double)w);       */
 /* w==0: C[c,:] = C[argmax(w),:] (first maximum; averaged already iff argmax < c, sklearn's loop     */
 /* order). Then center_shift[c] = sqrt(||C_new[c]-C_old[c]||^2) in the          */

@@ -129,7 +129,24 @@ def test_against_reference_fixture():
 
 
 def test_no_sp_and_rand():
-    gn, *_ = _normalized(300, 5.0, 74)
+    """'no_sp' hands the graph back; 'rand' (clustgdd_agent_transduct.py:207-222) takes, per class, the
+    first int(nnz * ratio) edges of torch.randperm(nnz) on torch's global CPU generator, carrying their
+    ER_estimator weights (the reference's "tried version" values)."""
+    gn, rp, col, val = _normalized(300, 5.0, 74)
     assert GC.graph_sparse(gn, 0.5, None, "no_sp")[0] is gn
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError):
         GC.graph_sparse(gn, 0.5, None, "rand")
+    ebd = torch.zeros((300, 3))
+    torch.manual_seed(7)
+    graphs = GC.graph_sparse(gn, 0.5, ebd, "rand")
+    er = O.vanilla_er(rp, col, val)
+    rows = np.repeat(np.arange(300), np.diff(rp))
+    torch.manual_seed(7)
+    m = int(gn.nnz * 0.5)
+    assert len(graphs) == 3
+    for g in graphs:
+        pick = np.sort(torch.randperm(gn.nnz)[:m].numpy())
+        A = g.to_scipy().tocoo()
+        o = np.lexsort((A.col, A.row))
+        assert np.array_equal(A.row[o], rows[pick]) and np.array_equal(A.col[o], col[pick])
+        assert np.array_equal(_bits(A.data[o].astype(np.float32)), _bits(er[pick]))

@@ -167,3 +167,72 @@ def test_group_by_label_is_a_stable_sort(n, k):
     assert o[-1] == valid.sum()
     assert np.array_equal(perm.cpu().numpy()[: valid.sum()], order.astype(np.int32))
     assert np.array_equal(o[:-1], np.searchsorted(np.sort(lab[valid]), np.arange(k), side="left"))
+
+
+def _device_chung_lu(n, avg_degree, seed):
+    """A Chung-Lu power-law graph (synth.chung_lu's model: weights rank^-1/1.5, symmetric, binary,
+    no self-loops) sampled and canonicalised on the device — the host generator needs minutes at
+    the products shape. Returns a gdd CSRGraph."""
+    from gdd.graph import CSRGraph
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    w = torch.arange(1, n + 1, device="cuda", dtype=torch.float64) ** (-1.0 / 1.5)
+    w = w[torch.randperm(n, device="cuda", generator=g)].float()
+    m = int(round(n * avg_degree / 2.0 * 1.04))
+    src = torch.multinomial(w, m, replacement=True, generator=g)
+    dst = torch.multinomial(w, m, replacement=True, generator=g)
+    keep = src != dst
+    src, dst = src[keep], dst[keep]
+    keys = torch.unique(torch.cat([src * n + dst, dst * n + src]))
+    del src, dst, keep
+    rows, col = keys // n, (keys % n).to(torch.int32)
+    rowptr = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    rowptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n), 0)
+    return CSRGraph(rowptr.to(torch.int32), col, None, n)
+
+
+def test_products_shape_propagate_matches_oracle():
+    """Config 5's propagation: N = 2,449,029, ~126M entries, d = 100, T = 3, alpha =
+    0.91 — the normalised graph and every bit of target and the last hop against the oracle (hub
+    rows split over many 256-entry segments, the fix-up pass, the d <= 112 lane group)."""
+    n, d = 2449029, 100
+    gr = _device_chung_lu(n, 50.5, 5)
+    X = synth.features(n, d, 5)
+    rp, co = gr.rowptr.cpu().numpy(), gr.col.cpu().numpy()
+    assert co.shape[0] > 120_000_000
+    ro, cn, vo = O.normalize_csr(rp, co, None, -1)
+    g = gdd.normalize_adj(gr)
+    assert np.array_equal(g.rowptr.cpu().numpy(), ro) and np.array_equal(g.col.cpu().numpy(), cn)
+    assert np.array_equal(bits(g.val.cpu().numpy()), bits(vo))
+    del gr
+    t, p = gdd.propagate(g, torch.from_numpy(X).cuda(), 3, 0.91)
+    t_ref, p_ref = O.propagate(ro, cn, vo, X, 3, 0.91)
+    assert np.array_equal(bits(t.cpu().numpy()), bits(t_ref))
+    assert np.array_equal(bits(p.cpu().numpy()), bits(p_ref))
+
+
+def test_reddit_shape_minibatch_matches_sklearn():
+    """Config 3's clustering at its full train shape (fixture G9b): MiniBatchKMeans(k=769, b=1000,
+    random_state=15) on 153,932 x 41 — k > b/2, so the fit takes the host-driven step loop whose
+    reassignment may take the argsort branch — labels, centres, inertia and n_steps_ as sklearn's."""
+    rec = load_json("golden_full_shapes.json")
+    X = synth.blobs(153932, 41, 769, seed=41)
+    m = gdd.MiniBatchKMeans(n_clusters=769, random_state=15, batch_size=1000).fit(X)
+    assert m.n_steps_ == rec["reddit_n_steps"]
+    assert sha(m.labels_.astype(np.int32)) == rec["reddit_labels_sha256"]
+    assert sha(np.ascontiguousarray(m.cluster_centers_, np.float32)) == rec["reddit_centers_sha256"]
+    assert m.inertia_ == rec["reddit_inertia"]
+
+
+def test_products_full_shape_kmeans_matches_sklearn():
+    """Config 5's clustering at its full shape (fixture G9b): KMeans(k=196) on 2,449,029 x 47 after
+    np.random.seed(15) — the multi-block (split) k-means++ rounds over 598 point blocks, the device
+    Lloyd loop — labels, centres, inertia and n_iter_ as sklearn's."""
+    rec = load_json("golden_full_shapes.json")
+    X = synth.blobs(2449029, 47, 196, seed=5)
+    np.random.seed(15)
+    m = gdd.KMeans(n_clusters=196).fit(X)
+    assert m.n_iter_ == rec["products_n_iter"]
+    assert sha(m.labels_.astype(np.int32)) == rec["products_labels_sha256"]
+    assert sha(np.ascontiguousarray(m.cluster_centers_, np.float32)) == rec["products_centers_sha256"]
+    assert m.inertia_ == rec["products_inertia"]

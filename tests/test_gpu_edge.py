@@ -123,14 +123,15 @@ def test_cluster_mean_more_clusters_than_one_launch():
 
 def test_lloyd_run_k_above_counting_sort():
     # k > 32,768: the device Lloyd loop groups the labels with the radix path (no LDS counters).
-    # One iteration from given centres (distinct data points, so no cluster is empty) against the
+    # One iteration from given centres (distinct data points far apart, no cluster empty) against the
     # oracle's _lloyd_iter: labels, new centres, weights and shifts bit for bit.
     from gdd import _lib
     import ctypes
-    n, dim, k = 34_000, 2, 33_000
+    n, dim, k = 34_000, 8, 33_000
     X = np.random.default_rng(11).standard_normal((n, dim)).astype(np.float32)
     C0 = X[:k].copy()
     lab_ref, c_ref, wic_ref, shift_ref = O._lloyd_iter(X, C0)
+    assert (wic_ref > 0).all()  # 8-d points far apart: every centre keeps its own point
     lib = _lib.device_lib()
     dev = torch.device("cuda")
     Xd = torch.from_numpy(X).to(dev)

@@ -135,12 +135,15 @@ def adversarial_points(n):
 
 
 def adversarial_uniforms(k, T, rnd):
-    """Round `rnd`'s trial 0 draws r = u * pot = 1 + 2^-48 (pot = 3 in round 1; 2 in round 2 once
+    """Round `rnd`'s trial 0 draws r = u * pot = 1 + 2^-50 (pot = 3 in round 1; 2 in round 2 once
     the point +1 is a centre): numpy's index is the second -1 point (n - 2); a blocked prefix says
-    an s entry. The other draws are ordinary (round 1's near 1: the +1 point)."""
+    an s entry. The round's other trials draw the first -1 point (index 1, the same potential), so
+    numpy's seeding takes index n - 2 (trial 0 wins the tie) and a blocked one index 1. Round 1's
+    draws before an adversarial round 2 all pick the +1 point; the later rounds are ordinary."""
     u = np.random.RandomState(k + T).uniform(size=(k - 1, T))
     u[0, :] = 0.9999
-    u[rnd - 1, 0] = (1.0 + 2.0 ** -48) / (3.0 if rnd == 1 else 2.0)
+    u[rnd - 1, :] = 0.25  # r < 1: the first -1 point (index 1), a tie with numpy's pick that trial 0 wins
+    u[rnd - 1, 0] = (1.0 + 2.0 ** -50) / (3.0 if rnd == 1 else 2.0)
     return u.ravel()
 
 
@@ -202,7 +205,7 @@ def test_kpp_cumsum_adversarial_weighted(monkeypatch, n):
     w[1] = 0.5
     w[n - 2] = 2.0
     u = adversarial_uniforms(k, T, 1)
-    u[0] = (0.5 + 2.0 ** -49) / 3.5  # w * closest = [0, 0.5, s, ..., s, 2, 1]
+    u[0] = (0.5 + 2.0 ** -50) / 3.5  # w * closest = [0, 0.5, s, ..., s, 2, 1]
     c_ref, idx_ref = O.kmeans_plusplus_draws(X, k, T, 0, u, w=w)
     assert idx_ref[1] == n - 2
     monkeypatch.setenv("GDD_KPP_EXACT", "1")

@@ -213,3 +213,50 @@ def test_distill_recsys_driver_vs_reference(tmp_path, capsys, monkeypatch):
     g = np.load(out / "condensed_graph.npz")
     assert np.array_equal(g["cu"], z["e2e_cu"]) and np.array_equal(g["ci"], z["e2e_ci"])
     np.testing.assert_allclose(g["w"], z["e2e_w"], rtol=1e-4, atol=1e-6)
+
+
+def _write_alidisplay(z, root):
+    os.makedirs(os.path.join(root, "Ali-Display"))
+    for split in ("train", "valid", "test"):
+        np.savetxt(os.path.join(root, "Ali-Display", f"{split}.txt"),
+                   np.stack([z[f"{split}_u"], z[f"{split}_i"]], 1), fmt="%d")
+
+
+ALI_LOSS_TOL = 1e-4  # 20 Adam steps on 51,539 condensed edges: SpMM vs index_add_ order drift
+
+
+def test_distill_recsys_real_alidisplay_vs_reference(tmp_path, capsys, monkeypatch):
+    """the drop-in driver on the real dataset the reference ships (Rankformer/data/
+    Ali-Display, 17,730 users x 10,036 items) with the reference's captured SVD embeddings and
+    flags: the clustering (KMeans k=1,773 and 1,004 on StandardScaled SVD-64), the condensed graph
+    and the artefacts bit for bit; the BPR losses within ALI_LOSS_TOL; every Recall@20 the
+    reference printed inside the oracle's tie bounds of this run's scores."""
+    from gdd import distill_recsys as D
+    z = load("golden_alidisplay.npz")
+    lines = open(__import__("golden_util").GOLDEN + "/golden_alidisplay_short_stdout.txt").read().splitlines()
+    _write_alidisplay(z, str(tmp_path))
+    seen = _recording_evaluator(monkeypatch)
+    argv = ["--data_dir", str(tmp_path)] + [a if a != "cpu" else "cuda" for a in lines[0].split()]
+    D.run(D.parse_args(argv), out_root=str(tmp_path / "out"), embeddings=(z["user_emb"], z["item_emb"]))
+    got = [l for l in capsys.readouterr().out.splitlines() if not l.startswith("[env]")]
+    ref = [l for l in lines[1:] if not l.startswith("[env]")]
+    assert len(got) == len(ref)
+    evals = iter(seen)
+    for g, r in zip(got, ref):
+        if g.startswith("[refine] ep=") or g.startswith("[eval]"):
+            v, (lo, hi, _) = next(evals)
+            rv = float(r.rsplit("=", 1)[1] if "=" in r.rsplit(" ", 1)[1] else r.rsplit(" ", 1)[1])
+            assert lo - 5e-7 <= v <= hi + 5e-7 and lo - 5e-7 <= rv <= hi + 5e-7, (g, r, lo, hi)
+            if g.startswith("[refine]"):
+                gl, rl = float(g.split("loss=")[1].split()[0]), float(r.split("loss=")[1].split()[0])
+                assert abs(gl - rl) <= ALI_LOSS_TOL, (g, r)
+        elif g.startswith("[save]"):
+            assert g.endswith("distilled_recsys/Ali-Display")
+        else:
+            assert g == r
+    out = tmp_path / "out" / "distilled_recsys" / "Ali-Display"
+    assert np.array_equal(np.load(out / "u2cu.npy"), z["u2cu"])
+    assert np.array_equal(np.load(out / "i2ci.npy"), z["i2ci"])
+    g = np.load(out / "condensed_graph.npz")
+    assert np.array_equal(g["cu"], z["cu"]) and np.array_equal(g["ci"], z["ci"])
+    np.testing.assert_allclose(g["w"], z["w"], rtol=1e-3, atol=1e-6)

@@ -80,3 +80,70 @@ def test_two_ranks_match_one():
         assert np.array_equal(_bits(p["mb_centers"]), _bits(mb.cluster_centers_))
         assert np.array_equal(p["counts"], cnt.cpu().numpy())
         assert np.array_equal(_bits(p["mean"]), _bits(fs.cpu().numpy()))
+
+
+def _pipelines(group, A, feat, logits, ind, logits_tr, E):
+    """The three hot-path entry points (transductive / inductive pretrained clustering, the recsys
+    kmeans_cluster), each with a MiniBatchKMeans and a Lloyd dataset branch."""
+    from gdd.pipeline import (kmeans_cluster, pretrained_clustering_hot_path,
+                              pretrained_clustering_induct_hot_path)
+    out = {}
+    for ds in ("ogbn-arxiv", "cora"):
+        np.random.seed(15)
+        fs, ls, cl = pretrained_clustering_hot_path(feat, A, 4, 0.8, logits, 60, dataset=ds, seed=15,
+                                                    cluster_minibatch=500, device="cuda:0", group=group)[:3]
+        out.update({f"{ds}_fs": fs.cpu().numpy(), f"{ds}_ls": ls.cpu().numpy(), f"{ds}_cl": cl.cpu().numpy()})
+    for ds in ("reddit", "flickr"):
+        np.random.seed(15)
+        fs, ls, cl = pretrained_clustering_induct_hot_path(ind, 3, 0.8, logits_tr, 40, dataset=ds, seed=15,
+                                                           cluster_minibatch=300, device="cuda:0",
+                                                           group=group)[:3]
+        out.update({f"{ds}_fs": fs.cpu().numpy(), f"{ds}_ls": ls.cpu().numpy(), f"{ds}_cl": cl.cpu().numpy()})
+    lab, cen = kmeans_cluster(E, n_clusters=150, seed=42, minibatch=False, device="cuda:0", group=group)
+    out.update(rs_labels=lab, rs_centers=cen)
+    return out
+
+
+def _pipeline_inputs():
+    from gdd import data as D
+    d = D.synthetic("cora", seed=5, d=48)
+    A = d.adj_full
+    logits = synth.linear_logits(d.feat_full, 7, 5)
+    logits_tr = synth.linear_logits(d.feat_train + 0.5, 7, 6)
+    E = synth.svd_like(3000, 32, seed=3)
+    return A, d.feat_full, logits, d, logits_tr, E
+
+
+def _pipeline_worker(rank, world, port, out):
+    sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE),
+                                                          "graph-distillation-for-recommendation_amd"), HERE]
+    import torch.distributed as dist
+    import gdd as G
+    from sharded_util import init_gloo
+    init_gloo(rank, world, port)
+    res = _pipelines(dist.group.WORLD, *_pipeline_inputs())
+    # ADVICE r2: with a process group up but group=None, each rank fits its own data on its own
+    own = G.MiniBatchKMeans(n_clusters=25, random_state=15, batch_size=400).fit(
+        synth.blobs(5000 + 1000 * rank, 12, 25, seed=100 + rank))
+    res.update(own_labels=own.labels_, own_inertia=own.inertia_)
+    np.savez(os.path.join(out, f"p{rank}.npz"), **res)
+    dist.destroy_process_group()
+
+
+def test_two_ranks_pipelines_match_one():
+    """pretrained_clustering_hot_path, pretrained_clustering_induct_hot_path and kmeans_cluster with a
+    two-rank group (MiniBatchKMeans: partitioned labels pass; Lloyd: ShardedKMeans; cluster means by
+    cluster slices) give one rank's outputs bit for bit; and MiniBatchKMeans(group=None) inside an
+    initialised process group stays a single-rank fit on each rank's own data."""
+    one = _pipelines(None, *_pipeline_inputs())
+    own = [gdd.MiniBatchKMeans(n_clusters=25, random_state=15, batch_size=400).fit(
+        synth.blobs(5000 + 1000 * r, 12, 25, seed=100 + r)) for r in range(2)]
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"gdd_pipes_{os.getpid()}")
+    os.makedirs(out, exist_ok=True)
+    mp.spawn(_pipeline_worker, args=(2, free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        p = np.load(os.path.join(out, f"p{r}.npz"))
+        for key, v in one.items():
+            a, b = np.ascontiguousarray(p[key]), np.ascontiguousarray(v)
+            assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8)), key
+        assert np.array_equal(p["own_labels"], own[r].labels_) and float(p["own_inertia"]) == own[r].inertia_

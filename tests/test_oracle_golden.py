@@ -192,7 +192,7 @@ class _InjectedDraws(np.random.RandomState):
 @pytest.mark.parametrize("n", [1000, 9000])
 def test_kmeans_plusplus_cumsum_adversarial_vs_sklearn(n, rnd):
     # 1-D points with distances [0, 1, s, ..., s, 1, 1] (s = 2^-58) to the first centre: numpy's
-    # sequential fp64 cumsum absorbs every s, a blocked one would not. The draw r = 1 + 2^-48 in
+    # sequential fp64 cumsum absorbs every s, a blocked one would not. The draw r = 1 + 2^-50 in
     # round `rnd` sits between the two (tests/test_gpu_kpp.py runs the device on the same draws);
     # scikit-learn picks the second -1 point (index n - 2), and so must the oracle.
     from sklearn.cluster import _kmeans as K
@@ -202,7 +202,8 @@ def test_kmeans_plusplus_cumsum_adversarial_vs_sklearn(n, rnd):
     X[0], X[1], X[n - 2], X[n - 1] = 0.0, -1.0, -1.0, 1.0
     u = np.random.RandomState(k + T).uniform(size=(k - 1, T))
     u[0, :] = 0.9999
-    u[rnd - 1, 0] = (1.0 + 2.0 ** -48) / (3.0 if rnd == 1 else 2.0)
+    u[rnd - 1, :] = 0.25  # r < 1: the first -1 point (index 1), a tie with numpy's pick that trial 0 wins
+    u[rnd - 1, 0] = (1.0 + 2.0 ** -50) / (3.0 if rnd == 1 else 2.0)
     ci, ii = K._kmeans_plusplus(X, k, row_norms(X, squared=True), np.ones(n, np.float32),
                                 _InjectedDraws(0, u), n_local_trials=T)
     co, io = O.kmeans_plusplus_draws(X, k, T, 0, u.ravel())

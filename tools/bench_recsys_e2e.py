@@ -6,7 +6,10 @@ Rankformer-format dataset: 6,040 users, 3,706 items, 1,000,209 unique interactio
 split), power-law user activity and item popularity. SVD embeddings: scipy svds on the host (timed, as in the reference).
 
 Prints the driver's own stdout and one JSON line with per-stage wall times.
-usage: bench_recsys_e2e.py [epochs]"""
+usage: bench_recsys_e2e.py [epochs]
+       bench_recsys_e2e.py alidisplay [epochs]   the real Rankformer/data/Ali-Display files (from the
+           fixture tests/golden/golden_alidisplay.npz, with the reference's captured SVD embeddings),
+           the reference's default flags; the JSON line carries both Recall@20 trajectories"""
 import json
 import os
 import sys
@@ -56,5 +59,43 @@ def main(epochs=500):
                       **tm}), flush=True)
 
 
+def alidisplay(epochs=500):
+    """The drop-in driver on the reference's real dataset beside the reference's own trajectory."""
+    import contextlib
+    import io
+    z = np.load(os.path.join(ROOT, "tests", "golden", "golden_alidisplay.npz"))
+    ref = open(os.path.join(ROOT, "tests", "golden", "golden_alidisplay_full_stdout.txt")).read().splitlines()
+    with tempfile.TemporaryDirectory() as tmp:
+        os.makedirs(os.path.join(tmp, "Ali-Display"))
+        for split in ("train", "valid", "test"):
+            np.savetxt(os.path.join(tmp, "Ali-Display", f"{split}.txt"),
+                       np.stack([z[f"{split}_u"], z[f"{split}_i"]], 1), fmt="%d")
+        args = D.parse_args(["--data_dir", tmp, "--dataset", "Ali-Display", "--refine_epochs", str(epochs)])
+        tm = {}
+        buf = io.StringIO()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with contextlib.redirect_stdout(buf):
+            D.run(args, out_root=os.path.join(tmp, "out"), timings=tm,
+                  embeddings=(z["user_emb"], z["item_emb"]))
+        torch.cuda.synchronize()
+        tm["total_s"] = time.perf_counter() - t0
+    out = buf.getvalue().splitlines()
+    print("\n".join(out))
+
+    def traj(lines):
+        return [(l.split()[1], float(l.rsplit("=", 1)[1])) for l in lines if l.startswith("[refine] ep=")]
+    tm["refine_ms_per_epoch"] = tm["refine_s"] / max(1, epochs) * 1e3
+    print(json.dumps({"workload": f"distill_recsys main on the real Ali-Display data (17,730 users x 10,036 "
+                                  f"items, 121,178 train interactions), default flags, {epochs} BPR epochs",
+                      **tm, "recall_gpu": traj(out), "recall_reference_cpu": traj(ref),
+                      "loss_gpu": [float(l.split("loss=")[1].split()[0]) for l in out if "loss=" in l],
+                      "loss_reference_cpu": [float(l.split("loss=")[1].split()[0]) for l in ref if "loss=" in l]}),
+          flush=True)
+
+
 if __name__ == "__main__":
-    main(*(int(a) for a in sys.argv[1:2]))
+    if sys.argv[1:2] == ["alidisplay"]:
+        alidisplay(*(int(a) for a in sys.argv[2:3]))
+    else:
+        main(*(int(a) for a in sys.argv[1:2]))

@@ -1,25 +1,58 @@
 #!/bin/bash
-# One GPU session: the changed parity tests first (fail fast), then the whole -m gpu suite, smoke, a
-# bench line (with the CPU baseline) and a rocprofv3 kernel-trace summary of a short bench.
-# Each GPU step has its own time limit; the first failure ends the script.
-# usage: tools/gpu_session.sh <tag> [first test files...]
-set -e
-TAG=${1:-s}
-shift || true
+# The one GPU-session runner: each named step runs under its own time limit with its log in
+# gpurun_out/<tag>/; the first failing step ends the session (no retries, nothing after a fault).
+#
+# usage: tools/gpu_session.sh <tag> <step>...
+#   tests[=file,file...]  pytest -m gpu (default: the whole tests/ directory)
+#   smoke                 __graft_entry__.smoke()
+#   bench                 python bench.py $BENCH_ARGS (the driver's default line, CPU baseline included)
+#   trace                 rocprofv3 --kernel-trace --stats of a short bench (kernel stats CSV)
+#   pmc-hop               rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE / TCC hit+miss) of tools/micro_prop.py
+#   phases                tools/phase_times.py (per-phase wall times of the bench step)
+#   kpp                   tools/micro_kpp.py (k-means++ round micro-benchmark)
+#   reddit | products     tools/bench_induct.py | tools/bench_products.py (config 3 / 5 shapes)
+#   recsys | alidisplay   tools/bench_recsys_e2e.py [alidisplay] (config 4 end to end)
+# e.g. /usr/local/graft/bin/gpurun -- 'bash tools/gpu_session.sh r03a tests=tests/test_gpu_kpp.py bench trace'
+set -o pipefail
+TAG=${1:?tag}
+shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-PYT="python -u -m pytest -x -v --timeout 170 --timeout-method thread -m gpu"
-if [ $# -gt 0 ]; then
-  timeout -k 10 600 $PYT "$@" > "$OUT/pytest_first.log" 2>&1 || { tail -60 "$OUT/pytest_first.log"; exit 1; }
-  tail -3 "$OUT/pytest_first.log"
-fi
-timeout -k 10 1000 $PYT tests > "$OUT/pytest_gpu.log" 2>&1 || { tail -60 "$OUT/pytest_gpu.log"; exit 1; }
-tail -3 "$OUT/pytest_gpu.log"
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -30 "$OUT/smoke.log"; exit 1; }
-tail -1 "$OUT/smoke.log"
-timeout -k 10 600 python bench.py ${BENCH_ARGS} > "$OUT/bench.log" 2>&1 || { tail -30 "$OUT/bench.log"; exit 1; }
-tail -1 "$OUT/bench.log"
-timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench \
-  -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/trace.log" 2>&1 || { tail -20 "$OUT/trace.log"; exit 1; }
-find "$OUT" -name "*stats.csv" | sort
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"
+
+run() {  # run <limit-seconds> <log-name> <command...>
+  local lim=$1 log=$2
+  shift 2
+  timeout -k 10 "$lim" "$@" > "$OUT/$log.log" 2>&1
+  local rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "step $log failed (rc $rc)"
+    tail -60 "$OUT/$log.log"
+    exit $rc
+  fi
+  tail -2 "$OUT/$log.log" | cut -c1-400
+}
+
+for step in "$@"; do
+  case "$step" in
+    tests) run 1500 pytest_gpu $PYT tests ;;
+    tests=*) run 1500 pytest_part $PYT $(echo "${step#tests=}" | tr ',' ' ') ;;
+    smoke) run 300 smoke python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run 600 bench python bench.py ${BENCH_ARGS} ;;
+    trace) run 420 trace rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench \
+             -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    pmc-hop)
+      run 120 pmc_fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o hop -- python3 tools/micro_prop.py
+      run 120 pmc_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o hop -- python3 tools/micro_prop.py
+      run 120 pmc_hit rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_hit" -o hop -- python3 tools/micro_prop.py ;;
+    phases) run 300 phases python tools/phase_times.py ;;
+    kpp) run 300 kpp python tools/micro_kpp.py ;;
+    reddit) run 400 reddit python tools/bench_induct.py ;;
+    products) run 600 products python tools/bench_products.py ;;
+    recsys) run 400 recsys python tools/bench_recsys_e2e.py ;;
+    alidisplay) run 400 alidisplay python tools/bench_recsys_e2e.py alidisplay ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "session $TAG done"

@@ -26,6 +26,8 @@ setting in which its Lloyd M-step merge order is deterministic.
                            on a 200,000 x 47 products-shaped input (global RNG after np.random.seed(15),
                            the agent's call) and distill_recsys.kmeans_cluster on ML-1M-shaped SVD
                            embeddings (6,040 users, k=604; 3,706 items, k=371; seed 42)
+  G9b golden_full_shapes.json  MiniBatchKMeans(k=769, b=1000) on 153,932 x 41 and KMeans(k=196) on
+                           the full 2,449,029 x 47 (config 3 / config 5 shapes), as hashes
   G10 golden_agent.npz  the reference ClustGDD transductive agent end to end on the CPU (train():
                            pretrained_clustering, graph_sparse('attaw'), graph_compress,
                            graph_refusion, then 5 x test_with_val) on gdd.data.synthetic('cora',
@@ -34,6 +36,8 @@ setting in which its Lloyd M-step merge order is deterministic.
                            distilled graph, the torch RNG state before the GCN runs and the five
                            [train, test] accuracies. The agents call .cuda() in test_with_val; the
                            generator maps Tensor.cuda to the CPU for this run (no arithmetic change)
+  G6r golden_alidisplay.npz  distill_recsys.main() on the real Rankformer/data/Ali-Display files
+                           (a 20-epoch refine with artefacts, and the default 500-epoch run's stdout)
   G12 golden_agent_induct_{flickr,reddit}.npz  the reference inductive agent end to end on the CPU
                            (clustgdd_agent_induct.ClustGDD.train on DataGraphSAINT files: KMeans /
                            MiniBatchKMeans, graph_sparse('attaw'), graph_compress, the reweighted
@@ -208,6 +212,37 @@ def g9_configs(recsys):
     rec["ml1m_call"] = "distill_recsys.kmeans_cluster(E, n_clusters=k, seed=42, minibatch=True)"
     np.savez_compressed(os.path.join(OUT, "golden_configs.npz"), **out)
     with open(os.path.join(OUT, "golden_configs.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+
+
+def g9b_full_shapes():
+    """k-means at the full config-3 and config-5 shapes, as hashes: MiniBatchKMeans(k=769,
+    b=1000, random_state=15) on a 153,932 x 41 Reddit-train-shaped input (k > b/2: the reassignment's
+    argsort branch can fire), and KMeans(k=196) on the full 2,449,029 x 47 products-shaped input after
+    np.random.seed(15) (the agent's random_state=None call)."""
+    import time
+    from sklearn.cluster import KMeans, MiniBatchKMeans
+    rec = {}
+    t = time.time()
+    X = synth.blobs(153932, 41, 769, seed=41)
+    m = MiniBatchKMeans(n_clusters=769, random_state=15, batch_size=1000).fit(X)
+    rec.update(reddit_input="gdd.synth.blobs(153932, 41, 769, seed=41)",
+               reddit_estimator="MiniBatchKMeans(n_clusters=769, random_state=15, batch_size=1000)",
+               reddit_n_steps=int(m.n_steps_), reddit_inertia=float(m.inertia_),
+               reddit_labels_sha256=sha(m.labels_.astype(np.int32)),
+               reddit_centers_sha256=sha(m.cluster_centers_.astype(np.float32)),
+               reddit_seconds=time.time() - t)
+    t = time.time()
+    X = synth.blobs(2449029, 47, 196, seed=5)
+    np.random.seed(15)
+    m = KMeans(n_clusters=196).fit(X)
+    rec.update(products_input="gdd.synth.blobs(2449029, 47, 196, seed=5)",
+               products_estimator="np.random.seed(15); KMeans(n_clusters=196) (random_state=None)",
+               products_n_iter=int(m.n_iter_), products_inertia=float(m.inertia_),
+               products_labels_sha256=sha(m.labels_.astype(np.int32)),
+               products_centers_sha256=sha(m.cluster_centers_.astype(np.float32)),
+               products_seconds=time.time() - t)
+    with open(os.path.join(OUT, "golden_full_shapes.json"), "w") as f:
         json.dump(rec, f, indent=1)
 
 
@@ -736,6 +771,59 @@ def g11_refine(recsys):
         f.write(" ".join(argv) + "\n" + buf.getvalue())
 
 
+def g6r_alidisplay(recsys):
+    """distill_recsys.main() on the real Ali-Display data the reference ships
+    (Rankformer/data/Ali-Display): a short refine (20 epochs, logged every 5) with
+    stdout and artefacts, and the default 500-epoch run's stdout (the Recall@20 trajectory). The
+    three split files are stored as integer arrays, the SVD embeddings as captured (svds draws its
+    start vector from numpy's global generator; BLAS orders make its last bits platform-dependent)."""
+    import contextlib
+    import io
+    import tempfile
+    data_dir = "/root/reference/Rankformer/data"
+    out = {}
+    for split in ("train", "valid", "test"):
+        a = np.loadtxt(os.path.join(data_dir, "Ali-Display", f"{split}.txt"), dtype=np.int64).reshape(-1, 2)
+        out[f"{split}_u"], out[f"{split}_i"] = a[:, 0].astype(np.int32), a[:, 1].astype(np.int32)
+    embs = []
+    orig_svd = recsys.compute_svd_embeddings
+
+    def svd_capture(*a, **k):
+        embs.append(orig_svd(*a, **k))
+        return embs[-1]
+    recsys.compute_svd_embeddings = svd_capture
+    runs = {"short": ["--refine_epochs", "20", "--log_every", "5"], "full": []}
+    stdout = {}
+    old_argv, cwd = sys.argv, os.getcwd()
+    try:
+        for tag, extra in runs.items():
+            with tempfile.TemporaryDirectory() as tmp:
+                argv = ["--data_dir", data_dir, "--dataset", "Ali-Display", "--device", "cpu"] + extra
+                sys.argv = ["distill_recsys.py"] + argv
+                os.chdir(tmp)
+                buf = io.StringIO()
+                with contextlib.redirect_stdout(buf):
+                    recsys.main()
+                stdout[tag] = " ".join(argv[2:]) + "\n" + buf.getvalue()
+                if tag == "short":
+                    base = os.path.join(tmp, "ClustGDD", "distilled_recsys", "Ali-Display")
+                    art = np.load(os.path.join(base, "condensed_graph.npz"))
+                    out.update({"cu": art["cu"], "ci": art["ci"], "w": art["w"],
+                                "u2cu": np.load(os.path.join(base, "u2cu.npy")),
+                                "i2ci": np.load(os.path.join(base, "i2ci.npy"))})
+                os.chdir(cwd)
+    finally:
+        sys.argv = old_argv
+        os.chdir(cwd)
+        recsys.compute_svd_embeddings = orig_svd
+    assert all(np.array_equal(embs[0][j], e[j]) for e in embs for j in range(2)), "svds not repeatable"
+    out["user_emb"], out["item_emb"] = embs[0]
+    np.savez_compressed(os.path.join(OUT, "golden_alidisplay.npz"), **out)
+    for tag, text in stdout.items():
+        with open(os.path.join(OUT, f"golden_alidisplay_{tag}_stdout.txt"), "w") as f:
+            f.write(text)
+
+
 def main():
     from threadpoolctl import threadpool_limits
     import sklearn
@@ -762,6 +850,11 @@ def main():
             g8_recsys(recsys)
         if "G9" in which:
             g9_configs(recsys)
+        if "G9b" in which:
+            g9b_full_shapes()
+        if "G6r" in which:
+            torch.set_num_threads(1)
+            g6r_alidisplay(recsys)
         if "G11" in which:
             torch.set_num_threads(1)
             g11_refine(recsys)
