@@ -480,26 +480,58 @@ __global__ void k_assign_finalize(int64_t n, int dim, const float* __restrict__ 
 
 
 // ---- persistent bf16 full pass (predict(precision="bf16")) ------------------
-// HBM-bound design: every block converts ALL centres once into v_mfma_f32_32x32x16_bf16 A-fragments
-// in LDS ([centre tile][k-step][lane] x 8 bf16, one ds_read_b128 per lane per MFMA) with the fp32
-// norms beside them (+inf past k), then each wave walks 32-point tiles: the tile's rows are one
-// contiguous span of X (float4 loads, the next tile in flight in registers while the current one
-// computes), staged in a wave-private LDS slot, turned into B-fragments (point = column, so every
-// lane owns one point's 16 centre rows per MFMA: the argmin is lane-local, then one lane^32 merge).
-// d = fma(-2, <x, c>_bf16, ||c||^2), first minimum; labels written directly (no key buffer, no
-// atomics, no finalize); sq_dist is the exact fp32 _euclidean_dense_dense to the chosen centre.
+// HBM-bound design (X is read once: 460 MB at products, ~77 us at the achievable 6 TB/s; the bf16
+// MFMAs are ~18 us of that shape's work and the argmin epilogue ~28 us of VALU):
+//   * the centres' v_mfma_f32_32x32x16_bf16 A-fragments ([centre tile][k-step][lane] x 8 bf16) and
+//     their fp32 norms (+inf past k) are built ONCE by k_bf16_frags into the workspace; every block
+//     copies them into LDS with coalesced 16-byte loads (building them per block from scalar loads of
+//     C cost more than the tiles at small n);
+//   * each wave walks 32-point tiles: a tile's rows are one contiguous span of X, read as float4 two
+//     tiles ahead of the compute (two register sets, the loop unrolled by two), scattered into a
+//     wave-private LDS slot with a row stride padded to a multiple of 16 floats (the pad columns stay
+//     zero), so each lane's B-fragment (one point's 8 features per k-step) is two ds_read_b128;
+//   * point = column of the 32x32 product, so the argmin over each centre tile is lane-local; one
+//     lane^32 merge at the end. d = fma(-2, <x, c>_bf16, ||c||^2), first minimum; labels written
+//     directly (no key buffer, no atomics); sq_dist (nullable) is the exact fp32
+//     _euclidean_dense_dense to the chosen centre.
+// The grid is the resident set (blocks per CU from the occupancy query x CUs), so no block waits for a
+// second wave of the grid.
 typedef float floatx4_t __attribute__((ext_vector_type(4)));
+
+__host__ __device__ inline int bf16p_stride(int dim) { return (dim + 15) & ~15; }
 
 __host__ __device__ inline size_t assign_bf16p_lds(int ktiles, int nsteps, int dim) {
   return (size_t)ktiles * nsteps * 64 * 16 + (size_t)ktiles * 32 * sizeof(float) +
-         (size_t)4 * 32 * dim * sizeof(float);
+         (size_t)4 * 32 * bf16p_stride(dim) * sizeof(float);
+}
+
+__host__ __device__ inline size_t bf16_frag_bytes(int ktiles, int nsteps) {
+  return (size_t)ktiles * nsteps * 64 * 16 + (size_t)ktiles * 32 * sizeof(float);
+}
+
+// the A-fragments of every centre tile and the norms (+inf past k), once per call
+__global__ void k_bf16_frags(int dim, int nsteps, int ktiles, int k, const float* __restrict__ C,
+                             const float* __restrict__ cn2, bf16x8_t* __restrict__ frags,
+                             float* __restrict__ cn_out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < ktiles * nsteps * 64) {
+    const int l = e & 63, rest = e >> 6;
+    const int st = rest % nsteps, ct = rest / nsteps;
+    const int c = ct * 32 + (l & 31), f0 = 16 * st + 8 * (l >> 5);
+    bf16x8_t v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)((c < k && f0 + j < dim) ? C[(int64_t)c * dim + f0 + j] : 0.f);
+    frags[e] = v;
+  }
+  if (e < ktiles * 32) cn_out[e] = e < k ? cn2[e] : __builtin_inff();
 }
 
 template <int PER>  // float4 loads per lane per 32-point tile: PER >= ceil(32 * dim / 256)
 __global__ __launch_bounds__(256) void k_assign_bf16p(int64_t n, int dim, int nsteps, int ktiles,
                                                       const float* __restrict__ X, int k,
+                                                      const bf16x8_t* __restrict__ frags,
+                                                      const float* __restrict__ cn_in,
                                                       const float* __restrict__ C,
-                                                      const float* __restrict__ cn2,
                                                       int32_t* __restrict__ labels,
                                                       float* __restrict__ sq_dist) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -508,52 +540,57 @@ __global__ __launch_bounds__(256) void k_assign_bf16p(int64_t n, int dim, int ns
   float* Pt = Cn + ktiles * 32;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, r = lane & 31;
-  for (int e = tid; e < ktiles * nsteps * 64; e += 256) {
-    const int l = e & 63, rest = e >> 6;
-    const int s = rest % nsteps, ct = rest / nsteps;
-    const int c = ct * 32 + (l & 31), f0 = 16 * s + 8 * (l >> 5);
-    bf16x8_t v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (__bf16)((c < k && f0 + j < dim) ? C[(int64_t)c * dim + f0 + j] : 0.f);
-    Af[e] = v;
+  const int SP = bf16p_stride(dim);
+  {  // the prebuilt fragments and norms: coalesced 16-byte copies
+    const int nfr = ktiles * nsteps * 64;
+    for (int e = tid; e < nfr; e += 256) Af[e] = frags[e];
+    for (int c = tid; c < ktiles * 32; c += 256) Cn[c] = cn_in[c];
   }
-  for (int c = tid; c < ktiles * 32; c += 256) Cn[c] = c < k ? cn2[c] : __builtin_inff();
+  float* my = Pt + wave * 32 * SP;
+  for (int e = lane; e < 32 * SP; e += 64) my[e] = 0.f;  // pad columns stay zero
   __syncthreads();
-  float* my = Pt + wave * 32 * dim;
   const int nf4 = 8 * dim;  // float4 per full tile (32 rows x dim floats)
   const int64_t ntiles = (n + 31) / 32, nfull = n / 32;
   const int64_t step = (int64_t)gridDim.x * 4;
-  int64_t t = (int64_t)blockIdx.x * 4 + wave;
-  float4 v[PER];
-  auto fetch = [&](int64_t tt) {
+  auto fetch = [&](int64_t tt, float4 (&v)[PER]) {
     if (tt >= nfull) return;  // the partial last tile is read scalar in stage()
     const float4* src = reinterpret_cast<const float4*>(X + tt * 32 * dim);
 #pragma unroll
     for (int q = 0; q < PER; ++q) v[q] = src[min(lane + 64 * q, nf4 - 1)];
   };
-  auto stage = [&](int64_t tt) {
+  auto stage = [&](int64_t tt, const float4 (&v)[PER]) {
     if (tt < nfull) {
-      float4* dst = reinterpret_cast<float4*>(my);
 #pragma unroll
-      for (int q = 0; q < PER; ++q)
-        if (lane + 64 * q < nf4) dst[lane + 64 * q] = v[q];
+      for (int q = 0; q < PER; ++q) {
+        const int e4 = lane + 64 * q;
+        if (e4 < nf4) {
+          const float w4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int e = 4 * e4 + j, row = e / dim;
+            my[row * SP + (e - row * dim)] = w4[j];
+          }
+        }
+      }
     } else {
       const int64_t rows = n - tt * 32;
-      for (int e = lane; e < 32 * dim; e += 64) my[e] = e < rows * dim ? X[tt * 32 * dim + e] : 0.f;
+      for (int e = lane; e < 32 * dim; e += 64) {
+        const int row = e / dim;
+        my[row * SP + (e - row * dim)] = e < rows * dim ? X[tt * 32 * dim + e] : 0.f;
+      }
     }
   };
-  fetch(t);
-  for (; t < ntiles; t += step) {
-    stage(t);
-    fetch(t + step);  // in flight while this tile computes
+  auto compute = [&](int64_t tt) {
     bf16x8_t b[8];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      if (s < nsteps) {
+    for (int st = 0; st < 8; ++st) {
+      if (st < nsteps) {
+        const floatx4_t lo = *reinterpret_cast<const floatx4_t*>(my + r * SP + 16 * st + 8 * h);
+        const floatx4_t hi = *reinterpret_cast<const floatx4_t*>(my + r * SP + 16 * st + 8 * h + 4);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int f = 16 * s + 8 * h + j;
-          b[s][j] = (__bf16)(f < dim ? my[r * dim + f] : 0.f);
+        for (int j = 0; j < 4; ++j) {
+          b[st][j] = (__bf16)lo[j];
+          b[st][4 + j] = (__bf16)hi[j];
         }
       }
     }
@@ -562,8 +599,8 @@ __global__ __launch_bounds__(256) void k_assign_bf16p(int64_t n, int dim, int ns
     for (int ct = 0; ct < ktiles; ++ct) {
       floatx16 acc = {};
 #pragma unroll
-      for (int s = 0; s < 8; ++s)
-        if (s < nsteps) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Af[(ct * nsteps + s) * 64 + lane], b[s], acc, 0, 0, 0);
+      for (int st = 0; st < 8; ++st)
+        if (st < nsteps) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Af[(ct * nsteps + st) * 64 + lane], b[st], acc, 0, 0, 0);
       const floatx4_t* cp = reinterpret_cast<const floatx4_t*>(Cn + ct * 32 + 4 * h);
       floatx4_t cn[4];
 #pragma unroll
@@ -583,11 +620,26 @@ __global__ __launch_bounds__(256) void k_assign_bf16p(int64_t n, int dim, int ns
       bestd = od;
       bestc = oc;
     }
-    const int64_t p = t * 32 + r;
+    const int64_t p = tt * 32 + r;
     if (h == 0 && p < n) {
       labels[p] = bestc;
-      if (sq_dist) sq_dist[p] = skl_sqdist(my + r * dim, C + (int64_t)bestc * dim, dim);
+      if (sq_dist) sq_dist[p] = skl_sqdist(my + r * SP, C + (int64_t)bestc * dim, dim);
     }
+  };
+  float4 va[PER], vb[PER];
+  int64_t t = (int64_t)blockIdx.x * 4 + wave;
+  fetch(t, va);
+  fetch(t + step, vb);
+  while (t < ntiles) {
+    stage(t, va);
+    fetch(t + 2 * step, va);  // two tiles in flight while this one computes
+    compute(t);
+    t += step;
+    if (t >= ntiles) break;
+    stage(t, vb);
+    fetch(t + 2 * step, vb);
+    compute(t);
+    t += step;
   }
 }
 
@@ -1438,14 +1490,25 @@ extern "C" int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const 
     const size_t lds = assign_bf16p_lds(ktiles, nsteps, dim);
     const int per_need = (8 * dim + 63) / 64;
     const bool aligned = (reinterpret_cast<uintptr_t>(X) & 15) == 0;
-    if (!rows && dim <= 128 && aligned && lds <= 150 * 1024) {
+    const size_t fb = bf16_frag_bytes(ktiles, nsteps);
+    if (!rows && dim <= 128 && aligned && lds <= 150 * 1024 && fb <= ws_bytes) {
       const int64_t ntiles = (n + 31) / 32;
-      const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 3) / 4, 1024));
+      bf16x8_t* frags = static_cast<bf16x8_t*>(ws);  // the keys are not used on this path
+      float* cn = reinterpret_cast<float*>(static_cast<char*>(ws) + (size_t)ktiles * nsteps * 64 * 16);
+      const int nfr = std::max(ktiles * nsteps * 64, ktiles * 32);
+      k_bf16_frags<<<(nfr + 255) / 256, 256, 0, s>>>(dim, nsteps, ktiles, k, C, c_norm2, frags, cn);
+      GDD_LAUNCHED();
       auto go = [&](auto P_) -> int {
         constexpr int P = decltype(P_)::value;
-        GDD_HIP(hipFuncSetAttribute((const void*)k_assign_bf16p<P>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds));
-        k_assign_bf16p<P><<<grid, 256, lds, s>>>(n, dim, nsteps, ktiles, X, k, C, c_norm2, labels, sq_dist);
+        const void* fn = (const void*)k_assign_bf16p<P>;
+        GDD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        int per_cu = 0, dev = 0, cus = 0;
+        GDD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds));
+        GDD_HIP(hipGetDevice(&dev));
+        GDD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        const int64_t resident = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
+        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 3) / 4, resident));
+        k_assign_bf16p<P><<<grid, 256, lds, s>>>(n, dim, nsteps, ktiles, X, k, frags, cn, C, labels, sq_dist);
         GDD_LAUNCHED();
         return GDD_OK;
       };

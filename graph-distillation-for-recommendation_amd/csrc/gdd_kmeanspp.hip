@@ -507,12 +507,58 @@ __device__ __forceinline__ double cum_tol(int exact, int64_t n, double r) {
 }
 
 // searchsorted_left(np.cumsum(w * row, dtype=float64), r): the products in fp32, the running sum in
-// fp64, entry by entry (row and w may be LDS or global)
+// fp64, entry by entry.
+// Rows in LDS (n <= 4096: the single-block paths): one thread, the plain walk.
 __device__ __noinline__ int64_t np_cumsum_search(const float* row, const float* w, int64_t n, double r) {
   double run = 0.0;
   for (int64_t e = 0; e < n; ++e) {
     run = run + (double)((w ? w[e] : 1.0f) * row[e]);
     if (!(run < r)) return e;
+  }
+  return n;
+}
+
+// Rows in global memory (the multi-block rounds, up to millions of entries): one whole wave. Lane j
+// loads entry e0 + j of the next 64-entry group (coalesced, a group ahead of the adds); every lane
+// runs the same dependent chain, taking entry j from lane j (readlane, uniform), and tests the
+// threshold off the chain; a group that reaches r is walked again entry by entry. Returns the same
+// value in every lane.
+__device__ __forceinline__ float lane_f(float x, int j) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), j));
+}
+
+__device__ __forceinline__ int64_t np_cumsum_search_wave(const float* row, const float* w, int64_t n,
+                                                         double r) {
+  const int lane = threadIdx.x & 63;
+  auto ld = [&](int64_t b) {
+    const int64_t e = min(b + lane, n - 1);  // past n: clamped, never added
+    return (w ? w[e] : 1.0f) * row[e];
+  };
+  double run = 0.0;
+  int64_t e0 = 0;
+  float xa = ld(0);
+  for (; e0 + 64 <= n; e0 += 64) {
+    const float xb = ld(e0 + 64);
+    double s = run;
+    bool hit = false;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      s = s + (double)lane_f(xa, j);
+      hit = hit || !(s < r);
+    }
+    if (hit) {
+      s = run;
+      for (int j = 0; j < 64; ++j) {
+        s = s + (double)lane_f(xa, j);
+        if (!(s < r)) return e0 + j;
+      }
+    }
+    run = s;
+    xa = xb;
+  }
+  for (int j = 0; e0 + j < n; ++j) {
+    run = run + (double)lane_f(xa, j);
+    if (!(run < r)) return e0 + j;
   }
   return n;
 }
@@ -886,9 +932,13 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   int64_t ct = n - 1;
   const int jb = s_jmin;
   const double tol = cum_tol(a.exact, n, r);
+  // the deciding prefixes: block jb's entries (pv) and the boundary before it (Pb), or the whole
+  // total when no block crosses
+  double pv[kPer];
+  const int64_t e0 = (int64_t)jb * kBlk + kPer * tid;
+  const double Pb = jb != INT_MAX ? s_P : s_tot;
   bool amb;  // a deciding prefix within tol of r (uniform across the workgroup)
   if (jb != INT_MAX) {  // count inside block jb (uniform branch)
-    const int64_t e0 = (int64_t)jb * kBlk + kPer * tid;
     double v[kPer], pre[kPer];
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
@@ -896,14 +946,13 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
       v[q] = e < n ? (double)(wv(a.w, e) * wrow[e]) : 0.0;
     }
     block_prefix(v, pre, s_wave);
-    const double P = s_P;
     int cw = 0;
     bool aw = false;
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
-      const double pv = P + pre[q];
-      cw += __popcll(__ballot(e0 + q < n && pv < r));
-      aw = aw || __ballot(e0 + q < n && fabs(pv - r) <= tol) != 0ull;
+      pv[q] = Pb + pre[q];
+      cw += __popcll(__ballot(e0 + q < n && pv[q] < r));
+      aw = aw || __ballot(e0 + q < n && fabs(pv[q] - r) <= tol) != 0ull;
     }
     if (lane == 0) {
       s_cnt[wave] = cw;
@@ -911,17 +960,64 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     }
     __syncthreads();
     int64_t cnt = 0;
-    amb = fabs(P - r) <= tol;  // the boundary before block jb (entries of earlier blocks)
+    amb = fabs(Pb - r) <= tol;  // the boundary before block jb (entries of earlier blocks)
     for (int q = 0; q < kWaves; ++q) {
       cnt += s_cnt[q];
       amb = amb || s_amb[q];
     }
     ct = min<int64_t>(n - 1, (int64_t)jb * kBlk + cnt);
   } else {
-    amb = fabs(s_tot - r) <= tol;
+    amb = fabs(Pb - r) <= tol;
+  }
+  if (amb && a.exact == 1) {
+    // cum_tol bounds numpy's rounding by 2.25 n u r whatever the row holds. A row-specific bound
+    // decides most of these draws without the replay: with g = ulp(total) (every partial sum is at
+    // most the total), an entry that is a multiple of g adds to numpy's running sum exactly unless the
+    // sum enters a new binade; each other ("fine") entry costs at most g / 2 and the binade entries
+    // together at most g (ulps double per binade), so |numpy - exact| <= A = (F / 2 + 1) g for F fine
+    // entries in the row. The blocked prefixes are trees of height <= h: |blocked - exact| <=
+    // gamma_h * exact (Higham eq. 4.4). A decision can differ from numpy's only if |p - r| <= A +
+    // 2 gamma_h max(p, r); only then does the replay run.
+    __syncthreads();  // s_cnt / s_amb reused below
+    // any g >= ulp(numpy's largest partial sum) will do: the total over-estimated by numpy's gamma_n
+    const double sup = s_tot * (1.0 + (double)(n + 256) * 0x1p-52);
+    const int E = sup > 0.0 ? ilogb(sup) : -1074;
+    const double ginv = ldexp(1.0, 52 - E);
+    int fine = 0;
+    for (int64_t e = tid; e < n; e += kThr) {
+      const double x = (double)(wv(a.w, e) * wrow[e]);
+      const double q = x * ginv;
+      fine += !(q == trunc(q)) ? 1 : 0;  // NaN / inf count as fine (the replay decides)
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) fine += __shfl_xor(fine, o);
+    if (lane == 0) s_cnt[wave] = fine;
+    __syncthreads();
+    int64_t F = 0;
+    for (int q = 0; q < kWaves; ++q) F += s_cnt[q];
+    const double g = ldexp(1.0, E - 52);
+    const double A = ((double)F * 0.5 + 1.0) * g;
+    const int64_t ch = (a.nblk + kThr - 1) / kThr;
+    const double gh = (double)(96 + ch) * 0x1p-53 * 1.01;
+    const bool finite = s_tot == s_tot && s_tot < __builtin_inf();
+    bool aw = !finite || fabs(Pb - r) <= A + 2.0 * gh * fmax(Pb, r);
+    if (jb != INT_MAX) {
+#pragma unroll
+      for (int q = 0; q < kPer; ++q)
+        aw = aw || (e0 + q < n && fabs(pv[q] - r) <= A + 2.0 * gh * fmax(pv[q], r));
+    }
+    aw = __ballot(aw) != 0ull;
+    __syncthreads();
+    if (lane == 0) s_amb[wave] = aw;
+    __syncthreads();
+    amb = false;
+    for (int q = 0; q < kWaves; ++q) amb = amb || s_amb[q];
   }
   if (amb) {  // numpy's sequential cumsum decides this draw
-    if (tid == 0) s_ct = min<int64_t>(n - 1, np_cumsum_search(wrow, a.w, n, r));
+    if (wave == 0) {
+      const int64_t e = np_cumsum_search_wave(wrow, a.w, n, r);
+      if (lane == 0) s_ct = min<int64_t>(n - 1, e);
+    }
     __syncthreads();
     ct = s_ct;
   }

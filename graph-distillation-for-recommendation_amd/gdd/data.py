@@ -6,7 +6,8 @@
 the same object from arrays; :func:`synthetic` makes a learnable stand-in of a named dataset's
 shape (the real Planetoid / OGB files cannot be downloaded here): class-conditioned Gaussian
 features and a homophilous power-law graph, with the public split sizes (Cora: 20 train nodes
-per class, 500 val, 1,000 test; ogbn-arxiv: 54 / 18 / 28 %). GraphSAINT-format directories load
+per class, 500 val, 1,000 test; ogbn-arxiv: OGB's 90,941 / 29,799 / 48,603; other shapes 54 / 18 / 28 %).
+GraphSAINT-format directories load
 through :func:`gdd.pipeline.load_graphsaint`.
 """
 from __future__ import annotations
@@ -22,6 +23,14 @@ SHAPES = {
     "ogbn-arxiv": (169343, 128, 40, 13.7, 0.65),
     "flickr": (89250, 500, 7, 10.1, 0.32),
     "reddit": (232965, 602, 41, 99.6, 0.78),
+}
+
+
+# public train / val / test sizes (ogbn-arxiv: OGB's time split; flickr / reddit: GraphSAINT's role.json)
+SPLITS = {
+    "ogbn-arxiv": (90941, 29799, 48603),
+    "flickr": (44625, 22312, 22313),
+    "reddit": (153932, 23699, 55334),
 }
 
 
@@ -86,6 +95,9 @@ def synthetic(name: str, seed: int = 15, n: int | None = None, d: int | None = N
         rest = np.setdiff1d(order, idx_train, assume_unique=False)
         rest = rest[rng.permutation(rest.shape[0])]
         idx_val, idx_test = np.sort(rest[:500]), np.sort(rest[500:1500])
+    elif name in SPLITS and n == n0:  # the public split sizes (train, val, test)
+        a, b = SPLITS[name][0], SPLITS[name][0] + SPLITS[name][1]
+        idx_train, idx_val, idx_test = np.arange(a), np.arange(a, b), np.arange(b, n)
     else:
         a, b = int(0.54 * n), int(0.72 * n)
         idx_train, idx_val, idx_test = np.arange(a), np.arange(a, b), np.arange(b, n)

@@ -43,6 +43,10 @@ def main():
         fl = 2.0 * n * k * dim
         res[name] = {"n": n, "dim": dim, "k": k, "fp32_ms": t32, "bf16_ms": t16,
                      "fp32_TFLOPs": fl / (t32 * 1e-3) / 1e12, "bf16_TFLOPs": fl / (t16 * 1e-3) / 1e12,
+                     # the bf16 pass is HBM-bound (2 n k dim flops on 4 n dim bytes: ~2k/4 flop/B
+                     # below the bf16 ridge): X's bytes per call time, against 8 TB/s
+                     "bf16_X_GBs": 4.0 * n * dim / (t16 * 1e-3) / 1e9,
+                     "bf16_hbm_frac": 4.0 * n * dim / (t16 * 1e-3) / 8e12,
                      "label_agreement": float((l32 == l16).float().mean())}
     print(json.dumps(res), flush=True)
 

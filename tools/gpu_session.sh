@@ -10,8 +10,11 @@
 #   pmc-hop               rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE / TCC hit+miss) of tools/micro_prop.py
 #   phases                tools/phase_times.py (per-phase wall times of the bench step)
 #   kpp                   tools/micro_kpp.py (k-means++ round micro-benchmark)
+#   assign                tools/bench_assign.py (full assignment pass, fp32 vs bf16, three shapes)
+#   hop-lanes             tools/micro_prop.py at arxiv / products with the XCD slice A/B switch
 #   reddit | products     tools/bench_induct.py | tools/bench_products.py (config 3 / 5 shapes)
 #   recsys | alidisplay   tools/bench_recsys_e2e.py [alidisplay] (config 4 end to end)
+#   agent                 the transductive drop-in on synthetic ogbn-arxiv (main_transduct.sh's r=0.5% line)
 # e.g. /usr/local/graft/bin/gpurun -- 'bash tools/gpu_session.sh r03a tests=tests/test_gpu_kpp.py bench trace'
 set -o pipefail
 TAG=${1:?tag}
@@ -48,10 +51,16 @@ for step in "$@"; do
       run 120 pmc_hit rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_hit" -o hop -- python3 tools/micro_prop.py ;;
     phases) run 300 phases python tools/phase_times.py ;;
     kpp) run 300 kpp python tools/micro_kpp.py ;;
+    assign) run 300 assign python tools/bench_assign.py ;;
+    hop-lanes) run 300 hop_lanes bash -c 'python tools/micro_prop.py && GDD_HOP_LANES=8 python tools/micro_prop.py && GDD_HOP_LANES=32 python tools/micro_prop.py && python tools/micro_prop.py products && GDD_HOP_LANES=8 python tools/micro_prop.py products' ;;
     reddit) run 400 reddit python tools/bench_induct.py ;;
     products) run 600 products python tools/bench_products.py ;;
     recsys) run 400 recsys python tools/bench_recsys_e2e.py ;;
     alidisplay) run 400 alidisplay python tools/bench_recsys_e2e.py alidisplay ;;
+    agent) run 600 agent env PYTHONPATH=graph-distillation-for-recommendation_amd python -m gdd.train_clustgdd_transduct \
+             --gpu_id 0 --dataset ogbn-arxiv --reduction_rate 0.005 --prop_num 18 --postprop_num 10 --alpha 0.91 \
+             --predropout 0.6 --sp_ratio 0.1 --preep 1000 --postep 1000 --frcoe 1.9 --predcoe 0.025 --save 1 \
+             --json "$OUT/agent_arxiv.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
