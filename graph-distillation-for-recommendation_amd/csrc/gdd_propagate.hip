@@ -164,6 +164,7 @@ __global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
                                              const float* __restrict__ x, float* __restrict__ y,
                                              float* __restrict__ acc_out, float acc_scale,
                                              const float* __restrict__ acc_init,
+                                             const float* __restrict__ acc_prev,
                                              float* __restrict__ partials) {
   const int lane = threadIdx.x & (G - 1);
   int64_t ib;  // item block
@@ -228,6 +229,12 @@ __global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
       } else {
         vload_nt<V>(acc_out + o, t);
       }
+      if (acc_prev) {  // the previous hop's deferred term: its output row (this hop's input x)
+        float q[V];
+        vload<V>(acc_prev + o, q);
+#pragma unroll
+        for (int v = 0; v < V; ++v) t[v] = t[v] + acc_scale * q[v];
+      }
 #pragma unroll
       for (int v = 0; v < V; ++v) t[v] = t[v] + acc_scale * acc[v];  // two roundings (agent :65)
       vstore_nt<V>(acc_out + o, t);
@@ -246,7 +253,7 @@ __global__ void k_fixup(const int32_t* __restrict__ counts, const int32_t* __res
                         const int32_t* __restrict__ long_off, const int32_t* __restrict__ rowptr,
                         int d, const float* __restrict__ partials, float* __restrict__ y,
                         float* __restrict__ acc_out, float acc_scale,
-                        const float* __restrict__ acc_init) {
+                        const float* __restrict__ acc_init, const float* __restrict__ acc_prev) {
   const int nl = counts[1];
   for (int r = blockIdx.x; r < nl; r += gridDim.x) {
     const int32_t row = long_rows[r], po = long_off[r];
@@ -266,7 +273,11 @@ __global__ void k_fixup(const int32_t* __restrict__ counts, const int32_t* __res
       for (; k < s; ++k) sum = sum + pp[(int64_t)k * d];
       const int64_t o = (int64_t)row * d + f;
       y[o] = sum;
-      if (acc_out) acc_out[o] = (acc_init ? acc_scale * acc_init[o] : acc_out[o]) + acc_scale * sum;
+      if (acc_out) {
+        float t = acc_init ? acc_scale * acc_init[o] : acc_out[o];
+        if (acc_prev) t = t + acc_scale * acc_prev[o];
+        acc_out[o] = t + acc_scale * sum;
+      }
     }
   }
 }
@@ -387,7 +398,8 @@ int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv,
 
 template <int V, int G>
 void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float scale, int d,
-                   const float* x, float* y, float* acc, float acc_scale, const float* acc_init, hipStream_t s) {
+                   const float* x, float* y, float* acc, float acc_scale, const float* acc_init,
+                   const float* acc_prev, hipStream_t s) {
   constexpr int kGroups = 256 / G;
   const int64_t iblocks = (pl.max_items + kGroups - 1) / kGroups;
   const int chunks = (d + G * V - 1) / (G * V);
@@ -395,7 +407,8 @@ void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float s
     constexpr int S = decltype(S_)::value;
     const int64_t groups = (iblocks + (8 / S) - 1) / (8 / S);
     k_hop<V, G, S><<<(unsigned)(groups * 8), 256, 0, s>>>(pl.items, pl.counts, col, val, scale, d,
-                                                          x, y, acc, acc_scale, acc_init, pl.partials);
+                                                          x, y, acc, acc_scale, acc_init, acc_prev,
+                                                          pl.partials);
   };
   if (chunks == 8)
     xcd_launch(std::integral_constant<int, 8>());
@@ -407,7 +420,7 @@ void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float s
     xcd_launch(std::integral_constant<int, 1>());
   else
     k_hop<V, G, 0><<<dim3((unsigned)iblocks, (unsigned)chunks), 256, 0, s>>>(
-        pl.items, pl.counts, col, val, scale, d, x, y, acc, acc_scale, acc_init, pl.partials);
+        pl.items, pl.counts, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, pl.partials);
 }
 
 // lanes per item: the whole row up to 64 lanes, or (GDD_HOP_LANES=8/16/32, V = 4) narrower groups
@@ -422,47 +435,51 @@ int hop_lanes_override() {
 
 template <int V>
 void launch_hop_v(const Plan& pl, const int32_t* col, const float* val, float scale, int d,
-                  const float* x, float* y, float* acc, float acc_scale, const float* acc_init, hipStream_t s) {
+                  const float* x, float* y, float* acc, float acc_scale, const float* acc_init,
+                  const float* acc_prev, hipStream_t s) {
   const int lanes = (d + V - 1) / V;
   const int ov = hop_lanes_override();
   if (ov == 8)
-    return launch_hop_vg<V, 8>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
+    return launch_hop_vg<V, 8>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
   if (ov == 16)
-    return launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
+    return launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
   // 29..32 lanes of float4 (d in (112, 128]): two XCD slices of 16 lanes each, so an XCD's L2 caches
   // half of every gathered row (measured at the arxiv shape, d = 128: 202 vs 208 us per hop; the
   // gathers' L2 hit rate rises, the instruction overhead of the narrower groups stays small). With
   // fewer lanes the second slice idles most of its lanes while reading the whole column/value stream
   // again: products' d = 100 (25 lanes) runs 9.5 ms per hop in one 32-lane group vs 12.4 sliced.
   if (lanes <= 16 || (V == 4 && lanes > 28 && lanes <= 32 && ov != 32))
-    launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
+    launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
   else if (lanes <= 32)
-    launch_hop_vg<V, 32>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
+    launch_hop_vg<V, 32>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
   else
-    launch_hop_vg<V, 64>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
+    launch_hop_vg<V, 64>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
 }
 
 // acc_init (nullable): the accumulator's previous value is acc_scale * acc_init instead of acc (the
-// first hop folds the initial target = fp32(1-alpha) * X, agent :59, into its epilogue)
+// first hop folds the initial target = fp32(1-alpha) * X, agent :59, into its epilogue).
+// acc_prev (nullable): a term the previous hop deferred, added first: acc = (acc + acc_scale *
+// acc_prev) + acc_scale * y — the same two roundings, in the same order, as two separate updates.
 int run_hop(const Plan& pl, const int32_t* rowptr, const int32_t* col, const float* val,
             float scale, int d, const float* x, float* y, float* acc, float acc_scale,
-            hipStream_t s, const float* acc_init = nullptr) {
+            hipStream_t s, const float* acc_init = nullptr, const float* acc_prev = nullptr) {
   // float4 rows need 16-byte aligned row starts: d % 4 == 0 and 16-byte aligned bases
   auto aligned = [](const void* p, int a) { return ((uintptr_t)p % a) == 0; };
   const bool a16 = aligned(x, 16) && aligned(y, 16) && (!acc || aligned(acc, 16)) &&
-                   (!acc_init || aligned(acc_init, 16)) && aligned(pl.partials, 16);
+                   (!acc_init || aligned(acc_init, 16)) && (!acc_prev || aligned(acc_prev, 16)) &&
+                   aligned(pl.partials, 16);
   const bool a8 = aligned(x, 8) && aligned(y, 8) && (!acc || aligned(acc, 8)) &&
-                  (!acc_init || aligned(acc_init, 8));
+                  (!acc_init || aligned(acc_init, 8)) && (!acc_prev || aligned(acc_prev, 8));
   if (d % 4 == 0 && a16)
-    launch_hop_v<4>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
+    launch_hop_v<4>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
   else if (d % 2 == 0 && a8)
-    launch_hop_v<2>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
+    launch_hop_v<2>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
   else
-    launch_hop_v<1>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, s);
+    launch_hop_v<1>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
   GDD_LAUNCHED();
   const unsigned fixup_grid = (unsigned)std::min<int64_t>(pl.max_long, kFixupBlocks);
   k_fixup<<<fixup_grid, 256, 0, s>>>(pl.counts, pl.long_rows, pl.long_off, rowptr, d, pl.partials, y,
-                                     acc, acc_scale, acc_init);
+                                     acc, acc_scale, acc_init, acc_prev);
   GDD_LAUNCHED();
   return GDD_OK;
 }
@@ -548,13 +565,31 @@ extern "C" int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, cons
   Plan pl;
   rc = build_plan(n, nnz, d, rowptr, cv, pl, s);
   if (rc) return rc;
-  // ping-pong so that hop T-1 lands in p_last
+  // ping-pong so that hop T-1 lands in p_last. The target update is paired: after the first hop,
+  // hop h (odd) leaves target alone and hop h+1 adds both terms, reading p_h back as its own input
+  // rows — one read-modify-write of target per two hops instead of per hop (the streamed bytes that
+  // push the gathered rows out of the Infinity Cache), bit-identical (GDD_PROP_PAIR=0: every hop)
+  static const bool pair = [] {
+    const char* e = getenv("GDD_PROP_PAIR");
+    return e == nullptr || atoi(e) != 0;
+  }();
   const int hops = T - 1;
   float* bufs[2] = {(hops % 2 == 1) ? p_last : p_tmp, (hops % 2 == 1) ? p_tmp : p_last};
   const float* in = X;
+  bool deferred = false;
   for (int h = 0; h < hops; ++h) {
     float* out = bufs[h % 2];
-    rc = run_hop(pl, rowptr, col, val, a32, d, in, out, target, w32, s, h == 0 ? X : nullptr);
+    if (h == 0) {
+      rc = run_hop(pl, rowptr, col, val, a32, d, in, out, target, w32, s, X);
+    } else if (deferred) {
+      rc = run_hop(pl, rowptr, col, val, a32, d, in, out, target, w32, s, nullptr, in);
+      deferred = false;
+    } else if (pair && h + 1 < hops) {
+      rc = run_hop(pl, rowptr, col, val, a32, d, in, out, nullptr, w32, s);
+      deferred = true;
+    } else {
+      rc = run_hop(pl, rowptr, col, val, a32, d, in, out, target, w32, s);
+    }
     if (rc) return rc;
     in = out;
   }

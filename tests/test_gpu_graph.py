@@ -53,8 +53,11 @@ def test_normalize_bitexact(case):
     assert np.array_equal(gn.val.cpu().numpy().view(np.uint32), vo.view(np.uint32))
 
 
+# T >= 4 runs paired target updates (one hop defers its term to the next); float4 / float2 / float
+# rows, odd and even hop counts, and the split hub row's fix-up path all take part
 @pytest.mark.parametrize("d,T,alpha", [(128, 18, 0.91), (64, 5, 0.8), (7, 3, 0.5), (41, 4, 0.95),
-                                       (602, 3, 0.95), (100, 2, 0.91), (1, 1, 0.8)])
+                                       (602, 3, 0.95), (602, 6, 0.95), (100, 2, 0.91), (1, 1, 0.8),
+                                       (3, 7, 0.8)])
 def test_propagate_bitexact(d, T, alpha):
     n = 3000
     A = _graph(n, 12.0, 5)

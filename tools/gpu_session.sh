@@ -12,6 +12,7 @@
 #   kpp                   tools/micro_kpp.py (k-means++ round micro-benchmark)
 #   assign                tools/bench_assign.py (full assignment pass, fp32 vs bf16, three shapes)
 #   hop-lanes             tools/micro_prop.py at arxiv / products with the XCD slice A/B switch
+#   prop-pair             tools/micro_prop.py at arxiv / products, paired target updates on / off
 #   reddit | products     tools/bench_induct.py | tools/bench_products.py (config 3 / 5 shapes)
 #   recsys | alidisplay   tools/bench_recsys_e2e.py [alidisplay] (config 4 end to end)
 #   agent                 the transductive drop-in on synthetic ogbn-arxiv (main_transduct.sh's r=0.5% line)
@@ -53,6 +54,7 @@ for step in "$@"; do
     kpp) run 300 kpp python tools/micro_kpp.py ;;
     assign) run 300 assign python tools/bench_assign.py ;;
     hop-lanes) run 300 hop_lanes bash -c 'python tools/micro_prop.py && GDD_HOP_LANES=8 python tools/micro_prop.py && GDD_HOP_LANES=32 python tools/micro_prop.py && python tools/micro_prop.py products && GDD_HOP_LANES=8 python tools/micro_prop.py products' ;;
+    prop-pair) run 300 prop_pair bash -c 'python tools/micro_prop.py && GDD_PROP_PAIR=0 python tools/micro_prop.py && python tools/micro_prop.py && GDD_PROP_PAIR=0 python tools/micro_prop.py && python tools/micro_prop.py products && GDD_PROP_PAIR=0 python tools/micro_prop.py products' ;;
     reddit) run 400 reddit python tools/bench_induct.py ;;
     products) run 600 products python tools/bench_products.py ;;
     recsys) run 400 recsys python tools/bench_recsys_e2e.py ;;
