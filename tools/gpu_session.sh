@@ -8,6 +8,9 @@
 #   bench                 python bench.py $BENCH_ARGS (the driver's default line, CPU baseline included)
 #   trace                 rocprofv3 --kernel-trace --stats of a short bench (kernel stats CSV)
 #   pmc-hop               rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE / TCC hit+miss) of tools/micro_prop.py
+#   pmc-bench             rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE / TCC hit+miss) of a short bench
+#                         with one target update per hop (GDD_PROP_PAIR=0: every k_hop launch is the
+#                         roofline's unpaired hop); summarise with tools/pmc_summary.py <dir>/pmcb ...
 #   phases                tools/phase_times.py (per-phase wall times of the bench step)
 #   kpp                   tools/micro_kpp.py (k-means++ round micro-benchmark)
 #   assign                tools/bench_assign.py (full assignment pass, fp32 vs bf16, three shapes)
@@ -50,6 +53,11 @@ for step in "$@"; do
       run 120 pmc_fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o hop -- python3 tools/micro_prop.py
       run 120 pmc_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o hop -- python3 tools/micro_prop.py
       run 120 pmc_hit rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_hit" -o hop -- python3 tools/micro_prop.py ;;
+    pmc-bench)
+      B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
+      run 240 pmcb_fetch env GDD_PROP_PAIR=0 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcb/pmc_fetch" -o bench -- $B
+      run 240 pmcb_write env GDD_PROP_PAIR=0 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcb/pmc_write" -o bench -- $B
+      run 240 pmcb_hit env GDD_PROP_PAIR=0 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmcb/pmc_hit" -o bench -- $B ;;
     phases) run 300 phases python tools/phase_times.py ;;
     kpp) run 300 kpp python tools/micro_kpp.py ;;
     assign) run 300 assign python tools/bench_assign.py ;;
