@@ -1216,6 +1216,7 @@ struct Kpp1Args {
   int64_t* candw2[2];    // [T*T][T]
   int64_t* candself2[2];  // [T*T]
   int exact;             // cum_tol's mode
+  int bsearch;           // 1: the folds' binary searches (GDD_KPP_BSEARCH, A/B); 0: two-ballot searches
 };
 
 __device__ __forceinline__ int kpp1_argmin(const float* __restrict__ pot, int T) {
@@ -1634,18 +1635,55 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
       (void)pot;
     }
     __syncthreads();
-    if (tid < T) {  // searchsorted_left(cum, u * pot) over the LDS cumulative potential
-      const double rr = ut * (double)s_pot;
-      int lo = 0, hi = n;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (s_cum[mid] < rr) lo = mid + 1; else hi = mid;
+    if (a.bsearch) {
+      if (tid < T) {  // searchsorted_left(cum, u * pot): binary search over the LDS cumulative potential
+        const double rr = ut * (double)s_pot;
+        int lo = 0, hi = n;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (s_cum[mid] < rr) lo = mid + 1; else hi = mid;
+        }
+        // the answer's two neighbours decide it (cum_tol): replay numpy's sum when either is close
+        const double tol = cum_tol(a.exact, n, rr);
+        if ((lo > 0 && fabs(s_cum[lo - 1] - rr) <= tol) || (lo < n && fabs(s_cum[lo] - rr) <= tol))
+          lo = (int)np_cumsum_search(s_d, a.w, n, rr);
+        cand_out[tid] = min(n - 1, lo);
       }
-      // the answer's two neighbours decide it (cum_tol): replay numpy's sum when either is close
-      const double tol = cum_tol(a.exact, n, rr);
-      if ((lo > 0 && fabs(s_cum[lo - 1] - rr) <= tol) || (lo < n && fabs(s_cum[lo] - rr) <= tol))
-        lo = (int)np_cumsum_search(s_d, a.w, n, rr);
-      cand_out[tid] = min(n - 1, lo);
+    } else {
+      // searchsorted_left(cum, u * pot) in two ballots: lane l of every wave holds the last value of
+      // block l (64 blocks of Bk = ceil(n / 64) entries); wave w takes uniforms w, w + 4, ...: the
+      // blocks below r counted by one ballot, then one LDS read per lane and a ballot inside the next
+      // block — two LDS trips instead of log2(n) dependent ones. The rounding check covers the block's
+      // entries and the entry before it (every deciding neighbour; a count that differs from numpy's
+      // needs a prefix within tol of r, non-monotone rounding steps included)
+      const int Bk = (n + 63) >> 6;
+      const int nb = (n + Bk - 1) / Bk;
+      const double cl = s_cum[min((lane + 1) * Bk, n) - 1];
+      const double pot = (double)s_pot;
+      for (int t2 = wave; t2 < T; t2 += (int)(blockDim.x >> 6)) {
+        const double rr = __shfl(ut, t2) * pot;
+        const double tol = cum_tol(a.exact, n, rr);
+        const int c0 = __popcll(__ballot(lane < nb && cl < rr));
+        int idx;
+        bool amb;
+        if (c0 >= nb) {
+          idx = n;
+          amb = fabs(__shfl(cl, nb - 1) - rr) <= tol;
+        } else {
+          const int e = c0 * Bk + lane;
+          const bool live = lane < Bk && e < n;
+          const double v = live ? s_cum[min(e, n - 1)] : 0.0;
+          idx = c0 * Bk + __popcll(__ballot(live && v < rr));
+          const double prev = __shfl(cl, c0 > 0 ? c0 - 1 : 0);
+          amb = __ballot(live && fabs(v - rr) <= tol) != 0ull || (c0 > 0 && fabs(prev - rr) <= tol);
+        }
+        if (amb) {
+          int rep = 0;
+          if (lane == 0) rep = (int)np_cumsum_search(s_d, a.w, n, rr);
+          idx = __shfl(rep, 0);
+        }
+        if (lane == 0) cand_out[t2] = min(n - 1, idx);
+      }
     }
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 74);
@@ -1757,7 +1795,7 @@ __global__ __launch_bounds__(256) void k_kpp1_fused(Kpp1Args a, int c) {
   if (!s_last) return;
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 62);
   // ---- fold trial t (its last workgroup): the row back with sc1 loads
-  const double ut = (c + 1 < a.k && tid < T) ? a.uniforms[(int64_t)c * T + tid] : 0.0;
+  const double ut = (c + 1 < a.k && (tid & 63) < T) ? a.uniforms[(int64_t)c * T + (tid & 63)] : 0.0;
   float r[16];
   {
     const float* row = a.dist[cq] + (int64_t)t * n;
@@ -1838,7 +1876,7 @@ __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __rest
     pv[q] = a.potv[pq][min(q, Tp - 1)];
     cw[q] = a.candw[pq][(int64_t)min(q, Tp - 1) * T + t];
   }
-  const double ut = (c + 1 < a.k && tid < T) ? a.uniforms[(int64_t)c * T + tid] : 0.0;
+  const double ut = (c + 1 < a.k && (tid & 63) < T) ? a.uniforms[(int64_t)c * T + (tid & 63)] : 0.0;
   int bw = 0;  // np.argmin: first minimum, a NaN wins at once
   float best = pv[0];
   int64_t ct = cw[0];
@@ -1945,8 +1983,8 @@ __global__ __launch_bounds__(256) void k_kpp1_dm2(Kpp1Args a, const float* __res
       a.indices[c - 1] = a.candself2[pl][j];
     }
   }
-  const double ut = (c + 1 < a.k && tid < T) ? a.uniforms[(int64_t)c * T + tid] : 0.0;
-  const double ut2 = (pair && c + 2 < a.k && tid < T) ? a.uniforms[(int64_t)(c + 1) * T + tid] : 0.0;
+  const double ut = (c + 1 < a.k && (tid & 63) < T) ? a.uniforms[(int64_t)c * T + (tid & 63)] : 0.0;
+  const double ut2 = (pair && c + 2 < a.k && (tid & 63) < T) ? a.uniforms[(int64_t)(c + 1) * T + (tid & 63)] : 0.0;
   if (tid == 0 && (!pair || t2 == 0)) a.candself[lq][w] = ct;
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && g == 0 && c == a.k - 3 + (a.k & 1)), 61);
   // trip 2: the closest distances and the candidate's table row
@@ -2231,6 +2269,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     b1.indices = indices;
     b1.plan = a.plan;
     b1.exact = a.exact;
+    b1.bsearch = getenv("GDD_KPP_BSEARCH") != nullptr ? 1 : 0;
     if (seq) {
       k_kpp_xt<<<(unsigned)((n * dim + 255) / 256), 256, 0, s>>>((int)n, dim, X, XT);
       GDD_LAUNCHED();

@@ -112,10 +112,11 @@ def test_kmeans_plusplus_round_forms(monkeypatch, n, dim, k):
     """Every single-block round form gives the oracle's seeding, bit for bit: two rounds per launch
     over the distance table (default for plain-chain plans, dim <= 48, k >= 16, T <= 8), one round
     per launch over the table (GDD_KPP_SINGLE_ROUND), and the fused distance + fold rounds
-    (GDD_KPP_NO_TABLE)."""
+    (GDD_KPP_NO_TABLE); the folds' two-ballot searches (default) and binary searches
+    (GDD_KPP_BSEARCH)."""
     X = np.ascontiguousarray(synth.blobs(n, dim, max(2, k // 4), seed=n + dim + 1), np.float32)
     c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
-    for var in (None, "GDD_KPP_SINGLE_ROUND", "GDD_KPP_NO_TABLE"):
+    for var in (None, "GDD_KPP_SINGLE_ROUND", "GDD_KPP_NO_TABLE", "GDD_KPP_BSEARCH"):
         if var:
             monkeypatch.setenv(var, "1")
         ops = _Ops("cuda", n, k, dim)
@@ -164,11 +165,13 @@ def _kpp_dev(X, k, T, first, u, w=None):
 
 
 # (n, env): every search form — the pick count (round 0 of the single-block paths and the two-launch
-# rounds), the fold's binary search (table pair / single rounds, fused rounds), the multi-block
-# round (per-(block, trial) and the split pick launch)
+# rounds), the fold's two-ballot search (default) and binary search (GDD_KPP_BSEARCH) in the table
+# pair / single rounds and the fused rounds, the multi-block round (per-(block, trial) and the split
+# pick launch)
 CUMSUM_FORMS = [
     (1000, ()), (4096, ()), (1000, ("GDD_KPP_SINGLE_ROUND",)), (1000, ("GDD_KPP_NO_TABLE",)),
-    (1000, ("GDD_KPP_NO_TABLE", "GDD_KPP_TWO_LAUNCH")), (9000, ()), (530000, ()),
+    (1000, ("GDD_KPP_NO_TABLE", "GDD_KPP_TWO_LAUNCH")), (1000, ("GDD_KPP_BSEARCH",)),
+    (4096, ("GDD_KPP_SINGLE_ROUND", "GDD_KPP_BSEARCH")), (9000, ()), (530000, ()),
 ]
 
 

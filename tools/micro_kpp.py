@@ -53,7 +53,8 @@ def run(n, dim, k, reps, check=True):
 def ab(n=3000, dim=40, k=454):
     """Same-process A/B of the round variants (devices differ by up to ~10% in clock), and of the
     cumulative-potential rounding check (GDD_KPP_EXACT: 0 off, 1 default, 2 replay every draw)."""
-    for var, val in (("", ""), ("GDD_KPP_SINGLE_ROUND", "1"), ("GDD_KPP_NO_TABLE", "1"),
+    for var, val in (("", ""), ("GDD_KPP_BSEARCH", "1"), ("", ""), ("GDD_KPP_BSEARCH", "1"),
+                     ("GDD_KPP_SINGLE_ROUND", "1"), ("GDD_KPP_NO_TABLE", "1"),
                      ("GDD_KPP_EXACT", "0"), ("", ""), ("GDD_KPP_EXACT", "2")):
         if var:
             os.environ[var] = val
