@@ -376,6 +376,174 @@ __global__ __launch_bounds__(256) void k_assign_persist(int64_t n, int dim, int 
   }
 }
 
+// Wave-tile variant (default for dimp <= 96): the same tiles, chains, order and key merge as
+// k_assign_persist (bit-exact), but every wave walks 32-point tiles of its own (t = global wave id,
+// + all waves) through its own LDS slot, so the tile loop has no workgroup barrier: the waves of a
+// SIMD drift apart and one wave's MFMA chain covers another's staging and argmin epilogue (the
+// persistent form synchronised all its waves twice per 128-point tile). With contiguous rows (no
+// row list) a tile is 32 consecutive rows = one contiguous run of 32*dim floats, fetched as float4
+// (coalesced, 16-byte aligned for any dim since 32*dim*4 is a multiple of 16) and scattered into the
+// zero-padded LDS rows; with a row list, two lanes per row as in k_assign_persist. The centre chunk
+// is staged once per block; W waves per block share it (W = 12 at the products shape: 3 per SIMD).
+// F: float4 per lane of a contiguous tile (6: dim <= 48); a row-list tile uses 4F elements per lane
+// (two lanes per row). Wider rows (dim 49..96) keep k_assign_persist: their prefetched tile would
+// spill at three waves per SIMD.
+template <int NT, int W, bool CONTIG, int F>
+__global__ __launch_bounds__(64 * W) void k_assign_waves(int64_t n, int dim, int dimp,
+                                                         const float* __restrict__ X,
+                                                         const int64_t* __restrict__ rows, int k,
+                                                         const float* __restrict__ C,
+                                                         const float* __restrict__ cn2, int cch,
+                                                         unsigned long long* __restrict__ keys,
+                                                         const int32_t* __restrict__ stop, int step_i) {
+  if (stopped(stop, step_i)) return;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int S = dimp + 1;
+  const int c0 = blockIdx.y * cch;
+  const int nc = min(k, c0 + cch) - c0;
+  const int ncp = (nc + 31) & ~31;
+  float* Cl = lds;
+  float* Nl = Cl + (size_t)ncp * S;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  float* Pw = Nl + ncp + (size_t)wave * 32 * S;
+  for (int idx = tid; idx < ncp * dimp; idx += blockDim.x) {
+    const int r = idx / dimp, c = idx - r * dimp;
+    Cl[r * S + c] = (r < nc && c < dim) ? C[(int64_t)(c0 + r) * dim + c] : 0.f;
+  }
+  for (int idx = tid; idx < ncp; idx += blockDim.x) Nl[idx] = idx < nc ? cn2[c0 + idx] : 0.f;
+  // the padding columns of the wave's rows stay zero (the scatter below writes columns < dim only)
+  for (int idx = lane; idx < 32 * S; idx += 64) Pw[idx] = 0.f;
+  __syncthreads();  // the only workgroup barrier: the centre chunk is read-only from here on
+  const int64_t ntiles = (n + 31) / 32;
+  const int64_t stride = (int64_t)gridDim.x * W;
+  int64_t t = (int64_t)blockIdx.x * W + wave;
+  const int tot = 32 * dim;  // floats per full tile
+  const float rdim = 1.0f / (float)dim;
+  float4 v4[CONTIG ? F : 1];
+  float v[CONTIG ? 1 : 4 * F];
+  const int pr = lane >> 1, ph = lane & 1;
+  const int half = (dim + 1 - ph) >> 1;
+  auto fetch = [&](int64_t tt) {
+    if constexpr (CONTIG) {
+      const int64_t base = tt * 32 * (int64_t)dim;
+      const int64_t lim = n * (int64_t)dim - base;  // floats left in X from the tile start
+      const float* xt = X + base;
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        const int e = 4 * (lane + 64 * j);
+        if (e + 3 < tot && e + 3 < lim) {
+          v4[j] = *reinterpret_cast<const float4*>(xt + e);
+        } else {  // the tile's (or X's) ragged end
+          float q[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) q[u] = (e + u < tot && e + u < lim) ? xt[e + u] : 0.f;
+          v4[j] = make_float4(q[0], q[1], q[2], q[3]);
+        }
+      }
+    } else {
+      const int64_t pi = tt * 32 + pr;
+      const bool ok = pi < n;
+      const float* xr = X + (ok ? (rows ? rows[pi] : pi) : 0) * dim;
+#pragma unroll
+      for (int j = 0; j < 4 * F; ++j) v[j] = xr[min(ph + 2 * j, dim - 1)];
+      if (!ok) {
+#pragma unroll
+        for (int j = 0; j < 4 * F; ++j) v[j] = 0.f;
+      }
+    }
+  };
+  auto stage = [&]() {
+    if constexpr (CONTIG) {
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        const int e = 4 * (lane + 64 * j);
+        const float q[4] = {v4[j].x, v4[j].y, v4[j].z, v4[j].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int ee = e + u;
+          if (ee < tot) {
+            // ee / dim by the fp32 reciprocal (ee < 3072: exact operands), corrected by one step
+            int r = (int)((float)ee * rdim);
+            int c = ee - r * dim;
+            if (c < 0) {
+              --r;
+              c += dim;
+            } else if (c >= dim) {
+              ++r;
+              c -= dim;
+            }
+            Pw[r * S + c] = q[u];
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4 * F; ++j) {
+        const int c = ph + 2 * j;
+        if (c < dim) Pw[pr * S + c] = (j < half) ? v[j] : 0.f;
+      }
+    }
+  };
+  if (t < ntiles) fetch(t);
+  const int kh = lane >> 5;
+  const float* bp = Pw + (lane & 31) * S + kh;
+  const int ns = dimp >> 1;
+  for (; t < ntiles; t += stride) {
+    // this wave's previous tile is done with its slot (the wave's LDS reads return in order)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    stage();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (t + stride < ntiles) fetch(t + stride);  // in flight during this tile's MFMAs
+    unsigned long long best = ~0ull;
+    auto pass = [&](auto M_, int ct) {
+      constexpr int M = decltype(M_)::value;
+      const float* ap[M];
+#pragma unroll
+      for (int q = 0; q < M; ++q) ap[q] = Cl + (ct + 32 * q + (lane & 31)) * S + kh;
+      floatx16 acc[M];
+#pragma unroll
+      for (int q = 0; q < M; ++q) acc[q] = floatx16{};
+      for (int s0 = 0; s0 < ns; s0 += 8) {
+        float a[M][8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int o = 2 * (s0 + u);
+#pragma unroll
+          for (int q = 0; q < M; ++q) a[q][u] = ap[q][o];
+          bv[u] = bp[o];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+#pragma unroll
+          for (int q = 0; q < M; ++q)
+            acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][u], bv[u], acc[q], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < M; ++q)
+        best = tile_best(acc[q], Nl + ct + 32 * q, c0 + ct + 32 * q, kh, c0 + nc, best);
+    };
+    int ct = 0;
+    for (; ct + 32 * NT <= ncp; ct += 32 * NT) pass(std::integral_constant<int, NT>(), ct);
+    if (ct < ncp) pass(std::integral_constant<int, 1>(), ct);
+    const unsigned long long other = __shfl_xor(best, 32);
+    best = other < best ? other : best;
+    if (lane < 32) {
+      const int64_t pi = t * 32 + lane;
+      if (pi < n && best != ~0ull) {
+        if (gridDim.y == 1)
+          keys[pi] = best;
+        else
+          atomicMin(keys + pi, best);
+      }
+    }
+  }
+}
+
 // ---- bf16 distance variant (configs 2, 3 and 5 carry fp32 and bf16 distances) ----
 // Same block shape and key merge as k_assign, but the X and C tiles are rounded to bf16 (nearest
 // even) in LDS and each 32x32 tile is a chain of v_mfma_f32_32x32x16_bf16 (fp32 accumulate). The
@@ -1390,7 +1558,53 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
     };
     // two centre tiles per pass: four accumulator chains would need 292 registers, one wave per SIMD
     // (measured 1.38 vs 0.91 ms at the products shape)
-    int rc0 = go(k_assign_persist<2>);
+    static const bool persist = getenv("GDD_ASSIGN_PERSIST") != nullptr;  // A/B: the r02 form
+    int rc0;
+    if (persist || dimp16 > 48) {  // wave tiles: dim <= 48 (every config's k-means input)
+      rc0 = go(k_assign_persist<2>);
+    } else {
+      // wave tiles: as many waves per block as the LDS holds with every centre in one chunk (the
+      // centre chunk is staged once per block), at least 4; else the persistent form's chunks.
+      // 12 waves (768 threads) leave 170 registers per lane: two chains and the prefetched tile
+      // without spills, three waves per SIMD
+      int Wn = 0;
+      for (int wv : {12, 8, 4})
+        if (Wn == 0 && assign_lds(wv, dimp16, (k + 31) & ~31) <= 150 * 1024) Wn = wv;
+      const int cchw = Wn ? ((k + 31) & ~31) : cch;
+      if (!Wn) Wn = 4;
+      const int gyw = (k + cchw - 1) / cchw;
+      const size_t ldsw = assign_lds(Wn, dimp16, cchw);
+      const int64_t wtiles = (n + 31) / 32;
+      const bool contig = rows == nullptr && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+      int dev = 0, cus = 0, occ = 0;
+      GDD_HIP(hipGetDevice(&dev));
+      GDD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      if (gyw > 1 && gy == 1) {
+        k_fill_u64<<<blocks_for(n), 256, 0, s>>>(n, keys, ~0ull, stop, step_i);
+        GDD_LAUNCHED();
+      }
+      auto gow = [&](auto kern, int wv) -> int {
+        if (ldsw > 65536)
+          GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsw));
+        GDD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64 * wv, ldsw));
+        const int64_t per = std::max<int64_t>(1, (int64_t)std::max(occ, 1) * cus / gyw);
+        const int64_t gxw = std::min<int64_t>((wtiles + wv - 1) / wv, per);
+        kern<<<dim3((unsigned)gxw, (unsigned)gyw), 64 * wv, ldsw, s>>>(n, dim, dimp16, X, rows, k, C,
+                                                                      c_norm2, cchw, keys, stop, step_i);
+        GDD_LAUNCHED();
+        return GDD_OK;
+      };
+      auto pick = [&](auto W_) -> int {
+        constexpr int Wc = decltype(W_)::value;
+        return contig ? gow(k_assign_waves<2, Wc, true, 6>, Wc) : gow(k_assign_waves<2, Wc, false, 6>, Wc);
+      };
+      if (Wn == 12)
+        rc0 = pick(std::integral_constant<int, 12>());
+      else if (Wn == 8)
+        rc0 = pick(std::integral_constant<int, 8>());
+      else
+        rc0 = pick(std::integral_constant<int, 4>());
+    }
     if (rc0) return rc0;
     k_assign_finalize<<<blocks_for(n), 256, 0, s>>>(n, dim, X, rows, C, keys, labels, sq_dist, stop,
                                                     step_i);

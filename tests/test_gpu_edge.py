@@ -33,6 +33,38 @@ def test_assign_edges(n, dim, k):
     assert np.array_equal(bits(sq.cpu().numpy()), bits(sq_ref))
 
 
+@pytest.mark.parametrize("n,dim,k,mode", [
+    (40001, 47, 196, "contig"),   # products' row width: 12 waves per block, ragged last tile
+    (20003, 1, 33, "contig"),     # n * dim not a multiple of 4: the scalar tail of the float4 fetch
+    (30000, 3, 454, "contig"),
+    (16385, 48, 900, "contig"),   # centres past one LDS chunk: chunked, atomically merged keys
+    (25000, 41, 769, "contig"),   # Reddit's shape class
+    (33000, 40, 454, "rows"),     # a row list: two lanes per gathered row
+    (20001, 47, 196, "offset"),   # X not 16-byte aligned: the per-row fetch without a row list
+])
+def test_assign_large_n_wave_tiles(n, dim, k, mode):
+    """The large-n labels pass (wave tiles, k_assign_waves) is the oracle's assignment bit for bit."""
+    rng = np.random.default_rng(n + k)
+    X = (rng.standard_normal((n, dim)) * 3).astype(np.float32)
+    C = X[rng.choice(n, size=k, replace=False)] + np.float32(0.01)
+    rows = rng.integers(0, n, n).astype(np.int64) if mode == "rows" else None
+    lab_ref, sq_ref = O.assign(X, C, rows=rows)
+    if mode == "offset":
+        buf = torch.empty(n * dim + 1, dtype=torch.float32, device="cuda")
+        Xd = buf[1:].view(n, dim)
+        Xd.copy_(torch.from_numpy(X))
+        assert Xd.data_ptr() % 16 != 0
+    else:
+        Xd = torch.from_numpy(X).cuda()
+    lab = torch.empty(n, dtype=torch.int32, device="cuda")
+    sq = torch.empty(n, dtype=torch.float32, device="cuda")
+    _Ops("cuda", n, k, dim).assign(Xd, torch.from_numpy(np.ascontiguousarray(C)).cuda(),
+                                   rows=None if rows is None else torch.from_numpy(rows).cuda(),
+                                   labels=lab, sq=sq)
+    assert np.array_equal(lab.cpu().numpy(), lab_ref)
+    assert np.array_equal(bits(sq.cpu().numpy()), bits(sq_ref))
+
+
 def test_assign_ties_between_tiles_and_zero_signs():
     # identical centres in different 32-centre tiles and chunks: the lowest index must win, also
     # when the distance is exactly zero (the packed key treats -0.0 and +0.0 as one value)

@@ -14,6 +14,7 @@
 #   phases                tools/phase_times.py (per-phase wall times of the bench step)
 #   kpp                   tools/micro_kpp.py (k-means++ round micro-benchmark)
 #   assign                tools/bench_assign.py (full assignment pass, fp32 vs bf16, three shapes)
+#   assign-ab             tools/bench_assign.py with the wave-tile fp32 pass vs GDD_ASSIGN_PERSIST=1
 #   hop-lanes             tools/micro_prop.py at arxiv / products with the XCD slice A/B switch
 #   prop-pair             tools/micro_prop.py at arxiv / products, paired target updates on / off
 #   reddit | products     tools/bench_induct.py | tools/bench_products.py (config 3 / 5 shapes)
@@ -61,6 +62,7 @@ for step in "$@"; do
     phases) run 300 phases python tools/phase_times.py ;;
     kpp) run 300 kpp python tools/micro_kpp.py ;;
     assign) run 300 assign python tools/bench_assign.py ;;
+    assign-ab) run 400 assign_ab bash -c 'python tools/bench_assign.py && GDD_ASSIGN_PERSIST=1 python tools/bench_assign.py && python tools/bench_assign.py' ;;
     hop-lanes) run 300 hop_lanes bash -c 'python tools/micro_prop.py && GDD_HOP_LANES=8 python tools/micro_prop.py && GDD_HOP_LANES=32 python tools/micro_prop.py && python tools/micro_prop.py products && GDD_HOP_LANES=8 python tools/micro_prop.py products' ;;
     prop-pair) run 300 prop_pair bash -c 'python tools/micro_prop.py && GDD_PROP_PAIR=0 python tools/micro_prop.py && python tools/micro_prop.py && GDD_PROP_PAIR=0 python tools/micro_prop.py && python tools/micro_prop.py products && GDD_PROP_PAIR=0 python tools/micro_prop.py products' ;;
     reddit) run 400 reddit python tools/bench_induct.py ;;
