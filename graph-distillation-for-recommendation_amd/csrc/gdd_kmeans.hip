@@ -1129,29 +1129,57 @@ struct MBState {
   int32_t pad[4];
 };
 
-// one thread; st->stop_at is published with an agent-scope atomic store (read by sibling blocks)
-__device__ void mb_converge(int step_i, int64_t bs, int64_t n, int max_no_improvement, float inertia,
-                            MBState* __restrict__ st) {
-  if (__hip_atomic_load(&st->stop_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+// one thread; st->stop_at is published with an agent-scope atomic store (read by sibling blocks).
+// The state is read into registers first (MbConv) — the tail block requests it before its inertia
+// fold, so the test after the fold costs no dependent memory trips; only this thread writes it.
+struct MbConv {
+  double ewa, ewa_min;
+  int32_t stop_at, has_ewa, has_min, no_improvement;
+};
+
+__device__ __forceinline__ MbConv mb_conv_load(const MBState* __restrict__ st) {
+  MbConv c;
+  c.stop_at = __hip_atomic_load(&st->stop_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  c.ewa = st->ewa;
+  c.ewa_min = st->ewa_min;
+  c.has_ewa = st->has_ewa;
+  c.has_min = st->has_min;
+  c.no_improvement = st->no_improvement;
+  return c;
+}
+
+__device__ void mb_converge_from(MbConv c, int step_i, int64_t bs, int64_t n, int max_no_improvement,
+                                 float inertia, MBState* __restrict__ st) {
+  if (c.stop_at) return;
   const double bi = (double)inertia / (double)bs;
   if (step_i == 0) return;  // the first step's inertia is the init's
-  if (!st->has_ewa) {
-    st->ewa = bi;
-    st->has_ewa = 1;
+  if (!c.has_ewa) {
+    c.ewa = bi;
+    c.has_ewa = 1;
   } else {
     double a = (double)bs * 2.0 / (double)(n + 1);
     a = a < 1.0 ? a : 1.0;
-    st->ewa = st->ewa * (1.0 - a) + bi * a;
+    c.ewa = c.ewa * (1.0 - a) + bi * a;
   }
-  if (!st->has_min || st->ewa < st->ewa_min) {
-    st->no_improvement = 0;
-    st->ewa_min = st->ewa;
-    st->has_min = 1;
+  if (!c.has_min || c.ewa < c.ewa_min) {
+    c.no_improvement = 0;
+    c.ewa_min = c.ewa;
+    c.has_min = 1;
   } else {
-    st->no_improvement += 1;
+    c.no_improvement += 1;
   }
-  if (max_no_improvement >= 0 && st->no_improvement >= max_no_improvement)
+  st->ewa = c.ewa;
+  st->ewa_min = c.ewa_min;
+  st->has_ewa = c.has_ewa;
+  st->has_min = c.has_min;
+  st->no_improvement = c.no_improvement;
+  if (max_no_improvement >= 0 && c.no_improvement >= max_no_improvement)
     __hip_atomic_store(&st->stop_at, step_i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ void mb_converge(int step_i, int64_t bs, int64_t n, int max_no_improvement, float inertia,
+                            MBState* __restrict__ st) {
+  mb_converge_from(mb_conv_load(st), step_i, bs, n, max_no_improvement, inertia, st);
 }
 
 // sequential fp32 inertia of one batch by one workgroup (staged in LDS 2048 at a time; lane 0
@@ -1192,10 +1220,12 @@ struct MbTail {
 };
 
 __device__ void mb_tail_block(const MbTail& tl, float* stage) {
+  MbConv c{};
+  if (threadIdx.x == 0 && tl.converge) c = mb_conv_load(tl.st);  // in flight during the fold
   const float inertia = mb_batch_inertia(tl.b, tl.sq, stage);
   if (threadIdx.x == 0) {
     tl.inertia[0] = inertia;
-    if (tl.converge) mb_converge(tl.step, tl.b, tl.n_samples, tl.max_ni, inertia, tl.st);
+    if (tl.converge) mb_converge_from(c, tl.step, tl.b, tl.n_samples, tl.max_ni, inertia, tl.st);
   }
 }
 
