@@ -14,6 +14,7 @@
 //   average / shift  _k_means_common.pyx:215-251
 // Loop control, RNG draws and rare branches (reassignment, relocation) live in the host layer.
 #include <algorithm>
+#include <mutex>
 #include <climits>
 #include <cstdlib>
 #include <type_traits>
@@ -1501,6 +1502,38 @@ extern "C" int gdd_row_norms(int64_t n, int dim, const float* X, float* out, gdd
 }
 
 namespace {
+// resident workgroups of a kernel on the current device (occupancy x CUs), cached per (device,
+// kernel, threads, LDS): the persistent launches size their grids by it on every call
+int resident_blocks(const void* fn, int threads, size_t lds, int* out) {
+  struct Entry {
+    int dev, threads;
+    const void* fn;
+    size_t lds;
+    int blocks;
+  };
+  static std::mutex mu;
+  static Entry cache[32];
+  static int used = 0;
+  int dev = 0;
+  GDD_HIP(hipGetDevice(&dev));
+  {
+    std::lock_guard<std::mutex> g(mu);
+    for (int i = 0; i < used; ++i)
+      if (cache[i].dev == dev && cache[i].fn == fn && cache[i].threads == threads && cache[i].lds == lds) {
+        *out = cache[i].blocks;
+        return GDD_OK;
+      }
+  }
+  int occ = 0, cus = 0;
+  GDD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, threads, lds));
+  GDD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  *out = std::max(occ, 1) * std::max(cus, 1);
+  std::lock_guard<std::mutex> g(mu);
+  cache[used % 32] = Entry{dev, threads, fn, lds, *out};
+  used = std::min(used + 1, 32);
+  return GDD_OK;
+}
+
 // LDS bytes of k_assign for a given geometry
 size_t assign_lds(int waves, int dimp, int cch) {
   const int S = dimp + 1;
@@ -1606,9 +1639,6 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
       const size_t ldsw = assign_lds(Wn, dimp16, cchw);
       const int64_t wtiles = (n + 31) / 32;
       const bool contig = rows == nullptr && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
-      int dev = 0, cus = 0, occ = 0;
-      GDD_HIP(hipGetDevice(&dev));
-      GDD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
       if (gyw > 1 && gy == 1) {
         k_fill_u64<<<blocks_for(n), 256, 0, s>>>(n, keys, ~0ull, stop, step_i);
         GDD_LAUNCHED();
@@ -1616,8 +1646,10 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
       auto gow = [&](auto kern, int wv) -> int {
         if (ldsw > 65536)
           GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsw));
-        GDD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64 * wv, ldsw));
-        const int64_t per = std::max<int64_t>(1, (int64_t)std::max(occ, 1) * cus / gyw);
+        int res = 0;
+        const int rrc = resident_blocks((const void*)kern, 64 * wv, ldsw, &res);
+        if (rrc) return rrc;
+        const int64_t per = std::max<int64_t>(1, (int64_t)res / gyw);
         const int64_t gxw = std::min<int64_t>((wtiles + wv - 1) / wv, per);
         kern<<<dim3((unsigned)gxw, (unsigned)gyw), 64 * wv, ldsw, s>>>(n, dim, dimp16, X, rows, k, C,
                                                                       c_norm2, cchw, keys, stop, step_i);
@@ -1746,11 +1778,10 @@ extern "C" int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const 
         constexpr int P = decltype(P_)::value;
         const void* fn = (const void*)k_assign_bf16p<P>;
         GDD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        int per_cu = 0, dev = 0, cus = 0;
-        GDD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds));
-        GDD_HIP(hipGetDevice(&dev));
-        GDD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        const int64_t resident = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
+        int res = 0;
+        const int rrc = resident_blocks(fn, 256, lds, &res);
+        if (rrc) return rrc;
+        const int64_t resident = res;
         const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 3) / 4, resident));
         k_assign_bf16p<P><<<grid, 256, lds, s>>>(n, dim, nsteps, ktiles, X, k, frags, cn, C, labels, sq_dist);
         GDD_LAUNCHED();

@@ -11,6 +11,7 @@
 #   pmc-bench             rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE / TCC hit+miss) of a short bench
 #                         with one target update per hop (GDD_PROP_PAIR=0: every k_hop launch is the
 #                         roofline's unpaired hop); summarise with tools/pmc_summary.py <dir>/pmcb ...
+#   lookahead-ab          bench.py (no CPU baseline) with GDD_MB_LOOKAHEAD = 1, 2, 3, 1, 2, 3
 #   phases                tools/phase_times.py (per-phase wall times of the bench step)
 #   kpp                   tools/micro_kpp.py (k-means++ round micro-benchmark)
 #   assign                tools/bench_assign.py (full assignment pass, fp32 vs bf16, three shapes)
@@ -59,6 +60,7 @@ for step in "$@"; do
       run 240 pmcb_fetch env GDD_PROP_PAIR=0 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcb/pmc_fetch" -o bench -- $B
       run 240 pmcb_write env GDD_PROP_PAIR=0 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcb/pmc_write" -o bench -- $B
       run 240 pmcb_hit env GDD_PROP_PAIR=0 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmcb/pmc_hit" -o bench -- $B ;;
+    lookahead-ab) run 900 lookahead_ab bash -c 'for la in 1 2 3 1 2 3; do echo "lookahead $la"; GDD_MB_LOOKAHEAD=$la python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
     phases) run 300 phases python tools/phase_times.py ;;
     kpp) run 300 kpp python tools/micro_kpp.py ;;
     assign) run 300 assign python tools/bench_assign.py ;;
