@@ -12,6 +12,8 @@
 #                         with one target update per hop (GDD_PROP_PAIR=0: every k_hop launch is the
 #                         roofline's unpaired hop); summarise with tools/pmc_summary.py <dir>/pmcb ...
 #   lookahead-ab          bench.py (no CPU baseline) with GDD_MB_LOOKAHEAD = 1, 2, 3, 1, 2, 3
+#   pmc-products          rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE / TCC hit+miss) of tools/micro_prop.py
+#                         products, the default hop and the 4-slice form (GDD_HOP_LANES=8)
 #   phases                tools/phase_times.py (per-phase wall times of the bench step)
 #   kpp                   tools/micro_kpp.py (k-means++ round micro-benchmark)
 #   assign                tools/bench_assign.py (full assignment pass, fp32 vs bf16, three shapes)
@@ -61,6 +63,13 @@ for step in "$@"; do
       run 240 pmcb_write env GDD_PROP_PAIR=0 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcb/pmc_write" -o bench -- $B
       run 240 pmcb_hit env GDD_PROP_PAIR=0 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmcb/pmc_hit" -o bench -- $B ;;
     lookahead-ab) run 900 lookahead_ab bash -c 'for la in 1 2 3 1 2 3; do echo "lookahead $la"; GDD_MB_LOOKAHEAD=$la python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
+    pmc-products)
+      for form in default lanes8; do
+        E="GDD_PROP_PAIR=0"; [ "$form" = lanes8 ] && E="GDD_PROP_PAIR=0 GDD_HOP_LANES=8"
+        run 300 pmcp_${form}_fetch env $E rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcp_$form/pmc_fetch" -o hop -- python3 tools/micro_prop.py products
+        run 300 pmcp_${form}_write env $E rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcp_$form/pmc_write" -o hop -- python3 tools/micro_prop.py products
+        run 300 pmcp_${form}_hit env $E rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmcp_$form/pmc_hit" -o hop -- python3 tools/micro_prop.py products
+      done ;;
     phases) run 300 phases python tools/phase_times.py ;;
     kpp) run 300 kpp python tools/micro_kpp.py ;;
     assign) run 300 assign python tools/bench_assign.py ;;
