@@ -716,6 +716,55 @@ __global__ void k_kpp_first(int64_t n, int dim, const float* __restrict__ X,
   for (int j = threadIdx.x; j < dim; j += blockDim.x) centers[j] = X[first_id * dim + j];
 }
 
+// the first centre's potential with unit weights for large n: the same 64 lane chains as
+// sdot_skx_wave (lane l adds entries l, l + 64, ... in order), with waves 1..15 staging chunks of
+// 256 x 64 entries (64 KB) into a two-slot LDS ring for wave 0 — one wave alone keeps only ~16 KB
+// of loads in flight (2.8 ms at 2.45M entries)
+constexpr int kFirstSteps = 256;  // 64-entry steps per staged chunk
+__global__ __launch_bounds__(1024) void k_kpp_first_big(int64_t n, int dim, const float* __restrict__ X,
+                                                        const float* __restrict__ closest0, int64_t first_id,
+                                                        KppState* __restrict__ st, float* __restrict__ centers,
+                                                        int64_t* __restrict__ indices) {
+  extern __shared__ __attribute__((aligned(16))) float ring[];  // 2 x kFirstSteps * 64 floats
+  __shared__ float scratch[192];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t n64 = n & ~63ll;
+  constexpr int kChunk = kFirstSteps * 64;
+  const int64_t nch = (n64 + kChunk - 1) / kChunk;
+  auto stage = [&](int64_t ch) {  // waves 1..15
+    float* dst = ring + (ch & 1) * kChunk;
+    const int64_t base = ch * kChunk;
+    for (int e = tid - 64; e < kChunk; e += 960) {
+      const int64_t i = base + e;
+      dst[e] = i < n64 ? closest0[i] : 0.f;
+    }
+  };
+  if (wave > 0 && nch > 0) stage(0);
+  __syncthreads();
+  float a = 0.f;
+  for (int64_t ch = 0; ch < nch; ++ch) {
+    if (wave > 0) {
+      if (ch + 1 < nch) stage(ch + 1);
+    } else {
+      const float* src = ring + (ch & 1) * kChunk + lane;
+      const int steps = (int)min<int64_t>(kFirstSteps, (n64 - ch * kChunk) >> 6);
+      for (int u = 0; u < steps; ++u) a = __builtin_fmaf(src[64 * u], 1.0f, a);
+    }
+    __syncthreads();
+  }
+  if (wave == 0) {
+    const int64_t ri = n64 + lane;
+    const float rx = ri < n ? closest0[ri] : 0.f;
+    const float ry = ri < n ? 1.0f : 0.f;
+    const float p = sdot_skx_finish(a, rx, ry, n, scratch);
+    if (lane == 0) {
+      st->pot = p;
+      indices[0] = first_id;
+    }
+    for (int j = lane; j < dim; j += 64) centers[j] = X[first_id * dim + j];
+  }
+}
+
 // T == 1: the single trial's potential is (1, n) @ (n, 1) -> sdot
 __global__ void k_kpp_pot1(int64_t n, const float* __restrict__ row, const float* __restrict__ w,
                            float* __restrict__ out) {
@@ -2057,11 +2106,23 @@ __global__ void k_kpp_gather_centres(int k, int dim, const float* __restrict__ X
 }
 
 // X^T (dim x n) for the single-block distance phase: coalesced loads
-__global__ void k_kpp_xt(int n, int dim, const float* __restrict__ X, float* __restrict__ XT) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * dim) return;
-  const int j = e / n, i = e - j * n;
-  XT[e] = X[(int64_t)i * dim + j];
+// X (n x dim) -> XT (dim x n) through 64 x 64 LDS tiles: rows read along the feature axis, columns
+// written along the point axis, both coalesced (the element-wise form read one line per element)
+constexpr int kXtTile = 64;
+__global__ __launch_bounds__(256) void k_kpp_xt(int n, int dim, const float* __restrict__ X,
+                                                float* __restrict__ XT) {
+  __shared__ float tile[kXtTile][kXtTile + 1];
+  const int i0 = blockIdx.x * kXtTile, j0 = blockIdx.y * kXtTile;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4 threads
+  for (int r = ty; r < kXtTile; r += 4) {
+    const int i = i0 + r, j = j0 + tx;
+    tile[r][tx] = (i < n && j < dim) ? X[(int64_t)i * dim + j] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < kXtTile; r += 4) {
+    const int j = j0 + r, i = i0 + tx;
+    if (j < dim && i < n) XT[(int64_t)j * n + i] = tile[tx][r];
+  }
 }
 
 // _euclidean_distances(C, X, squared=True) on its own (the distance of every round, exposed for
@@ -2243,12 +2304,19 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       GDD_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   }
   if (a.XT) {
-    k_kpp_xt<<<(unsigned)((n * dim + 255) / 256), 256, 0, s>>>((int)n, dim, X, XT);
+    k_kpp_xt<<<dim3((unsigned)((n + kXtTile - 1) / kXtTile), (unsigned)((dim + kXtTile - 1) / kXtTile)), 256, 0,
+               s>>>((int)n, dim, X, XT);
     GDD_LAUNCHED();
   }
   k_kpp_init<<<nblk, kThr, lds, s>>>(a, p1, first_id, xsq, closest0, fsum0);
   GDD_LAUNCHED();
-  k_kpp_first<<<1, 64, 0, s>>>(n, dim, X, w, closest0, first_id, st, centers, indices);
+  if (w == nullptr && n >= (int64_t)kFirstSteps * 64 * 2) {  // large n, unit weights: staged chains
+    const size_t fl = sizeof(float) * 2 * kFirstSteps * 64;
+    GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_first_big, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl));
+    k_kpp_first_big<<<1, 1024, fl, s>>>(n, dim, X, closest0, first_id, st, centers, indices);
+  } else {
+    k_kpp_first<<<1, 64, 0, s>>>(n, dim, X, w, closest0, first_id, st, centers, indices);
+  }
   GDD_LAUNCHED();
   if (k == 1) return GDD_OK;
   if (single) {
@@ -2271,7 +2339,8 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     b1.exact = a.exact;
     b1.bsearch = getenv("GDD_KPP_BSEARCH") != nullptr ? 1 : 0;
     if (seq) {
-      k_kpp_xt<<<(unsigned)((n * dim + 255) / 256), 256, 0, s>>>((int)n, dim, X, XT);
+      k_kpp_xt<<<dim3((unsigned)((n + kXtTile - 1) / kXtTile), (unsigned)((dim + kXtTile - 1) / kXtTile)), 256, 0,
+               s>>>((int)n, dim, X, XT);
       GDD_LAUNCHED();
     }
     const size_t lds1 = sizeof(double) * (size_t)T * std::max(dim, 48);

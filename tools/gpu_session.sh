@@ -72,6 +72,7 @@ for step in "$@"; do
       done ;;
     phases) run 300 phases python tools/phase_times.py ;;
     kpp) run 300 kpp python tools/micro_kpp.py ;;
+    kpp-products) run 300 kpp_products python tools/micro_kpp_products.py ;;
     assign) run 300 assign python tools/bench_assign.py ;;
     assign-ab) run 400 assign_ab bash -c 'python tools/bench_assign.py && GDD_ASSIGN_PERSIST=1 python tools/bench_assign.py && python tools/bench_assign.py' ;;
     hop-lanes) run 300 hop_lanes bash -c 'python tools/micro_prop.py && GDD_HOP_LANES=8 python tools/micro_prop.py && GDD_HOP_LANES=32 python tools/micro_prop.py && python tools/micro_prop.py products && GDD_HOP_LANES=8 python tools/micro_prop.py products' ;;
