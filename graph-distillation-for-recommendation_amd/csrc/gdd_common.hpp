@@ -86,6 +86,32 @@ int mb_loop_begin(int64_t b, int k, void* ws, size_t ws_bytes, hipStream_t s);
 int mb_loop_end(int64_t b, int k, int last_step, int64_t n_samples, int max_no_improvement,
                 void* state, void* ws, size_t ws_bytes, hipStream_t s);
 int mb_rng_launch(const DevMT* in, DevMT* out, int64_t n, int64_t bs, int64_t* rows, hipStream_t s);
+// one-launch steps of the device loop (k_mb_fused): the update of step upd_step (do_update) and the
+// assignment of step assign_step (do_assign) in one launch, plus the tail of step tail_step (>= 0)
+struct MbFusedCall {
+  int64_t b;
+  int dim;
+  const float* X;
+  int k;
+  int64_t n_samples;
+  int max_no_improvement;
+  void* state;
+  void* step_ws;
+  size_t step_ws_bytes;
+  unsigned long long* keys3;  // three key buffers of b entries (step j uses j % 3), ~0 initially
+  int do_update, do_assign;
+  int upd_step, assign_step, tail_step;
+  int gate;  // the launch is skipped once the stop word places step `gate` past the stop
+  const int64_t* rows_prev;  // batch upd_step
+  const int64_t* rows_cur;   // batch assign_step
+  const float* C_old;        // centres before the update (or the lone assignment's centres)
+  float* C_new;
+  const float* W_old;
+  float* W_new;
+  int norms_valid;  // lone assignment: the workspace norms match C_old
+};
+bool mb_fused_ok(int64_t b, int dim, int k);
+int mb_fused_launch(const MbFusedCall& c, const RngNext& rn, hipStream_t s);
 int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const float* X,
                        const int64_t* rows, float* C_new, float* counts, void* step_ws,
                        size_t step_ws_bytes, const DevMT* mt_in, DevMT* mt_mid, const RngNext& rn,

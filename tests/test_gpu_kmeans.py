@@ -245,3 +245,41 @@ def test_center_columns_matches_numpy(n, dim):
     assert np.array_equal(mean.cpu().numpy().view(np.uint32), m.view(np.uint32))
     assert np.array_equal(var.cpu().numpy().view(np.uint32), np.var(X, axis=0).view(np.uint32))
     assert np.array_equal(out.cpu().numpy().view(np.uint32), (X - m).view(np.uint32))
+
+
+# One-launch MiniBatch steps (k_mb_fused, opt-in with GDD_MB_FUSED=1): bit-identical to
+# scikit-learn and to the default two-launch loop on centres, labels, inertia, n_steps_ and
+# the RandomState left behind — across key-buffer groups (G = 1 and 4), row forms (dim % 4 != 0),
+# member rows over several LDS passes (GDD_MB_FUSED_MCAP), with and without reassignment, early
+# stopping and running to max_iter (the last step's lone update).
+@pytest.mark.parametrize("n,dim,k,bs,ratio,max_iter,mcap", [
+    (20000, 40, 454, 1000, 0.01, 100, None),
+    (5000, 40, 50, 1000, 0.01, 100, None),
+    (8000, 7, 70, 300, 0.01, 100, None),
+    (6000, 64, 200, 512, 0.01, 100, None),
+    (20000, 40, 454, 1000, 0.01, 100, 16),
+    (20000, 40, 454, 1000, 0.0, 100, None),
+    (3000, 12, 100, 2048, 0.5, 100, 40),
+    (12000, 40, 300, 1000, 0.01, 1, None),
+])
+def test_minibatch_fused_steps_match(monkeypatch, n, dim, k, bs, ratio, max_iter, mcap):
+    X = synth.blobs(n, dim, k, seed=n + k)
+    rs_ref = np.random.RandomState(15)
+    ref = O.minibatch_kmeans(X, k, random_state=rs_ref, batch_size=bs, reassignment_ratio=ratio,
+                             max_iter=max_iter)
+    if mcap:
+        monkeypatch.setenv("GDD_MB_FUSED_MCAP", str(mcap))
+    fits = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("GDD_MB_FUSED", fused)
+        rs = np.random.RandomState(15)
+        m = gdd.MiniBatchKMeans(n_clusters=k, random_state=rs, batch_size=bs,
+                                reassignment_ratio=ratio, max_iter=max_iter).fit(X)
+        fits.append((m, rs))
+    for m, rs in fits:
+        assert m.n_steps_ == ref["n_steps_"]
+        assert np.array_equal(m.labels_, ref["labels_"])
+        assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"]))
+        assert m.inertia_ == ref["inertia_"]
+        s1, s2 = rs_ref.get_state(), rs.get_state()
+        assert np.array_equal(s1[1], s2[1]) and s1[2] == s2[2]

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""In-kernel phase stamps of the MiniBatchKMeans step and k-means++ kernels (diagnostic build).
+"""In-kernel phase stamps (fused step: 60 start, 61 trip 1, 62 members sorted, 63 member rows in LDS,
+64 chains done, 65 point tile ready, 66 keys out; 70-74 the same for an update alone) of the MiniBatchKMeans step and k-means++ kernels (diagnostic build).
 
 Build: make -C graph-distillation-for-recommendation_amd/csrc STAMPS=1
 Run:   python tools/stamps.py   (uses lib/libgdd_stamps.so; stamps are s_memrealtime, 10 ns ticks)
@@ -45,6 +46,8 @@ def main():
         a = read(lib, "kmeans")
         p = read(lib, "kpp")
         print(f"rep {rep}: steps={km.n_steps_}")
+        show("fused step block0", a, list(range(60, 67)), 60)
+        show("update alone block0", a, list(range(70, 75)), 70)
         show("assign_small", a, [0, 2, 3, 4, 5, 6, 13, 14, 15, 16, 82, 80, 83, 81], 0)
         show("update block0", a, list(range(20, 26)), 20)
         show("update tail", a, list(range(30, 33)), 30)
