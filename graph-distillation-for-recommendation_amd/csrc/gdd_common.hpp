@@ -123,6 +123,12 @@ int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const 
 int kmeans_assign_dev(int64_t n, int dim, const float* X, int k, const float* C, float* cn2,
                       int32_t* labels, unsigned long long* keys, const int32_t* stop, int step_i,
                       hipStream_t s);
+// the bounded Lloyd E-step (gdd_lloyd.hip): top-2 distances of a (device-counted) row list
+bool lloyd_prune_ok(int dim, int k);
+int kmeans_assign_top2_dev(int64_t n_max, int dim, const float* X, const int64_t* rows,
+                           const int64_t* n_dev, int k, const float* C, float* cn2,
+                           unsigned long long* keys, float* sec, const int32_t* stop, int step_i,
+                           hipStream_t s);
 
 // `stop` (nullable) points at a device stop word (0 = running, s+1 = a test fired at step s; the
 // MiniBatch MBState::stop_at, the Lloyd LloydState::stop_at). Kernels of a later step return at

@@ -137,6 +137,30 @@ __device__ __forceinline__ unsigned long long tile_best(const floatx16& acc, con
   return key < best ? key : best;
 }
 
+// tile_best plus the second-smallest distance value (any other centre), for the Lloyd loop's
+// distance bounds: `bd` is the value packed in `best`, `sec` the smallest value among the rest
+__device__ __forceinline__ void tile_top2(const floatx16& acc, const float* Nw, int cb, int kh, int k,
+                                          unsigned long long& best, float& bd, float& sec) {
+  float nv[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) nv[r] = Nw[(r & 3) + 8 * (r >> 2) + 4 * kh];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int ci = cb + (r & 3) + 8 * (r >> 2) + 4 * kh;
+    const float d = __builtin_fmaf(-2.f, acc[r], nv[r]);
+    if (ci < k) {
+      const unsigned long long key = pack_key(d, ci);
+      if (key < best) {
+        sec = fminf(sec, bd);
+        best = key;
+        bd = d;
+      } else {
+        sec = fminf(sec, d);
+      }
+    }
+  }
+}
+
 __global__ void k_fill_u64(int64_t n, unsigned long long* p, unsigned long long v,
                            const int32_t* __restrict__ stop, int step_i) {
   if (stopped(stop, step_i)) return;
@@ -389,15 +413,20 @@ __global__ __launch_bounds__(256) void k_assign_persist(int64_t n, int dim, int 
 // F: float4 per lane of a contiguous tile (6: dim <= 48); a row-list tile uses 4F elements per lane
 // (two lanes per row). Wider rows (dim 49..96) keep k_assign_persist: their prefetched tile would
 // spill at three waves per SIMD.
-template <int NT, int W, bool CONTIG, int F>
+// TOP2 (one centre chunk, gridDim.y == 1): also sec[i] = the second-smallest distance of row i;
+// n_dev (nullable): the row count is read on the device (a row list built by an earlier kernel).
+template <int NT, int W, bool CONTIG, int F, bool TOP2 = false>
 __global__ __launch_bounds__(64 * W) void k_assign_waves(int64_t n, int dim, int dimp,
                                                          const float* __restrict__ X,
                                                          const int64_t* __restrict__ rows, int k,
                                                          const float* __restrict__ C,
                                                          const float* __restrict__ cn2, int cch,
                                                          unsigned long long* __restrict__ keys,
-                                                         const int32_t* __restrict__ stop, int step_i) {
+                                                         const int32_t* __restrict__ stop, int step_i,
+                                                         float* __restrict__ sec = nullptr,
+                                                         const int64_t* __restrict__ n_dev = nullptr) {
   if (stopped(stop, step_i)) return;
+  if (n_dev) n = *n_dev;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int S = dimp + 1;
   const int c0 = blockIdx.y * cch;
@@ -500,6 +529,7 @@ __global__ __launch_bounds__(64 * W) void k_assign_waves(int64_t n, int dim, int
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (t + stride < ntiles) fetch(t + stride);  // in flight during this tile's MFMAs
     unsigned long long best = ~0ull;
+    float bd = __builtin_inff(), sd = __builtin_inff();
     auto pass = [&](auto M_, int ct) {
       constexpr int M = decltype(M_)::value;
       const float* ap[M];
@@ -525,13 +555,21 @@ __global__ __launch_bounds__(64 * W) void k_assign_waves(int64_t n, int dim, int
         }
       }
 #pragma unroll
-      for (int q = 0; q < M; ++q)
-        best = tile_best(acc[q], Nl + ct + 32 * q, c0 + ct + 32 * q, kh, c0 + nc, best);
+      for (int q = 0; q < M; ++q) {
+        if constexpr (TOP2)
+          tile_top2(acc[q], Nl + ct + 32 * q, c0 + ct + 32 * q, kh, c0 + nc, best, bd, sd);
+        else
+          best = tile_best(acc[q], Nl + ct + 32 * q, c0 + ct + 32 * q, kh, c0 + nc, best);
+      }
     };
     int ct = 0;
     for (; ct + 32 * NT <= ncp; ct += 32 * NT) pass(std::integral_constant<int, NT>(), ct);
     if (ct < ncp) pass(std::integral_constant<int, 1>(), ct);
     const unsigned long long other = __shfl_xor(best, 32);
+    if constexpr (TOP2) {  // merge the two half-waves' (best, second) pairs
+      const float obd = __shfl_xor(bd, 32), osd = __shfl_xor(sd, 32);
+      sd = fminf(fminf(sd, osd), other < best ? bd : obd);
+    }
     best = other < best ? other : best;
     if (lane < 32) {
       const int64_t pi = t * 32 + lane;
@@ -540,6 +578,7 @@ __global__ __launch_bounds__(64 * W) void k_assign_waves(int64_t n, int dim, int
           keys[pi] = best;
         else
           atomicMin(keys + pi, best);
+        if constexpr (TOP2) sec[pi] = sd;
       }
     }
   }
@@ -2068,7 +2107,8 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
         const int64_t per = std::max<int64_t>(1, (int64_t)res / gyw);
         const int64_t gxw = std::min<int64_t>((wtiles + wv - 1) / wv, per);
         kern<<<dim3((unsigned)gxw, (unsigned)gyw), 64 * wv, ldsw, s>>>(n, dim, dimp16, X, rows, k, C,
-                                                                      c_norm2, cchw, keys, stop, step_i);
+                                                                      c_norm2, cchw, keys, stop, step_i,
+                                                                      nullptr, nullptr);
         GDD_LAUNCHED();
         return GDD_OK;
       };
@@ -2147,6 +2187,53 @@ int kmeans_assign_dev(int64_t n, int dim, const float* X, int k, const float* C,
   k_row_norms<<<blocks_for(k), 256, 0, s>>>(k, dim, C, cn2, stop, step_i);
   GDD_LAUNCHED();
   return launch_assign(n, dim, X, nullptr, k, C, cn2, labels, nullptr, keys, stop, step_i, s);
+}
+
+// the Lloyd loop's bounded E-step needs the top-2 wave-tile pass with every centre in one chunk
+static int top2_waves(int dim, int k) {
+  const int dimp16 = (dim + 15) & ~15;
+  if (dimp16 > 48) return 0;
+  for (int wv : {12, 8, 4})
+    if (assign_lds(wv, dimp16, (k + 31) & ~31) <= 150 * 1024) return wv;
+  return 0;
+}
+
+bool lloyd_prune_ok(int dim, int k) { return top2_waves(dim, k) > 0; }
+
+// ||C||^2 into cn2, then keys[p] (packed best distance + centre) and sec[p] (second-smallest
+// distance) for rows p < *n_dev (rows[p] with a row list, else p); n_max bounds the grid
+int kmeans_assign_top2_dev(int64_t n_max, int dim, const float* X, const int64_t* rows,
+                           const int64_t* n_dev, int k, const float* C, float* cn2,
+                           unsigned long long* keys, float* sec, const int32_t* stop, int step_i,
+                           hipStream_t s) {
+  const int Wn = top2_waves(dim, k);
+  GDD_REQUIRE(Wn > 0 && n_max > 0, "assign_top2: unsupported shape");
+  k_row_norms<<<blocks_for(k), 256, 0, s>>>(k, dim, C, cn2, stop, step_i);
+  GDD_LAUNCHED();
+  const int dimp16 = (dim + 15) & ~15;
+  const int cch = (k + 31) & ~31;
+  const size_t lds = assign_lds(Wn, dimp16, cch);
+  const int64_t wtiles = (n_max + 31) / 32;
+  const bool contig = rows == nullptr && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+  auto go = [&](auto kern, int wv) -> int {
+    if (lds > 65536)
+      GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int res = 0;
+    const int rrc = resident_blocks((const void*)kern, 64 * wv, lds, &res);
+    if (rrc) return rrc;
+    const int64_t gx = std::max<int64_t>(1, std::min<int64_t>((wtiles + wv - 1) / wv, res));
+    kern<<<dim3((unsigned)gx, 1), 64 * wv, lds, s>>>(n_max, dim, dimp16, X, rows, k, C, cn2, cch, keys,
+                                                     stop, step_i, sec, n_dev);
+    GDD_LAUNCHED();
+    return GDD_OK;
+  };
+  auto pick = [&](auto W_) -> int {
+    constexpr int Wc = decltype(W_)::value;
+    return contig ? go(k_assign_waves<2, Wc, true, 6, true>, Wc) : go(k_assign_waves<2, Wc, false, 6, true>, Wc);
+  };
+  if (Wn == 12) return pick(std::integral_constant<int, 12>());
+  if (Wn == 8) return pick(std::integral_constant<int, 8>());
+  return pick(std::integral_constant<int, 4>());
 }
 }  // namespace gdd
 

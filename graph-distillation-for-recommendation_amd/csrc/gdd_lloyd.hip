@@ -667,6 +667,181 @@ __global__ void k_relocate_distances(int64_t n, int dim, const float* __restrict
   out[i] = pw_sum<kPwDepth>([&](int j) { const float d = x[j] - cr[j]; return d * d; }, 0, dim);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Bounded E-step (Hamerly's bounds, kept exact). Per row: ub >= ||x - C[label]|| and
+// lb <= min over the other centres of ||x - c|| (true Euclidean distances, fp64). sklearn's label
+// is the argmin of its computed d~(x, c) = fma(-2, <x,c>_fp32 chain, ||c||^2_fp32), and
+// |d~(x, c) - (||x - c||^2 - ||x||^2)| <= E(x) = kappa (||x|| + max ||c||)^2 with
+// kappa = (2 dim + 8) 2^-24 (the dot product's gamma_dim, the norm's gamma_dim and the final
+// rounding). So when L = max(lb, sep[label] - ub) satisfies L^2 - ub^2 > 2 E(x), every other
+// centre's computed distance exceeds the label's strictly and the label stands (sklearn's argmin,
+// ties included). Rows failing the test get their full top-2 distance row (the same MFMA chains as
+// the unbounded pass) and fresh bounds: ub^2 = d~1 + ||x||^2 + E, lb^2 = d~2 + ||x||^2 - E. Between
+// iterations ub grows by the label's centre shift and lb shrinks by the largest shift (both
+// rounded up from sklearn's fp32 shifts).
+// ---------------------------------------------------------------------------------------------
+constexpr double kEps32 = 5.9604644775390625e-08;  // 2^-24
+
+// ||x|| in fp64 (upward margin); a block stages its 64 rows through LDS with coalesced loads
+__global__ __launch_bounds__(256) void k_row_norm64(int64_t n, int dim, const float* __restrict__ X,
+                                                   double* __restrict__ xn) {
+  __shared__ float s_x[64 * 49];  // dim <= 48 (the bounded E-step's shapes)
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  const int rows = (int)min<int64_t>(64, n - r0);
+  const float* src = X + r0 * dim;
+  for (int e = threadIdx.x; e < rows * dim; e += blockDim.x) s_x[(e / dim) * (dim + 1) + e % dim] = src[e];
+  __syncthreads();
+  if ((int)threadIdx.x >= rows) return;
+  const float* x = s_x + threadIdx.x * (dim + 1);
+  double s = 0.0;
+  for (int f = 0; f < dim; ++f) s = __builtin_fma((double)x[f], (double)x[f], s);
+  xn[r0 + threadIdx.x] = __builtin_sqrt(s) * (1.0 + 1e-12);
+}
+
+// block c < k: sep[c] <= min over c' != c of ||C_c - C_c'||; block k: glob[0] >= max ||C_c||,
+// glob[1] >= the largest centre shift (0 without shifts), and the failing-row counter cleared
+__global__ __launch_bounds__(256) void k_ham_centres(int k, int dim, const float* __restrict__ C,
+                                                     const float* __restrict__ shift, int have_shift,
+                                                     double* __restrict__ sep, double* __restrict__ glob,
+                                                     int64_t* __restrict__ count,
+                                                     const int32_t* stop, int step_i) {
+  if (stopped(stop, step_i)) return;
+  __shared__ double red[2][256];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const double inf = __builtin_inf();
+  if (c < k) {
+    double m = inf;
+    const float* cr = C + (int64_t)c * dim;
+    for (int o = tid; o < k; o += blockDim.x) {
+      if (o == c) continue;
+      const float* orow = C + (int64_t)o * dim;
+      double s2 = 0.0;
+      for (int f = 0; f < dim; ++f) {
+        const double d = (double)cr[f] - (double)orow[f];
+        s2 = __builtin_fma(d, d, s2);
+      }
+      m = fmin(m, s2);
+    }
+    red[0][tid] = m;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+      if (tid < w) red[0][tid] = fmin(red[0][tid], red[0][tid + w]);
+      __syncthreads();
+    }
+    if (tid == 0) sep[c] = red[0][0] == inf ? inf : __builtin_sqrt(red[0][0]) * (1.0 - 1e-12);
+  } else {
+    double cm = 0.0, dm = 0.0;
+    for (int o = tid; o < k; o += blockDim.x) {
+      const float* orow = C + (int64_t)o * dim;
+      double s2 = 0.0;
+      for (int f = 0; f < dim; ++f) s2 = __builtin_fma((double)orow[f], (double)orow[f], s2);
+      cm = fmax(cm, s2);
+      if (have_shift) dm = fmax(dm, (double)shift[o]);
+    }
+    red[0][tid] = cm;
+    red[1][tid] = dm;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+      if (tid < w) {
+        red[0][tid] = fmax(red[0][tid], red[0][tid + w]);
+        red[1][tid] = fmax(red[1][tid], red[1][tid + w]);
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      glob[0] = __builtin_sqrt(red[0][0]) * (1.0 + 1e-12);
+      glob[1] = red[1][0] * (1.0 + (dim + 8) * kEps32) + 1e-18;
+      *count = 0;
+    }
+  }
+}
+
+// the test, per row; failing rows are listed in index order inside each block's 4096-row range (one
+// counter add per block: a single word takes ~90 adds per us, so one add per 256 rows cost ~0.1 ms)
+constexpr int kHamRows = 16;  // rows per thread (strided by 256 inside the block's range)
+__global__ __launch_bounds__(256) void k_ham_test(int64_t n, int dim, const int32_t* __restrict__ labels,
+                                                  const double* __restrict__ xn, double* __restrict__ ub,
+                                                  double* __restrict__ lb, const float* __restrict__ shift,
+                                                  const double* __restrict__ sep,
+                                                  const double* __restrict__ glob, double kappa,
+                                                  int64_t* __restrict__ list, int64_t* __restrict__ count,
+                                                  const int32_t* stop, int step_i) {
+  if (stopped(stop, step_i)) return;
+  __shared__ int s_wc[kHamRows][4];
+  __shared__ int64_t s_base;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * 256 * kHamRows;
+  const double sscale = 1.0 + (dim + 8) * kEps32;
+  const double cmax = glob[0], dmax = glob[1];
+  unsigned long long masks[kHamRows];
+#pragma unroll
+  for (int q = 0; q < kHamRows; ++q) {
+    const int64_t i = r0 + q * 256 + tid;
+    bool fail = false;
+    if (i < n) {
+      const int a = labels[i];
+      const double u = ub[i] + ((double)shift[a] * sscale + 1e-18);
+      const double l = lb[i] - dmax;
+      const double L = fmax(l, sep[a] - u);
+      const double xm = xn[i] + cmax;
+      const double E = kappa * xm * xm;
+      fail = !(L > u * (1.0 + 1e-12) && (L - u) * (L + u) > 2.0 * E);
+      ub[i] = u;
+      lb[i] = l;
+    }
+    masks[q] = __ballot(fail);
+    if (lane == 0) s_wc[q][wave] = __popcll(masks[q]);
+  }
+  __syncthreads();
+  if (tid == 0) {  // exclusive offsets in row order (q-major, then wave)
+    int tot = 0;
+    for (int q = 0; q < kHamRows; ++q)
+      for (int w = 0; w < 4; ++w) {
+        const int c = s_wc[q][w];
+        s_wc[q][w] = tot;
+        tot += c;
+      }
+    s_base = tot ? (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(count), (unsigned long long)tot) : 0;
+  }
+  __syncthreads();
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int q = 0; q < kHamRows; ++q)
+    if ((masks[q] >> lane) & 1ull)
+      list[s_base + s_wc[q][wave] + __popcll(masks[q] & below)] = r0 + q * 256 + tid;
+}
+
+// rows p < m (list[p], or p when list is null): label and fresh bounds from the top-2 pass
+__global__ __launch_bounds__(256) void k_ham_finalize(const int64_t* __restrict__ count, int64_t n_all,
+                                                      const int64_t* __restrict__ list,
+                                                      const unsigned long long* __restrict__ keys,
+                                                      const float* __restrict__ sec,
+                                                      const double* __restrict__ xn,
+                                                      const double* __restrict__ glob, double kappa,
+                                                      int32_t* __restrict__ labels, double* __restrict__ ub,
+                                                      double* __restrict__ lb, const int32_t* stop,
+                                                      int step_i) {
+  if (stopped(stop, step_i)) return;
+  const int64_t m = list ? *count : n_all;
+  const double cmax = glob[0];
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < m;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = list ? list[p] : p;
+    const unsigned long long key = keys[p];
+    const unsigned hi = (unsigned)(key >> 32);
+    const float d1 = __uint_as_float((hi & 0x80000000u) ? (hi & 0x7fffffffu) : ~hi);  // pack_key inverse
+    const float d2 = sec[p];
+    const double x = xn[i];
+    const double xm = x + cmax;
+    const double E = kappa * xm * xm;
+    const double xlo = x / (1.0 + 3e-12);
+    labels[i] = (int32_t)(unsigned)(key & 0xffffffffull);
+    ub[i] = __builtin_sqrt(fmax(0.0, (double)d1 + x * x + E)) * (1.0 + 1e-12);
+    lb[i] = __builtin_isinf(d2) ? __builtin_inf()
+                                : __builtin_sqrt(fmax(0.0, (double)d2 + xlo * xlo - E)) * (1.0 - 1e-12);
+  }
+}
 }  // namespace
 }  // namespace gdd
 
@@ -742,11 +917,18 @@ extern "C" int gdd_relocate_distances(int64_t n, int dim, const float* X, const 
 // ---- the device-resident Lloyd loop -----------------------------------------------------------------
 extern "C" size_t gdd_lloyd_state_bytes(void) { return sizeof(LloydState); }
 
+// the bounded E-step's buffers: ||x|| (fp64), the two bounds (fp64), the failing-row list, second
+// distances, a counter, the centre separations and two global bounds
+static size_t prune_ws(int64_t n, int k) {
+  return 4 * align256(sizeof(double) * (size_t)n) + align256(sizeof(float) * (size_t)n) +
+         align256(sizeof(double) * (size_t)k) + 3 * 256;
+}
+
 extern "C" size_t gdd_kmeans_lloyd_ws_bytes(int64_t n, int dim, int k) {
   (void)dim;
   return align256(sizeof(unsigned long long) * (size_t)n) + align256(sizeof(float) * (size_t)k) +
          align256(sizeof(int32_t) * (size_t)n) + align256(sizeof(int32_t) * (size_t)(k + 1)) +
-         group_ws(n, k) + 1024;
+         group_ws(n, k) + prune_ws(n, k) + 1024;
 }
 
 extern "C" size_t gdd_kmeans_lloyd_host_ws_bytes(void) { return 4 * sizeof(LloydState); }
@@ -772,7 +954,25 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
   int32_t* offsets = cv.take<int32_t>(k + 1);
   const size_t gb = group_ws(n, k);
   void* gws = cv.take<char>(gb);
+  double* xn = cv.take<double>(n);
+  double* ub = cv.take<double>(n);
+  double* lb = cv.take<double>(n);
+  int64_t* list = cv.take<int64_t>(n);
+  float* sec = cv.take<float>(n);
+  double* sep = cv.take<double>(k);
+  double* glob = cv.take<double>(2);
+  int64_t* count = cv.take<int64_t>(1);
   if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans_lloyd_run: workspace too small");
+  // bounded E-steps (GDD_LLOYD_PRUNE=0: every row every iteration), from the run's first E-step on
+  const char* pe = getenv("GDD_LLOYD_PRUNE");
+  const bool prune = !(pe && pe[0] == '0') && lloyd_prune_ok(dim, k);
+  const int prune_first = resume ? it0 + 1 : it0;
+  const double kappa = (2.0 * dim + 8.0) * kEps32;
+  const unsigned fgrid = std::min<unsigned>(blocks_of(n), 2048);
+  if (prune) {
+    k_row_norm64<<<blocks_of(n, 64), 256, 0, s>>>(n, dim, X, xn);
+    GDD_LAUNCHED();
+  }
   LloydState* st = static_cast<LloydState*>(state);
   LloydState* hs = static_cast<LloydState*>(host_ws);
   // a fresh run (or a resume after the host's relocation) starts with the stop word clear; the
@@ -786,8 +986,27 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
     float* cout = (i & 1) ? C0 : C1;
     const int sa = 2 * i, sb = 2 * i + 1;
     if (phase_a) {
-      int rc = kmeans_assign_dev(n, dim, X, k, cin, cn2, labels, keys, &st->stop_at, sa, s);
-      if (rc) return rc;
+      int rc;
+      if (prune) {
+        const bool first = i == prune_first;
+        k_ham_centres<<<k + 1, 256, 0, s>>>(k, dim, cin, shift, first ? 0 : 1, sep, glob, count,
+                                            &st->stop_at, sa);
+        GDD_LAUNCHED();
+        if (!first) {
+          k_ham_test<<<blocks_of(n, 256 * kHamRows), 256, 0, s>>>(n, dim, labels, xn, ub, lb, shift, sep, glob, kappa,
+                                                 list, count, &st->stop_at, sa);
+          GDD_LAUNCHED();
+        }
+        rc = kmeans_assign_top2_dev(n, dim, X, first ? nullptr : list, first ? nullptr : count, k, cin,
+                                    cn2, keys, sec, &st->stop_at, sa, s);
+        if (rc) return rc;
+        k_ham_finalize<<<fgrid, 256, 0, s>>>(count, n, first ? nullptr : list, keys, sec, xn, glob,
+                                             kappa, labels, ub, lb, &st->stop_at, sa);
+        GDD_LAUNCHED();
+      } else {
+        rc = kmeans_assign_dev(n, dim, X, k, cin, cn2, labels, keys, &st->stop_at, sa, s);
+        if (rc) return rc;
+      }
       rc = group_dev(n, labels, k, perm, offsets, gws, gb, &st->stop_at, sa, s);
       if (rc) return rc;
       fa.out = cout;

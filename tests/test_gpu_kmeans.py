@@ -283,3 +283,43 @@ def test_minibatch_fused_steps_match(monkeypatch, n, dim, k, bs, ratio, max_iter
         assert m.inertia_ == ref["inertia_"]
         s1, s2 = rs_ref.get_state(), rs.get_state()
         assert np.array_equal(s1[1], s2[1]) and s1[2] == s2[2]
+
+
+# Bounded Lloyd E-steps (GDD_LLOYD_PRUNE, on by default where the top-2 pass fits): a row whose
+# bounds prove its label skips the distance pass. Labels, centres, inertia and n_iter_ must equal
+# the unbounded loop's bit for bit (and the oracle's where it is quick), also on data made of
+# near-ties: duplicated rows, rows on the midpoint of two others, a symmetric lattice.
+def _near_tie_data(n, dim, seed):
+    rng = np.random.default_rng(seed)
+    X = synth.blobs(n, dim, 12, seed=seed)
+    q = n // 8
+    X[:q] = X[q:2 * q]                                  # duplicated rows
+    a, b = rng.integers(2 * q, n, q), rng.integers(2 * q, n, q)
+    X[2 * q:3 * q] = (X[a] + X[b]) * np.float32(0.5)    # midpoints
+    g = np.stack(np.meshgrid(*[np.arange(3, dtype=np.float32)] * min(dim, 3)), -1).reshape(-1, min(dim, 3))
+    m = min(len(g), q)
+    X[3 * q:3 * q + m, :g.shape[1]] = g[:m]             # a lattice: exact distance ties
+    return np.ascontiguousarray(X, np.float32)
+
+
+@pytest.mark.parametrize("n,dim,k,near_ties", [(40000, 47, 196, False), (30000, 40, 454, False),
+                                               (20000, 7, 70, True), (16000, 3, 27, True),
+                                               (12000, 16, 1, False), (24000, 48, 100, True)])
+def test_kmeans_lloyd_bounded_estep_matches(monkeypatch, n, dim, k, near_ties):
+    X = _near_tie_data(n, dim, n + dim) if near_ties else synth.blobs(n, dim, max(2, k // 2), seed=n + k)
+    fits = []
+    for prune in ("1", "0"):
+        monkeypatch.setenv("GDD_LLOYD_PRUNE", prune)
+        np.random.seed(15)
+        fits.append(gdd.KMeans(n_clusters=k, n_init=1).fit(X))
+    a, b = fits
+    assert a.n_iter_ == b.n_iter_
+    assert np.array_equal(a.labels_, b.labels_)
+    assert np.array_equal(bits(a.cluster_centers_), bits(b.cluster_centers_))
+    assert a.inertia_ == b.inertia_
+    if n * k <= 2_000_000:
+        np.random.seed(15)
+        ref = O.kmeans(X, k, n_init=1)
+        assert a.n_iter_ == ref["n_iter_"]
+        assert np.array_equal(a.labels_, ref["labels_"])
+        assert np.array_equal(bits(a.cluster_centers_), bits(ref["cluster_centers_"]))

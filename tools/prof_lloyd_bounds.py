@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Bounded Lloyd E-step diagnostics at the ogbn-products k-means shape (2,449,029 x 47, k = 196):
+wall time of a fixed-iteration fit with the bounds on and off (GDD_LLOYD_PRUNE), on Gaussian
+"logits" (no cluster structure: the hard case) and on blobs. Run under rocprofv3 --kernel-trace
+for the per-kernel split (k_ham_test, the top-2 pass over the failing rows, k_ham_finalize)."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "graph-distillation-for-recommendation_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import gdd  # noqa: E402
+from gdd import synth  # noqa: E402
+
+
+def fit_ms(X, k, iters):
+    np.random.seed(15)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    km = gdd.KMeans(n_clusters=k, max_iter=iters).fit(X)
+    _ = km.labels_
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) * 1e3, int(km.n_iter_)
+
+
+def main(n=2449029, dim=47, k=196, iters=int(os.environ.get("ITERS", "300"))):
+    g = torch.Generator(device="cuda").manual_seed(3)
+    W = torch.randn(100, dim, device="cuda", generator=g) / 10.0
+    data = {
+        "gaussian_logits": (torch.randn(n, 100, device="cuda", generator=g) @ W).contiguous(),
+        "blobs": torch.from_numpy(synth.blobs(n, dim, k, seed=2)).cuda(),
+    }
+    for name, X in data.items():
+        for prune in ("1", "0", "1"):
+            os.environ["GDD_LLOYD_PRUNE"] = prune
+            ms, it = fit_ms(X, k, iters)
+            print(f"{name:16s} prune={prune}: {it} iterations, {ms:.1f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()
