@@ -323,3 +323,22 @@ def test_kmeans_lloyd_bounded_estep_matches(monkeypatch, n, dim, k, near_ties):
         assert a.n_iter_ == ref["n_iter_"]
         assert np.array_equal(a.labels_, ref["labels_"])
         assert np.array_equal(bits(a.cluster_centers_), bits(ref["cluster_centers_"]))
+
+
+@pytest.mark.parametrize("prune", ["1", "0"])
+def test_kmeans_lloyd_relocation_with_bounds(monkeypatch, prune):
+    """Fewer distinct points than clusters: k-means++ picks duplicate centres, so clusters go empty
+    and are relocated (sklearn _relocate_empty_clusters) — the loop resumes and the bounds restart."""
+    rng = np.random.default_rng(21)
+    base = rng.standard_normal((40, 8)).astype(np.float32)
+    X = np.ascontiguousarray(np.repeat(base, 60, axis=0)[rng.permutation(2400)])  # 40 distinct rows
+    k = 48  # > 40: duplicate centres, empty clusters, relocation (oracle == single-thread sklearn)
+    monkeypatch.setenv("GDD_LLOYD_PRUNE", prune)
+    np.random.seed(15)
+    ref = O.kmeans(X, k, n_init=1)
+    np.random.seed(15)
+    m = gdd.KMeans(n_clusters=k, n_init=1).fit(X)
+    assert m.n_iter_ == ref["n_iter_"]
+    assert np.array_equal(m.labels_, ref["labels_"])
+    assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"]))
+    assert m.inertia_ == ref["inertia_"]
