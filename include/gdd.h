@@ -244,6 +244,9 @@ int gdd_relocate_distances(int64_t n, int dim, const float* X, const int32_t* la
 /* *out_done (the caller relocates on C[(i+1)%2]/wsum, then calls again with it0=i, resume=1).      */
 /* Otherwise *out_done = iterations completed. labels_old starts as -1 (the caller fills it).      */
 /* state: gdd_lloyd_state_bytes() of device memory; host_ws: pinned, gdd_kmeans_lloyd_host_ws_bytes. */
+/* For dim <= 48 with every centre in one LDS chunk, the E-step is bounded: a row whose Hamerly      */
+/* bounds, widened by the fp32 rounding margin, prove sklearn's argmin keeps its label skips the     */
+/* distance pass (labels identical; the workspace holds the bounds; GDD_LLOYD_PRUNE=0 disables).     */
 size_t gdd_lloyd_state_bytes(void);
 size_t gdd_kmeans_lloyd_ws_bytes(int64_t n, int dim, int k);
 size_t gdd_kmeans_lloyd_host_ws_bytes(void);
