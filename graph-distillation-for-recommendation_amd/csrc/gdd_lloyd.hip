@@ -232,6 +232,9 @@ constexpr int kFoldMaxR = 1024;
 
 struct FoldArgs {
   int dim, fw_max, R;
+  // clusters of at least big_rows members (0: none) are folded in feature slices of fw_big columns,
+  // one workgroup per slice, R_big rows per chunk; Rmax = max(R, R_big) sizes the LDS id ring
+  int big_rows, fw_big, R_big, Rmax;
   int c0;                  // first cluster of this launch; outputs are indexed from c0 (a slice)
   const float* X;
   const float* w;          // Lloyd sample weights (nullable: unit weights)
@@ -296,16 +299,22 @@ __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int U = VEC ? 4 : 1;            // floats per staged element
   constexpr int Q = kFoldElems / (256 * U);  // staged elements per thread per chunk
-  const int R = a.R, dim = a.dim, tid = threadIdx.x;
-  float* Bbuf = smem;
-  int32_t* sid = reinterpret_cast<int32_t*>(smem + 2 * kFoldElems);  // 3 x R
-  float* Wbuf = smem + 2 * kFoldElems + 3 * R;                         // 3 x R (WEIGHTED)
+  const int dim = a.dim, tid = threadIdx.x;
   const int c = a.c0 + (int)blockIdx.y;
-  const int f0 = blockIdx.x * a.fw_max;
-  const int FW = min(a.fw_max, dim - f0);
-  const int FWu = FW / U;
   const int32_t b = a.offsets[c], e = a.offsets[c + 1];
   const int nm = e - b;
+  // a large cluster's columns are split over the grid's x slices (each column's chain is its own,
+  // so the order is unchanged): its CU gathers a third of each row instead of the whole row
+  const bool big = a.big_rows > 0 && nm >= a.big_rows;
+  const int fw = big ? a.fw_big : a.fw_max;
+  const int f0 = blockIdx.x * fw;
+  if (f0 >= dim) return;  // a slice only large clusters use
+  const int R = big ? a.R_big : a.R;
+  float* Bbuf = smem;
+  int32_t* sid = reinterpret_cast<int32_t*>(smem + 2 * kFoldElems);  // 3 x Rmax
+  float* Wbuf = smem + 2 * kFoldElems + 3 * a.Rmax;                    // 3 x Rmax (WEIGHTED)
+  const int FW = min(fw, dim - f0);
+  const int FWu = FW / U;
   ACC acc = 0;
   float wacc = 0.f;
   if (nm > 0) {
@@ -462,9 +471,20 @@ int fold_launch_one(const FoldArgs& a0, int count, bool mean, hipStream_t s) {
   R &= ~15;
   a.R = std::max(R, 16);
   const bool vec = a.dim % 4 == 0 && a.fw_max % 4 == 0 && (reinterpret_cast<uintptr_t>(a.X) & 15) == 0;
-  const unsigned nsl = (unsigned)((a.dim + a.fw_max - 1) / a.fw_max);
+  unsigned nsl = (unsigned)((a.dim + a.fw_max - 1) / a.fw_max);
+  constexpr int kSliceCols = 16;  // columns per slice of a large cluster (a multiple of 4)
+  if (a.big_rows > 0 && !mean && a.fw_max > kSliceCols) {
+    a.fw_big = kSliceCols;
+    a.R_big = std::max(16, std::min(kFoldMaxR, elems / kSliceCols) & ~15);
+    nsl = std::max<unsigned>(nsl, (unsigned)((a.dim + kSliceCols - 1) / kSliceCols));
+  } else {
+    a.big_rows = 0;
+    a.fw_big = a.fw_max;
+    a.R_big = a.R;
+  }
+  a.Rmax = std::max(a.R, a.R_big);
   if (count == 0) return GDD_OK;
-  const size_t lds = sizeof(float) * (2 * (size_t)elems + 3 * (size_t)a.R * (weighted ? 2 : 1));
+  const size_t lds = sizeof(float) * (2 * (size_t)elems + 3 * (size_t)a.Rmax * (weighted ? 2 : 1));
   dim3 grid(nsl, (unsigned)count);
   auto go = [&](auto kern) -> int {
     GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -863,7 +883,7 @@ extern "C" int gdd_segment_sum_f32(int64_t n, int dim, const float* X, const flo
                                    float* wsum, gdd_stream_t stream) {
   GDD_REQUIRE(n > 0 && dim > 0 && k > 0 && X && perm && offsets && sums && wsum,
               "segment_sum_f32: bad arguments");
-  FoldArgs a{dim, 0, 0, 0, X, w, perm, offsets, sums, wsum, nullptr, 0, nullptr, 0};
+  FoldArgs a{dim, 0, 0, 0, 0, 0, 0, 0, X, w, perm, offsets, sums, wsum, nullptr, 0, nullptr, 0};
   return fold_launch(a, k, false, to_hip(stream));
 }
 
@@ -874,7 +894,7 @@ extern "C" int gdd_segment_sum_f32_part(int64_t n, int dim, const float* X, cons
   GDD_REQUIRE(n > 0 && dim > 0 && k > 0 && 0 <= c0 && c0 <= c1 && c1 <= k && X && perm && offsets &&
                   (c0 == c1 || (sums_part && wsum_part)),
               "segment_sum_f32_part: bad arguments");
-  FoldArgs a{dim, 0, 0, c0, X, w, perm, offsets, sums_part, wsum_part, nullptr, 0, nullptr, 0};
+  FoldArgs a{dim, 0, 0, 0, 0, 0, 0, c0, X, w, perm, offsets, sums_part, wsum_part, nullptr, 0, nullptr, 0};
   return fold_launch(a, c1 - c0, false, to_hip(stream));
 }
 
@@ -883,7 +903,7 @@ extern "C" int gdd_cluster_mean(int64_t n, int d, const float* feat, const int32
                                 long long* counts, gdd_stream_t stream) {
   GDD_REQUIRE(n > 0 && d > 0 && k > 0 && feat && perm && offsets && feat_syn,
               "cluster_mean: bad arguments");
-  FoldArgs a{d, 0, 0, 0, feat, nullptr, perm, offsets, feat_syn, nullptr, counts, empty_as_zero, nullptr, 0};
+  FoldArgs a{d, 0, 0, 0, 0, 0, 0, 0, feat, nullptr, perm, offsets, feat_syn, nullptr, counts, empty_as_zero, nullptr, 0};
   return fold_launch(a, k, true, to_hip(stream));
 }
 
@@ -893,7 +913,7 @@ extern "C" int gdd_cluster_mean_part(int64_t n, int d, const float* feat, const 
   GDD_REQUIRE(n > 0 && d > 0 && k > 0 && 0 <= c0 && c0 <= c1 && c1 <= k && feat && perm && offsets &&
                   (c0 == c1 || feat_part),
               "cluster_mean_part: bad arguments");
-  FoldArgs a{d, 0, 0, c0, feat, nullptr, perm, offsets, feat_part, nullptr, counts_part, empty_as_zero,
+  FoldArgs a{d, 0, 0, 0, 0, 0, 0, c0, feat, nullptr, perm, offsets, feat_part, nullptr, counts_part, empty_as_zero,
              nullptr, 0};
   return fold_launch(a, c1 - c0, true, to_hip(stream));
 }
@@ -979,7 +999,13 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
   // changed flag is kept on resume (the E-step that set it already ran)
   GDD_HIP(hipMemsetAsync(st, 0, offsetof(LloydState, changed), s));
   if (!resume) GDD_HIP(hipMemsetAsync(&st->changed, 0, sizeof(int32_t), s));
-  FoldArgs fa{dim, 0, 0, 0, X, nullptr, perm, offsets, nullptr, wsum, nullptr, 0, &st->stop_at, 0};
+  FoldArgs fa{dim, 0, 0, 0, 0, 0, 0, 0, X, nullptr, perm, offsets, nullptr, wsum, nullptr, 0, &st->stop_at, 0};
+  {  // M-step: clusters above GDD_FOLD_SLICE x the mean size (default 1.5; 0: off) fold in slices
+    const char* fe = getenv("GDD_FOLD_SLICE");
+    const double f = fe ? atof(fe) : 1.5;
+    const double rows = f * (double)n / (double)k;
+    fa.big_rows = f > 0.0 ? (int)std::min<double>(std::max(rows, 4096.0), (double)INT_MAX) : 0;
+  }
   const unsigned cgrid = std::min<unsigned>(blocks_of(n), 2048);
   auto enqueue = [&](int i, bool phase_a) -> int {
     float* cin = (i & 1) ? C1 : C0;

@@ -342,3 +342,31 @@ def test_kmeans_lloyd_relocation_with_bounds(monkeypatch, prune):
     assert np.array_equal(m.labels_, ref["labels_"])
     assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"]))
     assert m.inertia_ == ref["inertia_"]
+
+
+@pytest.mark.parametrize("dim", [47, 48])
+def test_kmeans_lloyd_sliced_fold_matches(monkeypatch, dim):
+    """Large clusters (>= 1.5x the mean size and >= 4096 members) fold in 16-column slices, one
+    workgroup each; every column's sequential chain is unchanged, so the fit is bit-identical to the
+    unsliced fold and to the oracle (dim 47: scalar staging, 48: 16-byte staging)."""
+    rng = np.random.default_rng(dim)
+    sizes = [14000, 9000, 2500, 1500, 1000, 700, 500, 400, 250, 150]  # skewed: two big clusters
+    centres = rng.standard_normal((len(sizes), dim)).astype(np.float32) * np.float32(4.0)
+    X = np.concatenate([c + rng.standard_normal((m, dim)).astype(np.float32) for c, m in zip(centres, sizes)])
+    X = np.ascontiguousarray(X[rng.permutation(len(X))], np.float32)
+    k = 10
+    fits = []
+    for sl in ("1.5", "0"):
+        monkeypatch.setenv("GDD_FOLD_SLICE", sl)
+        np.random.seed(15)
+        fits.append(gdd.KMeans(n_clusters=k, n_init=1).fit(X))
+    a, b = fits
+    assert np.bincount(a.labels_, minlength=k).max() >= 1.5 * len(X) / k  # some cluster is sliced
+    assert a.n_iter_ == b.n_iter_ and a.inertia_ == b.inertia_
+    assert np.array_equal(a.labels_, b.labels_)
+    assert np.array_equal(bits(a.cluster_centers_), bits(b.cluster_centers_))
+    np.random.seed(15)
+    ref = O.kmeans(X, k, n_init=1)
+    assert a.n_iter_ == ref["n_iter_"]
+    assert np.array_equal(a.labels_, ref["labels_"])
+    assert np.array_equal(bits(a.cluster_centers_), bits(ref["cluster_centers_"]))
