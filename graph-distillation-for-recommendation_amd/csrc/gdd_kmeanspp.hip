@@ -1117,12 +1117,16 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
 // cumulative-potential block total (block_prefix) and the sgemv_t block term (wave t).
 constexpr int kSplitMaxT = 8;
 constexpr int kSplitMinBlocks = 128;
+// T is a template argument: with a runtime trial count every (feature, trial) pair of the chain
+// loop became its own branch with an LDS read waited on before its four fmas (the r03 products
+// profile: ~40 G fp64 fma/s per CU, a quarter of the issue rate).
+template <int T>
 __global__ __launch_bounds__(kThr) void k_kpp_dists(KppArgs a, int c) {
   extern __shared__ double s_cs[];  // T * dim doubles (candidate rows), then T * kBlk floats
   __shared__ double s_wave[kWaves];
   __shared__ double s_cn[kSplitMaxT];
   const int blk = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int T = a.T, dim = a.dim;
+  const int dim = a.dim;
   const int pq = (c - 1) & 1, cq = c & 1;
   const int64_t n = a.n, j0 = (int64_t)blk * kBlk;
   const float* wrow = c == 1 ? a.closest0 : a.dist[pq] + (int64_t)a.winq[cq] * n;
@@ -1133,36 +1137,66 @@ __global__ __launch_bounds__(kThr) void k_kpp_dists(KppArgs a, int c) {
   if (tid < T) s_cn[tid] = a.xsq[a.cand[cq][tid]];
   __syncthreads();
   float* s_d = reinterpret_cast<float*>(s_cs + T * dim);
-  int64_t ix[kPer];
+  // feature f of point j0 + off[q] is xt[f * n + off[q]]: a wave-uniform row base plus a 32-bit
+  // lane offset, so each load takes one scalar base and no 64-bit vector address
+  const float* __restrict__ xt = a.XT + j0;
+  uint32_t off[kPer];
   double dot[kSplitMaxT][kPer];
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
     const int64_t i = j0 + tid + kThr * q;
-    ix[q] = i < n ? i : j0;
+    off[q] = i < n ? (uint32_t)(tid + kThr * q) : 0u;
 #pragma unroll
     for (int t = 0; t < kSplitMaxT; ++t) dot[t][q] = 0.0;
   }
-  int j = 0;
-  for (; j + 4 <= dim; j += 4) {
-    float u[4][kPer];
+  // The chains are bound by the latency of their XT loads (one wave per SIMD slot, no room in LDS
+  // to stage the block): D trips of G features each are in flight ahead of the fmas that use them.
+  constexpr int G = 1;  // features per trip: 4 spilled at T = 7 under the 128-VGPR cap of 1024 threads
+  constexpr int D = 3;
+  const int ntrip = dim / G;
+  float buf[D][G][kPer];
 #pragma unroll
-    for (int v = 0; v < 4; ++v)
+  for (int d = 0; d < D; ++d)
+    if (d < ntrip) {
 #pragma unroll
-      for (int q = 0; q < kPer; ++q) u[v][q] = a.XT[(int64_t)(j + v) * n + ix[q]];
+      for (int v = 0; v < G; ++v)
 #pragma unroll
-    for (int v = 0; v < 4; ++v)
+        for (int q = 0; q < kPer; ++q) buf[d][v][q] = (xt + (int64_t)(d * G + v) * n)[off[q]];
+    }
+  for (int tr0 = 0; tr0 < ntrip; tr0 += D) {
 #pragma unroll
-      for (int t = 0; t < kSplitMaxT; ++t)
-        if (t < T) {
-          const double cv = s_cs[t * dim + j + v];
+    for (int d = 0; d < D; ++d) {
+      const int tr = tr0 + d;
+      if (tr >= ntrip) break;
+      float u[G][kPer];
 #pragma unroll
-          for (int q = 0; q < kPer; ++q) dot[t][q] = __builtin_fma(cv, (double)u[v][q], dot[t][q]);
-        }
+      for (int v = 0; v < G; ++v)
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) u[v][q] = buf[d][v][q];
+      if (tr + D < ntrip) {
+#pragma unroll
+        for (int v = 0; v < G; ++v)
+#pragma unroll
+          for (int q = 0; q < kPer; ++q)
+            buf[d][v][q] = (xt + (int64_t)((tr + D) * G + v) * n)[off[q]];
+      }
+      const int jj = tr * G;
+#pragma unroll
+      for (int v = 0; v < G; ++v)
+#pragma unroll
+        for (int t = 0; t < kSplitMaxT; ++t)
+          if (t < T) {
+            const double cv = s_cs[t * dim + jj + v];
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) dot[t][q] = __builtin_fma(cv, (double)u[v][q], dot[t][q]);
+          }
+    }
   }
+  int j = ntrip * G;
   for (; j < dim; ++j) {
     float u[kPer];
 #pragma unroll
-    for (int q = 0; q < kPer; ++q) u[q] = a.XT[(int64_t)j * n + ix[q]];
+    for (int q = 0; q < kPer; ++q) u[q] = (xt + (int64_t)j * n)[off[q]];
 #pragma unroll
     for (int t = 0; t < kSplitMaxT; ++t)
       if (t < T) {
@@ -2434,12 +2468,22 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   const bool split = seq && a.XT && T >= 2 && T <= kSplitMaxT && lds_split <= 150 * 1024 &&
                      nblk >= kSplitMinBlocks && getenv("GDD_KPP_FUSED_ROUND") == nullptr;
   if (split) {
-    GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dists, hipFuncAttributeMaxDynamicSharedMemorySize,
+    void (*dists)(KppArgs, int) = nullptr;
+    switch (T) {
+      case 2: dists = k_kpp_dists<2>; break;
+      case 3: dists = k_kpp_dists<3>; break;
+      case 4: dists = k_kpp_dists<4>; break;
+      case 5: dists = k_kpp_dists<5>; break;
+      case 6: dists = k_kpp_dists<6>; break;
+      case 7: dists = k_kpp_dists<7>; break;
+      default: dists = k_kpp_dists<8>; break;
+    }
+    GDD_HIP(hipFuncSetAttribute((const void*)dists, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_split));
     for (int c = 1; c < k; ++c) {
       k_kpp_round<true, true><<<dim3(1, T), kThr, lds, s>>>(a, c);   // fold, winner, candidates
       GDD_LAUNCHED();
-      k_kpp_dists<<<nblk, kThr, lds_split, s>>>(a, c);              // every trial's distances
+      dists<<<nblk, kThr, lds_split, s>>>(a, c);                    // every trial's distances
       GDD_LAUNCHED();
     }
     k_kpp_final<<<1, kThr, 0, s>>>(a, k - 1);
