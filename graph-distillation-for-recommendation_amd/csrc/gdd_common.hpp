@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <functional>
 #include <string>
 
 #include "gdd.h"
@@ -71,6 +72,18 @@ size_t sort_pairs_ws_bytes(int64_t n);
 int sort_pairs_i32(const int32_t* keys_in, int32_t* keys_out, const int32_t* vals_in,
                    int32_t* vals_out, int64_t n, int end_bit, void* ws, size_t ws_bytes,
                    hipStream_t s);
+
+// ---------------------------------------------------------------------------------------------
+// launch-sequence replay (hipGraph). A fixed sequence of dependent launches — the k-means++ round
+// chain, a chunk of MiniBatch steps — is recorded once into a graph and replayed: a graph kernel node
+// starts ~1 us sooner after its predecessor than a stream launch does (tools/probe/gap_probe.hip:
+// 1.6 vs 2.5-2.8 us per dependent launch). `key` (with `site`) must determine every argument of every
+// launch `enqueue` issues (pointers, sizes, step indices), so a replay is the same work as the
+// eager sequence. GDD_GRAPH=0 runs every sequence eagerly; 1 (default) records a key on its second
+// occurrence (one-off shapes never pay the recording); 2 records on the first (parity tests).
+// ---------------------------------------------------------------------------------------------
+int replay_or_run(const char* site, const void* key, size_t key_bytes, hipStream_t s,
+                  const std::function<int(hipStream_t)>& enqueue);
 
 // ---------------------------------------------------------------------------------------------
 // internal entry points of the device-resident MiniBatchKMeans loop (gdd_kmeans.hip, used by

@@ -143,18 +143,15 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n
     }
   } guard{ev};
   int32_t* stop_word = reinterpret_cast<int32_t*>(static_cast<char*>(w.state) + 16);
-  int64_t n_since = 0;
-  int64_t i = 0;
-  int64_t chunk = 0;
-  *stop_step = -1;
-  while (i < n_steps) {
-    const int64_t m = std::min<int64_t>(kDevChunk, n_steps - i);
+  // _random_reassign (:2029-2043): n_since grows by b per step and fires (then resets) at >= 10k,
+  // i.e. at steps 0, p, 2p, ... with p = ceil(10k / b)
+  const int64_t rr_period = (10 * (int64_t)k + bs - 1) / bs;
+  // the launches of steps [i0, i0 + m): every argument follows from the step indices and the fit's
+  // buffers, so a chunk is replayed as a recorded graph keyed by them (replay_or_run)
+  auto enqueue_chunk = [&](int64_t i0, int64_t m, hipStream_t cs) -> int {
     for (int64_t j = 0; j < m; ++j) {
-      const int64_t st = i + j;
-      n_since += bs;
-      const bool rr = st == 0 || n_since >= 10 * (int64_t)k;  // _random_reassign (:2029-2043)
-      if (rr) n_since = 0;
-      const bool do_rr = rr && reassign;
+      const int64_t st = i0 + j;
+      const bool do_rr = reassign && st % rr_period == 0;
       const bool has_next = st + 1 < n_steps;
       int64_t* rows_cur = w.rows_d + (st & 1) * bs;
       int64_t* rows_nxt = w.rows_d + ((st + 1) & 1) * bs;
@@ -165,21 +162,51 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n
       float* c_old = w.C[st % 2];
       float* c_new = w.C[(st + 1) % 2];
       const int flags = GDD_STEP_CONVERGE | (st > 0 ? GDD_STEP_NORMS_VALID : 0);
-      rc = minibatch_step_dev(bs, dim, X, rows_cur, k, c_old, c_new, w.counts, w.labels_b, (int)st, n,
-                              max_no_improvement, flags, w.state, w.step_ws, w.step_bytes,
-                              has_next ? next : none, s);  // at reassignment steps: speculative
-      if (rc) return rc;
+      int rc2 = minibatch_step_dev(bs, dim, X, rows_cur, k, c_old, c_new, w.counts, w.labels_b, (int)st,
+                                   n, max_no_improvement, flags, w.state, w.step_ws, w.step_bytes,
+                                   has_next ? next : none, cs);  // at reassignment steps: speculative
+      if (rc2) return rc2;
       if (do_rr) {
-        rc = mb_reassign_launch((int)st, bs, dim, k, reassignment_ratio, X, rows_cur, c_new, w.counts,
-                                w.step_ws, w.step_bytes, mt_cur, mt_cur, has_next ? next : none,
-                                w.state, s);
-        if (rc) return rc;
+        rc2 = mb_reassign_launch((int)st, bs, dim, k, reassignment_ratio, X, rows_cur, c_new, w.counts,
+                                 w.step_ws, w.step_bytes, mt_cur, mt_cur, has_next ? next : none,
+                                 w.state, cs);
+        if (rc2) return rc2;
       }
       if (!has_next) {  // the last step's inertia and convergence test (otherwise in step st+1)
-        rc = mb_loop_end(bs, k, (int)st, n, max_no_improvement, w.state, w.step_ws, w.step_bytes, s);
-        if (rc) return rc;
+        rc2 = mb_loop_end(bs, k, (int)st, n, max_no_improvement, w.state, w.step_ws, w.step_bytes, cs);
+        if (rc2) return rc2;
       }
     }
+    return GDD_OK;
+  };
+  struct {
+    const void* ptr[10];  // every buffer the launches touch
+    int64_t n, bs, n_steps, i0, m, dim, k, max_ni, step_bytes;
+    float ratio;
+    int pad;
+  } key;
+  std::memset(&key, 0, sizeof(key));
+  const void* ptrs[10] = {X, w.rows_d, w.C[0], w.C[1], w.counts, w.labels_b, w.state, w.step_ws, w.mtb,
+                          nullptr};
+  std::memcpy(key.ptr, ptrs, sizeof(ptrs));
+  key.step_bytes = (int64_t)w.step_bytes;
+  key.n = n;
+  key.bs = bs;
+  key.n_steps = n_steps;
+  key.dim = dim;
+  key.k = k;
+  key.max_ni = max_no_improvement;
+  key.ratio = reassignment_ratio;
+  int64_t i = 0;
+  int64_t chunk = 0;
+  *stop_step = -1;
+  while (i < n_steps) {
+    const int64_t m = std::min<int64_t>(kDevChunk, n_steps - i);
+    key.i0 = i;
+    key.m = m;
+    rc = replay_or_run("minibatch_chunk", &key, sizeof(key), s,
+                       [&](hipStream_t cs) { return enqueue_chunk(i, m, cs); });
+    if (rc) return rc;
     i += m;
     // this chunk's stop word, read back while the next chunks run
     const int slot = (int)(chunk & 3);

@@ -2321,13 +2321,14 @@ extern "C" int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const 
   return GDD_OK;
 }
 
-extern "C" int gdd_inertia(int64_t n, const float* sq_dist, const float* w, float* out,
-                           gdd_stream_t stream) {
-  GDD_REQUIRE(n >= 0 && out && (n == 0 || sq_dist), "inertia: bad arguments");
-  k_inertia<<<1, 256, 0, to_hip(stream)>>>(n, sq_dist, w, out, nullptr, 0);
+// the one-lane fold (GDD_INERTIA_SEQ=1; gdd_inertia itself is the exact parallel form, gdd_seqsum.hip)
+namespace gdd {
+int inertia_plain_launch(int64_t n, const float* sq, const float* w, float* out, hipStream_t s) {
+  k_inertia<<<1, 256, 0, s>>>(n, sq, w, out, nullptr, 0);
   GDD_LAUNCHED();
   return GDD_OK;
 }
+}  // namespace gdd
 
 extern "C" size_t gdd_minibatch_update_ws_bytes(int64_t b, int k) {
   (void)b;

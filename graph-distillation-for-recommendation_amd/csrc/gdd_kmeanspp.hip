@@ -34,6 +34,8 @@
 #include <cmath>
 #include <cstdlib>
 
+#include <cstring>
+
 #include "gdd_common.hpp"
 
 namespace gdd {
@@ -2286,7 +2288,8 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   for (int q = 0; q < 2; ++q) a.cand[q] = cv.take<int64_t>(kMaxTrials);
   a.pot1 = cv.take<float>(2);
   a.winq = cv.take<int>(2);
-  Kpp1Args b1{};
+  Kpp1Args b1;
+  std::memset(&b1, 0, sizeof(b1));  // padding too: b1 is part of the chain's replay key
   for (int q = 0; q < 2; ++q) b1.potv[q] = cv.take<float>(T);
   for (int q = 0; q < 2; ++q) b1.candw[q] = cv.take<int64_t>((size_t)T * T);
   for (int q = 0; q < 2; ++q) b1.candself[q] = cv.take<int64_t>(T);
@@ -2391,26 +2394,41 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       GDD_LAUNCHED();
       const bool plain = getenv("GDD_KPP_CHAIN_PLAIN") != nullptr;
       if (T <= kPairMaxT && getenv("GDD_KPP_SINGLE_ROUND") == nullptr) {
-        // two rounds per launch (a trailing odd round alone)
-        int lq = 1, pair = 0;
-        for (int c = 1; c < k; c += 2) {
-          lq = ((c - 1) / 2 + 1) & 1;
-          pair = c + 1 < k ? 1 : 0;
-          const unsigned grid = (unsigned)(pair ? T * T : T);
-          if (plain)
-            k_kpp1_dm2<false><<<grid, 256, 0, s>>>(b1, Dm, c, lq, pair);
-          else
-            k_kpp1_dm2<true><<<grid, 256, 0, s>>>(b1, Dm, c, lq, pair);
+        // two rounds per launch (a trailing odd round alone). The chain's arguments are fixed by
+        // (b1, Dm, k): it is replayed as one recorded graph (replay_or_run) — every launch then
+        // starts ~1 us sooner after the previous one
+        auto chain = [&](hipStream_t cs) -> int {
+          int lq = 1, pair = 0;
+          for (int c = 1; c < k; c += 2) {
+            lq = ((c - 1) / 2 + 1) & 1;
+            pair = c + 1 < k ? 1 : 0;
+            const unsigned grid = (unsigned)(pair ? T * T : T);
+            if (plain)
+              k_kpp1_dm2<false><<<grid, 256, 0, cs>>>(b1, Dm, c, lq, pair);
+            else
+              k_kpp1_dm2<true><<<grid, 256, 0, cs>>>(b1, Dm, c, lq, pair);
+            GDD_LAUNCHED();
+          }
+          k_kpp1_final2<<<1, 64, 0, cs>>>(b1, k - 1, lq, pair);
           GDD_LAUNCHED();
-        }
-        k_kpp1_final2<<<1, 64, 0, s>>>(b1, k - 1, lq, pair);
-        GDD_LAUNCHED();
-        if (k > 2) {
-          k_kpp_gather_centres<<<(unsigned)(((int64_t)k * dim + 255) / 256), 256, 0, s>>>(k, dim, X, indices,
-                                                                                           centers);
-          GDD_LAUNCHED();
-        }
-        return GDD_OK;
+          if (k > 2) {
+            k_kpp_gather_centres<<<(unsigned)(((int64_t)k * dim + 255) / 256), 256, 0, cs>>>(
+                k, dim, X, indices, centers);
+            GDD_LAUNCHED();
+          }
+          return GDD_OK;
+        };
+        struct {
+          Kpp1Args b1;
+          const float* Dm;
+          int k, plain;
+        } key;
+        std::memset(&key, 0, sizeof(key));
+        key.b1 = b1;
+        key.Dm = Dm;
+        key.k = k;
+        key.plain = plain ? 1 : 0;
+        return replay_or_run("kpp_pair_chain", &key, sizeof(key), s, chain);
       }
       for (int c = 1; c < k; ++c) {
         if (plain)

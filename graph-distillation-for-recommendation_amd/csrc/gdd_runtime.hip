@@ -4,6 +4,10 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+#include <mutex>
+#include <vector>
+
 namespace gdd {
 
 static thread_local std::string g_last_error;
@@ -60,6 +64,95 @@ int sort_pairs_i32(const int32_t* keys_in, int32_t* keys_out, const int32_t* val
   if (need > ws_bytes) return fail(GDD_E_WORKSPACE, "sort workspace %zu < %zu", ws_bytes, need);
   GDD_HIP(hipcub::DeviceRadixSort::SortPairs(ws, need, keys_in, keys_out, vals_in, vals_out,
                                              (int)n, 0, end_bit, s));
+  return GDD_OK;
+}
+
+// ---- launch-sequence replay --------------------------------------------------------------------
+namespace {
+struct GraphEntry {
+  std::string key;  // site, device, caller key
+  hipGraphExec_t exec = nullptr;
+  uint64_t last_use = 0;
+};
+std::mutex g_graph_mu;
+std::vector<GraphEntry> g_graphs;
+uint64_t g_graph_tick = 0;
+hipStream_t g_capture_stream[64] = {};
+constexpr size_t kGraphCap = 512;
+
+int graph_mode() {
+  const char* e = getenv("GDD_GRAPH");
+  return e ? atoi(e) : 1;
+}
+}  // namespace
+
+int replay_or_run(const char* site, const void* key, size_t key_bytes, hipStream_t s,
+                  const std::function<int(hipStream_t)>& enqueue) {
+  const int mode = graph_mode();
+  if (mode <= 0) return enqueue(s);
+  int dev = 0;
+  GDD_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return enqueue(s);
+  std::string k(site);
+  k.push_back('\0');
+  k.append(reinterpret_cast<const char*>(&dev), sizeof(dev));
+  k.append(static_cast<const char*>(key), key_bytes);
+  std::lock_guard<std::mutex> lock(g_graph_mu);
+  GraphEntry* e = nullptr;
+  for (auto& g : g_graphs)
+    if (g.key == k) {
+      e = &g;
+      break;
+    }
+  if (e && e->exec) {
+    e->last_use = ++g_graph_tick;
+    GDD_HIP(hipGraphLaunch(e->exec, s));
+    return GDD_OK;
+  }
+  auto make_room = [&]() -> int {  // least recently used entry out once the cache is full
+    if (g_graphs.size() < kGraphCap) return GDD_OK;
+    size_t old = 0;
+    for (size_t i = 1; i < g_graphs.size(); ++i)
+      if (g_graphs[i].last_use < g_graphs[old].last_use) old = i;
+    if (g_graphs[old].exec) {
+      GDD_HIP(hipDeviceSynchronize());  // eviction is rare; never destroy a graph in flight
+      GDD_HIP(hipGraphExecDestroy(g_graphs[old].exec));
+    }
+    g_graphs.erase(g_graphs.begin() + (long)old);
+    return GDD_OK;
+  };
+  if (!e && mode == 1) {  // first sight: run eagerly, record on the next occurrence
+    if (int rc = make_room()) return rc;
+    GraphEntry ne;
+    ne.key = k;
+    ne.last_use = ++g_graph_tick;
+    g_graphs.push_back(std::move(ne));
+    return enqueue(s);
+  }
+  if (!g_capture_stream[dev]) GDD_HIP(hipStreamCreateWithFlags(&g_capture_stream[dev], hipStreamNonBlocking));
+  hipStream_t cs = g_capture_stream[dev];
+  GDD_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+  const int rc = enqueue(cs);
+  hipGraph_t graph = nullptr;
+  const hipError_t ec = hipStreamEndCapture(cs, &graph);
+  if (rc) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return rc;
+  }
+  if (ec != hipSuccess) return fail((int)ec, "%s: graph capture failed: %s", site, hipGetErrorString(ec));
+  hipGraphExec_t exec = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  if (ei != hipSuccess) return fail((int)ei, "%s: graph instantiate failed: %s", site, hipGetErrorString(ei));
+  if (!e) {
+    if (int rc2 = make_room()) return rc2;
+    g_graphs.emplace_back();
+    e = &g_graphs.back();
+    e->key = k;
+  }
+  e->exec = exec;
+  e->last_use = ++g_graph_tick;
+  GDD_HIP(hipGraphLaunch(exec, s));
   return GDD_OK;
 }
 

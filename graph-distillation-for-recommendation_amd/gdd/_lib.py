@@ -48,6 +48,8 @@ SIGNATURES = {
     "gdd_kmeans_assign_bf16": (_c_int, [_c_i64, _c_int, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _vp,
                                    _c_size, _vp]),
     "gdd_inertia": (_c_int, [_c_i64, _vp, _vp, _vp, _vp]),
+    "gdd_inertia_ws_bytes": (_c_size, [_c_i64]),
+    "gdd_inertia_ws": (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _c_size, _vp]),
     "gdd_minibatch_update_ws_bytes": (_c_size, [_c_i64, _c_int]),
     "gdd_minibatch_update": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp,
                                       _vp, _c_size, _vp]),

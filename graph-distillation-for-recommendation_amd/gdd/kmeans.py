@@ -105,6 +105,21 @@ class _Ops:
 
 _SIDE_STREAMS = {}
 
+# Diagnostics: when a dict, KMeans.fit synchronises between its stages and adds their wall times
+# (ms) to it — "center_columns", "kmeans_plusplus", "lloyd_loop", "final_estep" — plus "lloyd_calls"
+# (host round trips of the device loop). None (the default) adds no synchronisation.
+PHASE_TIMING = None
+
+
+def _phase(name, t0):
+    import time
+    if PHASE_TIMING is None:
+        return t0
+    torch.cuda.synchronize()
+    now = time.perf_counter()
+    PHASE_TIMING[name] = PHASE_TIMING.get(name, 0.0) + (now - t0) * 1e3
+    return now
+
 
 def _side_inertia(sq: torch.Tensor):
     """gdd_inertia(sq) on a per-device side stream, ordered after the caller's stream; returns the
@@ -114,11 +129,15 @@ def _side_inertia(sq: torch.Tensor):
     if side is None:
         side = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
     out = torch.empty(1, dtype=torch.float32, device=dev)
-    side.wait_stream(torch.cuda.current_stream(dev))
     lib = _lib.device_lib()
-    _lib.check(lib.gdd_inertia(sq.shape[0], sq.data_ptr(), None, out.data_ptr(), side.cuda_stream))
+    n = sq.shape[0]
+    ws = _lib.workspace(lib.gdd_inertia_ws_bytes(n), dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    _lib.check(lib.gdd_inertia_ws(n, sq.data_ptr(), None, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                  side.cuda_stream))
     sq.record_stream(side)
     out.record_stream(side)
+    ws.record_stream(side)
     ev = torch.cuda.Event()
     ev.record(side)
     return out, ev
@@ -248,8 +267,9 @@ class MiniBatchKMeans(_BaseKMeans):
         n_steps, ewa = ctypes.c_int64(0), ctypes.c_double(0.0)
         max_ni = -1 if self.max_no_improvement is None else int(self.max_no_improvement)
         # compute_labels: the native fit enqueues the full labels pass (:2191-2197) as soon as the
-        # loop stops and leaves the per-sample distances in `sq`; their inertia (a sequential fp32
-        # fold bound by its add chain) runs on a side stream, read on first access of inertia_
+        # loop stops and leaves the per-sample distances in `sq`; their inertia (the sequential
+        # fp32 sum, evaluated in parallel by gdd_inertia_ws) runs on a side stream, read on first
+        # access of inertia_
         from .sharded import world_of
         # only an explicit group shards: with group=None a process in some other job's default
         # group (e.g. a DDP run clustering per rank) fits on its own data
@@ -418,6 +438,8 @@ class KMeans(_BaseKMeans):
             raise ValueError(f"n_samples={n} should be >= n_clusters={k}.")
         rs = check_random_state(self.random_state)
         dev = X0.device
+        import time
+        tph = time.perf_counter() if PHASE_TIMING is not None else 0.0
         # sklearn's centring and _tolerance on the device (numpy's sequential column sums): X - mean,
         # mean and var of the INPUT (sklearn/cluster/_kmeans.py:1476-1487, :279-288)
         Xd = torch.empty_like(X0)
@@ -429,6 +451,7 @@ class KMeans(_BaseKMeans):
         X_mean = mean_d.cpu().numpy()
         tol_ = 0 if self.tol == 0 else np.mean(var_d.cpu().numpy()) * self.tol
         del X0
+        tph = _phase("center_columns", tph)
         ops = _Ops(dev, n, k, dim)
         lib = ops.lib
         stream = ops.stream
@@ -446,6 +469,7 @@ class KMeans(_BaseKMeans):
         n_inits = self._n_init(10)
         for _ in range(n_inits):
             C0, _ = ops.kmeans_plusplus(Xd, k, rs)
+            tph = _phase("kmeans_plusplus", tph)
             Cb = (C0, torch.empty_like(C0))
             labels_old.fill_(-1)
             it0, resume = 0, 0
@@ -456,21 +480,25 @@ class KMeans(_BaseKMeans):
                     int(self.max_iter), float(tol_), state.data_ptr(), ctypes.addressof(done),
                     ctypes.addressof(reason), ws.data_ptr(), ws.numel(), hws.data_ptr(), hws.numel(),
                     stream))
+                if PHASE_TIMING is not None:
+                    PHASE_TIMING["lloyd_calls"] = PHASE_TIMING.get("lloyd_calls", 0) + 1
                 if reason.value != 3:
                     break
                 it = done.value  # an empty cluster at iteration `it`: relocate, then resume there
                 self._relocate(Xd, Cb[it % 2], Cb[(it + 1) % 2], wic, labels, ops)
                 it0, resume = it, 1
             n_iter = done.value
+            tph = _phase("lloyd_loop", tph)
             strict = reason.value == 1
             C = Cb[n_iter % 2]  # iteration i writes C[(i+1) % 2]
             if not strict:  # the final E-step with the last centres (:736-747)
                 ops.assign(Xd, C, labels=labels)
             _lib.check(lib.gdd_point_center_sqdist(n, dim, Xd.data_ptr(), labels.data_ptr(),
                                                    C.data_ptr(), sq.data_ptr(), stream))
+            tph = _phase("final_estep", tph)
             if n_inits == 1:
                 # one init: nothing to compare, so the fit returns without waiting on the device.
-                # The inertia (a sequential fp32 fold over n, bound by its add chain) runs on a side
+                # The inertia (the sequential fp32 sum over n, gdd_inertia_ws) runs on a side
                 # stream and is read on first access of inertia_; labels and centres stay on the
                 # device until their host attributes are read. cluster_centers_ = C + X_mean is the
                 # same fp32 add numpy makes.

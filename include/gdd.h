@@ -127,7 +127,15 @@ int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const int64_t* ro
 
 /* out[0] = sequential fp32 sum of sq_dist[i] * w[i] in sample order (w == NULL: ones); this is      */
 /* sklearn _inertia_dense with one OpenMP thread (_k_means_common.pyx:92-121).                       */
+/* Evaluated in parallel with the sequential result bit for bit (gdd_seqsum.hip: per-binade integer   */
+/* advances with a round-to-even parity carry, scanned by one workgroup). Non-negative finite terms   */
+/* take the parallel form; NaN, infinite or negative terms are added one at a time from there.       */
 int gdd_inertia(int64_t n, const float* sq_dist, const float* w, float* out, gdd_stream_t stream);
+/* The same sum for long arrays in three launches over ~2048-term segments (per-segment advances for  */
+/* the two likeliest binades, then one resolving workgroup); ws: gdd_inertia_ws_bytes(n) bytes.       */
+size_t gdd_inertia_ws_bytes(int64_t n);
+int gdd_inertia_ws(int64_t n, const float* sq_dist, const float* w, float* out, void* ws,
+                   size_t ws_bytes, gdd_stream_t stream);
 
 /* MiniBatchKMeans center update, sklearn _minibatch_update_dense (_k_means_minibatch.pyx:11-108):    */
 /* for each cluster c with batch weight ws > 0: C_new[c] = (C_old[c]*W[c] + sum_{i in c, batch order} */

@@ -155,6 +155,14 @@ def labels_inertia(X, C):
     return labels, float(lib().oracle_inertia(sq.shape[0], sq, None))
 
 
+def inertia(sq, w=None) -> np.float32:
+    """sklearn _inertia_dense with one OpenMP thread (_k_means_common.pyx:92-121): the sequential fp32
+    sum of sq[i] * w[i] in sample order (w None: ones)."""
+    sq = _c(sq, np.float32)
+    wc = None if w is None else _c(w, np.float32)
+    return np.float32(lib().oracle_inertia(sq.shape[0], sq, _ptr(wc)))
+
+
 def sdot_skx(x, y):
     x, y = _c(x, np.float32), _c(y, np.float32)
     return float(lib().oracle_sdot_skx(x, y, x.shape[0]))

@@ -236,3 +236,25 @@ def test_products_full_shape_kmeans_matches_sklearn():
     assert sha(m.labels_.astype(np.int32)) == rec["products_labels_sha256"]
     assert sha(np.ascontiguousarray(m.cluster_centers_, np.float32)) == rec["products_centers_sha256"]
     assert m.inertia_ == rec["products_inertia"]
+
+
+def test_reddit_shape_propagate_matches_oracle():
+    """Config 3's propagation at the Reddit train graph's full shape: N = 153,932,
+    ~10M entries, d = 602, T = 3, alpha = 0.95 (main_induct.sh:16-21; the induct loops
+    clustgdd_agent_induct.py:72-94) — the d > 128 float2 lanes with split hub rows and the fix-up,
+    every bit of target and the last hop against the oracle."""
+    n, d = 153932, 602
+    gr = _device_chung_lu(n, 65.0, 3)
+    X = synth.features(n, d, 3)
+    rp, co = gr.rowptr.cpu().numpy(), gr.col.cpu().numpy()
+    assert co.shape[0] > 9_000_000
+    assert np.diff(rp).max() > 256  # hub rows span several segments
+    ro, cn, vo = O.normalize_csr(rp, co, None, -1)
+    g = gdd.normalize_adj(gr)
+    assert np.array_equal(g.rowptr.cpu().numpy(), ro) and np.array_equal(g.col.cpu().numpy(), cn)
+    assert np.array_equal(bits(g.val.cpu().numpy()), bits(vo))
+    del gr
+    t, p = gdd.propagate(g, torch.from_numpy(X).cuda(), 3, 0.95)
+    t_ref, p_ref = O.propagate(ro, cn, vo, X, 3, 0.95)
+    assert np.array_equal(bits(t.cpu().numpy()), bits(t_ref))
+    assert np.array_equal(bits(p.cpu().numpy()), bits(p_ref))

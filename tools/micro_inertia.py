@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""The final labels pass's inertia fold (sequential fp32 sum of 169,343 terms): device time and
-parity with the sequential fp32 order."""
+"""The inertia (sequential fp32 sum of the per-sample distances) at the bench, Reddit and products
+shapes: device time of the one-lane fold (GDD_INERTIA_SEQ=1), the one-workgroup chunked walk
+(gdd_inertia) and the segmented form (gdd_inertia_ws), each checked against the sequential order."""
 import os
-import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -13,31 +13,38 @@ import torch  # noqa: E402
 from gdd import _lib  # noqa: E402
 
 
+def timed(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
 def main():
     lib = _lib.device_lib()
     s = _lib.stream_ptr()
+    mode = "one-lane fold" if os.environ.get("GDD_INERTIA_SEQ") == "1" else "parallel"
     for n in (169343, 153932, 2449029):
-        x = (np.random.default_rng(n).random(n) * 10).astype(np.float32)
-        ref = np.float32(0)
-        for v in x:  # the sequential fp32 order of the reference's one-thread inertia
-            ref = np.float32(ref + v)
+        rng = np.random.default_rng(n)
+        # inertia-like terms: squared distances in 40 / 47 dims
+        x = (rng.standard_normal((n, 8)).astype(np.float32) ** 2).sum(1).astype(np.float32) * 5
+        ref = np.cumsum(x, dtype=np.float32)[-1]
         xd = torch.from_numpy(x).cuda()
-        out = torch.empty(1, dtype=torch.float32, device="cuda")
-        _lib.check(lib.gdd_inertia(n, xd.data_ptr(), None, out.data_ptr(), s))
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(5):
-            lib.gdd_inertia(n, xd.data_ptr(), None, out.data_ptr(), s)
-        e1.record()
-        torch.cuda.synchronize()
-        ok = out.cpu().numpy()[0].view(np.uint32) == np.float32(ref).view(np.uint32)
-        mode = "lds-fold"
-        print(f"{mode}: n={n}: {e0.elapsed_time(e1) / 5 * 1e3:.1f} us  bit-exact={ok}", flush=True)
+        out = torch.zeros(2, dtype=torch.float32, device="cuda")
+        ws = _lib.workspace(lib.gdd_inertia_ws_bytes(n), xd.device)
+        t_walk = timed(lambda: lib.gdd_inertia(n, xd.data_ptr(), None, out.data_ptr(), s))
+        t_seg = timed(lambda: lib.gdd_inertia_ws(n, xd.data_ptr(), None, out.data_ptr() + 4,
+                                                 ws.data_ptr(), ws.numel(), s))
+        got = out.cpu().numpy()
+        ok = [bool(g.view(np.uint32) == ref.view(np.uint32)) for g in got]
+        print(f"{mode}: n={n}: walk {t_walk:.1f} us, segmented {t_seg:.1f} us, bit-exact {ok}",
+              flush=True)
 
 
 if __name__ == "__main__":
     main()
-    if False:
-        env = dict(os.environ, GDD_INERTIA_LDS="1")
-        subprocess.run([sys.executable, __file__], env=env, check=True)
