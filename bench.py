@@ -110,7 +110,7 @@ def main():
         if record:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        target, _ = gdd.propagate(gn, X, cfg.T, cfg.alpha)
+        target, _ = gdd.propagate(gn, X, cfg.T, cfg.alpha, group=group)
         if record:
             e1.record()
             prop_ev.append((e0, e1, gn.nnz))
@@ -182,7 +182,7 @@ def main():
         tp = time.perf_counter()
         gn_p = gdd.normalize_adj(graph)
         tp = mark("normalize", tp)
-        target_p, _ = gdd.propagate(gn_p, X, cfg.T, cfg.alpha)
+        target_p, _ = gdd.propagate(gn_p, X, cfg.T, cfg.alpha, group=group)
         tp = mark("propagate", tp)
         logits_p = torch.addmm(b, target_p, W)
         tp = mark("logits", tp)

@@ -85,14 +85,24 @@ __global__ void k_run_counts(const int32_t* __restrict__ nnz, const int32_t* __r
   if (s < nnz[0]) val_out[s] = (float)(starts[s + 1] - starts[s]);
 }
 
-// out[e] = sum_f a[ra[e], f] * b[rb[e], f] (fp32, f ascending), one wave per edge-group of 64
+// out[e] = sum_f a[ra[e], f] * b[rb[e], f] (fp32, f ascending), one wave per edge-group of 64.
+// Row ids outside [0, na) / [0, nb) are not read: the edge's output is NaN and *bad is set (a stale
+// or foreign index buffer becomes a reported error instead of an illegal address).
 __global__ __launch_bounds__(256) void k_edge_dots(int64_t E, int d, const int32_t* __restrict__ ra,
-                                                   const float* __restrict__ a, const int32_t* __restrict__ rb,
-                                                   const float* __restrict__ b, float* __restrict__ out) {
+                                                   const float* __restrict__ a, int64_t na,
+                                                   const int32_t* __restrict__ rb,
+                                                   const float* __restrict__ b, int64_t nb,
+                                                   float* __restrict__ out, int32_t* __restrict__ bad) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= E) return;
-  const float* x = a + (int64_t)ra[e] * d;
-  const float* y = b + (int64_t)rb[e] * d;
+  const int32_t ia = ra[e], ib = rb[e];
+  if (ia < 0 || ia >= na || ib < 0 || ib >= nb) {
+    out[e] = __builtin_nanf("");
+    if (bad) atomicOr(bad, 1);
+    return;
+  }
+  const float* x = a + (int64_t)ia * d;
+  const float* y = b + (int64_t)ib * d;
   float s = 0.f;
   for (int f = 0; f < d; ++f) s = __builtin_fmaf(x[f], y[f], s);
   out[e] = s;
@@ -162,12 +172,13 @@ extern "C" int gdd_bipartite_condense(int64_t E, const int32_t* train_u, const i
   return GDD_OK;
 }
 
-extern "C" int gdd_edge_dots(int64_t E, int d, const int32_t* ra, const float* a, const int32_t* rb,
-                             const float* b, float* out, gdd_stream_t stream) {
-  GDD_REQUIRE(E >= 0 && d > 0, "edge_dots: bad shape");
+extern "C" int gdd_edge_dots(int64_t E, int d, const int32_t* ra, const float* a, int64_t na,
+                             const int32_t* rb, const float* b, int64_t nb, float* out, int32_t* bad,
+                             gdd_stream_t stream) {
+  GDD_REQUIRE(E >= 0 && d > 0 && na >= 0 && nb >= 0, "edge_dots: bad shape");
   if (E == 0) return GDD_OK;
   GDD_REQUIRE(ra && a && rb && b && out, "edge_dots: null pointer");
-  k_edge_dots<<<grid1(E), kThreads, 0, to_hip(stream)>>>(E, d, ra, a, rb, b, out);
+  k_edge_dots<<<grid1(E), kThreads, 0, to_hip(stream)>>>(E, d, ra, a, na, rb, b, nb, out, bad);
   GDD_LAUNCHED();
   return GDD_OK;
 }

@@ -112,7 +112,7 @@ SIGNATURES = {
     "gdd_bipartite_condense_ws_bytes": (_c_size, [_c_i64, _c_int]),
     "gdd_bipartite_condense": (_c_int, [_c_i64, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_int, _c_int, _vp,
                                         _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
-    "gdd_edge_dots": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gdd_edge_dots": (_c_int, [_c_i64, _c_int, _vp, _vp, _c_i64, _vp, _vp, _c_i64, _vp, _vp, _vp]),
     "gdd_bpr_sample": (_c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "gdd_recall_at_k": (_c_int, [_c_int, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gdd_subgraph_ws_bytes": (_c_size, [_c_i64, _c_i64]),

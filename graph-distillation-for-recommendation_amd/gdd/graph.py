@@ -172,12 +172,22 @@ def _ws_propagate(adj: CSRGraph, d: int):
     return lib, _lib.workspace(lib.gdd_propagate_ws_bytes(adj.n, adj.nnz, d), adj.device)
 
 
-def propagate(adj_norm: CSRGraph, features: torch.Tensor, T: int, alpha: float):
+def propagate(adj_norm: CSRGraph, features: torch.Tensor, T: int, alpha: float, group=None):
     """The closed-form feature denoising loop of pretrained_clustering (transduct:55-65).
 
     Returns ``(target_feat, prop_feat)`` exactly as the loop leaves them: ``target_feat =
     (1-α)·Σ_{t<T} (αÂ)^t X`` accumulated hop by hop in fp32, ``prop_feat`` = the last hop.
+    ``group`` (a torch.distributed group over the GPUs of a node): when the size model of
+    :func:`gdd.sharded.propagation_shards_pay` says the gathers outweigh a per-hop all-gather
+    (ogbn-products, not ogbn-arxiv), the rows are partitioned over the ranks
+    (:func:`gdd.sharded.sharded_propagate`, bit-identical); otherwise every rank propagates.
     """
+    if group is not None:
+        from .sharded import propagation_shards_pay, sharded_propagate, world_of
+        world = world_of(group)[1]
+        if world > 1 and propagation_shards_pay(adj_norm.n, adj_norm.nnz, features.shape[1], world):
+            return sharded_propagate(adj_norm, features.to(torch.float32).contiguous(), T, alpha,
+                                     group=group)
     if T < 1:
         raise ValueError("prop_num must be >= 1 (the reference loop leaves target undefined)")
     X = features.contiguous()

@@ -176,7 +176,7 @@ def pretrained_clustering_hot_path(features, adj, T: int, alpha: float, logits, 
     X = features if isinstance(features, torch.Tensor) else torch.from_numpy(
         np.ascontiguousarray(features, np.float32))
     X = X.to(device=device, dtype=torch.float32).contiguous()
-    target_feat, prop_feat = propagate(adj_norm, X, T, alpha)  # transduct:59-65
+    target_feat, prop_feat = propagate(adj_norm, X, T, alpha, group=group)  # transduct:59-65
     out = logits(target_feat) if callable(logits) else logits
     if dataset == "ogbn-arxiv":                                  # transduct:102-105
         km = MiniBatchKMeans(n_clusters=nnodes_syn, random_state=seed, n_init=n_init,
@@ -212,7 +212,7 @@ def pretrained_clustering_induct_hot_path(data, T: int, alpha: float, logits_tra
         X = getattr(data, "feat_" + name)
         X = X if isinstance(X, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(X, np.float32))
         X = X.to(device=g.device, dtype=torch.float32).contiguous()
-        targets[name], _ = propagate(norms[name], X, T, alpha)                      # :67-94
+        targets[name], _ = propagate(norms[name], X, T, alpha, group=group)         # :67-94
     out = logits_train(targets["train"], targets["val"]) if callable(logits_train) else logits_train
     if dataset == "reddit":                                                         # :129-134
         km = MiniBatchKMeans(n_clusters=nnodes_syn, random_state=seed, batch_size=cluster_minibatch,

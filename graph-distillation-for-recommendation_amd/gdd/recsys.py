@@ -155,6 +155,7 @@ class _Bipartite:
                                          _lib.stream_ptr(dev)))
         self.perm_l = self.perm[:E].long()
         self._plans: Dict[Tuple[int, int], torch.Tensor] = {}
+        self.bad = torch.zeros(1, dtype=torch.int32, device=dev)  # set by gdd_edge_dots on a bad row id
 
     def _plan(self, side: int, d: int) -> torch.Tensor:
         ws = self._plans.get((side, d))
@@ -192,9 +193,14 @@ class _Bipartite:
         a, b = a.detach().float().contiguous(), b.detach().float().contiguous()
         out = torch.empty(self.E, dtype=torch.float32, device=a.device)
         _lib.check(lib.gdd_edge_dots(self.E, int(a.shape[1]), a_rows.data_ptr(), a.data_ptr(),
-                                     b_rows.data_ptr(), b.data_ptr(), out.data_ptr(),
-                                     _lib.stream_ptr(a.device)))
+                                     int(a.shape[0]), b_rows.data_ptr(), b.data_ptr(), int(b.shape[0]),
+                                     out.data_ptr(), self.bad.data_ptr(), _lib.stream_ptr(a.device)))
         return out
+
+    def check(self) -> None:
+        """Raise if an edge gradient met a row id outside its embedding table (one host read)."""
+        if int(self.bad.item()):
+            raise IndexError("gdd_edge_dots: edge row id out of range")
 
 
 class _BiMessage(torch.autograd.Function):

@@ -63,8 +63,11 @@ def all_gather_parts(t: torch.Tensor, m: int, n: int, group=None) -> torch.Tenso
     rank, world = world_of(group)
     if world == 1:
         return t[:n]
-    pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    pad[:t.shape[0]] = t
+    if t.shape[0] == m and t.is_contiguous():  # already a full slot (e.g. a padded hop output)
+        pad = t
+    else:
+        pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[:t.shape[0]] = t
     if t.is_cuda and dist.get_backend(group) == "nccl":
         out = torch.empty((world * m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out, pad, group=group)
@@ -153,6 +156,13 @@ class DeviceOps:
         _lib.check(self.lib.gdd_inertia(sq.shape[0], sq.data_ptr(), None, out.data_ptr(), self.stream))
         return float(out.item())
 
+    def rows_plan(self, rows_graph, d):
+        from .graph import SpMMPlan
+        return SpMMPlan(rows_graph, d)
+
+    def rows_hop(self, plan, x, y, scale, acc, acc_scale):
+        plan.hop(x, y, scale, acc, acc_scale)
+
     def cluster_mean(self, feat, grp, k, c0, c1, empty_as_zero):
         n, d = feat.shape
         perm, offsets = grp
@@ -162,6 +172,71 @@ class DeviceOps:
                                                   offsets.data_ptr(), k, c0, c1, int(empty_as_zero),
                                                   _lib.ptr(out), _lib.ptr(counts), self.stream))
         return out, counts
+
+
+# ------------------------------------------------------------------------------------------------
+# row-partitioned propagation
+# ------------------------------------------------------------------------------------------------
+HOP_GATHER_GBS = 5500.0  # random whole-row gathers from HBM (MI355X_MICROARCH.md), GB/s
+ALLGATHER_GBS = 300.0    # RCCL all-gather bus bandwidth per GPU over xGMI (planning figure), GB/s
+
+
+def propagation_shards_pay(n: int, nnz: int, d: int, world: int) -> bool:
+    """Size model for row-partitioned propagation: a hop's gathers (nnz rows of d fp32, whole 128-B
+    lines, at the HBM gather rate) shrink by (R-1)/R; each hop then all-gathers the N x d output
+    ((R-1)/R of it crosses xGMI). ogbn-products (130M entries, d=100): ~12 ms of gathers vs ~2.9 ms
+    of all-gather at R=8 -> shard; ogbn-arxiv (2.6M, d=128): 0.21 vs 0.25 ms -> replicate.
+    GDD_SHARD_PROP=1/0 forces the choice."""
+    import os
+    env = os.environ.get("GDD_SHARD_PROP")
+    if env is not None:
+        return env == "1" and world > 1
+    if world <= 1:
+        return False
+    line = 128
+    row_bytes = -(-4 * d // line) * line
+    frac = (world - 1) / world
+    hop_ms = nnz * row_bytes / (HOP_GATHER_GBS * 1e9) * 1e3
+    gather_ms = n * d * 4 * frac / (ALLGATHER_GBS * 1e9) * 1e3
+    return hop_ms * frac > gather_ms
+
+
+def sharded_propagate(adj_norm, X, T: int, alpha: float, group=None, ops=None):
+    """gdd.propagate with the rows partitioned over the ranks (north star: "graph nodes range-
+    partitioned across the 8 GPUs"; the loop of clustgdd_agent_transduct.py:59-65). Rank r computes
+    rows [r*m, (r+1)*m) of every hop from the whole previous hop and keeps those rows of target; ONE
+    all-gather of the hop's N x d output follows each hop, and one of target at the end. Every row's
+    arithmetic is the single-GPU hop's (its own entries, the same segment chains, the same two target
+    roundings; the first hop's initial target fp32(1-alpha)*X is the same single rounding), so
+    target and the last hop are bit-identical for every world size. Returns (target, p_last)."""
+    ops = ops or DeviceOps(X.device)
+    rank, world = world_of(group)
+    n, d = X.shape
+    if T < 1:
+        raise ValueError("prop_num must be >= 1 (the reference loop leaves target undefined)")
+    # gdd_propagate's constants: alpha crosses the C ABI as fp32; 1 - alpha in fp64, then fp32
+    a32 = float(np.float32(alpha))
+    w32 = np.float32(1.0 - a32)
+    r0, r1, m = part(n, rank, world)
+    rp = adj_norm.rowptr
+    e0, e1 = int(rp[r0]), int(rp[r1])
+    target_loc = torch.zeros((m, d), dtype=torch.float32, device=X.device)
+    target_loc[: r1 - r0] = X[r0:r1] * w32  # fp32(1 - alpha) * X (agent :59), one rounding
+    if T == 1:
+        return all_gather_parts(target_loc, m, n, group), X.clone()
+    plan = None
+    if r1 > r0:
+        from .graph import CSRGraph
+        rows = CSRGraph((rp[r0:r1 + 1] - rp[r0]).contiguous(), adj_norm.col[e0:e1],
+                        adj_norm.values()[e0:e1], r1 - r0)
+        plan = ops.rows_plan(rows, d)
+    x = X.contiguous()
+    for _ in range(T - 1):
+        y = torch.empty((m, d), dtype=torch.float32, device=X.device)
+        if plan is not None:
+            ops.rows_hop(plan, x, y[: r1 - r0], a32, target_loc[: r1 - r0], float(w32))
+        x = all_gather_parts(y, m, n, group)
+    return all_gather_parts(target_loc, m, n, group), x
 
 
 # ------------------------------------------------------------------------------------------------

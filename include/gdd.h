@@ -397,7 +397,8 @@ int gdd_csr_transpose(int64_t n, int64_t n_cols, int64_t nnz, const int32_t* row
 /* tocsr gives): rowptr_out (num_cu+1), col_out / val_out with capacity E, the stored count written */
 /* to nnz_out (device int). bad_out (device, nullable): nonzero if an id was out of range.          */
 /* gdd_edge_dots: out[e] = sum_f a[ra[e],f] * b[rb[e],f] (fp32 fma chain, f ascending) - the edge   */
-/* gradient of the LightGCN message passing (RecsysModel.propagate, :336-346).                       */
+/* gradient of the LightGCN message passing (RecsysModel.propagate, :336-346). a has na rows, b nb:   */
+/* an out-of-range row id is not read (out[e] = NaN) and sets *bad (device int, nullable).           */
 /* ---------------------------------------------------------------------------------------------- */
 size_t gdd_bipartite_condense_ws_bytes(int64_t E, int num_cu);
 int gdd_bipartite_condense(int64_t E, const int32_t* train_u, const int32_t* train_i, int64_t num_users,
@@ -405,8 +406,8 @@ int gdd_bipartite_condense(int64_t E, const int32_t* train_u, const int32_t* tra
                            int num_ci, int32_t* rowptr_out, int32_t* col_out, float* val_out,
                            int32_t* nnz_out, int32_t* bad_out, void* ws, size_t ws_bytes,
                            gdd_stream_t stream);
-int gdd_edge_dots(int64_t E, int d, const int32_t* ra, const float* a, const int32_t* rb, const float* b,
-                  float* out, gdd_stream_t stream);
+int gdd_edge_dots(int64_t E, int d, const int32_t* ra, const float* a, int64_t na, const int32_t* rb,
+                  const float* b, int64_t nb, float* out, int32_t* bad, gdd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------- */
 /* (f4) the recommender's refinement loop (distill_recsys.py:641-733).                              */

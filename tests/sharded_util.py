@@ -68,6 +68,14 @@ class OracleOps:
         s = np.ascontiguousarray(_np(sq), np.float32)
         return float(O.lib().oracle_inertia(s.shape[0], s, None))
 
+    def rows_plan(self, rows_graph, d):
+        return (_np(rows_graph.rowptr), _np(rows_graph.col), _np(rows_graph.values()))
+
+    def rows_hop(self, plan, x, y, scale, acc, acc_scale):
+        rowptr, col, val = plan
+        a = acc.numpy()  # a view: the oracle adds acc_scale * y into it in place
+        y.copy_(torch.from_numpy(O.spmm(rowptr, col, val, _np(x), scale, a, acc_scale)))
+
     def cluster_mean(self, feat, grp, k, c0, c1, empty_as_zero):
         out, counts = O.cluster_mean(_np(feat), grp, k, empty_as_zero=empty_as_zero)
         return torch.from_numpy(out[c0:c1].copy()), torch.from_numpy(counts[c0:c1].copy())

@@ -55,6 +55,13 @@ def _worker(rank, world, port, job, out_dir):
         lab, sq, inertia = sharded.sharded_labels(torch.from_numpy(X),
                                                   torch.from_numpy(r["cluster_centers_"]), ops=ops)
         res = dict(labels=lab.numpy(), inertia=inertia, centers=r["cluster_centers_"])
+    elif kind == "propagate":
+        rowptr, col, val, X, T, alpha = args
+        from gdd.graph import CSRGraph
+        g = CSRGraph(torch.from_numpy(rowptr), torch.from_numpy(col), torch.from_numpy(val),
+                     rowptr.shape[0] - 1)
+        t, p = sharded.sharded_propagate(g, torch.from_numpy(X), T, alpha, ops=ops)
+        res = dict(target=t.numpy(), p_last=p.numpy())
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     dist.destroy_process_group()
 
@@ -144,3 +151,43 @@ def test_sharded_minibatch_labels_equal_sklearn_order(tmp_path):
     assert np.array_equal(two["labels"], ref["labels_"])
     assert float(two["inertia"]) == ref["inertia_"]
     assert np.array_equal(two["centers"].view(np.uint32), ref["cluster_centers_"].view(np.uint32))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("T", [1, 2, 5])
+def test_sharded_propagate_equals_oracle(tmp_path, world, T):
+    """Row-partitioned propagation (gdd.sharded.sharded_propagate): rank r computes rows
+    [r*m, (r+1)*m) of each hop from the all-gathered previous hop; target and the last hop are
+    bit-identical to the one-rank loop and the oracle's, with hub rows longer than one 256-entry
+    segment, a ragged last shard (n % world != 0) and a rank-spanning degree skew."""
+    _paths()
+    import scipy.sparse as sp
+    from gdd import synth
+    from oracle import oracle as O
+    n, d, alpha = 1201, 24, 0.91
+    A = sp.csr_matrix(synth.chung_lu(n, 30.0, 11))
+    A = A.tolil()
+    A[3, :700] = 1  # a hub row spanning three segments
+    A[:700, 3] = 1
+    A = sp.csr_matrix(A)
+    A.setdiag(0)
+    A.eliminate_zeros()
+    A.sort_indices()
+    ro, co, vo = O.normalize_csr(A.indptr, A.indices, None, -1)
+    assert np.diff(ro).max() > 512
+    X = synth.features(n, d, 11)
+    t_ref, p_ref = O.propagate(ro, co, vo, X, T, alpha)
+    one = _run(1, ("propagate", (ro, co, vo, X, T, alpha)), tmp_path / "w1")
+    many = _run(world, ("propagate", (ro, co, vo, X, T, alpha)), tmp_path / f"w{world}")
+    _same(one, many)
+    assert np.array_equal(many["target"].view(np.uint32), t_ref.view(np.uint32))
+    assert np.array_equal(many["p_last"].view(np.uint32), p_ref.view(np.uint32))
+
+
+def test_propagation_size_model():
+    _paths()
+    from gdd.sharded import propagation_shards_pay
+    assert propagation_shards_pay(2449029, 130_000_000, 100, 8)    # ogbn-products: shard
+    assert propagation_shards_pay(2449029, 130_000_000, 100, 2)
+    assert not propagation_shards_pay(169343, 2_560_000, 128, 8)   # ogbn-arxiv: replicate
+    assert not propagation_shards_pay(169343, 2_560_000, 128, 1)
