@@ -246,6 +246,7 @@ struct FoldArgs {
   int empty_as_zero;
   const int32_t* stop;
   int step_i;
+  int ld = 0;  // row stride of X (0: dim). A column range [f0, f1) folds X + f0 with dim = f1 - f0
 };
 
 template <typename ACC, bool WEIGHTED>
@@ -300,6 +301,7 @@ __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
   constexpr int U = VEC ? 4 : 1;            // floats per staged element
   constexpr int Q = kFoldElems / (256 * U);  // staged elements per thread per chunk
   const int dim = a.dim, tid = threadIdx.x;
+  const int64_t ldx = a.ld ? a.ld : dim;
   const int c = a.c0 + (int)blockIdx.y;
   const int32_t b = a.offsets[c], e = a.offsets[c + 1];
   const int nm = e - b;
@@ -357,7 +359,7 @@ __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const int64_t id = ids[min(r, R - 1)];
-        const float* src = a.X + id * dim + f0 + f * U;
+        const float* src = a.X + id * ldx + f0 + f * U;
         if constexpr (VEC) {
           const float4 v = *reinterpret_cast<const float4*>(src);
           xv[4 * q] = v.x;
@@ -470,7 +472,9 @@ int fold_launch_one(const FoldArgs& a0, int count, bool mean, hipStream_t s) {
   int R = std::min(kFoldMaxR, elems / a.fw_max);
   R &= ~15;
   a.R = std::max(R, 16);
-  const bool vec = a.dim % 4 == 0 && a.fw_max % 4 == 0 && (reinterpret_cast<uintptr_t>(a.X) & 15) == 0;
+  const int ldx = a.ld ? a.ld : a.dim;
+  const bool vec = a.dim % 4 == 0 && ldx % 4 == 0 && a.fw_max % 4 == 0 &&
+                   (reinterpret_cast<uintptr_t>(a.X) & 15) == 0;
   unsigned nsl = (unsigned)((a.dim + a.fw_max - 1) / a.fw_max);
   constexpr int kSliceCols = 16;  // columns per slice of a large cluster (a multiple of 4)
   if (a.big_rows > 0 && !mean && a.fw_max > kSliceCols) {
@@ -944,6 +948,40 @@ static size_t prune_ws(int64_t n, int k) {
          align256(sizeof(double) * (size_t)k) + 3 * 256;
 }
 
+// the Lloyd loop's workspace (gdd_kmeans_lloyd_run and the phase entry points below)
+struct LloydWs {
+  unsigned long long* keys;
+  float* cn2;
+  int32_t* perm;
+  int32_t* offsets;
+  size_t gb;
+  void* gws;
+  double *xn, *ub, *lb;
+  int64_t* list;
+  float* sec;
+  double *sep, *glob;
+  int64_t* count;
+};
+
+static bool carve_lloyd(void* ws, size_t ws_bytes, int64_t n, int k, LloydWs* w) {
+  Carver cv(ws, ws_bytes);
+  w->keys = cv.take<unsigned long long>(n);
+  w->cn2 = cv.take<float>(k);
+  w->perm = cv.take<int32_t>(n);
+  w->offsets = cv.take<int32_t>(k + 1);
+  w->gb = group_ws(n, k);
+  w->gws = cv.take<char>(w->gb);
+  w->xn = cv.take<double>(n);
+  w->ub = cv.take<double>(n);
+  w->lb = cv.take<double>(n);
+  w->list = cv.take<int64_t>(n);
+  w->sec = cv.take<float>(n);
+  w->sep = cv.take<double>(k);
+  w->glob = cv.take<double>(2);
+  w->count = cv.take<int64_t>(1);
+  return cv.ok();
+}
+
 extern "C" size_t gdd_kmeans_lloyd_ws_bytes(int64_t n, int dim, int k) {
   (void)dim;
   return align256(sizeof(unsigned long long) * (size_t)n) + align256(sizeof(float) * (size_t)k) +
@@ -967,22 +1005,22 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
   if (host_ws_bytes < gdd_kmeans_lloyd_host_ws_bytes())
     return fail(GDD_E_WORKSPACE, "kmeans_lloyd_run: host workspace too small");
   hipStream_t s = to_hip(stream);
-  Carver cv(ws, ws_bytes);
-  auto* keys = cv.take<unsigned long long>(n);
-  float* cn2 = cv.take<float>(k);
-  int32_t* perm = cv.take<int32_t>(n);
-  int32_t* offsets = cv.take<int32_t>(k + 1);
-  const size_t gb = group_ws(n, k);
-  void* gws = cv.take<char>(gb);
-  double* xn = cv.take<double>(n);
-  double* ub = cv.take<double>(n);
-  double* lb = cv.take<double>(n);
-  int64_t* list = cv.take<int64_t>(n);
-  float* sec = cv.take<float>(n);
-  double* sep = cv.take<double>(k);
-  double* glob = cv.take<double>(2);
-  int64_t* count = cv.take<int64_t>(1);
-  if (!cv.ok()) return fail(GDD_E_WORKSPACE, "kmeans_lloyd_run: workspace too small");
+  LloydWs lw;
+  if (!carve_lloyd(ws, ws_bytes, n, k, &lw)) return fail(GDD_E_WORKSPACE, "kmeans_lloyd_run: workspace too small");
+  auto* keys = lw.keys;
+  float* cn2 = lw.cn2;
+  int32_t* perm = lw.perm;
+  int32_t* offsets = lw.offsets;
+  const size_t gb = lw.gb;
+  void* gws = lw.gws;
+  double* xn = lw.xn;
+  double* ub = lw.ub;
+  double* lb = lw.lb;
+  int64_t* list = lw.list;
+  float* sec = lw.sec;
+  double* sep = lw.sep;
+  double* glob = lw.glob;
+  int64_t* count = lw.count;
   // bounded E-steps (GDD_LLOYD_PRUNE=0: every row every iteration), from the run's first E-step on
   const char* pe = getenv("GDD_LLOYD_PRUNE");
   const bool prune = !(pe && pe[0] == '0') && lloyd_prune_ok(dim, k);
@@ -1101,5 +1139,137 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
   if (!stop) done = max_iter;  // ran out of iterations (sklearn's loop end)
   *out_done = done;
   *out_reason = reason;
+  return GDD_OK;
+}
+
+// ---- one Lloyd iteration in three phases, for a process group (gdd.sharded.ShardedKMeans) --------
+// Rank r runs the bounded E-step on its rows and the M-step fold on its columns; the caller
+// all-gathers the labels and the column slices of the sums in between (RCCL, stream-ordered), and
+// every rank runs the same replicated update. Every kernel is gated by the stop word exactly as in
+// gdd_kmeans_lloyd_run (iteration i = steps 2i and 2i+1), so the host enqueues chunks of iterations
+// and reads the state once per chunk. Each value comes from the single-GPU kernels on the same
+// operands: labels, sums, centres, iteration counts are bit-identical for every world size.
+namespace gdd {
+namespace {
+// C_new[c][f] = the ranks' column slices of the sums side by side: rank r's slot (k * fw floats at
+// r * k * fw) holds its k x w_r block row-major, w_r = min(fw, dim - r * fw) columns
+__global__ void k_assemble_cols(int k, int dim, int fw, const float* __restrict__ parts,
+                                float* __restrict__ C_new, const int32_t* stop, int step_i) {
+  if (stopped(stop, step_i)) return;
+  const int64_t total = (int64_t)k * dim;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e / dim), f = (int)(e - (int64_t)c * dim);
+    const int r = f / fw, w = min(fw, dim - r * fw);
+    C_new[e] = parts[(int64_t)r * k * fw + (int64_t)c * w + (f - r * fw)];
+  }
+}
+
+// unit weights: the weight sums the fold writes (a sequential fp32 count, which sticks at 2^24), for
+// a rank that folds no columns
+__global__ void k_wsum_offsets(int k, const int32_t* __restrict__ offsets, float* __restrict__ wsum,
+                               const int32_t* stop, int step_i) {
+  if (stopped(stop, step_i)) return;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < k) wsum[c] = fminf((float)(offsets[c + 1] - offsets[c]), 16777216.f);
+}
+}  // namespace
+}  // namespace gdd
+
+extern "C" int gdd_lloyd_estep(int64_t n, int64_t r0, int64_t r1, int dim, const float* X, int k,
+                               const float* C, const float* shift, int first, int32_t* labels,
+                               void* state, int it, void* ws, size_t ws_bytes, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && 0 <= r0 && r0 <= r1 && r1 <= n && dim > 0 && dim <= 512 && k > 0 && X && C &&
+                  labels && state && ws && (first || shift) && it >= 0,
+              "lloyd_estep: bad arguments");
+  hipStream_t s = to_hip(stream);
+  LloydWs lw;
+  if (!carve_lloyd(ws, ws_bytes, n, k, &lw)) return fail(GDD_E_WORKSPACE, "lloyd_estep: workspace too small");
+  LloydState* st = static_cast<LloydState*>(state);
+  const int sa = 2 * it;
+  const int64_t m = r1 - r0;
+  if (m == 0) return GDD_OK;
+  const float* Xr = X + r0 * dim;
+  const char* pe = getenv("GDD_LLOYD_PRUNE");
+  const bool prune = !(pe && pe[0] == '0') && lloyd_prune_ok(dim, k);
+  if (!prune) return kmeans_assign_dev(m, dim, Xr, k, C, lw.cn2, labels + r0, lw.keys, &st->stop_at, sa, s);
+  const double kappa = (2.0 * dim + 8.0) * kEps32;
+  if (first) {  // the rows' norms, once per fit (the bounds start at this E-step)
+    k_row_norm64<<<blocks_of(m, 64), 256, 0, s>>>(m, dim, Xr, lw.xn + r0);
+    GDD_LAUNCHED();
+  }
+  k_ham_centres<<<k + 1, 256, 0, s>>>(k, dim, C, shift, first ? 0 : 1, lw.sep, lw.glob, lw.count,
+                                      &st->stop_at, sa);
+  GDD_LAUNCHED();
+  if (!first) {
+    k_ham_test<<<blocks_of(m, 256 * kHamRows), 256, 0, s>>>(m, dim, labels + r0, lw.xn + r0, lw.ub + r0,
+                                                             lw.lb + r0, shift, lw.sep, lw.glob, kappa,
+                                                             lw.list, lw.count, &st->stop_at, sa);
+    GDD_LAUNCHED();
+  }
+  int rc = kmeans_assign_top2_dev(m, dim, Xr, first ? nullptr : lw.list, first ? nullptr : lw.count, k, C,
+                                  lw.cn2, lw.keys, lw.sec, &st->stop_at, sa, s);
+  if (rc) return rc;
+  const unsigned fgrid = std::min<unsigned>(blocks_of(m), 2048);
+  k_ham_finalize<<<fgrid, 256, 0, s>>>(lw.count, m, first ? nullptr : lw.list, lw.keys, lw.sec, lw.xn + r0,
+                                       lw.glob, kappa, labels + r0, lw.ub + r0, lw.lb + r0, &st->stop_at, sa);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" int gdd_lloyd_mstep(int64_t n, int dim, const float* X, const int32_t* labels, int k, int f0,
+                               int f1, float* sums_cols, float* wsum, void* state, int it, void* ws,
+                               size_t ws_bytes, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && dim > 0 && k > 0 && 0 <= f0 && f0 <= f1 && f1 <= dim && X && labels && wsum &&
+                  state && ws && (f0 == f1 || sums_cols) && it >= 0,
+              "lloyd_mstep: bad arguments");
+  hipStream_t s = to_hip(stream);
+  LloydWs lw;
+  if (!carve_lloyd(ws, ws_bytes, n, k, &lw)) return fail(GDD_E_WORKSPACE, "lloyd_mstep: workspace too small");
+  LloydState* st = static_cast<LloydState*>(state);
+  const int sa = 2 * it;
+  int rc = group_dev(n, labels, k, lw.perm, lw.offsets, lw.gws, lw.gb, &st->stop_at, sa, s);
+  if (rc) return rc;
+  if (f1 > f0) {
+    FoldArgs fa{f1 - f0, 0, 0, 0, 0, 0, 0, 0, X + f0, nullptr, lw.perm, lw.offsets, sums_cols, wsum,
+                nullptr, 0, &st->stop_at, sa, dim};
+    const char* fe = getenv("GDD_FOLD_SLICE");
+    const double fs = fe ? atof(fe) : 1.5;
+    const double rows = fs * (double)n / (double)k;
+    fa.big_rows = fs > 0.0 ? (int)std::min<double>(std::max(rows, 4096.0), (double)INT_MAX) : 0;
+    rc = fold_launch(fa, k, false, s);
+    if (rc) return rc;
+  } else {
+    k_wsum_offsets<<<blocks_of(k), 256, 0, s>>>(k, lw.offsets, wsum, &st->stop_at, sa);
+    GDD_LAUNCHED();
+  }
+  k_lloyd_check_empty<<<1, 256, 0, s>>>(k, wsum, st, it, sa);
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" int gdd_lloyd_update(int64_t n, int dim, int k, const float* parts, int fw, float* C_new,
+                                const float* wsum, const float* C_old, float* shift,
+                                const int32_t* labels, int32_t* labels_old, double tol, void* state,
+                                int it, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && dim > 0 && k > 0 && fw > 0 && C_new && wsum && C_old && shift && labels &&
+                  labels_old && state && it >= 0,
+              "lloyd_update: bad arguments");
+  hipStream_t s = to_hip(stream);
+  LloydState* st = static_cast<LloydState*>(state);
+  const int sb = 2 * it + 1;
+  if (parts) {
+    const int64_t total = (int64_t)k * dim;
+    k_assemble_cols<<<(unsigned)std::min<int64_t>((total + 255) / 256, 2048), 256, 0, s>>>(
+        k, dim, fw, parts, C_new, &st->stop_at, sb);
+    GDD_LAUNCHED();
+  }
+  k_avg_centers<<<k, 64, 0, s>>>(k, dim, C_new, wsum, C_old, shift, &st->stop_at, sb);
+  GDD_LAUNCHED();
+  const unsigned cgrid = std::min<unsigned>(blocks_of(n), 2048);
+  k_lloyd_changed<<<cgrid, 256, 0, s>>>(n, labels, labels_old, st, sb);
+  GDD_LAUNCHED();
+  k_lloyd_converge<<<1, 256, 0, s>>>(k, shift, tol, st, it, sb);
+  GDD_LAUNCHED();
   return GDD_OK;
 }

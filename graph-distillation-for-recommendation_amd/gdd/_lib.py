@@ -82,6 +82,12 @@ SIGNATURES = {
     "gdd_kmeans_lloyd_run": (_c_int, [_c_i64, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_int,
                                       _c_int, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _c_size,
                                       _vp, _c_size, _vp]),
+    "gdd_lloyd_estep": (_c_int, [_c_i64, _c_i64, _c_i64, _c_int, _vp, _c_int, _vp, _vp, _c_int, _vp,
+                                 _vp, _c_int, _vp, _c_size, _vp]),
+    "gdd_lloyd_mstep": (_c_int, [_c_i64, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp,
+                                 _c_int, _vp, _c_size, _vp]),
+    "gdd_lloyd_update": (_c_int, [_c_i64, _c_int, _c_int, _vp, _c_int, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  ctypes.c_double, _vp, _c_int, _vp]),
     "gdd_skl_sqdist": (_c_int, [_c_int, _vp, _c_i64, _c_int, _vp, _vp, _vp]),
     "gdd_kmeans_plusplus_ws_bytes": (_c_size, [_c_i64, _c_int, _c_int]),
     "gdd_kmeans_plusplus": (_c_int, [_c_i64, _c_int, _vp, _vp, _c_int, _c_int, _c_i64, _vp, _vp,

@@ -78,6 +78,33 @@ def all_gather_parts(t: torch.Tensor, m: int, n: int, group=None) -> torch.Tenso
     return torch.cat(parts, 0)[:n].to(t.device)
 
 
+def assemble_cols(parts: torch.Tensor, k: int, dim: int, fw: int, world: int) -> torch.Tensor:
+    """The k x dim sums from the ranks' column slices (slot r: a row-major k x w_r block, w_r =
+    min(fw, dim - r*fw)), as gdd_lloyd_update's k_assemble_cols places them."""
+    cols = []
+    for r in range(world):
+        w = min(fw, dim - r * fw)
+        if w > 0:
+            cols.append(parts[r * k * fw:r * k * fw + k * w].view(k, w))
+    return torch.cat(cols, 1)
+
+
+def all_gather_slots(buf: torch.Tensor, m: int, group=None) -> None:
+    """In place: buf holds world * m rows (elements) and rank r's own slot is buf[r*m:(r+1)*m]; every
+    rank ends with every slot. RCCL for device tensors (stream-ordered, no host sync); gloo host-stages."""
+    rank, world = world_of(group)
+    if world == 1:
+        return
+    mine = buf[rank * m:(rank + 1) * m]
+    if buf.is_cuda and dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(buf, mine, group=group)
+        return
+    host = mine.cpu()
+    parts = [torch.empty_like(host) for _ in range(world)]
+    dist.all_gather(parts, host, group=group)
+    buf.copy_(torch.cat(parts, 0).to(buf.device))
+
+
 # ------------------------------------------------------------------------------------------------
 # the device primitives (libgdd)
 # ------------------------------------------------------------------------------------------------
@@ -155,6 +182,60 @@ class DeviceOps:
         out = torch.empty(1, dtype=torch.float32, device=self.device)
         _lib.check(self.lib.gdd_inertia(sq.shape[0], sq.data_ptr(), None, out.data_ptr(), self.stream))
         return float(out.item())
+
+    # -- the Lloyd loop in phases (gdd_lloyd_estep / _mstep / _update) ------------------------------
+    def lloyd_begin(self, n, dim, k, world, m, fw):
+        """Per-fit buffers: the workspace (bounds persist across iterations), the state word, labels
+        padded to world * m slots, labels_old, wsum, shift, and the column-slice exchange buffer."""
+        from types import SimpleNamespace
+        dev = self.device
+        return SimpleNamespace(
+            n=n, dim=dim, k=k,
+            ws=_lib.workspace(self.lib.gdd_kmeans_lloyd_ws_bytes(n, dim, k), dev),
+            state=torch.zeros(self.lib.gdd_lloyd_state_bytes(), dtype=torch.uint8, device=dev),
+            labels=torch.zeros(world * m, dtype=torch.int32, device=dev),
+            labels_old=torch.empty(n, dtype=torch.int32, device=dev),
+            wsum=torch.empty(k, dtype=torch.float32, device=dev),
+            shift=torch.zeros(k, dtype=torch.float32, device=dev),
+            parts=torch.zeros(world * k * fw, dtype=torch.float32, device=dev))
+
+    def lloyd_clear(self, ctx, resume):
+        ctx.state[:12].zero_()  # stop_at, reason, iter
+        if not resume:
+            ctx.state[12:16].zero_()  # the labels-changed flag
+            ctx.labels_old.fill_(-1)
+
+    def lloyd_estep(self, ctx, X, C, r0, r1, first, it):
+        _lib.check(self.lib.gdd_lloyd_estep(ctx.n, r0, r1, ctx.dim, X.data_ptr(), ctx.k, C.data_ptr(),
+                                            ctx.shift.data_ptr(), int(first), ctx.labels.data_ptr(),
+                                            ctx.state.data_ptr(), it, ctx.ws.data_ptr(), ctx.ws.numel(),
+                                            self.stream))
+
+    def lloyd_mstep(self, ctx, X, f0, f1, out, it):
+        _lib.check(self.lib.gdd_lloyd_mstep(ctx.n, ctx.dim, X.data_ptr(), ctx.labels.data_ptr(), ctx.k,
+                                            f0, f1, out.data_ptr(), ctx.wsum.data_ptr(),
+                                            ctx.state.data_ptr(), it, ctx.ws.data_ptr(), ctx.ws.numel(),
+                                            self.stream))
+
+    def lloyd_update(self, ctx, parts, fw, C_new, C_old, tol, it):
+        _lib.check(self.lib.gdd_lloyd_update(ctx.n, ctx.dim, ctx.k, _lib.ptr(parts), fw, C_new.data_ptr(),
+                                             ctx.wsum.data_ptr(), C_old.data_ptr(), ctx.shift.data_ptr(),
+                                             ctx.labels.data_ptr(), ctx.labels_old.data_ptr(), float(tol),
+                                             ctx.state.data_ptr(), it, self.stream))
+
+    def lloyd_state_begin(self, ctx):
+        """Start the state's device-to-host copy (pinned, stream-ordered); lloyd_state_end waits."""
+        h = torch.empty(8, dtype=torch.int32, pin_memory=True)
+        h.copy_(ctx.state[:32].view(torch.int32), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return h, ev
+
+    def lloyd_state_end(self, handle):
+        """(stop_at, reason, iter, done) of the copy lloyd_state_begin started."""
+        h, ev = handle
+        ev.synchronize()
+        return int(h[0]), int(h[1]), int(h[2]), int(h[4])
 
     def rows_plan(self, rows_graph, d):
         from .graph import SpMMPlan
@@ -274,16 +355,6 @@ def sharded_cluster_mean(feat, labels, k: int, empty_as_zero: bool = False, grou
 # ------------------------------------------------------------------------------------------------
 # Lloyd KMeans over the ranks
 # ------------------------------------------------------------------------------------------------
-def _iteration_status(wsum, labels, labels_old, shift):
-    """(any empty cluster, labels changed since the last iteration, center shifts as numpy) with
-    one device-to-host copy per iteration."""
-    changed = (torch.ones(1, device=labels.device) if labels_old is None
-               else (labels != labels_old).any().float().reshape(1))
-    h = torch.cat([(wsum == 0).any().float().reshape(1).to(changed.device), changed,
-                   shift.float().reshape(-1).to(changed.device)]).cpu().numpy()
-    return bool(h[0]), bool(h[1]), h[2:].astype(np.float32)
-
-
 class ShardedKMeans:
     """sklearn KMeans(n_clusters, n_init, max_iter, tol, random_state).fit (Lloyd, _kmeans.py:
     1427-1530 / :624-752) with the E-step partitioned by rows and the M-step by clusters. ``fit``
@@ -312,56 +383,85 @@ class ShardedKMeans:
             raise ValueError(f"n_samples={n} should be >= n_clusters={k}.")
         rank, world = world_of(group)
         r0, r1, m = part(n, rank, world)
-        c0, c1, q = part(k, rank, world)
+        f0, f1, fw = part(dim, rank, world)  # this rank's feature columns of the M-step
         rs = check_random_state(self.random_state)
         # centring and _tolerance on the whole (replicated) input, numpy's orders (:1476-1487, :279-288)
         Xc, X_mean, var = ops.center(X)
         tol_ = 0 if self.tol == 0 else np.mean(var) * self.tol
         n_init = 1 if self.n_init == "auto" else int(self.n_init)
+        ctx = ops.lloyd_begin(n, dim, k, world, m, fw)
+        labels = ctx.labels[:n]
+        mine = ctx.parts[rank * k * fw:(rank + 1) * k * fw].view(k, fw)
         best = None
         for _ in range(n_init):
-            C = ops.kmeans_plusplus(Xc, k, rs)  # same RandomState on every rank: same centres
-            labels_old = None
-            strict = False
-            it = 0
-            for it in range(self.max_iter):  # _kmeans_single_lloyd
-                lab, _ = ops.assign(Xc, C, r0, r1)
-                labels = all_gather_parts(lab, m, n, group)
-                grp = ops.group(labels, k)
-                sp_, wp = ops.mstep(Xc, grp, k, c0, c1)
-                sums = all_gather_parts(sp_, q, k, group).contiguous()
-                wsum = all_gather_parts(wp, q, k, group).contiguous()
-                # average as if no cluster emptied, then ONE host read of (empty cluster?, labels
-                # changed?, the k shifts); on an empty cluster (rare) relocate and average again
-                C_new, shift = ops.average(sums, wsum, C)
-                empty, changed, shift_h = _iteration_status(wsum, labels, labels_old, shift)
-                if empty:
-                    ops.relocate(Xc, C, sums, wsum, labels)  # replicated, identical on every rank
-                    C_new, shift = ops.average(sums, wsum, C)
-                    shift_h = shift.cpu().numpy()
-                C = C_new
-                if labels_old is not None and not changed:
-                    strict = True
+            C0 = ops.kmeans_plusplus(Xc, k, rs)  # same RandomState on every rank: same centres
+            Cb = (C0.contiguous(), torch.empty_like(C0))
+            it0, resume, first_e = 0, False, 0
+            while True:  # _kmeans_single_lloyd (:690-735), enqueued in chunks of iterations
+                ops.lloyd_clear(ctx, resume)
+                stop_at, reason, it_r, done = self._run_chunks(ops, ctx, Xc, Cb, it0, resume, first_e,
+                                                              (r0, r1, m), (f0, f1, fw), mine, tol_, group)
+                if reason != 3:
                     break
-                if (shift_h ** 2).sum() <= tol_:  # numpy's fp32 sum, as sklearn (:724-726)
-                    break
-                labels_old = labels
+                # an empty cluster at iteration it_r (rare): the sums to C[(it+1) % 2], sklearn's
+                # relocation on the host (replicated, identical on every rank), then resume there
+                it = it_r
+                C_new = Cb[(it + 1) % 2]
+                C_new.copy_(assemble_cols(ctx.parts, k, dim, fw, world))
+                ops.relocate(Xc, Cb[it % 2], C_new, ctx.wsum, labels)
+                it0, resume, first_e = it, True, it + 1
+            n_iter = done
+            strict = reason == 1
+            C = Cb[n_iter % 2]  # iteration i writes C[(i+1) % 2]
             if not strict:  # the final E-step with the last centres (:736-747)
                 lab, _ = ops.assign(Xc, C, r0, r1)
-                labels = all_gather_parts(lab, m, n, group)
-            sq = all_gather_parts(ops.point_sqdist(Xc, labels, C, r0, r1), m, n, group)
+                lab_full = all_gather_parts(lab, m, n, group)
+            else:
+                lab_full = labels.clone()
+            sq = all_gather_parts(ops.point_sqdist(Xc, lab_full, C, r0, r1), m, n, group)
             inertia = ops.inertia(sq)
-            lab_h = labels.cpu().numpy()
+            lab_h = lab_full.cpu().numpy()
             if best is None or (inertia < best[1] and not _same_clustering(lab_h, best[0], k)):
-                best = (lab_h, inertia, C.clone(), it + 1, labels)
-        lab_h, inertia, C, n_iter, labels = best
+                best = (lab_h, inertia, C.clone(), n_iter, lab_full.clone())
+        lab_h, inertia, C, n_iter, labels_best = best
         self.labels_ = lab_h
-        self.labels_device_ = labels
+        self.labels_device_ = labels_best
         self.inertia_ = inertia
         self.cluster_centers_ = C.cpu().numpy() + X_mean
         self.cluster_centers_device_ = ops.tensor(self.cluster_centers_, dtype=torch.float32)
         self.n_iter_ = n_iter
         return self
+
+    def _run_chunks(self, ops, ctx, Xc, Cb, it0, resume, first_e, rows, cols, mine, tol_, group):
+        """Iterations it0.. until the state's stop word is set or max_iter: each iteration is the
+        E-step on this rank's rows, ONE all-gather of the labels, the M-step on this rank's columns,
+        ONE all-gather of the column slices, the replicated update; the host reads the state once per
+        chunk (2, 4, then 8 iterations), one chunk behind, as gdd_kmeans_lloyd_run does."""
+        r0, r1, m = rows
+        f0, f1, fw = cols
+        i, ch, pending = it0, 2, None
+        while i < self.max_iter:
+            for _ in range(min(ch, self.max_iter - i)):
+                if not (resume and i == it0):
+                    ops.lloyd_estep(ctx, Xc, Cb[i % 2], r0, r1, i == first_e, i)
+                    all_gather_slots(ctx.labels, m, group)
+                    ops.lloyd_mstep(ctx, Xc, f0, f1, mine, i)
+                    all_gather_slots(ctx.parts, ctx.k * fw, group)
+                    ops.lloyd_update(ctx, ctx.parts, fw, Cb[(i + 1) % 2], Cb[i % 2], tol_, i)
+                else:  # resume after a relocation: C[(i+1) % 2] already holds the relocated sums
+                    ops.lloyd_update(ctx, None, fw, Cb[(i + 1) % 2], Cb[i % 2], tol_, i)
+                i += 1
+            handle = ops.lloyd_state_begin(ctx)
+            if pending is not None:
+                st = ops.lloyd_state_end(pending)  # the previous chunk's decision, read while this one runs
+                if st[0]:
+                    return st
+            pending = handle
+            ch = min(ch * 2, 8)
+        st = ops.lloyd_state_end(pending) if pending is not None else (0, 0, 0, 0)
+        if st[0]:
+            return st
+        return 0, 0, 0, self.max_iter  # ran out of iterations (sklearn's loop end)
 
     def fit_predict(self, X, y=None, sample_weight=None):
         return self.fit(X, sample_weight=sample_weight).labels_

@@ -264,6 +264,31 @@ int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, float* C0, f
                          int32_t* out_reason, void* ws, size_t ws_bytes, void* host_ws,
                          size_t host_ws_bytes, gdd_stream_t stream);
 
+/* One iteration of the same loop in three phases, for a process group over the GPUs of a node      */
+/* (gdd.sharded.ShardedKMeans): rank r runs the E-step (bounded as above) on its rows [r0, r1) and   */
+/* the ordered M-step fold on its feature columns [f0, f1) of every cluster; between the phases the  */
+/* caller all-gathers the labels and the column slices (RCCL, stream-ordered), and every rank runs  */
+/* the same update. ws: gdd_kmeans_lloyd_ws_bytes(n, dim, k), kept across iterations (it holds the   */
+/* rows' bounds); state as above, its stop word gating every kernel (iteration `it` = steps 2it and */
+/* 2it+1), so chunks of iterations can be enqueued ahead of the host's read of the state.           */
+/* gdd_lloyd_estep: labels[r0:r1) for centres C (shift: the previous update's, unless `first` — the */
+/* first E-step of a fit or after a relocation, which sets the rows' bounds).                        */
+/* gdd_lloyd_mstep: groups the full labels, sums_cols = k x (f1-f0) column sums, wsum = k weights,    */
+/* then the empty-cluster check (reason 3).                                                          */
+/* gdd_lloyd_update: C_new = the column slices in `parts` (slot r of k*fw floats: rank r's columns   */
+/* [r*fw, min(dim, (r+1)*fw)) as a row-major k x w_r block; parts NULL: C_new already holds the      */
+/* sums), _average_centers,                                                                          */
+/* _center_shift, the labels-changed flag and the convergence test.                                  */
+int gdd_lloyd_estep(int64_t n, int64_t r0, int64_t r1, int dim, const float* X, int k, const float* C,
+                    const float* shift, int first, int32_t* labels, void* state, int it, void* ws,
+                    size_t ws_bytes, gdd_stream_t stream);
+int gdd_lloyd_mstep(int64_t n, int dim, const float* X, const int32_t* labels, int k, int f0, int f1,
+                    float* sums_cols, float* wsum, void* state, int it, void* ws, size_t ws_bytes,
+                    gdd_stream_t stream);
+int gdd_lloyd_update(int64_t n, int dim, int k, const float* parts, int fw, float* C_new,
+                     const float* wsum, const float* C_old, float* shift, const int32_t* labels,
+                     int32_t* labels_old, double tol, void* state, int it, gdd_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------------- */
 /* Greedy k-means++ seeding, sklearn _kmeans_plusplus (sklearn/cluster/_kmeans.py:174-272) on the    */
 /* device. Host supplies the reference RNG draws: first_id (random_state.choice) and                 */

@@ -68,6 +68,78 @@ class OracleOps:
         s = np.ascontiguousarray(_np(sq), np.float32)
         return float(O.lib().oracle_inertia(s.shape[0], s, None))
 
+    # -- the Lloyd loop in phases: the oracle's arithmetic with the device's stop-word gating ------
+    def lloyd_begin(self, n, dim, k, world, m, fw):
+        from types import SimpleNamespace
+        return SimpleNamespace(n=n, dim=dim, k=k, state=np.zeros(16, np.int32),
+                               labels=torch.zeros(world * m, dtype=torch.int32),
+                               labels_old=torch.empty(n, dtype=torch.int32),
+                               wsum=torch.empty(k, dtype=torch.float32),
+                               shift=torch.zeros(k, dtype=torch.float32),
+                               parts=torch.zeros(world * k * fw, dtype=torch.float32))
+
+    @staticmethod
+    def _stopped(ctx, step):
+        v = int(ctx.state[0])
+        return v != 0 and v - 1 < step
+
+    def lloyd_clear(self, ctx, resume):
+        ctx.state[:3] = 0
+        if not resume:
+            ctx.state[3] = 0
+            ctx.labels_old.fill_(-1)
+
+    def lloyd_estep(self, ctx, X, C, r0, r1, first, it):
+        if self._stopped(ctx, 2 * it) or r1 <= r0:
+            return
+        lab, _ = O.assign(_np(X)[r0:r1], _np(C))
+        ctx.labels[r0:r1] = torch.from_numpy(lab)
+
+    def lloyd_mstep(self, ctx, X, f0, f1, out, it):
+        if self._stopped(ctx, 2 * it):
+            return
+        x = np.ascontiguousarray(_np(X), np.float32)
+        k = ctx.k
+        sums = np.empty((k, x.shape[1]), np.float32)
+        wic = np.empty(k, np.float32)
+        lab = np.ascontiguousarray(ctx.labels[:ctx.n].numpy())
+        O.lib().oracle_segment_sum_f32(x.shape[0], x.shape[1], x, None, lab, k, sums, wic)
+        if f1 > f0:
+            out.view(-1)[:k * (f1 - f0)] = torch.from_numpy(np.ascontiguousarray(sums[:, f0:f1]).ravel())
+        ctx.wsum[:] = torch.from_numpy(wic)
+        if np.any(wic == 0):  # k_lloyd_check_empty
+            ctx.state[1], ctx.state[2], ctx.state[0] = 3, it, 2 * it + 1
+
+    def lloyd_update(self, ctx, parts, fw, C_new, C_old, tol, it):
+        if self._stopped(ctx, 2 * it + 1):
+            return
+        from gdd.sharded import assemble_cols
+        k, dim = ctx.k, ctx.dim
+        if parts is not None:
+            C_new.copy_(assemble_cols(parts, k, dim, fw, -(-dim // fw)))
+        cn, shift = self.average(C_new, ctx.wsum, C_old)
+        C_new.copy_(cn)
+        ctx.shift.copy_(shift)
+        lab = ctx.labels[:ctx.n]
+        if bool((lab != ctx.labels_old).any()):  # k_lloyd_changed
+            ctx.state[3] = 1
+            ctx.labels_old.copy_(lab)
+        reason = 0
+        if ctx.state[3] == 0:
+            reason = 1
+        elif float((shift.numpy() ** 2).sum()) <= tol:  # numpy's pairwise fp32 sum
+            reason = 2
+        ctx.state[3] = 0
+        ctx.state[4] = it + 1
+        if reason:
+            ctx.state[1], ctx.state[2], ctx.state[0] = reason, it, 2 * it + 2
+
+    def lloyd_state_begin(self, ctx):
+        return ctx.state.copy()
+
+    def lloyd_state_end(self, h):
+        return int(h[0]), int(h[1]), int(h[2]), int(h[4])
+
     def rows_plan(self, rows_graph, d):
         return (_np(rows_graph.rowptr), _np(rows_graph.col), _np(rows_graph.values()))
 

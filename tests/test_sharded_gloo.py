@@ -99,9 +99,11 @@ def test_sharded_lloyd_equals_sklearn_fixture(tmp_path, n_init):
     assert float(two["inertia"]) == float(z[f"{tag}_inertia"])
 
 
-@pytest.mark.parametrize("n,dim,k", [(3001, 8, 12), (50, 4, 50), (300, 3, 12)])
-def test_sharded_lloyd_equals_oracle_incl_relocation(tmp_path, n, dim, k):
-    # (50, 4, 50): duplicated rows and k = n, so clusters empty out and are relocated / copied
+@pytest.mark.parametrize("n,dim,k,world", [(3001, 8, 12, 2), (3001, 8, 12, 3), (50, 4, 50, 2),
+                                           (50, 4, 50, 3), (300, 3, 12, 2), (300, 3, 12, 4)])
+def test_sharded_lloyd_equals_oracle_incl_relocation(tmp_path, n, dim, k, world):
+    # (50, 4, 50): duplicated rows and k = n, so clusters empty out and are relocated / copied;
+    # world 3 splits 8 columns 3 + 3 + 2, world 4 leaves a rank with no column of dim 3
     _paths()
     from gdd import synth
     from oracle import oracle as O
@@ -109,7 +111,7 @@ def test_sharded_lloyd_equals_oracle_incl_relocation(tmp_path, n, dim, k):
     X[1::7] = X[0]
     ref = O.kmeans(X, k, random_state=7)
     one = _run(1, ("kmeans", (X, k, 1, 7)), tmp_path / "w1")
-    two = _run(2, ("kmeans", (X, k, 1, 7)), tmp_path / "w2")
+    two = _run(world, ("kmeans", (X, k, 1, 7)), tmp_path / f"w{world}")
     _same(one, two)
     assert int(two["n_iter"]) == ref["n_iter_"]
     assert np.array_equal(two["labels"], ref["labels_"])
