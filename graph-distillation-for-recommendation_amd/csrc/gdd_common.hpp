@@ -79,8 +79,11 @@ int sort_pairs_i32(const int32_t* keys_in, int32_t* keys_out, const int32_t* val
 // starts ~1 us sooner after its predecessor than a stream launch does (tools/probe/gap_probe.hip:
 // 1.6 vs 2.5-2.8 us per dependent launch). `key` (with `site`) must determine every argument of every
 // launch `enqueue` issues (pointers, sizes, step indices), so a replay is the same work as the
-// eager sequence. GDD_GRAPH=0 runs every sequence eagerly; 1 (default) records a key on its second
-// occurrence (one-off shapes never pay the recording); 2 records on the first (parity tests).
+// eager sequence. GDD_GRAPH=0 (default) runs every sequence eagerly; 1 records a key on its second
+// occurrence; 2 records on the first (parity tests). Measured (r04, tools/micro_graph.py): no gain
+// on the real kernels — the host enqueues far ahead of these 5-15 us kernels, so a stream launch's
+// gap is already the device's own (MiniBatchKMeans fit 14.05 ms replayed vs 14.00 eager, k-means++
+// 4.13 vs 4.20 ms) — and a recording costs a fit's worth of time, so it stays opt-in.
 // ---------------------------------------------------------------------------------------------
 int replay_or_run(const char* site, const void* key, size_t key_bytes, hipStream_t s,
                   const std::function<int(hipStream_t)>& enqueue);

@@ -1892,18 +1892,21 @@ __global__ __launch_bounds__(256) void k_kpp1_fused(Kpp1Args a, int c) {
                   a.candw[cq] + (int64_t)t * T);
 }
 
-// ---- single-block rounds from a distance table (plain-chain plans, dim <= 48, n <= 4096). The
+// ---- single-block rounds from a distance table (plain-chain plans, dim <= 64, n <= 4096). The
 // plain fp64 chain of a distance does not depend on the trial slot the candidate occupies, so every
 // distance a round can ask for is one entry of D[j][i] = the clamped fp32 upcast distance between
 // candidate point j and point i, computed once per fit by k_kpp_dmat in exactly the arithmetic of
-// the distance phase above (zero-padded 48-term fma chain, ((-2 dot) + |c|^2) + |x|^2, clamp).
+// the distance phase above (zero-padded 48- or 64-term fma chain, ((-2 dot) + |c|^2) + |x|^2, clamp).
 // A round is then ONE workgroup per trial: round c-1's potentials and this trial's candidate column
 // (trip 1), the winner's row = the closest distances and the candidate's D row (trip 2), the fold.
 // No distance phase, no write-through hand-off, no re-read of the row.
-constexpr int kDmX = 48;   // feature slots of the table's chain (dim <= kDmX, zero-padded)
+// The chain's feature slots: 48 (dim <= 48) or 64 (dim <= 64, e.g. the recsys SVD embeddings);
+// slots past dim are zero, and an fma with a zero operand leaves the chain unchanged.
+constexpr int kDmX = 64;   // widest table chain (dim <= kDmX)
 constexpr int kDmJ = 32;   // candidate rows per table workgroup
 constexpr int kDmMinK = 16;  // centres from which the table is built
 
+template <int kDmX>
 __global__ __launch_bounds__(256) void k_kpp_dmat(int n, int dim, const float* __restrict__ X,
                                                   const float* __restrict__ XT,
                                                   const double* __restrict__ xsq,
@@ -2389,8 +2392,11 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     GDD_LAUNCHED();
     // the distance table pays once the rounds it saves (~3 us each) cover its one-off build
     if (seq && Dm && k >= kDmMinK && getenv("GDD_KPP_NO_TABLE") == nullptr) {
-      k_kpp_dmat<<<dim3((unsigned)((n + 255) / 256), (unsigned)((n + kDmJ - 1) / kDmJ)), 256, 0, s>>>(
-          (int)n, dim, X, XT, xsq, Dm);
+      const dim3 gdm((unsigned)((n + 255) / 256), (unsigned)((n + kDmJ - 1) / kDmJ));
+      if (dim <= 48)
+        k_kpp_dmat<48><<<gdm, 256, 0, s>>>((int)n, dim, X, XT, xsq, Dm);
+      else
+        k_kpp_dmat<64><<<gdm, 256, 0, s>>>((int)n, dim, X, XT, xsq, Dm);
       GDD_LAUNCHED();
       const bool plain = getenv("GDD_KPP_CHAIN_PLAIN") != nullptr;
       if (T <= kPairMaxT && getenv("GDD_KPP_SINGLE_ROUND") == nullptr) {

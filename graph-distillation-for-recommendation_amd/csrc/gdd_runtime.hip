@@ -82,7 +82,7 @@ constexpr size_t kGraphCap = 512;
 
 int graph_mode() {
   const char* e = getenv("GDD_GRAPH");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 0;
 }
 }  // namespace
 

@@ -232,7 +232,7 @@ def run(args, out_root: str = "ClustGDD", embeddings=None, timings: Optional[dic
             with torch.no_grad():
                 r = evaluate()
             model.train()
-            model.graph.check()  # at a point that synchronises anyway: no edge row id out of range
+            model.graph().check()  # at a point that synchronises anyway: no edge row id out of range
             print(f"[refine] ep={ep:04d} loss={loss.item():.6f} Recall@{args.eval_topk}={r:.6f}")
     torch.cuda.synchronize()
     tm["refine_s"] = time.perf_counter() - t0

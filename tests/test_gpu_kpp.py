@@ -73,6 +73,9 @@ KPP_CASES = [
     (700, 600, 30, None, None),   # rows wider than the fused kernel's 512: two launches per round
     (10, 3, 2, None, None),       # k = 2: a single round, no centre gather
     (2708, 7, 70, None, None),    # Cora shape: T = 6, two trials on the 4-lane sgemv_t kernel
+    (3706, 64, 371, None, None),  # ML-1M items (recsys SVD dim 64): the 64-slot distance table
+    (3000, 57, 120, 5, None),     # a table chain with 7 zero slots, duplicates
+    (4096, 64, 60, None, None),
 ]
 
 
@@ -107,7 +110,8 @@ def test_kmeans_plusplus_two_launch_path(monkeypatch):
                                      (4095, 3, 1000), (37, 5, 16),
                                      # an even number of rounds: the last launch is a pair
                                      (3000, 40, 455), (2708, 7, 71), (1999, 20, 17), (37, 5, 17),
-                                     (4095, 3, 1097)])  # T = 9: one round per launch
+                                     (4095, 3, 1097),  # T = 9: one round per launch
+                                     (3706, 64, 371), (2000, 49, 101)])  # the 64-slot table
 def test_kmeans_plusplus_round_forms(monkeypatch, n, dim, k):
     """Every single-block round form gives the oracle's seeding, bit for bit: two rounds per launch
     over the distance table (default for plain-chain plans, dim <= 48, k >= 16, T <= 8), one round

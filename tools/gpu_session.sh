@@ -18,6 +18,7 @@
 #   kpp                   tools/micro_kpp.py (k-means++ round micro-benchmark)
 #   inertia               tools/micro_inertia.py (parallel exact inertia vs the one-lane fold)
 #   gap                   tools/probe/gap_probe (dependent launches: stream vs hipGraph replay)
+#   graph-ab              tools/micro_graph.py (MiniBatchKMeans / k-means++ fits, eager vs graph replay)
 #   assign                tools/bench_assign.py (full assignment pass, fp32 vs bf16, three shapes)
 #   assign-ab             tools/bench_assign.py with the wave-tile fp32 pass vs GDD_ASSIGN_PERSIST=1
 #   hop-lanes             tools/micro_prop.py at arxiv / products with the XCD slice A/B switch
@@ -76,6 +77,7 @@ for step in "$@"; do
     kpp) run 300 kpp python tools/micro_kpp.py ;;
     inertia) run 300 inertia bash -c 'python tools/micro_inertia.py && GDD_INERTIA_SEQ=1 python tools/micro_inertia.py' ;;
     gap) run 60 gap ./tools/probe/gap_probe ;;
+    graph-ab) run 300 graph_ab python tools/micro_graph.py ;;
     kpp-products) run 300 kpp_products python tools/micro_kpp_products.py ;;
     assign) run 300 assign python tools/bench_assign.py ;;
     assign-ab) run 400 assign_ab bash -c 'python tools/bench_assign.py && GDD_ASSIGN_PERSIST=1 python tools/bench_assign.py && python tools/bench_assign.py' ;;
