@@ -587,6 +587,7 @@ struct KppArgs {
   int64_t* indices;
   SklPlan plan;
   int exact;          // cum_tol's mode
+  const float* D;     // the n x n distance table (plain-chain plans, n <= kDmBigMax), or nullptr
 };
 
 __device__ __forceinline__ float wv(const float* w, int64_t i) { return w ? w[i] : 1.0f; }
@@ -1082,13 +1083,28 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 23);
   if constexpr (PICK) return;  // the split path: k_kpp_dists computes every trial's distances
   // ---- distances of this block's points to the candidate, np.minimum with the winner's row
-  const double cn = a.xsq[ct];
-  for (int j = tid; j < a.dim; j += kThr) s_c[j] = (double)a.X[ct * a.dim + j];
-  __syncthreads();
   float* s_d = reinterpret_cast<float*>(s_c + a.dim);
   const int64_t j0 = (int64_t)blk * kBlk;
   float* drow = a.dist[cq] + (int64_t)t * n;
-  block_dists<SEQ>(a, t, j0, cn, s_c, wrow, drow, s_d);
+  if (SEQ && a.D) {  // the distance table holds the plain chain's value for every (candidate, point)
+    const float* Drow = a.D + ct * n;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int o = tid + kThr * q;
+      const int64_t i = j0 + o;
+      float f = 0.f;
+      if (i < n) {
+        f = np_minimum(wrow[i], Drow[i]);
+        drow[i] = f;
+      }
+      s_d[o] = f;
+    }
+  } else {
+    const double cn = a.xsq[ct];
+    for (int j = tid; j < a.dim; j += kThr) s_c[j] = (double)a.X[ct * a.dim + j];
+    __syncthreads();
+    block_dists<SEQ>(a, t, j0, cn, s_c, wrow, drow, s_d);
+  }
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 24);
   // ---- the block's terms for round c+1: cumulative total, sgemv_t lane chains
@@ -2230,11 +2246,22 @@ extern "C" int gdd_skl_sqdist(int n_rows, const float* C, int64_t n, int dim, co
 
 size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k);
 
+// k (centres) only sizes the fused rounds' arrival counters and gates the tables; the query bounds
+// it by n
 extern "C" size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int dim, int n_trials) {
   return kpp_ws_bytes(n, dim, n_trials, (int)std::min<int64_t>(n, INT_MAX));
 }
 
-// k (centres) only sizes the fused rounds' arrival counters; the query bounds it by n
+// the multi-block rounds read their distances from an n x n table when every distance is the plain
+// chain (slot-independent) and the table is affordable: n <= kDmBigMax (4 GiB), dim <= kDmX, k >=
+// kDmMinK. ML-1M users (6,040 x 64, k = 604), Ali-Display users (17,730 x 64, k = 1,773)
+constexpr int64_t kDmBigMax = 32768;
+bool kpp_big_table(int64_t n, int dim, int T, int k) {
+  if (n <= kBlk || n > kDmBigMax || dim > kDmX || T < 2 || k < kDmMinK) return false;
+  if (getenv("GDD_KPP_NO_TABLE") != nullptr) return false;
+  return skl_all_seq(n, T, dim, skl_batch_size(T, n, dim));
+}
+
 size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k) {
   const size_t T = (size_t)std::max(n_trials, 1);
   const size_t nblk = (size_t)((n + kBlk - 1) / kBlk);
@@ -2256,6 +2283,7 @@ size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k) {
   b += align256(sizeof(int) * 2) + align256(sizeof(unsigned) * (size_t)std::max(k, 1) * T);  // counters
   if (n <= kBlk || (int64_t)n * std::max(dim, 1) < INT_MAX)
     b += align256(sizeof(float) * n * (size_t)std::max(dim, 1));  // XT
+  if (kpp_big_table(n, dim, (int)T, k)) b += align256(sizeof(float) * n * n);  // multi-block table
   if (n <= kBlk && dim <= kDmX && T >= 2) {
     b += align256(sizeof(float) * n * n);  // distance table
     b += 2 * (align256(sizeof(float) * T * T * n) + align256(sizeof(float) * T * T) +
@@ -2301,6 +2329,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   b1.win = cv.take<int>(2);
   b1.counter = cv.take<unsigned>((size_t)std::min<int64_t>(n, INT_MAX) * T);
   float* XT = (n <= kBlk || n * (int64_t)dim < INT_MAX) ? cv.take<float>((size_t)n * dim) : nullptr;
+  float* Dbig = kpp_big_table(n, dim, T, k) ? cv.take<float>((size_t)n * n) : nullptr;
   float* Dm = (n <= kBlk && dim <= kDmX && T >= 2) ? cv.take<float>((size_t)n * n) : nullptr;
   if (Dm) {
     for (int q = 0; q < 2; ++q) {
@@ -2513,6 +2542,15 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     k_kpp_final<<<1, kThr, 0, s>>>(a, k - 1);
     GDD_LAUNCHED();
     return GDD_OK;
+  }
+  if (Dbig && seq && a.XT) {  // the distances once per fit (~n^2 dim fp64 fmas), then table rounds
+    const dim3 gdm((unsigned)((n + 255) / 256), (unsigned)((n + kDmJ - 1) / kDmJ));
+    if (dim <= 48)
+      k_kpp_dmat<48><<<gdm, 256, 0, s>>>((int)n, dim, X, a.XT, xsq, Dbig);
+    else
+      k_kpp_dmat<64><<<gdm, 256, 0, s>>>((int)n, dim, X, a.XT, xsq, Dbig);
+    GDD_LAUNCHED();
+    a.D = Dbig;
   }
   for (int c = 1; c < k; ++c) {
     if (seq)

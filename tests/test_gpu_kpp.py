@@ -76,6 +76,8 @@ KPP_CASES = [
     (3706, 64, 371, None, None),  # ML-1M items (recsys SVD dim 64): the 64-slot distance table
     (3000, 57, 120, 5, None),     # a table chain with 7 zero slots, duplicates
     (4096, 64, 60, None, None),
+    (6040, 64, 200, None, None),  # ML-1M users' shape: multi-block rounds over the n x n table
+    (9001, 49, 100, 5, None),     # three blocks, duplicates
 ]
 
 
