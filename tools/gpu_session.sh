@@ -20,6 +20,7 @@
 #   gap                   tools/probe/gap_probe (dependent launches: stream vs hipGraph replay)
 #   graph-ab              tools/micro_graph.py (MiniBatchKMeans / k-means++ fits, eager vs graph replay)
 #   inertia-ab            bench.py (no CPU baseline) with the parallel inertia vs the one-lane fold, twice each
+#   fold-cols             tools/micro_fold_cols.py (products M-step over all columns vs one rank's slice)
 #   assign                tools/bench_assign.py (full assignment pass, fp32 vs bf16, three shapes)
 #   assign-ab             tools/bench_assign.py with the wave-tile fp32 pass vs GDD_ASSIGN_PERSIST=1
 #   hop-lanes             tools/micro_prop.py at arxiv / products with the XCD slice A/B switch
@@ -79,6 +80,7 @@ for step in "$@"; do
     inertia) run 300 inertia bash -c 'python tools/micro_inertia.py && GDD_INERTIA_SEQ=1 python tools/micro_inertia.py' ;;
     gap) run 60 gap ./tools/probe/gap_probe ;;
     graph-ab) run 300 graph_ab python tools/micro_graph.py ;;
+    fold-cols) run 300 fold_cols python tools/micro_fold_cols.py ;;
     inertia-ab) run 600 inertia_ab bash -c 'for v in 0 1 0 1; do echo "GDD_INERTIA_SEQ=$v"; GDD_INERTIA_SEQ=$v python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
     kpp-products) run 300 kpp_products python tools/micro_kpp_products.py ;;
     assign) run 300 assign python tools/bench_assign.py ;;
