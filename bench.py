@@ -563,6 +563,9 @@ def cpu_baseline(cfg, A, X_h):
     total = t5 - t0
     return {"value": n / total, "unit": "nodes/s", "cores": threads, "kind": "reference-library",
             "affinity_cpus": affinity, "omp_num_threads": omp or None, "cpu_model": _cpu_model(),
+            "threads_policy": ("min(affinity mask, OMP_NUM_THREADS): the GPU box's lease sets "
+                               "OMP_NUM_THREADS to its CPU share (16 on a one-GPU box) although the "
+                               "affinity mask shows the whole machine; the baseline runs that share"),
             "sample": (f"one whole step of the reference's CPU path on the bench's graph ({n} nodes): "
                        f"scipy normalize_adj, {cfg.T - 1} torch CPU sparse hops, logits GEMM, sklearn "
                        f"MiniBatchKMeans(k={cfg.k}, b={cfg.batch}, seed {cfg.seed}, {km.n_steps_} steps), "

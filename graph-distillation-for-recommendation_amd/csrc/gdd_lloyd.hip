@@ -228,6 +228,11 @@ constexpr int kFoldElemsMax = 16384;  // floats per LDS chunk buffer (64 KiB)
 // hundred clusters runs in one wave instead of two (each workgroup's chunk pipeline is latency-bound;
 // arxiv bench shape, 454 clusters: 62.5 -> 50.4 us per cluster_mean call; quarter size 54.3)
 constexpr int kFoldElemsMean = 8192;
+// Lloyd sums of small clusters (r04): 8 KiB chunk buffers, so ~8 workgroups share a CU and a few
+// hundred clusters of tens of members fold in one wave of workgroups instead of three (the recsys
+// KMeans shapes: 6,040 x 64 with k = 604, ~10 members per cluster); dim <= 128 keeps R >= 16
+constexpr int kFoldElemsSmall = 2048;
+constexpr int kFoldSmallAvgRows = 64;
 constexpr int kFoldMaxR = 1024;
 
 struct FoldArgs {
@@ -247,6 +252,7 @@ struct FoldArgs {
   const int32_t* stop;
   int step_i;
   int ld = 0;  // row stride of X (0: dim). A column range [f0, f1) folds X + f0 with dim = f1 - f0
+  int64_t avg_rows = 0;  // members per cluster on average (0: unknown); small averages fold in 8 KiB chunks
 };
 
 template <typename ACC, bool WEIGHTED>
@@ -468,7 +474,8 @@ int fold_launch_one(const FoldArgs& a0, int count, bool mean, hipStream_t s) {
   const bool weighted = a.w != nullptr;
   a.fw_max = std::min(a.dim, weighted ? 192 : 256);  // weighted: thread 255 folds the weights
   if (a.fw_max % 4 != 0 && a.fw_max < a.dim) a.fw_max &= ~3;
-  const int elems = mean ? kFoldElemsMean : kFoldElemsMax;
+  const bool small = !mean && a.avg_rows > 0 && a.avg_rows <= kFoldSmallAvgRows && a.dim <= 128;
+  const int elems = mean ? kFoldElemsMean : (small ? kFoldElemsSmall : kFoldElemsMax);
   int R = std::min(kFoldMaxR, elems / a.fw_max);
   R &= ~15;
   a.R = std::max(R, 16);
@@ -499,6 +506,13 @@ int fold_launch_one(const FoldArgs& a0, int count, bool mean, hipStream_t s) {
   if (mean)
     return vec ? go(k_seg_fold<double, true, false, true, kFoldElemsMean>)
                : go(k_seg_fold<double, false, false, true, kFoldElemsMean>);
+  if (small) {
+    if (weighted)
+      return vec ? go(k_seg_fold<float, true, true, false, kFoldElemsSmall>)
+                 : go(k_seg_fold<float, false, true, false, kFoldElemsSmall>);
+    return vec ? go(k_seg_fold<float, true, false, false, kFoldElemsSmall>)
+               : go(k_seg_fold<float, false, false, false, kFoldElemsSmall>);
+  }
   if (weighted)
     return vec ? go(k_seg_fold<float, true, true, false>) : go(k_seg_fold<float, false, true, false>);
   return vec ? go(k_seg_fold<float, true, false, false>) : go(k_seg_fold<float, false, false, false>);
@@ -649,26 +663,110 @@ __global__ __launch_bounds__(256) void k_lloyd_check_empty(int k, const float* _
   }
 }
 
+// numpy's pairwise sum of LDS values s[0..n), its leaves evaluated by the workgroup (r04): the leaves
+// of pw_sum's recursion (blocks of <= 128 values) in visit order, their eight interleaved accumulators
+// one per thread, each leaf's tree and tail, then thread 0 adds the leaf values up the same recursion.
+// Same operations, same order as pw_sum: the same bits. n <= kShiftLds.
+constexpr int kPwLeavesMax = 256;  // leaves hold >= 57 values once n > 128: 8192 / 57 < 256
+struct PwLds {
+  int off[kPwLeavesMax], len[kPwLeavesMax];
+  float acc[kPwLeavesMax * 8];
+  float leaf[kPwLeavesMax];
+  int nleaves;
+};
+
+template <int D>
+__device__ void pw_leaves_rec(int off, int n, PwLds& L) {
+  if constexpr (D == 0) {
+    L.off[L.nleaves] = off;
+    L.len[L.nleaves] = n;
+    ++L.nleaves;
+  } else {
+    if (n <= 128) {
+      L.off[L.nleaves] = off;
+      L.len[L.nleaves] = n;
+      ++L.nleaves;
+      return;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    pw_leaves_rec<D - 1>(off, n2, L);
+    pw_leaves_rec<D - 1>(off + n2, n - n2, L);
+  }
+}
+
+template <int D>
+__device__ float pw_combine(int n, const PwLds& L, int& li) {
+  if constexpr (D == 0) {
+    return L.leaf[li++];
+  } else {
+    if (n <= 128) return L.leaf[li++];
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    const float a = pw_combine<D - 1>(n2, L, li);
+    const float b = pw_combine<D - 1>(n - n2, L, li);
+    return a + b;
+  }
+}
+
+__device__ float pw_sum_block(const float* __restrict__ s, int n, PwLds& L) {
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    L.nleaves = 0;
+    pw_leaves_rec<8>(0, n, L);
+  }
+  __syncthreads();
+  const int nl = L.nleaves;
+  for (int q = tid; q < nl * 8; q += blockDim.x) {  // leaf q / 8, accumulator q % 8
+    const int off = L.off[q >> 3], len = L.len[q >> 3], j = q & 7;
+    if (len >= 8) {
+      float r = s[off + j];
+      for (int i = 8; i < len - (len % 8); i += 8) r = r + s[off + i + j];
+      L.acc[q] = r;
+    }
+  }
+  __syncthreads();
+  for (int l = tid; l < nl; l += blockDim.x) {
+    const int off = L.off[l], len = L.len[l];
+    float res;
+    int i;
+    if (len < 8) {
+      res = 0.f;
+      i = 0;
+    } else {
+      const float* r = L.acc + l * 8;
+      res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+      i = len - (len % 8);
+    }
+    for (; i < len; ++i) res = res + s[off + i];
+    L.leaf[l] = res;
+  }
+  __syncthreads();
+  int li = 0;
+  return pw_combine<8>(n, L, li);  // thread 0's value is the one used
+}
+
 constexpr int kShiftLds = 8192;
 __global__ __launch_bounds__(256) void k_lloyd_converge(int k, const float* __restrict__ shift,
                                                         double tol, LloydState* st, int it,
                                                         int step_i) {
   if (stopped(&st->stop_at, step_i)) return;
   __shared__ float sq[kShiftLds];
+  __shared__ PwLds pl;
   const bool in_lds = k <= kShiftLds;
   if (in_lds)
     for (int j = threadIdx.x; j < k; j += blockDim.x) sq[j] = shift[j] * shift[j];
   __syncthreads();
+  const int changed = st->changed;  // uniform: read by every thread before any write below
+  float tot = 0.f;
+  if (changed != 0 && in_lds) tot = pw_sum_block(sq, k, pl);  // every thread takes part
+  __syncthreads();
   if (threadIdx.x != 0) return;
   int reason = 0;
-  if (st->changed == 0) {
+  if (changed == 0) {
     reason = 1;  // np.array_equal(labels, labels_old)
   } else {
-    float tot;
-    if (in_lds)
-      tot = pw_sum<kPwDepth>([&](int j) { return sq[j]; }, 0, k);
-    else
-      tot = pw_sum<kPwDepth>([&](int j) { const float v = shift[j]; return v * v; }, 0, k);
+    if (!in_lds) tot = pw_sum<kPwDepth>([&](int j) { const float v = shift[j]; return v * v; }, 0, k);
     if ((double)tot <= tol) reason = 2;
   }
   st->changed = 0;
@@ -887,7 +985,7 @@ extern "C" int gdd_segment_sum_f32(int64_t n, int dim, const float* X, const flo
                                    float* wsum, gdd_stream_t stream) {
   GDD_REQUIRE(n > 0 && dim > 0 && k > 0 && X && perm && offsets && sums && wsum,
               "segment_sum_f32: bad arguments");
-  FoldArgs a{dim, 0, 0, 0, 0, 0, 0, 0, X, w, perm, offsets, sums, wsum, nullptr, 0, nullptr, 0};
+  FoldArgs a{dim, 0, 0, 0, 0, 0, 0, 0, X, w, perm, offsets, sums, wsum, nullptr, 0, nullptr, 0, 0, n / k};
   return fold_launch(a, k, false, to_hip(stream));
 }
 
@@ -898,7 +996,7 @@ extern "C" int gdd_segment_sum_f32_part(int64_t n, int dim, const float* X, cons
   GDD_REQUIRE(n > 0 && dim > 0 && k > 0 && 0 <= c0 && c0 <= c1 && c1 <= k && X && perm && offsets &&
                   (c0 == c1 || (sums_part && wsum_part)),
               "segment_sum_f32_part: bad arguments");
-  FoldArgs a{dim, 0, 0, 0, 0, 0, 0, c0, X, w, perm, offsets, sums_part, wsum_part, nullptr, 0, nullptr, 0};
+  FoldArgs a{dim, 0, 0, 0, 0, 0, 0, c0, X, w, perm, offsets, sums_part, wsum_part, nullptr, 0, nullptr, 0, 0, n / k};
   return fold_launch(a, c1 - c0, false, to_hip(stream));
 }
 
@@ -1038,6 +1136,7 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
   GDD_HIP(hipMemsetAsync(st, 0, offsetof(LloydState, changed), s));
   if (!resume) GDD_HIP(hipMemsetAsync(&st->changed, 0, sizeof(int32_t), s));
   FoldArgs fa{dim, 0, 0, 0, 0, 0, 0, 0, X, nullptr, perm, offsets, nullptr, wsum, nullptr, 0, &st->stop_at, 0};
+  fa.avg_rows = n / k;
   {  // M-step: clusters above GDD_FOLD_SLICE x the mean size (default 1.5; 0: off) fold in slices
     const char* fe = getenv("GDD_FOLD_SLICE");
     const double f = fe ? atof(fe) : 1.5;
@@ -1232,7 +1331,7 @@ extern "C" int gdd_lloyd_mstep(int64_t n, int dim, const float* X, const int32_t
   if (rc) return rc;
   if (f1 > f0) {
     FoldArgs fa{f1 - f0, 0, 0, 0, 0, 0, 0, 0, X + f0, nullptr, lw.perm, lw.offsets, sums_cols, wsum,
-                nullptr, 0, &st->stop_at, sa, dim};
+                nullptr, 0, &st->stop_at, sa, dim, n / k};
     const char* fe = getenv("GDD_FOLD_SLICE");
     const double fs = fe ? atof(fe) : 1.5;
     const double rows = fs * (double)n / (double)k;
