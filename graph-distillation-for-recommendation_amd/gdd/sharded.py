@@ -355,13 +355,41 @@ def sharded_cluster_mean(feat, labels, k: int, empty_as_zero: bool = False, grou
 # ------------------------------------------------------------------------------------------------
 # Lloyd KMeans over the ranks
 # ------------------------------------------------------------------------------------------------
+ESTEP_TFLOPS = 50.0  # the unbounded E-step's MFMA rate at large n (measured 46-88 TF/s)
+
+
+def lloyd_rows_pay(n: int, dim: int, k: int, world: int) -> bool:
+    """Size model for ShardedKMeans: splitting the E-step's rows over R ranks saves (R-1)/R of it and
+    adds an all-gather of the n int32 labels per iteration (~25 us + 4n(R-1)/R bytes at ~300 GB/s).
+    With the bounded E-step (dim <= 48) an iteration's E-step is a bounds test of ~40 us at
+    2.45M rows, so ogbn-products replicates; an unbounded E-step (2 n k dim flops) of 1 ms and more
+    shards. The M-step is not split: its ordered per-cluster folds are bound by the longest member
+    chain, not by the rows' bytes (a column split measured 1.53 -> 1.49 / 1.57 / 1.59 ms at 1/2, 1/4,
+    1/8 of the columns, `profiles/r04_fold_cols.txt`). GDD_SHARD_LLOYD=1/0 forces the choice."""
+    import os
+    env = os.environ.get("GDD_SHARD_LLOYD")
+    if env is not None:
+        return env == "1" and world > 1
+    if world <= 1:
+        return False
+    bounded = dim <= 48  # the bounded E-step's shapes (gdd_lloyd.hip lloyd_prune_ok)
+    estep_ms = (n * 8 / 5e12 * 1e3 + 0.03) if bounded else 2.0 * n * k * dim / (ESTEP_TFLOPS * 1e12) * 1e3
+    frac = (world - 1) / world
+    gather_ms = 0.025 + 4.0 * n * frac / 300e9 * 1e3
+    return estep_ms * frac > gather_ms
+
+
 class ShardedKMeans:
     """sklearn KMeans(n_clusters, n_init, max_iter, tol, random_state).fit (Lloyd, _kmeans.py:
-    1427-1530 / :624-752) with the E-step partitioned by rows and the M-step by clusters. ``fit``
-    takes the whole input on every rank; every rank ends with the same fitted attributes."""
+    1427-1530 / :624-752) over a process group. ``fit`` takes the whole input on every rank; every
+    rank ends with the same fitted attributes, bit-identical to one GPU. Where :func:`lloyd_rows_pay`
+    says a row split pays, the device loop runs in phases — the E-step on this rank's rows, an
+    all-gather of the labels, the replicated M-step (or, with ``split_columns``, this rank's feature
+    columns and an all-gather of the column slices) and update; otherwise every rank runs the
+    single-GPU device loop (`gdd.KMeans`) on the replicated input, with no collective at all."""
 
     def __init__(self, n_clusters=8, *, n_init="auto", max_iter=300, tol=1e-4, random_state=None,
-                 group=None, ops=None, device="cuda"):
+                 group=None, ops=None, device="cuda", split_columns=False):
         self.n_clusters = n_clusters
         self.n_init = n_init
         self.max_iter = max_iter
@@ -370,28 +398,42 @@ class ShardedKMeans:
         self.group = group
         self.ops = ops
         self.device = device
+        self.split_columns = split_columns
 
     def fit(self, X, y=None, sample_weight=None):
         if sample_weight is not None and not np.all(np.asarray(sample_weight) == 1):
             raise NotImplementedError("non-unit sample_weight is not used by the reference")
-        ops = self.ops or DeviceOps(self.device)
         group = self.group
+        rank, world = world_of(group)
+        n_all, dim_all = X.shape
+        if self.ops is None and not lloyd_rows_pay(n_all, dim_all, self.n_clusters, world):
+            # replicated: the single-GPU device loop on every rank (same RandomState, same bits)
+            km = KMeans(n_clusters=self.n_clusters, n_init=self.n_init, max_iter=self.max_iter,
+                        tol=self.tol, random_state=self.random_state, device=self.device).fit(X)
+            for a in ("labels_", "labels_device_", "inertia_", "cluster_centers_",
+                      "cluster_centers_device_", "n_iter_"):
+                setattr(self, a, getattr(km, a))
+            self.mode_ = "replicated"
+            return self
+        self.mode_ = "rows"
+        ops = self.ops or DeviceOps(self.device)
         X = ops.tensor(X, dtype=torch.float32)
         n, dim = X.shape
         k = self.n_clusters
         if k > n:
             raise ValueError(f"n_samples={n} should be >= n_clusters={k}.")
-        rank, world = world_of(group)
         r0, r1, m = part(n, rank, world)
-        f0, f1, fw = part(dim, rank, world)  # this rank's feature columns of the M-step
+        split = self.split_columns and world > 1
+        # this rank's feature columns of the M-step (all of them unless split_columns)
+        f0, f1, fw = part(dim, rank, world) if split else (0, dim, dim)
         rs = check_random_state(self.random_state)
         # centring and _tolerance on the whole (replicated) input, numpy's orders (:1476-1487, :279-288)
         Xc, X_mean, var = ops.center(X)
         tol_ = 0 if self.tol == 0 else np.mean(var) * self.tol
         n_init = 1 if self.n_init == "auto" else int(self.n_init)
-        ctx = ops.lloyd_begin(n, dim, k, world, m, fw)
+        ctx = ops.lloyd_begin(n, dim, k, world, m, fw if split else 1)
         labels = ctx.labels[:n]
-        mine = ctx.parts[rank * k * fw:(rank + 1) * k * fw].view(k, fw)
+        mine = ctx.parts[rank * k * fw:(rank + 1) * k * fw].view(k, fw) if split else None
         best = None
         for _ in range(n_init):
             C0 = ops.kmeans_plusplus(Xc, k, rs)  # same RandomState on every rank: same centres
@@ -400,14 +442,16 @@ class ShardedKMeans:
             while True:  # _kmeans_single_lloyd (:690-735), enqueued in chunks of iterations
                 ops.lloyd_clear(ctx, resume)
                 stop_at, reason, it_r, done = self._run_chunks(ops, ctx, Xc, Cb, it0, resume, first_e,
-                                                              (r0, r1, m), (f0, f1, fw), mine, tol_, group)
+                                                              (r0, r1, m), (f0, f1, fw, split), mine,
+                                                              tol_, group)
                 if reason != 3:
                     break
                 # an empty cluster at iteration it_r (rare): the sums to C[(it+1) % 2], sklearn's
                 # relocation on the host (replicated, identical on every rank), then resume there
                 it = it_r
                 C_new = Cb[(it + 1) % 2]
-                C_new.copy_(assemble_cols(ctx.parts, k, dim, fw, world))
+                if split:  # otherwise the M-step wrote the sums there itself
+                    C_new.copy_(assemble_cols(ctx.parts, k, dim, fw, world))
                 ops.relocate(Xc, Cb[it % 2], C_new, ctx.wsum, labels)
                 it0, resume, first_e = it, True, it + 1
             n_iter = done
@@ -434,20 +478,26 @@ class ShardedKMeans:
 
     def _run_chunks(self, ops, ctx, Xc, Cb, it0, resume, first_e, rows, cols, mine, tol_, group):
         """Iterations it0.. until the state's stop word is set or max_iter: each iteration is the
-        E-step on this rank's rows, ONE all-gather of the labels, the M-step on this rank's columns,
-        ONE all-gather of the column slices, the replicated update; the host reads the state once per
-        chunk (2, 4, then 8 iterations), one chunk behind, as gdd_kmeans_lloyd_run does."""
+        E-step on this rank's rows, ONE all-gather of the labels, the M-step (all columns, into the
+        next centres' buffer; or this rank's columns and ONE all-gather of the column slices), the
+        replicated update; the host reads the state once per chunk (2, 4, then 8 iterations), one
+        chunk behind, as gdd_kmeans_lloyd_run does. The M-step and update kernels are gated by the
+        stop word, so iterations enqueued past a stop change nothing."""
         r0, r1, m = rows
-        f0, f1, fw = cols
+        f0, f1, fw, split = cols
         i, ch, pending = it0, 2, None
         while i < self.max_iter:
             for _ in range(min(ch, self.max_iter - i)):
                 if not (resume and i == it0):
                     ops.lloyd_estep(ctx, Xc, Cb[i % 2], r0, r1, i == first_e, i)
                     all_gather_slots(ctx.labels, m, group)
-                    ops.lloyd_mstep(ctx, Xc, f0, f1, mine, i)
-                    all_gather_slots(ctx.parts, ctx.k * fw, group)
-                    ops.lloyd_update(ctx, ctx.parts, fw, Cb[(i + 1) % 2], Cb[i % 2], tol_, i)
+                    if split:
+                        ops.lloyd_mstep(ctx, Xc, f0, f1, mine, i)
+                        all_gather_slots(ctx.parts, ctx.k * fw, group)
+                        ops.lloyd_update(ctx, ctx.parts, fw, Cb[(i + 1) % 2], Cb[i % 2], tol_, i)
+                    else:
+                        ops.lloyd_mstep(ctx, Xc, 0, ctx.dim, Cb[(i + 1) % 2], i)
+                        ops.lloyd_update(ctx, None, ctx.dim, Cb[(i + 1) % 2], Cb[i % 2], tol_, i)
                 else:  # resume after a relocation: C[(i+1) % 2] already holds the relocated sums
                     ops.lloyd_update(ctx, None, fw, Cb[(i + 1) % 2], Cb[i % 2], tol_, i)
                 i += 1

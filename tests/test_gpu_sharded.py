@@ -41,6 +41,7 @@ def test_one_rank_equals_kmeans_and_sklearn():
 def _worker(rank, world, port, X, Xm, feat, out):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE),
                                                           "graph-distillation-for-recommendation_amd"), HERE]
+    os.environ["GDD_SHARD_LLOYD"] = "1"  # the phase loop (the size model would replicate here)
     import torch.distributed as dist
     import gdd as G
     from gdd.sharded import ShardedKMeans as SK
@@ -48,7 +49,7 @@ def _worker(rank, world, port, X, Xm, feat, out):
     init_gloo(rank, world, port)
     g = dist.group.WORLD
     np.random.seed(15)
-    m = SK(n_clusters=40, device="cuda:0", group=g).fit(X)
+    m = SK(n_clusters=40, device="cuda:0", group=g, split_columns=True).fit(X)  # pipelines: False
     mb = G.MiniBatchKMeans(n_clusters=30, random_state=15, batch_size=500, device="cuda:0", group=g).fit(Xm)
     fs, cnt = G.cluster_mean(torch.from_numpy(feat).cuda(), mb.labels_device_, 30, group=g)
     np.savez(os.path.join(out, f"r{rank}.npz"), labels=m.labels_, centers=m.cluster_centers_,
@@ -117,6 +118,7 @@ def _pipeline_inputs():
 def _pipeline_worker(rank, world, port, out):
     sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE),
                                                           "graph-distillation-for-recommendation_amd"), HERE]
+    os.environ["GDD_SHARD_LLOYD"] = "1"  # the phase loop (the size model would replicate here)
     import torch.distributed as dist
     import gdd as G
     from sharded_util import init_gloo

@@ -35,10 +35,12 @@ def _worker(rank, world, port, job, out_dir):
     kind, args = job
     res = {}
     if kind == "kmeans":
-        X, k, n_init, seed = args
+        X, k, n_init, seed = args[:4]
+        split = args[4] if len(args) > 4 else False
         if seed is None:
             np.random.seed(15)
-        m = sharded.ShardedKMeans(n_clusters=k, n_init=n_init, random_state=seed, ops=ops).fit(X)
+        m = sharded.ShardedKMeans(n_clusters=k, n_init=n_init, random_state=seed, ops=ops,
+                                  split_columns=split).fit(X)
         res = dict(labels=m.labels_, centers=m.cluster_centers_, n_iter=m.n_iter_, inertia=m.inertia_)
     elif kind == "labels_mean":
         X, C, feat, k = args
@@ -99,11 +101,13 @@ def test_sharded_lloyd_equals_sklearn_fixture(tmp_path, n_init):
     assert float(two["inertia"]) == float(z[f"{tag}_inertia"])
 
 
-@pytest.mark.parametrize("n,dim,k,world", [(3001, 8, 12, 2), (3001, 8, 12, 3), (50, 4, 50, 2),
-                                           (50, 4, 50, 3), (300, 3, 12, 2), (300, 3, 12, 4)])
-def test_sharded_lloyd_equals_oracle_incl_relocation(tmp_path, n, dim, k, world):
+@pytest.mark.parametrize("n,dim,k,world,split", [(3001, 8, 12, 2, False), (3001, 8, 12, 3, True),
+                                                 (50, 4, 50, 2, False), (50, 4, 50, 3, True),
+                                                 (300, 3, 12, 2, True), (300, 3, 12, 4, True)])
+def test_sharded_lloyd_equals_oracle_incl_relocation(tmp_path, n, dim, k, world, split):
     # (50, 4, 50): duplicated rows and k = n, so clusters empty out and are relocated / copied;
-    # world 3 splits 8 columns 3 + 3 + 2, world 4 leaves a rank with no column of dim 3
+    # with split_columns, world 3 splits 8 columns 3 + 3 + 2 and world 4 leaves a rank with no
+    # column of dim 3
     _paths()
     from gdd import synth
     from oracle import oracle as O
@@ -111,7 +115,7 @@ def test_sharded_lloyd_equals_oracle_incl_relocation(tmp_path, n, dim, k, world)
     X[1::7] = X[0]
     ref = O.kmeans(X, k, random_state=7)
     one = _run(1, ("kmeans", (X, k, 1, 7)), tmp_path / "w1")
-    two = _run(world, ("kmeans", (X, k, 1, 7)), tmp_path / f"w{world}")
+    two = _run(world, ("kmeans", (X, k, 1, 7, split)), tmp_path / f"w{world}")
     _same(one, two)
     assert int(two["n_iter"]) == ref["n_iter_"]
     assert np.array_equal(two["labels"], ref["labels_"])
