@@ -1968,7 +1968,7 @@ int resident_blocks(const void* fn, int threads, size_t lds, int* out) {
   };
   static std::mutex mu;
   static Entry cache[32];
-  static int used = 0;
+  static int used = 0, next = 0;  // filled slots; round-robin slot to replace once full
   int dev = 0;
   GDD_HIP(hipGetDevice(&dev));
   {
@@ -1984,8 +1984,12 @@ int resident_blocks(const void* fn, int threads, size_t lds, int* out) {
   GDD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   *out = std::max(occ, 1) * std::max(cus, 1);
   std::lock_guard<std::mutex> g(mu);
-  cache[used % 32] = Entry{dev, threads, fn, lds, *out};
-  used = std::min(used + 1, 32);
+  if (used < 32) {
+    cache[used++] = Entry{dev, threads, fn, lds, *out};
+  } else {
+    cache[next] = Entry{dev, threads, fn, lds, *out};
+    next = (next + 1) % 32;
+  }
   return GDD_OK;
 }
 

@@ -1061,7 +1061,7 @@ struct LloydWs {
   int64_t* count;
 };
 
-static bool carve_lloyd(void* ws, size_t ws_bytes, int64_t n, int k, LloydWs* w) {
+static bool carve_lloyd(void* ws, size_t ws_bytes, int64_t n, int dim, int k, LloydWs* w) {
   Carver cv(ws, ws_bytes);
   w->keys = cv.take<unsigned long long>(n);
   w->cn2 = cv.take<float>(k);
@@ -1069,22 +1069,24 @@ static bool carve_lloyd(void* ws, size_t ws_bytes, int64_t n, int k, LloydWs* w)
   w->offsets = cv.take<int32_t>(k + 1);
   w->gb = group_ws(n, k);
   w->gws = cv.take<char>(w->gb);
-  w->xn = cv.take<double>(n);
-  w->ub = cv.take<double>(n);
-  w->lb = cv.take<double>(n);
-  w->list = cv.take<int64_t>(n);
-  w->sec = cv.take<float>(n);
-  w->sep = cv.take<double>(k);
+  const int64_t pn = lloyd_prune_ok(dim, k) ? n : 0;  // the bounded E-step's per-row buffers
+  const int64_t pk = lloyd_prune_ok(dim, k) ? k : 0;
+  w->xn = cv.take<double>(pn);
+  w->ub = cv.take<double>(pn);
+  w->lb = cv.take<double>(pn);
+  w->list = cv.take<int64_t>(pn);
+  w->sec = cv.take<float>(pn);
+  w->sep = cv.take<double>(pk);
   w->glob = cv.take<double>(2);
   w->count = cv.take<int64_t>(1);
   return cv.ok();
 }
 
 extern "C" size_t gdd_kmeans_lloyd_ws_bytes(int64_t n, int dim, int k) {
-  (void)dim;
+  // the bounded E-step's buffers (~36 B per row) only where it can run
   return align256(sizeof(unsigned long long) * (size_t)n) + align256(sizeof(float) * (size_t)k) +
          align256(sizeof(int32_t) * (size_t)n) + align256(sizeof(int32_t) * (size_t)(k + 1)) +
-         group_ws(n, k) + prune_ws(n, k) + 1024;
+         group_ws(n, k) + (lloyd_prune_ok(dim, k) ? prune_ws(n, k) : 3 * 256) + 1024;
 }
 
 extern "C" size_t gdd_kmeans_lloyd_host_ws_bytes(void) { return 4 * sizeof(LloydState); }
@@ -1104,7 +1106,7 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
     return fail(GDD_E_WORKSPACE, "kmeans_lloyd_run: host workspace too small");
   hipStream_t s = to_hip(stream);
   LloydWs lw;
-  if (!carve_lloyd(ws, ws_bytes, n, k, &lw)) return fail(GDD_E_WORKSPACE, "kmeans_lloyd_run: workspace too small");
+  if (!carve_lloyd(ws, ws_bytes, n, dim, k, &lw)) return fail(GDD_E_WORKSPACE, "kmeans_lloyd_run: workspace too small");
   auto* keys = lw.keys;
   float* cn2 = lw.cn2;
   int32_t* perm = lw.perm;
@@ -1283,7 +1285,7 @@ extern "C" int gdd_lloyd_estep(int64_t n, int64_t r0, int64_t r1, int dim, const
               "lloyd_estep: bad arguments");
   hipStream_t s = to_hip(stream);
   LloydWs lw;
-  if (!carve_lloyd(ws, ws_bytes, n, k, &lw)) return fail(GDD_E_WORKSPACE, "lloyd_estep: workspace too small");
+  if (!carve_lloyd(ws, ws_bytes, n, dim, k, &lw)) return fail(GDD_E_WORKSPACE, "lloyd_estep: workspace too small");
   LloydState* st = static_cast<LloydState*>(state);
   const int sa = 2 * it;
   const int64_t m = r1 - r0;
@@ -1324,7 +1326,7 @@ extern "C" int gdd_lloyd_mstep(int64_t n, int dim, const float* X, const int32_t
               "lloyd_mstep: bad arguments");
   hipStream_t s = to_hip(stream);
   LloydWs lw;
-  if (!carve_lloyd(ws, ws_bytes, n, k, &lw)) return fail(GDD_E_WORKSPACE, "lloyd_mstep: workspace too small");
+  if (!carve_lloyd(ws, ws_bytes, n, dim, k, &lw)) return fail(GDD_E_WORKSPACE, "lloyd_mstep: workspace too small");
   LloydState* st = static_cast<LloydState*>(state);
   const int sa = 2 * it;
   int rc = group_dev(n, labels, k, lw.perm, lw.offsets, lw.gws, lw.gb, &st->stop_at, sa, s);

@@ -405,23 +405,33 @@ class RecallEvaluator:
         return float(int(hits.item()) / max(1, self.total))
 
     def _sorted_hits(self, scores: torch.Tensor, chunk: int = 1024) -> float:
-        """k above gdd_recall_at_k's one-pick-per-thread limit: the same mask, then a stable
-        descending sort per user (equal scores keep ascending item order, the kernel's rule) and the
-        hits among the first k, in chunks of users."""
+        """k above gdd_recall_at_k's one-pick-per-thread limit: the same mask, then per user the k-th
+        largest score t (one top-k); a test item is a hit when its score is above t, or equal to t and
+        among the first k - #{score > t} items scoring t in ascending item order (the kernel's tie
+        rule). Test items are read through their CSR, chunks of users at a time."""
         B, I = scores.shape
-        tr_row = torch.repeat_interleave(torch.arange(B, device=self.device),
+        dev = self.device
+        tr_row = torch.repeat_interleave(torch.arange(B, device=dev),
                                          (self.tr_ptr[1:] - self.tr_ptr[:-1]).long())
         scores[tr_row, self.tr_col.long()] = -1e9
-        te_row = torch.repeat_interleave(torch.arange(B, device=self.device),
+        te_row = torch.repeat_interleave(torch.arange(B, device=dev),
                                          (self.te_ptr[1:] - self.te_ptr[:-1]).long())
-        hits = torch.zeros((), dtype=torch.int64, device=self.device)
+        te_col = self.te_col.long()
+        hits = torch.zeros((), dtype=torch.int64, device=dev)
         for b0 in range(0, B, chunk):
             b1 = min(B, b0 + chunk)
-            top = torch.sort(scores[b0:b1], dim=1, descending=True, stable=True).indices[:, :self.k]
-            truth = torch.zeros((b1 - b0, I), dtype=torch.bool, device=self.device)
+            sc = scores[b0:b1]
+            t = torch.topk(sc, self.k, dim=1, largest=True, sorted=False).values.min(dim=1).values
+            need = self.k - (sc > t[:, None]).sum(dim=1)  # tie slots left at the threshold
             sel = (te_row >= b0) & (te_row < b1)
-            truth[te_row[sel] - b0, self.te_col[sel].long()] = True
-            hits += truth.gather(1, top).sum()
+            r, c = te_row[sel] - b0, te_col[sel]
+            s, tr = sc[r, c], t[r]
+            hit = s > tr
+            tie = s == tr
+            if bool(tie.any()):
+                eq_rank = torch.cumsum((sc == t[:, None]).to(torch.int32), dim=1)  # 1-based among ties
+                hit |= tie & (eq_rank[r, c] <= need[r])
+            hits += hit.sum()
         return float(int(hits.item()) / max(1, self.total))
 
 

@@ -141,6 +141,22 @@ def test_recall_at_k_device_vs_oracle_shapes(k, max_users):
     assert r == R.recall(ue, ie, tr.indptr, tr.indices, tu, ti, k, max_users=max_users)
 
 
+@pytest.mark.parametrize("k", [5, 100, 256, 257, 300, 650])
+def test_recall_at_k_tied_scores(k):
+    """Small-integer embeddings: many users' k-th score is shared by dozens of items, so the tie rule
+    (equal scores in ascending item order) decides hits — in the kernel (k <= 256) and in the top-k
+    threshold path above it."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(1000 + k)
+    nu, ni = 300, 700
+    ue = rng.integers(-1, 2, (nu, 2)).astype(np.float32)
+    ie = rng.integers(-1, 2, (ni, 2)).astype(np.float32)
+    tr = sp.random(nu, ni, density=0.03, format="csr", random_state=k, dtype=np.float32)
+    tu, ti = rng.integers(0, nu, 6000), rng.integers(0, ni, 6000)
+    r = recsys.recall_at_k(torch.from_numpy(ue).cuda(), torch.from_numpy(ie).cuda(), tr, tu, ti, k, "cuda")
+    assert r == R.recall(ue, ie, tr.indptr, tr.indices, tu, ti, k)
+
+
 # scores within this relative distance of a user's k-th score count as tied when bounding the
 # reference's Recall from this run's embeddings: they follow the reference's within fp32 drift (losses
 # agree to 2e-5 after 6 Adam steps), so two distinct scores that close may swap between the runs
