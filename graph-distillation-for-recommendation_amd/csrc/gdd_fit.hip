@@ -108,9 +108,18 @@ int local_trials(int k) { return 2 + (int)std::log((double)k); }
 // The step loop with every draw and decision on the device (see the dev_loop comment in the fit).
 // Per step s: the assignment launch (plus a workgroup finishing step s-1 — its batch inertia and
 // convergence test — and, unless s reassigns, a workgroup drawing batch s+1), the update launch,
-// and at scheduled reassignment steps the reassignment launch (which then draws batch s+1). Chunks of kDevChunk steps are
-// enqueued back to back; the host reads the stop word of chunk c while chunk c+1 runs.
-constexpr int kDevChunk = 16;
+// and at scheduled reassignment steps the reassignment launch (which then draws batch s+1). Chunks of
+// dev_chunk() steps are enqueued back to back; the host reads the stop word of chunk c while chunk
+// c+1 runs. Smaller chunks leave fewer no-op launches after the stop (about half a chunk plus the
+// lookahead's chunks) but give the host a shorter runway (GDD_MB_CHUNK, 2..64, default 16).
+int dev_chunk() {
+  static const int v = [] {
+    const char* e = getenv("GDD_MB_CHUNK");
+    const int c = e ? atoi(e) : 16;
+    return c < 2 ? 2 : (c > 64 ? 64 : c);
+  }();
+  return v;
+}
 
 int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n_steps,
                 int max_no_improvement, float reassignment_ratio, MTState* rng, const FitWs& w,
@@ -201,7 +210,7 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n
   int64_t chunk = 0;
   *stop_step = -1;
   while (i < n_steps) {
-    const int64_t m = std::min<int64_t>(kDevChunk, n_steps - i);
+    const int64_t m = std::min<int64_t>(dev_chunk(), n_steps - i);
     key.i0 = i;
     key.m = m;
     rc = replay_or_run("minibatch_chunk", &key, sizeof(key), s,
@@ -284,7 +293,7 @@ int device_loop_fused(int64_t n, int dim, const float* X, int k, int64_t bs, int
   bool prev_split = true;  // step 0 starts with an assignment alone
   *stop_step = -1;
   while (i < n_steps) {
-    const int64_t m = std::min<int64_t>(kDevChunk, n_steps - i);
+    const int64_t m = std::min<int64_t>(dev_chunk(), n_steps - i);
     for (int64_t j = 0; j < m; ++j) {
       const int64_t st = i + j;
       n_since += bs;

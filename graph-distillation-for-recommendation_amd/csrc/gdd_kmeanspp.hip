@@ -2151,6 +2151,189 @@ __global__ __launch_bounds__(64) void k_kpp1_final(Kpp1Args a, int c) {
   for (int j = threadIdx.x; j < a.dim; j += 64) a.centers[(int64_t)c * a.dim + j] = a.X[src * a.dim + j];
 }
 
+// ---- table rounds for 4096 < n <= 32768 (r04): ONE 1024-thread workgroup per trial, as k_kpp1_dm
+// (no per-block partial terms, no fold launch reading T x blocks values). The ML-1M users (6,040 x 64,
+// k = 604) and Ali-Display users (17,730 x 64, k = 1,773) shapes of the recsys clustering. Per round c:
+//   trip 1   round c-1's T potentials (np.argmin) and this trial's candidate if that trial won;
+//   trip 2   the winner's row (the closest distances) and the candidate's table row, coalesced
+//            (entry tid + 1024 q), np.minimum, stored for round c+1's winner read and into LDS;
+//   fold     thread j takes entries [EPT j, EPT j + EPT) from LDS: its fp64 run, a wave scan and the
+//            wave totals give every entry's cumulative potential; waves b < nsg run the sgemv_t lane
+//            chains of 4096-entry block b (sgemv_block_wave, the multi-block rounds' own block term),
+//            added in block order, then the n % 4 tail — the same potential bits as k_kpp_round;
+//   draws    searchsorted_left(cum, u * pot) for round c+1's T uniforms as a count of entries below
+//            the threshold (only the thread whose segment straddles it walks its entries); a prefix
+//            within cum_tol of the threshold replays numpy's left-to-right sum (np_cumsum_search).
+// Round 0 (c == 0, one workgroup) draws round 1's candidates from the first centre's closest0 and
+// its sdot potential. LDS: the row, 4 * 1024 * EPT bytes (dynamic).
+constexpr int kBigThr = 1024;
+constexpr int kBigWaves = kBigThr / 64;
+constexpr int64_t kBig1Max = 32768;
+
+template <int EPT>
+__global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* __restrict__ D, int c) {
+  extern __shared__ __attribute__((aligned(16))) float s_row[];  // kBigThr * EPT floats
+  __shared__ double s_wt[kBigWaves];
+  __shared__ float s_vb[8];
+  __shared__ float s_pot;
+  __shared__ int s_cnt[kBigWaves][kMaxTrials];
+  __shared__ int s_amb[kBigWaves][kMaxTrials];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = a.T;
+  const int n = (int)a.n, m1 = (int)a.m1;
+  const int t = blockIdx.x;
+  const int cq = c & 1, pq = (c - 1) & 1;
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 90);
+  // ---- trip 1 (rounds >= 2): round c-1's winner and this slot's candidate
+  const float* wrow = a.closest0;
+  int64_t ct = 0;
+  if (c >= 1) {
+    int bw = 0;
+    if (c >= 2) {
+      float best = a.potv[pq][0];
+      for (int q = 1; q < T; ++q) {  // np.argmin: first minimum, a NaN wins at once
+        const float pt = a.potv[pq][q];
+        if (best == best && (pt < best || pt != pt)) {
+          bw = q;
+          best = pt;
+        }
+      }
+      wrow = a.dist[pq] + (int64_t)bw * n;
+    }
+    ct = a.candw[pq][(int64_t)bw * T + t];
+    if (tid == 0) {
+      a.candself[cq][t] = ct;
+      if (c >= 2 && t == 0) a.indices[c - 1] = a.candself[pq][bw];
+    }
+  }
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 91);
+  // ---- trip 2: the closest distances and the candidate's table row
+  {
+    float wi[EPT], dd[EPT];
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = min(tid + kBigThr * q, n - 1);
+      wi[q] = wrow[e];
+      dd[q] = c >= 1 ? D[ct * n + e] : 0.f;
+    }
+    float* orow = a.dist[cq] + (int64_t)t * n;
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + kBigThr * q;
+      const float f = c >= 1 ? np_minimum(wi[q], dd[q]) : wi[q];
+      if (e < n) {
+        if (c >= 1) orow[e] = f;
+        s_row[e] = f;
+      } else {
+        s_row[e] = 0.f;
+      }
+    }
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 92);
+  // ---- this thread's segment: products (fp32) and its fp64 run
+  const int e0 = EPT * tid;
+  float v[EPT];
+#pragma unroll
+  for (int q = 0; q < EPT; q += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(s_row + e0 + q);
+    v[q] = x.x;
+    v[q + 1] = x.y;
+    v[q + 2] = x.z;
+    v[q + 3] = x.w;
+  }
+  if (a.w) {
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) v[q] = e0 + q < n ? a.w[e0 + q] * v[q] : 0.f;
+  }
+  double tot = 0.0;
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) tot = tot + (double)v[q];
+  double inc = tot;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double y = __shfl_up(inc, o);
+    if (lane >= o) inc = inc + y;
+  }
+  double ex = __shfl_up(inc, 1);
+  if (lane == 0) ex = 0.0;
+  if (lane == 63) s_wt[wave] = inc;
+  // the sgemv_t block terms (rounds >= 1)
+  const int nsg = (m1 + kBlk - 1) / kBlk;
+  if (c >= 1 && wave < nsg) {
+    const int j0 = wave * kBlk;
+    const float vb = sgemv_block_wave(s_row + j0, a.w ? a.w + j0 : nullptr, min(kBlk, m1 - j0), t, T);
+    if (lane == 0) s_vb[wave] = vb;
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 93);
+  if (tid == 0) {
+    float y;
+    if (c == 0) {
+      y = a.st->pot;
+    } else {
+      y = 0.f;
+      for (int b = 0; b < nsg; ++b) y = y + s_vb[b];
+      if (m1 < n) {
+        float sx = s_row[m1] * wv(a.w, m1);
+        for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_row[o], wv(a.w, o), sx);
+        y = y + sx;
+      }
+      a.potv[cq][t] = y;
+    }
+    s_pot = y;
+  }
+  double off = ex;
+  for (int q = 0; q < wave; ++q) off = off + s_wt[q];
+  __syncthreads();
+  if (c + 1 >= a.k) return;
+  // ---- draws for round c+1 if this trial wins
+  const double pot = (double)s_pot;
+  const double first = off + (double)v[0];  // the segment's first cumulative value (as the walk's)
+  const double last = off + tot;  // its last, to within EPT roundings (far inside cum_tol)
+#pragma unroll 1
+  for (int t2 = 0; t2 < T; ++t2) {
+    const double rr = a.uniforms[(int64_t)c * T + t2] * pot;
+    const double tol = cum_tol(a.exact, n, rr);
+    const bool strict = !(tol < 0.0);  // tol < 0 (GDD_KPP_EXACT=0, tests): every segment walks
+    int cnt = 0;
+    bool amb = false;
+    const bool live = e0 < n;
+    if (live && strict && last < rr - 2.0 * tol) {
+      cnt = min(EPT, n - e0);  // the whole segment is below, none within tol (the run only climbs)
+    } else if (live && !(strict && first > rr + tol)) {
+      double run = off;
+#pragma unroll
+      for (int q = 0; q < EPT; ++q) {
+        run = run + (double)v[q];
+        if (e0 + q < n) {
+          cnt += run < rr;
+          amb = amb || fabs(run - rr) <= tol;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    const bool wamb = __ballot(amb) != 0ull;
+    if (lane == 0) {
+      s_cnt[wave][t2] = cnt;
+      s_amb[wave][t2] = wamb;
+    }
+  }
+  __syncthreads();
+  if (tid < T) {
+    int64_t cnt = 0;
+    bool amb = false;
+    for (int q = 0; q < kBigWaves; ++q) {
+      cnt += s_cnt[q][tid];
+      amb = amb || s_amb[q][tid];
+    }
+    if (amb) cnt = np_cumsum_search(s_row, a.w, n, a.uniforms[(int64_t)c * T + tid] * pot);
+    a.candw[cq][(int64_t)t * T + tid] = min<int64_t>(n - 1, cnt);
+  }
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 94);
+}
+
 // centres from their indices (fused rounds record only the index of each round's winner)
 __global__ void k_kpp_gather_centres(int k, int dim, const float* __restrict__ X,
                                      const int64_t* __restrict__ indices, float* __restrict__ centers) {
@@ -2551,6 +2734,53 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       k_kpp_dmat<64><<<gdm, 256, 0, s>>>((int)n, dim, X, a.XT, xsq, Dbig);
     GDD_LAUNCHED();
     a.D = Dbig;
+    if (n <= kBig1Max && T >= 2 && getenv("GDD_KPP_NO_BIG1") == nullptr) {
+      // one 1024-thread workgroup per trial (k_kpp1_big); GDD_KPP_NO_BIG1 keeps the per-block rounds
+      b1.n = n;
+      b1.m1 = a.m1;
+      b1.dim = dim;
+      b1.T = T;
+      b1.k = k;
+      b1.X = X;
+      b1.w = w;
+      b1.xsq = xsq;
+      b1.closest0 = closest0;
+      b1.st = st;
+      b1.uniforms = uniforms;
+      for (int q = 0; q < 2; ++q) b1.dist[q] = a.dist[q];
+      b1.centers = centers;
+      b1.indices = indices;
+      b1.plan = a.plan;
+      b1.exact = a.exact;
+      void (*big)(Kpp1Args, const float*, int) = nullptr;
+      int ept = 0;
+      if (n <= (int64_t)kBigThr * 8) {
+        big = k_kpp1_big<8>;
+        ept = 8;
+      } else if (n <= (int64_t)kBigThr * 16) {
+        big = k_kpp1_big<16>;
+        ept = 16;
+      } else {
+        big = k_kpp1_big<32>;
+        ept = 32;
+      }
+      const size_t lds_big = sizeof(float) * (size_t)kBigThr * ept;
+      GDD_HIP(hipFuncSetAttribute((const void*)big, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_big));
+      big<<<1, kBigThr, lds_big, s>>>(b1, Dbig, 0);  // round 1's candidates from the first centre
+      GDD_LAUNCHED();
+      for (int c = 1; c < k; ++c) {
+        big<<<(unsigned)T, kBigThr, lds_big, s>>>(b1, Dbig, c);
+        GDD_LAUNCHED();
+      }
+      k_kpp1_final<<<1, 64, 0, s>>>(b1, k - 1);
+      GDD_LAUNCHED();
+      if (k > 2) {
+        k_kpp_gather_centres<<<(unsigned)(((int64_t)k * dim + 255) / 256), 256, 0, s>>>(k, dim, X, indices,
+                                                                                         centers);
+        GDD_LAUNCHED();
+      }
+      return GDD_OK;
+    }
   }
   for (int c = 1; c < k; ++c) {
     if (seq)

@@ -177,7 +177,8 @@ def _kpp_dev(X, k, T, first, u, w=None):
 CUMSUM_FORMS = [
     (1000, ()), (4096, ()), (1000, ("GDD_KPP_SINGLE_ROUND",)), (1000, ("GDD_KPP_NO_TABLE",)),
     (1000, ("GDD_KPP_NO_TABLE", "GDD_KPP_TWO_LAUNCH")), (1000, ("GDD_KPP_BSEARCH",)),
-    (4096, ("GDD_KPP_SINGLE_ROUND", "GDD_KPP_BSEARCH")), (9000, ()), (530000, ()),
+    (4096, ("GDD_KPP_SINGLE_ROUND", "GDD_KPP_BSEARCH")), (9000, ()), (9000, ("GDD_KPP_NO_BIG1",)),
+    (20000, ()), (530000, ()),
 ]
 
 
@@ -205,7 +206,7 @@ def test_kpp_cumsum_adversarial(monkeypatch, n, env, rnd):
     assert idx[rnd] != idx_ref[rnd], "the blocked prefix did not cross the threshold"
 
 
-@pytest.mark.parametrize("n", [1000, 9000])
+@pytest.mark.parametrize("n", [1000, 9000, 20000])
 def test_kpp_cumsum_adversarial_weighted(monkeypatch, n):
     """The same with sample weights (w * closest in fp32, then the fp64 sum)."""
     k, T = 16, 4
@@ -233,3 +234,44 @@ def test_kpp_replay_every_draw(monkeypatch, n, dim, k):
                                                      np.random.RandomState(15))
     assert np.array_equal(idx.cpu().numpy(), idx_ref)
     assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref))
+
+
+# ---- table rounds with one 1024-thread workgroup per trial (k_kpp1_big, 4096 < n <= 32768) ----------
+@pytest.mark.parametrize("n,dim,k,oracle", [
+    (4097, 64, 40, True), (6040, 64, 604, True),  # ML-1M users' shape, its k
+    (8192, 40, 100, True), (8193, 33, 50, True),  # the 8- / 16-entry segment boundary
+    (12003, 64, 120, True), (16384, 7, 30, True), (16385, 64, 25, False),
+    (17730, 64, 1773, False),  # Ali-Display users' shape and k: T = 9
+    (32768, 16, 40, False)])
+def test_kmeans_plusplus_big_rounds(monkeypatch, n, dim, k, oracle):
+    """k_kpp1_big (the default for table plans with 4096 < n <= 32768) gives the seeding of the
+    per-(block, trial) table rounds (GDD_KPP_NO_BIG1) and, where the oracle is run, the oracle's —
+    bit for bit, over the 8-, 16- and 32-entry segment forms, odd n (the sgemv_t tail) and T = 9."""
+    X = synth.blobs(n, dim, max(2, k // 4), seed=n + dim + 3)
+    X = np.ascontiguousarray(X - X.mean(axis=0), np.float32)
+    ops = _Ops("cuda", n, k, dim)
+    Xd = torch.from_numpy(X).cuda()
+    c, idx = ops.kmeans_plusplus(Xd, k, np.random.RandomState(42))
+    monkeypatch.setenv("GDD_KPP_NO_BIG1", "1")
+    c2, idx2 = ops.kmeans_plusplus(Xd, k, np.random.RandomState(42))
+    assert np.array_equal(idx.cpu().numpy(), idx2.cpu().numpy())
+    assert np.array_equal(bits(c.cpu().numpy()), bits(c2.cpu().numpy()))
+    if oracle:
+        c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(42))
+        assert np.array_equal(idx.cpu().numpy(), idx_ref)
+        assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref))
+
+
+def test_kmeans_plusplus_big_rounds_weighted_and_replayed(monkeypatch):
+    """Sample weights (w * row in fp32 for the cumulative, the weighted sgemv_t lane chains) and
+    every draw replayed (GDD_KPP_EXACT=2) on the one-workgroup-per-trial rounds."""
+    n, dim, k, T = 9001, 24, 40, 5
+    X = np.ascontiguousarray(synth.blobs(n, dim, 10, seed=77), np.float32)
+    w = np.random.default_rng(3).uniform(0.5, 2.0, n).astype(np.float32)
+    u = np.random.RandomState(9).uniform(size=(k - 1) * T)
+    c_ref, idx_ref = O.kmeans_plusplus_draws(X, k, T, 17, u, w=w)
+    for mode in ("1", "2"):
+        monkeypatch.setenv("GDD_KPP_EXACT", mode)
+        c, idx = _kpp_dev(X, k, T, 17, u, w=w)
+        assert np.array_equal(idx, idx_ref), mode
+        assert np.array_equal(bits(c), bits(c_ref)), mode

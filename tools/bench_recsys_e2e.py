@@ -22,6 +22,28 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from gdd import distill_recsys as D  # noqa: E402
+from gdd import kmeans as K  # noqa: E402
+
+
+def warm_kmeans(args, user_emb, item_emb, num_cu, num_ci, reps=3):
+    """The clustering stage again in the same process (libraries loaded, workspaces cached): per call
+    wall time and gdd.kmeans phases — against the driver's first-call kmeans_s."""
+    out = {}
+    for name, emb, k in (("users", user_emb, num_cu), ("items", item_emb, num_ci)):
+        best = None
+        for _ in range(reps):
+            K.PHASE_TIMING = {}
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            D.kmeans_cluster(emb, n_clusters=k, seed=args.seed, minibatch=args.kmeans_minibatch,
+                             batch_size=args.kmeans_batch_size, device="cuda")
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3
+            if best is None or ms < best["ms"]:
+                best = {"ms": ms, "phases_ms": dict(K.PHASE_TIMING)}
+        K.PHASE_TIMING = None
+        out[name] = best
+    return out
 
 
 def write_dataset(root, nu=6040, ni=3706, E=1000209, seed=4):
@@ -53,6 +75,11 @@ def main(epochs=500):
         D.run(args, out_root=os.path.join(tmp, "out"), timings=tm)
         torch.cuda.synchronize()
         tm["total_s"] = time.perf_counter() - t0
+        ds = D.load_rankformer_dataset(tmp, "ml1m")
+        R_train = D.build_interaction_matrix(ds.num_users, ds.num_items, ds.train_u, ds.train_i)
+        ue, ie = D.compute_svd_embeddings(R_train, dim=args.svd_dim, seed=args.seed)
+        tm["kmeans_warm"] = warm_kmeans(args, ue, ie, int(np.ceil(ds.num_users * args.reduction_rate)),
+                                        int(np.ceil(ds.num_items * args.reduction_rate)))
     tm["refine_ms_per_epoch"] = tm["refine_s"] / max(1, epochs) * 1e3
     print(json.dumps({"workload": f"distill_recsys main, ML-1M shape: 6040 users x 3706 items, {n} unique "
                                   f"interactions, reduction 0.1, svd 64, KMeans, {epochs} BPR epochs b=4096",
@@ -80,6 +107,7 @@ def alidisplay(epochs=500):
                   embeddings=(z["user_emb"], z["item_emb"]))
         torch.cuda.synchronize()
         tm["total_s"] = time.perf_counter() - t0
+        tm["kmeans_warm"] = warm_kmeans(args, z["user_emb"], z["item_emb"], 1773, 1004)
     out = buf.getvalue().splitlines()
     print("\n".join(out))
 

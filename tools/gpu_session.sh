@@ -20,7 +20,9 @@
 #   gap                   tools/probe/gap_probe (dependent launches: stream vs hipGraph replay)
 #   graph-ab              tools/micro_graph.py (MiniBatchKMeans / k-means++ fits, eager vs graph replay)
 #   inertia-ab            bench.py (no CPU baseline) with the parallel inertia vs the one-lane fold, twice each
+#   chunk-ab              bench.py (no CPU baseline) with GDD_MB_CHUNK = 16, 8, 4 x GDD_MB_LOOKAHEAD = 1, 2, twice
 #   fold-cols             tools/micro_fold_cols.py (products M-step over all columns vs one rank's slice)
+#   capture-probe         tools/probe_capture_h2d.py (what a graph-captured pageable H2D copy reads at replay)
 #   assign                tools/bench_assign.py (full assignment pass, fp32 vs bf16, three shapes)
 #   assign-ab             tools/bench_assign.py with the wave-tile fp32 pass vs GDD_ASSIGN_PERSIST=1
 #   hop-lanes             tools/micro_prop.py at arxiv / products with the XCD slice A/B switch
@@ -68,6 +70,7 @@ for step in "$@"; do
       run 240 pmcb_write env GDD_PROP_PAIR=0 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcb/pmc_write" -o bench -- $B
       run 240 pmcb_hit env GDD_PROP_PAIR=0 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmcb/pmc_hit" -o bench -- $B ;;
     lookahead-ab) run 900 lookahead_ab bash -c 'for la in 1 2 3 1 2 3; do echo "lookahead $la"; GDD_MB_LOOKAHEAD=$la python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
+    chunk-ab) run 900 chunk_ab bash -c 'for c in 16 8 4 16 8 4; do for la in 1 2; do echo "chunk $c lookahead $la"; GDD_MB_CHUNK=$c GDD_MB_LOOKAHEAD=$la python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done; done' ;;
     pmc-products)
       for form in default lanes8; do
         E="GDD_PROP_PAIR=0"; [ "$form" = lanes8 ] && E="GDD_PROP_PAIR=0 GDD_HOP_LANES=8"
@@ -81,6 +84,7 @@ for step in "$@"; do
     gap) run 60 gap ./tools/probe/gap_probe ;;
     graph-ab) run 300 graph_ab python tools/micro_graph.py ;;
     fold-cols) run 300 fold_cols python tools/micro_fold_cols.py ;;
+    capture-probe) run 120 capture_probe python tools/probe_capture_h2d.py ;;
     inertia-ab) run 600 inertia_ab bash -c 'for v in 0 1 0 1; do echo "GDD_INERTIA_SEQ=$v"; GDD_INERTIA_SEQ=$v python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
     kpp-products) run 300 kpp_products python tools/micro_kpp_products.py ;;
     assign) run 300 assign python tools/bench_assign.py ;;
