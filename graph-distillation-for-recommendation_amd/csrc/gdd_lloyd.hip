@@ -134,6 +134,93 @@ __global__ __launch_bounds__(256) void k_grp_scatter(int64_t n, const int32_t* _
   }
 }
 
+// The same counting sort in ONE workgroup for small inputs (r04; n <= 32,768, k <= 2,048: the recsys
+// KMeans shapes), instead of three dependent launches (histograms, scan, scatter: ~16 us of latency
+// per Lloyd iteration there). Wave w owns tile w (M * 1024 labels, index order); its k counters sit in
+// LDS. Then thread t owns clusters 2t and 2t+1: each column's exclusive prefix over the waves, the
+// block's exclusive scan of the cluster totals, and the tile offsets; then the scatter of
+// k_grp_scatter. Tiles, chunks and lanes are taken in index order: the same stable permutation.
+constexpr int kGrpThr = 1024;
+constexpr int kGrpWaves = kGrpThr / 64;
+constexpr int64_t kGrpSmallMaxN = (int64_t)kGrpWaves * 2 * kTileUnit;  // M <= 2
+constexpr int kGrpSmallMaxK = 2 * kGrpThr;
+
+template <int M>
+__global__ __launch_bounds__(kGrpThr) void k_grp_small(int64_t n, const int32_t* __restrict__ labels, int k,
+                                                       int bits, int32_t* __restrict__ perm,
+                                                       int32_t* __restrict__ offsets, const int32_t* stop,
+                                                       int step_i) {
+  if (stopped(stop, step_i)) return;
+  extern __shared__ int32_t sh_grp[];  // [kGrpWaves][k]: counts, then each tile's running offsets
+  __shared__ int32_t s_wt[kGrpWaves];
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  int32_t* h = sh_grp + (size_t)wv * k;
+  for (int c = lane; c < k; c += 64) h[c] = 0;
+  int32_t lv[M * 16];
+  const int64_t base = (int64_t)wv * (M * kTileUnit);
+  load_tile<M>(n, labels, base, lane, lv);
+#pragma unroll
+  for (int q = 0; q < M * 16; ++q)
+    if ((unsigned)lv[q] < (unsigned)k) atomicAdd(&h[lv[q]], 1);
+  __syncthreads();
+  // columns 2t, 2t+1: exclusive prefix over the waves (in place) and the totals
+  int tot[2] = {0, 0};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = 2 * tid + u;
+    if (c < k) {
+      int run = 0;
+      for (int w = 0; w < kGrpWaves; ++w) {
+        const int v = sh_grp[(size_t)w * k + c];
+        sh_grp[(size_t)w * k + c] = run;
+        run += v;
+      }
+      tot[u] = run;
+    }
+  }
+  // exclusive scan of the cluster totals in cluster order
+  const int mine = tot[0] + tot[1];
+  int inc = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) s_wt[wv] = inc;
+  __syncthreads();
+  int ex = inc - mine;
+  for (int w = 0; w < wv; ++w) ex += s_wt[w];
+  const int b0 = ex, b1 = ex + tot[0];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = 2 * tid + u;
+    if (c < k) {
+      const int bc = u ? b1 : b0;
+      offsets[c] = bc;
+      for (int w = 0; w < kGrpWaves; ++w) sh_grp[(size_t)w * k + c] += bc;
+      if (c == k - 1) offsets[k] = bc + tot[u];  // members with a label in [0, k)
+    }
+  }
+  __syncthreads();
+  const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int q = 0; q < M * 16; ++q) {
+    const int l = lv[q];
+    const bool ok = (unsigned)l < (unsigned)k;
+    uint64_t peers = __ballot(ok);
+    for (int b = 0; b < bits; ++b) {
+      const bool bit = (l >> b) & 1;
+      const uint64_t m = __ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    if (ok) {
+      const int32_t pos = h[l] + __popcll(peers & below);
+      perm[pos] = (int32_t)(base + (int64_t)q * 64 + lane);
+    }
+    if (ok && (peers & below) == 0) h[l] += __popcll(peers);
+  }
+}
+
 // radix fallback (k > kCountMaxK): stable sort of (label, index), then first-position offsets
 __global__ void k_iota(int64_t n, int32_t* p) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -161,6 +248,17 @@ size_t group_ws(int64_t n, int k) {
 int group_dev(int64_t n, const int32_t* labels, int k, int32_t* perm, int32_t* offsets, void* ws,
               size_t ws_bytes, const int32_t* stop, int step_i, hipStream_t s) {
   Carver cv(ws, ws_bytes);
+  if (n <= kGrpSmallMaxN && k <= kGrpSmallMaxK && getenv("GDD_GROUP_SPLIT") == nullptr) {
+    int bits = 1;
+    while ((1ll << bits) < (long long)k) ++bits;
+    const size_t lds = sizeof(int32_t) * (size_t)kGrpWaves * k;
+    auto fn = n <= (int64_t)kGrpWaves * kTileUnit ? k_grp_small<1> : k_grp_small<2>;
+    if (lds > 65536)
+      GDD_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    fn<<<1, kGrpThr, lds, s>>>(n, labels, k, bits, perm, offsets, stop, step_i);
+    GDD_LAUNCHED();
+    return GDD_OK;
+  }
   if (k <= kCountMaxK) {
     const GroupPlan p = group_plan(n, k);
     const int64_t cells = (int64_t)k * p.ntiles;
@@ -778,6 +876,124 @@ __global__ __launch_bounds__(256) void k_lloyd_converge(int k, const float* __re
   }
 }
 
+// The update step of a small Lloyd problem in ONE workgroup (r04): the empty-cluster check of step
+// 2i (check != 0), then step 2i+1's _average_centers + shifts, labels-changed and convergence test —
+// the operations of k_lloyd_check_empty, k_avg_centers, k_lloyd_changed and k_lloyd_converge, in
+// their order, on one CU instead of four dependent launches (recsys shapes: ~4 us each, latency).
+// Empty clusters: with the check they stop the loop at step 2i+1 exactly as k_lloyd_check_empty
+// (nothing else runs); without it (the iteration resumed after the host's relocation) the heaviest
+// cluster donates its row as in k_avg_centers: raw to empties before it, averaged to those after.
+constexpr int kUpdThr = 1024;
+constexpr int64_t kUpdMaxN = 131072;      // labels compared by one workgroup
+constexpr int64_t kUpdMaxKD = 262144;     // centre entries averaged by one workgroup
+__global__ __launch_bounds__(kUpdThr) void k_lloyd_update_small(
+    int64_t n, int k, int dim, float* __restrict__ C_new, const float* __restrict__ wsum,
+    const float* __restrict__ C_old, float* __restrict__ shift, const int32_t* __restrict__ labels,
+    int32_t* __restrict__ old, double tol, LloydState* st, int it, int check, int step_i) {
+  if (stopped(&st->stop_at, step_i)) return;
+  __shared__ float sq[kShiftLds];
+  __shared__ PwLds pl;
+  __shared__ float s_bv[kUpdThr / 64];
+  __shared__ int s_bi[kUpdThr / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // heaviest cluster (first maximum) and whether any cluster is empty
+  float bv = -1.f;
+  int bi = INT_MAX, any_empty = 0;
+  for (int j = tid; j < k; j += kUpdThr) {
+    const float v = wsum[j];
+    if (v > bv) {
+      bv = v;
+      bi = j;
+    }
+    any_empty |= !(v > 0.f);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o);
+    const int oi = __shfl_xor(bi, o);
+    if (ov > bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  if (lane == 0) {
+    s_bv[wave] = bv;
+    s_bi[wave] = bi;
+  }
+  any_empty = __syncthreads_or(any_empty);
+  bv = s_bv[0];
+  bi = s_bi[0];
+  for (int q = 1; q < kUpdThr / 64; ++q)
+    if (s_bv[q] > bv || (s_bv[q] == bv && s_bi[q] < bi)) {
+      bv = s_bv[q];
+      bi = s_bi[q];
+    }
+  if (any_empty && check) {  // k_lloyd_check_empty: the host relocates, then resumes
+    if (tid == 0) {
+      st->reason = 3;
+      st->iter = it;
+      __hip_atomic_store(&st->stop_at, step_i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  // _average_centers: empties first take the donor's row (raw, or averaged if the donor comes first)
+  if (any_empty) {
+    const float ad = (float)(1.0 / (double)wsum[bi]);
+    const int64_t db = (int64_t)bi * dim;
+    for (int j = 0; j < k; ++j) {
+      if (wsum[j] > 0.f) continue;
+      const int64_t jb = (int64_t)j * dim;
+      for (int f = tid; f < dim; f += kUpdThr) {
+        const float raw = C_new[db + f];
+        C_new[jb + f] = bi < j ? raw * ad : raw;
+      }
+    }
+    __syncthreads();
+  }
+  for (int c = wave; c < k; c += kUpdThr / 64) {  // one wave per row
+    const float wc = wsum[c];
+    if (!(wc > 0.f)) continue;
+    const float alpha = (float)(1.0 / (double)wc);  // `1.0 / weight` is a C double division
+    const int64_t cb = (int64_t)c * dim;
+    for (int f = lane; f < dim; f += 64) C_new[cb + f] = C_new[cb + f] * alpha;
+  }
+  // labels changed (np.array_equal(labels, labels_old)), labels_old = labels
+  int diff = 0;
+  for (int64_t i = tid; i < n; i += kUpdThr) {
+    const int32_t a = labels[i];
+    if (a != old[i]) {
+      diff = 1;
+      old[i] = a;
+    }
+  }
+  const int changed = __syncthreads_or(diff) | st->changed;  // the barrier also publishes C_new
+  for (int c = tid; c < k; c += kUpdThr) {
+    const int64_t cb = (int64_t)c * dim;
+    const float sh = sqrtf(skl_sqdist(C_new + cb, C_old + cb, dim));
+    if (shift) shift[c] = sh;
+    sq[c] = sh * sh;
+  }
+  __syncthreads();
+  float tot = 0.f;
+  if (changed != 0) tot = pw_sum_block(sq, k, pl);  // every thread takes part
+  __syncthreads();
+  if (tid != 0) return;
+  int reason = 0;
+  if (changed == 0) reason = 1;
+  else if ((double)tot <= tol) reason = 2;
+  st->changed = 0;
+  st->done = it + 1;
+  if (reason) {
+    st->reason = reason;
+    st->iter = it;
+    __hip_atomic_store(&st->stop_at, step_i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__host__ __forceinline__ bool lloyd_update_small(int64_t n, int dim, int k) {
+  return getenv("GDD_LLOYD_UPDATE_SPLIT") == nullptr && n <= kUpdMaxN && k <= kShiftLds && (int64_t)k * dim <= kUpdMaxKD;
+}
+
 // ((X - C[labels])**2).sum(axis=1) in numpy's order: fp32 squares, pairwise per contiguous row
 __global__ void k_relocate_distances(int64_t n, int dim, const float* __restrict__ X,
                                      const int32_t* __restrict__ labels, const float* __restrict__ C,
@@ -1146,6 +1362,7 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
     fa.big_rows = f > 0.0 ? (int)std::min<double>(std::max(rows, 4096.0), (double)INT_MAX) : 0;
   }
   const unsigned cgrid = std::min<unsigned>(blocks_of(n), 2048);
+  const bool small_update = lloyd_update_small(n, dim, k);
   auto enqueue = [&](int i, bool phase_a) -> int {
     float* cin = (i & 1) ? C1 : C0;
     float* cout = (i & 1) ? C0 : C1;
@@ -1178,8 +1395,16 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
       fa.step_i = sa;
       rc = fold_launch(fa, k, false, s);
       if (rc) return rc;
-      k_lloyd_check_empty<<<1, 256, 0, s>>>(k, wsum, st, i, sa);
+      if (!small_update) {
+        k_lloyd_check_empty<<<1, 256, 0, s>>>(k, wsum, st, i, sa);
+        GDD_LAUNCHED();
+      }
+    }
+    if (small_update) {  // the check (when the E-step ran), average, changed, convergence: one launch
+      k_lloyd_update_small<<<1, kUpdThr, 0, s>>>(n, k, dim, cout, wsum, cin, shift, labels, labels_old, tol,
+                                                 st, i, phase_a ? 1 : 0, sb);
       GDD_LAUNCHED();
+      return GDD_OK;
     }
     k_avg_centers<<<k, 64, 0, s>>>(k, dim, cout, wsum, cin, shift, &st->stop_at, sb);
     GDD_LAUNCHED();
@@ -1364,6 +1589,12 @@ extern "C" int gdd_lloyd_update(int64_t n, int dim, int k, const float* parts, i
     k_assemble_cols<<<(unsigned)std::min<int64_t>((total + 255) / 256, 2048), 256, 0, s>>>(
         k, dim, fw, parts, C_new, &st->stop_at, sb);
     GDD_LAUNCHED();
+  }
+  if (lloyd_update_small(n, dim, k)) {  // one launch (the empty check ran in gdd_lloyd_mstep)
+    k_lloyd_update_small<<<1, kUpdThr, 0, s>>>(n, k, dim, C_new, wsum, C_old, shift, labels, labels_old, tol,
+                                               st, it, 0, sb);
+    GDD_LAUNCHED();
+    return GDD_OK;
   }
   k_avg_centers<<<k, 64, 0, s>>>(k, dim, C_new, wsum, C_old, shift, &st->stop_at, sb);
   GDD_LAUNCHED();

@@ -153,7 +153,11 @@ def test_average_centers_empty_cluster_copies_first_heaviest_in_loop_order():
     assert not np.array_equal(got[1], got[4])  # raw vs averaged copy
 
 
-@pytest.mark.parametrize("n,k", [(1, 1), (1000, 3), (70000, 454), (2500000, 196), (5000, 9000)])
+@pytest.mark.parametrize("n,k", [(1, 1), (1000, 3), (70000, 454), (2500000, 196), (5000, 9000),
+                                 # the one-workgroup form (n <= 32,768, k <= 2,048): both tile sizes,
+                                 # odd k, the limits
+                                 (6040, 604), (16384, 2048), (16385, 1773), (32768, 1), (32768, 2047),
+                                 (17730, 1773), (3706, 371)])
 def test_group_by_label_is_a_stable_sort(n, k):
     rng = np.random.default_rng(n + k)
     lab = rng.integers(0, k, n).astype(np.int32)

@@ -370,3 +370,43 @@ def test_kmeans_lloyd_sliced_fold_matches(monkeypatch, dim):
     assert a.n_iter_ == ref["n_iter_"]
     assert np.array_equal(a.labels_, ref["labels_"])
     assert np.array_equal(bits(a.cluster_centers_), bits(ref["cluster_centers_"]))
+
+
+@pytest.mark.parametrize("case", ["ml1m_users", "ml1m_items", "relocation", "tol0", "large_n"])
+def test_kmeans_lloyd_update_forms(monkeypatch, case):
+    """The one-workgroup update (empty check, _average_centers + shifts, labels changed, convergence
+    test in one launch; the default for n <= 131,072 and k * dim <= 262,144) and the four-launch
+    update (GDD_LLOYD_UPDATE_SPLIT) give the same fit, bit for bit, and the oracle's: recsys shapes,
+    empty-cluster relocation (the resumed iteration's update runs without the check), a strict
+    convergence run (tol = 0) and a shape above the one-workgroup limit (both forms the four launches)."""
+    rng = np.random.default_rng(5)
+    kw = {}
+    if case == "ml1m_users":
+        X, k = synth.blobs(6040, 64, 151, seed=6040), 604
+    elif case == "ml1m_items":
+        X, k = synth.blobs(3706, 64, 92, seed=3706), 371
+    elif case == "relocation":
+        base = rng.standard_normal((40, 8)).astype(np.float32)
+        X, k = np.repeat(base, 60, axis=0)[rng.permutation(2400)], 48
+    elif case == "tol0":
+        X, k = synth.blobs(5000, 16, 20, seed=50), 30
+        kw = {"tol": 0.0}
+    else:
+        X, k = synth.blobs(140000, 8, 10, seed=14), 12
+    X = np.ascontiguousarray(X, np.float32)
+    fits = []
+    for split in (False, True):
+        if split:
+            monkeypatch.setenv("GDD_LLOYD_UPDATE_SPLIT", "1")
+        np.random.seed(15)
+        fits.append(gdd.KMeans(n_clusters=k, n_init=1, **kw).fit(X))
+    a, b = fits
+    assert a.n_iter_ == b.n_iter_ and a.inertia_ == b.inertia_
+    assert np.array_equal(a.labels_, b.labels_)
+    assert np.array_equal(bits(a.cluster_centers_), bits(b.cluster_centers_))
+    if X.shape[0] * k <= 4_000_000:
+        np.random.seed(15)
+        ref = O.kmeans(X, k, n_init=1, **kw)
+        assert a.n_iter_ == ref["n_iter_"]
+        assert np.array_equal(a.labels_, ref["labels_"])
+        assert np.array_equal(bits(a.cluster_centers_), bits(ref["cluster_centers_"]))
