@@ -2154,78 +2154,165 @@ __global__ __launch_bounds__(64) void k_kpp1_final(Kpp1Args a, int c) {
 // ---- table rounds for 4096 < n <= 32768 (r04): ONE 1024-thread workgroup per trial, as k_kpp1_dm
 // (no per-block partial terms, no fold launch reading T x blocks values). The ML-1M users (6,040 x 64,
 // k = 604) and Ali-Display users (17,730 x 64, k = 1,773) shapes of the recsys clustering. Per round c:
-//   trip 1   round c-1's T potentials (np.argmin) and this trial's candidate if that trial won;
+//   trip 1   lane q of every wave loads round c-1's potential q, this slot's candidate if q won and
+//            q's own candidate, and round c+1's uniform q; np.argmin over lanes;
 //   trip 2   the winner's row (the closest distances) and the candidate's table row, coalesced
-//            (entry tid + 1024 q), np.minimum, stored for round c+1's winner read and into LDS;
-//   fold     thread j takes entries [EPT j, EPT j + EPT) from LDS: its fp64 run, a wave scan and the
-//            wave totals give every entry's cumulative potential; waves b < nsg run the sgemv_t lane
-//            chains of 4096-entry block b (sgemv_block_wave, the multi-block rounds' own block term),
-//            added in block order, then the n % 4 tail — the same potential bits as k_kpp_round;
+//            (entry tid + 1024 q), np.minimum, stored for round c+1's winner read and into LDS with one
+//            pad float per EPT entries (entry e at e + e / EPT), so that thread j's segment [EPT j,
+//            EPT j + EPT) is read without bank conflicts (lane stride EPT + 1 floats);
+//   fold     each thread's fp64 run over its segment, a wave scan and the wave totals give every
+//            entry's cumulative potential; waves b < nsg run the sgemv_t lane chains of 4096-entry block
+//            b (the order of sgemv_block_wave, the multi-block rounds' block term), added in block
+//            order, then the n % 4 tail — the same potential bits as k_kpp_round;
 //   draws    searchsorted_left(cum, u * pot) for round c+1's T uniforms as a count of entries below
-//            the threshold (only the thread whose segment straddles it walks its entries); a prefix
-//            within cum_tol of the threshold replays numpy's left-to-right sum (np_cumsum_search).
+//            the threshold: whole segments below by ballot counts, the segment that straddles it by a
+//            walk (LDS add); a prefix within cum_tol of the threshold replays numpy's left-to-right sum.
 // Round 0 (c == 0, one workgroup) draws round 1's candidates from the first centre's closest0 and
-// its sdot potential. LDS: the row, 4 * 1024 * EPT bytes (dynamic).
+// its sdot potential. LDS: the padded row, 4 * 1024 * (EPT + 1) bytes (dynamic).
 constexpr int kBigThr = 1024;
 constexpr int kBigWaves = kBigThr / 64;
 constexpr int64_t kBig1Max = 32768;
 
 template <int EPT>
+__device__ __forceinline__ int pad_idx(int e) { return e + e / EPT; }
+
+// sgemv_block_wave over entries [j0, j0 + NB) of the padded row: the same lanes, order and
+// operations (8 lanes: first NB & 4 entries on lanes 0..3, then lane (o - h4) % 8, fma with the weight
+// — fma(x, 1, acc) == acc + x; the 4-lane trials: product, then add). Two 16-entry register groups
+// alternate so the LDS reads run a group ahead of the dependent adds.
+template <int EPT>
+__device__ float sgemv_block_pad(const float* __restrict__ s, const float* __restrict__ w, int n, int j0,
+                                 int NB, int t, int T) {
+  const int lane = threadIdx.x & 63;
+  const bool k4x2 = (T & 2) && t >= (T & ~3) && t < (T & ~3) + 2;
+  const int nl = k4x2 ? 4 : 8;
+  const int h4 = k4x2 ? 0 : (NB & 4);
+  float acc = 0.f;
+  if (lane < nl) {
+    auto at = [&](int o) { return s[pad_idx<EPT>(min(j0 + o, n - 1))]; };
+    auto wt = [&](int o) { return w ? w[j0 + o] : 1.0f; };
+    if (lane < h4) acc = __builtin_fmaf(at(lane), wt(lane), acc);
+    const int o0 = h4 + lane;
+    const int L = o0 < NB ? (NB - o0 + nl - 1) / nl : 0;  // this lane's chain length
+    float A[16], B[16];
+    auto load = [&](float (&R)[16], int m) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) R[q] = at(o0 + nl * (m + q));
+    };
+    auto add = [&](const float (&R)[16], int m, int cnt) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        if (q < cnt) {
+          const int o = o0 + nl * (m + q);
+          if (k4x2)
+            acc = acc + R[q] * wt(o);
+          else
+            acc = __builtin_fmaf(R[q], wt(o), acc);
+        }
+      }
+    };
+    int m = 0;
+    load(A, 0);
+    for (; m + 32 <= L; m += 32) {
+      load(B, m + 16);
+      add(A, m, 16);
+      load(A, m + 32);
+      add(B, m + 16, 16);
+    }
+    if (m < L) {
+      load(B, m + 16);
+      add(A, m, min(16, L - m));
+      if (m + 16 < L) add(B, m + 16, L - m - 16);
+    }
+  }
+  if (k4x2) {
+    const float a1 = __shfl(acc, 1), a2 = __shfl(acc, 2), a3 = __shfl(acc, 3);
+    return (acc + a1) + (a2 + a3);
+  }
+  const float ql = acc + __shfl(acc, (lane + 4) & 63);  // q_l = a_l + a_{l+4}
+  const float q1 = __shfl(ql, 1), q2 = __shfl(ql, 2), q3 = __shfl(ql, 3);
+  return (ql + q1) + (q2 + q3);
+}
+
+// np_cumsum_search over the padded LDS row (one thread; the rare replay)
+template <int EPT>
+__device__ __noinline__ int64_t np_cumsum_search_pad(const float* s, const float* w, int n, double r) {
+  double run = 0.0;
+  for (int e = 0; e < n; ++e) {
+    run = run + (double)((w ? w[e] : 1.0f) * s[pad_idx<EPT>(e)]);
+    if (!(run < r)) return e;
+  }
+  return n;
+}
+
+template <int EPT>
 __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* __restrict__ D, int c) {
-  extern __shared__ __attribute__((aligned(16))) float s_row[];  // kBigThr * EPT floats
+  extern __shared__ float s_row[];  // kBigThr * (EPT + 1) floats: entry e at e + e / EPT
   __shared__ double s_wt[kBigWaves];
   __shared__ float s_vb[8];
   __shared__ float s_pot;
   __shared__ int s_cnt[kBigWaves][kMaxTrials];
-  __shared__ int s_amb[kBigWaves][kMaxTrials];
+  __shared__ int s_part[kMaxTrials];
+  __shared__ int s_amb[kMaxTrials];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = a.T;
   const int n = (int)a.n, m1 = (int)a.m1;
   const int t = blockIdx.x;
   const int cq = c & 1, pq = (c - 1) & 1;
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 90);
-  // ---- trip 1 (rounds >= 2): round c-1's winner and this slot's candidate
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 1), 95);
+  if (tid < kMaxTrials) {
+    s_part[tid] = 0;
+    s_amb[tid] = 0;
+  }
+  // ---- trip 1, every load at once (lane q): round c-1's potential q, this slot's candidate if q
+  // won, q's own candidate, round c+1's uniform q
+  const double ut = (c + 1 < a.k && lane < T) ? a.uniforms[(int64_t)c * T + lane] : 0.0;
   const float* wrow = a.closest0;
   int64_t ct = 0;
   if (c >= 1) {
-    int bw = 0;
-    if (c >= 2) {
-      float best = a.potv[pq][0];
-      for (int q = 1; q < T; ++q) {  // np.argmin: first minimum, a NaN wins at once
-        const float pt = a.potv[pq][q];
-        if (best == best && (pt < best || pt != pt)) {
-          bw = q;
-          best = pt;
-        }
+    const int Tp = c >= 2 ? T : 1;  // round 0 has one "trial": the first centre
+    const int ql = min(lane, Tp - 1);
+    const float pvl = a.potv[pq][ql];  // round 0 writes none: unused when Tp == 1
+    const int64_t cwl = a.candw[pq][(int64_t)ql * T + t];
+    const int64_t csl = a.candself[pq][ql];
+    int bw = 0;  // np.argmin: first minimum, a NaN wins at once
+    float best = __shfl(pvl, 0);
+    for (int q = 1; q < Tp; ++q) {
+      const float pt = __shfl(pvl, q);
+      if (best == best && (pt < best || pt != pt)) {
+        bw = q;
+        best = pt;
       }
-      wrow = a.dist[pq] + (int64_t)bw * n;
     }
-    ct = a.candw[pq][(int64_t)bw * T + t];
+    ct = __shfl(cwl, bw);
+    const int64_t sw = __shfl(csl, bw);
+    if (c >= 2) wrow = a.dist[pq] + (int64_t)bw * n;
     if (tid == 0) {
       a.candself[cq][t] = ct;
-      if (c >= 2 && t == 0) a.indices[c - 1] = a.candself[pq][bw];
+      if (c >= 2 && t == 0) a.indices[c - 1] = sw;
     }
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 91);
   // ---- trip 2: the closest distances and the candidate's table row
   {
-    float wi[EPT], dd[EPT];
-#pragma unroll
-    for (int q = 0; q < EPT; ++q) {
-      const int e = min(tid + kBigThr * q, n - 1);
-      wi[q] = wrow[e];
-      dd[q] = c >= 1 ? D[ct * n + e] : 0.f;
-    }
+    constexpr int QC = EPT < 16 ? EPT : 16;  // loads in flight per thread and row (registers)
     float* orow = a.dist[cq] + (int64_t)t * n;
 #pragma unroll
-    for (int q = 0; q < EPT; ++q) {
-      const int e = tid + kBigThr * q;
-      const float f = c >= 1 ? np_minimum(wi[q], dd[q]) : wi[q];
-      if (e < n) {
-        if (c >= 1) orow[e] = f;
-        s_row[e] = f;
-      } else {
-        s_row[e] = 0.f;
+    for (int q0 = 0; q0 < EPT; q0 += QC) {
+      float wi[QC], dd[QC];
+#pragma unroll
+      for (int q = 0; q < QC; ++q) {
+        const int e = min(tid + kBigThr * (q0 + q), n - 1);
+        wi[q] = wrow[e];
+        dd[q] = c >= 1 ? D[ct * n + e] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < QC; ++q) {
+        const int e = tid + kBigThr * (q0 + q);
+        const float f = c >= 1 ? np_minimum(wi[q], dd[q]) : wi[q];
+        if (e < n && c >= 1) orow[e] = f;
+        s_row[pad_idx<EPT>(e)] = e < n ? f : 0.f;
       }
     }
   }
@@ -2233,15 +2320,10 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 92);
   // ---- this thread's segment: products (fp32) and its fp64 run
   const int e0 = EPT * tid;
+  const int sb = (EPT + 1) * tid;
   float v[EPT];
 #pragma unroll
-  for (int q = 0; q < EPT; q += 4) {
-    const float4 x = *reinterpret_cast<const float4*>(s_row + e0 + q);
-    v[q] = x.x;
-    v[q + 1] = x.y;
-    v[q + 2] = x.z;
-    v[q + 3] = x.w;
-  }
+  for (int q = 0; q < EPT; ++q) v[q] = s_row[sb + q];
   if (a.w) {
 #pragma unroll
     for (int q = 0; q < EPT; ++q) v[q] = e0 + q < n ? a.w[e0 + q] * v[q] : 0.f;
@@ -2262,7 +2344,7 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   const int nsg = (m1 + kBlk - 1) / kBlk;
   if (c >= 1 && wave < nsg) {
     const int j0 = wave * kBlk;
-    const float vb = sgemv_block_wave(s_row + j0, a.w ? a.w + j0 : nullptr, min(kBlk, m1 - j0), t, T);
+    const float vb = sgemv_block_pad<EPT>(s_row, a.w, n, j0, min(kBlk, m1 - j0), t, T);
     if (lane == 0) s_vb[wave] = vb;
   }
   __syncthreads();
@@ -2275,8 +2357,8 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
       y = 0.f;
       for (int b = 0; b < nsg; ++b) y = y + s_vb[b];
       if (m1 < n) {
-        float sx = s_row[m1] * wv(a.w, m1);
-        for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_row[o], wv(a.w, o), sx);
+        float sx = s_row[pad_idx<EPT>(m1)] * wv(a.w, m1);
+        for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_row[pad_idx<EPT>(o)], wv(a.w, o), sx);
         y = y + sx;
       }
       a.potv[cq][t] = y;
@@ -2291,17 +2373,19 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   const double pot = (double)s_pot;
   const double first = off + (double)v[0];  // the segment's first cumulative value (as the walk's)
   const double last = off + tot;  // its last, to within EPT roundings (far inside cum_tol)
+  const bool live = e0 < n, whole = e0 + EPT <= n;
 #pragma unroll 1
   for (int t2 = 0; t2 < T; ++t2) {
-    const double rr = a.uniforms[(int64_t)c * T + t2] * pot;
+    const double rr = __shfl(ut, t2) * pot;
     const double tol = cum_tol(a.exact, n, rr);
     const bool strict = !(tol < 0.0);  // tol < 0 (GDD_KPP_EXACT=0, tests): every segment walks
-    int cnt = 0;
-    bool amb = false;
-    const bool live = e0 < n;
-    if (live && strict && last < rr - 2.0 * tol) {
-      cnt = min(EPT, n - e0);  // the whole segment is below, none within tol (the run only climbs)
-    } else if (live && !(strict && first > rr + tol)) {
+    // a whole segment below, none of it within tol (the run only climbs): counted by ballot
+    const bool below = live && whole && strict && last < rr - 2.0 * tol;
+    const unsigned long long bb = __ballot(below);
+    if (lane == 0) s_cnt[wave][t2] = EPT * __popcll(bb);
+    if (live && !below && !(strict && first > rr + tol)) {
+      int cnt = 0;
+      bool amb = false;
       double run = off;
 #pragma unroll
       for (int q = 0; q < EPT; ++q) {
@@ -2311,24 +2395,15 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
           amb = amb || fabs(run - rr) <= tol;
         }
       }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-    const bool wamb = __ballot(amb) != 0ull;
-    if (lane == 0) {
-      s_cnt[wave][t2] = cnt;
-      s_amb[wave][t2] = wamb;
+      if (cnt) atomicAdd(&s_part[t2], cnt);
+      if (amb) s_amb[t2] = 1;
     }
   }
   __syncthreads();
   if (tid < T) {
-    int64_t cnt = 0;
-    bool amb = false;
-    for (int q = 0; q < kBigWaves; ++q) {
-      cnt += s_cnt[q][tid];
-      amb = amb || s_amb[q][tid];
-    }
-    if (amb) cnt = np_cumsum_search(s_row, a.w, n, a.uniforms[(int64_t)c * T + tid] * pot);
+    int64_t cnt = s_part[tid];
+    for (int q = 0; q < kBigWaves; ++q) cnt += s_cnt[q][tid];
+    if (s_amb[tid]) cnt = np_cumsum_search_pad<EPT>(s_row, a.w, n, ut * pot);  // lane tid holds u_tid
     a.candw[cq][(int64_t)t * T + tid] = min<int64_t>(n - 1, cnt);
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 94);
@@ -2764,7 +2839,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
         big = k_kpp1_big<32>;
         ept = 32;
       }
-      const size_t lds_big = sizeof(float) * (size_t)kBigThr * ept;
+      const size_t lds_big = sizeof(float) * (size_t)kBigThr * (ept + 1);
       GDD_HIP(hipFuncSetAttribute((const void*)big, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_big));
       big<<<1, kBigThr, lds_big, s>>>(b1, Dbig, 0);  // round 1's candidates from the first centre
       GDD_LAUNCHED();

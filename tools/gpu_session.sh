@@ -16,6 +16,7 @@
 #                         products, the default hop and the 4-slice form (GDD_HOP_LANES=8)
 #   phases                tools/phase_times.py (per-phase wall times of the bench step)
 #   kpp                   tools/micro_kpp.py (k-means++ round micro-benchmark)
+#   kpp-big               tools/micro_kpp.py big (one workgroup per trial vs per-block rounds) + in-kernel stamps
 #   inertia               tools/micro_inertia.py (parallel exact inertia vs the one-lane fold)
 #   gap                   tools/probe/gap_probe (dependent launches: stream vs hipGraph replay)
 #   graph-ab              tools/micro_graph.py (MiniBatchKMeans / k-means++ fits, eager vs graph replay)
@@ -80,6 +81,7 @@ for step in "$@"; do
       done ;;
     phases) run 300 phases python tools/phase_times.py ;;
     kpp) run 300 kpp python tools/micro_kpp.py ;;
+    kpp-big) run 300 kpp_big bash -c 'python tools/micro_kpp.py big && python tools/stamps.py kpp-big' ;;
     inertia) run 300 inertia bash -c 'python tools/micro_inertia.py && GDD_INERTIA_SEQ=1 python tools/micro_inertia.py' ;;
     gap) run 60 gap ./tools/probe/gap_probe ;;
     graph-ab) run 300 graph_ab python tools/micro_graph.py ;;

@@ -64,7 +64,23 @@ def ab(n=3000, dim=40, k=454):
             del os.environ[var]
 
 
+def ab_big():
+    """One 1024-thread workgroup per trial (k_kpp1_big, default for 4096 < n <= 32768 table plans)
+    against the per-(block, trial) table rounds (GDD_KPP_NO_BIG1), same process."""
+    for (n, dim, k) in [(6040, 64, 604), (9001, 24, 200), (17730, 64, 1773)]:
+        for var in ("", "GDD_KPP_NO_BIG1", "", "GDD_KPP_NO_BIG1"):
+            if var:
+                os.environ[var] = "1"
+            print(f"variant {var or 'default'}:", end=" ", flush=True)
+            run(n, dim, k, 3, check=False)
+            if var:
+                del os.environ[var]
+
+
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["big"]:
+        ab_big()
+        sys.exit(0)
     ab()
     for (n, dim, k) in [(3000, 40, 454), (2708, 7, 70), (6040, 64, 604), (3000, 41, 769), (17730, 64, 1773)]:
         run(n, dim, k, 3, check=n * k < 3e7)

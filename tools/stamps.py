@@ -35,7 +35,26 @@ def show(title, st, slots, base):
     print(f"{title:22s} (us from slot {base}) " + " ".join(parts), flush=True)
 
 
+def kpp_big():
+    """k_kpp1_big's phases in round k-2 (trial 0) and the start of round k-1 (us)."""
+    lib = _lib.device_lib()
+    from gdd.kmeans import _Ops
+    for (n, dim, k) in [(6040, 64, 604), (17730, 64, 1773)]:
+        X = torch.from_numpy(synth.blobs(n, dim, k // 4, seed=n + dim)).cuda()
+        for rep in range(2):
+            _Ops("cuda", n, k, dim).kmeans_plusplus(X, k, np.random.RandomState(15))
+            torch.cuda.synchronize()
+            p = read(lib, "kpp")
+            t0 = p[90]
+            lab = {90: "start", 91: "winner + candidate", 92: "rows in LDS", 93: "prefix + chains",
+                   94: "draws", 95: "next start"}
+            print(f"n={n} k={k} rep {rep} (us): " + ", ".join(
+                f"{lab[q]} {(p[q] - t0) / 100:.2f}" for q in [90, 91, 92, 93, 94, 95]), flush=True)
+
+
 def main():
+    if sys.argv[1:2] == ["kpp-big"]:
+        return kpp_big()
     lib = _lib.device_lib()
     cfg = synth.CONFIGS["arxiv"]
     X = torch.from_numpy(synth.blobs(cfg.n, cfg.n_classes, cfg.k, seed=1)).cuda()
