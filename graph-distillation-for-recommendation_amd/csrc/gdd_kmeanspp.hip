@@ -2157,72 +2157,76 @@ __global__ __launch_bounds__(64) void k_kpp1_final(Kpp1Args a, int c) {
 //   trip 1   lane q of every wave loads round c-1's potential q, this slot's candidate if q won and
 //            q's own candidate, and round c+1's uniform q; np.argmin over lanes;
 //   trip 2   the winner's row (the closest distances) and the candidate's table row, coalesced
-//            (entry tid + 1024 q), np.minimum, stored for round c+1's winner read and into LDS with one
-//            pad float per EPT entries (entry e at e + e / EPT), so that thread j's segment [EPT j,
-//            EPT j + EPT) is read without bank conflicts (lane stride EPT + 1 floats);
+//            (entry tid + 1024 q), np.minimum, stored for round c+1's winner read and into LDS;
 //   fold     each thread's fp64 run over its segment, a wave scan and the wave totals give every
 //            entry's cumulative potential; waves b < nsg run the sgemv_t lane chains of 4096-entry block
-//            b (the order of sgemv_block_wave, the multi-block rounds' block term), added in block
+//            b (the order of sgemv_block_wave, the multi-block rounds' block term; unit weights read
+//            with immediate offsets, a 16-entry group ahead of the adds), added in block
 //            order, then the n % 4 tail — the same potential bits as k_kpp_round;
 //   draws    searchsorted_left(cum, u * pot) for round c+1's T uniforms as a count of entries below
 //            the threshold: whole segments below by ballot counts, the segment that straddles it by a
 //            walk (LDS add); a prefix within cum_tol of the threshold replays numpy's left-to-right sum.
 // Round 0 (c == 0, one workgroup) draws round 1's candidates from the first centre's closest0 and
-// its sdot potential. LDS: the padded row, 4 * 1024 * (EPT + 1) bytes (dynamic).
+// its sdot potential. LDS: the row, 4 * (1024 * EPT + kChainPad) bytes (dynamic).
 constexpr int kBigThr = 1024;
 constexpr int kBigWaves = kBigThr / 64;
 constexpr int64_t kBig1Max = 32768;
 
-template <int EPT>
-__device__ __forceinline__ int pad_idx(int e) { return e + e / EPT; }
+// One unit-weight sgemv_t lane chain in LDS: acc + x over p[0], p[S], p[2S], ... (L entries). Two
+// 16-entry register groups alternate: a group's reads (immediate offsets from one address) are
+// issued a whole group of dependent adds ahead of their use (scheduling barriers keep them there, as
+// in chain_add). Reads run at most 32 S entries past the chain: the row buffer is padded for them.
+template <int S>
+__device__ __forceinline__ float chain_unit_lds(const float* __restrict__ p, int L, float acc) {
+  float A[16], B[16];
+  auto ld = [&](float (&R)[16], int m) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) R[q] = p[S * (m + q)];
+  };
+  int m = 0;
+  ld(A, 0);
+  for (; m + 32 <= L; m += 32) {
+    ld(B, m + 16);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc = acc + A[q];
+    __builtin_amdgcn_sched_barrier(0);
+    ld(A, m + 32);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc = acc + B[q];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  ld(B, m + 16);  // A holds entries m .. m + 15; fewer than 32 remain
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc = m + q < L ? acc + A[q] : acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc = m + 16 + q < L ? acc + B[q] : acc;
+  return acc;
+}
+constexpr int kChainPad = 32 * 8 + 16;  // floats past the row that the chains' look-ahead may read
 
-// sgemv_block_wave over entries [j0, j0 + NB) of the padded row: the same lanes, order and
-// operations (8 lanes: first NB & 4 entries on lanes 0..3, then lane (o - h4) % 8, fma with the weight
-// — fma(x, 1, acc) == acc + x; the 4-lane trials: product, then add). Two 16-entry register groups
-// alternate so the LDS reads run a group ahead of the dependent adds.
-template <int EPT>
-__device__ float sgemv_block_pad(const float* __restrict__ s, const float* __restrict__ w, int n, int j0,
-                                 int NB, int t, int T) {
+// sgemv_block_wave over entries [j0, j0 + NB) of the LDS row: the same lanes, order and operations
+// (8 lanes: first NB & 4 entries on lanes 0..3, then lane (o - h4) % 8, fma with the weight —
+// fma(x, 1, acc) == acc + x; the 4-lane trials: product, then add — x * 1 == x).
+__device__ __forceinline__ float sgemv_block_lds(const float* __restrict__ s, const float* __restrict__ w,
+                                                 int j0, int NB, int t, int T) {
   const int lane = threadIdx.x & 63;
   const bool k4x2 = (T & 2) && t >= (T & ~3) && t < (T & ~3) + 2;
   const int nl = k4x2 ? 4 : 8;
   const int h4 = k4x2 ? 0 : (NB & 4);
   float acc = 0.f;
   if (lane < nl) {
-    auto at = [&](int o) { return s[pad_idx<EPT>(min(j0 + o, n - 1))]; };
-    auto wt = [&](int o) { return w ? w[j0 + o] : 1.0f; };
-    if (lane < h4) acc = __builtin_fmaf(at(lane), wt(lane), acc);
+    if (lane < h4) acc = __builtin_fmaf(s[j0 + lane], w ? w[j0 + lane] : 1.0f, acc);
     const int o0 = h4 + lane;
     const int L = o0 < NB ? (NB - o0 + nl - 1) / nl : 0;  // this lane's chain length
-    float A[16], B[16];
-    auto load = [&](float (&R)[16], int m) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) R[q] = at(o0 + nl * (m + q));
-    };
-    auto add = [&](const float (&R)[16], int m, int cnt) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        if (q < cnt) {
-          const int o = o0 + nl * (m + q);
-          if (k4x2)
-            acc = acc + R[q] * wt(o);
-          else
-            acc = __builtin_fmaf(R[q], wt(o), acc);
-        }
+    if (w == nullptr) {
+      acc = k4x2 ? chain_unit_lds<4>(s + j0 + o0, L, acc) : chain_unit_lds<8>(s + j0 + o0, L, acc);
+    } else {
+      for (int m = 0; m < L; ++m) {
+        const int e = j0 + o0 + nl * m;
+        acc = k4x2 ? acc + s[e] * w[e] : __builtin_fmaf(s[e], w[e], acc);
       }
-    };
-    int m = 0;
-    load(A, 0);
-    for (; m + 32 <= L; m += 32) {
-      load(B, m + 16);
-      add(A, m, 16);
-      load(A, m + 32);
-      add(B, m + 16, 16);
-    }
-    if (m < L) {
-      load(B, m + 16);
-      add(A, m, min(16, L - m));
-      if (m + 16 < L) add(B, m + 16, L - m - 16);
     }
   }
   if (k4x2) {
@@ -2234,26 +2238,23 @@ __device__ float sgemv_block_pad(const float* __restrict__ s, const float* __res
   return (ql + q1) + (q2 + q3);
 }
 
-// np_cumsum_search over the padded LDS row (one thread; the rare replay)
-template <int EPT>
-__device__ __noinline__ int64_t np_cumsum_search_pad(const float* s, const float* w, int n, double r) {
-  double run = 0.0;
-  for (int e = 0; e < n; ++e) {
-    run = run + (double)((w ? w[e] : 1.0f) * s[pad_idx<EPT>(e)]);
-    if (!(run < r)) return e;
-  }
-  return n;
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const unsigned long long b = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 template <int EPT>
 __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* __restrict__ D, int c) {
-  extern __shared__ float s_row[];  // kBigThr * (EPT + 1) floats: entry e at e + e / EPT
+  extern __shared__ __attribute__((aligned(16))) float s_row[];  // kBigThr * EPT + kChainPad floats
   __shared__ double s_wt[kBigWaves];
   __shared__ float s_vb[8];
   __shared__ float s_pot;
-  __shared__ int s_cnt[kBigWaves][kMaxTrials];
+  __shared__ int s_cnt[1][kMaxTrials];
   __shared__ int s_part[kMaxTrials];
   __shared__ int s_amb[kMaxTrials];
+  __shared__ double s_off[kBigThr], s_last[kBigThr];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = a.T;
   const int n = (int)a.n, m1 = (int)a.m1;
@@ -2312,7 +2313,7 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
         const int e = tid + kBigThr * (q0 + q);
         const float f = c >= 1 ? np_minimum(wi[q], dd[q]) : wi[q];
         if (e < n && c >= 1) orow[e] = f;
-        s_row[pad_idx<EPT>(e)] = e < n ? f : 0.f;
+        s_row[e] = e < n ? f : 0.f;
       }
     }
   }
@@ -2320,10 +2321,15 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 92);
   // ---- this thread's segment: products (fp32) and its fp64 run
   const int e0 = EPT * tid;
-  const int sb = (EPT + 1) * tid;
   float v[EPT];
 #pragma unroll
-  for (int q = 0; q < EPT; ++q) v[q] = s_row[sb + q];
+  for (int q = 0; q < EPT; q += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(s_row + e0 + q);
+    v[q] = x.x;
+    v[q + 1] = x.y;
+    v[q + 2] = x.z;
+    v[q + 3] = x.w;
+  }
   if (a.w) {
 #pragma unroll
     for (int q = 0; q < EPT; ++q) v[q] = e0 + q < n ? a.w[e0 + q] * v[q] : 0.f;
@@ -2344,11 +2350,15 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   const int nsg = (m1 + kBlk - 1) / kBlk;
   if (c >= 1 && wave < nsg) {
     const int j0 = wave * kBlk;
-    const float vb = sgemv_block_pad<EPT>(s_row, a.w, n, j0, min(kBlk, m1 - j0), t, T);
+    const float vb = sgemv_block_lds(s_row, a.w, j0, min(kBlk, m1 - j0), t, T);
     if (lane == 0) s_vb[wave] = vb;
   }
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 93);
+  double off = ex;
+  for (int q = 0; q < wave; ++q) off = off + s_wt[q];
+  s_off[tid] = off;
+  s_last[tid] = off + tot;  // the segment's last cumulative value, to within EPT roundings
   if (tid == 0) {
     float y;
     if (c == 0) {
@@ -2357,53 +2367,59 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
       y = 0.f;
       for (int b = 0; b < nsg; ++b) y = y + s_vb[b];
       if (m1 < n) {
-        float sx = s_row[pad_idx<EPT>(m1)] * wv(a.w, m1);
-        for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_row[pad_idx<EPT>(o)], wv(a.w, o), sx);
+        float sx = s_row[m1] * wv(a.w, m1);
+        for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_row[o], wv(a.w, o), sx);
         y = y + sx;
       }
       a.potv[cq][t] = y;
     }
     s_pot = y;
   }
-  double off = ex;
-  for (int q = 0; q < wave; ++q) off = off + s_wt[q];
   __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 96);
   if (c + 1 >= a.k) return;
-  // ---- draws for round c+1 if this trial wins
-  const double pot = (double)s_pot;
-  const double first = off + (double)v[0];  // the segment's first cumulative value (as the walk's)
-  const double last = off + tot;  // its last, to within EPT roundings (far inside cum_tol)
-  const bool live = e0 < n, whole = e0 + EPT <= n;
-#pragma unroll 1
-  for (int t2 = 0; t2 < T; ++t2) {
-    const double rr = __shfl(ut, t2) * pot;
+  // ---- draws for round c+1 if this trial wins: wave t2 takes uniform t2 over every segment (lane l:
+  // segments l, l + 64, ...): whole segments below are counted by ballot, a segment that straddles
+  // the threshold is walked by its lane — the owner's run, recomputed from LDS in the same order
+  if (wave < T) {
+    const int t2 = wave;
+    const double pot = (double)s_pot;
+    const double rr = readlane_f64(ut, t2) * pot;  // wave-uniform: a scalar read of lane t2
     const double tol = cum_tol(a.exact, n, rr);
     const bool strict = !(tol < 0.0);  // tol < 0 (GDD_KPP_EXACT=0, tests): every segment walks
-    // a whole segment below, none of it within tol (the run only climbs): counted by ballot
-    const bool below = live && whole && strict && last < rr - 2.0 * tol;
-    const unsigned long long bb = __ballot(below);
-    if (lane == 0) s_cnt[wave][t2] = EPT * __popcll(bb);
-    if (live && !below && !(strict && first > rr + tol)) {
-      int cnt = 0;
-      bool amb = false;
-      double run = off;
-#pragma unroll
-      for (int q = 0; q < EPT; ++q) {
-        run = run + (double)v[q];
-        if (e0 + q < n) {
-          cnt += run < rr;
-          amb = amb || fabs(run - rr) <= tol;
+    int full = 0, part = 0;
+    bool amb = false;
+#pragma unroll 4
+    for (int i = 0; i < kBigThr / 64; ++i) {
+      const int j = lane + 64 * i;
+      const int ej = EPT * j;
+      const bool live = ej < n;
+      // a whole segment below, none of it within tol (the run only climbs)
+      const bool below = live && ej + EPT <= n && strict && s_last[j] < rr - 2.0 * tol;
+      full += __popcll(__ballot(below));
+      if (live && !below) {
+        const double oj = s_off[j];
+        const float v0 = s_row[ej] * (a.w ? a.w[ej] : 1.0f);
+        if (!(strict && oj + (double)v0 > rr + tol)) {  // not wholly above: walk it
+          double run = oj;
+          for (int q = 0; q < EPT && ej + q < n; ++q) {
+            const float vq = a.w ? a.w[ej + q] * s_row[ej + q] : s_row[ej + q];
+            run = run + (double)vq;
+            part += run < rr;
+            amb = amb || fabs(run - rr) <= tol;
+          }
         }
       }
-      if (cnt) atomicAdd(&s_part[t2], cnt);
-      if (amb) s_amb[t2] = 1;
     }
+    if (part) atomicAdd(&s_part[t2], part);
+    if (amb) s_amb[t2] = 1;
+    if (lane == 0) s_cnt[0][t2] = EPT * full;
   }
   __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 97);
   if (tid < T) {
-    int64_t cnt = s_part[tid];
-    for (int q = 0; q < kBigWaves; ++q) cnt += s_cnt[q][tid];
-    if (s_amb[tid]) cnt = np_cumsum_search_pad<EPT>(s_row, a.w, n, ut * pot);  // lane tid holds u_tid
+    int64_t cnt = (int64_t)s_cnt[0][tid] + s_part[tid];
+    if (s_amb[tid]) cnt = np_cumsum_search(s_row, a.w, n, ut * (double)s_pot);  // lane tid holds u_tid
     a.candw[cq][(int64_t)t * T + tid] = min<int64_t>(n - 1, cnt);
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 94);
@@ -2839,7 +2855,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
         big = k_kpp1_big<32>;
         ept = 32;
       }
-      const size_t lds_big = sizeof(float) * (size_t)kBigThr * (ept + 1);
+      const size_t lds_big = sizeof(float) * ((size_t)kBigThr * ept + kChainPad);
       GDD_HIP(hipFuncSetAttribute((const void*)big, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_big));
       big<<<1, kBigThr, lds_big, s>>>(b1, Dbig, 0);  // round 1's candidates from the first centre
       GDD_LAUNCHED();

@@ -47,9 +47,9 @@ def kpp_big():
             p = read(lib, "kpp")
             t0 = p[90]
             lab = {90: "start", 91: "winner + candidate", 92: "rows in LDS", 93: "prefix + chains",
-                   94: "draws", 95: "next start"}
+                   96: "potential", 97: "draws", 94: "candidates out", 95: "next start"}
             print(f"n={n} k={k} rep {rep} (us): " + ", ".join(
-                f"{lab[q]} {(p[q] - t0) / 100:.2f}" for q in [90, 91, 92, 93, 94, 95]), flush=True)
+                f"{lab[q]} {(p[q] - t0) / 100:.2f}" for q in [90, 91, 92, 93, 96, 97, 94, 95]), flush=True)
 
 
 def main():
