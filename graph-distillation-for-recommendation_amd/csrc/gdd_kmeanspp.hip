@@ -2254,7 +2254,7 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   __shared__ int s_cnt[1][kMaxTrials];
   __shared__ int s_part[kMaxTrials];
   __shared__ int s_amb[kMaxTrials];
-  __shared__ double s_off[kBigThr], s_last[kBigThr];
+  __shared__ double s_off[kBigThr], s_first[kBigThr], s_last[kBigThr];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = a.T;
   const int n = (int)a.n, m1 = (int)a.m1;
@@ -2358,7 +2358,8 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   double off = ex;
   for (int q = 0; q < wave; ++q) off = off + s_wt[q];
   s_off[tid] = off;
-  s_last[tid] = off + tot;  // the segment's last cumulative value, to within EPT roundings
+  s_first[tid] = off + (double)v[0];  // the segment's first cumulative value (as the walk's)
+  s_last[tid] = off + tot;            // its last, to within EPT roundings (far inside cum_tol)
   if (tid == 0) {
     float y;
     if (c == 0) {
@@ -2389,24 +2390,44 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
     const bool strict = !(tol < 0.0);  // tol < 0 (GDD_KPP_EXACT=0, tests): every segment walks
     int full = 0, part = 0;
     bool amb = false;
-#pragma unroll 4
+    double fj[kBigThr / 64], lj[kBigThr / 64];  // every segment's first and last value, read at once
+#pragma unroll
+    for (int i = 0; i < kBigThr / 64; ++i) {
+      fj[i] = s_first[lane + 64 * i];
+      lj[i] = s_last[lane + 64 * i];
+    }
+#pragma unroll
     for (int i = 0; i < kBigThr / 64; ++i) {
       const int j = lane + 64 * i;
       const int ej = EPT * j;
       const bool live = ej < n;
       // a whole segment below, none of it within tol (the run only climbs)
-      const bool below = live && ej + EPT <= n && strict && s_last[j] < rr - 2.0 * tol;
+      const bool below = live && ej + EPT <= n && strict && lj[i] < rr - 2.0 * tol;
       full += __popcll(__ballot(below));
-      if (live && !below) {
+      if (live && !below && !(strict && fj[i] > rr + tol)) {  // not wholly above either: walk it
         const double oj = s_off[j];
-        const float v0 = s_row[ej] * (a.w ? a.w[ej] : 1.0f);
-        if (!(strict && oj + (double)v0 > rr + tol)) {  // not wholly above: walk it
+        {
+          float vs[EPT];  // the segment's terms, every read issued before the run
+#pragma unroll
+          for (int q = 0; q < EPT; q += 4) {
+            const float4 x = *reinterpret_cast<const float4*>(s_row + ej + q);
+            vs[q] = x.x;
+            vs[q + 1] = x.y;
+            vs[q + 2] = x.z;
+            vs[q + 3] = x.w;
+          }
+          if (a.w) {
+#pragma unroll
+            for (int q = 0; q < EPT; ++q) vs[q] = ej + q < n ? a.w[ej + q] * vs[q] : 0.f;
+          }
           double run = oj;
-          for (int q = 0; q < EPT && ej + q < n; ++q) {
-            const float vq = a.w ? a.w[ej + q] * s_row[ej + q] : s_row[ej + q];
-            run = run + (double)vq;
-            part += run < rr;
-            amb = amb || fabs(run - rr) <= tol;
+#pragma unroll
+          for (int q = 0; q < EPT; ++q) {
+            run = run + (double)vs[q];
+            if (ej + q < n) {
+              part += run < rr;
+              amb = amb || fabs(run - rr) <= tol;
+            }
           }
         }
       }
@@ -2530,6 +2551,14 @@ extern "C" size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int dim, int n_trials)
 // chain (slot-independent) and the table is affordable: n <= kDmBigMax (4 GiB), dim <= kDmX, k >=
 // kDmMinK. ML-1M users (6,040 x 64, k = 604), Ali-Display users (17,730 x 64, k = 1,773)
 constexpr int64_t kDmBigMax = 32768;
+// largest n for k_kpp1_big (one workgroup per trial): beyond ~16K points one CU's share of the row
+// traffic (two rows in, one out per round) outweighs the per-block rounds' extra launch work
+// (Ali-Display users, 17,730 points: 35.2 vs 23.5 us per round); GDD_KPP_BIG1_MAX overrides (tests)
+int64_t kpp_big1_max() {
+  const char* e = getenv("GDD_KPP_BIG1_MAX");
+  const int64_t v = e ? atoll(e) : 16384;
+  return v < kBig1Max ? v : kBig1Max;
+}
 bool kpp_big_table(int64_t n, int dim, int T, int k) {
   if (n <= kBlk || n > kDmBigMax || dim > kDmX || T < 2 || k < kDmMinK) return false;
   if (getenv("GDD_KPP_NO_TABLE") != nullptr) return false;
@@ -2825,7 +2854,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       k_kpp_dmat<64><<<gdm, 256, 0, s>>>((int)n, dim, X, a.XT, xsq, Dbig);
     GDD_LAUNCHED();
     a.D = Dbig;
-    if (n <= kBig1Max && T >= 2 && getenv("GDD_KPP_NO_BIG1") == nullptr) {
+    if (n <= kpp_big1_max() && T >= 2 && getenv("GDD_KPP_NO_BIG1") == nullptr) {
       // one 1024-thread workgroup per trial (k_kpp1_big); GDD_KPP_NO_BIG1 keeps the per-block rounds
       b1.n = n;
       b1.m1 = a.m1;

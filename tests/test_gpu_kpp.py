@@ -178,7 +178,7 @@ CUMSUM_FORMS = [
     (1000, ()), (4096, ()), (1000, ("GDD_KPP_SINGLE_ROUND",)), (1000, ("GDD_KPP_NO_TABLE",)),
     (1000, ("GDD_KPP_NO_TABLE", "GDD_KPP_TWO_LAUNCH")), (1000, ("GDD_KPP_BSEARCH",)),
     (4096, ("GDD_KPP_SINGLE_ROUND", "GDD_KPP_BSEARCH")), (9000, ()), (9000, ("GDD_KPP_NO_BIG1",)),
-    (20000, ()), (530000, ()),
+    (20000, ()), (20000, ("GDD_KPP_BIG1_MAX=32768",)), (530000, ()),
 ]
 
 
@@ -195,7 +195,8 @@ def test_kpp_cumsum_adversarial(monkeypatch, n, env, rnd):
     c_ref, idx_ref = O.kmeans_plusplus_draws(X, k, T, 0, u)
     assert idx_ref[rnd] == n - 2
     for var in env:
-        monkeypatch.setenv(var, "1")
+        key, _, val = var.partition("=")
+        monkeypatch.setenv(key, val or "1")
     for mode in ("1", "2"):
         monkeypatch.setenv("GDD_KPP_EXACT", mode)
         c, idx = _kpp_dev(X, k, T, 0, u)
@@ -209,6 +210,7 @@ def test_kpp_cumsum_adversarial(monkeypatch, n, env, rnd):
 @pytest.mark.parametrize("n", [1000, 9000, 20000])
 def test_kpp_cumsum_adversarial_weighted(monkeypatch, n):
     """The same with sample weights (w * closest in fp32, then the fp64 sum)."""
+    monkeypatch.setenv("GDD_KPP_BIG1_MAX", "32768")
     k, T = 16, 4
     X = adversarial_points(n)
     w = np.ones(n, np.float32)
@@ -249,6 +251,7 @@ def test_kmeans_plusplus_big_rounds(monkeypatch, n, dim, k, oracle):
     bit for bit, over the 8-, 16- and 32-entry segment forms, odd n (the sgemv_t tail) and T = 9."""
     X = synth.blobs(n, dim, max(2, k // 4), seed=n + dim + 3)
     X = np.ascontiguousarray(X - X.mean(axis=0), np.float32)
+    monkeypatch.setenv("GDD_KPP_BIG1_MAX", "32768")  # the 32-entry segments too (default limit 16,384)
     ops = _Ops("cuda", n, k, dim)
     Xd = torch.from_numpy(X).cuda()
     c, idx = ops.kmeans_plusplus(Xd, k, np.random.RandomState(42))
