@@ -77,7 +77,23 @@ def ab_big():
                 del os.environ[var]
 
 
+def ab_spec():
+    """The pair launches' speculative trip 3 (default) against reading the row after the exact draw
+    (GDD_KPP_NO_SPEC), same process, at the MiniBatchKMeans init shape and two others."""
+    for (n, dim, k) in [(3000, 40, 454), (3000, 41, 769), (3706, 64, 371)]:
+        for var in ("", "GDD_KPP_NO_SPEC", "", "GDD_KPP_NO_SPEC"):
+            if var:
+                os.environ[var] = "1"
+            print(f"variant {var or 'default'}:", end=" ", flush=True)
+            run(n, dim, k, 5, check=(var == ""))
+            if var:
+                del os.environ[var]
+
+
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["spec"]:
+        ab_spec()
+        sys.exit(0)
     if sys.argv[1:2] == ["big"]:
         ab_big()
         sys.exit(0)
