@@ -1318,7 +1318,6 @@ struct Kpp1Args {
   int64_t* candself2[2];  // [T*T]
   int exact;             // cum_tol's mode
   int bsearch;           // 1: the folds' binary searches (GDD_KPP_BSEARCH, A/B); 0: two-ballot searches
-  int spec;              // pair launches: speculative trip 3 (KppSpec; GDD_KPP_NO_SPEC turns it off)
 };
 
 __device__ __forceinline__ int kpp1_argmin(const float* __restrict__ pot, int T) {
@@ -1632,19 +1631,6 @@ __global__ __launch_bounds__(kThr) void k_kpp1_pick(Kpp1Args a, int c) {
 
 constexpr int kFPW = 22;     // prefix entries per thread of waves 1..3 in the fold (192 x 22 >= 4096)
 
-// Speculative trip 3 of the pair launch (k_kpp1_dm2, r04): while wave 0 runs round c's lane chains
-// (the exact potential, ~2 us of dependent adds), waves 2 and 3 draw slot t2's round-(c+1) candidate
-// with the fp64 total standing in for the potential and stage that candidate's table row in LDS;
-// wave 1 alone writes the cumulative potential. After the chains the exact draw decides: the staged
-// row is used when the candidates agree (all but ~1e-3 of the draws: a prefix would have to fall
-// between the two thresholds), else the row is read from the table as before.
-struct KppSpec {
-  int t2;              // the round-(c+1) slot this workgroup folds next
-  const float* D;      // the distance table
-  float* s_row;        // LDS: the speculative candidate's table row (n floats)
-  int64_t* s_cand;     // LDS: the speculative candidate
-};
-
 // the fold of round c's trial t by one 256-thread workgroup holding the trial's row in registers
 // (r[q] = entry tid + 256 q): the exact sgemv_t potential, the fp64 cumulative potential and the
 // candidates every trial would draw in round c+1 if t wins
@@ -1654,8 +1640,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
                                                 double ut, float* __restrict__ s_d,
                                                 float* __restrict__ s_ch, double* __restrict__ s_cum,
                                                 double* __restrict__ s_wave, float* __restrict__ s_pot_p,
-                                                float* pot_out, int64_t* cand_out,
-                                                const KppSpec* sp = nullptr) {
+                                                float* pot_out, int64_t* cand_out) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = a.T;
   const int n = (int)a.n;
@@ -1716,55 +1701,6 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
       s_pot = y;
       if (pot_out) *pot_out = y;
     }
-  } else if (sp && c + 1 < a.k) {  // speculation (see KppSpec): lane l's entries [SEG l, SEG l + SEG)
-    const int SEG = (n + 63) >> 6;
-    const int b0 = min(n, lane * SEG), b1 = min(n, b0 + SEG);
-    double run = 0.0;
-    for (int e = b0; e < b1; ++e) run = run + (double)(wv(a.w, e) * s_d[e]);
-    double inc = run;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const double y = __shfl_up(inc, o);
-      if (lane >= o) inc = inc + y;
-    }
-    double ex = __shfl_up(inc, 1);
-    if (lane == 0) ex = 0.0;
-    if (wave == 1) {  // the cumulative potential, for the exact draws after the barrier
-      double cur = ex;
-      for (int e = b0; e < b1; ++e) {
-        cur = cur + (double)(wv(a.w, e) * s_d[e]);
-        s_cum[e] = cur;
-      }
-    } else {  // waves 2, 3: slot t2's draw with the fp64 total, then half of that row each
-      const double total = __shfl(inc, 63);
-      const double rr = a.uniforms[(int64_t)c * T + sp->t2] * (double)(float)total;
-      int cnt = 0;
-      if (b0 < b1 && ex < rr) {
-        if (ex + run < rr) {
-          cnt = b1 - b0;
-        } else {
-          double cur = ex;
-          for (int e = b0; e < b1; ++e) {
-            cur = cur + (double)(wv(a.w, e) * s_d[e]);
-            cnt += cur < rr;
-          }
-        }
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-      const int64_t c1 = min(n - 1, cnt);
-      const float* drow = sp->D + c1 * n;
-      const int h = wave - 2;
-      float x[32];
-#pragma unroll
-      for (int q = 0; q < 32; ++q) x[q] = drow[min(h * 64 + lane + 128 * q, n - 1)];
-#pragma unroll
-      for (int q = 0; q < 32; ++q) {
-        const int e = h * 64 + lane + 128 * q;
-        if (e < n) sp->s_row[e] = x[q];
-      }
-      if (wave == 2 && lane == 0) *sp->s_cand = c1;
-    }
   } else {  // the cumulative potential: thread runs and the wave's inclusive scan
     double run = 0.0;
 #pragma unroll
@@ -1788,7 +1724,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 70);
   if (c + 1 < a.k) {
-    if (wave > 0 && !sp) {
+    if (wave > 0) {
       double B = 0.0;
       for (int q = 0; q < wave - 1; ++q) B = B + s_wave[q];
       const double pot = (double)s_pot;
@@ -2104,8 +2040,6 @@ __global__ __launch_bounds__(256) void k_kpp1_dm2(Kpp1Args a, const float* __res
   __shared__ double s_wave[4];
   __shared__ float s_pot;
   __shared__ int64_t s_cand[kMaxTrials];
-  __shared__ float s_d2[kBlk];   // the speculative candidate's table row
-  __shared__ int64_t s_c1;       // and the candidate
   const int tid = threadIdx.x, lane = tid & 63;
   const int T = a.T, pl = lq ^ 1, TT = T * T;
   const int n = (int)a.n;
@@ -2173,24 +2107,17 @@ __global__ __launch_bounds__(256) void k_kpp1_dm2(Kpp1Args a, const float* __res
                           a.candw[lq] + (int64_t)w * T);
     return;
   }
-  const KppSpec spec{t2, D, s_d2, &s_c1};
   kpp1_fold_trial<PIPE>(a, c, w, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot,
-                        t2 == 0 ? a.potv[lq] + w : nullptr, s_cand, a.spec ? &spec : nullptr);
+                        t2 == 0 ? a.potv[lq] + w : nullptr, s_cand);
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && g == 0 && c == a.k - 3 + (a.k & 1)), 62);
-  // trip 3: round c+1's candidate for slot t2 if w wins, and its table row (staged in LDS by the
-  // speculation when its candidate was the right one)
+  // trip 3: round c+1's candidate for slot t2 if w wins, and its table row
   const int64_t c1 = s_cand[t2];
   const int j = w * T + t2;
   if (tid == 0) a.candself2[lq][j] = c1;
-  if (a.spec && s_c1 == c1) {
+  const float* drow2 = D + c1 * n;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) dd[q] = s_d2[min(tid + 256 * q, n - 1)];
-  } else {
-    const float* drow2 = D + c1 * n;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) dd[q] = drow2[min(tid + 256 * q, n - 1)];
-  }
+  for (int q = 0; q < 16; ++q) dd[q] = drow2[min(tid + 256 * q, n - 1)];
   float* orow = a.dist2[lq] + (int64_t)j * n;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -2783,7 +2710,6 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     b1.plan = a.plan;
     b1.exact = a.exact;
     b1.bsearch = getenv("GDD_KPP_BSEARCH") != nullptr ? 1 : 0;
-    b1.spec = getenv("GDD_KPP_NO_SPEC") != nullptr ? 0 : 1;
     if (seq) {
       k_kpp_xt<<<dim3((unsigned)((n + kXtTile - 1) / kXtTile), (unsigned)((dim + kXtTile - 1) / kXtTile)), 256, 0,
                s>>>((int)n, dim, X, XT);
