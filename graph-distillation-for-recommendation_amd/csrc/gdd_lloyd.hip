@@ -876,13 +876,43 @@ __global__ __launch_bounds__(256) void k_lloyd_converge(int k, const float* __re
   }
 }
 
-// The update step of a small Lloyd problem in ONE workgroup (r04): the empty-cluster check of step
+// The update step of a small Lloyd problem in ONE workgroup (r04, opt-in: see lloyd_update_small): the empty-cluster check of step
 // 2i (check != 0), then step 2i+1's _average_centers + shifts, labels-changed and convergence test —
 // the operations of k_lloyd_check_empty, k_avg_centers, k_lloyd_changed and k_lloyd_converge, in
 // their order, on one CU instead of four dependent launches (recsys shapes: ~4 us each, latency).
 // Empty clusters: with the check they stop the loop at step 2i+1 exactly as k_lloyd_check_empty
 // (nothing else runs); without it (the iteration resumed after the host's relocation) the heaviest
 // cluster donates its row as in k_avg_centers: raw to empties before it, averaged to those after.
+// skl_sqdist with its operands read 32 entries at a time (every load of a chunk in flight before the
+// chunk's arithmetic, which is skl_sqdist's: groups of four, then the tail)
+__device__ __forceinline__ float skl_sqdist_staged(const float* __restrict__ a, const float* __restrict__ b,
+                                                   int dim) {
+  float r = 0.f;
+  int j = 0;
+  for (; j + 32 <= dim; j += 32) {
+    float x[32], y[32];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      x[q] = a[j + q];
+      y[q] = b[j + q];
+    }
+#pragma unroll
+    for (int q = 0; q < 32; q += 4) {
+      const float d0 = x[q] - y[q], d1 = x[q + 1] - y[q + 1], d2 = x[q + 2] - y[q + 2], d3 = x[q + 3] - y[q + 3];
+      r = r + (((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
+    }
+  }
+  for (; j + 4 <= dim; j += 4) {
+    const float d0 = a[j] - b[j], d1 = a[j + 1] - b[j + 1], d2 = a[j + 2] - b[j + 2], d3 = a[j + 3] - b[j + 3];
+    r = r + (((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
+  }
+  for (; j < dim; ++j) {
+    const float d0 = a[j] - b[j];
+    r = r + d0 * d0;
+  }
+  return r;
+}
+
 constexpr int kUpdThr = 1024;
 constexpr int64_t kUpdMaxN = 131072;      // labels compared by one workgroup
 constexpr int64_t kUpdMaxKD = 262144;     // centre entries averaged by one workgroup
@@ -892,6 +922,7 @@ __global__ __launch_bounds__(kUpdThr) void k_lloyd_update_small(
     int32_t* __restrict__ old, double tol, LloydState* st, int it, int check, int step_i) {
   if (stopped(&st->stop_at, step_i)) return;
   __shared__ float sq[kShiftLds];
+  __shared__ float s_alpha[kShiftLds];
   __shared__ PwLds pl;
   __shared__ float s_bv[kUpdThr / 64];
   __shared__ int s_bi[kUpdThr / 64];
@@ -950,12 +981,29 @@ __global__ __launch_bounds__(kUpdThr) void k_lloyd_update_small(
     }
     __syncthreads();
   }
-  for (int c = wave; c < k; c += kUpdThr / 64) {  // one wave per row
+  // every row's scale first (`1.0 / weight` is a C double division; -1: an empty row, left as is),
+  // then the rows in batches of 8 entries per thread with every load issued before the stores
+  for (int c = tid; c < k; c += kUpdThr) {
     const float wc = wsum[c];
-    if (!(wc > 0.f)) continue;
-    const float alpha = (float)(1.0 / (double)wc);  // `1.0 / weight` is a C double division
-    const int64_t cb = (int64_t)c * dim;
-    for (int f = lane; f < dim; f += 64) C_new[cb + f] = C_new[cb + f] * alpha;
+    s_alpha[c] = wc > 0.f ? (float)(1.0 / (double)wc) : -1.f;
+  }
+  __syncthreads();
+  const int64_t KD = (int64_t)k * dim;
+  for (int64_t e0 = tid; e0 < KD; e0 += 8 * kUpdThr) {
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t e = e0 + (int64_t)u * kUpdThr;
+      x[u] = e < KD ? C_new[e] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t e = e0 + (int64_t)u * kUpdThr;
+      if (e < KD) {
+        const float al = s_alpha[(int)(e / dim)];
+        if (al >= 0.f) C_new[e] = x[u] * al;
+      }
+    }
   }
   // labels changed (np.array_equal(labels, labels_old)), labels_old = labels
   int diff = 0;
@@ -969,7 +1017,7 @@ __global__ __launch_bounds__(kUpdThr) void k_lloyd_update_small(
   const int changed = __syncthreads_or(diff) | st->changed;  // the barrier also publishes C_new
   for (int c = tid; c < k; c += kUpdThr) {
     const int64_t cb = (int64_t)c * dim;
-    const float sh = sqrtf(skl_sqdist(C_new + cb, C_old + cb, dim));
+    const float sh = sqrtf(skl_sqdist_staged(C_new + cb, C_old + cb, dim));
     if (shift) shift[c] = sh;
     sq[c] = sh * sh;
   }
@@ -991,7 +1039,10 @@ __global__ __launch_bounds__(kUpdThr) void k_lloyd_update_small(
 }
 
 __host__ __forceinline__ bool lloyd_update_small(int64_t n, int dim, int k) {
-  return getenv("GDD_LLOYD_UPDATE_SPLIT") == nullptr && n <= kUpdMaxN && k <= kShiftLds && (int64_t)k * dim <= kUpdMaxKD;
+  // opt-in (GDD_LLOYD_UPDATE_SMALL=1): measured slower than the four launches at the recsys shapes
+  // (ML-1M users 81.5 vs 71.5 us per iteration, profiles/r04_lloyd_small.txt) — one CU runs phases the
+  // four launches spread over the chip
+  return getenv("GDD_LLOYD_UPDATE_SMALL") != nullptr && n <= kUpdMaxN && k <= kShiftLds && (int64_t)k * dim <= kUpdMaxKD;
 }
 
 // ((X - C[labels])**2).sum(axis=1) in numpy's order: fp32 squares, pairwise per contiguous row
