@@ -653,6 +653,19 @@ __device__ __attribute__((noinline)) float pw_sum(F val, int off, int n) {
 }
 constexpr int kPwDepth = 24;  // n < 128 * 2^24
 
+// the Lloyd loop's control words
+// Iteration i runs as two steps: 2i (E-step labels, grouping, sums, the empty-cluster check) and
+// 2i+1 (average + shift, labels changed, convergence). stop_at = s+1 skips every later step.
+struct LloydState {
+  int32_t stop_at;   // offset 0
+  int32_t reason;    // 0 running/max_iter, 1 strict, 2 tol, 3 needs relocation
+  int32_t iter;      // iteration the reason refers to
+  int32_t changed;   // labels changed in the current iteration
+  int32_t done;      // iterations completed (the convergence step's count)
+  int32_t pad[11];
+};
+static_assert(sizeof(LloydState) == 64, "LloydState is 64 bytes");
+
 // ---------------------------------------------------------------------------------------------
 // _average_centers + _center_shift
 // ---------------------------------------------------------------------------------------------
@@ -661,15 +674,19 @@ constexpr int kPwDepth = 24;  // n < 128 * 2^24
 // moment, i.e. averaged when argmax < j. Here the heaviest cluster's block writes every empty row
 // (from its raw and its averaged values) before averaging its own, so no block reads a row another
 // block is rescaling; empty blocks return at once. Shifts: sqrt(_euclidean_dense_dense).
+// check_st (the device loop, r04): the empty-cluster check of step 2i folded in — any empty
+// cluster stops the loop at this step (reason 3, what k_lloyd_check_empty recorded one launch
+// earlier) and no block writes; the host relocates and resumes without the check.
 __global__ __launch_bounds__(64) void k_avg_centers(int k, int dim, float* __restrict__ C_new,
                                                     const float* __restrict__ wsum,
                                                     const float* __restrict__ C_old,
                                                     float* __restrict__ shift, const int32_t* stop,
-                                                    int step_i) {
+                                                    int step_i, LloydState* check_st = nullptr,
+                                                    int it = 0) {
   if (stopped(stop, step_i)) return;
   const int c = blockIdx.x, lane = threadIdx.x;
   const float wc = wsum[c];
-  if (!(wc > 0.f)) return;
+  if (!(wc > 0.f) && !check_st) return;
   float bv = -1.f;
   int bi = INT_MAX, any_empty = 0;
   for (int j = lane; j < k; j += 64) {
@@ -690,6 +707,15 @@ __global__ __launch_bounds__(64) void k_avg_centers(int k, int dim, float* __res
     }
     any_empty |= __shfl_xor(any_empty, o);
   }
+  if (check_st && any_empty) {
+    if (c == 0 && lane == 0) {
+      check_st->reason = 3;
+      check_st->iter = it;
+      __hip_atomic_store(&check_st->stop_at, step_i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  if (!(wc > 0.f)) return;
   const float alpha = (float)(1.0 / (double)wc);  // `1.0 / weight` is a C double division
   const int64_t cb = (int64_t)c * dim;
   const bool donor = any_empty && bi == c;
@@ -717,17 +743,6 @@ __global__ __launch_bounds__(64) void k_avg_centers(int k, int dim, float* __res
 // ---------------------------------------------------------------------------------------------
 // the Lloyd loop's control words
 // ---------------------------------------------------------------------------------------------
-// Iteration i runs as two steps: 2i (E-step labels, grouping, sums, the empty-cluster check) and
-// 2i+1 (average + shift, labels changed, convergence). stop_at = s+1 skips every later step.
-struct LloydState {
-  int32_t stop_at;   // offset 0
-  int32_t reason;    // 0 running/max_iter, 1 strict, 2 tol, 3 needs relocation
-  int32_t iter;      // iteration the reason refers to
-  int32_t changed;   // labels changed in the current iteration
-  int32_t done;      // iterations completed (the convergence step's count)
-  int32_t pad[11];
-};
-static_assert(sizeof(LloydState) == 64, "LloydState is 64 bytes");
 
 __global__ void k_lloyd_changed(int64_t n, const int32_t* __restrict__ labels,
                                 int32_t* __restrict__ old, LloydState* st, int step_i) {
@@ -1446,10 +1461,8 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
       fa.step_i = sa;
       rc = fold_launch(fa, k, false, s);
       if (rc) return rc;
-      if (!small_update) {
-        k_lloyd_check_empty<<<1, 256, 0, s>>>(k, wsum, st, i, sa);
-        GDD_LAUNCHED();
-      }
+      // the empty-cluster check rides in the average's launch (check_st) unless the one-workgroup
+      // update (opt-in) does it
     }
     if (small_update) {  // the check (when the E-step ran), average, changed, convergence: one launch
       k_lloyd_update_small<<<1, kUpdThr, 0, s>>>(n, k, dim, cout, wsum, cin, shift, labels, labels_old, tol,
@@ -1457,7 +1470,7 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
       GDD_LAUNCHED();
       return GDD_OK;
     }
-    k_avg_centers<<<k, 64, 0, s>>>(k, dim, cout, wsum, cin, shift, &st->stop_at, sb);
+    k_avg_centers<<<k, 64, 0, s>>>(k, dim, cout, wsum, cin, shift, &st->stop_at, sb, phase_a ? st : nullptr, i);
     GDD_LAUNCHED();
     k_lloyd_changed<<<cgrid, 256, 0, s>>>(n, labels, labels_old, st, sb);
     GDD_LAUNCHED();

@@ -375,8 +375,9 @@ def test_kmeans_lloyd_sliced_fold_matches(monkeypatch, dim):
 @pytest.mark.parametrize("case", ["ml1m_users", "ml1m_items", "relocation", "tol0", "large_n"])
 def test_kmeans_lloyd_update_forms(monkeypatch, case):
     """The one-workgroup update (empty check, _average_centers + shifts, labels changed, convergence
-    test in one launch; opt-in GDD_LLOYD_UPDATE_SMALL for n <= 131,072 and k * dim <= 262,144) and
-    the four-launch update (default) give the same fit, bit for bit, and the oracle's: recsys shapes,
+    test in one launch; opt-in GDD_LLOYD_UPDATE_SMALL for n <= 131,072 and k * dim <= 262,144) and the
+    default update (the average with the empty check folded in, labels changed, the convergence test)
+    give the same fit, bit for bit, and the oracle's: recsys shapes,
     empty-cluster relocation (the resumed iteration's update runs without the check), a strict
     convergence run (tol = 0) and a shape above the one-workgroup limit (both forms the four launches)."""
     rng = np.random.default_rng(5)
@@ -395,17 +396,17 @@ def test_kmeans_lloyd_update_forms(monkeypatch, case):
         X, k = synth.blobs(140000, 8, 10, seed=14), 12
     X = np.ascontiguousarray(X, np.float32)
     fits = []
-    for small in (True, False):
-        if small:
-            monkeypatch.setenv("GDD_LLOYD_UPDATE_SMALL", "1")
-        else:
-            monkeypatch.delenv("GDD_LLOYD_UPDATE_SMALL", raising=False)
+    for env in ("GDD_LLOYD_UPDATE_SMALL", None):
+        monkeypatch.delenv("GDD_LLOYD_UPDATE_SMALL", raising=False)
+        if env:
+            monkeypatch.setenv(env, "1")
         np.random.seed(15)
         fits.append(gdd.KMeans(n_clusters=k, n_init=1, **kw).fit(X))
-    a, b = fits
-    assert a.n_iter_ == b.n_iter_ and a.inertia_ == b.inertia_
-    assert np.array_equal(a.labels_, b.labels_)
-    assert np.array_equal(bits(a.cluster_centers_), bits(b.cluster_centers_))
+    a = fits[1]
+    for b in (fits[0],):
+        assert a.n_iter_ == b.n_iter_ and a.inertia_ == b.inertia_
+        assert np.array_equal(a.labels_, b.labels_)
+        assert np.array_equal(bits(a.cluster_centers_), bits(b.cluster_centers_))
     if X.shape[0] * k <= 4_000_000:
         np.random.seed(15)
         ref = O.kmeans(X, k, n_init=1, **kw)
