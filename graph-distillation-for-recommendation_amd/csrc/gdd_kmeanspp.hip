@@ -1318,6 +1318,7 @@ struct Kpp1Args {
   int64_t* candself2[2];  // [T*T]
   int exact;             // cum_tol's mode
   int bsearch;           // 1: the folds' binary searches (GDD_KPP_BSEARCH, A/B); 0: two-ballot searches
+  int spec_search;       // the folds' speculative searches, T <= 7 (GDD_KPP_SPEC_SEARCH=0 turns them off)
 };
 
 __device__ __forceinline__ int kpp1_argmin(const float* __restrict__ pot, int T) {
@@ -1631,6 +1632,18 @@ __global__ __launch_bounds__(kThr) void k_kpp1_pick(Kpp1Args a, int c) {
 
 constexpr int kFPW = 22;     // prefix entries per thread of waves 1..3 in the fold (192 x 22 >= 4096)
 
+// waves 1-3 only (the fold's prefix waves): every calling wave's earlier LDS writes are visible to
+// the others once the count reaches target; false if the spin gave up (bounded)
+__device__ __forceinline__ bool prefix_waves_sync(int* ctr, int target) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (int it = 0; it < (1 << 16); ++it) {
+    if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+
 // the fold of round c's trial t by one 256-thread workgroup holding the trial's row in registers
 // (r[q] = entry tid + 256 q): the exact sgemv_t potential, the fp64 cumulative potential and the
 // candidates every trial would draw in round c+1 if t wins
@@ -1649,6 +1662,23 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
   const bool k4x2 = (T & 2) && t >= (T & ~3) && t < (T & ~3) + 2;
   const int h4 = k4x2 ? 0 : (m1 & 4);
   const bool perm = a.w == nullptr;
+  // speculative searches (r04, a.spec_search): while wave 0 runs the lane chains (~2 us of dependent
+  // adds), waves 1-3 finish the cumulative potential among themselves (an LDS arrival counter, not the
+  // workgroup barrier) and search every uniform with the fp64 total standing in for the potential.
+  // After the chains each result is checked against the exact potential (it is numpy's index when
+  // the exact threshold falls between the same two prefixes, neither within 4 cum_tol of it); any
+  // other case runs the regular search for that uniform.
+  __shared__ int s_sync;
+  __shared__ int s_sidx[kMaxTrials];
+  __shared__ int s_sok;
+  // measured (profiles/r04_kpp_spec_search.txt): faster at T = 6 (2708 x 7, k = 70: 9.68 vs 9.97 us
+  // per round) and T = 7 (3706 x 64, k = 371: 10.44 vs 11.33), slower at T = 8 (3000 x 40, k = 454:
+  // 8.58 vs 8.14 — the prefix waves' share no longer fits under the 375-add chains)
+  const bool spec = a.spec_search && !a.bsearch && c + 1 < a.k && T <= 7;
+  if (tid == 0) {
+    s_sync = 0;
+    s_sok = 1;
+  }
   {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -1720,11 +1750,64 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
     if (lane == 63) s_wave[wave - 1] = inc;
 #pragma unroll
     for (int q = 0; q < kFPW; ++q) pre[q] = ex + pre[q];
+    if (spec) {
+      bool ok = prefix_waves_sync(&s_sync, 3);
+      double B = 0.0;
+      for (int q = 0; q < wave - 1; ++q) B = B + s_wave[q];
+#pragma unroll
+      for (int q = 0; q < kFPW; ++q) {
+        const int e = kFPW * jp + q;
+        if (e < n) s_cum[e] = B + pre[q];
+      }
+      ok = prefix_waves_sync(&s_sync, 6) && ok;
+      const double pot_s = (double)(float)s_cum[n - 1];
+      // searchsorted_left(cum, u * pot_s) in two ballots (the regular search's form, no rounding check)
+      const int Bk = (n + 63) >> 6;
+      const int nb = (n + Bk - 1) / Bk;
+      const double cl = s_cum[min((lane + 1) * Bk, n) - 1];
+      for (int t2 = wave - 1; t2 < T; t2 += 3) {
+        const double rr = __shfl(ut, t2) * pot_s;
+        const int c0 = __popcll(__ballot(lane < nb && cl < rr));
+        int idx = n;
+        if (c0 < nb) {
+          const int e = c0 * Bk + lane;
+          const bool live = lane < Bk && e < n;
+          const double v = live ? s_cum[min(e, n - 1)] : 0.0;
+          idx = c0 * Bk + __popcll(__ballot(live && v < rr));
+        }
+        if (lane == 0) s_sidx[t2] = idx;
+      }
+      if (!ok && lane == 0) s_sok = 0;
+    }
   }
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 70);
+  unsigned long long redo = ~0ull;  // the uniforms the regular search below takes
+  if (spec) {
+    // the check, one lane per uniform; s_cum is complete (written before the barrier)
+    bool good = false;
+    if (tid < T && s_sok) {
+      const double rr = ut * (double)s_pot;
+      const double tol = cum_tol(a.exact, n, rr);
+      const int idx = s_sidx[tid];
+      const double lo = idx > 0 ? s_cum[idx - 1] : -1.0;
+      const double hi = idx < n ? s_cum[idx] : 0.0;
+      good = tol >= 0.0 && (idx == 0 || (lo < rr && fabs(lo - rr) > 4.0 * tol)) &&
+             (idx == n || (!(hi < rr) && fabs(hi - rr) > 4.0 * tol));
+      if (good) cand_out[tid] = min(n - 1, idx);
+    }
+    redo = __ballot(tid < T && !good);  // wave 0's lanes tid < T
+    __shared__ unsigned long long s_redo;
+    if (tid == 0) s_redo = redo;
+    __syncthreads();
+    redo = s_redo;
+    if (redo == 0ull) {
+      GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 74);
+      return;
+    }
+  }
   if (c + 1 < a.k) {
-    if (wave > 0) {
+    if (wave > 0 && !spec) {
       double B = 0.0;
       for (int q = 0; q < wave - 1; ++q) B = B + s_wave[q];
       const double pot = (double)s_pot;
@@ -1762,6 +1845,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
       const double cl = s_cum[min((lane + 1) * Bk, n) - 1];
       const double pot = (double)s_pot;
       for (int t2 = wave; t2 < T; t2 += (int)(blockDim.x >> 6)) {
+        if (!((redo >> t2) & 1ull)) continue;
         const double rr = __shfl(ut, t2) * pot;
         const double tol = cum_tol(a.exact, n, rr);
         const int c0 = __popcll(__ballot(lane < nb && cl < rr));
@@ -2710,6 +2794,10 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     b1.plan = a.plan;
     b1.exact = a.exact;
     b1.bsearch = getenv("GDD_KPP_BSEARCH") != nullptr ? 1 : 0;
+    {
+      const char* ss = getenv("GDD_KPP_SPEC_SEARCH");
+      b1.spec_search = (ss && ss[0] == '0') ? 0 : 1;
+    }
     if (seq) {
       k_kpp_xt<<<dim3((unsigned)((n + kXtTile - 1) / kXtTile), (unsigned)((dim + kXtTile - 1) / kXtTile)), 256, 0,
                s>>>((int)n, dim, X, XT);

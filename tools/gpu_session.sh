@@ -16,7 +16,7 @@
 #                         products, the default hop and the 4-slice form (GDD_HOP_LANES=8)
 #   phases                tools/phase_times.py (per-phase wall times of the bench step)
 #   kpp                   tools/micro_kpp.py (k-means++ round micro-benchmark)
-#   spec-ab               k-means++ pair launches with / without the speculative trip 3 (micro + bench, twice)
+#   spec-ab               k-means++ folds with / without the speculative searches (micro + bench, twice)
 #   lloyd-small           tools/micro_lloyd_small.py (recsys KMeans: one-workgroup update / grouping on and off)
 #   kpp-big               tools/micro_kpp.py big (one workgroup per trial vs per-block rounds) + in-kernel stamps
 #   inertia               tools/micro_inertia.py (parallel exact inertia vs the one-lane fold)
@@ -83,7 +83,7 @@ for step in "$@"; do
       done ;;
     phases) run 300 phases python tools/phase_times.py ;;
     kpp) run 300 kpp python tools/micro_kpp.py ;;
-    spec-ab) run 900 spec_ab bash -c 'python tools/micro_kpp.py spec && for v in 0 1 0 1; do echo "GDD_KPP_NO_SPEC=$v"; if [ $v = 1 ]; then export GDD_KPP_NO_SPEC=1; else unset GDD_KPP_NO_SPEC; fi; python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
+    spec-ab) run 900 spec_ab bash -c 'python tools/micro_kpp.py spec && for v in 1 0 1 0; do echo "GDD_KPP_SPEC_SEARCH=$v"; export GDD_KPP_SPEC_SEARCH=$v; python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
     lloyd-small) run 300 lloyd_small python tools/micro_lloyd_small.py ;;
     kpp-big) run 300 kpp_big bash -c 'python tools/micro_kpp.py big && python tools/stamps.py kpp-big' ;;
     inertia) run 300 inertia bash -c 'python tools/micro_inertia.py && GDD_INERTIA_SEQ=1 python tools/micro_inertia.py' ;;

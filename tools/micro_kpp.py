@@ -78,16 +78,14 @@ def ab_big():
 
 
 def ab_spec():
-    """The pair launches' speculative trip 3 (default) against reading the row after the exact draw
-    (GDD_KPP_NO_SPEC), same process, at the MiniBatchKMeans init shape and two others."""
-    for (n, dim, k) in [(3000, 40, 454), (3000, 41, 769), (3706, 64, 371)]:
-        for var in ("", "GDD_KPP_NO_SPEC", "", "GDD_KPP_NO_SPEC"):
-            if var:
-                os.environ[var] = "1"
-            print(f"variant {var or 'default'}:", end=" ", flush=True)
-            run(n, dim, k, 5, check=(var == ""))
-            if var:
-                del os.environ[var]
+    """The folds' speculative searches (default) against searching after the lane chains
+    (GDD_KPP_SPEC_SEARCH=0), same process, at the MiniBatchKMeans init shape and two others."""
+    for (n, dim, k) in [(3000, 40, 454), (3000, 41, 769), (3706, 64, 371), (2708, 7, 70)]:
+        for val in ("1", "0", "1", "0"):
+            os.environ["GDD_KPP_SPEC_SEARCH"] = val
+            print(f"variant GDD_KPP_SPEC_SEARCH={val}:", end=" ", flush=True)
+            run(n, dim, k, 5, check=(val == "1"))
+        del os.environ["GDD_KPP_SPEC_SEARCH"]
 
 
 if __name__ == "__main__":
