@@ -1674,7 +1674,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
   // measured (profiles/r04_kpp_spec_search.txt): faster at T = 6 (2708 x 7, k = 70: 9.68 vs 9.97 us
   // per round) and T = 7 (3706 x 64, k = 371: 10.44 vs 11.33), slower at T = 8 (3000 x 40, k = 454:
   // 8.58 vs 8.14 — the prefix waves' share no longer fits under the 375-add chains)
-  const bool spec = a.spec_search && !a.bsearch && c + 1 < a.k && T <= 7;
+  const bool spec = a.spec_search && !a.bsearch && c + 1 < a.k && T <= (a.spec_search == 2 ? 12 : 7);
   if (tid == 0) {
     s_sync = 0;
     s_sok = 1;
@@ -1731,6 +1731,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
       s_pot = y;
       if (pot_out) *pot_out = y;
     }
+    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 76);
   } else {  // the cumulative potential: thread runs and the wave's inclusive scan
     double run = 0.0;
 #pragma unroll
@@ -1750,6 +1751,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
     if (lane == 63) s_wave[wave - 1] = inc;
 #pragma unroll
     for (int q = 0; q < kFPW; ++q) pre[q] = ex + pre[q];
+    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 64 && t == 0 && c == a.k - 2), 75);
     if (spec) {
       bool ok = prefix_waves_sync(&s_sync, 3);
       double B = 0.0;
@@ -1778,6 +1780,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
         if (lane == 0) s_sidx[t2] = idx;
       }
       if (!ok && lane == 0) s_sok = 0;
+      GDD_STAMP_WHEN(g_stamps_kpp, (tid == 64 && t == 0 && c == a.k - 2), 77);
     }
   }
   __syncthreads();
@@ -2795,8 +2798,8 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     b1.exact = a.exact;
     b1.bsearch = getenv("GDD_KPP_BSEARCH") != nullptr ? 1 : 0;
     {
-      const char* ss = getenv("GDD_KPP_SPEC_SEARCH");
-      b1.spec_search = (ss && ss[0] == '0') ? 0 : 1;
+      const char* ss = getenv("GDD_KPP_SPEC_SEARCH");  // 0 off, 1 (default) T <= 7, 2 every T <= 12
+      b1.spec_search = (ss && ss[0] == '0') ? 0 : (ss && ss[0] == '2') ? 2 : 1;
     }
     if (seq) {
       k_kpp_xt<<<dim3((unsigned)((n + kXtTile - 1) / kXtTile), (unsigned)((dim + kXtTile - 1) / kXtTile)), 256, 0,

@@ -18,6 +18,7 @@
 #   kpp                   tools/micro_kpp.py (k-means++ round micro-benchmark)
 #   spec-ab               k-means++ folds with / without the speculative searches (micro + bench, twice)
 #   lloyd-small           tools/micro_lloyd_small.py (recsys KMeans: one-workgroup update / grouping on and off)
+#   stamps-kpp            tools/stamps.py (MiniBatch step + k-means++ pair launch stamps), speculative searches off / on
 #   kpp-big               tools/micro_kpp.py big (one workgroup per trial vs per-block rounds) + in-kernel stamps
 #   inertia               tools/micro_inertia.py (parallel exact inertia vs the one-lane fold)
 #   gap                   tools/probe/gap_probe (dependent launches: stream vs hipGraph replay)
@@ -85,6 +86,7 @@ for step in "$@"; do
     kpp) run 300 kpp python tools/micro_kpp.py ;;
     spec-ab) run 900 spec_ab bash -c 'python tools/micro_kpp.py spec && for v in 1 0 1 0; do echo "GDD_KPP_SPEC_SEARCH=$v"; export GDD_KPP_SPEC_SEARCH=$v; python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
     lloyd-small) run 300 lloyd_small python tools/micro_lloyd_small.py ;;
+    stamps-kpp) run 300 stamps_kpp bash -c 'GDD_KPP_SPEC_SEARCH=0 python tools/stamps.py && GDD_KPP_SPEC_SEARCH=2 python tools/stamps.py' ;;
     kpp-big) run 300 kpp_big bash -c 'python tools/micro_kpp.py big && python tools/stamps.py kpp-big' ;;
     inertia) run 300 inertia bash -c 'python tools/micro_inertia.py && GDD_INERTIA_SEQ=1 python tools/micro_inertia.py' ;;
     gap) run 60 gap ./tools/probe/gap_probe ;;

@@ -74,9 +74,11 @@ def main():
         show(f"reassign m={a[57]}", a, list(range(50, 57)), 50)
         t0 = p[60]
         lab = {60: "start", 61: "winners resolved", 62: "level-1 fold done", 63: "level-2 row in LDS",
-               70: "chains+prefix", 74: "search+table", 65: "next start"}
+               75: "wave-1 prefix done", 76: "wave-0 chains done", 77: "wave-1 speculative searches done",
+               70: "fold barrier", 74: "search+table", 65: "next start"}
         print("kpp pair launch (rounds k-3, k-2) (us): " + ", ".join(
-            f"{lab[q]} {(p[q] - t0) / 100:.2f}" for q in [60, 61, 62, 63, 70, 74, 65]))
+            f"{lab[q]} {(p[q] - t0) / 100:.2f}" for q in [60, 61, 62, 63, 75, 76, 77, 70, 74, 65]
+            if p[q] >= t0 and p[q] - t0 < 10 ** 6))
 
 
 if __name__ == "__main__":
