@@ -1464,18 +1464,24 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
     const float alpha = 1.0f / Wn;  // Cython `1 / weight_sums[c]` with float operands
     for (int f = lane; f < dim; f += 64) {
       float acc = C_old[cb + f] * W;
-      int t = 0;
-      for (; t + 4 <= count; t += 4) {  // four gathers in flight ahead of the ordered adds
-        float v[4], wi[4];
+      // up to 16 member gathers in flight ahead of the ordered adds (r04: the tail members were
+      // gathered one dependent load at a time, and most centres have fewer than four members);
+      // x * 1.0f == x, so unit weights skip the product
+      for (int t0 = 0; t0 < count; t0 += 16) {
+        const int m = min(16, count - t0);
+        float v[16];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          v[u] = X[src[t + u] * dim + f];
-          wi[u] = w ? w[mem[t + u]] : 1.0f;
+        for (int u = 0; u < 16; ++u) v[u] = u < m ? X[src[t0 + u] * dim + f] : 0.f;
+        if (w) {
+#pragma unroll
+          for (int u = 0; u < 16; ++u)
+            if (u < m) acc = acc + v[u] * w[mem[t0 + u]];
+        } else {
+#pragma unroll
+          for (int u = 0; u < 16; ++u)
+            if (u < m) acc = acc + v[u];
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc = acc + v[u] * wi[u];
       }
-      for (; t < count; ++t) acc = acc + X[src[t] * dim + f] * (w ? w[mem[t]] : 1.0f);
       const float v = acc * alpha;
       C_new[cb + f] = v;
       row_out[f] = v;

@@ -1318,7 +1318,7 @@ struct Kpp1Args {
   int64_t* candself2[2];  // [T*T]
   int exact;             // cum_tol's mode
   int bsearch;           // 1: the folds' binary searches (GDD_KPP_BSEARCH, A/B); 0: two-ballot searches
-  int spec_search;       // the folds' speculative searches, T <= 7 (GDD_KPP_SPEC_SEARCH=0 turns them off)
+  int spec_search;       // the folds' speculative searches, T <= 12 (GDD_KPP_SPEC_SEARCH=0 turns them off)
 };
 
 __device__ __forceinline__ int kpp1_argmin(const float* __restrict__ pot, int T) {
@@ -1671,10 +1671,10 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
   __shared__ int s_sync;
   __shared__ int s_sidx[kMaxTrials];
   __shared__ int s_sok;
-  // measured (profiles/r04_kpp_spec_search.txt): faster at T = 6 (2708 x 7, k = 70: 9.68 vs 9.97 us
-  // per round) and T = 7 (3706 x 64, k = 371: 10.44 vs 11.33), slower at T = 8 (3000 x 40, k = 454:
-  // 8.58 vs 8.14 — the prefix waves' share no longer fits under the 375-add chains)
-  const bool spec = a.spec_search && !a.bsearch && c + 1 < a.k && T <= (a.spec_search == 2 ? 12 : 7);
+  // measured (profiles/r04_kpp_spec_search.txt): T = 8 (3000 x 40, k = 454) 8.07 -> 7.44 us per round
+  // once the prefix reads are batched (before that the prefix alone took as long as the chains and the
+  // speculation lost); T = 7 (3706 x 64, k = 371) 11.33 -> 10.44, T = 6 (Cora) 9.97 -> 9.68
+  const bool spec = a.spec_search && !a.bsearch && c + 1 < a.k && T <= 12;
   if (tid == 0) {
     s_sync = 0;
     s_sok = 1;
@@ -1733,11 +1733,25 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
     }
     GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 76);
   } else {  // the cumulative potential: thread runs and the wave's inclusive scan
+    // every read issued before the run (a per-entry weight branch had each read waited on alone:
+    // ~2 us, as long as the chains, r04 stamps); entries past n add +0.0, as before
+    float xv[kFPW];
+#pragma unroll
+    for (int q = 0; q < kFPW; ++q) xv[q] = s_d[min(kFPW * jp + q, n - 1)];
+    if (a.w) {
+#pragma unroll
+      for (int q = 0; q < kFPW; ++q) {
+        const int e = kFPW * jp + q;
+        xv[q] = e < n ? a.w[min(e, n - 1)] * xv[q] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < kFPW; ++q) xv[q] = kFPW * jp + q < n ? xv[q] : 0.f;  // 1.0f * x == x
+    }
     double run = 0.0;
 #pragma unroll
     for (int q = 0; q < kFPW; ++q) {
-      const int e = kFPW * jp + q;
-      run = run + (e < n ? (double)(wv(a.w, e) * s_d[min(e, n - 1)]) : 0.0);
+      run = run + (double)xv[q];
       pre[q] = run;
     }
     double inc = run;
@@ -2798,8 +2812,8 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     b1.exact = a.exact;
     b1.bsearch = getenv("GDD_KPP_BSEARCH") != nullptr ? 1 : 0;
     {
-      const char* ss = getenv("GDD_KPP_SPEC_SEARCH");  // 0 off, 1 (default) T <= 7, 2 every T <= 12
-      b1.spec_search = (ss && ss[0] == '0') ? 0 : (ss && ss[0] == '2') ? 2 : 1;
+      const char* ss = getenv("GDD_KPP_SPEC_SEARCH");  // 0 off; default on for T <= 12
+      b1.spec_search = (ss && ss[0] == '0') ? 0 : 1;
     }
     if (seq) {
       k_kpp_xt<<<dim3((unsigned)((n + kXtTile - 1) / kXtTile), (unsigned)((dim + kXtTile - 1) / kXtTile)), 256, 0,

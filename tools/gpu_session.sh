@@ -86,7 +86,8 @@ for step in "$@"; do
     kpp) run 300 kpp python tools/micro_kpp.py ;;
     spec-ab) run 900 spec_ab bash -c 'python tools/micro_kpp.py spec && for v in 1 0 1 0; do echo "GDD_KPP_SPEC_SEARCH=$v"; export GDD_KPP_SPEC_SEARCH=$v; python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
     lloyd-small) run 300 lloyd_small python tools/micro_lloyd_small.py ;;
-    stamps-kpp) run 300 stamps_kpp bash -c 'GDD_KPP_SPEC_SEARCH=0 python tools/stamps.py && GDD_KPP_SPEC_SEARCH=2 python tools/stamps.py' ;;
+    stamps-kpp) run 300 stamps_kpp bash -c 'GDD_KPP_SPEC_SEARCH=0 python tools/stamps.py && GDD_KPP_SPEC_SEARCH=1 python tools/stamps.py' ;;
+    spec8-ab) run 600 spec8_ab bash -c 'for v in 0 1 0 1; do echo "GDD_KPP_SPEC_SEARCH=$v"; GDD_KPP_SPEC_SEARCH=$v python tools/micro_kpp.py one || exit 1; done; for v in 0 1 0 1; do echo "GDD_KPP_SPEC_SEARCH=$v"; GDD_KPP_SPEC_SEARCH=$v python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
     kpp-big) run 300 kpp_big bash -c 'python tools/micro_kpp.py big && python tools/stamps.py kpp-big' ;;
     inertia) run 300 inertia bash -c 'python tools/micro_inertia.py && GDD_INERTIA_SEQ=1 python tools/micro_inertia.py' ;;
     gap) run 60 gap ./tools/probe/gap_probe ;;

@@ -89,6 +89,9 @@ def ab_spec():
 
 
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["one"]:  # the MiniBatchKMeans init shape alone, parity checked
+        run(3000, 40, 454, 5)
+        sys.exit(0)
     if sys.argv[1:2] == ["spec"]:
         ab_spec()
         sys.exit(0)
