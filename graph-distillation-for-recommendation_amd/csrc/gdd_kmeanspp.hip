@@ -695,10 +695,13 @@ __global__ __launch_bounds__(kThr) void k_kpp_init(KppArgs a, SklPlan p1, int64_
   }
   __syncthreads();
   double v[kPer], pre[kPer];
+  float xs[kPer];  // every read before the weights' branches (r04)
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) xs[u] = s_d[kPer * tid + u];
 #pragma unroll
   for (int u = 0; u < kPer; ++u) {
     const int64_t e = j0 + kPer * tid + u;
-    v[u] = e < a.n ? (double)(wv(a.w, e) * s_d[kPer * tid + u]) : 0.0;
+    v[u] = e < a.n ? (double)(wv(a.w, e) * xs[u]) : 0.0;
   }
   block_prefix(v, pre, s_wave);
   const int64_t last = min<int64_t>(a.n, j0 + kBlk) - 1 - j0;
@@ -993,9 +996,11 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   if (jb != INT_MAX) {  // count inside block jb (uniform branch)
     double v[kPer], pre[kPer];
 #pragma unroll
+    for (int q = 0; q < kPer; ++q) v[q] = (double)wrow[min<int64_t>(e0 + q, n - 1)];  // reads first
+#pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const int64_t e = e0 + q;
-      v[q] = e < n ? (double)(wv(a.w, e) * wrow[e]) : 0.0;
+      v[q] = e < n ? (double)(wv(a.w, e) * (float)v[q]) : 0.0;
     }
     block_prefix(v, pre, s_wave);
     int cw = 0;
@@ -1110,10 +1115,13 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   // ---- the block's terms for round c+1: cumulative total, sgemv_t lane chains
   {
     double v[kPer], pre[kPer];
+    float xs[kPer];  // every read before the weights' branches (r04)
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) xs[q] = s_d[kPer * tid + q];
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const int64_t e = j0 + kPer * tid + q;
-      v[q] = e < n ? (double)(wv(a.w, e) * s_d[kPer * tid + q]) : 0.0;
+      v[q] = e < n ? (double)(wv(a.w, e) * xs[q]) : 0.0;
     }
     block_prefix(v, pre, s_wave);
     const int64_t last = min<int64_t>(n, j0 + kBlk) - 1 - j0;
@@ -1250,10 +1258,13 @@ __global__ __launch_bounds__(kThr) void k_kpp_dists(KppArgs a, int c) {
   __syncthreads();
   for (int t = 0; t < T; ++t) {  // the block's cumulative-potential total, per trial
     double v[kPer], pre[kPer];
+    float xs[kPer];  // every read before the weights' branches (r04)
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) xs[q] = s_d[t * kBlk + kPer * tid + q];
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const int64_t e = j0 + kPer * tid + q;
-      v[q] = e < n ? (double)(wv(a.w, e) * s_d[t * kBlk + kPer * tid + q]) : 0.0;
+      v[q] = e < n ? (double)(wv(a.w, e) * xs[q]) : 0.0;
     }
     block_prefix(v, pre, s_wave);
     const int64_t last = min<int64_t>(n, j0 + kBlk) - 1 - j0;
@@ -1551,10 +1562,13 @@ __global__ __launch_bounds__(kThr) void k_kpp1_pick(Kpp1Args a, int c) {
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 71);
   double v[kPer], pre[kPer];
+  float xs[kPer];  // every read before the weights' branches (r04)
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) xs[q] = s_d[kPer * tid + q];
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
     const int e = kPer * tid + q;
-    v[q] = e < n ? (double)(wv(a.w, e) * s_d[kPer * tid + q]) : 0.0;
+    v[q] = e < n ? (double)(wv(a.w, e) * xs[q]) : 0.0;
   }
   block_prefix(v, pre, s_wave);
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 72);
