@@ -1648,6 +1648,20 @@ constexpr int kFPW = 22;     // prefix entries per thread of waves 1..3 in the f
 
 // waves 1-3 only (the fold's prefix waves): every calling wave's earlier LDS writes are visible to
 // the others once the count reaches target; false if the spin gave up (bounded)
+// k_kpp1_big's speculative draws: every wave arrives (its earlier LDS writes then visible to a
+// waiting wave); waves_wait spins until target waves arrived, false if the spin gave up (bounded)
+__device__ __forceinline__ void waves_arrive(int* ctr) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool waves_wait(int* ctr, int target) {
+  for (int it = 0; it < (1 << 16); ++it) {
+    if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+
 __device__ __forceinline__ bool prefix_waves_sync(int* ctr, int target) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2370,17 +2384,25 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   __shared__ int s_part[kMaxTrials];
   __shared__ int s_amb[kMaxTrials];
   __shared__ double s_off[kBigThr], s_first[kBigThr], s_last[kBigThr];
+  __shared__ int s_arr;                 // speculative draws: waves that wrote their prefix data
+  __shared__ int s_sidx[kMaxTrials];    // speculative draws: counts (-1: not usable)
+  __shared__ unsigned long long s_redo;  // the uniforms the regular draws take
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = a.T;
   const int n = (int)a.n, m1 = (int)a.m1;
   const int t = blockIdx.x;
   const int cq = c & 1, pq = (c - 1) & 1;
+  const int nsg = (m1 + kBlk - 1) / kBlk;  // chain waves (4096-entry sgemv_t blocks)
+  // speculative draws (r04): waves nsg .. nsg + T - 1 draw round c+1's candidates while waves < nsg
+  // run the lane chains, the fp64 total standing in for the potential; checked after it (below)
+  const bool spec = a.spec_search && c >= 1 && c + 1 < a.k && nsg + T <= kBigWaves;
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 90);
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 1), 95);
   if (tid < kMaxTrials) {
     s_part[tid] = 0;
     s_amb[tid] = 0;
   }
+  if (tid == 0) s_arr = 0;
   // ---- trip 1, every load at once (lane q): round c-1's potential q, this slot's candidate if q
   // won, q's own candidate, round c+1's uniform q
   const double ut = (c + 1 < a.k && lane < T) ? a.uniforms[(int64_t)c * T + lane] : 0.0;
@@ -2461,12 +2483,70 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   double ex = __shfl_up(inc, 1);
   if (lane == 0) ex = 0.0;
   if (lane == 63) s_wt[wave] = inc;
+  if (spec) {  // until the barrier below s_off / s_last hold each segment's in-wave prefix and total
+    s_off[tid] = ex;
+    s_last[tid] = tot;
+    waves_arrive(&s_arr);
+  }
   // the sgemv_t block terms (rounds >= 1)
-  const int nsg = (m1 + kBlk - 1) / kBlk;
   if (c >= 1 && wave < nsg) {
     const int j0 = wave * kBlk;
     const float vb = sgemv_block_lds(s_row, a.w, j0, min(kBlk, m1 - j0), t, T);
     if (lane == 0) s_vb[wave] = vb;
+  } else if (spec && wave - nsg < T) {
+    // searchsorted_left(cum, u * pot_s), pot_s = fp32(fp64 total): the regular draw's segment
+    // counts without the rounding check, offsets from one running sum of the wave totals (within
+    // fp64 roundings of the regular ones: a count they change has a value within 4 cum_tol of the
+    // threshold, which the check after the potential refuses)
+    const int t2 = wave - nsg;
+    bool ok = waves_wait(&s_arr, kBigWaves);
+    double tall = 0.0;
+    for (int q = 0; q < kBigWaves; ++q) tall = tall + s_wt[q];
+    const double rr = readlane_f64(ut, t2) * (double)(float)tall;
+    int full = 0, wi = -1;
+    double wo = 0.0, W = 0.0;
+#pragma unroll
+    for (int i0 = 0; i0 < kBigWaves; i0 += 4) {
+      double exi[4], tti[4];
+      float v0[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = lane + 64 * (i0 + i);
+        exi[i] = s_off[j];
+        tti[i] = s_last[j];
+        v0[i] = s_row[EPT * j];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ej = EPT * (lane + 64 * (i0 + i));
+        const bool live = ej < n;
+        const float x0 = a.w ? (live ? a.w[ej] * v0[i] : 0.f) : v0[i];
+        const double oj = exi[i] + W;
+        const bool below = live && ej + EPT <= n && oj + tti[i] < rr;
+        full += __popcll(__ballot(below));
+        if (live && !below && oj + (double)x0 < rr) {  // may straddle the threshold: walked below
+          ok = ok && wi < 0;  // one per lane (the values only climb)
+          wi = i0 + i;
+          wo = oj;
+        }
+        W = W + s_wt[i0 + i];
+      }
+    }
+    int part = 0;
+    if (wi >= 0) {
+      const int ej = EPT * (lane + 64 * wi);
+      double run = wo;
+#pragma unroll 8
+      for (int q = 0; q < EPT; ++q) {
+        const float x = s_row[ej + q];
+        run = run + (double)(a.w ? (ej + q < n ? a.w[ej + q] * x : 0.f) : x);
+        if (ej + q < n) part += run < rr;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o);
+    ok = __ballot(!ok) == 0ull;
+    if (lane == 0) s_sidx[t2] = ok ? EPT * full + part : -1;
   }
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 93);
@@ -2494,10 +2574,65 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 96);
   if (c + 1 >= a.k) return;
+  unsigned long long redo = ~0ull;  // the uniforms the regular draws take
+  if (spec) {
+    // the check, one lane per uniform: the speculative count is numpy's index when the exact
+    // threshold falls between the same two cumulative values (the walk's, recomputed here), neither
+    // within 4 cum_tol of it (the fold's check)
+    bool good = false;
+    if (tid < T) {
+      const int idx = s_sidx[tid];
+      if (idx >= 0) {
+        const double rr = ut * (double)s_pot;
+        const double tol = cum_tol(a.exact, n, rr);
+        // the walk's cumulative values of entries idx - 1 and idx (one or two segments, each
+        // segment's reads issued before its run)
+        double lo = -1.0, hi = 0.0;
+        const int jl = idx > 0 ? (idx - 1) / EPT : -1, jh = idx < n ? idx / EPT : -1;
+        for (int pass = 0; pass < 2; ++pass) {
+          const int j = pass == 0 ? jl : jh;
+          if (j < 0 || (pass == 1 && j == jl)) continue;
+          const int ej = EPT * j;
+          float vs[EPT];
+#pragma unroll
+          for (int q = 0; q < EPT; q += 4) {
+            const float4 x = *reinterpret_cast<const float4*>(s_row + ej + q);
+            vs[q] = x.x;
+            vs[q + 1] = x.y;
+            vs[q + 2] = x.z;
+            vs[q + 3] = x.w;
+          }
+          if (a.w) {
+#pragma unroll
+            for (int q = 0; q < EPT; ++q) vs[q] = ej + q < n ? a.w[ej + q] * vs[q] : 0.f;
+          }
+          double run = s_off[j];
+#pragma unroll
+          for (int q = 0; q < EPT; ++q) {
+            run = run + (double)vs[q];
+            if (ej + q == idx - 1) lo = run;
+            if (ej + q == idx) hi = run;
+          }
+        }
+        good = tol >= 0.0 && (idx == 0 || (lo < rr && fabs(lo - rr) > 4.0 * tol)) &&
+               (idx == n || (!(hi < rr) && fabs(hi - rr) > 4.0 * tol));
+        if (good) a.candw[cq][(int64_t)t * T + tid] = min(n - 1, idx);
+      }
+    }
+    redo = __ballot(tid < T && !good);  // wave 0's lanes tid < T
+    if (tid == 0) s_redo = redo;
+    __syncthreads();
+    redo = s_redo;
+    if (redo == 0ull) {
+      GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 97);
+      GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 94);
+      return;
+    }
+  }
   // ---- draws for round c+1 if this trial wins: wave t2 takes uniform t2 over every segment (lane l:
   // segments l, l + 64, ...): whole segments below are counted by ballot, a segment that straddles
   // the threshold is walked by its lane — the owner's run, recomputed from LDS in the same order
-  if (wave < T) {
+  if (wave < T && ((redo >> wave) & 1ull)) {
     const int t2 = wave;
     const double pot = (double)s_pot;
     const double rr = readlane_f64(ut, t2) * pot;  // wave-uniform: a scalar read of lane t2
@@ -2553,7 +2688,7 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   }
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 97);
-  if (tid < T) {
+  if (tid < T && ((redo >> tid) & 1ull)) {
     int64_t cnt = (int64_t)s_cnt[0][tid] + s_part[tid];
     if (s_amb[tid]) cnt = np_cumsum_search(s_row, a.w, n, ut * (double)s_pot);  // lane tid holds u_tid
     a.candw[cq][(int64_t)t * T + tid] = min<int64_t>(n - 1, cnt);
@@ -2991,6 +3126,10 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       b1.indices = indices;
       b1.plan = a.plan;
       b1.exact = a.exact;
+      {
+        const char* ss = getenv("GDD_KPP_SPEC_SEARCH");  // 0 off (the regular draws)
+        b1.spec_search = (ss && ss[0] == '0') ? 0 : 1;
+      }
       void (*big)(Kpp1Args, const float*, int) = nullptr;
       int ept = 0;
       if (n <= (int64_t)kBigThr * 8) {

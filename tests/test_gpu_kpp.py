@@ -179,6 +179,7 @@ CUMSUM_FORMS = [
     (1000, ("GDD_KPP_NO_TABLE", "GDD_KPP_TWO_LAUNCH")), (1000, ("GDD_KPP_BSEARCH",)),
     (4096, ("GDD_KPP_SINGLE_ROUND", "GDD_KPP_BSEARCH")), (9000, ()), (9000, ("GDD_KPP_NO_BIG1",)),
     (20000, ()), (20000, ("GDD_KPP_BIG1_MAX=32768",)), (530000, ()),
+    (9000, ("GDD_KPP_SPEC_SEARCH=0",)),  # k_kpp1_big's regular draws (default: speculative + check)
 ]
 
 

@@ -88,6 +88,7 @@ for step in "$@"; do
     lloyd-small) run 300 lloyd_small python tools/micro_lloyd_small.py ;;
     stamps-kpp) run 300 stamps_kpp bash -c 'GDD_KPP_SPEC_SEARCH=0 python tools/stamps.py && GDD_KPP_SPEC_SEARCH=1 python tools/stamps.py' ;;
     spec8-ab) run 600 spec8_ab bash -c 'for v in 0 1 0 1; do echo "GDD_KPP_SPEC_SEARCH=$v"; GDD_KPP_SPEC_SEARCH=$v python tools/micro_kpp.py one || exit 1; done; for v in 0 1 0 1; do echo "GDD_KPP_SPEC_SEARCH=$v"; GDD_KPP_SPEC_SEARCH=$v python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
+    bigspec-ab) run 600 bigspec_ab bash -c 'for v in 0 1 0 1; do echo "GDD_KPP_SPEC_SEARCH=$v"; GDD_KPP_SPEC_SEARCH=$v python tools/micro_kpp.py big || exit 1; done && python tools/stamps.py kpp-big' ;;
     kpp-big) run 300 kpp_big bash -c 'python tools/micro_kpp.py big && python tools/stamps.py kpp-big' ;;
     inertia) run 300 inertia bash -c 'python tools/micro_inertia.py && GDD_INERTIA_SEQ=1 python tools/micro_inertia.py' ;;
     gap) run 60 gap ./tools/probe/gap_probe ;;
