@@ -2386,6 +2386,7 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   __shared__ double s_off[kBigThr], s_first[kBigThr], s_last[kBigThr];
   __shared__ int s_arr;                 // speculative draws: waves that wrote their prefix data
   __shared__ int s_sidx[kMaxTrials];    // speculative draws: counts (-1: not usable)
+  __shared__ double s_lo[kMaxTrials], s_hi[kMaxTrials];  // and their deciding neighbours
   __shared__ unsigned long long s_redo;  // the uniforms the regular draws take
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = a.T;
@@ -2494,59 +2495,99 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
     const float vb = sgemv_block_lds(s_row, a.w, j0, min(kBlk, m1 - j0), t, T);
     if (lane == 0) s_vb[wave] = vb;
   } else if (spec && wave - nsg < T) {
-    // searchsorted_left(cum, u * pot_s), pot_s = fp32(fp64 total): the regular draw's segment
-    // counts without the rounding check, offsets from one running sum of the wave totals (within
-    // fp64 roundings of the regular ones: a count they change has a value within 4 cum_tol of the
-    // threshold, which the check after the potential refuses)
+    // searchsorted_left(cum, u * pot_s), pot_s = fp32(fp64 total), without the rounding check (the
+    // check after the potential decides): the wave totals' running sum finds the group of 64
+    // segments (contiguous entries) holding the threshold, one ballot over that group's segment
+    // ends counts the segments below, the segment that straddles it is walked. Offsets are the
+    // group's running sum plus the in-wave prefix — within fp64 roundings of the regular ones: a
+    // count they change has a value within 4 cum_tol of the threshold, which the check refuses.
+    // One group per uniform keeps the LDS reads beside the chains small.
     const int t2 = wave - nsg;
     bool ok = waves_wait(&s_arr, kBigWaves);
     double tall = 0.0;
     for (int q = 0; q < kBigWaves; ++q) tall = tall + s_wt[q];
     const double rr = readlane_f64(ut, t2) * (double)(float)tall;
-    int full = 0, wi = -1;
-    double wo = 0.0, W = 0.0;
-#pragma unroll
-    for (int i0 = 0; i0 < kBigWaves; i0 += 4) {
-      double exi[4], tti[4];
-      float v0[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int j = lane + 64 * (i0 + i);
-        exi[i] = s_off[j];
-        tti[i] = s_last[j];
-        v0[i] = s_row[EPT * j];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ej = EPT * (lane + 64 * (i0 + i));
-        const bool live = ej < n;
-        const float x0 = a.w ? (live ? a.w[ej] * v0[i] : 0.f) : v0[i];
-        const double oj = exi[i] + W;
-        const bool below = live && ej + EPT <= n && oj + tti[i] < rr;
-        full += __popcll(__ballot(below));
-        if (live && !below && oj + (double)x0 < rr) {  // may straddle the threshold: walked below
-          ok = ok && wi < 0;  // one per lane (the values only climb)
-          wi = i0 + i;
-          wo = oj;
-        }
-        W = W + s_wt[i0 + i];
+    int g = 0;
+    double W = 0.0, Wg = 0.0;
+    for (int q = 0; q < kBigWaves; ++q) {
+      W = W + s_wt[q];
+      if (W < rr) {
+        g = q + 1;
+        Wg = W;
       }
     }
-    int part = 0;
-    if (wi >= 0) {
-      const int ej = EPT * (lane + 64 * wi);
-      double run = wo;
-#pragma unroll 8
-      for (int q = 0; q < EPT; ++q) {
-        const float x = s_row[ej + q];
-        run = run + (double)(a.w ? (ej + q < n ? a.w[ej + q] * x : 0.f) : x);
-        if (ej + q < n) part += run < rr;
+    int full = 0, part = 0;
+    if (g >= kBigWaves) {
+      full = n;  // every entry below (idx = n)
+    } else {
+      const int j = lane + 64 * g, ej = EPT * j;
+      const bool live = ej < n;
+      const double oj = s_off[j] + Wg;
+      const double tt = s_last[j];
+      float x0 = s_row[ej];
+      if (a.w) x0 = live ? a.w[ej] * x0 : 0.f;
+      const bool below = live && ej + EPT <= n && oj + tt < rr;
+      full = 64 * EPT * g + EPT * __popcll(__ballot(below));
+      if (live && !below && oj + (double)x0 < rr) {  // may straddle the threshold: walk it
+        float vs[EPT];
+#pragma unroll
+        for (int q = 0; q < EPT; q += 4) {
+          const float4 x = *reinterpret_cast<const float4*>(s_row + ej + q);
+          vs[q] = x.x;
+          vs[q + 1] = x.y;
+          vs[q + 2] = x.z;
+          vs[q + 3] = x.w;
+        }
+        if (a.w) {
+#pragma unroll
+          for (int q = 0; q < EPT; ++q) vs[q] = ej + q < n ? a.w[ej + q] * vs[q] : 0.f;
+        }
+        double run = oj;
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) {
+          run = run + (double)vs[q];
+          if (ej + q < n) part += run < rr;
+        }
       }
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o);
     ok = __ballot(!ok) == 0ull;
-    if (lane == 0) s_sidx[t2] = ok ? EPT * full + part : -1;
+    // the deciding neighbours for the check, independent of the potential: the walk's cumulative
+    // values of entries idx - 1 (lane 0) and idx (lane 1), with the regular offsets (in-wave prefix,
+    // then the wave totals in order) and each segment's reads issued before its run
+    const int idx = full + part;
+    double nv = lane == 0 ? -1.0 : 0.0;
+    const int e = idx - 1 + lane;
+    if (lane < 2 && e >= 0 && e < n) {
+      const int j = e / EPT, ej = EPT * j;
+      float vs[EPT];
+#pragma unroll
+      for (int q = 0; q < EPT; q += 4) {
+        const float4 x = *reinterpret_cast<const float4*>(s_row + ej + q);
+        vs[q] = x.x;
+        vs[q + 1] = x.y;
+        vs[q + 2] = x.z;
+        vs[q + 3] = x.w;
+      }
+      if (a.w) {
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) vs[q] = ej + q < n ? a.w[ej + q] * vs[q] : 0.f;
+      }
+      double run = s_off[j];  // ex of segment j until the barrier below
+      for (int q = 0; q < (j >> 6); ++q) run = run + s_wt[q];
+#pragma unroll
+      for (int q = 0; q < EPT; ++q) {
+        run = run + (double)vs[q];
+        if (ej + q == e) nv = run;
+      }
+    }
+    const double hi = __shfl(nv, 1);
+    if (lane == 0) {
+      s_sidx[t2] = ok ? idx : -1;
+      s_lo[t2] = nv;
+      s_hi[t2] = hi;
+    }
   }
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 93);
@@ -2555,79 +2596,66 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   s_off[tid] = off;
   s_first[tid] = off + (double)v[0];  // the segment's first cumulative value (as the walk's)
   s_last[tid] = off + tot;            // its last, to within EPT roundings (far inside cum_tol)
-  if (tid == 0) {
-    float y;
-    if (c == 0) {
-      y = a.st->pot;
-    } else {
-      y = 0.f;
+  unsigned long long redo = ~0ull;  // the uniforms the regular draws take
+  if (spec) {
+    // wave 0: the potential (every lane the same sums), then the check, one lane per uniform — the
+    // speculative count is numpy's index when the exact threshold falls between the same two
+    // cumulative values, neither within 4 cum_tol of it (the fold's check); one barrier
+    if (wave == 0) {
+      float y = 0.f;
       for (int b = 0; b < nsg; ++b) y = y + s_vb[b];
       if (m1 < n) {
         float sx = s_row[m1] * wv(a.w, m1);
         for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_row[o], wv(a.w, o), sx);
         y = y + sx;
       }
-      a.potv[cq][t] = y;
-    }
-    s_pot = y;
-  }
-  __syncthreads();
-  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 96);
-  if (c + 1 >= a.k) return;
-  unsigned long long redo = ~0ull;  // the uniforms the regular draws take
-  if (spec) {
-    // the check, one lane per uniform: the speculative count is numpy's index when the exact
-    // threshold falls between the same two cumulative values (the walk's, recomputed here), neither
-    // within 4 cum_tol of it (the fold's check)
-    bool good = false;
-    if (tid < T) {
-      const int idx = s_sidx[tid];
-      if (idx >= 0) {
-        const double rr = ut * (double)s_pot;
-        const double tol = cum_tol(a.exact, n, rr);
-        // the walk's cumulative values of entries idx - 1 and idx (one or two segments, each
-        // segment's reads issued before its run)
-        double lo = -1.0, hi = 0.0;
-        const int jl = idx > 0 ? (idx - 1) / EPT : -1, jh = idx < n ? idx / EPT : -1;
-        for (int pass = 0; pass < 2; ++pass) {
-          const int j = pass == 0 ? jl : jh;
-          if (j < 0 || (pass == 1 && j == jl)) continue;
-          const int ej = EPT * j;
-          float vs[EPT];
-#pragma unroll
-          for (int q = 0; q < EPT; q += 4) {
-            const float4 x = *reinterpret_cast<const float4*>(s_row + ej + q);
-            vs[q] = x.x;
-            vs[q + 1] = x.y;
-            vs[q + 2] = x.z;
-            vs[q + 3] = x.w;
-          }
-          if (a.w) {
-#pragma unroll
-            for (int q = 0; q < EPT; ++q) vs[q] = ej + q < n ? a.w[ej + q] * vs[q] : 0.f;
-          }
-          double run = s_off[j];
-#pragma unroll
-          for (int q = 0; q < EPT; ++q) {
-            run = run + (double)vs[q];
-            if (ej + q == idx - 1) lo = run;
-            if (ej + q == idx) hi = run;
-          }
-        }
-        good = tol >= 0.0 && (idx == 0 || (lo < rr && fabs(lo - rr) > 4.0 * tol)) &&
-               (idx == n || (!(hi < rr) && fabs(hi - rr) > 4.0 * tol));
-        if (good) a.candw[cq][(int64_t)t * T + tid] = min(n - 1, idx);
+      if (lane == 0) {
+        a.potv[cq][t] = y;
+        s_pot = y;
       }
+      bool good = false;
+      if (lane < T) {
+        const int idx = s_sidx[lane];
+        if (idx >= 0) {
+          const double rr = ut * (double)y;
+          const double tol = cum_tol(a.exact, n, rr);
+          const double lo = s_lo[lane], hi = s_hi[lane];
+          good = tol >= 0.0 && (idx == 0 || (lo < rr && fabs(lo - rr) > 4.0 * tol)) &&
+                 (idx == n || (!(hi < rr) && fabs(hi - rr) > 4.0 * tol));
+          if (good) a.candw[cq][(int64_t)t * T + lane] = min(n - 1, idx);
+        }
+      }
+      const unsigned long long r = __ballot(lane < T && !good);
+      if (lane == 0) s_redo = r;
     }
-    redo = __ballot(tid < T && !good);  // wave 0's lanes tid < T
-    if (tid == 0) s_redo = redo;
     __syncthreads();
+    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 96);
     redo = s_redo;
     if (redo == 0ull) {
       GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 97);
       GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 94);
       return;
     }
+  } else {
+    if (tid == 0) {
+      float y;
+      if (c == 0) {
+        y = a.st->pot;
+      } else {
+        y = 0.f;
+        for (int b = 0; b < nsg; ++b) y = y + s_vb[b];
+        if (m1 < n) {
+          float sx = s_row[m1] * wv(a.w, m1);
+          for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_row[o], wv(a.w, o), sx);
+          y = y + sx;
+        }
+        a.potv[cq][t] = y;
+      }
+      s_pot = y;
+    }
+    __syncthreads();
+    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 96);
+    if (c + 1 >= a.k) return;
   }
   // ---- draws for round c+1 if this trial wins: wave t2 takes uniform t2 over every segment (lane l:
   // segments l, l + 64, ...): whole segments below are counted by ballot, a segment that straddles
