@@ -1809,15 +1809,30 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
       const int Bk = (n + 63) >> 6;
       const int nb = (n + Bk - 1) / Bk;
       const double cl = s_cum[min((lane + 1) * Bk, n) - 1];
-      for (int t2 = wave - 1; t2 < T; t2 += 3) {
-        const double rr = __shfl(ut, t2) * pot_s;
-        const int c0 = __popcll(__ballot(lane < nb && cl < rr));
+      // this wave's uniforms (wave - 1, wave + 2, ... < T <= 12): every first ballot, then every
+      // second-level read issued together, then the second ballots
+      double rrs[4], vv[4];
+      int c0s[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t2 = wave - 1 + 3 * i;
+        rrs[i] = __shfl(ut, min(t2, T - 1)) * pot_s;
+        c0s[i] = __popcll(__ballot(lane < nb && cl < rrs[i]));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = c0s[i] * Bk + lane;
+        vv[i] = s_cum[min(e, n - 1)];  // c0s[i] == nb: unused
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t2 = wave - 1 + 3 * i;
+        if (t2 >= T) continue;
         int idx = n;
-        if (c0 < nb) {
-          const int e = c0 * Bk + lane;
+        if (c0s[i] < nb) {
+          const int e = c0s[i] * Bk + lane;
           const bool live = lane < Bk && e < n;
-          const double v = live ? s_cum[min(e, n - 1)] : 0.0;
-          idx = c0 * Bk + __popcll(__ballot(live && v < rr));
+          idx = c0s[i] * Bk + __popcll(__ballot(live && vv[i] < rrs[i]));
         }
         if (lane == 0) s_sidx[t2] = idx;
       }
