@@ -2608,9 +2608,11 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 93);
   double off = ex;
   for (int q = 0; q < wave; ++q) off = off + s_wt[q];
-  s_off[tid] = off;
-  s_first[tid] = off + (double)v[0];  // the segment's first cumulative value (as the walk's)
-  s_last[tid] = off + tot;            // its last, to within EPT roundings (far inside cum_tol)
+  if (!spec) {  // speculative draws: written only if some uniform takes the regular draws
+    s_off[tid] = off;
+    s_first[tid] = off + (double)v[0];  // the segment's first cumulative value (as the walk's)
+    s_last[tid] = off + tot;            // its last, to within EPT roundings (far inside cum_tol)
+  }
   unsigned long long redo = ~0ull;  // the uniforms the regular draws take
   if (spec) {
     // wave 0: the potential (every lane the same sums), then the check, one lane per uniform — the
@@ -2651,6 +2653,10 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
       GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 94);
       return;
     }
+    s_off[tid] = off;
+    s_first[tid] = off + (double)v[0];
+    s_last[tid] = off + tot;
+    __syncthreads();
   } else {
     if (tid == 0) {
       float y;
