@@ -76,7 +76,7 @@ size_t fit_ws(void* base, size_t cap, int64_t n, int dim, int k, int64_t bs, int
   Carver cv(base, cap);
   FitWs f;
   f.Xi = cv.take<float>((size_t)isz * dim);
-  f.kpp_bytes = gdd_kmeans_plusplus_ws_bytes(isz, dim, T);
+  f.kpp_bytes = gdd_kmeans_plusplus_ws_bytes_k(isz, dim, T, k);
   f.kpp_ws = cv.take<char>(f.kpp_bytes);
   f.step_bytes = gdd_minibatch_step_ws_bytes(bs, k);
   f.step_ws = cv.take<char>(f.step_bytes);

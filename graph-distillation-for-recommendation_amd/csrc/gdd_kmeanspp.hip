@@ -2840,10 +2840,14 @@ extern "C" int gdd_skl_sqdist(int n_rows, const float* C, int64_t n, int dim, co
 
 size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k);
 
-// k (centres) only sizes the fused rounds' arrival counters and gates the tables; the query bounds
-// it by n
+// k (centres) sizes the fused rounds' arrival counters and gates the tables. This query bounds it
+// by n (an upper bound for every k); gdd_kmeans_plusplus_ws_bytes_k sizes for the caller's k
 extern "C" size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int dim, int n_trials) {
   return kpp_ws_bytes(n, dim, n_trials, (int)std::min<int64_t>(n, INT_MAX));
+}
+
+extern "C" size_t gdd_kmeans_plusplus_ws_bytes_k(int64_t n, int dim, int n_trials, int k) {
+  return kpp_ws_bytes(n, dim, n_trials, std::max(1, k));
 }
 
 // the multi-block rounds read their distances from an n x n table when every distance is the plain
@@ -2858,10 +2862,23 @@ int64_t kpp_big1_max() {
   const int64_t v = e ? atoll(e) : 16384;
   return v < kBig1Max ? v : kBig1Max;
 }
+// the table costs n^2 dim fp64 fmas once (~0.45 ms at 6,040 x 64, i.e. ~5e12 fma/s) and saves each
+// of the k - 1 rounds its distance phase (>= ~5 us per round beyond 4096 points): build it only when
+// (k - 1) x 5 us covers n^2 dim / 5e12 s, i.e. (k - 1) 2.5e7 >= n^2 dim (k = 20 at
+// n = 32,768 would build a 4 GiB table for 19 rounds). ML-1M users (6,040 x 64, k = 604): 1.5e10 >=
+// 2.3e9; Ali-Display users (17,730 x 64, k = 1,773): 4.4e10 >= 2.0e10
+bool kpp_table_pays(int64_t n, int dim, int k) {
+  return (double)(k - 1) * 2.5e7 >= (double)n * (double)n * (double)std::max(dim, 1);
+}
 bool kpp_big_table(int64_t n, int dim, int T, int k) {
   if (n <= kBlk || n > kDmBigMax || dim > kDmX || T < 2 || k < kDmMinK) return false;
   if (getenv("GDD_KPP_NO_TABLE") != nullptr) return false;
+  if (!kpp_table_pays(n, dim, k) && getenv("GDD_KPP_FORCE_TABLE") == nullptr) return false;
   return skl_all_seq(n, T, dim, skl_batch_size(T, n, dim));
+}
+// the single-block table (n <= 4096, at most 64 MiB): built from kDmMinK centres on
+bool kpp_small_table(int64_t n, int dim, int T, int k) {
+  return n <= kBlk && dim <= kDmX && T >= 2 && k >= kDmMinK;
 }
 
 size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k) {
@@ -2886,7 +2903,7 @@ size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k) {
   if (n <= kBlk || (int64_t)n * std::max(dim, 1) < INT_MAX)
     b += align256(sizeof(float) * n * (size_t)std::max(dim, 1));  // XT
   if (kpp_big_table(n, dim, (int)T, k)) b += align256(sizeof(float) * n * n);  // multi-block table
-  if (n <= kBlk && dim <= kDmX && T >= 2) {
+  if (kpp_small_table(n, dim, (int)T, k)) {
     b += align256(sizeof(float) * n * n);  // distance table
     b += 2 * (align256(sizeof(float) * T * T * n) + align256(sizeof(float) * T * T) +
               align256(sizeof(int64_t) * T * T * T) + align256(sizeof(int64_t) * T * T));  // pair rounds
@@ -2932,7 +2949,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   b1.counter = cv.take<unsigned>((size_t)std::min<int64_t>(n, INT_MAX) * T);
   float* XT = (n <= kBlk || n * (int64_t)dim < INT_MAX) ? cv.take<float>((size_t)n * dim) : nullptr;
   float* Dbig = kpp_big_table(n, dim, T, k) ? cv.take<float>((size_t)n * n) : nullptr;
-  float* Dm = (n <= kBlk && dim <= kDmX && T >= 2) ? cv.take<float>((size_t)n * n) : nullptr;
+  float* Dm = kpp_small_table(n, dim, T, k) ? cv.take<float>((size_t)n * n) : nullptr;
   if (Dm) {
     for (int q = 0; q < 2; ++q) {
       b1.dist2[q] = cv.take<float>((size_t)T * T * n);

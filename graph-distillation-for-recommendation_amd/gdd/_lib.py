@@ -90,6 +90,7 @@ SIGNATURES = {
                                   ctypes.c_double, _vp, _c_int, _vp]),
     "gdd_skl_sqdist": (_c_int, [_c_int, _vp, _c_i64, _c_int, _vp, _vp, _vp]),
     "gdd_kmeans_plusplus_ws_bytes": (_c_size, [_c_i64, _c_int, _c_int]),
+    "gdd_kmeans_plusplus_ws_bytes_k": (_c_size, [_c_i64, _c_int, _c_int, _c_int]),
     "gdd_kmeans_plusplus": (_c_int, [_c_i64, _c_int, _vp, _vp, _c_int, _c_int, _c_i64, _vp, _vp,
                                      _vp, _vp, _c_size, _vp]),
     "gdd_standard_scaler": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),

@@ -222,6 +222,9 @@ class ClustGDD:
         t1, t_pc, t2 = self.distill()
         max_memory = torch.cuda.max_memory_allocated(self.device) \
             if torch.device(self.device).type == "cuda" else 0
+        # the printed stage times, also kept for callers (bench.py's e2e record)
+        self.times = {"pretraining_s": t_pc - t1, "refinement_s": t2 - t_pc, "total_s": t2 - t1,
+                      "max_memory_mb": max_memory / (1024 ** 2)}
         self.results = None
         if not getattr(self.args, "tm_rec", False):
             res = np.array([self.test_with_val(i) for i in range(5)])

@@ -182,12 +182,7 @@ def propagate(adj_norm: CSRGraph, features: torch.Tensor, T: int, alpha: float, 
     (ogbn-products, not ogbn-arxiv), the rows are partitioned over the ranks
     (:func:`gdd.sharded.sharded_propagate`, bit-identical); otherwise every rank propagates.
     """
-    if group is not None:
-        from .sharded import propagation_shards_pay, sharded_propagate, world_of
-        world = world_of(group)[1]
-        if world > 1 and propagation_shards_pay(adj_norm.n, adj_norm.nnz, features.shape[1], world):
-            return sharded_propagate(adj_norm, features.to(torch.float32).contiguous(), T, alpha,
-                                     group=group)
+    # the same input checks for both paths (ADVICE r4: the sharded dispatch used to come first)
     if T < 1:
         raise ValueError("prop_num must be >= 1 (the reference loop leaves target undefined)")
     X = features.contiguous()
@@ -198,6 +193,11 @@ def propagate(adj_norm: CSRGraph, features: torch.Tensor, T: int, alpha: float, 
     n, d = X.shape
     if n != adj_norm.n:
         raise ValueError(f"features have {n} rows, adjacency {adj_norm.n}")
+    if group is not None:
+        from .sharded import propagation_shards_pay, sharded_propagate, world_of
+        world = world_of(group)[1]
+        if world > 1 and propagation_shards_pay(adj_norm.n, adj_norm.nnz, d, world):
+            return sharded_propagate(adj_norm, X, T, alpha, group=group)
     lib, ws = _ws_propagate(adj_norm, d)
     target = torch.empty_like(X)
     p_last = torch.empty_like(X)

@@ -96,7 +96,7 @@ class _Ops:
         u_d = torch.from_numpy(u.astype(np.float64)).to(self.device)
         centers = torch.empty((k, self.dim), dtype=torch.float32, device=self.device)
         idx = torch.empty(k, dtype=torch.int64, device=self.device)
-        ws = _lib.workspace(self.lib.gdd_kmeans_plusplus_ws_bytes(n, self.dim, T), self.device)
+        ws = _lib.workspace(self.lib.gdd_kmeans_plusplus_ws_bytes_k(n, self.dim, T, k), self.device)
         _lib.check(self.lib.gdd_kmeans_plusplus(n, self.dim, Xi.data_ptr(), None, k, T, int(first),
                                                 u_d.data_ptr(), centers.data_ptr(), idx.data_ptr(),
                                                 ws.data_ptr(), ws.numel(), self.stream))

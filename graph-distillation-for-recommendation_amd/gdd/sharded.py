@@ -57,9 +57,10 @@ def shard_rows(n: int, rank: int, world: int):
     return a, b
 
 
-def all_gather_parts(t: torch.Tensor, m: int, n: int, group=None) -> torch.Tensor:
+def all_gather_parts(t: torch.Tensor, m: int, n: int, group=None, out: torch.Tensor = None) -> torch.Tensor:
     """Concatenate every rank's slice (rank r's first dim holds at most m rows) into the first n rows
-    of the whole, in rank order."""
+    of the whole, in rank order. ``out`` (optional, world * m rows, not aliasing ``t``) receives the
+    RCCL gather, so a loop can reuse one buffer instead of allocating a fresh one per call."""
     rank, world = world_of(group)
     if world == 1:
         return t[:n]
@@ -69,13 +70,18 @@ def all_gather_parts(t: torch.Tensor, m: int, n: int, group=None) -> torch.Tenso
         pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         pad[:t.shape[0]] = t
     if t.is_cuda and dist.get_backend(group) == "nccl":
-        out = torch.empty((world * m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if out is None:
+            out = torch.empty((world * m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out, pad, group=group)
         return out[:n]
     host = pad.cpu()
     parts = [torch.empty_like(host) for _ in range(world)]
     dist.all_gather(parts, host, group=group)
-    return torch.cat(parts, 0)[:n].to(t.device)
+    whole = torch.cat(parts, 0)
+    if out is not None:
+        out.copy_(whole)
+        return out[:n]
+    return whole[:n].to(t.device)
 
 
 def assemble_cols(parts: torch.Tensor, k: int, dim: int, fw: int, world: int) -> torch.Tensor:
@@ -97,7 +103,9 @@ def all_gather_slots(buf: torch.Tensor, m: int, group=None) -> None:
         return
     mine = buf[rank * m:(rank + 1) * m]
     if buf.is_cuda and dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(buf, mine, group=group)
+        # a copy of the own slot as the input: the in-place form (input a view into the
+        # output) is NCCL-legal but untested on hardware here; the copy is m elements
+        dist.all_gather_into_tensor(buf, mine.clone(), group=group)
         return
     host = mine.cpu()
     parts = [torch.empty_like(host) for _ in range(world)]
@@ -312,11 +320,18 @@ def sharded_propagate(adj_norm, X, T: int, alpha: float, group=None, ops=None):
                         adj_norm.values()[e0:e1], r1 - r0)
         plan = ops.rows_plan(rows, d)
     x = X.contiguous()
-    for _ in range(T - 1):
-        y = torch.empty((m, d), dtype=torch.float32, device=X.device)
+    # one hop-output slot and two gathered N x d buffers for the whole loop (a fresh slot
+    # and a fresh output per hop went through the caching allocator, ~1 GB per rank per hop at
+    # ogbn-products); hop h reads gathered buffer (h - 1) % 2 and its gather fills h % 2
+    # (one rank: the hop output is the next hop's input, so two slots alternate instead)
+    ys = [torch.empty((m, d), dtype=torch.float32, device=X.device) for _ in range(1 if world > 1 else 2)]
+    gathered = [torch.empty((world * m, d), dtype=torch.float32, device=X.device) for _ in range(2)] \
+        if world > 1 else [None, None]
+    for h in range(T - 1):
+        y = ys[h % len(ys)]
         if plan is not None:
             ops.rows_hop(plan, x, y[: r1 - r0], a32, target_loc[: r1 - r0], float(w32))
-        x = all_gather_parts(y, m, n, group)
+        x = all_gather_parts(y, m, n, group, out=gathered[h % 2])
     return all_gather_parts(target_loc, m, n, group), x
 
 

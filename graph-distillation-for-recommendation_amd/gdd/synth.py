@@ -62,6 +62,30 @@ def chung_lu(n: int, avg_degree: float, seed: int, gamma: float = 2.5) -> sp.csr
     return A
 
 
+def chung_lu_device(n: int, avg_degree: float, seed: int, device="cuda"):
+    """:func:`chung_lu`'s model (weights rank^-1/1.5, symmetric, binary, no self-loops) sampled and
+    canonicalised on the device with torch's generator — the host generator needs minutes at the
+    ogbn-products shape. Not the same draws as :func:`chung_lu`. Returns a gdd CSRGraph."""
+    import torch
+    from .graph import CSRGraph
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    w = torch.arange(1, n + 1, device=device, dtype=torch.float64) ** (-1.0 / 1.5)
+    w = w[torch.randperm(n, device=device, generator=g)].float()
+    m = int(round(n * avg_degree / 2.0 * 1.04))
+    src = torch.multinomial(w, m, replacement=True, generator=g)
+    dst = torch.multinomial(w, m, replacement=True, generator=g)
+    keep = src != dst
+    src, dst = src[keep], dst[keep]
+    keys = torch.unique(torch.cat([src * n + dst, dst * n + src]))
+    del src, dst, keep
+    rows, col = keys // n, (keys % n).to(torch.int32)
+    del keys
+    rowptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    rowptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n), 0)
+    return CSRGraph(rowptr.to(torch.int32), col, None, n)
+
+
 def uniform_graph(n: int, avg_degree: float, seed: int) -> sp.csr_matrix:
     """Erdős–Rényi-style symmetric binary graph (worst-case gather locality variant)."""
     rng = np.random.default_rng(seed)

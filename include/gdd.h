@@ -297,7 +297,10 @@ int gdd_lloyd_update(int64_t n, int dim, int k, const float* parts, int fw, floa
 /* in OpenBLAS's per-shape summation orders (gdd_skl_sqdist). Potentials: the first as sdot, the     */
 /* trials' as sgemv_t (_kmeans.py:239-251). Writes centers (k x dim) and indices. 1 <= n_trials <= 16. */
 /* ---------------------------------------------------------------------------------------------- */
-size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int dim, int n_trials);
+size_t gdd_kmeans_plusplus_ws_bytes(int64_t n, int dim, int n_trials);  /* bound for every k <= n */
+/* the workspace for this k: the n x n distance tables only where they are built (the multi-block  */
+/* table when (k - 1) 2.5e7 >= n^2 dim, i.e. when the rounds it saves cover its one-off build)      */
+size_t gdd_kmeans_plusplus_ws_bytes_k(int64_t n, int dim, int n_trials, int k);
 int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const float* w, int k, int n_trials,
                         int64_t first_id, const double* uniforms, float* centers, int64_t* indices,
                         void* ws, size_t ws_bytes, gdd_stream_t stream);

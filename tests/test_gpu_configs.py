@@ -174,25 +174,8 @@ def test_group_by_label_is_a_stable_sort(n, k):
 
 
 def _device_chung_lu(n, avg_degree, seed):
-    """A Chung-Lu power-law graph (synth.chung_lu's model: weights rank^-1/1.5, symmetric, binary,
-    no self-loops) sampled and canonicalised on the device — the host generator needs minutes at
-    the products shape. Returns a gdd CSRGraph."""
-    from gdd.graph import CSRGraph
-    g = torch.Generator(device="cuda")
-    g.manual_seed(seed)
-    w = torch.arange(1, n + 1, device="cuda", dtype=torch.float64) ** (-1.0 / 1.5)
-    w = w[torch.randperm(n, device="cuda", generator=g)].float()
-    m = int(round(n * avg_degree / 2.0 * 1.04))
-    src = torch.multinomial(w, m, replacement=True, generator=g)
-    dst = torch.multinomial(w, m, replacement=True, generator=g)
-    keep = src != dst
-    src, dst = src[keep], dst[keep]
-    keys = torch.unique(torch.cat([src * n + dst, dst * n + src]))
-    del src, dst, keep
-    rows, col = keys // n, (keys % n).to(torch.int32)
-    rowptr = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
-    rowptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n), 0)
-    return CSRGraph(rowptr.to(torch.int32), col, None, n)
+    """synth.chung_lu_device (the host generator needs minutes at the products shape)."""
+    return synth.chung_lu_device(n, avg_degree, seed)
 
 
 def test_products_shape_propagate_matches_oracle():

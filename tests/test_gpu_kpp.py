@@ -191,6 +191,7 @@ def test_kpp_cumsum_adversarial(monkeypatch, n, env, rnd):
     numpy's; with the check disabled (GDD_KPP_EXACT=0) it is not — so the case is adversarial for
     that form and the check is what makes it exact."""
     k, T = 16, 4
+    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")  # the multi-block table rounds at k = 16 too
     X = adversarial_points(n)
     u = adversarial_uniforms(k, T, rnd)
     c_ref, idx_ref = O.kmeans_plusplus_draws(X, k, T, 0, u)
@@ -212,6 +213,7 @@ def test_kpp_cumsum_adversarial(monkeypatch, n, env, rnd):
 def test_kpp_cumsum_adversarial_weighted(monkeypatch, n):
     """The same with sample weights (w * closest in fp32, then the fp64 sum)."""
     monkeypatch.setenv("GDD_KPP_BIG1_MAX", "32768")
+    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")
     k, T = 16, 4
     X = adversarial_points(n)
     w = np.ones(n, np.float32)
@@ -253,6 +255,7 @@ def test_kmeans_plusplus_big_rounds(monkeypatch, n, dim, k, oracle):
     X = synth.blobs(n, dim, max(2, k // 4), seed=n + dim + 3)
     X = np.ascontiguousarray(X - X.mean(axis=0), np.float32)
     monkeypatch.setenv("GDD_KPP_BIG1_MAX", "32768")  # the 32-entry segments too (default limit 16,384)
+    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")  # small k: the table is built although it does not pay
     ops = _Ops("cuda", n, k, dim)
     Xd = torch.from_numpy(X).cuda()
     c, idx = ops.kmeans_plusplus(Xd, k, np.random.RandomState(42))
@@ -270,6 +273,7 @@ def test_kmeans_plusplus_big_rounds_weighted_and_replayed(monkeypatch):
     """Sample weights (w * row in fp32 for the cumulative, the weighted sgemv_t lane chains) and
     every draw replayed (GDD_KPP_EXACT=2) on the one-workgroup-per-trial rounds."""
     n, dim, k, T = 9001, 24, 40, 5
+    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")
     X = np.ascontiguousarray(synth.blobs(n, dim, 10, seed=77), np.float32)
     w = np.random.default_rng(3).uniform(0.5, 2.0, n).astype(np.float32)
     u = np.random.RandomState(9).uniform(size=(k - 1) * T)
@@ -279,3 +283,22 @@ def test_kmeans_plusplus_big_rounds_weighted_and_replayed(monkeypatch):
         c, idx = _kpp_dev(X, k, T, 17, u, w=w)
         assert np.array_equal(idx, idx_ref), mode
         assert np.array_equal(bits(c), bits(c_ref)), mode
+
+
+@pytest.mark.parametrize("n,dim,k", [(16384, 64, 20), (32768, 16, 40)])
+def test_kmeans_plusplus_small_k_skips_the_table(monkeypatch, n, dim, k):
+    """with few centres the n x n table does not pay (its build costs more than the
+    rounds it saves), so neither the workspace nor the fit builds it; the per-block rounds give the
+    same seeding as the forced table rounds."""
+    lib = _lib.device_lib()
+    T = 2 + int(np.log(k))
+    assert lib.gdd_kmeans_plusplus_ws_bytes_k(n, dim, T, k) < 4 * n * n // 4
+    X = synth.blobs(n, dim, max(2, k // 4), seed=n + dim + 11)
+    X = np.ascontiguousarray(X - X.mean(axis=0), np.float32)
+    ops = _Ops("cuda", n, k, dim)
+    Xd = torch.from_numpy(X).cuda()
+    c, idx = ops.kmeans_plusplus(Xd, k, np.random.RandomState(5))
+    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")
+    c2, idx2 = ops.kmeans_plusplus(Xd, k, np.random.RandomState(5))
+    assert np.array_equal(idx.cpu().numpy(), idx2.cpu().numpy())
+    assert np.array_equal(bits(c.cpu().numpy()), bits(c2.cpu().numpy()))

@@ -78,3 +78,22 @@ def test_product_path_refuses_without_device(monkeypatch):
     monkeypatch.setattr(_lib, "_device_checked", False)
     with pytest.raises(RuntimeError):
         _lib.device_lib()
+
+
+def test_kmeans_plusplus_workspace_follows_k(lib):
+    """the k-aware query sizes the n x n tables only where they are built (host-only
+    arithmetic, no device call): ML-1M users' k builds the multi-block table, k = 20 at 32,768
+    points does not, and the k-free query stays the bound for every k."""
+    lib.gdd_kmeans_plusplus_ws_bytes_k.restype = ctypes.c_size_t
+    lib.gdd_kmeans_plusplus_ws_bytes_k.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.gdd_kmeans_plusplus_ws_bytes.restype = ctypes.c_size_t
+    lib.gdd_kmeans_plusplus_ws_bytes.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+    big = lib.gdd_kmeans_plusplus_ws_bytes_k(6040, 64, 8, 604)
+    assert big >= 4 * 6040 * 6040
+    small = lib.gdd_kmeans_plusplus_ws_bytes_k(32768, 64, 4, 20)
+    assert small < 4 * 32768 * 32768 // 16
+    assert lib.gdd_kmeans_plusplus_ws_bytes(32768, 64, 4) >= 4 * 32768 * 32768
+    assert lib.gdd_kmeans_plusplus_ws_bytes(6040, 64, 8) >= big
+    # the single-block table only from 16 centres
+    assert lib.gdd_kmeans_plusplus_ws_bytes_k(4000, 40, 3, 8) < 4 * 4000 * 4000
+    assert lib.gdd_kmeans_plusplus_ws_bytes_k(4000, 40, 4, 16) >= 4 * 4000 * 4000

@@ -63,18 +63,18 @@ for step in "$@"; do
     smoke) run 300 smoke python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run 600 bench python bench.py ${BENCH_ARGS} ;;
     trace) run 420 trace rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench \
-             -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+             -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra ;;
     pmc-hop)
       run 120 pmc_fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o hop -- python3 tools/micro_prop.py
       run 120 pmc_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o hop -- python3 tools/micro_prop.py
       run 120 pmc_hit rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_hit" -o hop -- python3 tools/micro_prop.py ;;
     pmc-bench)
-      B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
+      B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extra"
       run 240 pmcb_fetch env GDD_PROP_PAIR=0 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcb/pmc_fetch" -o bench -- $B
       run 240 pmcb_write env GDD_PROP_PAIR=0 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcb/pmc_write" -o bench -- $B
       run 240 pmcb_hit env GDD_PROP_PAIR=0 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmcb/pmc_hit" -o bench -- $B ;;
-    lookahead-ab) run 900 lookahead_ab bash -c 'for la in 1 2 3 1 2 3; do echo "lookahead $la"; GDD_MB_LOOKAHEAD=$la python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
-    chunk-ab) run 900 chunk_ab bash -c 'for c in 16 8 4 16 8 4; do for la in 1 2; do echo "chunk $c lookahead $la"; GDD_MB_CHUNK=$c GDD_MB_LOOKAHEAD=$la python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done; done' ;;
+    lookahead-ab) run 900 lookahead_ab bash -c 'for la in 1 2 3 1 2 3; do echo "lookahead $la"; GDD_MB_LOOKAHEAD=$la python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done' ;;
+    chunk-ab) run 900 chunk_ab bash -c 'for c in 16 8 4 16 8 4; do for la in 1 2; do echo "chunk $c lookahead $la"; GDD_MB_CHUNK=$c GDD_MB_LOOKAHEAD=$la python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done; done' ;;
     pmc-products)
       for form in default lanes8; do
         E="GDD_PROP_PAIR=0"; [ "$form" = lanes8 ] && E="GDD_PROP_PAIR=0 GDD_HOP_LANES=8"
@@ -84,10 +84,10 @@ for step in "$@"; do
       done ;;
     phases) run 300 phases python tools/phase_times.py ;;
     kpp) run 300 kpp python tools/micro_kpp.py ;;
-    spec-ab) run 900 spec_ab bash -c 'python tools/micro_kpp.py spec && for v in 1 0 1 0; do echo "GDD_KPP_SPEC_SEARCH=$v"; export GDD_KPP_SPEC_SEARCH=$v; python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
+    spec-ab) run 900 spec_ab bash -c 'python tools/micro_kpp.py spec && for v in 1 0 1 0; do echo "GDD_KPP_SPEC_SEARCH=$v"; export GDD_KPP_SPEC_SEARCH=$v; python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done' ;;
     lloyd-small) run 300 lloyd_small python tools/micro_lloyd_small.py ;;
     stamps-kpp) run 300 stamps_kpp bash -c 'GDD_KPP_SPEC_SEARCH=0 python tools/stamps.py && GDD_KPP_SPEC_SEARCH=1 python tools/stamps.py' ;;
-    spec8-ab) run 600 spec8_ab bash -c 'for v in 0 1 0 1; do echo "GDD_KPP_SPEC_SEARCH=$v"; GDD_KPP_SPEC_SEARCH=$v python tools/micro_kpp.py one || exit 1; done; for v in 0 1 0 1; do echo "GDD_KPP_SPEC_SEARCH=$v"; GDD_KPP_SPEC_SEARCH=$v python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
+    spec8-ab) run 600 spec8_ab bash -c 'for v in 0 1 0 1; do echo "GDD_KPP_SPEC_SEARCH=$v"; GDD_KPP_SPEC_SEARCH=$v python tools/micro_kpp.py one || exit 1; done; for v in 0 1 0 1; do echo "GDD_KPP_SPEC_SEARCH=$v"; GDD_KPP_SPEC_SEARCH=$v python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done' ;;
     bigspec-ab) run 600 bigspec_ab bash -c 'for v in 0 1 0 1; do echo "GDD_KPP_SPEC_SEARCH=$v"; GDD_KPP_SPEC_SEARCH=$v python tools/micro_kpp.py big || exit 1; done && python tools/stamps.py kpp-big' ;;
     kpp-big) run 300 kpp_big bash -c 'python tools/micro_kpp.py big && python tools/stamps.py kpp-big' ;;
     inertia) run 300 inertia bash -c 'python tools/micro_inertia.py && GDD_INERTIA_SEQ=1 python tools/micro_inertia.py' ;;
@@ -95,7 +95,7 @@ for step in "$@"; do
     graph-ab) run 300 graph_ab python tools/micro_graph.py ;;
     fold-cols) run 300 fold_cols python tools/micro_fold_cols.py ;;
     capture-probe) run 120 capture_probe python tools/probe_capture_h2d.py ;;
-    inertia-ab) run 600 inertia_ab bash -c 'for v in 0 1 0 1; do echo "GDD_INERTIA_SEQ=$v"; GDD_INERTIA_SEQ=$v python bench.py --no-cpu-baseline --steps 20 --warmup 3 || exit 1; done' ;;
+    inertia-ab) run 600 inertia_ab bash -c 'for v in 0 1 0 1; do echo "GDD_INERTIA_SEQ=$v"; GDD_INERTIA_SEQ=$v python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done' ;;
     kpp-products) run 300 kpp_products python tools/micro_kpp_products.py ;;
     assign) run 300 assign python tools/bench_assign.py ;;
     assign-ab) run 400 assign_ab bash -c 'python tools/bench_assign.py && GDD_ASSIGN_PERSIST=1 python tools/bench_assign.py && python tools/bench_assign.py' ;;
