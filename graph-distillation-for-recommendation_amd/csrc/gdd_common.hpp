@@ -128,10 +128,18 @@ struct MbFusedCall {
 };
 bool mb_fused_ok(int64_t b, int dim, int k);
 int mb_fused_launch(const MbFusedCall& c, const RngNext& rn, hipStream_t s);
+// the device reassignment (k_mb_reassign): any k whose swap table fits the LDS; a step with more
+// than b/2 centres due (np.argsort's branch) is handed to the host through MBState.handoff
+constexpr size_t kReassignLdsCap = 150 * 1024;
+size_t mb_reassign_lds(int64_t bs, int k);
+bool mb_reassign_ok(int64_t bs, int k);
 int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const float* X,
                        const int64_t* rows, float* C_new, float* counts, void* step_ws,
                        size_t step_ws_bytes, const DevMT* mt_in, DevMT* mt_mid, const RngNext& rn,
                        void* state, hipStream_t s);
+// minibatch_step_dev flag: the step has no tail for step_i - 1 (the first step of a device segment
+// resumed after host steps, whose convergence tests the host already ran)
+constexpr int kStepNoTail = 1 << 16;
 
 // internal entry point of the k-means assignment (gdd_kmeans.hip), used by the Lloyd loop
 // (gdd_lloyd.hip): ||C||² into cn2, then labels of all n rows; every kernel skips once `stop`

@@ -121,17 +121,24 @@ int dev_chunk() {
   return v;
 }
 
-int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n_steps,
-                int max_no_improvement, float reassignment_ratio, MTState* rng, const FitWs& w,
-                int32_t* h_flag /* pinned, >= 4 ints */, int64_t* stop_step, hipStream_t s) {
-  // the host RNG state after the initialisation draws becomes device slot 2 (= step -1)
+// Steps [i0, n_steps) on the device. rr_base: the last reassignment step (the next ones every
+// rr_period steps from it); norms_valid0: the workspace norms match step i0's centres. Returns the
+// convergence stop in *stop_step, or in *handoff_step a step whose reassignment needs the host (more
+// than b/2 centres due: np.argsort's branch) — that step's update has run, its tail and reassignment
+// have not, and the generator (written back to rng) is after its batch draws.
+int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t i0, int64_t rr_base,
+                bool norms_valid0, int64_t n_steps, int max_no_improvement, float reassignment_ratio,
+                MTState* rng, const FitWs& w, int32_t* h_flag /* pinned, >= 64 ints */,
+                int64_t* stop_step, int64_t* handoff_step, hipStream_t s) {
+  // the host RNG state (after the initialisation draws, or after the host's step i0 - 1) becomes
+  // the device slot of step i0 - 1
   static_assert(sizeof(DevMT) == 624 * 4 + 8, "DevMT layout");
   DevMT* h_mt = reinterpret_cast<DevMT*>(h_flag + 64);  // pinned scratch after the flags
   std::memcpy(h_mt->key, rng->key, sizeof(h_mt->key));
   h_mt->pos = rng->pos;
   h_mt->pad = 0;
-  GDD_HIP(hipMemcpyAsync(w.mtb + 2, h_mt, sizeof(DevMT), hipMemcpyHostToDevice, s));
-  int rc = mb_rng_launch(w.mtb + 2, w.mtb + 0, n, bs, w.rows_d, s);
+  GDD_HIP(hipMemcpyAsync(w.mtb + (i0 + 2) % 3, h_mt, sizeof(DevMT), hipMemcpyHostToDevice, s));
+  int rc = mb_rng_launch(w.mtb + (i0 + 2) % 3, w.mtb + i0 % 3, n, bs, w.rows_d + (i0 & 1) * bs, s);
   if (rc) return rc;
   rc = mb_loop_begin(bs, k, w.step_ws, w.step_bytes, s);
   if (rc) return rc;
@@ -160,7 +167,7 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n
   auto enqueue_chunk = [&](int64_t i0, int64_t m, hipStream_t cs) -> int {
     for (int64_t j = 0; j < m; ++j) {
       const int64_t st = i0 + j;
-      const bool do_rr = reassign && st % rr_period == 0;
+      const bool do_rr = reassign && st >= rr_base && (st - rr_base) % rr_period == 0;
       const bool has_next = st + 1 < n_steps;
       int64_t* rows_cur = w.rows_d + (st & 1) * bs;
       int64_t* rows_nxt = w.rows_d + ((st + 1) & 1) * bs;
@@ -170,7 +177,8 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n
       const RngNext next{mt_cur, mt_nxt, rows_nxt, n, bs};
       float* c_old = w.C[st % 2];
       float* c_new = w.C[(st + 1) % 2];
-      const int flags = GDD_STEP_CONVERGE | (st > 0 ? GDD_STEP_NORMS_VALID : 0);
+      const int flags = GDD_STEP_CONVERGE | ((st > i0 || norms_valid0) ? GDD_STEP_NORMS_VALID : 0) |
+                        ((st == i0 && i0 > 0) ? kStepNoTail : 0);
       int rc2 = minibatch_step_dev(bs, dim, X, rows_cur, k, c_old, c_new, w.counts, w.labels_b, (int)st,
                                    n, max_no_improvement, flags, w.state, w.step_ws, w.step_bytes,
                                    has_next ? next : none, cs);  // at reassignment steps: speculative
@@ -190,9 +198,9 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n
   };
   struct {
     const void* ptr[10];  // every buffer the launches touch
-    int64_t n, bs, n_steps, i0, m, dim, k, max_ni, step_bytes;
+    int64_t n, bs, n_steps, i0, m, dim, k, max_ni, step_bytes, seg0, rr_base;
     float ratio;
-    int pad;
+    int nv0;
   } key;
   std::memset(&key, 0, sizeof(key));
   const void* ptrs[10] = {X, w.rows_d, w.C[0], w.C[1], w.counts, w.labels_b, w.state, w.step_ws, w.mtb,
@@ -206,9 +214,13 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n
   key.k = k;
   key.max_ni = max_no_improvement;
   key.ratio = reassignment_ratio;
-  int64_t i = 0;
+  key.seg0 = i0;
+  key.rr_base = rr_base;
+  key.nv0 = norms_valid0 ? 1 : 0;
+  int64_t i = i0;
   int64_t chunk = 0;
   *stop_step = -1;
+  *handoff_step = -1;
   while (i < n_steps) {
     const int64_t m = std::min<int64_t>(dev_chunk(), n_steps - i);
     key.i0 = i;
@@ -228,11 +240,17 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n
     }
     ++chunk;
   }
-  GDD_HIP(hipMemcpyAsync(h_flag + 4, stop_word, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  // the whole state word block (stop_at at byte 16, handoff at byte 32)
+  GDD_HIP(hipMemcpyAsync(h_flag + 16, w.state, 48, hipMemcpyDeviceToHost, s));
   GDD_HIP(hipStreamSynchronize(s));
-  if (h_flag[4]) *stop_step = h_flag[4] - 1;
-  const int64_t last = *stop_step >= 0 ? *stop_step : n_steps - 1;
-  // the caller's RandomState ends where sklearn's does: after the draws of the last step
+  const int32_t stop_at = h_flag[16 + 4], handoff = h_flag[16 + 8];
+  if (handoff && handoff == stop_at)
+    *handoff_step = handoff - 1;
+  else if (stop_at)
+    *stop_step = stop_at - 1;
+  const int64_t last = *handoff_step >= 0 ? *handoff_step : (*stop_step >= 0 ? *stop_step : n_steps - 1);
+  // the caller's RandomState ends where sklearn's does: after the draws of the last step (at a
+  // handoff: after that step's batch draws, before its reassignment's)
   GDD_HIP(hipMemcpyAsync(h_mt, w.mtb + last % 3, sizeof(DevMT), hipMemcpyDeviceToHost, s));
   GDD_HIP(hipStreamSynchronize(s));
   std::memcpy(rng->key, h_mt->key, sizeof(h_mt->key));
@@ -495,26 +513,112 @@ extern "C" int gdd_minibatch_kmeans_fit(
   bool norms_valid = false;
   int64_t n_since = 0;
   int64_t i = 0, stop_step = -1;
-  // Device-resident loop: when k <= b/2 at most b/2 centres can be due for reassignment, so the
-  // argsort branch never runs and, after step 0, no weight sum is ever zero — the reassignment
-  // steps are then known in advance (every ceil(10k/b) steps) and the whole loop, draws included,
-  // runs on the device with one host round trip per chunk of steps (overlapped with the next).
-  const bool dev_loop = 2 * (int64_t)k <= bs && n_steps > 0 && getenv("GDD_HOST_LOOP") == nullptr;
-  // GDD_MB_FUSED=1: one launch per step (k_mb_fused, measured slower at the arxiv shape: every
-  // point block redoes its centre group's update); default: the two-launch loop
-  const char* fused_e = getenv("GDD_MB_FUSED");
-  const bool fused_env = fused_e && fused_e[0] == '1';
-  if (dev_loop) {
-    const bool fused = fused_env && mb_fused_ok(bs, dim, k);
-    int rc = (fused ? device_loop_fused : device_loop)(
-        n, dim, X, k, bs, n_steps, max_no_improvement, reassignment_ratio,
-        static_cast<MTState*>(rng_state), w, h_flag, &stop_step, s);
-    if (rc) return rc;
-    i = n_steps;  // skip the host loop below
-  }
   std::vector<float> W(k);
   std::vector<int64_t> order;
+  // _mini_batch_step's reassignment branch (:1640-1667) on the host, numpy float32 semantics, after
+  // the step's update (h_counts = its weight sums, read back by the caller): the argsort branch when
+  // more than b/2 centres are due, the permutation draws, the row copies, the weight-sum reset
+  auto host_reassign = [&](const int64_t* rows, float* c_new) -> int {
+    float wmax = h_counts[0];
+    for (int c = 1; c < k; ++c) wmax = std::max(wmax, h_counts[c]);
+    const float thr = (float)reassignment_ratio * wmax;
+    std::vector<char> to(k);
+    int64_t cnt = 0;
+    for (int c = 0; c < k; ++c) {
+      to[c] = h_counts[c] < thr;
+      cnt += to[c];
+    }
+    if ((double)cnt > 0.5 * (double)bs) {
+      if (!argsort_cb) return fail(GDD_E_INVALID, "mbk_fit: argsort callback required (k > b/2)");
+      order.assign(k, 0);
+      argsort_cb(h_counts, k, order.data());  // np.argsort(weight_sums) (quicksort order)
+      for (int64_t q = (int64_t)(0.5 * (double)bs); q < k; ++q) to[order[q]] = 0;
+      cnt = 0;
+      for (int c = 0; c < k; ++c) cnt += to[c];
+    }
+    if (cnt) {
+      std::vector<int64_t> perm = rng.permutation(bs);  // choice(bs, replace=False, size=cnt)
+      int64_t q = 0;
+      for (int c = 0; c < k; ++c)
+        if (to[c]) {
+          h_pairs[2 * q] = c;
+          h_pairs[2 * q + 1] = perm[q];
+          ++q;
+        }
+      GDD_HIP(hipMemcpyAsync(w.pairs, h_pairs, sizeof(int64_t) * 2 * cnt, hipMemcpyHostToDevice, s));
+      k_reassign_rows<<<(unsigned)cnt, 64, 0, s>>>((int)cnt, dim, X, rows, w.pairs, c_new);
+      GDD_LAUNCHED();
+      norms_valid = false;  // reassigned rows: the next step recomputes the norms
+    }
+    float mn = 0.f;
+    bool first_min = true;
+    for (int c = 0; c < k; ++c)
+      if (!to[c] && (first_min || h_counts[c] < mn)) {
+        mn = h_counts[c];
+        first_min = false;
+      }
+    bool zero = false;
+    for (int c = 0; c < k; ++c) {
+      if (to[c]) h_counts[c] = mn;
+      zero |= h_counts[c] == 0.f;
+    }
+    any_zero = zero;
+    GDD_HIP(hipMemcpyAsync(w.counts, h_counts, sizeof(float) * k, hipMemcpyHostToDevice, s));
+    return GDD_OK;
+  };
+  // Device-resident loop (any k whose reassignment swap table fits the LDS): the batch draws, the
+  // scheduled reassignments and the convergence test run on the device with one host round trip
+  // per chunk of steps (overlapped with the next chunk). A reassignment leaves no empty cluster
+  // unless more than b/2 centres are due (then np.argsort decides which stay), so the reassignment
+  // steps are periodic (every ceil(10k/b) steps from the last one) as long as that branch does not
+  // fire — always when k <= b/2. When it fires (k > b/2 only), the device stops at that step and
+  // hands it to the host (host_reassign); the host then runs steps while some weight sum is zero
+  // (sklearn reassigns at every such step) and resumes the device loop once none is.
+  const bool dev_ok = n_steps > 0 && getenv("GDD_HOST_LOOP") == nullptr && mb_reassign_ok(bs, k);
+  // GDD_MB_FUSED=1: one launch per step (k_mb_fused, measured slower at the arxiv shape: every
+  // point block redoes its centre group's update); k <= b/2 only; default: the
+  // two-launch loop
+  const char* fused_e = getenv("GDD_MB_FUSED");
+  const bool fused_env = fused_e && fused_e[0] == '1';
+  if (dev_ok && fused_env && 2 * (int64_t)k <= bs && mb_fused_ok(bs, dim, k)) {
+    int rc = device_loop_fused(n, dim, X, k, bs, n_steps, max_no_improvement, reassignment_ratio,
+                               static_cast<MTState*>(rng_state), w, h_flag, &stop_step, s);
+    if (rc) return rc;
+    i = n_steps;  // skip the loops below
+  }
+  bool use_dev = dev_ok;
+  int64_t rr_base = 0;
   while (i < n_steps && stop_step < 0) {
+    if (use_dev) {
+      int64_t handoff = -1;
+      int rc = device_loop(n, dim, X, k, bs, i, rr_base, norms_valid, n_steps, max_no_improvement,
+                           reassignment_ratio, static_cast<MTState*>(rng_state), w, h_flag, &stop_step,
+                           &handoff, s);
+      if (rc) return rc;
+      if (handoff < 0) break;  // ran to the end or stopped
+      // step `handoff`: its update ran on the device; its convergence test (the tail the next
+      // launch would have run) and its reassignment run here, in sklearn's order of effects
+      const int64_t h = handoff;
+      GDD_HIP(hipMemsetAsync(static_cast<char*>(w.state) + 16, 0, sizeof(int32_t), s));  // stop_at
+      GDD_HIP(hipMemsetAsync(static_cast<char*>(w.state) + 32, 0, sizeof(int32_t), s));  // handoff
+      rc = mb_loop_end(bs, k, (int)h, n, max_no_improvement, w.state, w.step_ws, w.step_bytes, s);
+      if (rc) return rc;
+      GDD_HIP(hipMemcpyAsync(h_flag, static_cast<char*>(w.state) + 16, sizeof(int32_t),
+                             hipMemcpyDeviceToHost, s));
+      GDD_HIP(hipMemcpyAsync(h_counts, w.counts, sizeof(float) * k, hipMemcpyDeviceToHost, s));
+      GDD_HIP(hipStreamSynchronize(s));
+      const int32_t stop_at = h_flag[0];
+      norms_valid = true;  // the device update left ||C_new||^2 behind
+      rc = host_reassign(w.rows_d + (h & 1) * bs, w.C[(h + 1) % 2]);
+      if (rc) return rc;
+      GDD_HIP(hipStreamSynchronize(s));  // the pinned staging's H2D copies are done
+      if (stop_at) stop_step = stop_at - 1;  // converged at h (after its reassignment, as sklearn)
+      i = h + 1;
+      n_since = 0;
+      rr_base = h;
+      use_dev = !any_zero;
+      continue;
+    }
     const MTState snapshot = *static_cast<MTState*>(rng_state);
     std::vector<char> chunk_rr;
     while (i + (int64_t)chunk_rr.size() < n_steps && (int)chunk_rr.size() < kChunkCap) {
@@ -530,7 +634,7 @@ extern "C" int gdd_minibatch_kmeans_fit(
     // sync at the end of every chunk guarantees it
     GDD_HIP(hipMemcpyAsync(w.rows_d, h_rows, sizeof(int64_t) * (size_t)m * bs, hipMemcpyHostToDevice,
                            s));
-    bool synced = false;
+    bool resume_dev = false;
     for (int j = 0; j < m; ++j) {
       const int64_t st = i + j;
       float* c_old = w.C[st % 2];
@@ -547,60 +651,19 @@ extern "C" int gdd_minibatch_kmeans_fit(
                                hipMemcpyDeviceToHost, s));
         GDD_HIP(hipMemcpyAsync(h_counts, w.counts, sizeof(float) * k, hipMemcpyDeviceToHost, s));
         GDD_HIP(hipStreamSynchronize(s));
-        synced = true;
         const int32_t stop_at = h_flag[0];
         if (stop_at && stop_at - 1 < st) {  // stopped earlier in this chunk: step st never ran
           stop_step = stop_at - 1;
           break;
         }
-        // _mini_batch_step reassignment (:1640-1667), numpy float32 semantics
-        float wmax = h_counts[0];
-        for (int c = 1; c < k; ++c) wmax = std::max(wmax, h_counts[c]);
-        const float thr = (float)reassignment_ratio * wmax;
-        std::vector<char> to(k);
-        int64_t cnt = 0;
-        for (int c = 0; c < k; ++c) {
-          to[c] = h_counts[c] < thr;
-          cnt += to[c];
-        }
-        if ((double)cnt > 0.5 * (double)bs) {
-          if (!argsort_cb) return fail(GDD_E_INVALID, "mbk_fit: argsort callback required (k > b/2)");
-          order.assign(k, 0);
-          argsort_cb(h_counts, k, order.data());  // np.argsort(weight_sums) (quicksort order)
-          for (int64_t q = (int64_t)(0.5 * (double)bs); q < k; ++q) to[order[q]] = 0;
-          cnt = 0;
-          for (int c = 0; c < k; ++c) cnt += to[c];
-        }
-        if (cnt) {
-          std::vector<int64_t> perm = rng.permutation(bs);  // choice(bs, replace=False, size=cnt)
-          int64_t q = 0;
-          for (int c = 0; c < k; ++c)
-            if (to[c]) {
-              h_pairs[2 * q] = c;
-              h_pairs[2 * q + 1] = perm[q];
-              ++q;
-            }
-          GDD_HIP(hipMemcpyAsync(w.pairs, h_pairs, sizeof(int64_t) * 2 * cnt, hipMemcpyHostToDevice,
-                                 s));
-          k_reassign_rows<<<(unsigned)cnt, 64, 0, s>>>((int)cnt, dim, X, rows, w.pairs, c_new);
-          GDD_LAUNCHED();
-          norms_valid = false;  // reassigned rows: the next step recomputes the norms
-        }
-        float mn = 0.f;
-        bool first_min = true;
-        for (int c = 0; c < k; ++c)
-          if (!to[c] && (first_min || h_counts[c] < mn)) {
-            mn = h_counts[c];
-            first_min = false;
-          }
-        bool zero = false;
-        for (int c = 0; c < k; ++c) {
-          if (to[c]) h_counts[c] = mn;
-          zero |= h_counts[c] == 0.f;
-        }
-        any_zero = zero;
-        GDD_HIP(hipMemcpyAsync(w.counts, h_counts, sizeof(float) * k, hipMemcpyHostToDevice, s));
+        rc = host_reassign(rows, c_new);
+        if (rc) return rc;
         if (stop_at) stop_step = stop_at - 1;
+        // no weight sum left at zero: the next reassignments are periodic again (device loop)
+        if (stop_at == 0 && !any_zero && dev_ok) {
+          resume_dev = true;
+          rr_base = st;
+        }
       }
     }
     if (stop_step < 0) {
@@ -613,13 +676,13 @@ extern "C" int gdd_minibatch_kmeans_fit(
       // (h_pairs, h_counts) are still queued, and that buffer may be reused once we return
       GDD_HIP(hipStreamSynchronize(s));
     }
-    (void)synced;
     if (stop_step >= 0 && stop_step < i + m - 1) {
       // sklearn drew batch indices only up to the stopping step: rewind the generator
       *static_cast<MTState*>(rng_state) = snapshot;
       for (int64_t q = i; q <= stop_step; ++q) rng.randint(0, n, bs, h_rows);
     }
     i += m;
+    use_dev = resume_dev && stop_step < 0;
   }
   const int64_t last = stop_step >= 0 ? stop_step : n_steps - 1;
   *n_steps_out = last + 1;

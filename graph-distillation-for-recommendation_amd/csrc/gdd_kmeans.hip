@@ -1166,7 +1166,8 @@ struct MBState {
   double ewa, ewa_min;
   int32_t stop_at;       // offset 16: 0 while running, s+1 once the test fired at step s
   int32_t has_ewa, has_min, no_improvement;
-  int32_t pad[4];
+  int32_t handoff;       // offset 32: s+1 once step s's reassignment needs the host (np.argsort branch)
+  int32_t pad[3];
 };
 
 // one thread; st->stop_at is published with an agent-scope atomic store (read by sibling blocks).
@@ -2510,7 +2511,7 @@ int gdd::minibatch_step_dev(int64_t b, int dim, const float* X, const int64_t* r
   const int cur = step_i & 1, prev = cur ^ 1;
   const float* cn2 = (flags & GDD_STEP_NORMS_VALID) ? w.cn2 : nullptr;
   const MbTail tl{w.sq[prev], w.inertia, st, b, n_samples, max_no_improvement, step_i - 1,
-                  (flags & GDD_STEP_CONVERGE) ? 1 : 0, step_i > 0 ? 1 : 0};
+                  (flags & GDD_STEP_CONVERGE) ? 1 : 0, (step_i > 0 && !(flags & kStepNoTail)) ? 1 : 0};
   int rc = launch_mb_assign(b, dim, X, rows, k, C_old, cn2, w.keys[cur], stop, step_i, tl, rn, s);
   if (rc) return rc;
   return launch_update(b, dim, X, rows, nullptr, nullptr, w.keys[cur], k, C_old, C_new,
@@ -2656,12 +2657,16 @@ __global__ __launch_bounds__(1024) void k_mb_rng(const DevMT* __restrict__ in, D
 // the last step); with rn.rows the workgroup then draws the next step's batch.
 // Wave 0 does the serial parts without block barriers (the count statistics, then the shuffle's
 // draws); all waves then trace permutation(b)[r] for r < m (one wave per r) and copy the rows.
-// Requires m <= b/2 (true whenever k <= b/2; the host keeps other shapes on its own loop).
+// m > b/2 (possible only when k > b/2) needs np.argsort's order of the weight sums (numpy's
+// introsort: its tie order is numpy's own): the workgroup then changes nothing, records the step in
+// st->handoff and stops the loop there (stop_at = step + 1, so every later launch no-ops); the host
+// runs this step's convergence test and reassignment and resumes (gdd_fit.hip).
 __global__ __launch_bounds__(1024) void k_mb_reassign(
     int step, int64_t bs, int dim, int k, float ratio, const float* __restrict__ X,
     const int64_t* __restrict__ rows, float* __restrict__ C_new, float* __restrict__ counts,
     float* __restrict__ cn2, const DevMT* __restrict__ mt_in, DevMT* __restrict__ mt_mid,
-    RngNext rn, const int32_t* __restrict__ stop) {
+    RngNext rn, MBState* __restrict__ mbs) {
+  int32_t* stop = &mbs->stop_at;
   if (stopped(stop, step)) return;
 #ifdef GDD_STAMPS
   unsigned long long tl[7] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0};
@@ -2720,6 +2725,13 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
   __syncthreads();
   const int m = s_m;
   const float thr = s_thr, cmin = s_min;
+  if (2 * (int64_t)m > bs) {  // the argsort branch (_kmeans.py:1644-1648): the host's
+    if (t == 0) {
+      mbs->handoff = step + 1;
+      __hip_atomic_store(stop, step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 41);
   RS_STAMP(41);
   GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 42);
@@ -2780,20 +2792,24 @@ int mb_rng_launch(const DevMT* in, DevMT* out, int64_t n, int64_t bs, int64_t* r
   return GDD_OK;
 }
 
+size_t mb_reassign_lds(int64_t bs, int k) {
+  return sizeof(int) * (size_t)((bs + 1) & ~1ll) + sizeof(int) * (size_t)k + kMtRingBytes;
+}
+
+bool mb_reassign_ok(int64_t bs, int k) { return mb_reassign_lds(bs, k) <= kReassignLdsCap; }
+
 int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const float* X,
                        const int64_t* rows, float* C_new, float* counts, void* step_ws,
                        size_t step_ws_bytes, const DevMT* mt_in, DevMT* mt_mid, const RngNext& rn,
                        void* state, hipStream_t s) {
-  GDD_REQUIRE(2 * (int64_t)k <= bs, "mb_reassign: needs k <= batch/2");
   StepWs w = carve_step(step_ws, step_ws_bytes, bs, k);
-  const size_t lds = sizeof(int) * (size_t)((bs + 1) & ~1ll) + sizeof(int) * (size_t)k + kMtRingBytes;
-  GDD_REQUIRE(lds <= 150 * 1024, "mb_reassign: batch too large for the LDS swap table");
+  const size_t lds = mb_reassign_lds(bs, k);
+  GDD_REQUIRE(lds <= kReassignLdsCap, "mb_reassign: batch too large for the LDS swap table");
   if (lds > 65536)
     GDD_HIP(hipFuncSetAttribute((const void*)k_mb_reassign, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds));
-  const int32_t* stop = &static_cast<MBState*>(state)->stop_at;
   k_mb_reassign<<<1, 1024, lds, s>>>(step, bs, dim, k, ratio, X, rows, C_new, counts, w.cn2, mt_in,
-                                     mt_mid, rn, stop);
+                                     mt_mid, rn, static_cast<MBState*>(state));
   GDD_LAUNCHED();
   return GDD_OK;
 }

@@ -2946,7 +2946,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   for (int q = 0; q < 2; ++q) b1.candr[q] = cv.take<int64_t>(T);
   for (int q = 0; q < 2; ++q) b1.candn[q] = cv.take<double>(T);
   b1.win = cv.take<int>(2);
-  b1.counter = cv.take<unsigned>((size_t)std::min<int64_t>(n, INT_MAX) * T);
+  b1.counter = cv.take<unsigned>((size_t)std::max(k, 1) * T);  // rounds c < k, trial t
   float* XT = (n <= kBlk || n * (int64_t)dim < INT_MAX) ? cv.take<float>((size_t)n * dim) : nullptr;
   float* Dbig = kpp_big_table(n, dim, T, k) ? cv.take<float>((size_t)n * n) : nullptr;
   float* Dm = kpp_small_table(n, dim, T, k) ? cv.take<float>((size_t)n * n) : nullptr;

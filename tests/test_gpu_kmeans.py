@@ -413,3 +413,29 @@ def test_kmeans_lloyd_update_forms(monkeypatch, case):
         assert a.n_iter_ == ref["n_iter_"]
         assert np.array_equal(a.labels_, ref["labels_"])
         assert np.array_equal(bits(a.cluster_centers_), bits(ref["cluster_centers_"]))
+
+
+@pytest.mark.parametrize("n,dim,k,bs", [(6000, 12, 400, 200), (20000, 8, 300, 500), (3000, 16, 700, 256),
+                                        (8000, 10, 120, 64)])
+def test_minibatch_k_above_half_batch(monkeypatch, n, dim, k, bs):
+    """k > b/2 (config 3's k = 769 > b/2 = 500): the device loop runs these fits too.
+    A reassignment with more than b/2 centres due (np.argsort's branch — certain at step 0 when
+    k >= 2b, since a batch leaves at least k - b clusters empty) stops the device loop at that step;
+    the host runs its convergence test and reassignment, steps on while a weight sum is zero, and
+    resumes the device loop. Labels, centres, inertia, n_steps_ and the generator's final state equal
+    the oracle's and the host-driven loop's (GDD_HOST_LOOP=1)."""
+    X = synth.blobs(n, dim, max(2, k // 3), seed=n + k)
+    rs_ref = np.random.RandomState(11)
+    ref = O.minibatch_kmeans(X, k, random_state=rs_ref, batch_size=bs)
+    s_ref = rs_ref.get_state()
+    for host in (False, True):
+        if host:
+            monkeypatch.setenv("GDD_HOST_LOOP", "1")
+        rs = np.random.RandomState(11)
+        m = gdd.MiniBatchKMeans(n_clusters=k, random_state=rs, batch_size=bs).fit(X)
+        assert m.n_steps_ == ref["n_steps_"], host
+        assert np.array_equal(m.labels_, ref["labels_"]), host
+        assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"])), host
+        assert m.inertia_ == ref["inertia_"], host
+        s = rs.get_state()
+        assert np.array_equal(s[1], s_ref[1]) and s[2] == s_ref[2], host
