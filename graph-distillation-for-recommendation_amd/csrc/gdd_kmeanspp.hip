@@ -1672,11 +1672,194 @@ __device__ __forceinline__ bool prefix_waves_sync(int* ctr, int target) {
   return false;
 }
 
+// ---- exact parallel sgemv_t lane chains (r05) -----------------------------------
+// A unit-weight lane chain (acc = acc + x over L <= 1024 non-negative fp32 entries) evaluated with
+// the bits of the sequential loop but without its L dependent adds. While the running sum s stays in
+// one binade [2^e, 2^(e+1)) it is a multiple of u = 2^(e-23), and adding x moves it by a whole number
+// of quanta that depends on x and, at an exact tie, on the parity of s/u — so a run of entries that
+// keeps the sum inside the binade maps s to s + D[parity(s/u)] u with two integers D0, D1: the run
+// evaluated in hardware from 2^e (even) and from 2^e + u (odd) — equal starting parities take equal
+// advances at every entry, by induction. Runs in one binade compose: the parity after the first run
+// picks the second run's D. Entries where the sum may change binade are added in hardware from the
+// exact running value. The binades come from an fp32 prefix of the chain, within 2^-13 of every
+// exact partial sum (the chain's own rounding is <= L 2^-24 <= 2^-14 relative, all terms >= 0); an
+// entry is a possible crossing unless the prefixes before and after it, widened by 2^-9, share an
+// exponent, so every run's binade is proven. Each applied run is checked anyway (s in its binade, no
+// carry out of it) and a failed check replays the whole chain serially.
+// Layout (512-thread workgroups): wave 0's lane c adds chain c's first kParHead entries serially
+// while waves 4..7 (256 / nl lanes per chain, <= kParMaxSeg entries each) classify the rest, evaluate
+// their runs from 2^e and 2^e + u, and compose them with a segmented scan that restarts after every
+// crossing; lane c then applies the composed runs and adds only the crossing entries.
+constexpr int kParHead = 32;     // entries of each chain the walker adds serially first
+constexpr int kParMaxSeg = 16;   // entries per precompute lane (nl = 4: 64 lanes x 16 >= 1024 - 32)
+constexpr int kParIdE = -1;      // identity run
+constexpr int kParBadE = -2;     // two runs in different binades (never built: a failed check)
+
+struct ParT {
+  int e, d0, d1;  // biased exponent field of the binade, advances from even / odd s/u
+};
+
+__device__ __forceinline__ ParT par_compose(ParT A, ParT B) {  // A, then B
+  if (A.e == kParIdE) return B;
+  if (B.e == kParIdE) return A;
+  if (A.e != B.e) return ParT{kParBadE, 0, 0};
+  ParT C;
+  C.e = A.e;
+  C.d0 = A.d0 + ((A.d0 & 1) ? B.d1 : B.d0);  // even start: parity after A is A.d0's
+  C.d1 = A.d1 + ((A.d1 & 1) ? B.d0 : B.d1);  // odd start: parity after A is 1 + A.d1's
+  return C;
+}
+
+// s (the exact running value) advanced by run T; false when s is not in T's binade or the run would
+// carry it out (then s is left as it was)
+__device__ __forceinline__ bool par_apply(ParT T, float& s) {
+  if (T.e == kParIdE) return true;
+  const int bs = __float_as_int(s);
+  if ((bs >> 23) != T.e) return false;  // also s < 0, and kParBadE (never an exponent field)
+  const int nb = bs + ((bs & 1) ? T.d1 : T.d0);
+  if ((nb >> 23) != T.e) return false;
+  s = __int_as_float(nb);
+  return true;
+}
+
+struct ParLane {     // one precompute lane's result (LDS)
+  int ae, ad0, ad1;  // its runs before its crossing entries (all of them when it has none)
+  int ie, id0, id1;  // the segmented inclusive scan up to and including this lane
+  int x0, x1;        // chain positions added in hardware by the walker
+  int kind;          // 0 no crossing, 1 contiguous crossing entries, 2 walked serially
+};
+
+// waves 4..7 of a 512-thread fold: lane p = tid - 256 owns segment g of chain c
+__device__ __forceinline__ void par_chain_lanes(const float* __restrict__ s_ch,
+                                                const float* __restrict__ s_d, int nl, int h4, int m1,
+                                                ParLane* __restrict__ s_par,
+                                                unsigned long long* __restrict__ s_mask) {
+  const int p = (int)threadIdx.x - 256;
+  const int G = 256 / nl;  // 32 (nl = 8) or 64 (nl = 4): within one wave
+  const int c = p / G, g = p - c * G;
+  const int L = max((m1 - h4 - c + nl - 1) / nl, 0);
+  const int H = min(kParHead, L);
+  const int seg = min(kParMaxSeg, ((L - H + G - 1) / G + 3) & ~3);
+  const int a = H + g * seg;
+  const int cnt = max(0, min(seg, L - a));
+  const float* src = s_ch + c * kChainLd;
+  float x[kParMaxSeg];
+#pragma unroll
+  for (int q = 0; q < kParMaxSeg / 4; ++q) {  // a is a multiple of 4; reads stay inside the padded row
+    const float4 v = *reinterpret_cast<const float4*>(src + min(a, 1024) + 4 * q);
+    x[4 * q] = v.x;
+    x[4 * q + 1] = v.y;
+    x[4 * q + 2] = v.z;
+    x[4 * q + 3] = v.w;
+  }
+  const float acc0 = c < h4 ? s_d[c] : 0.f;
+  float hx = g < H ? src[g] : 0.f;  // head entries, one per lane (G >= kParHead)
+  float loc[kParMaxSeg];
+  float run = 0.f;
+#pragma unroll
+  for (int i = 0; i < kParMaxSeg; ++i) {
+    x[i] = i < cnt ? x[i] : 0.f;
+    run = run + x[i];
+    loc[i] = run;
+  }
+  float inc = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    if (o < G) {
+      const float y = __shfl_up(inc, o, G);
+      if (g >= o) inc = inc + y;
+      hx = hx + __shfl_xor(hx, o, G);
+    }
+  }
+  const float ps = (acc0 + hx) + (inc - run);  // approximate exact value before the segment
+  constexpr float kLo = 1.0f - 1.0f / 512, kHi = 1.0f + 1.0f / 512;
+  unsigned cm = 0u;  // entries where the sum may change binade
+#pragma unroll
+  for (int i = 0; i < kParMaxSeg; ++i) {
+    const float prev = i ? ps + loc[i - 1] : ps;
+    const float cur = ps + loc[i];
+    const int el = __float_as_int(prev * kLo) >> 23, eh = __float_as_int(cur * kHi) >> 23;
+    if (i < cnt && !(el == eh && el >= 1 && eh <= 253)) cm |= 1u << i;
+  }
+  const int j1 = cm ? __builtin_ctz(cm) : cnt;
+  const int j2 = cm ? 31 - __builtin_clz(cm) : cnt - 1;
+  int kind = cm == 0u ? 0 : ((cm >> j1) == ((2u << (j2 - j1)) - 1u) ? 1 : 2);
+  const int eA = j1 > 0 ? __float_as_int(ps) >> 23 : 127;
+  const int eB = (kind == 1 && j2 < cnt - 1) ? __float_as_int(ps + loc[cnt - 1]) >> 23 : 127;
+  // the runs before the crossing entries (A) and after them (B), from 2^e and 2^e + u
+  float a0 = __int_as_float(eA << 23), a1 = __int_as_float((eA << 23) + 1);
+  float b0 = __int_as_float(eB << 23), b1 = __int_as_float((eB << 23) + 1);
+#pragma unroll
+  for (int i = 0; i < kParMaxSeg; ++i) {
+    const float xa = i < j1 ? x[i] : 0.f;
+    const float xb = (i > j2 && i < cnt) ? x[i] : 0.f;
+    a0 = a0 + xa;
+    a1 = a1 + xa;
+    b0 = b0 + xb;
+    b1 = b1 + xb;
+  }
+  const ParT id{kParIdE, 0, 0};
+  ParT A = id, B = id;
+  if (j1 > 0) A = ParT{eA, __float_as_int(a0) - (eA << 23), __float_as_int(a1) - (eA << 23) - 1};
+  if (kind == 1 && j2 < cnt - 1) B = ParT{eB, __float_as_int(b0) - (eB << 23), __float_as_int(b1) - (eB << 23) - 1};
+  if ((j1 > 0 && (__float_as_int(a1) >> 23) != eA) || (kind == 1 && j2 < cnt - 1 && (__float_as_int(b1) >> 23) != eB))
+    kind = 2;  // a run left its binade (cannot happen with the margins above): walk it
+  // segmented inclusive scan: (f, T) = (f_l | f_r, f_r ? T_r : T_l then T_r)
+  int f = kind != 0;
+  ParT T = kind == 0 ? A : (kind == 1 ? B : id);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    if (o < G) {
+      const int lf = __shfl_up(f, o, G), le = __shfl_up(T.e, o, G);
+      const int l0 = __shfl_up(T.d0, o, G), l1 = __shfl_up(T.d1, o, G);
+      if (g >= o && !f) {
+        T = par_compose(ParT{le, l0, l1}, T);
+        f = lf;
+      }
+    }
+  }
+  ParLane r;
+  r.ae = A.e;
+  r.ad0 = A.d0;
+  r.ad1 = A.d1;
+  r.ie = T.e;
+  r.id0 = T.d0;
+  r.id1 = T.d1;
+  r.x0 = kind == 2 ? a : a + j1;
+  r.x1 = kind == 2 ? a + cnt : (kind == 1 ? a + j2 + 1 : a + j1);
+  r.kind = kind;
+  s_par[p] = r;
+  const unsigned long long bal = __ballot(kind != 0);
+  const unsigned long long gm = G == 64 ? bal : ((bal >> ((threadIdx.x & 63) & 32)) & 0xffffffffull);
+  if (g == 0) s_mask[c] = gm;
+}
+
+// wave 0's lane c < nl: the chain's exact value from the head result s and the published runs
+__device__ __forceinline__ float par_chain_walk(const float* __restrict__ src, int c, int nl, float s,
+                                                const ParLane* __restrict__ s_par,
+                                                const unsigned long long* __restrict__ s_mask, bool& ok) {
+  const int G = 256 / nl;
+  const ParLane* rl = s_par + c * G;
+  unsigned long long m = s_mask[c];
+  while (m) {
+    const int q = __builtin_ctzll(m);
+    m &= m - 1;
+    if (q > 0) ok = par_apply(ParT{rl[q - 1].ie, rl[q - 1].id0, rl[q - 1].id1}, s) && ok;
+    const ParLane r = rl[q];
+    if (r.kind == 1) ok = par_apply(ParT{r.ae, r.ad0, r.ad1}, s) && ok;
+    for (int i = r.x0; i < r.x1; ++i) s = s + src[i];
+  }
+  ok = par_apply(ParT{rl[G - 1].ie, rl[G - 1].id0, rl[G - 1].id1}, s) && ok;
+  return s;
+}
+
 // the fold of round c's trial t by one 256-thread workgroup holding the trial's row in registers
 // (r[q] = entry tid + 256 q): the exact sgemv_t potential, the fp64 cumulative potential and the
 // candidates every trial would draw in round c+1 if t wins
 // pot_out (nullable) receives the potential, cand_out[0..T) the candidates (global memory or LDS)
-template <bool PIPE = true>
+// PAR (512-thread workgroups, r05): the lane chains by par_chain_lanes / par_chain_walk (waves 4..7
+// precompute, wave 0 walks); threads 0..255 hold the row as before
+template <bool PIPE = true, bool PAR = false>
 __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t, const float (&r)[16],
                                                 double ut, float* __restrict__ s_d,
                                                 float* __restrict__ s_ch, double* __restrict__ s_cum,
@@ -1699,6 +1882,10 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
   __shared__ int s_sync;
   __shared__ int s_sidx[kMaxTrials];
   __shared__ int s_sok;
+  __shared__ ParLane s_par[PAR ? 256 : 1];
+  __shared__ unsigned long long s_pmask[8];
+  __shared__ int s_parsync;
+  const bool par = PAR && perm && m1 > 0;  // uniform over the workgroup
   // measured (profiles/r04_kpp_spec_search.txt): T = 8 (3000 x 40, k = 454) 8.07 -> 7.44 us per round
   // once the prefix reads are batched (before that the prefix alone took as long as the chains and the
   // speculation lost); T = 7 (3706 x 64, k = 371) 11.33 -> 10.44, T = 6 (Cora) 9.97 -> 9.68
@@ -1706,8 +1893,9 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
   if (tid == 0) {
     s_sync = 0;
     s_sok = 1;
+    s_parsync = 0;
   }
-  {
+  if (!PAR || tid < 256) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = tid + 256 * q;
@@ -1733,7 +1921,24 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
       if (perm) {
         const int nl = k4x2 ? 4 : 8;
         float acc = 0.f;
-        if (lane < nl) {
+        if (par) {  // head serially, then the walk over waves 4..7's runs
+          const int L = max((m1 - h4 - lane + nl - 1) / nl, 0);
+          if (lane < nl) {
+            if (lane < h4) acc = acc + s_d[lane];
+            acc = chain_add<PIPE>(s_ch + lane * kChainLd, min(L, kParHead), acc);
+          }
+          bool ok = waves_wait(&s_parsync, 4);
+          if (lane < nl) {
+            const float s = par_chain_walk(s_ch + lane * kChainLd, lane, nl, acc, s_par, s_pmask, ok);
+            if (ok) {
+              acc = s;
+            } else {  // a failed check (or a spin that gave up): the sequential loop
+              acc = 0.f;
+              if (lane < h4) acc = acc + s_d[lane];
+              acc = chain_add<PIPE>(s_ch + lane * kChainLd, L, acc);
+            }
+          }
+        } else if (lane < nl) {
           if (lane < h4) acc = acc + s_d[lane];
           const int L = (m1 - h4 - lane + nl - 1) / nl;
           acc = chain_add<PIPE>(s_ch + lane * kChainLd, max(L, 0), acc);
@@ -1760,6 +1965,11 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
       if (pot_out) *pot_out = y;
     }
     GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 76);
+  } else if (PAR && wave >= 4) {  // the lane chains' runs (par_chain_lanes)
+    if (par) {
+      par_chain_lanes(s_ch, s_d, k4x2 ? 4 : 8, h4, m1, s_par, s_pmask);
+      waves_arrive(&s_parsync);
+    }
   } else {  // the cumulative potential: thread runs and the wave's inclusive scan
     // every read issued before the run (a per-entry weight branch had each read waited on alone:
     // ~2 us, as long as the chains, r04 stamps); entries past n add +0.0, as before
@@ -1867,7 +2077,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
     }
   }
   if (c + 1 < a.k) {
-    if (wave > 0 && !spec) {
+    if (wave > 0 && (!PAR || wave < 4) && !spec) {
       double B = 0.0;
       for (int q = 0; q < wave - 1; ++q) B = B + s_wave[q];
       const double pot = (double)s_pot;
@@ -2174,10 +2384,12 @@ __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __rest
 // launch (lq); round 1 reads the first centre's slot-0 candidates, so the first launch writes slot 1.
 // Per round this halves the launches and their two leading trips (k_kpp1_dm: 9.2 us per round).
 constexpr int kPairMaxT = 8;  // T * T <= 64: one wave lane per round-(c-1) candidate
+constexpr bool kParChainDefault = false;  // set from the same-box A/B (DESIGN.md §4 k-means++)
 
-template <bool PIPE>
-__global__ __launch_bounds__(256) void k_kpp1_dm2(Kpp1Args a, const float* __restrict__ D, int c, int lq,
-                                                  int pair) {
+// PAR: 512 threads, the exact parallel lane chains (threads 0..255 hold the rows)
+template <bool PIPE, bool PAR = false>
+__global__ __launch_bounds__(PAR ? 512 : 256) void k_kpp1_dm2(Kpp1Args a, const float* __restrict__ D, int c,
+                                                              int lq, int pair) {
   __shared__ float s_d[kBlk];
   __shared__ float s_ch[8 * kChainLd];
   __shared__ double s_cum[kBlk];
@@ -2236,23 +2448,26 @@ __global__ __launch_bounds__(256) void k_kpp1_dm2(Kpp1Args a, const float* __res
   if (tid == 0 && (!pair || t2 == 0)) a.candself[lq][w] = ct;
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && g == 0 && c == a.k - 3 + (a.k & 1)), 61);
   // trip 2: the closest distances and the candidate's table row
+  const bool rowt = !PAR || tid < 256;  // the threads that hold the row
   const float* drow = D + ct * n;
   float wi[16], dd[16], r[16];
+  if (rowt) {
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int e = min(tid + 256 * q, n - 1);
-    wi[q] = wrow[e];
-    dd[q] = drow[e];
+    for (int q = 0; q < 16; ++q) {
+      const int e = min(tid + 256 * q, n - 1);
+      wi[q] = wrow[e];
+      dd[q] = drow[e];
+    }
   }
 #pragma unroll
   for (int q = 0; q < 16; ++q) r[q] = np_minimum(wi[q], dd[q]);
   if (!pair) {  // the last round alone: as k_kpp1_dm
-    kpp1_fold_trial<PIPE>(a, c, w, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv[lq] + w,
-                          a.candw[lq] + (int64_t)w * T);
+    kpp1_fold_trial<PIPE, PAR>(a, c, w, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv[lq] + w,
+                               a.candw[lq] + (int64_t)w * T);
     return;
   }
-  kpp1_fold_trial<PIPE>(a, c, w, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot,
-                        t2 == 0 ? a.potv[lq] + w : nullptr, s_cand);
+  kpp1_fold_trial<PIPE, PAR>(a, c, w, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot,
+                             t2 == 0 ? a.potv[lq] + w : nullptr, s_cand);
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && g == 0 && c == a.k - 3 + (a.k & 1)), 62);
   // trip 3: round c+1's candidate for slot t2 if w wins, and its table row
@@ -2260,16 +2475,18 @@ __global__ __launch_bounds__(256) void k_kpp1_dm2(Kpp1Args a, const float* __res
   const int j = w * T + t2;
   if (tid == 0) a.candself2[lq][j] = c1;
   const float* drow2 = D + c1 * n;
+  if (rowt) {
 #pragma unroll
-  for (int q = 0; q < 16; ++q) dd[q] = drow2[min(tid + 256 * q, n - 1)];
-  float* orow = a.dist2[lq] + (int64_t)j * n;
+    for (int q = 0; q < 16; ++q) dd[q] = drow2[min(tid + 256 * q, n - 1)];
+    float* orow = a.dist2[lq] + (int64_t)j * n;
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    wi[q] = np_minimum(r[q], dd[q]);
-    if (tid + 256 * q < n) orow[tid + 256 * q] = wi[q];
+    for (int q = 0; q < 16; ++q) {
+      wi[q] = np_minimum(r[q], dd[q]);
+      if (tid + 256 * q < n) orow[tid + 256 * q] = wi[q];
+    }
   }
-  kpp1_fold_trial<PIPE>(a, c + 1, t2, wi, ut2, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv2[lq] + j,
-                        a.candw2[lq] + (int64_t)j * T);
+  kpp1_fold_trial<PIPE, PAR>(a, c + 1, t2, wi, ut2, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv2[lq] + j,
+                             a.candw2[lq] + (int64_t)j * T);
 }
 
 // after the last launch of k_kpp1_dm2: its winner(s) and the last centre
@@ -3051,6 +3268,10 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
         k_kpp_dmat<64><<<gdm, 256, 0, s>>>((int)n, dim, X, XT, xsq, Dm);
       GDD_LAUNCHED();
       const bool plain = getenv("GDD_KPP_CHAIN_PLAIN") != nullptr;
+      // GDD_KPP_PAR_CHAIN: 1 = the exact parallel lane chains (512-thread pair launches), 0 = the
+      // sequential lane chains
+      const char* pce = getenv("GDD_KPP_PAR_CHAIN");
+      const bool par_chain = pce ? pce[0] == '1' : kParChainDefault;
       if (T <= kPairMaxT && getenv("GDD_KPP_SINGLE_ROUND") == nullptr) {
         // two rounds per launch (a trailing odd round alone). The chain's arguments are fixed by
         // (b1, Dm, k): it is replayed as one recorded graph (replay_or_run) — every launch then
@@ -3063,6 +3284,8 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
             const unsigned grid = (unsigned)(pair ? T * T : T);
             if (plain)
               k_kpp1_dm2<false><<<grid, 256, 0, cs>>>(b1, Dm, c, lq, pair);
+            else if (par_chain)
+              k_kpp1_dm2<true, true><<<grid, 512, 0, cs>>>(b1, Dm, c, lq, pair);
             else
               k_kpp1_dm2<true><<<grid, 256, 0, cs>>>(b1, Dm, c, lq, pair);
             GDD_LAUNCHED();
@@ -3079,13 +3302,14 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
         struct {
           Kpp1Args b1;
           const float* Dm;
-          int k, plain;
+          int k, plain, par;
         } key;
         std::memset(&key, 0, sizeof(key));
         key.b1 = b1;
         key.Dm = Dm;
         key.k = k;
         key.plain = plain ? 1 : 0;
+        key.par = par_chain ? 1 : 0;
         return replay_or_run("kpp_pair_chain", &key, sizeof(key), s, chain);
       }
       for (int c = 1; c < k; ++c) {

@@ -302,3 +302,35 @@ def test_kmeans_plusplus_small_k_skips_the_table(monkeypatch, n, dim, k):
     c2, idx2 = ops.kmeans_plusplus(Xd, k, np.random.RandomState(5))
     assert np.array_equal(idx.cpu().numpy(), idx2.cpu().numpy())
     assert np.array_equal(bits(c.cpu().numpy()), bits(c2.cpu().numpy()))
+
+
+def _par_case_points(case, n, dim, seed):
+    rng = np.random.default_rng(seed)
+    if case == "integers":  # exact integer distances: the running sums pass 2^24, so ties are common
+        return rng.integers(-300, 300, (n, dim)).astype(np.float32)
+    X = synth.blobs(n, dim, 24, seed=seed)
+    if case == "dupes":  # zero distances, long runs of them
+        X[1::3] = X[0]
+        X[n // 2:n // 2 + 400] = X[5]
+    elif case == "range":  # twelve decades: crossings everywhere, tiny terms absorbed
+        X *= (10.0 ** rng.uniform(-6, 6, (n, 1))).astype(np.float32)
+    return np.ascontiguousarray(X, np.float32)
+
+
+@pytest.mark.parametrize("case", ["blobs", "integers", "dupes", "range"])
+@pytest.mark.parametrize("n,dim,k", [(3000, 40, 454), (2708, 7, 70), (4093, 3, 200), (3706, 64, 371),
+                                     (1001, 5, 33)])
+def test_kmeans_plusplus_parallel_chains(monkeypatch, case, n, dim, k):
+    """The exact parallel sgemv_t lane chains (GDD_KPP_PAR_CHAIN=1: runs inside one binade from
+    2^e and 2^e + u, composed by parity, crossings added in hardware) give the sequential chains'
+    bits: the seeding equals the oracle's with and without them, on data with exact ties (integer
+    distances past 2^24), zero distances, twelve decades of magnitudes, 8- and 4-lane trials
+    (T = 6 at the Cora shape) and n % 4 tails."""
+    X = _par_case_points(case, n, dim, n + dim + k)
+    c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
+    for val in ("1", "0"):
+        monkeypatch.setenv("GDD_KPP_PAR_CHAIN", val)
+        ops = _Ops("cuda", n, k, dim)
+        c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(15))
+        assert np.array_equal(idx.cpu().numpy(), idx_ref), val
+        assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref)), val

@@ -88,7 +88,21 @@ def ab_spec():
         del os.environ["GDD_KPP_SPEC_SEARCH"]
 
 
+def ab_par():
+    """The exact parallel lane chains (GDD_KPP_PAR_CHAIN=1, 512-thread pair launches) against the
+    sequential lane chains (=0), same process, parity checked on the first pass of each."""
+    for (n, dim, k) in [(3000, 40, 454), (3706, 64, 371), (2708, 7, 70), (3000, 41, 769)]:
+        for i, val in enumerate(("0", "1", "0", "1")):
+            os.environ["GDD_KPP_PAR_CHAIN"] = val
+            print(f"variant GDD_KPP_PAR_CHAIN={val}:", end=" ", flush=True)
+            run(n, dim, k, 5, check=i < 2)
+        del os.environ["GDD_KPP_PAR_CHAIN"]
+
+
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["par"]:
+        ab_par()
+        sys.exit(0)
     if sys.argv[1:2] == ["one"]:  # the MiniBatchKMeans init shape alone, parity checked
         run(3000, 40, 454, 5)
         sys.exit(0)
