@@ -126,6 +126,8 @@ int dev_chunk() {
 // convergence stop in *stop_step, or in *handoff_step a step whose reassignment needs the host (more
 // than b/2 centres due: np.argsort's branch) — that step's update has run, its tail and reassignment
 // have not, and the generator (written back to rng) is after its batch draws.
+constexpr int kNearStopDefault = 0;  // set from the same-box A/B (DESIGN.md §4 MiniBatch)
+
 int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t i0, int64_t rr_base,
                 bool norms_valid0, int64_t n_steps, int max_no_improvement, float reassignment_ratio,
                 MTState* rng, const FitWs& w, int32_t* h_flag /* pinned, >= 64 ints */,
@@ -149,6 +151,10 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t i
     const char* e = getenv("GDD_MB_LOOKAHEAD");
     const int v = e ? atoi(e) : 1;
     return v < 1 ? 1 : (v > 3 ? 3 : v);
+  }();
+  static const int near_stop = [] {
+    const char* e = getenv("GDD_MB_NEAR_STOP");
+    return e ? atoi(e) : kNearStopDefault;
   }();
   hipEvent_t ev[4];
   for (int q = 0; q < 4; ++q) GDD_HIP(hipEventCreateWithFlags(&ev[q], hipEventDisableTiming));
@@ -229,14 +235,32 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t i
                        [&](hipStream_t cs) { return enqueue_chunk(i, m, cs); });
     if (rc) return rc;
     i += m;
-    // this chunk's stop word, read back while the next chunks run
+    // this chunk's stop word and no-improvement count (state bytes 16..31), read back while the next
+    // chunks run: slot q at h_flag[32 + 4 q]
     const int slot = (int)(chunk & 3);
-    GDD_HIP(hipMemcpyAsync(h_flag + slot, stop_word, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    int32_t* hs = h_flag + 32 + 4 * slot;
+    GDD_HIP(hipMemcpyAsync(hs, stop_word, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     GDD_HIP(hipEventRecord(ev[slot], s));
     if (chunk >= lookahead) {
       const int old = (int)((chunk - lookahead) & 3);
       GDD_HIP(hipEventSynchronize(ev[old]));
-      if (h_flag[old]) break;  // the later kernels already enqueued are no-ops
+      const int32_t* ho = h_flag + 32 + 4 * old;
+      if (ho[0]) break;  // the later kernels already enqueued are no-ops
+      // near the stop (the no-improvement count of the chunk just read is within near_stop of
+      // max_no_improvement): wait for the chunks in flight before enqueuing more, so a stop inside
+      // them leaves no chunk of no-op launches behind (GDD_MB_NEAR_STOP, 0 = off)
+      if (near_stop > 0 && max_no_improvement > 0 && ho[3] >= max_no_improvement - near_stop &&
+          i < n_steps) {
+        bool stopped_now = false;
+        for (int64_t q = chunk - lookahead + 1; q <= chunk; ++q) {
+          GDD_HIP(hipEventSynchronize(ev[q & 3]));
+          if (h_flag[32 + 4 * (q & 3)]) {
+            stopped_now = true;
+            break;
+          }
+        }
+        if (stopped_now) break;
+      }
     }
     ++chunk;
   }
