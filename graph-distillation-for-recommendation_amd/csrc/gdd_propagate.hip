@@ -165,7 +165,9 @@ __global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
                                              float* __restrict__ acc_out, float acc_scale,
                                              const float* __restrict__ acc_init,
                                              const float* __restrict__ acc_prev,
-                                             float* __restrict__ partials) {
+                                             float* __restrict__ partials,
+                                             const int32_t* __restrict__ ymap,
+                                             const int32_t* __restrict__ pmap) {
   const int lane = threadIdx.x & (G - 1);
   int64_t ib;  // item block
   int chunk;   // feature chunk of G*V
@@ -218,8 +220,11 @@ __global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
   }
   if (!fa) return;
   if (it.pslot < 0) {
+    // relabelled layout (gdd_propagate_relabeled): y's row of node `row` is ymap[row] (nullptr: the
+    // node's own id), acc_prev's is pmap[row]; target and acc_init keep the original ids
     const int64_t o = (int64_t)it.row * d + f;
-    vstore<V>(y + o, acc);  // gathered by the next hop: default policy
+    const int64_t oy = ymap ? (int64_t)ymap[it.row] * d + f : o;
+    vstore<V>(y + oy, acc);  // gathered by the next hop: default policy
     if (acc_out) {
       float t[V];
       if (acc_init) {  // first hop: the initial target fp32(1-alpha) * X (agent :59), one rounding
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
       }
       if (acc_prev) {  // the previous hop's deferred term: its output row (this hop's input x)
         float q[V];
-        vload<V>(acc_prev + o, q);
+        vload<V>(acc_prev + (pmap ? (int64_t)pmap[it.row] * d + f : o), q);
 #pragma unroll
         for (int v = 0; v < V; ++v) t[v] = t[v] + acc_scale * q[v];
       }
@@ -253,7 +258,8 @@ __global__ void k_fixup(const int32_t* __restrict__ counts, const int32_t* __res
                         const int32_t* __restrict__ long_off, const int32_t* __restrict__ rowptr,
                         int d, const float* __restrict__ partials, float* __restrict__ y,
                         float* __restrict__ acc_out, float acc_scale,
-                        const float* __restrict__ acc_init, const float* __restrict__ acc_prev) {
+                        const float* __restrict__ acc_init, const float* __restrict__ acc_prev,
+                        const int32_t* __restrict__ ymap, const int32_t* __restrict__ pmap) {
   const int nl = counts[1];
   for (int r = blockIdx.x; r < nl; r += gridDim.x) {
     const int32_t row = long_rows[r], po = long_off[r];
@@ -272,10 +278,10 @@ __global__ void k_fixup(const int32_t* __restrict__ counts, const int32_t* __res
       }
       for (; k < s; ++k) sum = sum + pp[(int64_t)k * d];
       const int64_t o = (int64_t)row * d + f;
-      y[o] = sum;
+      y[ymap ? (int64_t)ymap[row] * d + f : o] = sum;
       if (acc_out) {
         float t = acc_init ? acc_scale * acc_init[o] : acc_out[o];
-        if (acc_prev) t = t + acc_scale * acc_prev[o];
+        if (acc_prev) t = t + acc_scale * acc_prev[pmap ? (int64_t)pmap[row] * d + f : o];
         acc_out[o] = t + acc_scale * sum;
       }
     }
@@ -396,10 +402,15 @@ int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv,
   return GDD_OK;
 }
 
+struct RowMaps {  // relabelled layouts (nullptr: original ids)
+  const int32_t* y;
+  const int32_t* prev;
+};
+
 template <int V, int G>
 void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float scale, int d,
                    const float* x, float* y, float* acc, float acc_scale, const float* acc_init,
-                   const float* acc_prev, hipStream_t s) {
+                   const float* acc_prev, RowMaps rm, hipStream_t s) {
   constexpr int kGroups = 256 / G;
   const int64_t iblocks = (pl.max_items + kGroups - 1) / kGroups;
   const int chunks = (d + G * V - 1) / (G * V);
@@ -408,7 +419,7 @@ void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float s
     const int64_t groups = (iblocks + (8 / S) - 1) / (8 / S);
     k_hop<V, G, S><<<(unsigned)(groups * 8), 256, 0, s>>>(pl.items, pl.counts, col, val, scale, d,
                                                           x, y, acc, acc_scale, acc_init, acc_prev,
-                                                          pl.partials);
+                                                          pl.partials, rm.y, rm.prev);
   };
   if (chunks == 8)
     xcd_launch(std::integral_constant<int, 8>());
@@ -420,7 +431,8 @@ void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float s
     xcd_launch(std::integral_constant<int, 1>());
   else
     k_hop<V, G, 0><<<dim3((unsigned)iblocks, (unsigned)chunks), 256, 0, s>>>(
-        pl.items, pl.counts, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, pl.partials);
+        pl.items, pl.counts, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, pl.partials,
+        rm.y, rm.prev);
 }
 
 // lanes per item: the whole row up to 64 lanes, or (GDD_HOP_LANES=8/16/32, V = 4) narrower groups
@@ -436,24 +448,24 @@ int hop_lanes_override() {
 template <int V>
 void launch_hop_v(const Plan& pl, const int32_t* col, const float* val, float scale, int d,
                   const float* x, float* y, float* acc, float acc_scale, const float* acc_init,
-                  const float* acc_prev, hipStream_t s) {
+                  const float* acc_prev, RowMaps rm, hipStream_t s) {
   const int lanes = (d + V - 1) / V;
   const int ov = hop_lanes_override();
   if (ov == 8)
-    return launch_hop_vg<V, 8>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
+    return launch_hop_vg<V, 8>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, rm, s);
   if (ov == 16)
-    return launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
+    return launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, rm, s);
   // 29..32 lanes of float4 (d in (112, 128]): two XCD slices of 16 lanes each, so an XCD's L2 caches
   // half of every gathered row (measured at the arxiv shape, d = 128: 202 vs 208 us per hop; the
   // gathers' L2 hit rate rises, the instruction overhead of the narrower groups stays small). With
   // fewer lanes the second slice idles most of its lanes while reading the whole column/value stream
   // again: products' d = 100 (25 lanes) runs 9.5 ms per hop in one 32-lane group vs 12.4 sliced.
   if (lanes <= 16 || (V == 4 && lanes > 28 && lanes <= 32 && ov != 32))
-    launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
+    launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, rm, s);
   else if (lanes <= 32)
-    launch_hop_vg<V, 32>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
+    launch_hop_vg<V, 32>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, rm, s);
   else
-    launch_hop_vg<V, 64>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
+    launch_hop_vg<V, 64>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, rm, s);
 }
 
 // acc_init (nullable): the accumulator's previous value is acc_scale * acc_init instead of acc (the
@@ -462,7 +474,8 @@ void launch_hop_v(const Plan& pl, const int32_t* col, const float* val, float sc
 // acc_prev) + acc_scale * y — the same two roundings, in the same order, as two separate updates.
 int run_hop(const Plan& pl, const int32_t* rowptr, const int32_t* col, const float* val,
             float scale, int d, const float* x, float* y, float* acc, float acc_scale,
-            hipStream_t s, const float* acc_init = nullptr, const float* acc_prev = nullptr) {
+            hipStream_t s, const float* acc_init = nullptr, const float* acc_prev = nullptr,
+            RowMaps rm = RowMaps{nullptr, nullptr}) {
   // float4 rows need 16-byte aligned row starts: d % 4 == 0 and 16-byte aligned bases
   auto aligned = [](const void* p, int a) { return ((uintptr_t)p % a) == 0; };
   const bool a16 = aligned(x, 16) && aligned(y, 16) && (!acc || aligned(acc, 16)) &&
@@ -471,15 +484,15 @@ int run_hop(const Plan& pl, const int32_t* rowptr, const int32_t* col, const flo
   const bool a8 = aligned(x, 8) && aligned(y, 8) && (!acc || aligned(acc, 8)) &&
                   (!acc_init || aligned(acc_init, 8)) && (!acc_prev || aligned(acc_prev, 8));
   if (d % 4 == 0 && a16)
-    launch_hop_v<4>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
+    launch_hop_v<4>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, rm, s);
   else if (d % 2 == 0 && a8)
-    launch_hop_v<2>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
+    launch_hop_v<2>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, rm, s);
   else
-    launch_hop_v<1>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, s);
+    launch_hop_v<1>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, rm, s);
   GDD_LAUNCHED();
   const unsigned fixup_grid = (unsigned)std::min<int64_t>(pl.max_long, kFixupBlocks);
   k_fixup<<<fixup_grid, 256, 0, s>>>(pl.counts, pl.long_rows, pl.long_off, rowptr, d, pl.partials, y,
-                                     acc, acc_scale, acc_init, acc_prev);
+                                     acc, acc_scale, acc_init, acc_prev, rm.y, rm.prev);
   GDD_LAUNCHED();
   return GDD_OK;
 }
@@ -542,15 +555,21 @@ extern "C" int gdd_spmm_planned(int64_t n, int64_t nnz, const int32_t* rowptr, c
   return run_hop(pl, rowptr, col, val, scale, d, x, y, acc, acc_scale, to_hip(stream));
 }
 
-extern "C" int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
-                             const float* val, int d, const float* X, int T, float alpha,
-                             float* target, float* p_last, float* p_tmp, void* ws,
-                             size_t ws_bytes, gdd_stream_t stream) {
-  int rc = check_csr_args(n, nnz, rowptr, col, val, d);
-  if (rc) return rc;
-  GDD_REQUIRE(T >= 1, "propagate: T=%d must be >= 1", T);
-  GDD_REQUIRE(X && target && p_last && ws && (T <= 2 || p_tmp), "propagate: null pointer");
-  hipStream_t s = to_hip(stream);
+namespace gdd {
+namespace {
+__global__ void k_relabel_cols(int64_t nnz, const int32_t* __restrict__ col, const int32_t* __restrict__ rho,
+                               int32_t* __restrict__ col_r) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < nnz) col_r[e] = rho[col[e]];
+}
+
+// gdd_propagate; with rho the intermediate hops run in the relabelled layout (node r's row of p at
+// rho[r], gathered through col_r = rho[col]): hop 1 gathers X by the original ids, target keeps the
+// original ids throughout, the last hop stores p_last by the original ids
+int propagate_impl(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* val,
+                   const int32_t* rho, int d, const float* X, int T, float alpha, float* target,
+                   float* p_last, float* p_tmp, void* ws, size_t ws_bytes, hipStream_t s) {
+  int rc = 0;
   // the reference's Python doubles, rounded where they meet fp32 tensors
   const float a32 = alpha;
   const float w32 = (float)(1.0 - (double)alpha);
@@ -565,6 +584,15 @@ extern "C" int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, cons
   Plan pl;
   rc = build_plan(n, nnz, d, rowptr, cv, pl, s);
   if (rc) return rc;
+  int32_t* col_r = nullptr;
+  if (rho) {
+    col_r = cv.take<int32_t>((size_t)std::max<int64_t>(nnz, 1));
+    if (!cv.ok()) return fail(GDD_E_WORKSPACE, "propagate_relabeled: workspace too small");
+    if (nnz > 0) {
+      k_relabel_cols<<<(unsigned)((nnz + 255) / 256), 256, 0, s>>>(nnz, col, rho, col_r);
+      GDD_LAUNCHED();
+    }
+  }
   // ping-pong so that hop T-1 lands in p_last. The target update is paired: after the first hop,
   // hop h (odd) leaves target alone and hop h+1 adds both terms, reading p_h back as its own input
   // rows — one read-modify-write of target per two hops instead of per hop (the streamed bytes that
@@ -579,19 +607,53 @@ extern "C" int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, cons
   bool deferred = false;
   for (int h = 0; h < hops; ++h) {
     float* out = bufs[h % 2];
+    // relabelled: hops after the first gather through col_r, every hop but the last stores its rows
+    // at rho, and a deferred term (the previous hop's output) is read at rho
+    const int32_t* cc = (rho && h > 0) ? col_r : col;
+    const RowMaps rm{(rho && h + 1 < hops) ? rho : nullptr, (rho && h > 0) ? rho : nullptr};
     if (h == 0) {
-      rc = run_hop(pl, rowptr, col, val, a32, d, in, out, target, w32, s, X);
+      rc = run_hop(pl, rowptr, cc, val, a32, d, in, out, target, w32, s, X, nullptr, rm);
     } else if (deferred) {
-      rc = run_hop(pl, rowptr, col, val, a32, d, in, out, target, w32, s, nullptr, in);
+      rc = run_hop(pl, rowptr, cc, val, a32, d, in, out, target, w32, s, nullptr, in, rm);
       deferred = false;
     } else if (pair && h + 1 < hops) {
-      rc = run_hop(pl, rowptr, col, val, a32, d, in, out, nullptr, w32, s);
+      rc = run_hop(pl, rowptr, cc, val, a32, d, in, out, nullptr, w32, s, nullptr, nullptr, rm);
       deferred = true;
     } else {
-      rc = run_hop(pl, rowptr, col, val, a32, d, in, out, target, w32, s);
+      rc = run_hop(pl, rowptr, cc, val, a32, d, in, out, target, w32, s, nullptr, nullptr, rm);
     }
     if (rc) return rc;
     in = out;
   }
   return GDD_OK;
+}
+}  // namespace
+}  // namespace gdd
+
+extern "C" int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
+                             const float* val, int d, const float* X, int T, float alpha,
+                             float* target, float* p_last, float* p_tmp, void* ws,
+                             size_t ws_bytes, gdd_stream_t stream) {
+  int rc = check_csr_args(n, nnz, rowptr, col, val, d);
+  if (rc) return rc;
+  GDD_REQUIRE(T >= 1, "propagate: T=%d must be >= 1", T);
+  GDD_REQUIRE(X && target && p_last && ws && (T <= 2 || p_tmp), "propagate: null pointer");
+  return propagate_impl(n, nnz, rowptr, col, val, nullptr, d, X, T, alpha, target, p_last, p_tmp, ws,
+                        ws_bytes, to_hip(stream));
+}
+
+extern "C" size_t gdd_propagate_relabeled_ws_bytes(int64_t n, int64_t nnz, int d) {
+  return plan_ws_bytes(n, nnz, d) + align256(sizeof(int32_t) * (size_t)std::max<int64_t>(nnz, 1)) + 256;
+}
+
+extern "C" int gdd_propagate_relabeled(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
+                                       const float* val, const int32_t* rho, int d, const float* X, int T,
+                                       float alpha, float* target, float* p_last, float* p_tmp,
+                                       void* ws, size_t ws_bytes, gdd_stream_t stream) {
+  int rc = check_csr_args(n, nnz, rowptr, col, val, d);
+  if (rc) return rc;
+  GDD_REQUIRE(T >= 1, "propagate: T=%d must be >= 1", T);
+  GDD_REQUIRE(rho && X && target && p_last && ws && (T <= 2 || p_tmp), "propagate_relabeled: null pointer");
+  return propagate_impl(n, nnz, rowptr, col, val, rho, d, X, T, alpha, target, p_last, p_tmp, ws,
+                        ws_bytes, to_hip(stream));
 }

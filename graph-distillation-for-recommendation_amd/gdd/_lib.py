@@ -36,6 +36,9 @@ SIGNATURES = {
     "gdd_propagate_ws_bytes": (_c_size, [_c_i64, _c_i64, _c_int]),
     "gdd_propagate": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _c_int, _vp, _c_int, _c_f32, _vp,
                                _vp, _vp, _vp, _c_size, _vp]),
+    "gdd_propagate_relabeled_ws_bytes": (_c_size, [_c_i64, _c_i64, _c_int]),
+    "gdd_propagate_relabeled": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_int, _vp, _c_int, _c_f32,
+                                         _vp, _vp, _vp, _vp, _c_size, _vp]),
     "gdd_spmm": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _c_int, _c_f32, _vp, _vp, _vp, _c_f32,
                           _vp, _c_size, _vp]),
     "gdd_spmm_plan": (_c_int, [_c_i64, _c_i64, _vp, _c_int, _vp, _c_size, _vp]),

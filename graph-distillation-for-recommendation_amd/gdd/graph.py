@@ -172,7 +172,29 @@ def _ws_propagate(adj: CSRGraph, d: int):
     return lib, _lib.workspace(lib.gdd_propagate_ws_bytes(adj.n, adj.nnz, d), adj.device)
 
 
-def propagate(adj_norm: CSRGraph, features: torch.Tensor, T: int, alpha: float, group=None):
+def locality_order(adj: CSRGraph, kind: str = "degree") -> torch.Tensor:
+    """A node relabelling for :func:`propagate`'s ``relabel`` (rho: node r's row of the intermediate
+    hops at rho[r], int32 on the graph's device). ``"degree"``: rows by descending length, ties by id
+    (the hubs every hop gathers most sit together); ``"rcm"``: reverse Cuthill-McKee of the pattern
+    (scipy, on the host), which recovers the community blocks of a graph whose ids were shuffled."""
+    dev = adj.device
+    n = adj.n
+    if kind == "degree":
+        deg = (adj.rowptr[1:] - adj.rowptr[:-1]).to(torch.int64)
+        order = torch.sort(-deg, stable=True).indices
+    elif kind == "rcm":
+        from scipy.sparse.csgraph import reverse_cuthill_mckee
+        order = torch.from_numpy(np.ascontiguousarray(
+            reverse_cuthill_mckee(adj.to_scipy().tocsr(), symmetric_mode=True), np.int64)).to(dev)
+    else:
+        raise ValueError(f"unknown locality order {kind!r}")
+    rho = torch.empty(n, dtype=torch.int32, device=dev)
+    rho[order] = torch.arange(n, dtype=torch.int32, device=dev)
+    return rho
+
+
+def propagate(adj_norm: CSRGraph, features: torch.Tensor, T: int, alpha: float, group=None,
+              relabel=None):
     """The closed-form feature denoising loop of pretrained_clustering (transduct:55-65).
 
     Returns ``(target_feat, prop_feat)`` exactly as the loop leaves them: ``target_feat =
@@ -181,6 +203,9 @@ def propagate(adj_norm: CSRGraph, features: torch.Tensor, T: int, alpha: float, 
     :func:`gdd.sharded.propagation_shards_pay` says the gathers outweigh a per-hop all-gather
     (ogbn-products, not ogbn-arxiv), the rows are partitioned over the ranks
     (:func:`gdd.sharded.sharded_propagate`, bit-identical); otherwise every rank propagates.
+    ``relabel`` (opt-in): ``"degree"``, ``"rcm"`` or a permutation rho (node r -> row rho[r]): the
+    intermediate hops run in that node order (gdd_propagate_relabeled) — same bits, different
+    gather locality.
     """
     # the same input checks for both paths (ADVICE r4: the sharded dispatch used to come first)
     if T < 1:
@@ -198,6 +223,23 @@ def propagate(adj_norm: CSRGraph, features: torch.Tensor, T: int, alpha: float, 
         world = world_of(group)[1]
         if world > 1 and propagation_shards_pay(adj_norm.n, adj_norm.nnz, d, world):
             return sharded_propagate(adj_norm, X, T, alpha, group=group)
+    if relabel is not None:
+        rho = locality_order(adj_norm, relabel) if isinstance(relabel, str) else relabel
+        rho = torch.as_tensor(rho, device=X.device).to(torch.int32).contiguous()
+        if rho.shape != (n,) or not torch.equal(torch.sort(rho).values,
+                                               torch.arange(n, dtype=torch.int32, device=X.device)):
+            raise ValueError("relabel must be a permutation of range(n)")
+        lib = _lib.device_lib()
+        ws = _lib.workspace(lib.gdd_propagate_relabeled_ws_bytes(n, adj_norm.nnz, d), X.device)
+        target = torch.empty_like(X)
+        p_last = torch.empty_like(X)
+        p_tmp = torch.empty_like(X) if T > 2 else None
+        _lib.check(lib.gdd_propagate_relabeled(
+            n, adj_norm.nnz, adj_norm.rowptr.data_ptr(), _lib.ptr(adj_norm.col),
+            _lib.ptr(adj_norm.values()), rho.data_ptr(), d, X.data_ptr(), int(T), float(alpha),
+            target.data_ptr(), p_last.data_ptr(), _lib.ptr(p_tmp), ws.data_ptr(), ws.numel(),
+            _lib.stream_ptr(X.device)))
+        return target, p_last
     lib, ws = _ws_propagate(adj_norm, d)
     target = torch.empty_like(X)
     p_last = torch.empty_like(X)

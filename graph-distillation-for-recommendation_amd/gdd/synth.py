@@ -86,6 +86,36 @@ def chung_lu_device(n: int, avg_degree: float, seed: int, device="cuda"):
     return CSRGraph(rowptr.to(torch.int32), col, None, n)
 
 
+def sbm_device(n: int, avg_degree: float, seed: int, block: int = 1024, p_in: float = 0.9,
+               shuffle: bool = True, device="cuda"):
+    """A community-structured graph (stochastic block model: blocks of `block` consecutive nodes, a
+    fraction p_in of each node's edges inside its block, the rest uniform), symmetric, binary, no
+    self-loops, sampled on the device. With `shuffle` the node ids are permuted at random, as real
+    graphs' ids carry no locality order. Returns a gdd CSRGraph."""
+    import torch
+    from .graph import CSRGraph
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    m = int(round(n * avg_degree / 2.0 * 1.04))
+    src = torch.randint(0, n, (m,), device=device, generator=g)
+    inside = torch.rand(m, device=device, generator=g) < p_in
+    b0 = (src // block) * block
+    bsz = torch.clamp(n - b0, max=block)
+    dst_in = b0 + (torch.rand(m, device=device, generator=g) * bsz).long().clamp(max=block - 1)
+    dst = torch.where(inside, torch.minimum(dst_in, torch.full_like(dst_in, n - 1)),
+                      torch.randint(0, n, (m,), device=device, generator=g))
+    if shuffle:
+        perm = torch.randperm(n, device=device, generator=g)
+        src, dst = perm[src], perm[dst]
+    keep = src != dst
+    src, dst = src[keep], dst[keep]
+    keys = torch.unique(torch.cat([src * n + dst, dst * n + src]))
+    rows, col = keys // n, (keys % n).to(torch.int32)
+    rowptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    rowptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n), 0)
+    return CSRGraph(rowptr.to(torch.int32), col, None, n)
+
+
 def uniform_graph(n: int, avg_degree: float, seed: int) -> sp.csr_matrix:
     """Erdős–Rényi-style symmetric binary graph (worst-case gather locality variant)."""
     rng = np.random.default_rng(seed)

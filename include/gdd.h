@@ -77,6 +77,17 @@ size_t gdd_propagate_ws_bytes(int64_t n, int64_t nnz, int d);
 int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* val,
                   int d, const float* X, int T, float alpha, float* target, float* p_last,
                   float* p_tmp, void* ws, size_t ws_bytes, gdd_stream_t stream);
+/* The same propagation with the intermediate hops in a relabelled node order (r05):  */
+/* rho (device, a permutation of [0, n)) gives node r's row of the intermediate p at rho[r] and the   */
+/* gathers after the first go through rho[col]; every row keeps its entries in CSR order, so target  */
+/* and p_last (both by the original ids: the first hop reads X by them, the last hop stores by them)  */
+/* are bit-identical to gdd_propagate's. A locality order (hubs first, RCM, communities) lets the    */
+/* gathered rows of a hop share cache lines and pages; no separate permutation pass.                  */
+size_t gdd_propagate_relabeled_ws_bytes(int64_t n, int64_t nnz, int d);
+int gdd_propagate_relabeled(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
+                            const float* val, const int32_t* rho, int d, const float* X, int T,
+                            float alpha, float* target, float* p_last, float* p_tmp, void* ws,
+                            size_t ws_bytes, gdd_stream_t stream);
 /* one hop: y = (scale * Â) @ x with the canonical order above; if acc != NULL also                   */
 /*   acc = acc + acc_scale * y  (two fp32 roundings, no contraction).                               */
 int gdd_spmm(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* val,

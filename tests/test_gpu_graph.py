@@ -130,3 +130,30 @@ def test_planned_hop_matches_oracle_and_accumulates(d):
         plan.hop(xd, y, 0.91, acc, 0.09)
         assert np.array_equal(y.cpu().numpy().view(np.uint32), y_ref.view(np.uint32))
         assert np.array_equal(acc.cpu().numpy().view(np.uint32), acc_ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("relabel", ["degree", "rcm", "random"])
+@pytest.mark.parametrize("d,T,alpha", [(128, 18, 0.91), (64, 5, 0.8), (41, 4, 0.95), (602, 3, 0.95),
+                                       (100, 2, 0.91), (3, 7, 0.8)])
+def test_propagate_relabeled_bitexact(relabel, d, T, alpha):
+    """gdd_propagate_relabeled: the intermediate hops in another node order (rows of
+    p at rho[r], gathers through rho[col], every row's entries in CSR order), the first hop reading
+    X and the last storing p_last by the original ids, target by them throughout — target and p_last
+    bit-identical to the oracle's, with the split hub row's fix-up and paired updates."""
+    n = 3000
+    A = _graph(n, 12.0, 5).tolil()
+    A[11, :] = 0
+    A[11, np.arange(0, n, 4)] = 1
+    A = sp.csr_matrix(A)
+    A.sort_indices()
+    rp, col, _ = _csr_host(A)
+    ro, co, vo = O.normalize_csr(rp, col, None, -1)
+    X = synth.features(n, d, 9)
+    t_ref, p_ref = O.propagate(ro, co, vo, X, T, alpha)
+    g = gdd.normalize_adj(gdd.to_csr(A))
+    rho = np.random.default_rng(1).permutation(n).astype(np.int32) if relabel == "random" else relabel
+    t, p = gdd.propagate(g, torch.from_numpy(X).cuda(), T, alpha, relabel=rho)
+    assert np.array_equal(t.cpu().numpy().view(np.uint32), t_ref.view(np.uint32))
+    assert np.array_equal(p.cpu().numpy().view(np.uint32), p_ref.view(np.uint32))
+    with pytest.raises(ValueError):
+        gdd.propagate(g, torch.from_numpy(X).cuda(), T, alpha, relabel=np.zeros(n, np.int32))

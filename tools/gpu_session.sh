@@ -85,6 +85,7 @@ for step in "$@"; do
     phases) run 300 phases python tools/phase_times.py ;;
     kpp) run 300 kpp python tools/micro_kpp.py ;;
     kpp-par) run 300 kpp_par python tools/micro_kpp.py par ;;
+    relabel) run 600 relabel python tools/micro_relabel.py ;;
     par-ab) run 900 par_ab bash -c 'for v in 0 1 0 1; do echo "GDD_KPP_PAR_CHAIN=$v"; GDD_KPP_PAR_CHAIN=$v python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done' ;;
     near-ab) run 900 near_ab bash -c 'for v in 0 3 6 0 3 6; do echo "GDD_MB_NEAR_STOP=$v"; GDD_MB_NEAR_STOP=$v python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done' ;;
     spec-ab) run 900 spec_ab bash -c 'python tools/micro_kpp.py spec && for v in 1 0 1 0; do echo "GDD_KPP_SPEC_SEARCH=$v"; export GDD_KPP_SPEC_SEARCH=$v; python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done' ;;
