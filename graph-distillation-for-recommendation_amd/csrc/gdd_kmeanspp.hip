@@ -1330,6 +1330,7 @@ struct Kpp1Args {
   int exact;             // cum_tol's mode
   int bsearch;           // 1: the folds' binary searches (GDD_KPP_BSEARCH, A/B); 0: two-ballot searches
   int spec_search;       // the folds' speculative searches, T <= 12 (GDD_KPP_SPEC_SEARCH=0 turns them off)
+  int par_chain;         // k_kpp1_big: block 0's lane chains by the exact parallel runs (r05)
 };
 
 __device__ __forceinline__ int kpp1_argmin(const float* __restrict__ pot, int T) {
@@ -1729,12 +1730,20 @@ struct ParLane {     // one precompute lane's result (LDS)
   int kind;          // 0 no crossing, 1 contiguous crossing entries, 2 walked serially
 };
 
-// waves 4..7 of a 512-thread fold: lane p = tid - 256 owns segment g of chain c
-__device__ __forceinline__ void par_chain_lanes(const float* __restrict__ s_ch,
+// chain c's entry m: S == 0 chain-major rows (s_ch + c kChainLd + m, the pair launches), S > 0 the
+// natural LDS row (base + c + S m, k_kpp1_big's sgemv_t blocks)
+template <int S>
+__device__ __forceinline__ const float* par_chain_src(const float* base, int c) {
+  return S == 0 ? base + c * kChainLd : base + c;
+}
+
+// 256 lanes (p = 0..255, four whole waves) precompute nl chains: lane p owns segment g of chain c.
+// L = (m1 - h4 - c + nl - 1) / nl entries per chain; acc0 the chain's start value (s_d[c] for c < h4)
+template <int S>
+__device__ __forceinline__ void par_chain_lanes(int p, const float* __restrict__ base,
                                                 const float* __restrict__ s_d, int nl, int h4, int m1,
                                                 ParLane* __restrict__ s_par,
                                                 unsigned long long* __restrict__ s_mask) {
-  const int p = (int)threadIdx.x - 256;
   const int G = 256 / nl;  // 32 (nl = 8) or 64 (nl = 4): within one wave
   const int c = p / G, g = p - c * G;
   const int L = max((m1 - h4 - c + nl - 1) / nl, 0);
@@ -1742,18 +1751,23 @@ __device__ __forceinline__ void par_chain_lanes(const float* __restrict__ s_ch,
   const int seg = min(kParMaxSeg, ((L - H + G - 1) / G + 3) & ~3);
   const int a = H + g * seg;
   const int cnt = max(0, min(seg, L - a));
-  const float* src = s_ch + c * kChainLd;
+  const float* src = par_chain_src<S>(base, c);
   float x[kParMaxSeg];
+  if constexpr (S == 0) {
 #pragma unroll
-  for (int q = 0; q < kParMaxSeg / 4; ++q) {  // a is a multiple of 4; reads stay inside the padded row
-    const float4 v = *reinterpret_cast<const float4*>(src + min(a, 1024) + 4 * q);
-    x[4 * q] = v.x;
-    x[4 * q + 1] = v.y;
-    x[4 * q + 2] = v.z;
-    x[4 * q + 3] = v.w;
+    for (int q = 0; q < kParMaxSeg / 4; ++q) {  // a is a multiple of 4; reads stay inside the padded row
+      const float4 v = *reinterpret_cast<const float4*>(src + min(a, 1024) + 4 * q);
+      x[4 * q] = v.x;
+      x[4 * q + 1] = v.y;
+      x[4 * q + 2] = v.z;
+      x[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < kParMaxSeg; ++q) x[q] = src[S * min(a + q, max(L - 1, 0))];
   }
   const float acc0 = c < h4 ? s_d[c] : 0.f;
-  float hx = g < H ? src[g] : 0.f;  // head entries, one per lane (G >= kParHead)
+  float hx = g < H ? src[S == 0 ? g : S * g] : 0.f;  // head entries, one per lane (G >= kParHead)
   float loc[kParMaxSeg];
   float run = 0.f;
 #pragma unroll
@@ -1834,7 +1848,9 @@ __device__ __forceinline__ void par_chain_lanes(const float* __restrict__ s_ch,
   if (g == 0) s_mask[c] = gm;
 }
 
-// wave 0's lane c < nl: the chain's exact value from the head result s and the published runs
+// the walker (lane c < nl of one wave): the chain's exact value from the head result s and the
+// published runs; src = chain c's first entry (stride S, or contiguous for S == 0)
+template <int S = 0>
 __device__ __forceinline__ float par_chain_walk(const float* __restrict__ src, int c, int nl, float s,
                                                 const ParLane* __restrict__ s_par,
                                                 const unsigned long long* __restrict__ s_mask, bool& ok) {
@@ -1847,7 +1863,7 @@ __device__ __forceinline__ float par_chain_walk(const float* __restrict__ src, i
     if (q > 0) ok = par_apply(ParT{rl[q - 1].ie, rl[q - 1].id0, rl[q - 1].id1}, s) && ok;
     const ParLane r = rl[q];
     if (r.kind == 1) ok = par_apply(ParT{r.ae, r.ad0, r.ad1}, s) && ok;
-    for (int i = r.x0; i < r.x1; ++i) s = s + src[i];
+    for (int i = r.x0; i < r.x1; ++i) s = s + src[S == 0 ? i : S * i];
   }
   ok = par_apply(ParT{rl[G - 1].ie, rl[G - 1].id0, rl[G - 1].id1}, s) && ok;
   return s;
@@ -1967,7 +1983,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
     GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 76);
   } else if (PAR && wave >= 4) {  // the lane chains' runs (par_chain_lanes)
     if (par) {
-      par_chain_lanes(s_ch, s_d, k4x2 ? 4 : 8, h4, m1, s_par, s_pmask);
+      par_chain_lanes<0>((int)threadIdx.x - 256, s_ch, s_d, k4x2 ? 4 : 8, h4, m1, s_par, s_pmask);
       waves_arrive(&s_parsync);
     }
   } else {  // the cumulative potential: thread runs and the wave's inclusive scan
@@ -2529,6 +2545,7 @@ __global__ __launch_bounds__(64) void k_kpp1_final(Kpp1Args a, int c) {
 //            walk (LDS add); a prefix within cum_tol of the threshold replays numpy's left-to-right sum.
 // Round 0 (c == 0, one workgroup) draws round 1's candidates from the first centre's closest0 and
 // its sdot potential. LDS: the row, 4 * (1024 * EPT + kChainPad) bytes (dynamic).
+constexpr int kParMinBlock = 2048;  // k_kpp1_big: block 0 of at least this many entries takes the runs
 constexpr int kBigThr = 1024;
 constexpr int kBigWaves = kBigThr / 64;
 constexpr int64_t kBig1Max = 32768;
@@ -2599,6 +2616,35 @@ __device__ __forceinline__ float sgemv_block_lds(const float* __restrict__ s, co
   return (ql + q1) + (q2 + q3);
 }
 
+// sgemv_block_lds's unit-weight block 0 (entries [0, NB)) with the exact parallel lane chains:
+// this wave's lanes < nl add each chain's head and walk the runs that waves kBigWaves - 4 .. 15
+// (par_chain_lanes<nl>, the natural row at stride nl) published; a failed check: the plain chain
+template <int NL>
+__device__ __forceinline__ float sgemv_block0_par(const float* __restrict__ s, int NB, bool k4x2,
+                                                  int* s_parsync, const ParLane* __restrict__ s_par,
+                                                  const unsigned long long* __restrict__ s_pmask) {
+  const int lane = threadIdx.x & 63;
+  const int h4 = k4x2 ? 0 : (NB & 4);
+  const float* base = s + h4;
+  const int L = lane < NL ? max((NB - h4 - lane + NL - 1) / NL, 0) : 0;
+  float acc0 = 0.f;
+  if (lane < h4) acc0 = __builtin_fmaf(s[lane], 1.0f, acc0);
+  float acc = 0.f;
+  if (lane < NL) acc = chain_unit_lds<NL>(base + lane, min(L, kParHead), acc0);
+  bool ok = waves_wait(s_parsync, 4);
+  if (lane < NL) {
+    const float r = par_chain_walk<NL>(base + lane, lane, NL, acc, s_par, s_pmask, ok);
+    acc = ok ? r : chain_unit_lds<NL>(base + lane, L, acc0);
+  }
+  if (k4x2) {
+    const float a1 = __shfl(acc, 1), a2 = __shfl(acc, 2), a3 = __shfl(acc, 3);
+    return (acc + a1) + (a2 + a3);
+  }
+  const float ql = acc + __shfl(acc, (lane + 4) & 63);
+  const float q1 = __shfl(ql, 1), q2 = __shfl(ql, 2), q3 = __shfl(ql, 3);
+  return (ql + q1) + (q2 + q3);
+}
+
 __device__ __forceinline__ double readlane_f64(double v, int l) {
   const unsigned long long b = __double_as_longlong(v);
   const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
@@ -2620,12 +2666,21 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   __shared__ int s_sidx[kMaxTrials];    // speculative draws: counts (-1: not usable)
   __shared__ double s_lo[kMaxTrials], s_hi[kMaxTrials];  // and their deciding neighbours
   __shared__ unsigned long long s_redo;  // the uniforms the regular draws take
+  constexpr bool kParOk = EPT <= 16;     // EPT = 32: no LDS to spare (132 KB of row)
+  __shared__ ParLane s_par[kParOk ? 256 : 1];  // exact parallel chains of block 0 (r05)
+  __shared__ unsigned long long s_pmask[8];
+  __shared__ int s_parsync;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = a.T;
   const int n = (int)a.n, m1 = (int)a.m1;
   const int t = blockIdx.x;
   const int cq = c & 1, pq = (c - 1) & 1;
   const int nsg = (m1 + kBlk - 1) / kBlk;  // chain waves (4096-entry sgemv_t blocks)
+  const bool k4x2 = (T & 2) && t >= (T & ~3) && t < (T & ~3) + 2;
+  // block 0's lane chains by the exact parallel runs (a.par_chain) when four waves are free of the
+  // chains and the speculative draws, the weights are unit and the chains are long enough to pay
+  const bool par = kParOk && a.par_chain && c >= 1 && a.w == nullptr && min(kBlk, m1) >= kParMinBlock &&
+                   nsg + T <= kBigWaves - 4;
   // speculative draws (r04): waves nsg .. nsg + T - 1 draw round c+1's candidates while waves < nsg
   // run the lane chains, the fp64 total standing in for the potential; checked after it (below)
   const bool spec = a.spec_search && c >= 1 && c + 1 < a.k && nsg + T <= kBigWaves;
@@ -2635,7 +2690,10 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
     s_part[tid] = 0;
     s_amb[tid] = 0;
   }
-  if (tid == 0) s_arr = 0;
+  if (tid == 0) {
+    s_arr = 0;
+    s_parsync = 0;
+  }
   // ---- trip 1, every load at once (lane q): round c-1's potential q, this slot's candidate if q
   // won, q's own candidate, round c+1's uniform q
   const double ut = (c + 1 < a.k && lane < T) ? a.uniforms[(int64_t)c * T + lane] : 0.0;
@@ -2724,8 +2782,27 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   // the sgemv_t block terms (rounds >= 1)
   if (c >= 1 && wave < nsg) {
     const int j0 = wave * kBlk;
-    const float vb = sgemv_block_lds(s_row, a.w, j0, min(kBlk, m1 - j0), t, T);
+    float vb;
+    if constexpr (kParOk) {
+      if (par && wave == 0)
+        vb = k4x2 ? sgemv_block0_par<4>(s_row, min(kBlk, m1), true, &s_parsync, s_par, s_pmask)
+                  : sgemv_block0_par<8>(s_row, min(kBlk, m1), false, &s_parsync, s_par, s_pmask);
+      else
+        vb = sgemv_block_lds(s_row, a.w, j0, min(kBlk, m1 - j0), t, T);
+    } else {
+      vb = sgemv_block_lds(s_row, a.w, j0, min(kBlk, m1 - j0), t, T);
+    }
     if (lane == 0) s_vb[wave] = vb;
+  } else if (par && wave >= kBigWaves - 4) {  // block 0's runs for the walk above
+    if constexpr (kParOk) {
+      const int NB = min(kBlk, m1), h4 = k4x2 ? 0 : (NB & 4);
+      const int p = tid - 64 * (kBigWaves - 4);
+      if (k4x2)
+        par_chain_lanes<4>(p, s_row + h4, s_row, 4, h4, NB, s_par, s_pmask);
+      else
+        par_chain_lanes<8>(p, s_row + h4, s_row, 8, h4, NB, s_par, s_pmask);
+      waves_arrive(&s_parsync);
+    }
   } else if (spec && wave - nsg < T) {
     // searchsorted_left(cum, u * pot_s), pot_s = fp32(fp64 total), without the rounding check (the
     // check after the potential decides): the wave totals' running sum finds the group of 64
@@ -3419,6 +3496,8 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       {
         const char* ss = getenv("GDD_KPP_SPEC_SEARCH");  // 0 off (the regular draws)
         b1.spec_search = (ss && ss[0] == '0') ? 0 : 1;
+        const char* pce = getenv("GDD_KPP_PAR_CHAIN");
+        b1.par_chain = (pce ? pce[0] == '1' : kParChainDefault) ? 1 : 0;
       }
       void (*big)(Kpp1Args, const float*, int) = nullptr;
       int ept = 0;

@@ -334,3 +334,26 @@ def test_kmeans_plusplus_parallel_chains(monkeypatch, case, n, dim, k):
         c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(15))
         assert np.array_equal(idx.cpu().numpy(), idx_ref), val
         assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref)), val
+
+
+@pytest.mark.parametrize("case", ["blobs", "integers", "dupes", "range"])
+@pytest.mark.parametrize("n,dim,k", [(6040, 64, 604), (9001, 24, 200), (12003, 7, 120), (5003, 33, 60)])
+def test_kmeans_plusplus_big_rounds_parallel_chains(monkeypatch, case, n, dim, k):
+    """k_kpp1_big (one 1024-thread workgroup per trial) with block 0's lane chains by the exact
+    parallel runs (GDD_KPP_PAR_CHAIN=1: four spare waves precompute, block 0's wave walks; the
+    natural LDS row at stride 8, or 4 for the 4-lane trials) equals the sequential chains and the
+    oracle (where run) bit for bit."""
+    X = _par_case_points(case, n, dim, n + dim + k)
+    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")
+    out = {}
+    for val in ("1", "0"):
+        monkeypatch.setenv("GDD_KPP_PAR_CHAIN", val)
+        c, idx = _Ops("cuda", n, k, dim).kmeans_plusplus(torch.from_numpy(X).cuda(), k,
+                                                         np.random.RandomState(15))
+        out[val] = (idx.cpu().numpy(), bits(c.cpu().numpy()))
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert np.array_equal(out["1"][1], out["0"][1])
+    if n * k <= 6040 * 604:
+        c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
+        assert np.array_equal(out["1"][0], idx_ref)
+        assert np.array_equal(out["1"][1], bits(c_ref))

@@ -91,7 +91,8 @@ def ab_spec():
 def ab_par():
     """The exact parallel lane chains (GDD_KPP_PAR_CHAIN=1, 512-thread pair launches) against the
     sequential lane chains (=0), same process, parity checked on the first pass of each."""
-    for (n, dim, k) in [(3000, 40, 454), (3706, 64, 371), (2708, 7, 70), (3000, 41, 769)]:
+    for (n, dim, k) in [(3000, 40, 454), (3706, 64, 371), (2708, 7, 70), (3000, 41, 769),
+                        (6040, 64, 604), (9001, 24, 200)]:
         for i, val in enumerate(("0", "1", "0", "1")):
             os.environ["GDD_KPP_PAR_CHAIN"] = val
             print(f"variant GDD_KPP_PAR_CHAIN={val}:", end=" ", flush=True)
