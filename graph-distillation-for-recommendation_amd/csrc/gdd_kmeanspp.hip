@@ -588,6 +588,7 @@ struct KppArgs {
   SklPlan plan;
   int exact;          // cum_tol's mode
   const float* D;     // the n x n distance table (plain-chain plans, n <= kDmBigMax), or nullptr
+  int par_chain;      // the block terms' lane chains by the exact parallel runs (r05)
 };
 
 __device__ __forceinline__ float wv(const float* w, int64_t i) { return w ? w[i] : 1.0f; }
@@ -908,6 +909,60 @@ __device__ float sgemv_block_wave(const float* __restrict__ s_d, const float* __
   return (ql + q1) + (q2 + q3);
 }
 
+// the exact parallel sgemv_t lane chains (r05): types and run algebra; the method is described with
+// par_chain_lanes below
+constexpr int kParHead = 32;     // entries of each chain the walker adds serially first
+constexpr int kParMaxSeg = 16;   // entries per precompute lane (nl = 4: 64 lanes x 16 >= 1024 - 32)
+constexpr int kParIdE = -1;      // identity run
+constexpr int kParBadE = -2;     // two runs in different binades (never built: a failed check)
+constexpr int kParMinBlock = 2048;  // sgemv_t blocks of at least this many entries take the runs
+
+struct ParT {
+  int e, d0, d1;  // biased exponent field of the binade, advances from even / odd s/u
+};
+
+__device__ __forceinline__ ParT par_compose(ParT A, ParT B) {  // A, then B
+  if (A.e == kParIdE) return B;
+  if (B.e == kParIdE) return A;
+  if (A.e != B.e) return ParT{kParBadE, 0, 0};
+  ParT C;
+  C.e = A.e;
+  C.d0 = A.d0 + ((A.d0 & 1) ? B.d1 : B.d0);  // even start: parity after A is A.d0's
+  C.d1 = A.d1 + ((A.d1 & 1) ? B.d0 : B.d1);  // odd start: parity after A is 1 + A.d1's
+  return C;
+}
+
+// s (the exact running value) advanced by run T; false when s is not in T's binade or the run would
+// carry it out (then s is left as it was)
+__device__ __forceinline__ bool par_apply(ParT T, float& s) {
+  if (T.e == kParIdE) return true;
+  const int bs = __float_as_int(s);
+  if ((bs >> 23) != T.e) return false;  // also s < 0, and kParBadE (never an exponent field)
+  const int nb = bs + ((bs & 1) ? T.d1 : T.d0);
+  if ((nb >> 23) != T.e) return false;
+  s = __int_as_float(nb);
+  return true;
+}
+
+struct ParLane {     // one precompute lane's result (LDS)
+  int ae, ad0, ad1;  // its runs before its crossing entries (all of them when it has none)
+  int ie, id0, id1;  // the segmented inclusive scan up to and including this lane
+  int x0, x1;        // chain positions added in hardware by the walker
+  int kind;          // 0 no crossing, 1 contiguous crossing entries, 2 walked serially
+};
+
+// defined with the pair launches' folds below
+template <int S>
+__device__ __forceinline__ void par_chain_lanes(int p, const float* __restrict__ base,
+                                                const float* __restrict__ s_d, int nl, int h4, int m1,
+                                                ParLane* __restrict__ s_par,
+                                                unsigned long long* __restrict__ s_mask);
+template <int NL>
+__device__ __forceinline__ float sgemv_block0_par(const float* __restrict__ s, int NB, bool k4x2,
+                                                  int* s_parsync, const ParLane* __restrict__ s_par,
+                                                  const unsigned long long* __restrict__ s_pmask);
+__device__ __forceinline__ void waves_arrive(int* ctr);
+
 // ---- one seeding round ------------------------------------------------------------------------------
 template <bool SEQ, bool PICK = false>
 __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
@@ -918,13 +973,19 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   __shared__ double s_P, s_tot;
   __shared__ int s_cnt[kWaves], s_amb[kWaves];
   __shared__ int64_t s_ct;
+  __shared__ ParLane s_par[PICK ? 1 : 256];  // the block terms' parallel lane chains (r05)
+  __shared__ unsigned long long s_pmask[8];
+  __shared__ int s_parsync;
   const int t = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int pq = (c - 1) & 1, cq = c & 1;
   const int64_t n = a.n;
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 20);
   const double u = a.uniforms[(int64_t)(c - 1) * a.T + t];
-  if (tid == 0) s_jmin = INT_MAX;
+  if (tid == 0) {
+    s_jmin = INT_MAX;
+    s_parsync = 0;
+  }
   // ---- fold round c-1 (round 0: the first centre)
   int bw = 0;
   float pot;
@@ -1128,9 +1189,26 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     if (tid == (int)(last / kPer)) a.fsum[cq][(int64_t)t * a.nblk + blk] = pre[last % kPer];
   }
   const int64_t NB = min<int64_t>(kBlk, a.m1 - j0);
+  // the block's lane chains by the exact parallel runs (waves 12..15 precompute, wave 0 walks) when
+  // the weights are unit and the chains are long enough to pay
+  const bool par = !PICK && a.par_chain && a.w == nullptr && NB >= kParMinBlock && a.T > 1;
+  const bool k4x2 = (a.T & 2) && t >= (a.T & ~3) && t < (a.T & ~3) + 2;
   if (NB > 0 && a.T > 1 && wave == 0) {
-    const float v = sgemv_block_wave(s_d, a.w ? a.w + j0 : nullptr, NB, t, a.T);
+    float v;
+    if (par)
+      v = k4x2 ? sgemv_block0_par<4>(s_d, (int)NB, true, &s_parsync, s_par, s_pmask)
+               : sgemv_block0_par<8>(s_d, (int)NB, false, &s_parsync, s_par, s_pmask);
+    else
+      v = sgemv_block_wave(s_d, a.w ? a.w + j0 : nullptr, NB, t, a.T);
     if (lane == 0) a.vblk[cq][(int64_t)t * a.nblk + blk] = v;
+  } else if (par && wave >= kWaves - 4) {
+    const int h4 = k4x2 ? 0 : (int)(NB & 4);
+    const int p = tid - 64 * (kWaves - 4);
+    if (k4x2)
+      par_chain_lanes<4>(p, s_d + h4, s_d, 4, h4, (int)NB, s_par, s_pmask);
+    else
+      par_chain_lanes<8>(p, s_d + h4, s_d, 8, h4, (int)NB, s_par, s_pmask);
+    waves_arrive(&s_parsync);
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 25);
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0 && c < 128), 128 + c);
@@ -1691,44 +1769,6 @@ __device__ __forceinline__ bool prefix_waves_sync(int* ctr, int target) {
 // while waves 4..7 (256 / nl lanes per chain, <= kParMaxSeg entries each) classify the rest, evaluate
 // their runs from 2^e and 2^e + u, and compose them with a segmented scan that restarts after every
 // crossing; lane c then applies the composed runs and adds only the crossing entries.
-constexpr int kParHead = 32;     // entries of each chain the walker adds serially first
-constexpr int kParMaxSeg = 16;   // entries per precompute lane (nl = 4: 64 lanes x 16 >= 1024 - 32)
-constexpr int kParIdE = -1;      // identity run
-constexpr int kParBadE = -2;     // two runs in different binades (never built: a failed check)
-
-struct ParT {
-  int e, d0, d1;  // biased exponent field of the binade, advances from even / odd s/u
-};
-
-__device__ __forceinline__ ParT par_compose(ParT A, ParT B) {  // A, then B
-  if (A.e == kParIdE) return B;
-  if (B.e == kParIdE) return A;
-  if (A.e != B.e) return ParT{kParBadE, 0, 0};
-  ParT C;
-  C.e = A.e;
-  C.d0 = A.d0 + ((A.d0 & 1) ? B.d1 : B.d0);  // even start: parity after A is A.d0's
-  C.d1 = A.d1 + ((A.d1 & 1) ? B.d0 : B.d1);  // odd start: parity after A is 1 + A.d1's
-  return C;
-}
-
-// s (the exact running value) advanced by run T; false when s is not in T's binade or the run would
-// carry it out (then s is left as it was)
-__device__ __forceinline__ bool par_apply(ParT T, float& s) {
-  if (T.e == kParIdE) return true;
-  const int bs = __float_as_int(s);
-  if ((bs >> 23) != T.e) return false;  // also s < 0, and kParBadE (never an exponent field)
-  const int nb = bs + ((bs & 1) ? T.d1 : T.d0);
-  if ((nb >> 23) != T.e) return false;
-  s = __int_as_float(nb);
-  return true;
-}
-
-struct ParLane {     // one precompute lane's result (LDS)
-  int ae, ad0, ad1;  // its runs before its crossing entries (all of them when it has none)
-  int ie, id0, id1;  // the segmented inclusive scan up to and including this lane
-  int x0, x1;        // chain positions added in hardware by the walker
-  int kind;          // 0 no crossing, 1 contiguous crossing entries, 2 walked serially
-};
 
 // chain c's entry m: S == 0 chain-major rows (s_ch + c kChainLd + m, the pair launches), S > 0 the
 // natural LDS row (base + c + S m, k_kpp1_big's sgemv_t blocks)
@@ -2545,7 +2585,6 @@ __global__ __launch_bounds__(64) void k_kpp1_final(Kpp1Args a, int c) {
 //            walk (LDS add); a prefix within cum_tol of the threshold replays numpy's left-to-right sum.
 // Round 0 (c == 0, one workgroup) draws round 1's candidates from the first centre's closest0 and
 // its sdot potential. LDS: the row, 4 * (1024 * EPT + kChainPad) bytes (dynamic).
-constexpr int kParMinBlock = 2048;  // k_kpp1_big: block 0 of at least this many entries takes the runs
 constexpr int kBigThr = 1024;
 constexpr int kBigWaves = kBigThr / 64;
 constexpr int64_t kBig1Max = 32768;
@@ -3274,6 +3313,8 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   {  // cum_tol's mode: GDD_KPP_EXACT=0 (never replay; tests only) / 2 (always replay)
     const char* ex = getenv("GDD_KPP_EXACT");
     a.exact = ex ? atoi(ex) : 1;
+    const char* pce = getenv("GDD_KPP_PAR_CHAIN");
+    a.par_chain = (pce ? pce[0] == '1' : kParChainDefault) ? 1 : 0;
   }
   const SklPlan p1{n, skl_batch_size(1, n, dim), 1, dim, 0, 0};
   const size_t lds = sizeof(double) * (size_t)dim + sizeof(float) * kBlk;

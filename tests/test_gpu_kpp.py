@@ -357,3 +357,26 @@ def test_kmeans_plusplus_big_rounds_parallel_chains(monkeypatch, case, n, dim, k
         c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
         assert np.array_equal(out["1"][0], idx_ref)
         assert np.array_equal(out["1"][1], bits(c_ref))
+
+
+@pytest.mark.parametrize("case", ["blobs", "integers", "range"])
+@pytest.mark.parametrize("n,dim,k,env", [(6040, 64, 604, ("GDD_KPP_NO_BIG1",)),
+                                         (17730, 64, 300, ()),  # Ali-Display users' n: per-block rounds
+                                         (9001, 24, 200, ("GDD_KPP_NO_BIG1",)),
+                                         (8195, 5, 30, ("GDD_KPP_NO_TABLE",))])  # distances per round
+def test_kmeans_plusplus_block_rounds_parallel_chains(monkeypatch, case, n, dim, k, env):
+    """The per-(block, trial) rounds (k_kpp_round) with each block's lane chains by the exact
+    parallel runs (GDD_KPP_PAR_CHAIN=1: waves 12..15 precompute, wave 0 walks) equal the sequential
+    chains bit for bit, with and without the distance table."""
+    X = _par_case_points(case, n, dim, n + dim + k + 1)
+    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")
+    for var in env:
+        monkeypatch.setenv(var, "1")
+    out = {}
+    for val in ("1", "0"):
+        monkeypatch.setenv("GDD_KPP_PAR_CHAIN", val)
+        c, idx = _Ops("cuda", n, k, dim).kmeans_plusplus(torch.from_numpy(X).cuda(), k,
+                                                         np.random.RandomState(15))
+        out[val] = (idx.cpu().numpy(), bits(c.cpu().numpy()))
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert np.array_equal(out["1"][1], out["0"][1])
