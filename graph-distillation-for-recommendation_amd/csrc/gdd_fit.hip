@@ -142,6 +142,7 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t i
   GDD_HIP(hipMemcpyAsync(w.mtb + (i0 + 2) % 3, h_mt, sizeof(DevMT), hipMemcpyHostToDevice, s));
   int rc = mb_rng_launch(w.mtb + (i0 + 2) % 3, w.mtb + i0 % 3, n, bs, w.rows_d + (i0 & 1) * bs, s);
   if (rc) return rc;
+  const int64_t seg0 = i0;  // the chunk lambda below has a parameter of that name
   rc = mb_loop_begin(bs, k, w.step_ws, w.step_bytes, s);
   if (rc) return rc;
   const bool reassign = reassignment_ratio > 0.f;
@@ -183,8 +184,10 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t i
       const RngNext next{mt_cur, mt_nxt, rows_nxt, n, bs};
       float* c_old = w.C[st % 2];
       float* c_new = w.C[(st + 1) % 2];
-      const int flags = GDD_STEP_CONVERGE | ((st > i0 || norms_valid0) ? GDD_STEP_NORMS_VALID : 0) |
-                        ((st == i0 && i0 > 0) ? kStepNoTail : 0);
+      // seg0 (the segment's first step), not this chunk's i0: only the segment's first step has no
+      // tail (its predecessor's convergence test ran on the host)
+      const int flags = GDD_STEP_CONVERGE | ((st > seg0 || norms_valid0) ? GDD_STEP_NORMS_VALID : 0) |
+                        ((st == seg0 && seg0 > 0) ? kStepNoTail : 0);
       int rc2 = minibatch_step_dev(bs, dim, X, rows_cur, k, c_old, c_new, w.counts, w.labels_b, (int)st,
                                    n, max_no_improvement, flags, w.state, w.step_ws, w.step_bytes,
                                    has_next ? next : none, cs);  // at reassignment steps: speculative
