@@ -187,3 +187,57 @@ def test_ranks_row_partitioned_propagate_matches_one(world, T):
         p = np.load(os.path.join(out, f"g{r}.npz"))
         assert np.array_equal(_bits(p["target"]), _bits(t1.cpu().numpy()))
         assert np.array_equal(_bits(p["p_last"]), _bits(p1.cpu().numpy()))
+
+
+def _nccl_worker(rank, world, port, X, feat, out):
+    sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE),
+                                                          "graph-distillation-for-recommendation_amd"), HERE]
+    os.environ["GDD_SHARD_LLOYD"] = "1"
+    os.environ["GDD_SHARD_PROP"] = "1"
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    import gdd as G
+    from gdd.sharded import ShardedKMeans as SK
+    dev = torch.device("cuda", rank)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    g = dist.group.WORLD
+    res = {}
+    for split in (False, True):
+        np.random.seed(15)
+        m = SK(n_clusters=40, device=dev, group=g, split_columns=split).fit(X)
+        res.update({f"labels{int(split)}": m.labels_, f"centers{int(split)}": m.cluster_centers_,
+                    f"n_iter{int(split)}": m.n_iter_, f"inertia{int(split)}": m.inertia_})
+    A = synth.chung_lu(6000, 12.0, 3)
+    gn = G.normalize_adj(G.to_csr(A, device=dev))
+    t, p = G.propagate(gn, torch.from_numpy(feat).to(dev), 5, 0.9, group=g)
+    res.update(target=t.cpu().numpy(), p_last=p.cpu().numpy())
+    np.savez(os.path.join(out, f"n{rank}.npz"), **res)
+    dist.destroy_process_group()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL needs one GPU per rank (2 GPUs)")
+def test_two_ranks_rccl_match_one():
+    """the RCCL branches (in-place slot all-gathers of ShardedKMeans' phase loop, with and
+    without the column split, and the row-partitioned propagation's per-hop all-gathers into the
+    persistent buffers), two ranks on two GPUs, bit-identical to one GPU. Skipped on one-GPU boxes."""
+    X = synth.blobs(20000, 24, 40, seed=4)
+    X[1::9] = X[0]
+    feat = synth.features(6000, 100, 6)
+    np.random.seed(15)
+    one = gdd.KMeans(n_clusters=40).fit(X)
+    gn = gdd.normalize_adj(gdd.to_csr(synth.chung_lu(6000, 12.0, 3)))
+    t1, p1 = gdd.propagate(gn, torch.from_numpy(feat).cuda(), 5, 0.9)
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"gdd_rccl_{os.getpid()}")
+    os.makedirs(out, exist_ok=True)
+    mp.spawn(_nccl_worker, args=(2, free_port(), X, feat, out), nprocs=2, join=True)
+    for r in range(2):
+        p = np.load(os.path.join(out, f"n{r}.npz"))
+        for s in ("0", "1"):
+            assert int(p["n_iter" + s]) == one.n_iter_
+            assert np.array_equal(p["labels" + s], one.labels_)
+            assert np.array_equal(_bits(p["centers" + s]), _bits(one.cluster_centers_))
+            assert float(p["inertia" + s]) == one.inertia_
+        assert np.array_equal(_bits(p["target"]), _bits(t1.cpu().numpy()))
+        assert np.array_equal(_bits(p["p_last"]), _bits(p1.cpu().numpy()))
