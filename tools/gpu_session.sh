@@ -82,6 +82,11 @@ for step in "$@"; do
         run 300 pmcp_${form}_write env $E rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcp_$form/pmc_write" -o hop -- python3 tools/micro_prop.py products
         run 300 pmcp_${form}_hit env $E rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmcp_$form/pmc_hit" -o hop -- python3 tools/micro_prop.py products
       done ;;
+    pmc-prod)  # the products hop's counters, default form only (three separate passes)
+      E="GDD_PROP_PAIR=0"
+      run 300 pmcp_fetch env $E rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcp/pmc_fetch" -o hop -- python3 tools/micro_prop.py products
+      run 300 pmcp_write env $E rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcp/pmc_write" -o hop -- python3 tools/micro_prop.py products
+      run 300 pmcp_hit env $E rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmcp/pmc_hit" -o hop -- python3 tools/micro_prop.py products ;;
     phases) run 300 phases python tools/phase_times.py ;;
     kpp) run 300 kpp python tools/micro_kpp.py ;;
     kpp-par) run 300 kpp_par python tools/micro_kpp.py par ;;

@@ -13,9 +13,15 @@ from gdd import synth  # noqa: E402
 
 def main(cfg_name="arxiv", reps=10):
     cfg = synth.CONFIGS[cfg_name]
-    A = synth.chung_lu(cfg.n, cfg.avg_degree, cfg.seed)
-    X = torch.from_numpy(synth.features(cfg.n, cfg.d, cfg.seed)).cuda()
-    gn = gdd.normalize_adj(gdd.to_csr(A))
+    if cfg.n > 1_000_000:  # the host generator needs minutes at the products shape
+        g = synth.chung_lu_device(cfg.n, cfg.avg_degree, cfg.seed)
+        gen = torch.Generator(device="cuda")
+        gen.manual_seed(cfg.seed)
+        X = torch.randn(cfg.n, cfg.d, device="cuda", generator=gen)
+    else:
+        g = gdd.to_csr(synth.chung_lu(cfg.n, cfg.avg_degree, cfg.seed))
+        X = torch.from_numpy(synth.features(cfg.n, cfg.d, cfg.seed)).cuda()
+    gn = gdd.normalize_adj(g)
     for _ in range(2):
         gdd.propagate(gn, X, cfg.T, cfg.alpha)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
