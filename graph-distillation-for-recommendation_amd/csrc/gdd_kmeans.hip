@@ -2647,6 +2647,24 @@ __global__ __launch_bounds__(1024) void k_mb_rng(const DevMT* __restrict__ in, D
   mt_randint_from(in, ring, 0, n, bs, rows, out);
 }
 
+constexpr int kRsBlockShuffle = 1;  // k_mb_reassign: the shuffle's draws by the whole block
+constexpr int kRsParCopy = 2;       // row copies in three block trips beside a one-wave next draw
+
+// LDS arrival counters among some of a workgroup's waves (the others busy elsewhere): every
+// arriving wave's earlier LDS and global writes are visible to a wave whose wait returned true;
+// false if the bounded spin gave up
+__device__ __forceinline__ void waves_arrive_rs(int* ctr) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool waves_wait_rs(int* ctr, int target) {
+  for (int it = 0; it < (1 << 16); ++it) {
+    if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+
 // The reassignment branch of _mini_batch_step (sklearn/cluster/_kmeans.py:1640-1667) at a step
 // the host scheduled (_random_reassign :2029-2043), one workgroup, after that step's update:
 //   to = counts < fp32(ratio) * max(counts); with m = |to| > 0:
@@ -2665,7 +2683,7 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
     int step, int64_t bs, int dim, int k, float ratio, const float* __restrict__ X,
     const int64_t* __restrict__ rows, float* __restrict__ C_new, float* __restrict__ counts,
     float* __restrict__ cn2, const DevMT* __restrict__ mt_in, DevMT* __restrict__ mt_mid,
-    RngNext rn, MBState* __restrict__ mbs) {
+    RngNext rn, MBState* __restrict__ mbs, int form) {
   int32_t* stop = &mbs->stop_at;
   if (stopped(stop, step)) return;
 #ifdef GDD_STAMPS
@@ -2675,12 +2693,16 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
 #define RS_STAMP(q) do {} while (0)
 #endif
   GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 40);
-  extern __shared__ int J[];  // bs shuffle draws, then the reassigned clusters in order (k ints)
+  extern __shared__ __attribute__((aligned(16))) int J[];  // bs shuffle draws, then the reassigned clusters in order (k ints)
   __shared__ MTScratch ms;
   __shared__ float s_thr, s_min;
   __shared__ int s_m;
+  __shared__ int s_sync[2], s_bad;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = blockDim.x >> 6;
   int* s_list = J + ((bs + 1) & ~1ll);
+  uint32_t* ring = reinterpret_cast<uint32_t*>(s_list + k);  // + 64 ints of scratch
+  if (t < 2) s_sync[t] = 0;
+  if (t == 0) s_bad = 0;
   // the key block's loads go out with wave 0's loads of the counts
   const uint32_t kreg = t < 624 ? mt_in->key[t] : 0u;
   const int preg = mt_in->pos;
@@ -2720,7 +2742,10 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
       s_m = base;
     }
   }
-  if (t < 624) ms.key[t] = kreg;
+  if (t < 624) {
+    ms.key[t] = kreg;
+    if (form & kRsBlockShuffle) ring[t] = kreg;  // slot 0 of the block shuffle's ring
+  }
   if (t == 0) ms.pos = preg;
   __syncthreads();
   const int m = s_m;
@@ -2736,12 +2761,75 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
   RS_STAMP(41);
   GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 42);
   RS_STAMP(42);
-  if (m > 0) {
+  if (m > 0 && (form & kRsBlockShuffle)) {
+    if (t == 0) J[0] = 0;  // swap 0 <-> 0: lets position 0 trace like the others
+    int pe;
+    const int lb = mt_shuffle_draws_block(ring, ms.pos, (int)bs, J, &pe);
+    const uint32_t* kb = ring + (lb % kMtRing) * 624;
+    for (int i = t; i < 624; i += blockDim.x) ms.key[i] = kb[i];
+    if (t == 0) ms.pos = pe;
+    __syncthreads();
+  } else if (m > 0) {
     if (wave == 0) {
-      if (lane == 0) J[0] = 0;  // swap 0 <-> 0: lets position 0 trace like the others
+      if (lane == 0) J[0] = 0;
       mt_shuffle_draws_wave(&ms, (int)bs, J);
     }
     __syncthreads();
+  }
+  if (m > 0 && (form & kRsParCopy)) {
+    // r05: the next batch draw (one wave: mt_randint_wave) beside the row copies, and the copies in
+    // three block-wide trips instead of one dependent chain per reassigned cluster: every trace
+    // first, then every batch row index, then every row and norm; the copy waves meet on LDS
+    // counters so the drawing wave is never waited for. A timed-out counter wait is redone after the
+    // closing barrier (the copies are plain overwrites).
+    GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 43);
+    RS_STAMP(43);
+    const bool draw = rn.rows != nullptr;
+    const int nc = draw ? nw - 1 : nw;  // copy waves
+    const size_t src_off = (sizeof(int) * (size_t)(((bs + 1) & ~1ll) + k) + kMtRingBytes + 7) & ~(size_t)7;
+    int64_t* s_src = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(J) + src_off);
+    int* s_pos = reinterpret_cast<int*>(s_src + (bs / 2 + 1));
+    auto rows_in = [&](int tc, int stride) {
+      for (int r = tc; r < m; r += stride) s_src[r] = rows[s_pos[r]];
+    };
+    auto rows_out = [&](int tc, int stride) {
+      const int md = m * dim;
+      for (int e = tc; e < md; e += stride) {
+        const int r = e / dim, f = e - r * dim;
+        C_new[(int64_t)s_list[r] * dim + f] = X[s_src[r] * dim + f];
+      }
+      for (int r = tc; r < m; r += stride) cn2[s_list[r]] = npy_sumsq(X + s_src[r] * dim, dim);
+    };
+    if (draw && wave == nw - 1) {
+      mt_store_wave(&ms, mt_mid);  // before the draw twists the key block in place
+      mt_randint_wave(&ms, 0, rn.n, rn.bs, rn.rows);
+      mt_store_wave(&ms, rn.out);
+    } else {
+      if (!draw) mt_store(&ms, mt_mid);  // every wave copies here
+      const int tc = 64 * wave + lane, stride = 64 * nc;
+      for (int r = wave; r < m; r += nc) {
+        const int q = shuffle_trace_wave(J, (int)bs, r);
+        if (lane == 0) s_pos[r] = q;
+      }
+      waves_arrive_rs(&s_sync[0]);
+      bool ok = waves_wait_rs(&s_sync[0], nc);
+      rows_in(tc, stride);
+      waves_arrive_rs(&s_sync[1]);
+      ok = waves_wait_rs(&s_sync[1], nc) && ok;
+      rows_out(tc, stride);
+      for (int c = tc; c < k; c += stride)
+        if (counts[c] < thr) counts[c] = cmin;
+      if (!ok) s_bad = 1;
+    }
+    __syncthreads();
+    if (s_bad) {  // a counter wait gave up: every trace is in now, redo the copies in order
+      rows_in(t, blockDim.x);
+      __syncthreads();
+      rows_out(t, blockDim.x);
+    }
+    GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 45);
+    RS_STAMP(45);
+  } else if (m > 0) {
     GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 43);
     RS_STAMP(43);
     mt_store(&ms, mt_mid);
@@ -2758,7 +2846,6 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
     GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 44);
     RS_STAMP(44);
     if (rn.rows) {  // the next batch after the permutation (replaces the speculative one)
-      uint32_t* ring = reinterpret_cast<uint32_t*>(s_list + k);
       for (int i = t; i < 624; i += blockDim.x) ring[i] = ms.key[i];
       __syncthreads();
       mt_randint_ring(ring, ms.pos, 0, rn.n, rn.bs, rn.rows, rn.out);
@@ -2803,13 +2890,24 @@ int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const 
                        size_t step_ws_bytes, const DevMT* mt_in, DevMT* mt_mid, const RngNext& rn,
                        void* state, hipStream_t s) {
   StepWs w = carve_step(step_ws, step_ws_bytes, bs, k);
-  const size_t lds = mb_reassign_lds(bs, k);
+  size_t lds = mb_reassign_lds(bs, k);
   GDD_REQUIRE(lds <= kReassignLdsCap, "mb_reassign: batch too large for the LDS swap table");
+  // GDD_MB_REASSIGN_FORM (A/B): bit 0 the block shuffle, bit 1 the parallel copies (default both);
+  // the copies' index tables (bs/2 + 1 rows: m <= bs/2 here) follow the base layout where they fit
+  const char* fe = getenv("GDD_MB_REASSIGN_FORM");
+  int form = fe ? atoi(fe) : (kRsBlockShuffle | kRsParCopy);
+  const size_t par_lds =
+      ((sizeof(int) * (size_t)(((bs + 1) & ~1ll) + k) + kMtRingBytes + 7) & ~(size_t)7) +
+      12 * (size_t)(bs / 2 + 1);
+  if ((form & kRsParCopy) && par_lds <= kReassignLdsCap)
+    lds = std::max(lds, par_lds);
+  else
+    form &= ~kRsParCopy;
   if (lds > 65536)
     GDD_HIP(hipFuncSetAttribute((const void*)k_mb_reassign, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds));
   k_mb_reassign<<<1, 1024, lds, s>>>(step, bs, dim, k, ratio, X, rows, C_new, counts, w.cn2, mt_in,
-                                     mt_mid, rn, static_cast<MBState*>(state));
+                                     mt_mid, rn, static_cast<MBState*>(state), form);
   GDD_LAUNCHED();
   return GDD_OK;
 }

@@ -415,6 +415,31 @@ def test_kmeans_lloyd_update_forms(monkeypatch, case):
         assert np.array_equal(bits(a.cluster_centers_), bits(ref["cluster_centers_"]))
 
 
+@pytest.mark.parametrize("n,dim,k,bs", [(20000, 40, 454, 1000), (30000, 8, 200, 2048), (6000, 12, 400, 200),
+                                        (8000, 10, 120, 64)])
+def test_minibatch_reassign_forms(monkeypatch, n, dim, k, bs):
+    """k_mb_reassign's forms (r05, GDD_MB_REASSIGN_FORM): bit 0 the shuffle's draws by the whole
+    workgroup (mt_shuffle_draws_block, a Jacobi fixed point over per-thread counts) instead of one
+    wave; bit 1 the row copies in three block trips beside a one-wave next-batch draw. Blob inputs
+    with fewer blobs than centres leave many clusters empty, so reassignments fire often and large
+    (m up to b/2; b = 2048 takes two 2048-word passes). Every form equals the oracle: labels, centres,
+    inertia, n_steps_ and the generator's final state."""
+    X = synth.blobs(n, dim, max(2, k // 4), seed=n + k)
+    rs_ref = np.random.RandomState(5)
+    ref = O.minibatch_kmeans(X, k, random_state=rs_ref, batch_size=bs)
+    s_ref = rs_ref.get_state()
+    for form in ("0", "1", "2", "3"):
+        monkeypatch.setenv("GDD_MB_REASSIGN_FORM", form)
+        rs = np.random.RandomState(5)
+        m = gdd.MiniBatchKMeans(n_clusters=k, random_state=rs, batch_size=bs).fit(X)
+        assert m.n_steps_ == ref["n_steps_"], form
+        assert np.array_equal(m.labels_, ref["labels_"]), form
+        assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"])), form
+        assert m.inertia_ == ref["inertia_"], form
+        s = rs.get_state()
+        assert np.array_equal(s[1], s_ref[1]) and s[2] == s_ref[2], form
+
+
 @pytest.mark.parametrize("n,dim,k,bs", [(6000, 12, 400, 200), (20000, 8, 300, 500), (3000, 16, 700, 256),
                                         (8000, 10, 120, 64)])
 def test_minibatch_k_above_half_batch(monkeypatch, n, dim, k, bs):
