@@ -17,6 +17,7 @@
 // randint walks the key block in windows of blockDim.x words); every thread of the block calls in.
 #pragma once
 
+#include <climits>
 #include <cstdint>
 
 namespace gdd {
@@ -399,10 +400,13 @@ __device__ inline void mt_permutation_prefix_block(MTScratch* s, int64_t n, int 
 }
 
 // out[0..count) = randint(low, high, count) by ONE wave (no block barriers; the other waves are
-// free meanwhile). Same words, same acceptance as mt_randint_block. Writes s->pos from lane 0.
+// free meanwhile). Same words, same acceptance as mt_randint_block. A key block at a time: lane l
+// reads words pos + 64 j + l (j < 10, every read issued before the first use), and one ballot per
+// 64-word slice places the accepted values in order. Writes s->pos from lane 0.
 __device__ inline void mt_randint_wave(MTScratch* s, int64_t low, int64_t high, int64_t count,
                                        int64_t* __restrict__ out) {
   const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
   const uint32_t rng = (uint32_t)(high - 1 - low);
   if (rng == 0) {
     for (int64_t i = lane; i < count; i += 64) out[i] = low;
@@ -416,24 +420,36 @@ __device__ inline void mt_randint_wave(MTScratch* s, int64_t low, int64_t high, 
       mt_twist_wave(s->key);
       pos = 0;
     }
-    const int wn = min(64, 624 - pos);
-    uint32_t v = 0;
-    bool ok = false;
-    if (lane < wn) {
-      v = mt_temper(s->key[pos + lane]) & mask;
-      ok = v <= rng;
+    uint32_t v[10];
+    unsigned live = 0;  // bit j: word pos + 64 j + lane is inside the key block
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const int idx = pos + 64 * j + lane;
+      v[j] = idx < 624 ? mt_temper(s->key[idx]) & mask : 0u;
+      live |= (idx < 624 ? 1u : 0u) << j;
     }
-    const unsigned long long b = __ballot(ok);
-    const int before = __popcll(b & ((1ull << lane) - 1ull));
-    const int64_t need = count - produced;
-    if (ok && before < need) out[produced + before] = low + (int64_t)v;
-    const int tot = __popcll(b);
-    if (tot >= need) {
-      pos += __ffsll((long long)__ballot(ok && before == need - 1));  // through the last word used
+    int64_t base = produced;
+    bool done = false;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      if (!done) {
+        const bool ok = ((live >> j) & 1u) && v[j] <= rng;
+        const unsigned long long b = __ballot(ok);
+        const int64_t r = base + __popcll(b & below);
+        if (ok && r < count) out[r] = low + (int64_t)v[j];
+        if (base + __popcll(b) >= count) {  // the last draw is in this slice
+          const unsigned long long lb = __ballot(ok && r == count - 1);
+          pos = pos + 64 * j + __ffsll((long long)lb);  // through the last word used
+          done = true;
+        }
+        base += __popcll(b);
+      }
+    }
+    if (done) {
       produced = count;
     } else {
-      pos += wn;
-      produced += tot;
+      produced = base;
+      pos = 624;
     }
     asm volatile("" ::: "memory");
   }
@@ -491,7 +507,8 @@ __device__ inline void mt_shuffle_draws_wave(MTScratch* s, int n, int* J) {
 // and `pos` its position (624: exhausted); returns the stream index b of the key block holding the
 // last word consumed (ring slot b % kMtRing) and sets *pos_out to the position after that word.
 // Scratch: the 64 ints after the ring.
-__device__ inline int mt_shuffle_draws_block(uint32_t* ring, int pos, int n, int* J, int* pos_out) {
+__device__ inline int mt_shuffle_draws_block(uint32_t* ring, int pos, int n, int* J, int* pos_out,
+                                              int* iters = nullptr) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nwv = blockDim.x >> 6;
   int* scr = reinterpret_cast<int*>(ring + kMtRing * 624);
   const int wpt = 2048 / (int)blockDim.x;  // 2, 4 or 8
@@ -551,6 +568,7 @@ __device__ inline int mt_shuffle_draws_block(uint32_t* ring, int pos, int n, int
       }
       par ^= 1;  // the other slot next: this one is rewritten only after the next barrier
       prev = cnt;
+      if (iters) ++*iters;
       if (!any) break;  // no count changed: the scan of these counts is A itself
       A = wb + inc - cnt;
     }
@@ -607,6 +625,33 @@ __device__ inline int shuffle_trace_wave(const int* J, int n, int p) {
       i0 = q + 1;
     } else {
       i0 += 64;
+    }
+  }
+  return q;
+}
+
+// shuffle_trace_wave reading J 256 entries per step (lane l: one 16-byte read of entries
+// a0 + 4l .. a0 + 4l + 3, a0 = the current start rounded down to a multiple of 4; J 16-byte aligned).
+// Entries before the start or past n are masked; reads past n stay inside the workgroup's LDS.
+__device__ inline int shuffle_trace_wave4(const int* J, int n, int p) {
+  const int lane = threadIdx.x & 63;
+  int q = J[p];
+  int i0 = p + 1;
+  while (i0 < n) {
+    const int a0 = i0 & ~3;
+    const int e0 = a0 + 4 * lane;
+    const int4 v = *reinterpret_cast<const int4*>(J + e0);
+    const int vv[4] = {v.x, v.y, v.z, v.w};
+    int hit = INT_MAX;
+#pragma unroll
+    for (int u = 3; u >= 0; --u)
+      if (e0 + u >= i0 && e0 + u < n && vv[u] == q) hit = e0 + u;
+    const unsigned long long b = __ballot(hit != INT_MAX);
+    if (b) {
+      q = __shfl(hit, __ffsll((long long)b) - 1);  // the first match: the lowest lane's lowest entry
+      i0 = q + 1;
+    } else {
+      i0 = a0 + 256;
     }
   }
   return q;

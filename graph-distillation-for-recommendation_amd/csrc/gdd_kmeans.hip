@@ -1260,10 +1260,12 @@ struct MbTail {
   int active;
 };
 
-__device__ void mb_tail_block(const MbTail& tl, float* stage) {
+// stp: the loop stopped before this launch's step (tested after the fold's loads, before the writes)
+__device__ void mb_tail_block(const MbTail& tl, float* stage, bool stp = false) {
   MbConv c{};
   if (threadIdx.x == 0 && tl.converge) c = mb_conv_load(tl.st);  // in flight during the fold
   const float inertia = mb_batch_inertia(tl.b, tl.sq, stage);
+  if (stp) return;
   if (threadIdx.x == 0) {
     tl.inertia[0] = inertia;
     if (tl.converge) mb_converge_from(c, tl.step, tl.b, tl.n_samples, tl.max_ni, inertia, tl.st);
@@ -1297,18 +1299,30 @@ __global__ __launch_bounds__(64 * W) void k_mb_assign(
     int k, const float* __restrict__ C, const float* __restrict__ cn2,
     unsigned long long* __restrict__ keys, int G, int P, const int32_t* __restrict__ stop,
     int step_i, MbTail tl, RngNext rn) {
-  if (stopped(stop, step_i)) return;
+  // the stop word goes out with trip 1's loads and is tested before the first global store (r05:
+  // tested first it cost each launch one more dependent round trip); a block that runs on after
+  // the loop stopped only writes buffers no later step reads, as a block that started first would
+#ifdef GDD_STOP_AT_ENTRY
+  if (stopped(stop, step_i)) return;  // the r04 order: the stop word alone first (A/B build)
+#endif
+  const int32_t sv = stop ? __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  const bool stp = sv != 0 && sv - 1 < step_i;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int blk = blockIdx.x;
   if (blk >= P * G) {
     const int e = blk - P * G;
     if (tl.active && e == 0) {
       GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 82);
-      mb_tail_block(tl, lds);
+      mb_tail_block(tl, lds, stp);
       GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 80);
     } else if (rn.rows) {
       GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 83);
-      mt_randint_from(rn.in, reinterpret_cast<uint32_t*>(lds), 0, rn.n, rn.bs, rn.rows, rn.out);
+      uint32_t* ring = reinterpret_cast<uint32_t*>(lds);
+      for (int i = threadIdx.x; i < 624; i += blockDim.x) ring[i] = rn.in->key[i];
+      const int pos = rn.in->pos;
+      __syncthreads();
+      if (stp) return;
+      mt_randint_ring(ring, pos, 0, rn.n, rn.bs, rn.rows, rn.out);
       GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 81);
     }
     return;
@@ -1339,6 +1353,7 @@ __global__ __launch_bounds__(64 * W) void k_mb_assign(
   }
   if (tid < 32) s_rows[tid] = my_row;
   __syncthreads();
+  if (stp) return;
   // trip 2: the point rows
   stage_rows32<VEC, 4>(Pl, S, [&](int r) { return X + s_rows[r] * dim; }, np, dim, dimp, tid,
                        64 * W);
@@ -1399,14 +1414,16 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
                                                         int32_t* __restrict__ labels_out,
                                                         float* __restrict__ sq_out,
                                                         unsigned long long* __restrict__ keys_reset) {
-  if (stopped(stop, step_i)) return;
+  // the stop word goes out with the label loads and is tested before the first global store (r05)
+#ifdef GDD_STOP_AT_ENTRY
+  if (stopped(stop, step_i)) return;  // the r04 order: the stop word alone first (A/B build)
+#endif
+  const int32_t sv = stop ? __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 20);
   extern __shared__ __attribute__((aligned(16))) float mb_lds[];
   const int c = blockIdx.x;
   const int lane = threadIdx.x;
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 21);
-  if (keys_reset)
-    for (int64_t i = (int64_t)c * 64 + lane; i < b; i += (int64_t)gridDim.x * 64) keys_reset[i] = ~0ull;
   if (sq_out) {  // the old centre row, for the member distances (after the new row in LDS)
     float* crow = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(reinterpret_cast<int64_t*>(mb_lds) + b) + b) + dim;
     for (int f = lane; f < dim; f += 64) crow[f] = C_old[(int64_t)c * dim + f];
@@ -1433,6 +1450,9 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
     }
   }
   __syncthreads();
+  if (sv != 0 && sv - 1 < step_i) return;
+  if (keys_reset)
+    for (int64_t i = (int64_t)c * 64 + lane; i < b; i += (int64_t)gridDim.x * 64) keys_reset[i] = ~0ull;
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 22);
   // the members' source rows: one dependent trip for the few members only (requesting all b batch
   // rows with the labels measured slower: 454 workgroups x 8 KB more L2 reads, 6.9 -> 7.8 us)
@@ -2685,7 +2705,11 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
     float* __restrict__ cn2, const DevMT* __restrict__ mt_in, DevMT* __restrict__ mt_mid,
     RngNext rn, MBState* __restrict__ mbs, int form) {
   int32_t* stop = &mbs->stop_at;
-  if (stopped(stop, step)) return;
+  // the stop word goes out with the first loads and is tested after the first barrier (r05)
+#ifdef GDD_STOP_AT_ENTRY
+  if (stopped(stop, step)) return;  // the r04 order: the stop word alone first (A/B build)
+#endif
+  const int32_t sv = __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef GDD_STAMPS
   unsigned long long tl[7] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0};
 #define RS_STAMP(q) tl[(q) - 40] = __builtin_amdgcn_s_memrealtime()
@@ -2748,6 +2772,7 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
   }
   if (t == 0) ms.pos = preg;
   __syncthreads();
+  if (sv != 0 && sv - 1 < step) return;
   const int m = s_m;
   const float thr = s_thr, cmin = s_min;
   if (2 * (int64_t)m > bs) {  // the argsort branch (_kmeans.py:1644-1648): the host's
@@ -2761,10 +2786,19 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
   RS_STAMP(41);
   GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 42);
   RS_STAMP(42);
+  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0 && m > 0, 48);
   if (m > 0 && (form & kRsBlockShuffle)) {
     if (t == 0) J[0] = 0;  // swap 0 <-> 0: lets position 0 trace like the others
-    int pe;
-    const int lb = mt_shuffle_draws_block(ring, ms.pos, (int)bs, J, &pe);
+    int pe, iters = 0;
+    const int lb = mt_shuffle_draws_block(ring, ms.pos, (int)bs, J, &pe, &iters);
+#ifdef GDD_STAMPS
+    if (t == 0) {
+      g_stamps_kmeans[62] = (unsigned long long)iters;
+      g_stamps_kmeans[63] = (unsigned long long)pe;
+    }
+#else
+    (void)iters;
+#endif
     const uint32_t* kb = ring + (lb % kMtRing) * 624;
     for (int i = t; i < 624; i += blockDim.x) ms.key[i] = kb[i];
     if (t == 0) ms.pos = pe;
@@ -2776,6 +2810,7 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
     }
     __syncthreads();
   }
+  GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0 && m > 0, 49);
   if (m > 0 && (form & kRsParCopy)) {
     // r05: the next batch draw (one wave: mt_randint_wave) beside the row copies, and the copies in
     // three block-wide trips instead of one dependent chain per reassigned cluster: every trace
@@ -2785,7 +2820,11 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
     GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 43);
     RS_STAMP(43);
     const bool draw = rn.rows != nullptr;
-    const int nc = draw ? nw - 1 : nw;  // copy waves
+    // with a draw, the drawing wave (the last: w % 4 == 3) keeps its SIMD to itself — waves
+    // w % 4 == 3 copy nothing — and raises its issue priority
+    const bool copier = !draw || (wave & 3) != 3;
+    const int nc = draw ? nw - (nw >> 2) : nw;  // copy waves
+    const int ci = draw ? wave - (wave >> 2) : wave;  // this copy wave's index
     const size_t src_off = (sizeof(int) * (size_t)(((bs + 1) & ~1ll) + k) + kMtRingBytes + 7) & ~(size_t)7;
     int64_t* s_src = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(J) + src_off);
     int* s_pos = reinterpret_cast<int*>(s_src + (bs / 2 + 1));
@@ -2801,14 +2840,18 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
       for (int r = tc; r < m; r += stride) cn2[s_list[r]] = npy_sumsq(X + s_src[r] * dim, dim);
     };
     if (draw && wave == nw - 1) {
+      __builtin_amdgcn_s_setprio(3);
       mt_store_wave(&ms, mt_mid);  // before the draw twists the key block in place
+      GDD_STAMP_WHEN(g_stamps_kmeans, lane == 0, 64);
       mt_randint_wave(&ms, 0, rn.n, rn.bs, rn.rows);
+      GDD_STAMP_WHEN(g_stamps_kmeans, lane == 0, 65);
       mt_store_wave(&ms, rn.out);
-    } else {
+      GDD_STAMP_WHEN(g_stamps_kmeans, lane == 0, 58);
+    } else if (copier) {
       if (!draw) mt_store(&ms, mt_mid);  // every wave copies here
-      const int tc = 64 * wave + lane, stride = 64 * nc;
-      for (int r = wave; r < m; r += nc) {
-        const int q = shuffle_trace_wave(J, (int)bs, r);
+      const int tc = 64 * ci + lane, stride = 64 * nc;
+      for (int r = ci; r < m; r += nc) {
+        const int q = shuffle_trace_wave4(J, (int)bs, r);
         if (lane == 0) s_pos[r] = q;
       }
       waves_arrive_rs(&s_sync[0]);
@@ -2820,6 +2863,7 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
       for (int c = tc; c < k; c += stride)
         if (counts[c] < thr) counts[c] = cmin;
       if (!ok) s_bad = 1;
+      GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 59);
     }
     __syncthreads();
     if (s_bad) {  // a counter wait gave up: every trace is in now, redo the copies in order
@@ -2892,10 +2936,10 @@ int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const 
   StepWs w = carve_step(step_ws, step_ws_bytes, bs, k);
   size_t lds = mb_reassign_lds(bs, k);
   GDD_REQUIRE(lds <= kReassignLdsCap, "mb_reassign: batch too large for the LDS swap table");
-  // GDD_MB_REASSIGN_FORM (A/B): bit 0 the block shuffle, bit 1 the parallel copies (default both);
+  // GDD_MB_REASSIGN_FORM (A/B): bit 0 the block shuffle, bit 1 the parallel copies (default 2);
   // the copies' index tables (bs/2 + 1 rows: m <= bs/2 here) follow the base layout where they fit
   const char* fe = getenv("GDD_MB_REASSIGN_FORM");
-  int form = fe ? atoi(fe) : (kRsBlockShuffle | kRsParCopy);
+  int form = fe ? atoi(fe) : kRsParCopy;  // the block shuffle measured slower
   const size_t par_lds =
       ((sizeof(int) * (size_t)(((bs + 1) & ~1ll) + k) + kMtRingBytes + 7) & ~(size_t)7) +
       12 * (size_t)(bs / 2 + 1);

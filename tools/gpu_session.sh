@@ -16,6 +16,10 @@
 #                         products, the default hop and the 4-slice form (GDD_HOP_LANES=8)
 #   phases                tools/phase_times.py (per-phase wall times of the bench step)
 #   kernarg-ab            micro_kpp arxiv + bench: default / HIP_FORCE_DEV_KERNARG=1 / kernarg-preload build / both, twice
+#   reassign-ab           bench.py with GDD_MB_REASSIGN_FORM = 0 / 3 (the r04 reassignment vs block shuffle + parallel copies), twice
+#   reassign-trace        rocprofv3 kernel trace of a short bench at GDD_MB_REASSIGN_FORM = 0..3 + k_mb_reassign durations
+#   reassign-stamps       tools/stamps.py (STAMPS=1 build) at GDD_MB_REASSIGN_FORM = 0..3
+#   stop-ab               bench.py: stop word loaded with trip 1 (default) vs tested alone at entry (libgdd_stopentry.so), twice
 #   kpp                   tools/micro_kpp.py (k-means++ round micro-benchmark)
 #   spec-ab               k-means++ folds with / without the speculative searches (micro + bench, twice)
 #   lloyd-small           tools/micro_lloyd_small.py (recsys KMeans: one-workgroup update / grouping on and off)
@@ -93,7 +97,16 @@ for step in "$@"; do
     kpp-par) run 300 kpp_par python tools/micro_kpp.py par ;;
     relabel) run 600 relabel python tools/micro_relabel.py ;;
     par-ab) run 900 par_ab bash -c 'for v in 0 1 0 1; do echo "GDD_KPP_PAR_CHAIN=$v"; GDD_KPP_PAR_CHAIN=$v python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done' ;;
-    kernarg-ab) run 1000 kernarg_ab bash -c 'P=graph-distillation-for-recommendation_amd/gdd/lib/libgdd_preload.so; for r in 1 2; do for v in base devkarg preload both; do echo "variant $v"; case $v in base) E="";; devkarg) E="HIP_FORCE_DEV_KERNARG=1";; preload) E="GDD_LIB_PATH=$P";; both) E="HIP_FORCE_DEV_KERNARG=1 GDD_LIB_PATH=$P";; esac; env $E python tools/micro_kpp.py arxiv || exit 1; env $E python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done; done' ;;
+    kernarg-ab) run 1000 kernarg_ab bash -c 'P=graph-distillation-for-recommendation_amd/gdd/lib/libgdd_preload.so; for r in ${KARG_REPS:-1}; do for v in base devkarg preload both; do echo "variant $v"; case $v in base) E="";; devkarg) E="HIP_FORCE_DEV_KERNARG=1";; preload) E="GDD_LIB_PATH=$P";; both) E="HIP_FORCE_DEV_KERNARG=1 GDD_LIB_PATH=$P";; esac; env $E python tools/micro_kpp.py arxiv || exit 1; env $E python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done; done' ;;
+    reassign-ab) run 900 reassign_ab bash -c 'for v in 0 2 0 2; do echo "GDD_MB_REASSIGN_FORM=$v"; GDD_MB_REASSIGN_FORM=$v python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done' ;;
+    reassign-trace)
+      for v in 0 1 2 3; do
+        run 420 reassign_trace$v env GDD_MB_REASSIGN_FORM=$v rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rtrace$v" -o bench \
+             -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra || exit 1
+        echo "form $v"; python3 tools/kernel_durations.py "$OUT/rtrace$v/bench_kernel_trace.csv" k_mb_reassign 24
+      done ;;
+    reassign-stamps) run 300 reassign_stamps bash -c 'for v in 0 1 2 3; do echo "GDD_MB_REASSIGN_FORM=$v"; GDD_MB_REASSIGN_FORM=$v python tools/stamps.py || exit 1; done' ;;
+    stop-ab) run 900 stop_ab bash -c 'P=graph-distillation-for-recommendation_amd/gdd/lib/libgdd_stopentry.so; for v in hoisted entry hoisted entry; do echo "variant $v"; if [ $v = entry ]; then E="GDD_LIB_PATH=$P"; else E=""; fi; env $E python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done' ;;
     near-ab) run 900 near_ab bash -c 'for v in 0 3 6 0 3 6; do echo "GDD_MB_NEAR_STOP=$v"; GDD_MB_NEAR_STOP=$v python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done' ;;
     spec-ab) run 900 spec_ab bash -c 'python tools/micro_kpp.py spec && for v in 1 0 1 0; do echo "GDD_KPP_SPEC_SEARCH=$v"; export GDD_KPP_SPEC_SEARCH=$v; python bench.py --no-cpu-baseline --no-extra --steps 20 --warmup 3 || exit 1; done' ;;
     lloyd-small) run 300 lloyd_small python tools/micro_lloyd_small.py ;;

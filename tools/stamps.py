@@ -72,6 +72,8 @@ def main():
         show("update tail", a, list(range(30, 33)), 30)
         show("mb_reassign", a, list(range(40, 47)), 40)
         show(f"reassign m={a[57]}", a, list(range(50, 57)), 50)
+        show("reassign r05 forms", a, [48, 49, 64, 65, 59, 58], 48)  # shuffle start, end, mid stored, drawn, copies, draw stored
+        print(f"block shuffle: {a[62]} Jacobi iterations, final pos {a[63]}")
         t0 = p[60]
         lab = {60: "start", 61: "winners resolved", 62: "level-1 fold done", 63: "level-2 row in LDS",
                75: "wave-1 prefix done", 76: "wave-0 chains done", 77: "wave-1 speculative searches done",
