@@ -523,6 +523,19 @@ def _sync_mark(ph, name, t_prev):
     return now
 
 
+def _products_pmc_traffic():
+    """HBM bytes per products hop from the latest committed PMC record (profiles/<round>_hop_products_pmc.json,
+    tools/pmc_summary.py over three separate rocprofv3 --pmc passes; a counter run cannot share this
+    process), or (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hop_products_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        rec = json.load(f)
+    return rec.get("default", {}).get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def _hop_roofline(gn, X, alpha, reps=10):
     """One unpaired planned hop (SpMMPlan.hop with the target update, the same plan gdd_propagate
     builds per call), timed with HIP events on the stream gdd launches on (torch's current stream):
@@ -614,6 +627,7 @@ def products_record(dev, with_cpu):
     n_iter = int(km.n_iter_)
     total_ms = sum(ph.values())
     hop = _hop_roofline(gn, X, cfg.alpha)
+    hop["traffic"], hop["traffic_source"] = _products_pmc_traffic()
     # the labels pass at fp32 (exact, sklearn's bits) and bf16 (opt-in, config 5), same centres
     C = km.cluster_centers_device_.contiguous()
     ops = _Ops(dev, cfg.n, cfg.k, cfg.n_classes)
