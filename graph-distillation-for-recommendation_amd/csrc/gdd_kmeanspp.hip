@@ -2369,6 +2369,97 @@ __global__ __launch_bounds__(256) void k_kpp_dmat(int n, int dim, const float* _
   }
 }
 
+// The same table by register tiles (r05): a 256-thread block computes 64 points i x 64 candidates j,
+// thread (ti, tj) the 4 x 4 pairs i0 + 4 ti + b, j0 + 4 tj + a. Both operand tiles come from X^T
+// (coalesced) into LDS as fp64, feature-major, so per feature a thread reads its four x and four c
+// values with four 16-byte LDS reads and issues 16 fp64 fmas (the row form read one LDS value per
+// fma). Each pair's dot product is the same chain: fma over the features in order from 0 — the row
+// form's zero-padded tail adds +-0 products, which leave every nonzero dot unchanged and change
+// only the sign of a zero dot, invisible after + ||c||^2 — so the table has the same bits.
+// LDS: 2 x 64 x dim doubles (dynamic, dim <= kDmX).
+__global__ __launch_bounds__(256) void k_kpp_dmat_t(int n, int dim, const float* __restrict__ XT,
+                                                    const double* __restrict__ xsq,
+                                                    float* __restrict__ D) {
+  extern __shared__ __attribute__((aligned(16))) double s_dm[];
+  double* s_x = s_dm;             // [dim][64] points
+  double* s_c = s_dm + 64 * dim;  // [dim][64] candidates
+  const int tid = threadIdx.x, ti = tid & 15, tj = tid >> 4;
+  const int i0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
+  for (int e = tid; e < 64 * dim; e += 256) {
+    const int v = e >> 6, q = e & 63;
+    s_x[e] = (double)XT[(int64_t)v * n + min(i0 + q, n - 1)];
+    s_c[e] = (double)XT[(int64_t)v * n + min(j0 + q, n - 1)];
+  }
+  double xs[4], cn[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    xs[b] = xsq[min(i0 + 4 * ti + b, n - 1)];
+    cn[b] = xsq[min(j0 + 4 * tj + b, n - 1)];
+  }
+  __syncthreads();
+  double dot[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) dot[a][b] = 0.0;
+  const double* px = s_x + 4 * ti;
+  const double* pc = s_c + 4 * tj;
+  for (int v = 0; v < dim; ++v) {
+    const double2 x01 = *reinterpret_cast<const double2*>(px + 64 * v);
+    const double2 x23 = *reinterpret_cast<const double2*>(px + 64 * v + 2);
+    const double2 c01 = *reinterpret_cast<const double2*>(pc + 64 * v);
+    const double2 c23 = *reinterpret_cast<const double2*>(pc + 64 * v + 2);
+    const double xv[4] = {x01.x, x01.y, x23.x, x23.y};
+    const double cv[4] = {c01.x, c01.y, c23.x, c23.y};
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) dot[a][b] = __builtin_fma(cv[a], xv[b], dot[a][b]);
+  }
+  const int ib = i0 + 4 * ti;
+  const bool vec = (n & 3) == 0 && ib + 3 < n;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int j = j0 + 4 * tj + a;
+    if (j >= n) break;
+    float f[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      f[b] = (float)(((-2.0 * dot[a][b]) + cn[a]) + xs[b]);
+      f[b] = f[b] < 0.f ? 0.f : f[b];
+    }
+    float* out = D + (int64_t)j * n + ib;
+    if (vec) {
+      *reinterpret_cast<float4*>(out) = make_float4(f[0], f[1], f[2], f[3]);
+    } else {
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if (ib + b < n) out[b] = f[b];
+    }
+  }
+}
+
+// the n x n distance table (k_kpp_dmat_t; GDD_KPP_DMAT_ROWS: the r04 row form, A/B)
+int launch_kpp_dmat(int64_t n, int dim, const float* X, const float* XT, const double* xsq, float* D,
+                    hipStream_t s) {
+  if (getenv("GDD_KPP_DMAT_ROWS") == nullptr) {
+    const size_t lds = sizeof(double) * 128 * (size_t)dim;
+    if (lds > 65536)
+      GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dmat_t, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+    const dim3 g((unsigned)((n + 63) / 64), (unsigned)((n + 63) / 64));
+    k_kpp_dmat_t<<<g, 256, lds, s>>>((int)n, dim, XT, xsq, D);
+  } else {
+    const dim3 gdm((unsigned)((n + 255) / 256), (unsigned)((n + kDmJ - 1) / kDmJ));
+    if (dim <= 48)
+      k_kpp_dmat<48><<<gdm, 256, 0, s>>>((int)n, dim, X, XT, xsq, D);
+    else
+      k_kpp_dmat<64><<<gdm, 256, 0, s>>>((int)n, dim, X, XT, xsq, D);
+  }
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
 template <bool PIPE>
 __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __restrict__ D, int c) {
   __shared__ float s_d[kBlk];
@@ -3379,12 +3470,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     GDD_LAUNCHED();
     // the distance table pays once the rounds it saves (~3 us each) cover its one-off build
     if (seq && Dm && k >= kDmMinK && getenv("GDD_KPP_NO_TABLE") == nullptr) {
-      const dim3 gdm((unsigned)((n + 255) / 256), (unsigned)((n + kDmJ - 1) / kDmJ));
-      if (dim <= 48)
-        k_kpp_dmat<48><<<gdm, 256, 0, s>>>((int)n, dim, X, XT, xsq, Dm);
-      else
-        k_kpp_dmat<64><<<gdm, 256, 0, s>>>((int)n, dim, X, XT, xsq, Dm);
-      GDD_LAUNCHED();
+      if (const int rc = launch_kpp_dmat(n, dim, X, XT, xsq, Dm, s)) return rc;
       const bool plain = getenv("GDD_KPP_CHAIN_PLAIN") != nullptr;
       // GDD_KPP_PAR_CHAIN: 1 = the exact parallel lane chains (512-thread pair launches), 0 = the
       // sequential lane chains
@@ -3509,12 +3595,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     return GDD_OK;
   }
   if (Dbig && seq && a.XT) {  // the distances once per fit (~n^2 dim fp64 fmas), then table rounds
-    const dim3 gdm((unsigned)((n + 255) / 256), (unsigned)((n + kDmJ - 1) / kDmJ));
-    if (dim <= 48)
-      k_kpp_dmat<48><<<gdm, 256, 0, s>>>((int)n, dim, X, a.XT, xsq, Dbig);
-    else
-      k_kpp_dmat<64><<<gdm, 256, 0, s>>>((int)n, dim, X, a.XT, xsq, Dbig);
-    GDD_LAUNCHED();
+    if (const int rc = launch_kpp_dmat(n, dim, X, a.XT, xsq, Dbig, s)) return rc;
     a.D = Dbig;
     if (n <= kpp_big1_max() && T >= 2 && getenv("GDD_KPP_NO_BIG1") == nullptr) {
       // one 1024-thread workgroup per trial (k_kpp1_big); GDD_KPP_NO_BIG1 keeps the per-block rounds

@@ -318,6 +318,25 @@ def _par_case_points(case, n, dim, seed):
 
 
 @pytest.mark.parametrize("case", ["blobs", "integers", "dupes", "range"])
+@pytest.mark.parametrize("n,dim,k", [(3000, 40, 454), (2708, 7, 70), (1001, 5, 33), (6040, 64, 604),
+                                     (5003, 33, 60)])
+def test_kmeans_plusplus_table_forms(monkeypatch, case, n, dim, k):
+    """The n x n distance table by 4 x 4 register tiles (k_kpp_dmat_t, r05 default) and by rows
+    (GDD_KPP_DMAT_ROWS=1, the r04 form) give the same seeding as the oracle: the single-block table
+    rounds (n <= 4096), the one-workgroup rounds on the big table, n % 4 tails (scalar stores), dim
+    64 (the 64 KB tile) and data with exact ties, zero distances and twelve decades."""
+    X = _par_case_points(case, n, dim, n + dim + k)
+    c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
+    for rows in (False, True):
+        if rows:
+            monkeypatch.setenv("GDD_KPP_DMAT_ROWS", "1")
+        ops = _Ops("cuda", n, k, dim)
+        c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(15))
+        assert np.array_equal(idx.cpu().numpy(), idx_ref), rows
+        assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref)), rows
+
+
+@pytest.mark.parametrize("case", ["blobs", "integers", "dupes", "range"])
 @pytest.mark.parametrize("n,dim,k", [(3000, 40, 454), (2708, 7, 70), (4093, 3, 200), (3706, 64, 371),
                                      (1001, 5, 33)])
 def test_kmeans_plusplus_parallel_chains(monkeypatch, case, n, dim, k):
