@@ -589,6 +589,7 @@ struct KppArgs {
   int exact;          // cum_tol's mode
   const float* D;     // the n x n distance table (plain-chain plans, n <= kDmBigMax), or nullptr
   int par_chain;      // the block terms' lane chains by the exact parallel runs (r05)
+  int preload;        // k_kpp_round: every trial's block totals requested with the fold (r05, A/B)
 };
 
 __device__ __forceinline__ float wv(const float* w, int64_t i) { return w ? w[i] : 1.0f; }
@@ -628,6 +629,19 @@ __device__ int fold_round(const KppArgs& a, int q, float* s_pot) {
     if (tid == 0) s_pot[0] = a.pot1[q];
   } else {
     float y = 0.f;
+    // the n % 4 tail (<= 3 entries past the sgemv_t blocks) requested with the block terms (r05:
+    // read after the blocks' barrier it was a dependent trip of its own)
+    const int64_t nt = a.n - a.m1;
+    float tx[3] = {0.f, 0.f, 0.f}, tw[3] = {1.f, 1.f, 1.f};
+    if (tid < a.T && nt <= 3 && (a.preload & 2)) {
+      const float* row = a.dist[q] + (int64_t)tid * a.n;
+#pragma unroll
+      for (int o = 0; o < 3; ++o)
+        if (o < nt) {
+          tx[o] = row[a.m1 + o];
+          tw[o] = wv(a.w, a.m1 + o);
+        }
+    }
     for (int64_t b0 = 0; b0 < a.nsg; b0 += kFoldChunk) {
       const int m = (int)min<int64_t>(kFoldChunk, a.nsg - b0);
       for (int e = tid; e < m * a.T; e += blockDim.x) {
@@ -643,9 +657,17 @@ __device__ int fold_round(const KppArgs& a, int q, float* s_pot) {
     }
     if (tid < a.T) {
       if (a.m1 < a.n) {
-        const float* row = a.dist[q] + (int64_t)tid * a.n;
-        float sx = row[a.m1] * wv(a.w, a.m1);
-        for (int64_t o = a.m1 + 1; o < a.n; ++o) sx = __builtin_fmaf(row[o], wv(a.w, o), sx);
+        float sx;
+        if (nt <= 3 && (a.preload & 2)) {  // the same operations on the requested values
+          sx = tx[0] * tw[0];
+#pragma unroll
+          for (int o = 1; o < 3; ++o)
+            if (o < nt) sx = __builtin_fmaf(tx[o], tw[o], sx);
+        } else {
+          const float* row = a.dist[q] + (int64_t)tid * a.n;
+          sx = row[a.m1] * wv(a.w, a.m1);
+          for (int64_t o = a.m1 + 1; o < a.n; ++o) sx = __builtin_fmaf(row[o], wv(a.w, o), sx);
+        }
         y = y + sx;
       }
       s_pot[tid] = y;
@@ -986,6 +1008,16 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     s_jmin = INT_MAX;
     s_parsync = 0;
   }
+  // r05: requested with the fold's block terms instead of after the winner is known (each was a
+  // dependent trip): round c-1's candidates (lane q: trial q's) and, with one block per thread, every
+  // trial's block totals of this thread's block
+  const int64_t csl = (c >= 2 && (a.preload & 4)) ? a.cand[pq][min(lane, a.T - 1)] : 0;
+  constexpr int kFsT = 12;  // T = 2 + ln k <= 12 up to k = 22,026
+  const bool fpre = (a.preload & 1) && c >= 2 && a.nblk <= kThr && a.T <= kFsT;
+  double fs[kFsT];
+#pragma unroll
+  for (int q = 0; q < kFsT; ++q)
+    fs[q] = (fpre && q < a.T && tid < a.nblk) ? a.fsum[pq][(int64_t)q * a.nblk + tid] : 0.0;
   // ---- fold round c-1 (round 0: the first centre)
   int bw = 0;
   float pot;
@@ -1002,6 +1034,11 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     wrow = a.dist[pq] + (int64_t)bw * n;
     wfs = a.fsum[pq] + (int64_t)bw * a.nblk;
   }
+  double fw = 0.0;  // the winner's total of block tid (fpre)
+#pragma unroll
+  for (int q = 0; q < kFsT; ++q)
+    if (q == bw) fw = fs[q];
+  const int64_t src_prev = (a.preload & 4) ? __shfl(csl, bw) : (c >= 2 ? a.cand[pq][bw] : 0);
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 21);
   const double r = u * (double)pot;
   // ---- the block where the cumulative potential reaches r
@@ -1009,7 +1046,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     const int64_t ch = (a.nblk + kThr - 1) / kThr;
     const int64_t lo = min<int64_t>(a.nblk, tid * ch), hi = min<int64_t>(a.nblk, lo + ch);
     double run = 0.0;
-    for (int64_t j = lo; j < hi; ++j) run = run + wfs[j];
+    for (int64_t j = lo; j < hi; ++j) run = run + (fpre ? fw : wfs[j]);
     double inc = run;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1026,7 +1063,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     int found = INT_MAX;
     double Pf = 0.0;
     for (int64_t j = lo; j < hi; ++j) {
-      const double Pn = P + wfs[j];
+      const double Pn = P + (fpre ? fw : wfs[j]);
       if (Pn >= r) {
         found = (int)j;
         Pf = P;
@@ -1141,11 +1178,8 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   }
   if (blk == 0 && tid == 0) a.cand[cq][t] = ct;
   if (PICK && blk == 0 && t == 0 && tid == 0) a.winq[cq] = bw;
-  if (c >= 2 && blk == 0 && t == 0) {  // round c-1's centre (round 0's is written by k_kpp_first)
-    const int64_t src = a.cand[pq][bw];
-    if (tid == 0) a.indices[c - 1] = src;
-    for (int j = tid; j < a.dim; j += kThr) a.centers[(int64_t)(c - 1) * a.dim + j] = a.X[src * a.dim + j];
-  }
+  // round c-1's centre: its index (the rows are gathered after the rounds, k_kpp_gather_centres)
+  if (c >= 2 && blk == 0 && t == 0 && tid == 0) a.indices[c - 1] = src_prev;
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 23);
   if constexpr (PICK) return;  // the split path: k_kpp_dists computes every trial's distances
   // ---- distances of this block's points to the candidate, np.minimum with the winner's row
@@ -2377,63 +2411,76 @@ __global__ __launch_bounds__(256) void k_kpp_dmat(int n, int dim, const float* _
 // form's zero-padded tail adds +-0 products, which leave every nonzero dot unchanged and change
 // only the sign of a zero dot, invisible after + ||c||^2 — so the table has the same bits.
 // LDS: 2 x 64 x dim doubles (dynamic, dim <= kDmX).
+template <int TI, int TJ>
 __global__ __launch_bounds__(256) void k_kpp_dmat_t(int n, int dim, const float* __restrict__ XT,
                                                     const double* __restrict__ xsq,
                                                     float* __restrict__ D) {
+  constexpr int BI = 16 * TI, BJ = 16 * TJ;  // block tile: BI points x BJ candidates
   extern __shared__ __attribute__((aligned(16))) double s_dm[];
-  double* s_x = s_dm;             // [dim][64] points
-  double* s_c = s_dm + 64 * dim;  // [dim][64] candidates
+  double* s_x = s_dm;             // [dim][BI] points
+  double* s_c = s_dm + BI * dim;  // [dim][BJ] candidates
   const int tid = threadIdx.x, ti = tid & 15, tj = tid >> 4;
-  const int i0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
-  for (int e = tid; e < 64 * dim; e += 256) {
-    const int v = e >> 6, q = e & 63;
+  const int i0 = blockIdx.x * BI, j0 = blockIdx.y * BJ;
+  for (int e = tid; e < BI * dim; e += 256) {
+    const int v = e / BI, q = e - v * BI;
     s_x[e] = (double)XT[(int64_t)v * n + min(i0 + q, n - 1)];
+  }
+  for (int e = tid; e < BJ * dim; e += 256) {
+    const int v = e / BJ, q = e - v * BJ;
     s_c[e] = (double)XT[(int64_t)v * n + min(j0 + q, n - 1)];
   }
-  double xs[4], cn[4];
+  double xs[TI], cn[TJ];
 #pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    xs[b] = xsq[min(i0 + 4 * ti + b, n - 1)];
-    cn[b] = xsq[min(j0 + 4 * tj + b, n - 1)];
-  }
+  for (int b = 0; b < TI; ++b) xs[b] = xsq[min(i0 + TI * ti + b, n - 1)];
+#pragma unroll
+  for (int a = 0; a < TJ; ++a) cn[a] = xsq[min(j0 + TJ * tj + a, n - 1)];
   __syncthreads();
-  double dot[4][4];
+  double dot[TJ][TI];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < TJ; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) dot[a][b] = 0.0;
-  const double* px = s_x + 4 * ti;
-  const double* pc = s_c + 4 * tj;
+    for (int b = 0; b < TI; ++b) dot[a][b] = 0.0;
+  const double* px = s_x + TI * ti;
+  const double* pc = s_c + TJ * tj;
   for (int v = 0; v < dim; ++v) {
-    const double2 x01 = *reinterpret_cast<const double2*>(px + 64 * v);
-    const double2 x23 = *reinterpret_cast<const double2*>(px + 64 * v + 2);
-    const double2 c01 = *reinterpret_cast<const double2*>(pc + 64 * v);
-    const double2 c23 = *reinterpret_cast<const double2*>(pc + 64 * v + 2);
-    const double xv[4] = {x01.x, x01.y, x23.x, x23.y};
-    const double cv[4] = {c01.x, c01.y, c23.x, c23.y};
+    double xv[TI], cv[TJ];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < TI; b += 2) {
+      const double2 t = *reinterpret_cast<const double2*>(px + BI * v + b);
+      xv[b] = t.x;
+      xv[b + 1] = t.y;
+    }
 #pragma unroll
-      for (int b = 0; b < 4; ++b) dot[a][b] = __builtin_fma(cv[a], xv[b], dot[a][b]);
+    for (int a = 0; a < TJ; a += 2) {
+      const double2 t = *reinterpret_cast<const double2*>(pc + BJ * v + a);
+      cv[a] = t.x;
+      cv[a + 1] = t.y;
+    }
+#pragma unroll
+    for (int a = 0; a < TJ; ++a)
+#pragma unroll
+      for (int b = 0; b < TI; ++b) dot[a][b] = __builtin_fma(cv[a], xv[b], dot[a][b]);
   }
-  const int ib = i0 + 4 * ti;
-  const bool vec = (n & 3) == 0 && ib + 3 < n;
+  const int ib = i0 + TI * ti;
+  const bool vec = (n & 3) == 0 && ib + TI - 1 < n;
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const int j = j0 + 4 * tj + a;
+  for (int a = 0; a < TJ; ++a) {
+    const int j = j0 + TJ * tj + a;
     if (j >= n) break;
-    float f[4];
+    float f[TI];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
+    for (int b = 0; b < TI; ++b) {
       f[b] = (float)(((-2.0 * dot[a][b]) + cn[a]) + xs[b]);
       f[b] = f[b] < 0.f ? 0.f : f[b];
     }
     float* out = D + (int64_t)j * n + ib;
     if (vec) {
-      *reinterpret_cast<float4*>(out) = make_float4(f[0], f[1], f[2], f[3]);
+#pragma unroll
+      for (int b = 0; b < TI; b += 4)
+        *reinterpret_cast<float4*>(out + b) = make_float4(f[b], f[b + 1], f[b + 2], f[b + 3]);
     } else {
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
+      for (int b = 0; b < TI; ++b)
         if (ib + b < n) out[b] = f[b];
     }
   }
@@ -2443,12 +2490,23 @@ __global__ __launch_bounds__(256) void k_kpp_dmat_t(int n, int dim, const float*
 int launch_kpp_dmat(int64_t n, int dim, const float* X, const float* XT, const double* xsq, float* D,
                     hipStream_t s) {
   if (getenv("GDD_KPP_DMAT_ROWS") == nullptr) {
-    const size_t lds = sizeof(double) * 128 * (size_t)dim;
-    if (lds > 65536)
-      GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dmat_t, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds));
-    const dim3 g((unsigned)((n + 63) / 64), (unsigned)((n + 63) / 64));
-    k_kpp_dmat_t<<<g, 256, lds, s>>>((int)n, dim, XT, xsq, D);
+    // GDD_KPP_DMAT_TILE (A/B): per-thread tile 44 (default), 84 or 88 (points x candidates)
+    const char* te = getenv("GDD_KPP_DMAT_TILE");
+    const int tile = te ? atoi(te) : 44;
+    auto go = [&](auto kern, int ti, int tj) -> int {
+      const size_t lds = sizeof(double) * 16 * (size_t)(ti + tj) * dim;
+      if (lds > 65536)
+        GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      const dim3 g((unsigned)((n + 16 * ti - 1) / (16 * ti)), (unsigned)((n + 16 * tj - 1) / (16 * tj)));
+      kern<<<g, 256, lds, s>>>((int)n, dim, XT, xsq, D);
+      return 0;
+    };
+    if (tile == 88)
+      go(k_kpp_dmat_t<8, 8>, 8, 8);
+    else if (tile == 84)
+      go(k_kpp_dmat_t<8, 4>, 8, 4);
+    else
+      go(k_kpp_dmat_t<4, 4>, 4, 4);
   } else {
     const dim3 gdm((unsigned)((n + 255) / 256), (unsigned)((n + kDmJ - 1) / kDmJ));
     if (dim <= 48)
@@ -2482,6 +2540,8 @@ __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __rest
     cw[q] = a.candw[pq][(int64_t)min(q, Tp - 1) * T + t];
   }
   const double ut = (c + 1 < a.k && (tid & 63) < T) ? a.uniforms[(int64_t)c * T + (tid & 63)] : 0.0;
+  // round c-1's own candidates with the potentials (not a dependent trip after the argmin)
+  const int64_t csl = c >= 2 ? a.candself[pq][min(tid & 63, T - 1)] : 0;
   int bw = 0;  // np.argmin: first minimum, a NaN wins at once
   float best = pv[0];
   int64_t ct = cw[0];
@@ -2494,9 +2554,10 @@ __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __rest
       ct = cw[q];
     }
   }
+  const int64_t sw = __shfl(csl, bw);
   if (tid == 0) {
     a.candself[cq][t] = ct;
-    if (c >= 2 && t == 0) a.indices[c - 1] = a.candself[pq][bw];  // rows gathered after the rounds
+    if (c >= 2 && t == 0) a.indices[c - 1] = sw;  // rows gathered after the rounds
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 61);
   // trip 2: the closest distances (round c-1's winning row) and the candidate's table row
@@ -2563,6 +2624,10 @@ __global__ __launch_bounds__(PAR ? 512 : 256) void k_kpp1_dm2(Kpp1Args a, const 
     for (int q = 0; q < kPairMaxT; ++q) pv[q] = a.potv[pl][min(q, T - 1)];
     const float p2 = a.potv2[pl][min(lane, TT - 1)];
     const int64_t c2 = a.candw2[pl][(int64_t)min(lane, TT - 1) * T + w];
+    // the previous launch's own candidates, requested with the potentials (r05: read after the
+    // argmin they were a second dependent trip on workgroup 0's wave 0, the launch's straggler)
+    const int64_t cs1 = a.candself[pl][min(lane, T - 1)];
+    const int64_t cs2 = a.candself2[pl][min(lane, TT - 1)];
     int bw = 0;  // np.argmin: first minimum, a NaN wins at once
     float best = pv[0];
 #pragma unroll
@@ -2585,9 +2650,10 @@ __global__ __launch_bounds__(PAR ? 512 : 256) void k_kpp1_dm2(Kpp1Args a, const 
     const int j = bw * T + bv;
     ct = __shfl(c2, j);
     wrow = a.dist2[pl] + (int64_t)j * n;
+    const int64_t i1 = __shfl(cs1, bw), i2 = __shfl(cs2, j);
     if (g == 0 && tid == 0) {  // rows gathered after the rounds
-      a.indices[c - 2] = a.candself[pl][bw];
-      a.indices[c - 1] = a.candself2[pl][j];
+      a.indices[c - 2] = i1;
+      a.indices[c - 1] = i2;
     }
   }
   const double ut = (c + 1 < a.k && (tid & 63) < T) ? a.uniforms[(int64_t)c * T + (tid & 63)] : 0.0;
@@ -3406,6 +3472,8 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     a.exact = ex ? atoi(ex) : 1;
     const char* pce = getenv("GDD_KPP_PAR_CHAIN");
     a.par_chain = (pce ? pce[0] == '1' : kParChainDefault) ? 1 : 0;
+    const char* pre = getenv("GDD_KPP_ROUND_PRELOAD");  // bits: 1 block totals, 2 fold tail, 4 candidates
+    a.preload = pre ? atoi(pre) : 7;
   }
   const SklPlan p1{n, skl_batch_size(1, n, dim), 1, dim, 0, 0};
   const size_t lds = sizeof(double) * (size_t)dim + sizeof(float) * kBlk;
@@ -3592,6 +3660,9 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     }
     k_kpp_final<<<1, kThr, 0, s>>>(a, k - 1);
     GDD_LAUNCHED();
+    k_kpp_gather_centres<<<(unsigned)(((int64_t)k * dim + 255) / 256), 256, 0, s>>>(k, dim, X, indices,
+                                                                                     centers);
+    GDD_LAUNCHED();
     return GDD_OK;
   }
   if (Dbig && seq && a.XT) {  // the distances once per fit (~n^2 dim fp64 fmas), then table rounds
@@ -3663,6 +3734,9 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     }
   }
   k_kpp_final<<<1, kThr, 0, s>>>(a, k - 1);
+  GDD_LAUNCHED();
+  k_kpp_gather_centres<<<(unsigned)(((int64_t)k * dim + 255) / 256), 256, 0, s>>>(k, dim, X, indices,
+                                                                                   centers);
   GDD_LAUNCHED();
   return GDD_OK;
 }

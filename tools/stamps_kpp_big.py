@@ -35,4 +35,7 @@ def main(n=2449029, dim=47, k=24):
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) == 4:  # n dim k, e.g. the Ali-Display users' per-block table rounds: 17730 64 1773
+        main(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]))
+    else:
+        main()
