@@ -986,6 +986,7 @@ __device__ __forceinline__ float sgemv_block0_par(const float* __restrict__ s, i
 __device__ __forceinline__ void waves_arrive(int* ctr);
 
 // ---- one seeding round ------------------------------------------------------------------------------
+constexpr int kWaveFoldBlk = 16;  // k_kpp_round's barrier-free fold: up to this many sgemv_t blocks
 template <bool SEQ, bool PICK = false>
 __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   extern __shared__ double s_c[];  // dim doubles, then the block's distances (fp32)
@@ -1015,9 +1016,10 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   constexpr int kFsT = 12;  // T = 2 + ln k <= 12 up to k = 22,026
   const bool fpre = (a.preload & 1) && c >= 2 && a.nblk <= kThr && a.T <= kFsT;
   double fs[kFsT];
+  const int fj = a.nblk <= 64 ? lane : tid;  // the block this thread folds in the search below
 #pragma unroll
   for (int q = 0; q < kFsT; ++q)
-    fs[q] = (fpre && q < a.T && tid < a.nblk) ? a.fsum[pq][(int64_t)q * a.nblk + tid] : 0.0;
+    fs[q] = (fpre && q < a.T && fj < a.nblk) ? a.fsum[pq][(int64_t)q * a.nblk + fj] : 0.0;
   // ---- fold round c-1 (round 0: the first centre)
   int bw = 0;
   float pot;
@@ -1028,13 +1030,55 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     wrow = a.closest0;
     wfs = a.fsum0;
     __syncthreads();
+  } else if ((a.preload & 8) && a.T > 1 && a.T <= 64 && a.nsg <= kWaveFoldBlk && a.n - a.m1 <= 3) {
+    // r05: every wave folds every trial (lane q: trial q's block terms in block order, then the
+    // n % 4 tail: fold_round's operations) and takes the argmin by shuffles, so no barrier
+    const int tq = min(lane, a.T - 1);
+    float vb[kWaveFoldBlk], tx[3] = {0.f, 0.f, 0.f}, tw[3] = {1.f, 1.f, 1.f};
+    const int64_t nt = a.n - a.m1;
+#pragma unroll
+    for (int b = 0; b < kWaveFoldBlk; ++b)
+      vb[b] = b < a.nsg ? a.vblk[pq][(int64_t)tq * a.nblk + b] : 0.f;
+    {
+      const float* row = a.dist[pq] + (int64_t)tq * a.n;
+#pragma unroll
+      for (int o = 0; o < 3; ++o)
+        if (o < nt) {
+          tx[o] = row[a.m1 + o];
+          tw[o] = wv(a.w, a.m1 + o);
+        }
+    }
+    float y = 0.f;
+#pragma unroll
+    for (int b = 0; b < kWaveFoldBlk; ++b)
+      if (b < a.nsg) y = y + vb[b];
+    if (nt > 0) {
+      float sx = tx[0] * tw[0];
+#pragma unroll
+      for (int o = 1; o < 3; ++o)
+        if (o < nt) sx = __builtin_fmaf(tx[o], tw[o], sx);
+      y = y + sx;
+    }
+    int b = 0;  // np.argmin: first minimum, a NaN wins at once
+    float pb = __shfl(y, 0);
+    for (int q = 1; q < a.T; ++q) {
+      const float pt = __shfl(y, q);
+      if (pb == pb && (pt < pb || pt != pt)) {
+        b = q;
+        pb = pt;
+      }
+    }
+    bw = b;
+    pot = pb;
+    wrow = a.dist[pq] + (int64_t)bw * n;
+    wfs = a.fsum[pq] + (int64_t)bw * a.nblk;
   } else {
     bw = fold_round(a, pq, s_pot);
     pot = s_pot[bw];
     wrow = a.dist[pq] + (int64_t)bw * n;
     wfs = a.fsum[pq] + (int64_t)bw * a.nblk;
   }
-  double fw = 0.0;  // the winner's total of block tid (fpre)
+  double fw = 0.0;  // the winner's total of block fj (fpre)
 #pragma unroll
   for (int q = 0; q < kFsT; ++q)
     if (q == bw) fw = fs[q];
@@ -1042,7 +1086,30 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 21);
   const double r = u * (double)pot;
   // ---- the block where the cumulative potential reaches r
-  {
+  int jb = INT_MAX;
+  double Pf_b = 0.0, tot_b = 0.0;
+  if (a.nblk <= 64) {
+    // r05: one block per lane and every wave the same scan — wave 0's operations in the workgroup
+    // form below, where wave 0's lanes hold every block and the other waves' totals are zeros — so
+    // every wave knows the block without a barrier
+    const double wj = lane < a.nblk ? (fpre ? fw : wfs[lane]) : 0.0;
+    double inc = wj;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double y = __shfl_up(inc, o);
+      if (lane >= o) inc = inc + y;
+    }
+    double ex = __shfl_up(inc, 1);
+    if (lane == 0) ex = 0.0;
+    const double P = 0.0 + ex;
+    const double Pn = P + wj;
+    const unsigned long long hit = __ballot(lane < a.nblk && Pn >= r);
+    if (hit) {
+      jb = __ffsll((long long)hit) - 1;
+      Pf_b = __shfl(P, jb);
+    }
+    tot_b = 0.0 + __shfl(inc, 63);  // + the other waves' zero totals: unchanged
+  } else {
     const int64_t ch = (a.nblk + kThr - 1) / kThr;
     const int64_t lo = min<int64_t>(a.nblk, tid * ch), hi = min<int64_t>(a.nblk, lo + ch);
     double run = 0.0;
@@ -1080,16 +1147,18 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
       s_tot = tot;
     }
     __syncthreads();
+    jb = s_jmin;
+    Pf_b = s_P;
+    tot_b = s_tot;
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 22);
   int64_t ct = n - 1;
-  const int jb = s_jmin;
   const double tol = cum_tol(a.exact, n, r);
   // the deciding prefixes: block jb's entries (pv) and the boundary before it (Pb), or the whole
   // total when no block crosses
   double pv[kPer];
   const int64_t e0 = (int64_t)jb * kBlk + kPer * tid;
-  const double Pb = jb != INT_MAX ? s_P : s_tot;
+  const double Pb = jb != INT_MAX ? Pf_b : tot_b;
   bool amb;  // a deciding prefix within tol of r (uniform across the workgroup)
   if (jb != INT_MAX) {  // count inside block jb (uniform branch)
     double v[kPer], pre[kPer];
@@ -1135,7 +1204,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     // 2 gamma_h max(p, r); only then does the replay run.
     __syncthreads();  // s_cnt / s_amb reused below
     // any g >= ulp(numpy's largest partial sum) will do: the total over-estimated by numpy's gamma_n
-    const double sup = s_tot * (1.0 + (double)(n + 256) * 0x1p-52);
+    const double sup = tot_b * (1.0 + (double)(n + 256) * 0x1p-52);
     const int E = sup > 0.0 ? ilogb(sup) : -1074;
     const double ginv = ldexp(1.0, 52 - E);
     int fine = 0;
@@ -1154,7 +1223,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     const double A = ((double)F * 0.5 + 1.0) * g;
     const int64_t ch = (a.nblk + kThr - 1) / kThr;
     const double gh = (double)(96 + ch) * 0x1p-53 * 1.01;
-    const bool finite = s_tot == s_tot && s_tot < __builtin_inf();
+    const bool finite = tot_b == tot_b && tot_b < __builtin_inf();
     bool aw = !finite || fabs(Pb - r) <= A + 2.0 * gh * fmax(Pb, r);
     if (jb != INT_MAX) {
 #pragma unroll
@@ -3472,8 +3541,9 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     a.exact = ex ? atoi(ex) : 1;
     const char* pce = getenv("GDD_KPP_PAR_CHAIN");
     a.par_chain = (pce ? pce[0] == '1' : kParChainDefault) ? 1 : 0;
-    const char* pre = getenv("GDD_KPP_ROUND_PRELOAD");  // bits: 1 block totals, 2 fold tail, 4 candidates
-    a.preload = pre ? atoi(pre) : 7;
+    // A/B bits (r05): 1 block totals, 2 fold tail, 4 candidates, 8 the barrier-free wave fold
+    const char* pre = getenv("GDD_KPP_ROUND_PRELOAD");
+    a.preload = pre ? atoi(pre) : (4 | 8);
   }
   const SklPlan p1{n, skl_batch_size(1, n, dim), 1, dim, 0, 0};
   const size_t lds = sizeof(double) * (size_t)dim + sizeof(float) * kBlk;
