@@ -538,7 +538,10 @@ __global__ __launch_bounds__(64 * W) void k_assign_waves(int64_t n, int dim, int
       floatx16 acc[M];
 #pragma unroll
       for (int q = 0; q < M; ++q) acc[q] = floatx16{};
-      for (int s0 = 0; s0 < ns; s0 += 8) {
+      // groups of eight K-steps, then the rest (r05: rows padded to an even width, not to 16 —
+      // the padding's zero steps only ever added +0 to the chains)
+      const int nfull = ns & ~7;
+      for (int s0 = 0; s0 < nfull; s0 += 8) {
         float a[M][8], bv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -552,6 +555,25 @@ __global__ __launch_bounds__(64 * W) void k_assign_waves(int64_t n, int dim, int
 #pragma unroll
           for (int q = 0; q < M; ++q)
             acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][u], bv[u], acc[q], 0, 0, 0);
+        }
+      }
+      if (nfull < ns) {
+        const int rem = ns - nfull;
+        float a[M][8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int o = 2 * (nfull + min(u, rem - 1));
+#pragma unroll
+          for (int q = 0; q < M; ++q) a[q][u] = ap[q][o];
+          bv[u] = bp[o];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (u < rem) {
+#pragma unroll
+            for (int q = 0; q < M; ++q)
+              acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][u], bv[u], acc[q], 0, 0, 0);
+          }
         }
       }
 #pragma unroll
@@ -2116,13 +2138,14 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
       // centre chunk is staged once per block), at least 4; else the persistent form's chunks.
       // 12 waves (768 threads) leave 170 registers per lane: two chains and the prefetched tile
       // without spills, three waves per SIMD
+      const int dimpw = (dim + 1) & ~1;  // even row width: the K = 2 steps (r05; was 16-padded)
       int Wn = 0;
       for (int wv : {12, 8, 4})
-        if (Wn == 0 && assign_lds(wv, dimp16, (k + 31) & ~31) <= 150 * 1024) Wn = wv;
+        if (Wn == 0 && assign_lds(wv, dimpw, (k + 31) & ~31) <= 150 * 1024) Wn = wv;
       const int cchw = Wn ? ((k + 31) & ~31) : cch;
       if (!Wn) Wn = 4;
       const int gyw = (k + cchw - 1) / cchw;
-      const size_t ldsw = assign_lds(Wn, dimp16, cchw);
+      const size_t ldsw = assign_lds(Wn, dimpw, cchw);
       const int64_t wtiles = (n + 31) / 32;
       const bool contig = rows == nullptr && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
       if (gyw > 1 && gy == 1) {
@@ -2137,7 +2160,7 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
         if (rrc) return rrc;
         const int64_t per = std::max<int64_t>(1, (int64_t)res / gyw);
         const int64_t gxw = std::min<int64_t>((wtiles + wv - 1) / wv, per);
-        kern<<<dim3((unsigned)gxw, (unsigned)gyw), 64 * wv, ldsw, s>>>(n, dim, dimp16, X, rows, k, C,
+        kern<<<dim3((unsigned)gxw, (unsigned)gyw), 64 * wv, ldsw, s>>>(n, dim, dimpw, X, rows, k, C,
                                                                       c_norm2, cchw, keys, stop, step_i,
                                                                       nullptr, nullptr);
         GDD_LAUNCHED();
@@ -2224,8 +2247,9 @@ int kmeans_assign_dev(int64_t n, int dim, const float* X, int k, const float* C,
 static int top2_waves(int dim, int k) {
   const int dimp16 = (dim + 15) & ~15;
   if (dimp16 > 48) return 0;
+  const int dimpw = (dim + 1) & ~1;
   for (int wv : {12, 8, 4})
-    if (assign_lds(wv, dimp16, (k + 31) & ~31) <= 150 * 1024) return wv;
+    if (assign_lds(wv, dimpw, (k + 31) & ~31) <= 150 * 1024) return wv;
   return 0;
 }
 
@@ -2241,9 +2265,9 @@ int kmeans_assign_top2_dev(int64_t n_max, int dim, const float* X, const int64_t
   GDD_REQUIRE(Wn > 0 && n_max > 0, "assign_top2: unsupported shape");
   k_row_norms<<<blocks_for(k), 256, 0, s>>>(k, dim, C, cn2, stop, step_i);
   GDD_LAUNCHED();
-  const int dimp16 = (dim + 15) & ~15;
+  const int dimpw = (dim + 1) & ~1;
   const int cch = (k + 31) & ~31;
-  const size_t lds = assign_lds(Wn, dimp16, cch);
+  const size_t lds = assign_lds(Wn, dimpw, cch);
   const int64_t wtiles = (n_max + 31) / 32;
   const bool contig = rows == nullptr && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
   auto go = [&](auto kern, int wv) -> int {
@@ -2253,7 +2277,7 @@ int kmeans_assign_top2_dev(int64_t n_max, int dim, const float* X, const int64_t
     const int rrc = resident_blocks((const void*)kern, 64 * wv, lds, &res);
     if (rrc) return rrc;
     const int64_t gx = std::max<int64_t>(1, std::min<int64_t>((wtiles + wv - 1) / wv, res));
-    kern<<<dim3((unsigned)gx, 1), 64 * wv, lds, s>>>(n_max, dim, dimp16, X, rows, k, C, cn2, cch, keys,
+    kern<<<dim3((unsigned)gx, 1), 64 * wv, lds, s>>>(n_max, dim, dimpw, X, rows, k, C, cn2, cch, keys,
                                                      stop, step_i, sec, n_dev);
     GDD_LAUNCHED();
     return GDD_OK;
