@@ -114,11 +114,14 @@ def test_recsys_kmeans_cluster_device_scaler():
     assert np.array_equal(bits(cen), bits(z["rs_centers"]))
 
 
-def test_standard_scaler_vs_oracle():
+@pytest.mark.parametrize("n,dim", [(17730, 64), (6040, 64), (6041, 100), (129, 3), (1, 5), (128, 64)])
+def test_standard_scaler_vs_oracle(n, dim):
+    """The device scaler equals the oracle's numpy-order statistics: n % 8 tails, 64-column groups
+    with a partial last group, a single row, a constant column."""
     from oracle import oracle as O
     from gdd import pipeline
-    X = (np.random.default_rng(6).standard_normal((17730, 64)) * 2 - 1).astype(np.float32)
-    X[:, 5] = 3.0  # a constant column: scale 1
+    X = (np.random.default_rng(6).standard_normal((n, dim)) * 2 - 1).astype(np.float32)
+    X[:, min(5, dim - 1)] = 3.0  # a constant column: scale 1
     out, mean, scale = pipeline.standard_scaler(X)
     ref, m_ref, s_ref = O.standard_scaler(X)
     assert np.array_equal(bits(out.cpu().numpy()), bits(ref))
