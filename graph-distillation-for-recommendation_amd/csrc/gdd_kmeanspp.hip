@@ -878,6 +878,57 @@ __device__ __forceinline__ void block_dists(const KppArgs& a, int t, int64_t j0,
   }
 }
 
+// x, or -0.0 (the identity of +: acc + -0.0 == acc for every acc, signed zeros and NaN included) when
+// !in, by a bit mask: a masked chain entry then costs one dependent add. Written as `in ? acc + x : acc`
+// the select sat on the chain after each add (v_add, s_nop, v_cndmask per entry; r05).
+__device__ __forceinline__ float add_operand(float x, bool in) {
+  return __int_as_float(__float_as_int(x) & (in ? 0xffffffffu : 0x80000000u));
+}
+
+// One unit-weight sgemv_t lane chain in LDS: acc + x over p[0], p[S], p[2S], ... (L entries). Two
+// 16-entry register groups alternate: a group's reads (immediate offsets from one address) are
+// issued a whole group of dependent adds ahead of their use (scheduling barriers keep them there, as
+// in chain_add). Reads run at most 32 S entries past the chain: the row buffer is padded for them.
+template <int S>
+__device__ __forceinline__ float chain_unit_lds(const float* __restrict__ p, int L, float acc) {
+  float A[16], B[16];
+  auto ld = [&](float (&R)[16], int m) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) R[q] = p[S * (m + q)];
+  };
+  int m = 0;
+  ld(A, 0);
+  for (; m + 32 <= L; m += 32) {
+    ld(B, m + 16);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc = acc + A[q];
+    __builtin_amdgcn_sched_barrier(0);
+    ld(A, m + 32);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc = acc + B[q];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  ld(B, m + 16);  // A holds entries m .. m + 15; fewer than 32 remain
+  auto grp = [&](const float* g, int e) {  // as chain_add's rest: groups of four
+    if (e + 3 < L) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = acc + g[r];
+    } else if (e < L) {
+      acc = acc + g[0];
+      acc = acc + add_operand(g[1], e + 1 < L);
+      acc = acc + add_operand(g[2], e + 2 < L);
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < 16; q += 4) grp(A + q, m + q);
+#pragma unroll
+  for (int q = 0; q < 16; q += 4) grp(B + q, m + 16 + q);
+  return acc;
+}
+constexpr int kChainPad = 32 * 8 + 16;  // floats past the row that the chains' look-ahead may read
+
 // sgemv_t block result of trial t over the NB (> 0) entries of s_d (weights wb, nullptr: ones), run by
 // one wave; lane 0 returns it
 __device__ float sgemv_block_wave(const float* __restrict__ s_d, const float* __restrict__ wb,
@@ -905,6 +956,8 @@ __device__ float sgemv_block_wave(const float* __restrict__ s_d, const float* __
   if (lane < 8) {
     if (lane < h4) acc = __builtin_fmaf(s_d[lane], wb ? wb[lane] : 1.0f, acc);
     int64_t o = h4 + lane;
+    // (r05: chain_unit_lds' two 16-entry read-ahead groups measured slower here, 5.1 vs 3.8 us per
+    // 4096-entry block at the Ali-Display shape)
     if (!wb) {  // unit weights: fma(x, 1, acc) == acc + x; 32 LDS reads ahead of the chain
       for (; o + 8 * 31 < NB; o += 256) {
         float x[32];
@@ -1684,22 +1737,24 @@ __device__ __forceinline__ float chain_add(const float* __restrict__ p, int L, f
   // A holds entries m .. m+31 (L - m < 64): the rest without single-entry LDS round trips
   float4 B[8];
   chain_load32(p + m + 32, B);
+  // the rest in groups of four: whole groups plain, the group that ends the chain with its extra
+  // entries masked to -0.0 (L differs by at most one between lanes, so only that group branches)
+  auto grp = [&](const float4& g, int e) {
+    if (e + 3 < L) {
+      acc = acc + g.x;
+      acc = acc + g.y;
+      acc = acc + g.z;
+      acc = acc + g.w;
+    } else if (e < L) {
+      acc = acc + g.x;
+      acc = acc + add_operand(g.y, e + 1 < L);
+      acc = acc + add_operand(g.z, e + 2 < L);
+    }
+  };
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int e = m + 4 * u;
-    if (e < L) acc = acc + A[u].x;
-    if (e + 1 < L) acc = acc + A[u].y;
-    if (e + 2 < L) acc = acc + A[u].z;
-    if (e + 3 < L) acc = acc + A[u].w;
-  }
+  for (int u = 0; u < 8; ++u) grp(A[u], m + 4 * u);
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int e = m + 32 + 4 * u;
-    if (e < L) acc = acc + B[u].x;
-    if (e + 1 < L) acc = acc + B[u].y;
-    if (e + 2 < L) acc = acc + B[u].z;
-    if (e + 3 < L) acc = acc + B[u].w;
-  }
+  for (int u = 0; u < 8; ++u) grp(B[u], m + 32 + 4 * u);
   return acc;
 }
 
@@ -2815,39 +2870,6 @@ constexpr int kBigThr = 1024;
 constexpr int kBigWaves = kBigThr / 64;
 constexpr int64_t kBig1Max = 32768;
 
-// One unit-weight sgemv_t lane chain in LDS: acc + x over p[0], p[S], p[2S], ... (L entries). Two
-// 16-entry register groups alternate: a group's reads (immediate offsets from one address) are
-// issued a whole group of dependent adds ahead of their use (scheduling barriers keep them there, as
-// in chain_add). Reads run at most 32 S entries past the chain: the row buffer is padded for them.
-template <int S>
-__device__ __forceinline__ float chain_unit_lds(const float* __restrict__ p, int L, float acc) {
-  float A[16], B[16];
-  auto ld = [&](float (&R)[16], int m) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) R[q] = p[S * (m + q)];
-  };
-  int m = 0;
-  ld(A, 0);
-  for (; m + 32 <= L; m += 32) {
-    ld(B, m + 16);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc = acc + A[q];
-    __builtin_amdgcn_sched_barrier(0);
-    ld(A, m + 32);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc = acc + B[q];
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  ld(B, m + 16);  // A holds entries m .. m + 15; fewer than 32 remain
-#pragma unroll
-  for (int q = 0; q < 16; ++q) acc = m + q < L ? acc + A[q] : acc;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) acc = m + 16 + q < L ? acc + B[q] : acc;
-  return acc;
-}
-constexpr int kChainPad = 32 * 8 + 16;  // floats past the row that the chains' look-ahead may read
 
 // sgemv_block_wave over entries [j0, j0 + NB) of the LDS row: the same lanes, order and operations
 // (8 lanes: first NB & 4 entries on lanes 0..3, then lane (o - h4) % 8, fma with the weight —
@@ -3546,7 +3568,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     a.preload = pre ? atoi(pre) : (4 | 8);
   }
   const SklPlan p1{n, skl_batch_size(1, n, dim), 1, dim, 0, 0};
-  const size_t lds = sizeof(double) * (size_t)dim + sizeof(float) * kBlk;
+  const size_t lds = sizeof(double) * (size_t)dim + sizeof(float) * (kBlk + kChainPad);  // + chain read-ahead
   const bool seq = a.plan.all_seq != 0;
   const bool single = nblk == 1 && T >= 2 && (!seq || XT);
   if (lds > 65536) {
