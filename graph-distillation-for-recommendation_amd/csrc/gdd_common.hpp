@@ -132,6 +132,7 @@ int mb_fused_launch(const MbFusedCall& c, const RngNext& rn, hipStream_t s);
 // than b/2 centres due (np.argsort's branch) is handed to the host through MBState.handoff
 constexpr size_t kReassignLdsCap = 150 * 1024;
 size_t mb_reassign_lds(int64_t bs, int k);
+void mb_reassign_form_refresh();  // re-reads GDD_MB_REASSIGN_FORM (once per fit)
 bool mb_reassign_ok(int64_t bs, int k);
 int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const float* X,
                        const int64_t* rows, float* C_new, float* counts, void* step_ws,

@@ -601,6 +601,7 @@ extern "C" int gdd_minibatch_kmeans_fit(
   // fire — always when k <= b/2. When it fires (k > b/2 only), the device stops at that step and
   // hands it to the host (host_reassign); the host then runs steps while some weight sum is zero
   // (sklearn reassigns at every such step) and resumes the device loop once none is.
+  mb_reassign_form_refresh();
   const bool dev_ok = n_steps > 0 && getenv("GDD_HOST_LOOP") == nullptr && mb_reassign_ok(bs, k);
   // GDD_MB_FUSED=1: one launch per step (k_mb_fused, measured slower at the arxiv shape: every
   // point block redoes its centre group's update); k <= b/2 only; default: the

@@ -2944,6 +2944,13 @@ int mb_rng_launch(const DevMT* in, DevMT* out, int64_t n, int64_t bs, int64_t* r
   return GDD_OK;
 }
 
+// GDD_MB_REASSIGN_FORM (A/B; default kRsParCopy: the block shuffle measured slower)
+static int g_rs_form = kRsParCopy;
+void mb_reassign_form_refresh() {
+  const char* fe = getenv("GDD_MB_REASSIGN_FORM");
+  g_rs_form = fe ? atoi(fe) : kRsParCopy;
+}
+
 size_t mb_reassign_lds(int64_t bs, int k) {
   return sizeof(int) * (size_t)((bs + 1) & ~1ll) + sizeof(int) * (size_t)k + kMtRingBytes;
 }
@@ -2959,8 +2966,7 @@ int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const 
   GDD_REQUIRE(lds <= kReassignLdsCap, "mb_reassign: batch too large for the LDS swap table");
   // GDD_MB_REASSIGN_FORM (A/B): bit 0 the block shuffle, bit 1 the parallel copies (default 2);
   // the copies' index tables (bs/2 + 1 rows: m <= bs/2 here) follow the base layout where they fit
-  const char* fe = getenv("GDD_MB_REASSIGN_FORM");
-  int form = fe ? atoi(fe) : kRsParCopy;  // the block shuffle measured slower
+  int form = g_rs_form;  // read once per fit (mb_reassign_form_refresh): no getenv per launch
   const size_t par_lds =
       ((sizeof(int) * (size_t)(((bs + 1) & ~1ll) + k) + kMtRingBytes + 7) & ~(size_t)7) +
       12 * (size_t)(bs / 2 + 1);
