@@ -332,6 +332,7 @@ constexpr int kFoldElemsMean = 8192;
 constexpr int kFoldElemsSmall = 2048;
 constexpr int kFoldSmallAvgRows = 64;
 constexpr int kFoldMaxR = 1024;
+constexpr int64_t kFoldPadMinRows = 65536;  // the M-step folds a zero-padded copy of X from here (dim % 4 != 0)
 
 struct FoldArgs {
   int dim, fw_max, R;
@@ -351,6 +352,8 @@ struct FoldArgs {
   int step_i;
   int ld = 0;  // row stride of X (0: dim). A column range [f0, f1) folds X + f0 with dim = f1 - f0
   int64_t avg_rows = 0;  // members per cluster on average (0: unknown); small averages fold in 8 KiB chunks
+  int out_dim = 0;  // output row stride and columns written (0: dim); folding a zero-padded copy of X
+                    // (dim a multiple of 4) writes only its first out_dim columns
 };
 
 template <typename ACC, bool WEIGHTED>
@@ -531,7 +534,8 @@ __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
     }
   }
   const int cs = c - a.c0;  // row of the output slice
-  const int64_t ob = (int64_t)cs * dim + f0;
+  const int dout = a.out_dim ? a.out_dim : dim;
+  const int64_t ob = (int64_t)cs * dout + f0;
   if constexpr (MEAN) {
     if (tid < FW) {
       float r;
@@ -543,7 +547,7 @@ __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
     }
     if (blockIdx.x == 0 && tid == 0 && a.counts) a.counts[cs] = nm;
   } else {
-    if (tid < FW) a.out[ob + tid] = (float)acc;
+    if (tid < FW && f0 + tid < dout) a.out[ob + tid] = (float)acc;
     // unit weights: a sequential fp32 count, which sticks at 2^24
     if (blockIdx.x == 0 && tid == 255) a.wsum[cs] = WEIGHTED ? wacc : fminf((float)nm, 16777216.f);
   }
@@ -558,7 +562,7 @@ int fold_launch(const FoldArgs& a0, int count, bool mean, hipStream_t s) {
   for (int off = 0; off < count; off += kFoldMaxGridY) {
     FoldArgs a = a0;
     a.c0 = a0.c0 + off;
-    a.out = a0.out + (int64_t)off * a0.dim;
+    a.out = a0.out + (int64_t)off * (a0.out_dim ? a0.out_dim : a0.dim);
     if (a0.wsum) a.wsum = a0.wsum + off;
     if (a0.counts) a.counts = a0.counts + off;
     const int rc = fold_launch_one(a, std::min(kFoldMaxGridY, count - off), mean, s);
@@ -1328,6 +1332,37 @@ static size_t prune_ws(int64_t n, int k) {
          align256(sizeof(double) * (size_t)k) + 3 * 256;
 }
 
+// The M-step's zero-padded copy of X (r05): for dim % 4 != 0 the fold gathers its rows one float at a
+// time (a 188-byte row is 16-byte aligned one time in four, and unaligned 16-byte loads measured
+// slower, §4); a copy with rows of round4(dim) floats, made once per run, lets it gather 16-byte
+// pieces of aligned rows. Each column's chain is unchanged and the pad columns are not written, so the
+// sums are the same bits.
+static int fold_pad_dim(int64_t n, int dim) {
+  return (dim % 4 != 0 && n >= kFoldPadMinRows) ? (dim + 3) & ~3 : 0;
+}
+
+static size_t fold_pad_ws(int64_t n, int dim) {
+  const int dp = fold_pad_dim(n, dim);
+  return dp ? align256(sizeof(float) * (size_t)n * (size_t)dp) + 256 : 0;
+}
+
+__global__ void k_pad_rows(int64_t n, int dim, int dp, const float* __restrict__ X, float* __restrict__ Xp) {
+  const int q4 = dp / 4;
+  const int64_t total = n * q4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / q4;
+    const int f = (int)(i - r * q4) * 4;
+    const float* src = X + r * dim;
+    float4 v;
+    v.x = f < dim ? src[f] : 0.f;
+    v.y = f + 1 < dim ? src[f + 1] : 0.f;
+    v.z = f + 2 < dim ? src[f + 2] : 0.f;
+    v.w = f + 3 < dim ? src[f + 3] : 0.f;
+    reinterpret_cast<float4*>(Xp)[i] = v;
+  }
+}
+
 // the Lloyd loop's workspace (gdd_kmeans_lloyd_run and the phase entry points below)
 struct LloydWs {
   unsigned long long* keys;
@@ -1368,7 +1403,7 @@ extern "C" size_t gdd_kmeans_lloyd_ws_bytes(int64_t n, int dim, int k) {
   // the bounded E-step's buffers (~36 B per row) only where it can run
   return align256(sizeof(unsigned long long) * (size_t)n) + align256(sizeof(float) * (size_t)k) +
          align256(sizeof(int32_t) * (size_t)n) + align256(sizeof(int32_t) * (size_t)(k + 1)) +
-         group_ws(n, k) + (lloyd_prune_ok(dim, k) ? prune_ws(n, k) : 3 * 256) + 1024;
+         group_ws(n, k) + (lloyd_prune_ok(dim, k) ? prune_ws(n, k) : 3 * 256) + 1024 + fold_pad_ws(n, dim);
 }
 
 extern "C" size_t gdd_kmeans_lloyd_host_ws_bytes(void) { return 4 * sizeof(LloydState); }
@@ -1421,6 +1456,21 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
   if (!resume) GDD_HIP(hipMemsetAsync(&st->changed, 0, sizeof(int32_t), s));
   FoldArgs fa{dim, 0, 0, 0, 0, 0, 0, 0, X, nullptr, perm, offsets, nullptr, wsum, nullptr, 0, &st->stop_at, 0};
   fa.avg_rows = n / k;
+  {  // the fold's zero-padded copy of X at the end of the workspace (GDD_FOLD_PAD=0: gather X itself)
+    const char* pe2 = getenv("GDD_FOLD_PAD");
+    const int dp = fold_pad_dim(n, dim);
+    const size_t base = gdd_kmeans_lloyd_ws_bytes(n, dim, k) - fold_pad_ws(n, dim);
+    const uintptr_t at = (reinterpret_cast<uintptr_t>(ws) + base + 255) & ~uintptr_t(255);
+    if (dp && !(pe2 && pe2[0] == '0') && ws_bytes >= base + fold_pad_ws(n, dim)) {
+      float* Xp = reinterpret_cast<float*>(at);
+      const int64_t total = n * (dp / 4);
+      k_pad_rows<<<(unsigned)std::min<int64_t>((total + 255) / 256, 8192), 256, 0, s>>>(n, dim, dp, X, Xp);
+      GDD_LAUNCHED();
+      fa.X = Xp;
+      fa.dim = dp;
+      fa.out_dim = dim;
+    }
+  }
   {  // M-step: clusters above GDD_FOLD_SLICE x the mean size (default 1.5; 0: off) fold in slices
     const char* fe = getenv("GDD_FOLD_SLICE");
     const double f = fe ? atof(fe) : 1.5;

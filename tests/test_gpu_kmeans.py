@@ -372,6 +372,37 @@ def test_kmeans_lloyd_sliced_fold_matches(monkeypatch, dim):
     assert np.array_equal(bits(a.cluster_centers_), bits(ref["cluster_centers_"]))
 
 
+@pytest.mark.parametrize("dim,prune", [(47, "1"), (47, "0"), (30, "1"), (5, "0")])
+def test_kmeans_lloyd_padded_fold_matches(monkeypatch, dim, prune):
+    """From 65,536 rows with dim % 4 != 0 the M-step folds a zero-padded copy of X (rows of
+    round4(dim) floats, 16-byte gathers; r05) and writes only the real columns: the fit is
+    bit-identical to the fold over X itself (GDD_FOLD_PAD=0), sliced large clusters included, and to
+    the oracle."""
+    rng = np.random.default_rng(100 + dim)
+    sizes = [30000, 16000, 9000, 6000, 4000, 2500, 1500, 800, 400, 200]  # skewed: sliced clusters
+    centres = rng.standard_normal((len(sizes), dim)).astype(np.float32) * np.float32(3.0)
+    X = np.concatenate([c + rng.standard_normal((m, dim)).astype(np.float32) for c, m in zip(centres, sizes)])
+    X = np.ascontiguousarray(X[rng.permutation(len(X))], np.float32)
+    assert len(X) >= 65536
+    k = 10
+    monkeypatch.setenv("GDD_LLOYD_PRUNE", prune)
+    fits = []
+    for pad in ("1", "0"):
+        monkeypatch.setenv("GDD_FOLD_PAD", pad)
+        np.random.seed(15)
+        fits.append(gdd.KMeans(n_clusters=k, n_init=1).fit(X))
+    a, b = fits
+    assert a.n_iter_ == b.n_iter_ and a.inertia_ == b.inertia_
+    assert np.array_equal(a.labels_, b.labels_)
+    assert np.array_equal(bits(a.cluster_centers_), bits(b.cluster_centers_))
+    if dim == 47 and prune == "1":
+        np.random.seed(15)
+        ref = O.kmeans(X, k, n_init=1)
+        assert a.n_iter_ == ref["n_iter_"]
+        assert np.array_equal(a.labels_, ref["labels_"])
+        assert np.array_equal(bits(a.cluster_centers_), bits(ref["cluster_centers_"]))
+
+
 @pytest.mark.parametrize("case", ["ml1m_users", "ml1m_items", "relocation", "tol0", "large_n"])
 def test_kmeans_lloyd_update_forms(monkeypatch, case):
     """The one-workgroup update (empty check, _average_centers + shifts, labels changed, convergence

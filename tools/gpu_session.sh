@@ -38,6 +38,9 @@
 #   prop-pair             tools/micro_prop.py at arxiv / products, paired target updates on / off
 #   reddit | products     tools/bench_induct.py | tools/bench_products.py (config 3 / 5 shapes)
 #   recsys | alidisplay   tools/bench_recsys_e2e.py [alidisplay] (config 4 end to end)
+#   products-lloyd        tools/prof_products_lloyd.py under rocprofv3 --kernel-trace --stats (the products
+#                         record's KMeans, per-kernel split + final cluster sizes)
+#   pad-ab                tools/prof_products_lloyd.py with the fold's padded copy on / off (GDD_FOLD_PAD), 3x
 #   agent                 the transductive drop-in on synthetic ogbn-arxiv (main_transduct.sh's r=0.5% line)
 # e.g. /usr/local/graft/bin/gpurun -- 'bash tools/gpu_session.sh r03a tests=tests/test_gpu_kpp.py bench trace'
 set -o pipefail
@@ -127,6 +130,9 @@ for step in "$@"; do
     prop-pair) run 300 prop_pair bash -c 'python tools/micro_prop.py && GDD_PROP_PAIR=0 python tools/micro_prop.py && python tools/micro_prop.py && GDD_PROP_PAIR=0 python tools/micro_prop.py && python tools/micro_prop.py products && GDD_PROP_PAIR=0 python tools/micro_prop.py products' ;;
     reddit) run 400 reddit python tools/bench_induct.py ;;
     products) run 600 products python tools/bench_products.py ;;
+    pad-ab) run 400 pad_ab env PADS=1,0,1,0,1,0 python tools/prof_products_lloyd.py "$OUT/cluster_sizes.npy" ;;
+    products-lloyd) run 400 products_lloyd rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$OUT/lloyd" -o lloyd -- python3 tools/prof_products_lloyd.py "$OUT/cluster_sizes.npy" ;;
     recsys) run 400 recsys python tools/bench_recsys_e2e.py ;;
     alidisplay) run 400 alidisplay python tools/bench_recsys_e2e.py alidisplay ;;
     agent) run 600 agent env PYTHONPATH=graph-distillation-for-recommendation_amd python -m gdd.train_clustgdd_transduct \
