@@ -153,7 +153,7 @@ bool lloyd_prune_ok(int dim, int k);
 int kmeans_assign_top2_dev(int64_t n_max, int dim, const float* X, const int64_t* rows,
                            const int64_t* n_dev, int k, const float* C, float* cn2,
                            unsigned long long* keys, float* sec, const int32_t* stop, int step_i,
-                           hipStream_t s);
+                           hipStream_t s, const float* Xp = nullptr, int ldp = 0);
 
 // `stop` (nullable) points at a device stop word (0 = running, s+1 = a test fired at step s; the
 // MiniBatch MBState::stop_at, the Lloyd LloydState::stop_at). Kernels of a later step return at

@@ -415,7 +415,9 @@ __global__ __launch_bounds__(256) void k_assign_persist(int64_t n, int dim, int 
 // spill at three waves per SIMD.
 // TOP2 (one centre chunk, gridDim.y == 1): also sec[i] = the second-smallest distance of row i;
 // n_dev (nullable): the row count is read on the device (a row list built by an earlier kernel).
-template <int NT, int W, bool CONTIG, int F, bool TOP2 = false>
+// ROW4 (row lists only): X is a zero-padded copy with 16-byte aligned rows of ldx floats (the Lloyd
+// run's M-step copy, r05); each lane of a row's pair reads F 16-byte pieces instead of 4F floats
+template <int NT, int W, bool CONTIG, int F, bool TOP2 = false, bool ROW4 = false>
 __global__ __launch_bounds__(64 * W) void k_assign_waves(int64_t n, int dim, int dimp,
                                                          const float* __restrict__ X,
                                                          const int64_t* __restrict__ rows, int k,
@@ -424,7 +426,8 @@ __global__ __launch_bounds__(64 * W) void k_assign_waves(int64_t n, int dim, int
                                                          unsigned long long* __restrict__ keys,
                                                          const int32_t* __restrict__ stop, int step_i,
                                                          float* __restrict__ sec = nullptr,
-                                                         const int64_t* __restrict__ n_dev = nullptr) {
+                                                         const int64_t* __restrict__ n_dev = nullptr,
+                                                         int ldx = 0) {
   if (stopped(stop, step_i)) return;
   if (n_dev) n = *n_dev;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -470,6 +473,19 @@ __global__ __launch_bounds__(64 * W) void k_assign_waves(int64_t n, int dim, int
           v4[j] = make_float4(q[0], q[1], q[2], q[3]);
         }
       }
+    } else if constexpr (ROW4) {
+      const int64_t pi = tt * 32 + pr;
+      const bool ok = pi < n;
+      const float4* xr4 = reinterpret_cast<const float4*>(X + (ok ? (rows ? rows[pi] : pi) : 0) * (int64_t)ldx);
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        const int q = 2 * j + ph;
+        const float4 w = (ok && 4 * q < dim) ? xr4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[4 * j] = w.x;
+        v[4 * j + 1] = w.y;
+        v[4 * j + 2] = w.z;
+        v[4 * j + 3] = w.w;
+      }
     } else {
       const int64_t pi = tt * 32 + pr;
       const bool ok = pi < n;
@@ -504,6 +520,15 @@ __global__ __launch_bounds__(64 * W) void k_assign_waves(int64_t n, int dim, int
             }
             Pw[r * S + c] = q[u];
           }
+        }
+      }
+    } else if constexpr (ROW4) {
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int c = 4 * (2 * j + ph) + u;
+          if (c < dim) Pw[pr * S + c] = v[4 * j + u];
         }
       }
     } else {
@@ -2162,7 +2187,7 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
         const int64_t gxw = std::min<int64_t>((wtiles + wv - 1) / wv, per);
         kern<<<dim3((unsigned)gxw, (unsigned)gyw), 64 * wv, ldsw, s>>>(n, dim, dimpw, X, rows, k, C,
                                                                       c_norm2, cchw, keys, stop, step_i,
-                                                                      nullptr, nullptr);
+                                                                      nullptr, nullptr, 0);
         GDD_LAUNCHED();
         return GDD_OK;
       };
@@ -2260,7 +2285,7 @@ bool lloyd_prune_ok(int dim, int k) { return top2_waves(dim, k) > 0; }
 int kmeans_assign_top2_dev(int64_t n_max, int dim, const float* X, const int64_t* rows,
                            const int64_t* n_dev, int k, const float* C, float* cn2,
                            unsigned long long* keys, float* sec, const int32_t* stop, int step_i,
-                           hipStream_t s) {
+                           hipStream_t s, const float* Xp, int ldp) {
   const int Wn = top2_waves(dim, k);
   GDD_REQUIRE(Wn > 0 && n_max > 0, "assign_top2: unsupported shape");
   k_row_norms<<<blocks_for(k), 256, 0, s>>>(k, dim, C, cn2, stop, step_i);
@@ -2270,6 +2295,9 @@ int kmeans_assign_top2_dev(int64_t n_max, int dim, const float* X, const int64_t
   const size_t lds = assign_lds(Wn, dimpw, cch);
   const int64_t wtiles = (n_max + 31) / 32;
   const bool contig = rows == nullptr && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+  // a row list over the padded copy: 16-byte pieces of aligned rows (F = 6 pieces per lane cover 48)
+  const bool row4 = !contig && Xp && ldp % 4 == 0 && ldp >= dim && ldp <= 48 &&
+                    (reinterpret_cast<uintptr_t>(Xp) & 15) == 0;
   auto go = [&](auto kern, int wv) -> int {
     if (lds > 65536)
       GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2277,14 +2305,15 @@ int kmeans_assign_top2_dev(int64_t n_max, int dim, const float* X, const int64_t
     const int rrc = resident_blocks((const void*)kern, 64 * wv, lds, &res);
     if (rrc) return rrc;
     const int64_t gx = std::max<int64_t>(1, std::min<int64_t>((wtiles + wv - 1) / wv, res));
-    kern<<<dim3((unsigned)gx, 1), 64 * wv, lds, s>>>(n_max, dim, dimpw, X, rows, k, C, cn2, cch, keys,
-                                                     stop, step_i, sec, n_dev);
+    kern<<<dim3((unsigned)gx, 1), 64 * wv, lds, s>>>(n_max, dim, dimpw, row4 ? Xp : X, rows, k, C, cn2, cch,
+                                                     keys, stop, step_i, sec, n_dev, row4 ? ldp : 0);
     GDD_LAUNCHED();
     return GDD_OK;
   };
   auto pick = [&](auto W_) -> int {
     constexpr int Wc = decltype(W_)::value;
-    return contig ? go(k_assign_waves<2, Wc, true, 6, true>, Wc) : go(k_assign_waves<2, Wc, false, 6, true>, Wc);
+    if (contig) return go(k_assign_waves<2, Wc, true, 6, true>, Wc);
+    return row4 ? go(k_assign_waves<2, Wc, false, 6, true, true>, Wc) : go(k_assign_waves<2, Wc, false, 6, true>, Wc);
   };
   if (Wn == 12) return pick(std::integral_constant<int, 12>());
   if (Wn == 8) return pick(std::integral_constant<int, 8>());

@@ -1456,6 +1456,8 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
   if (!resume) GDD_HIP(hipMemsetAsync(&st->changed, 0, sizeof(int32_t), s));
   FoldArgs fa{dim, 0, 0, 0, 0, 0, 0, 0, X, nullptr, perm, offsets, nullptr, wsum, nullptr, 0, &st->stop_at, 0};
   fa.avg_rows = n / k;
+  const float* Xpad = nullptr;  // the padded copy for the bounded E-step's row lists (GDD_ESTEP_PAD=0: X)
+  int dpad = 0;
   {  // the fold's zero-padded copy of X at the end of the workspace (GDD_FOLD_PAD=0: gather X itself)
     const char* pe2 = getenv("GDD_FOLD_PAD");
     const int dp = fold_pad_dim(n, dim);
@@ -1469,6 +1471,11 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
       fa.X = Xp;
       fa.dim = dp;
       fa.out_dim = dim;
+      const char* pe3 = getenv("GDD_ESTEP_PAD");
+      if (!(pe3 && pe3[0] == '0')) {
+        Xpad = Xp;
+        dpad = dp;
+      }
     }
   }
   {  // M-step: clusters above GDD_FOLD_SLICE x the mean size (default 1.5; 0: off) fold in slices
@@ -1496,7 +1503,7 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
           GDD_LAUNCHED();
         }
         rc = kmeans_assign_top2_dev(n, dim, X, first ? nullptr : list, first ? nullptr : count, k, cin,
-                                    cn2, keys, sec, &st->stop_at, sa, s);
+                                    cn2, keys, sec, &st->stop_at, sa, s, Xpad, dpad);
         if (rc) return rc;
         k_ham_finalize<<<fgrid, 256, 0, s>>>(count, n, first ? nullptr : list, keys, sec, xn, glob,
                                              kappa, labels, ub, lb, &st->stop_at, sa);

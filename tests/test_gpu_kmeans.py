@@ -375,9 +375,9 @@ def test_kmeans_lloyd_sliced_fold_matches(monkeypatch, dim):
 @pytest.mark.parametrize("dim,prune", [(47, "1"), (47, "0"), (30, "1"), (5, "0")])
 def test_kmeans_lloyd_padded_fold_matches(monkeypatch, dim, prune):
     """From 65,536 rows with dim % 4 != 0 the M-step folds a zero-padded copy of X (rows of
-    round4(dim) floats, 16-byte gathers; r05) and writes only the real columns: the fit is
-    bit-identical to the fold over X itself (GDD_FOLD_PAD=0), sliced large clusters included, and to
-    the oracle."""
+    round4(dim) floats, 16-byte gathers; r05) and writes only the real columns, and the bounded
+    E-step reads its row lists from the same copy: the fit is bit-identical to the passes over X
+    itself (GDD_FOLD_PAD=0 / GDD_ESTEP_PAD=0), sliced large clusters included, and to the oracle."""
     rng = np.random.default_rng(100 + dim)
     sizes = [30000, 16000, 9000, 6000, 4000, 2500, 1500, 800, 400, 200]  # skewed: sliced clusters
     centres = rng.standard_normal((len(sizes), dim)).astype(np.float32) * np.float32(3.0)
@@ -387,14 +387,17 @@ def test_kmeans_lloyd_padded_fold_matches(monkeypatch, dim, prune):
     k = 10
     monkeypatch.setenv("GDD_LLOYD_PRUNE", prune)
     fits = []
-    for pad in ("1", "0"):
+    # the bounded E-step's row lists also read the padded copy (GDD_ESTEP_PAD; r05)
+    for pad, epad in (("1", "1"), ("1", "0"), ("0", "0")):
         monkeypatch.setenv("GDD_FOLD_PAD", pad)
+        monkeypatch.setenv("GDD_ESTEP_PAD", epad)
         np.random.seed(15)
         fits.append(gdd.KMeans(n_clusters=k, n_init=1).fit(X))
-    a, b = fits
-    assert a.n_iter_ == b.n_iter_ and a.inertia_ == b.inertia_
-    assert np.array_equal(a.labels_, b.labels_)
-    assert np.array_equal(bits(a.cluster_centers_), bits(b.cluster_centers_))
+    a = fits[0]
+    for b in fits[1:]:
+        assert a.n_iter_ == b.n_iter_ and a.inertia_ == b.inertia_
+        assert np.array_equal(a.labels_, b.labels_)
+        assert np.array_equal(bits(a.cluster_centers_), bits(b.cluster_centers_))
     if dim == 47 and prune == "1":
         np.random.seed(15)
         ref = O.kmeans(X, k, n_init=1)

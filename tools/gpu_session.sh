@@ -130,7 +130,7 @@ for step in "$@"; do
     prop-pair) run 300 prop_pair bash -c 'python tools/micro_prop.py && GDD_PROP_PAIR=0 python tools/micro_prop.py && python tools/micro_prop.py && GDD_PROP_PAIR=0 python tools/micro_prop.py && python tools/micro_prop.py products && GDD_PROP_PAIR=0 python tools/micro_prop.py products' ;;
     reddit) run 400 reddit python tools/bench_induct.py ;;
     products) run 600 products python tools/bench_products.py ;;
-    pad-ab) run 400 pad_ab env PADS=1,0,1,0,1,0 python tools/prof_products_lloyd.py "$OUT/cluster_sizes.npy" ;;
+    pad-ab) run 400 pad_ab env PADS=${PADS:-11,10,11,10,11,10} python tools/prof_products_lloyd.py "$OUT/cluster_sizes.npy" ;;
     products-lloyd) run 400 products_lloyd rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/lloyd" -o lloyd -- python3 tools/prof_products_lloyd.py "$OUT/cluster_sizes.npy" ;;
     recsys) run 400 recsys python tools/bench_recsys_e2e.py ;;
