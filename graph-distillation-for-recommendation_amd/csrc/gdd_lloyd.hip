@@ -553,6 +553,172 @@ __global__ __launch_bounds__(256) void k_seg_fold(const FoldArgs a) {
   }
 }
 
+// The Lloyd sums over 16-byte aligned rows (r05; unit weights, FW <= 64): one wave folds, three
+// gather. k_seg_fold's folding threads read one LDS float per add from row-major chunks while the same
+// waves gather, and at the products shape (a 48-float padded row, 336-row chunks) the fold's dependent
+// chain set the chunk time. Here the chunks are stored column-major (column f's rows contiguous,
+// stride RS = R + 4 floats: RS/4 odd spreads eight consecutive columns over distinct bank groups), so
+// lane f of wave 0 reads four rows per 16-byte LDS read, eight reads (32 rows) ahead of its adds, and
+// waves 1..3 keep chunk i+2's rows in flight (registers) and chunk i+3's member ids (a three-slot LDS
+// ring) while chunk i is folded. Same chains, same order: rows past a chunk's end are staged as +0.0.
+constexpr int kCmGatherThreads = 192;
+
+__global__ __launch_bounds__(256) void k_seg_fold_cm(const FoldArgs a) {
+  if (stopped(a.stop, a.step_i)) return;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int dim = a.dim, tid = threadIdx.x;
+  const int64_t ldx = a.ld ? a.ld : dim;
+  const int c = a.c0 + (int)blockIdx.y;
+  const int32_t b = a.offsets[c], e = a.offsets[c + 1];
+  const int nm = e - b;
+  const bool big = a.big_rows > 0 && nm >= a.big_rows;
+  const int fw = big ? a.fw_big : a.fw_max;
+  const int f0 = blockIdx.x * fw;
+  if (f0 >= dim) return;
+  const int R = big ? a.R_big : a.R;
+  const int RS = R + 4;
+  const int FW = min(fw, dim - f0);
+  const int FWu = FW >> 2;
+  // two column-major chunk buffers of FW x RS floats
+  const int bufsz = max(a.fw_max * (a.R + 4), a.fw_big * (a.R_big + 4));
+  float* Bb = smem;
+  float acc = 0.f;
+  if (nm > 0) {
+    const int nch = (nm + R - 1) / R;
+    const bool gat = tid >= 64;
+    const int g = tid - 64;
+    // gather slots: idx = g + 192 j over R x FWu float4 pieces (row r = idx / FWu, piece q = idx % FWu)
+    const int dr = kCmGatherThreads / FWu, dq = kCmGatherThreads % FWu;
+    const int r_init = gat ? g / FWu : 0, q_init = gat ? g % FWu : 0;
+    // every slot loads (rows past R repeat row R-1 and are not stored): the outstanding-load counts
+    // are static, so waiting for one chunk's rows never waits for the next chunk's ids
+    constexpr int kMaxSlot = 22;  // R * FWu <= 16384 / 4 = 4096 pieces over 192 threads
+    float4 xv[kMaxSlot];
+    int32_t idr[kMaxSlot];
+    auto fetch_ids = [&](int chunk) {  // each slot's member id, straight from perm
+      const int m0 = chunk * R;
+      const int last = min(R, nm - m0) - 1;
+      int r = r_init, q = q_init;
+#pragma unroll
+      for (int j = 0; j < kMaxSlot; ++j) {
+        idr[j] = a.perm[b + m0 + min(r, last)];
+        r += dr;
+        q += dq;
+        if (q >= FWu) {
+          q -= FWu;
+          ++r;
+        }
+      }
+    };
+    auto gather = [&]() {
+      int r = r_init, q = q_init;
+#pragma unroll
+      for (int j = 0; j < kMaxSlot; ++j) {
+        (void)r;
+        xv[j] = *reinterpret_cast<const float4*>(a.X + (int64_t)idr[j] * ldx + f0 + 4 * q);
+        r += dr;
+        q += dq;
+        if (q >= FWu) {
+          q -= FWu;
+          ++r;
+        }
+      }
+    };
+    auto store = [&](int chunk) {
+      float* B = Bb + (chunk & 1) * bufsz;
+      const int rows = min(R, nm - chunk * R);
+      int r = r_init, q = q_init;
+#pragma unroll
+      for (int j = 0; j < kMaxSlot; ++j) {
+        if (r < R) {
+          const bool live = r < rows;
+          float* d = B + (4 * q) * RS + r;
+          d[0] = live ? xv[j].x : 0.f;
+          d[RS] = live ? xv[j].y : 0.f;
+          d[2 * RS] = live ? xv[j].z : 0.f;
+          d[3 * RS] = live ? xv[j].w : 0.f;
+        }
+        r += dr;
+        q += dq;
+        if (q >= FWu) {
+          q -= FWu;
+          ++r;
+        }
+      }
+    };
+    // prologue: chunk 0 staged, chunk 1's rows and chunk 2's ids in flight
+    if (gat) {
+      fetch_ids(0);
+      gather();
+      store(0);
+      if (nch > 1) {
+        fetch_ids(1);
+        gather();
+      }
+      if (nch > 2) fetch_ids(2);
+    }
+    __syncthreads();
+    for (int i = 0; i < nch; ++i) {
+      if (tid < 64) {
+        if (tid < FW) {  // column tid of chunk i: 16-byte reads, eight (32 rows) ahead of the adds
+          const float* col = Bb + (i & 1) * bufsz + tid * RS;
+          const int rows = min(R, nm - i * R);
+          const int n4 = (rows + 3) >> 2;
+          float4 A[8], Bv[8];
+          auto ld = [&](float4(&v)[8], int g0) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = reinterpret_cast<const float4*>(col)[min(g0 + u, (R >> 2) - 1)];
+          };
+          auto add = [&](const float4(&v)[8], int g0) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              if (g0 + u < n4) {
+                acc = acc + v[u].x;
+                acc = acc + v[u].y;
+                acc = acc + v[u].z;
+                acc = acc + v[u].w;
+              }
+            }
+          };
+          ld(A, 0);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(A[u].x), "+v"(A[u].y), "+v"(A[u].z), "+v"(A[u].w));
+          int g0 = 0;
+          for (; g0 + 16 <= n4; g0 += 16) {
+            ld(Bv, g0 + 8);
+            __builtin_amdgcn_sched_barrier(0);
+            add(A, g0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (g0 + 16 < n4) ld(A, g0 + 16);
+            __builtin_amdgcn_sched_barrier(0);
+            add(Bv, g0 + 8);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if (g0 < n4) {
+            add(A, g0);
+            if (g0 + 8 < n4) {
+              ld(Bv, g0 + 8);
+              add(Bv, g0 + 8);
+            }
+          }
+        }
+      } else if (gat) {
+        if (i + 1 < nch) store(i + 1);  // buffer (i+1)&1 was last read in iteration i-1
+        if (i + 2 < nch) {
+          gather();                      // chunk i+2's rows (its ids landed an iteration ago)
+          if (i + 3 < nch) fetch_ids(i + 3);
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int cs = c - a.c0;
+  const int dout = a.out_dim ? a.out_dim : dim;
+  const int64_t ob = (int64_t)cs * dout + f0;
+  if (tid < FW && f0 + tid < dout) a.out[ob + tid] = acc;
+  if (blockIdx.x == 0 && tid == 255) a.wsum[cs] = fminf((float)nm, 16777216.f);
+}
+
 // clusters [a0.c0, a0.c0 + count): launches of at most kFoldMaxGridY clusters (grid.y), each
 // writing its slice of the outputs
 constexpr int kFoldMaxGridY = 65535;
@@ -597,8 +763,20 @@ int fold_launch_one(const FoldArgs& a0, int count, bool mean, hipStream_t s) {
   }
   a.Rmax = std::max(a.R, a.R_big);
   if (count == 0) return GDD_OK;
-  const size_t lds = sizeof(float) * (2 * (size_t)elems + 3 * (size_t)a.Rmax * (weighted ? 2 : 1));
   dim3 grid(nsl, (unsigned)count);
+  {  // unit-weight Lloyd sums over 16-byte aligned rows: the column-major form (GDD_FOLD_CM=0: off)
+    const char* ce = getenv("GDD_FOLD_CM");
+    if (!mean && !weighted && !small && vec && a.fw_max <= 64 && a.fw_big <= 64 && !(ce && ce[0] == '0')) {
+      const size_t bufsz = std::max<size_t>((size_t)a.fw_max * (a.R + 4), (size_t)a.fw_big * (a.R_big + 4));
+      const size_t lds_cm = sizeof(float) * 2 * bufsz;
+      GDD_HIP(hipFuncSetAttribute((const void*)k_seg_fold_cm, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds_cm));
+      k_seg_fold_cm<<<grid, 256, lds_cm, s>>>(a);
+      GDD_LAUNCHED();
+      return GDD_OK;
+    }
+  }
+  const size_t lds = sizeof(float) * (2 * (size_t)elems + 3 * (size_t)a.Rmax * (weighted ? 2 : 1));
   auto go = [&](auto kern) -> int {
     GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     kern<<<grid, 256, lds, s>>>(a);
