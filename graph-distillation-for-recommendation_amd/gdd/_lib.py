@@ -98,6 +98,8 @@ SIGNATURES = {
                                      _vp, _vp, _c_size, _vp]),
     "gdd_standard_scaler": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "gdd_center_columns": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "gdd_center_columns_ws_bytes": (_c_size, [_c_i64, _c_int]),
+    "gdd_center_columns_ws": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
     "gdd_standard_scaler_transform": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "gdd_cluster_mean": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _c_int, _c_int, _vp, _vp, _vp]),
     "gdd_cluster_mean_part": (_c_int, [_c_i64, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,

@@ -445,9 +445,11 @@ class KMeans(_BaseKMeans):
         Xd = torch.empty_like(X0)
         mean_d = torch.empty(dim, dtype=torch.float32, device=dev)
         var_d = torch.empty(dim, dtype=torch.float32, device=dev)
-        _lib.check(_lib.device_lib().gdd_center_columns(n, dim, X0.data_ptr(), Xd.data_ptr(),
-                                                        mean_d.data_ptr(), var_d.data_ptr(),
-                                                        _lib.stream_ptr(dev)))
+        clib = _lib.device_lib()
+        cws = _lib.workspace(clib.gdd_center_columns_ws_bytes(n, dim), dev)
+        _lib.check(clib.gdd_center_columns_ws(n, dim, X0.data_ptr(), Xd.data_ptr(), mean_d.data_ptr(),
+                                              var_d.data_ptr(), cws.data_ptr(), cws.numel(),
+                                              _lib.stream_ptr(dev)))
         X_mean = mean_d.cpu().numpy()
         tol_ = 0 if self.tol == 0 else np.mean(var_d.cpu().numpy()) * self.tol
         del X0

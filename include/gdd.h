@@ -337,6 +337,12 @@ int gdd_standard_scaler(int64_t n, int dim, const float* X, float* X_out, double
 /* X_out = X - mean (fp32). mean/var: dim floats. X_out may not alias X.                           */
 int gdd_center_columns(int64_t n, int dim, const float* X, float* X_out, float* mean, float* var,
                        gdd_stream_t stream);
+/* The same with a workspace (r05): from 65,536 rows and 2 <= dim <= 256 the column chains run in the   */
+/* exact parallel form (gdd_colsum.hip: per-segment transducers of the sequential fp32 sum, signed     */
+/* terms); otherwise, or with GDD_CENTER_PAR=0, gdd_center_columns. Same bits either way.              */
+size_t gdd_center_columns_ws_bytes(int64_t n, int dim);
+int gdd_center_columns_ws(int64_t n, int dim, const float* X, float* X_out, float* mean, float* var,
+                          void* ws, size_t ws_bytes, gdd_stream_t stream);
 /* StandardScaler.transform with a fitted mean/scale (utils_graphsaint.py:41-44 fits on the train   */
 /* rows and transforms every row): X_out = fp32(fp32(x - mean) / scale).                            */
 int gdd_standard_scaler_transform(int64_t n, int dim, const float* X, const double* mean,

@@ -247,6 +247,56 @@ def test_center_columns_matches_numpy(n, dim):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), (X - m).view(np.uint32))
 
 
+def _colsum_cases():
+    rng = np.random.default_rng(11)
+    yield "gaussian", 100000, 47, (rng.standard_normal((100000, 47)) * 3 + 1).astype(np.float32)
+    # zero-mean columns: the running sums wander across binades and signs (many re-walked segments)
+    yield "zero-mean", 70001, 64, rng.standard_normal((70001, 64)).astype(np.float32)
+    X = rng.standard_normal((131072, 5)).astype(np.float32)
+    X[:, 1] = (rng.integers(-4, 5, 131072) * 0.5 + 2 ** 22).astype(np.float32)  # ties past 2^24
+    X[:, 2] = np.float32(0.1)                                                 # constant
+    X[::2, 3] = np.float32(1e-3)                                              # cancel to zero
+    X[1::2, 3] = np.float32(-1e-3)
+    X[:, 4] = (rng.standard_normal(131072) * 10.0 ** rng.integers(-20, 20, 131072)).astype(np.float32)
+    yield "adversarial", 131072, 5, X
+    X = rng.standard_normal((65536, 3)).astype(np.float32)
+    X[4097, 1] = np.inf
+    X[60000, 2] = np.nan
+    yield "non-finite", 65536, 3, X
+    yield "wide", 66000, 256, (rng.standard_normal((66000, 256)) + 0.01).astype(np.float32)
+    yield "two columns", 300000, 2, (rng.standard_normal((300000, 2)) - 0.2).astype(np.float32)
+
+
+@pytest.mark.parametrize("name,n,dim,X", list(_colsum_cases()), ids=[c[0] for c in _colsum_cases()])
+def test_center_columns_parallel_matches_numpy(monkeypatch, name, n, dim, X):
+    """gdd_center_columns_ws (r05): from 65,536 rows the column chains run in the exact parallel form
+    (per-segment transducers of the sequential fp32 sum of signed terms, gdd_colsum.hip; CPU model in
+    tests/test_signed_chain_model.py): mean, var and X - mean bit for bit against numpy and against
+    the sequential chains (GDD_CENTER_PAR=0)."""
+    lib = _lib.device_lib()
+    Xd = torch.from_numpy(X).cuda()
+    res = []
+    for par in ("1", "0"):
+        monkeypatch.setenv("GDD_CENTER_PAR", par)
+        out = torch.empty_like(Xd)
+        mean = torch.empty(dim, dtype=torch.float32, device="cuda")
+        var = torch.empty(dim, dtype=torch.float32, device="cuda")
+        ws = _lib.workspace(lib.gdd_center_columns_ws_bytes(n, dim), "cuda")
+        _lib.check(lib.gdd_center_columns_ws(n, dim, Xd.data_ptr(), out.data_ptr(), mean.data_ptr(),
+                                             var.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_ptr("cuda")))
+        res.append((mean.cpu().numpy(), var.cpu().numpy(), out.cpu().numpy()))
+    with np.errstate(all="ignore"):
+        m = X.mean(axis=0)
+        v = np.var(X, axis=0)
+        o = X - m
+    def same(a, b):  # bit for bit; NaNs compare by position (their sign and payload are the FPU's)
+        na, nb = np.isnan(a), np.isnan(b)
+        return np.array_equal(na, nb) and np.array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
+
+    for mean, var, out in res:
+        assert same(mean, m) and same(var, v) and same(out, o), name
+
+
 # One-launch MiniBatch steps (k_mb_fused, opt-in with GDD_MB_FUSED=1): bit-identical to
 # scikit-learn and to the default two-launch loop on centres, labels, inertia, n_steps_ and
 # the RandomState left behind — across key-buffer groups (G = 1 and 4), row forms (dim % 4 != 0),
