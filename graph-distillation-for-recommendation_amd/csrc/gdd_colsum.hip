@@ -16,9 +16,9 @@
 //   above 2^23 + 1/2 on the side nearer zero (under 2^e the grid halves), checked as >= 2^23 + 1.
 // * Three launches per pass: per-segment fp64 column sums (k_cs_segsum); per (segment, column) the
 //   transducers for the two binades the running sum most likely has there — the fp64 prefix's binade
-//   and its nearer neighbour (k_cs_records); one workgroup per column (k_cs_resolve) scanning the
+//   and its nearer neighbour (k_cs_records); one wave per column (k_cs_resolve) scanning the
 //   segments' transducers from the exact running sum and re-walking a segment where none applies
-//   (k_cs_walk: 4096-term chunks, the first term that leaves the binade added in hardware, resume).
+//   (k_cs_walk: 512-term passes, the first term that leaves the binade added in hardware, resume).
 // * A NaN or infinite term or sum: the rest of that column is added one term at a time.
 #include <cmath>
 #include <cstdlib>
@@ -31,9 +31,9 @@ namespace {
 constexpr int kCsSat = 1 << 27;
 constexpr int kCsTop = 1 << 24;
 constexpr int kCsLow = 1 << 23;
-constexpr int kCsSeg = 4096;   // rows per segment
+constexpr int kCsSeg = 512;    // rows per segment
 constexpr int kCsThr = 256;
-constexpr int kCsWalkE = 16;   // terms per thread per walk chunk (kCsThr * kCsWalkE = kCsSeg)
+constexpr int kCsWalkE = 8;    // terms per lane per walk pass (one wave: 64 * 8 = kCsSeg)
 constexpr int64_t kCsMinRows = 65536;
 
 struct Tr {
@@ -231,12 +231,29 @@ __global__ __launch_bounds__(kCsThr) void k_cs_segsum(int64_t n, int dim, const 
   if (tid < dim) segsum[(int64_t)blockIdx.x * dim + tid] = total;
 }
 
-// exclusive fp64 prefix of the segment sums, one thread per column
-__global__ void k_cs_prefix(int nseg, int dim, const double* __restrict__ segsum, double* __restrict__ pref) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= dim) return;
-  double p = 0.0;
-  for (int b = 0; b < nseg; ++b) {
+// exclusive fp64 prefix of the segment sums, one workgroup per column (thread t sums a contiguous
+// slice, a block scan of the slice totals, then each slice's prefixes; fp64 guesses, any order)
+__global__ __launch_bounds__(kCsThr) void k_cs_prefix(int nseg, int dim, const double* __restrict__ segsum,
+                                                      double* __restrict__ pref) {
+  __shared__ double tot[kCsThr];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int per = (nseg + kCsThr - 1) / kCsThr;
+  const int b0 = min(nseg, tid * per), b1 = min(nseg, b0 + per);
+  double a = 0.0;
+  for (int b = b0; b < b1; ++b) a += segsum[(int64_t)b * dim + c];
+  tot[tid] = a;
+  __syncthreads();
+  if (tid == 0) {
+    double p = 0.0;
+    for (int i = 0; i < kCsThr; ++i) {
+      const double t = tot[i];
+      tot[i] = p;
+      p += t;
+    }
+  }
+  __syncthreads();
+  double p = tot[tid];
+  for (int b = b0; b < b1; ++b) {
     pref[(int64_t)b * dim + c] = p;
     p += segsum[(int64_t)b * dim + c];
   }
@@ -313,65 +330,51 @@ __global__ __launch_bounds__(kCsThr) void k_cs_records(int64_t n, int dim, const
 
 size_t cs_lds_bytes() { return sizeof(float) * (kCsChunk + kCsThr) + sizeof(Tr) * 2 * kCsThr + sizeof(int) * kCsThr; }
 
-// ---- the resolve: one workgroup per column ---------------------------------------------------------
-struct CsLds {
-  Tr scan[kCsThr / 64];
-  int first[kCsThr / 64];
-  float s_new;
-  long long pos_new;
-};
+// ---- the resolve: one wave per column ---------------------------------------------------------------
+__device__ __forceinline__ Tr tr_shfl_up(const Tr& v, int o) {
+  Tr u;
+  u.a0 = __shfl_up(v.a0, o); u.n0 = __shfl_up(v.n0, o); u.x0 = __shfl_up(v.x0, o);
+  u.a1 = __shfl_up(v.a1, o); u.n1 = __shfl_up(v.n1, o); u.x1 = __shfl_up(v.x1, o);
+  return u;
+}
 
-// exclusive in-order scan of one Tr per thread; *total = all composed. Ends with a barrier.
-__device__ Tr cs_block_scan(Tr v, CsLds& L, Tr* total) {
-  constexpr int NW = kCsThr / 64;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+__device__ __forceinline__ Tr tr_shfl(const Tr& v, int l) {
+  Tr u;
+  u.a0 = __shfl(v.a0, l); u.n0 = __shfl(v.n0, l); u.x0 = __shfl(v.x0, l);
+  u.a1 = __shfl(v.a1, l); u.n1 = __shfl(v.n1, l); u.x1 = __shfl(v.x1, l);
+  return u;
+}
+
+// exclusive in-order scan of one Tr per lane of a wave; *total = all 64 composed
+__device__ __forceinline__ Tr cs_wave_scan(const Tr& v, Tr* total) {
+  const int lane = threadIdx.x & 63;
   Tr inc = v;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    Tr up;
-    up.a0 = __shfl_up(inc.a0, o); up.n0 = __shfl_up(inc.n0, o); up.x0 = __shfl_up(inc.x0, o);
-    up.a1 = __shfl_up(inc.a1, o); up.n1 = __shfl_up(inc.n1, o); up.x1 = __shfl_up(inc.x1, o);
+    const Tr up = tr_shfl_up(inc, o);
     if (lane >= o) inc = tr_compose(up, inc);
   }
-  Tr ex;
-  ex.a0 = __shfl_up(inc.a0, 1); ex.n0 = __shfl_up(inc.n0, 1); ex.x0 = __shfl_up(inc.x0, 1);
-  ex.a1 = __shfl_up(inc.a1, 1); ex.n1 = __shfl_up(inc.n1, 1); ex.x1 = __shfl_up(inc.x1, 1);
+  *total = tr_shfl(inc, 63);
+  Tr ex = tr_shfl_up(inc, 1);
   if (lane == 0) ex = tr_ident();
-  if (lane == 63) L.scan[wv] = inc;
-  __syncthreads();
-  Tr wp = tr_ident(), tot = tr_ident();
-#pragma unroll
-  for (int i = 0; i < NW; ++i) {
-    const Tr t = L.scan[i];
-    if (i < wv) wp = tr_compose(wp, t);
-    tot = tr_compose(tot, t);
-  }
-  *total = tot;
-  __syncthreads();
-  return tr_compose(wp, ex);
+  return ex;
 }
 
-__device__ int cs_block_first(bool flag, CsLds& L) {
-  constexpr int NW = kCsThr / 64;
+__device__ __forceinline__ int cs_wave_first(bool flag) {
   const unsigned long long b = __ballot(flag);
-  const int wv = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) L.first[wv] = b ? wv * 64 + __builtin_ctzll(b) : 0x7fffffff;
-  __syncthreads();
-  int mn = 0x7fffffff;
-#pragma unroll
-  for (int i = 0; i < NW; ++i) mn = min(mn, L.first[i]);
-  __syncthreads();
-  return mn;
+  return b ? __builtin_ctzll(b) : 64;
 }
 
-// the workgroup continues column c's sequential sum s over rows [lo, hi) and returns it (all threads)
+// the wave continues column c's sequential sum s over rows [lo, hi) and returns it (every lane): passes
+// of 64 x 8 terms; where the composed path leaves the binade, the lane holding that point walks its
+// terms, adds the leaving one in hardware, and the pass restarts after it
 __device__ float cs_walk(const float* __restrict__ X, int dim, int c, const float* __restrict__ m,
-                         int64_t lo, int64_t hi, float s, CsLds& L) {
-  const int tid = threadIdx.x;
+                         int64_t lo, int64_t hi, float s) {
+  const int lane = threadIdx.x & 63;
   int64_t pos = lo;
   while (pos < hi) {
     if (!(fabsf(s) < __builtin_inff())) break;
-    const int64_t b = pos + (int64_t)tid * kCsWalkE;
+    const int64_t b = pos + (int64_t)lane * kCsWalkE;
     float t[kCsWalkE];
     bool bad = false;
 #pragma unroll
@@ -379,7 +382,7 @@ __device__ float cs_walk(const float* __restrict__ X, int dim, int c, const floa
       t[j] = b + j < hi ? cs_term(X, dim, b + j, c, m) : 0.f;
       bad |= !(fabsf(t[j]) < __builtin_inff());
     }
-    if (__syncthreads_or(bad)) break;
+    if (__ballot(bad) != 0ull) break;
     const int e = cs_binade(s);
     const int S0 = (int)ldexpf(s, 23 - e);
     Tr f = tr_ident();
@@ -392,16 +395,19 @@ __device__ float cs_walk(const float* __restrict__ X, int dim, int c, const floa
       }
     }
     Tr tot;
-    const Tr ex = cs_block_scan(f, L, &tot);
+    const Tr ex = cs_wave_scan(f, &tot);
     const int Sb = S0 + tr_adv(ex, S0);
     const bool fail = !(tr_applies(S0, e, ex) && tr_applies(Sb, e, f));
-    const int cf = cs_block_first(fail, L);
-    if (cf == 0x7fffffff) {
+    const int cf = cs_wave_first(fail);
+    if (cf == 64) {
       s = ldexpf((float)(S0 + tr_adv(tot, S0)), e - 23);
-      pos += (int64_t)kCsThr * kCsWalkE;
+      pos += 64 * kCsWalkE;
       continue;
     }
-    if (tid == cf) {  // its run's prefix applies; find the term that leaves and add it in hardware
+    // lane cf: its run's prefix applies; find the term that leaves and add it in hardware
+    float s_new = 0.f;
+    int j_new = kCsWalkE;
+    if (lane == cf) {
       int S = Sb;
       bool left = false;
 #pragma unroll
@@ -413,52 +419,48 @@ __device__ float cs_walk(const float* __restrict__ X, int dim, int c, const floa
           if (tr_applies(S, e, g)) {
             S += tr_adv(g, S);
           } else {
-            L.s_new = ldexpf((float)S, e - 23) + t[j];
-            L.pos_new = b + j + 1;
+            s_new = ldexpf((float)S, e - 23) + t[j];
+            j_new = j + 1;
             left = true;
           }
         }
       }
     }
-    __syncthreads();
-    s = L.s_new;
-    pos = L.pos_new;
-    __syncthreads();
+    s = __shfl(s_new, cf);
+    pos = pos + (int64_t)cf * kCsWalkE + __shfl(j_new, cf);
   }
-  if (pos < hi) {  // non-finite terms or sum: one term at a time (rare)
-    if (tid == 0) {
-      for (int64_t r = pos; r < hi; ++r) s = s + cs_term(X, dim, r, c, m);
-      L.s_new = s;
-    }
-    __syncthreads();
-    s = L.s_new;
-    __syncthreads();
+  if (pos < hi) {  // non-finite terms or sum: one term at a time (rare), lane 0, then broadcast
+    float r = s;
+    if (lane == 0)
+      for (int64_t i = pos; i < hi; ++i) r = r + cs_term(X, dim, i, c, m);
+    s = __shfl(r, 0);
   }
   return s;
 }
 
-// one workgroup per column: windows of 256 segments, one per thread; in the current binade the
-// segments whose transducer applies are scanned together, the first that does not is walked.
-__global__ __launch_bounds__(kCsThr) void k_cs_resolve(int64_t n, int dim, int nseg, const float* __restrict__ X,
-                                                       const float* __restrict__ m, const CsRec* __restrict__ rec,
-                                                       float* __restrict__ out) {
-  __shared__ CsLds L;
-  const int c = blockIdx.x, tid = threadIdx.x;
+// one wave per column: windows of 64 segments, one per lane; in the current binade the segments whose
+// transducer applies are scanned together, the first that does not is walked
+__global__ __launch_bounds__(64) void k_cs_resolve(int64_t n, int dim, int nseg, const float* __restrict__ X,
+                                                   const float* __restrict__ m, const CsRec* __restrict__ rec,
+                                                   float* __restrict__ out) {
+  const int c = blockIdx.x, lane = threadIdx.x;
   float s = 0.f;
-  for (int g0 = 0; g0 < nseg; g0 += kCsThr) {
-    const int gn = min(kCsThr, nseg - g0);
-    CsRec my{};
-    if (tid < gn) my = rec[(int64_t)(g0 + tid) * dim + c];
+  CsRec nxt{};
+  if (lane < nseg) nxt = rec[(int64_t)lane * dim + c];
+  for (int g0 = 0; g0 < nseg; g0 += 64) {
+    const int gn = min(64, nseg - g0);
+    const CsRec my = nxt;
+    if (g0 + 64 + lane < nseg) nxt = rec[(int64_t)(g0 + 64 + lane) * dim + c];  // the next window in flight
     int b0 = 0;
     while (b0 < gn) {
       if (!(fabsf(s) < __builtin_inff())) {  // the rest one term at a time
-        s = cs_walk(X, dim, c, m, (int64_t)(g0 + b0) * kCsSeg, n, s, L);
+        s = cs_walk(X, dim, c, m, (int64_t)(g0 + b0) * kCsSeg, n, s);
         g0 = nseg;
         break;
       }
       const int e = cs_binade(s);
       const int S0 = (int)ldexpf(s, 23 - e);
-      const bool mine = tid >= b0 && tid < gn;
+      const bool mine = lane >= b0 && lane < gn;
       Tr f = tr_ident();
       bool usable = false;
       if (mine && !my.bad) {
@@ -471,24 +473,21 @@ __global__ __launch_bounds__(kCsThr) void k_cs_resolve(int64_t n, int dim, int n
         }
       }
       Tr tot;
-      const Tr ex = cs_block_scan(f, L, &tot);
+      const Tr ex = cs_wave_scan(f, &tot);
       const int Sb = S0 + tr_adv(ex, S0);
       const bool fail = mine && !(usable && tr_applies(S0, e, ex) && tr_applies(Sb, e, f));
-      const int cf = cs_block_first(fail, L);
-      if (cf == 0x7fffffff) {
+      const int cf = cs_wave_first(fail);
+      if (cf == 64) {
         s = ldexpf((float)(S0 + tr_adv(tot, S0)), e - 23);
         break;
       }
-      if (tid == cf) L.s_new = ldexpf((float)Sb, e - 23);  // the exact sum before segment cf
-      __syncthreads();
-      s = L.s_new;
-      __syncthreads();
+      s = ldexpf((float)__shfl(Sb, cf), e - 23);  // the exact sum before segment cf
       const int64_t lo = (int64_t)(g0 + cf) * kCsSeg, hi = min<int64_t>(n, lo + kCsSeg);
-      s = cs_walk(X, dim, c, m, lo, hi, s, L);
+      s = cs_walk(X, dim, c, m, lo, hi, s);
       b0 = cf + 1;
     }
   }
-  if (tid == 0) out[c] = (float)((double)s / (double)n);  // numpy: sum / n, rounded to fp32
+  if (lane == 0) out[c] = (float)((double)s / (double)n);  // numpy: sum / n, rounded to fp32
 }
 
 int cs_nseg(int64_t n) { return (int)((n + kCsSeg - 1) / kCsSeg); }
@@ -527,11 +526,11 @@ extern "C" int gdd_center_columns_ws(int64_t n, int dim, const float* X, float* 
     float* o = pass == 0 ? mean : var;
     k_cs_segsum<<<(unsigned)nseg, kCsThr, lds, s>>>(n, dim, X, m, pass ? X_out : nullptr, segsum);
     GDD_LAUNCHED();
-    k_cs_prefix<<<(unsigned)((dim + 63) / 64), 64, 0, s>>>(nseg, dim, segsum, pref);
+    k_cs_prefix<<<(unsigned)dim, kCsThr, 0, s>>>(nseg, dim, segsum, pref);
     GDD_LAUNCHED();
     k_cs_records<<<(unsigned)nseg, kCsThr, lds, s>>>(n, dim, X, m, pref, rec);
     GDD_LAUNCHED();
-    k_cs_resolve<<<(unsigned)dim, kCsThr, 0, s>>>(n, dim, nseg, X, m, rec, o);
+    k_cs_resolve<<<(unsigned)dim, 64, 0, s>>>(n, dim, nseg, X, m, rec, o);
     GDD_LAUNCHED();
   }
   return GDD_OK;
