@@ -87,8 +87,7 @@ class _Ops:
         """_kmeans_plusplus (sklearn/cluster/_kmeans.py:174-272) with unit sample weights."""
         n = Xi.shape[0]
         T = 2 + int(np.log(k)) if n_local_trials is None else int(n_local_trials)
-        w = np.ones(n, dtype=np.float32)
-        first = rs.choice(n, p=w / w.sum())
+        first = choice_unit_weights(rs, n)
         if k > 1:
             u = np.concatenate([rs.uniform(size=T) for _ in range(k - 1)])
         else:
@@ -101,6 +100,26 @@ class _Ops:
                                                 u_d.data_ptr(), centers.data_ptr(), idx.data_ptr(),
                                                 ws.data_ptr(), ws.numel(), self.stream))
         return centers, idx
+
+
+def choice_unit_weights(rs, n):
+    """`rs.choice(n, p=w / w.sum())` for unit float32 weights (sklearn/cluster/_kmeans.py:226, the
+    first centre) without numpy's O(n) host arrays (~15 ms at 2.45M points). numpy draws one double u
+    (random_sample) and returns searchsorted(cdf, u, 'right'), cdf = cumsum(p) / cumsum(p)[-1] in fp64,
+    p_i = c = float32(1 / float32(n)). Below 2^24 points every partial sum (i + 1) * c is exact in fp64
+    (c has 24 significant bits, its lowest at or above 2^-45, every partial sum below 2), so
+    cdf[i] = fl64((i + 1) / n), which Python's int division rounds the same way: the index is the first
+    i with (i + 1) / n > u. Pinned against numpy in tests/test_kmeans_host.py."""
+    if n >= 1 << 24:
+        w = np.ones(n, dtype=np.float32)
+        return int(rs.choice(n, p=w / w.sum()))
+    u = rs.random_sample()
+    i = min(n - 1, int(u * n))
+    while i > 0 and i / n > u:  # cdf[i - 1] = i / n > u: step left
+        i -= 1
+    while (i + 1) / n <= u:  # cdf[i] <= u: step right
+        i += 1
+    return i
 
 
 _SIDE_STREAMS = {}
