@@ -1679,6 +1679,12 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
           k_ham_test<<<blocks_of(n, 256 * kHamRows), 256, 0, s>>>(n, dim, labels, xn, ub, lb, shift, sep, glob, kappa,
                                                  list, count, &st->stop_at, sa);
           GDD_LAUNCHED();
+          if (getenv("GDD_LLOYD_LISTLEN")) {  // diagnostics: the bounded E-step's row count (synchronises)
+            int64_t cnt = 0;
+            GDD_HIP(hipMemcpyAsync(&cnt, count, sizeof(cnt), hipMemcpyDeviceToHost, s));
+            GDD_HIP(hipStreamSynchronize(s));
+            fprintf(stderr, "lloyd iteration %d: %lld of %lld rows listed\n", i, (long long)cnt, (long long)n);
+          }
         }
         rc = kmeans_assign_top2_dev(n, dim, X, first ? nullptr : list, first ? nullptr : count, k, cin,
                                     cn2, keys, sec, &st->stop_at, sa, s, Xpad, dpad);
