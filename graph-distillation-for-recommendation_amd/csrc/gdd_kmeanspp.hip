@@ -578,6 +578,7 @@ struct KppArgs {
   float* dist[2];     // [T][n] by round parity
   float* vblk[2];     // [T][nblk] sgemv_t block results
   double* fsum[2];    // [T][nblk] cumulative-potential block totals
+  double* pfx[2];     // [T][n] the block prefixes behind fsum (nullptr: recomputed by the count)
   int64_t* cand[2];   // [kMaxTrials]
   float* pot1;        // [2] T == 1: the round's potential (sdot), by parity
   int* winq;          // [2] round c-1's winning trial, by the parity of c (the split-round path)
@@ -1215,14 +1216,20 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   bool amb;  // a deciding prefix within tol of r (uniform across the workgroup)
   if (jb != INT_MAX) {  // count inside block jb (uniform branch)
     double v[kPer], pre[kPer];
+    if (c >= 2 && a.pfx[pq]) {  // r05: the previous round stored the winner's block prefixes
+      const double* pf = a.pfx[pq] + (int64_t)bw * n;
 #pragma unroll
-    for (int q = 0; q < kPer; ++q) v[q] = (double)wrow[min<int64_t>(e0 + q, n - 1)];  // reads first
+      for (int q = 0; q < kPer; ++q) pre[q] = pf[min<int64_t>(e0 + q, n - 1)];
+    } else {
 #pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-      const int64_t e = e0 + q;
-      v[q] = e < n ? (double)(wv(a.w, e) * (float)v[q]) : 0.0;
+      for (int q = 0; q < kPer; ++q) v[q] = (double)wrow[min<int64_t>(e0 + q, n - 1)];  // reads first
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        const int64_t e = e0 + q;
+        v[q] = e < n ? (double)(wv(a.w, e) * (float)v[q]) : 0.0;
+      }
+      block_prefix(v, pre, s_wave);
     }
-    block_prefix(v, pre, s_wave);
     int cw = 0;
     bool aw = false;
 #pragma unroll
@@ -1343,6 +1350,12 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     block_prefix(v, pre, s_wave);
     const int64_t last = min<int64_t>(n, j0 + kBlk) - 1 - j0;
     if (tid == (int)(last / kPer)) a.fsum[cq][(int64_t)t * a.nblk + blk] = pre[last % kPer];
+    if (a.pfx[cq]) {  // r05: the next round's count inside the winner's block reads these back
+      double* pf = a.pfx[cq] + (int64_t)t * n + j0 + kPer * tid;
+#pragma unroll
+      for (int q = 0; q < kPer; ++q)
+        if (j0 + kPer * tid + q < n) pf[q] = pre[q];
+    }
   }
   const int64_t NB = min<int64_t>(kBlk, a.m1 - j0);
   // the block's lane chains by the exact parallel runs (waves 12..15 precompute, wave 0 walks) when
@@ -3483,7 +3496,8 @@ size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k) {
   b += align256(sizeof(int) * 2) + align256(sizeof(unsigned) * (size_t)std::max(k, 1) * T);  // counters
   if (n <= kBlk || (int64_t)n * std::max(dim, 1) < INT_MAX)
     b += align256(sizeof(float) * n * (size_t)std::max(dim, 1));  // XT
-  if (kpp_big_table(n, dim, (int)T, k)) b += align256(sizeof(float) * n * n);  // multi-block table
+  if (kpp_big_table(n, dim, (int)T, k))
+    b += align256(sizeof(float) * n * n) + 2 * align256(sizeof(double) * n * T);  // table, block prefixes
   if (kpp_small_table(n, dim, (int)T, k)) {
     b += align256(sizeof(float) * n * n);  // distance table
     b += 2 * (align256(sizeof(float) * T * T * n) + align256(sizeof(float) * T * T) +
@@ -3530,6 +3544,13 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   b1.counter = cv.take<unsigned>((size_t)std::max(k, 1) * T);  // rounds c < k, trial t
   float* XT = (n <= kBlk || n * (int64_t)dim < INT_MAX) ? cv.take<float>((size_t)n * dim) : nullptr;
   float* Dbig = kpp_big_table(n, dim, T, k) ? cv.take<float>((size_t)n * n) : nullptr;
+  // the per-block table rounds keep each round's block prefixes (r05; GDD_KPP_STORE_PFX=0: recompute)
+  {
+    const char* pe = getenv("GDD_KPP_STORE_PFX");
+    const bool big1 = n <= kpp_big1_max() && T >= 2 && getenv("GDD_KPP_NO_BIG1") == nullptr;
+    const bool keep_pfx = Dbig && !big1 && !(pe && pe[0] == '0');
+    for (int q = 0; q < 2; ++q) a.pfx[q] = keep_pfx ? cv.take<double>((size_t)n * T) : nullptr;
+  }
   float* Dm = kpp_small_table(n, dim, T, k) ? cv.take<float>((size_t)n * n) : nullptr;
   if (Dm) {
     for (int q = 0; q < 2; ++q) {
