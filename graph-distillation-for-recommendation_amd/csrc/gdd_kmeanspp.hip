@@ -1503,19 +1503,55 @@ __global__ __launch_bounds__(kThr) void k_kpp_dists(KppArgs a, int c) {
     }
   }
   __syncthreads();
-  for (int t = 0; t < T; ++t) {  // the block's cumulative-potential total, per trial
-    double v[kPer], pre[kPer];
-    float xs[kPer];  // every read before the weights' branches (r04)
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) xs[q] = s_d[t * kBlk + kPer * tid + q];
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-      const int64_t e = j0 + kPer * tid + q;
-      v[q] = e < n ? (double)(wv(a.w, e) * xs[q]) : 0.0;
-    }
-    block_prefix(v, pre, s_wave);
+  // the block's cumulative-potential total per trial: block_prefix's operations for every trial with
+  // one barrier (r05; the per-trial calls paid two barriers each), the total kept by the thread that
+  // owns the block's last entry
+  {
+    __shared__ double s_wt[kSplitMaxT][kWaves];
     const int64_t last = min<int64_t>(n, j0 + kBlk) - 1 - j0;
-    if (tid == (int)(last / kPer)) a.fsum[cq][(int64_t)t * a.nblk + blk] = pre[last % kPer];
+    const bool owner = tid == (int)(last / kPer);
+    double rl[kSplitMaxT], exl[kSplitMaxT];
+#pragma unroll
+    for (int t = 0; t < kSplitMaxT; ++t) {
+      rl[t] = 0.0;
+      exl[t] = 0.0;
+      if (t < T) {
+        float xs[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) xs[q] = s_d[t * kBlk + kPer * tid + q];
+        double run = 0.0, r[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+          const int64_t e = j0 + kPer * tid + q;
+          run = run + (e < n ? (double)(wv(a.w, e) * xs[q]) : 0.0);
+          r[q] = run;
+        }
+        double inc = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const double y = __shfl_up(inc, o);
+          if (lane >= o) inc = inc + y;
+        }
+        double ex = __shfl_up(inc, 1);
+        if (lane == 0) ex = 0.0;
+        if (lane == 63) s_wt[t][wave] = inc;
+        exl[t] = ex;
+#pragma unroll
+        for (int q = 0; q < kPer; ++q)
+          if (q == (int)(last % kPer)) rl[t] = r[q];
+      }
+    }
+    __syncthreads();
+    if (owner) {
+#pragma unroll
+      for (int t = 0; t < kSplitMaxT; ++t) {
+        if (t < T) {
+          double B = 0.0;
+          for (int q = 0; q < wave; ++q) B = B + s_wt[t][q];
+          a.fsum[cq][(int64_t)t * a.nblk + blk] = (B + exl[t]) + rl[t];
+        }
+      }
+    }
   }
   const int64_t NB = min<int64_t>(kBlk, a.m1 - j0);
   if (NB > 0 && wave < T) {  // wave t: trial t's sgemv_t block term
