@@ -1038,6 +1038,7 @@ __device__ __forceinline__ float sgemv_block0_par(const float* __restrict__ s, i
                                                   int* s_parsync, const ParLane* __restrict__ s_par,
                                                   const unsigned long long* __restrict__ s_pmask);
 __device__ __forceinline__ void waves_arrive(int* ctr);
+__device__ __forceinline__ bool waves_wait(int* ctr, int target);
 
 // ---- one seeding round ------------------------------------------------------------------------------
 constexpr int kWaveFoldBlk = 16;  // k_kpp_round's barrier-free fold: up to this many sgemv_t blocks
@@ -1052,7 +1053,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   __shared__ int64_t s_ct;
   __shared__ ParLane s_par[PICK ? 1 : 256];  // the block terms' parallel lane chains (r05)
   __shared__ unsigned long long s_pmask[8];
-  __shared__ int s_parsync;
+  __shared__ int s_parsync, s_pfxsync, s_pfxfail;
   const int t = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int pq = (c - 1) & 1, cq = c & 1;
@@ -1062,6 +1063,8 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   if (tid == 0) {
     s_jmin = INT_MAX;
     s_parsync = 0;
+    s_pfxsync = 0;
+    s_pfxfail = 0;
   }
   // r05: requested with the fold's block terms instead of after the winner is known (each was a
   // dependent trip): round c-1's candidates (lane q: trial q's) and, with one block per thread, every
@@ -1337,6 +1340,16 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 24);
   // ---- the block's terms for round c+1: cumulative total, sgemv_t lane chains
+  const int64_t NB = min<int64_t>(kBlk, a.m1 - j0);
+  // the block's lane chains by the exact parallel runs (waves 12..15 precompute, wave 0 walks) when
+  // the weights are unit and the chains are long enough to pay
+  const bool par = !PICK && a.par_chain && a.w == nullptr && NB >= kParMinBlock && a.T > 1;
+  const bool k4x2 = (a.T & 2) && t >= (a.T & ~3) && t < (a.T & ~3) + 2;
+  // r05 (preload bit 32): the block prefix beside the lane chain instead of before it. Every wave posts
+  // its scan total and arrives on an LDS counter; wave 0 (no waves before it: block_prefix's B = 0)
+  // stores its prefixes and runs the chain, the others wait for the count and finish theirs. A wait
+  // that gave up is redone with block_prefix after a closing barrier.
+  const bool ovl = !PICK && !par && (a.preload & 32) && NB > 0 && a.T > 1;
   {
     double v[kPer], pre[kPer];
     float xs[kPer];  // every read before the weights' branches (r04)
@@ -1347,22 +1360,62 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
       const int64_t e = j0 + kPer * tid + q;
       v[q] = e < n ? (double)(wv(a.w, e) * xs[q]) : 0.0;
     }
-    block_prefix(v, pre, s_wave);
     const int64_t last = min<int64_t>(n, j0 + kBlk) - 1 - j0;
-    if (tid == (int)(last / kPer)) a.fsum[cq][(int64_t)t * a.nblk + blk] = pre[last % kPer];
-    if (a.pfx[cq]) {  // r05: the next round's count inside the winner's block reads these back
-      double* pf = a.pfx[cq] + (int64_t)t * n + j0 + kPer * tid;
+    auto emit = [&]() {
+      if (tid == (int)(last / kPer)) a.fsum[cq][(int64_t)t * a.nblk + blk] = pre[last % kPer];
+      if (a.pfx[cq]) {  // r05: the next round's count inside the winner's block reads these back
+        double* pf = a.pfx[cq] + (int64_t)t * n + j0 + kPer * tid;
 #pragma unroll
-      for (int q = 0; q < kPer; ++q)
-        if (j0 + kPer * tid + q < n) pf[q] = pre[q];
+        for (int q = 0; q < kPer; ++q)
+          if (j0 + kPer * tid + q < n) pf[q] = pre[q];
+      }
+    };
+    if (ovl) {
+      double r[kPer];
+      double run = 0.0;
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        run = run + v[q];
+        r[q] = run;
+      }
+      double inc = run;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_up(inc, o);
+        if (lane >= o) inc = inc + y;
+      }
+      double ex = __shfl_up(inc, 1);
+      if (lane == 0) ex = 0.0;
+      if (lane == 63) s_wave[wave] = inc;
+      waves_arrive(&s_pfxsync);
+      bool ok = true;
+      double B = 0.0;
+      if (wave > 0) {
+        ok = waves_wait(&s_pfxsync, kWaves);
+        for (int q = 0; q < wave; ++q) B = B + s_wave[q];
+      }
+      const double base = B + ex;
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) pre[q] = base + r[q];
+      if (ok) emit();
+      else if (lane == 0) s_pfxfail = 1;
+    } else {
+      block_prefix(v, pre, s_wave);
+      emit();
+    }
+    if (ovl && wave == 0) {  // the chain, beside the other waves' prefixes
+      const float y = sgemv_block_wave(s_d, a.w ? a.w + j0 : nullptr, NB, t, a.T);
+      if (lane == 0) a.vblk[cq][(int64_t)t * a.nblk + blk] = y;
+    }
+    if (ovl) {
+      __syncthreads();
+      if (s_pfxfail) {  // a bounded wait gave up: the prefixes again, with barriers
+        block_prefix(v, pre, s_wave);
+        emit();
+      }
     }
   }
-  const int64_t NB = min<int64_t>(kBlk, a.m1 - j0);
-  // the block's lane chains by the exact parallel runs (waves 12..15 precompute, wave 0 walks) when
-  // the weights are unit and the chains are long enough to pay
-  const bool par = !PICK && a.par_chain && a.w == nullptr && NB >= kParMinBlock && a.T > 1;
-  const bool k4x2 = (a.T & 2) && t >= (a.T & ~3) && t < (a.T & ~3) + 2;
-  if (NB > 0 && a.T > 1 && wave == 0) {
+  if (!ovl && NB > 0 && a.T > 1 && wave == 0) {
     float v;
     if (par)
       v = k4x2 ? sgemv_block0_par<4>(s_d, (int)NB, true, &s_parsync, s_par, s_pmask)
@@ -3620,9 +3673,10 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     a.exact = ex ? atoi(ex) : 1;
     const char* pce = getenv("GDD_KPP_PAR_CHAIN");
     a.par_chain = (pce ? pce[0] == '1' : kParChainDefault) ? 1 : 0;
-    // A/B bits (r05): 1 block totals, 2 fold tail, 4 candidates, 8 the barrier-free wave fold
+    // A/B bits (r05): 1 block totals, 2 fold tail, 4 candidates, 8 the barrier-free wave fold,
+    // 32 the block prefix beside the lane chain
     const char* pre = getenv("GDD_KPP_ROUND_PRELOAD");
-    a.preload = pre ? atoi(pre) : (4 | 8);
+    a.preload = pre ? atoi(pre) : (4 | 8 | 32);
   }
   const SklPlan p1{n, skl_batch_size(1, n, dim), 1, dim, 0, 0};
   const size_t lds = sizeof(double) * (size_t)dim + sizeof(float) * (kBlk + kChainPad);  // + chain read-ahead
