@@ -422,7 +422,7 @@ def test_kmeans_lloyd_sliced_fold_matches(monkeypatch, dim):
     assert np.array_equal(bits(a.cluster_centers_), bits(ref["cluster_centers_"]))
 
 
-@pytest.mark.parametrize("dim,prune", [(47, "1"), (47, "0"), (30, "1"), (5, "0")])
+@pytest.mark.parametrize("dim,prune", [(47, "1"), (47, "0"), (30, "1"), (5, "0"), (101, "0")])
 def test_kmeans_lloyd_padded_fold_matches(monkeypatch, dim, prune):
     """From 65,536 rows with dim % 4 != 0 the M-step folds a zero-padded copy of X (rows of
     round4(dim) floats, 16-byte gathers; r05) and writes only the real columns, and the bounded
