@@ -108,6 +108,10 @@ if __name__ == "__main__":
         for (n, dim, k, reps) in [(3000, 40, 454, 5), (6040, 64, 604, 3), (17730, 64, 1773, 1)]:
             run(n, dim, k, reps, check=False)
         sys.exit(0)
+    if sys.argv[1:2] == ["shape"]:  # timing only: micro_kpp.py shape n dim k [reps]
+        n_, d_, k_ = (int(v) for v in sys.argv[2:5])
+        run(n_, d_, k_, int(sys.argv[5]) if len(sys.argv) > 5 else 5, check=False)
+        sys.exit(0)
     if sys.argv[1:2] == ["one"]:  # the MiniBatchKMeans init shape alone, parity checked
         run(3000, 40, 454, 5)
         sys.exit(0)
