@@ -60,7 +60,10 @@ def main():
     X = torch.from_numpy(synth.blobs(cfg.n, cfg.n_classes, cfg.k, seed=1)).cuda()
     for rep in range(2):
         torch.cuda.synchronize()
-        km = gdd.MiniBatchKMeans(n_clusters=cfg.k, random_state=cfg.seed, batch_size=cfg.batch).fit(X)
+        # "nostop": no early stop, so the last step launches are real steps (their stamps complete)
+        extra = dict(max_no_improvement=None, max_iter=1) if sys.argv[1:2] == ["nostop"] else {}
+        km = gdd.MiniBatchKMeans(n_clusters=cfg.k, random_state=cfg.seed, batch_size=cfg.batch,
+                                 **extra).fit(X)
         torch.cuda.synchronize()
         a = read(lib, "kmeans")
         p = read(lib, "kpp")
