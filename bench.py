@@ -21,10 +21,12 @@ star partitions it (gdd.sharded: labels pass by rows, cluster means by clusters,
 bit-identical to one GPU; "scaling": "strong"); at N > 1 the replicas line also carries that mode's
 time for the same graph under ``one_graph``.
 
-At N = 1 the same line carries single-GPU sub-records measured in this run: ``recsys`` (config 4's
-kmeans_cluster pair), ``products`` (config 5 at full shape, fp32 vs bf16 labels pass), ``reddit``
-(config 3's train graph), ``e2e`` (the drop-in agent with main_transduct.sh's arxiv flags: stage
-times and the five GCN accuracies), each with its CPU baseline.
+The same line carries sub-records measured in this run: ``recsys`` (config 4's kmeans_cluster pair),
+``products`` (config 5 at full shape; at N = 1 also fp32 vs bf16 labels pass), ``reddit`` (config
+3's whole inductive path: GraphSAINT split, three role graphs, fit, means), and at N = 1 ``e2e``
+(the drop-in agent with main_transduct.sh's arxiv flags: stage times and the five GCN accuracies)
+and the CPU baselines. At N > 1 the recsys/products/reddit records distil ONE instance over all
+ranks as north_star splits it.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config arxiv] [--mode replicas|one-graph]
                        [--no-cpu-baseline] [--no-extra] [--no-e2e]
@@ -233,14 +235,19 @@ def main():
     copy_gbs = copy_peak(dev)
     mfma = assign_mfma(cfg, dev)
     with_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
-    # the single-GPU sub-records run at N = 1 only (the N > 1 lines measure the replicas/one-graph step)
-    extra = cfg.name == "ogbn-arxiv" and not args.no_extra and world == 1
-    recsys = recsys_record(dev, with_cpu=with_cpu) if extra else None
-    # config 5 and config 3 at their full shapes, and the drop-in agent end to end (VERDICT r4
-    # "What's missing" #1/#2): measured in this run, not read from a committed profile
-    products = products_record(dev, with_cpu=with_cpu) if extra else None
-    reddit = reddit_record(dev, with_cpu=with_cpu) if extra else None
-    e2e = e2e_record(dev) if extra and not args.no_e2e else None
+    # configs 4, 5 and 3 at their full shapes, measured in this run: at N = 1 on one GPU; at N > 1
+    # ONE instance over all ranks as north_star splits it (recsys: the users' and items' fits on
+    # ranks 0 and 1; products: row-partitioned propagation; Reddit: the role graphs on different
+    # ranks) — VERDICT r5 #1/#5. The drop-in agent end to end runs at N = 1.
+    extra = cfg.name == "ogbn-arxiv" and not args.no_extra
+    g_all = None
+    if world > 1:
+        import torch.distributed as dist
+        g_all = dist.group.WORLD
+    recsys = recsys_record(dev, with_cpu=with_cpu, group=g_all, world=world) if extra else None
+    products = products_record(dev, with_cpu=with_cpu, group=g_all, world=world) if extra else None
+    reddit = reddit_record(dev, with_cpu=with_cpu, group=g_all, world=world) if extra else None
+    e2e = e2e_record(dev) if extra and world == 1 and not args.no_e2e else None
 
     out = {
         "metric": "distill wallclock (SpMM+k-means) & test-acc parity, ogbn-arxiv r=0.5% @1-8 GPU",
@@ -305,28 +312,36 @@ def main():
         dist.destroy_process_group()
 
 
-def recsys_record(dev, with_cpu, reps=5):
+def recsys_record(dev, with_cpu, reps=5, group=None, world=1):
     """Config 4's clustering stage on the bipartite recsys graph (north_star's second target):
     distill_recsys.kmeans_cluster (distill_recsys.py:158-181) as main() calls it (:565-583) — users
     then items, StandardScaler + KMeans(n_clusters=k, random_state=42, n_init="auto") — on
     ML-1M-shaped synthetic SVD embeddings (6,040 users x 64 with k = 604, 3,706 items x 64 with
-    k = 371: reduction 0.1, svd 64). Warm calls; wallclock per pair of calls, a synchronised phase
-    split of one more call each, nodes clustered per second, the Lloyd assignment's MFMA use, and
-    the reference's own scikit-learn calls on the host cores beside it."""
+    k = 371: reduction 0.1, svd 64), through gdd.pipeline.kmeans_cluster_pair: at N > 1 the users' fit
+    on rank 0 and the items' on rank 1, results broadcast over RCCL (bit-identical to one GPU). Warm
+    calls; wallclock per pair (max over ranks), nodes clustered per second; at N = 1 also a
+    synchronised phase split of one more call each, the Lloyd assignment's MFMA use, and the
+    reference's own scikit-learn calls on the host cores beside it."""
     from gdd import kmeans as gk
     from gdd import synth
-    from gdd.pipeline import kmeans_cluster, standard_scaler
+    from gdd.pipeline import kmeans_cluster_pair, standard_scaler
     shapes = [("users", 6040, 604), ("items", 3706, 371)]
     E = {name: synth.svd_like(n, 64, seed=n) for name, n, _ in shapes}
-    for name, n, k in shapes:  # warm-up (first-launch code-object loads, allocator)
-        kmeans_cluster(E[name], n_clusters=k, seed=42, minibatch=True, device=dev)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        for name, n, k in shapes:
-            kmeans_cluster(E[name], n_clusters=k, seed=42, minibatch=True, device=dev)
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / reps * 1e3
+
+    def pair():
+        return kmeans_cluster_pair(E["users"], E["items"], 604, 371, seed=42, minibatch=True,
+                                   device=dev, group=group)
+    ms = _timed_ms(pair, reps, world, dev)
+    nodes = sum(n for _, n, _ in shapes)
+    rec = {"workload": "distill_recsys.kmeans_cluster x2 (users 6040x64 k=604, items 3706x64 k=371; "
+                       "StandardScaler + KMeans(random_state=42, n_init='auto')), ML-1M shape",
+           "data": "synthetic SVD-like embeddings (gdd.synth.svd_like)",
+           "parallelism": ("single GPU" if world == 1 else
+                           f"{world} ranks: users' fit on rank 0, items' on rank 1 (independent "
+                           "random_state each), labels and centres broadcast over RCCL"),
+           "ms_per_pair": ms, "nodes_clustered_per_s": nodes / (ms * 1e-3), "cpu_baseline": None}
+    if world > 1:
+        return rec
     phases = {}
     for name, n, k in shapes:
         ph = {}
@@ -364,18 +379,30 @@ def recsys_record(dev, with_cpu, reps=5):
     torch.cuda.synchronize()
     a_ms = ev[0].elapsed_time(ev[1]) / 20
     tf = 2.0 * n * k * 64 / (a_ms * 1e-3) / 1e12
-    nodes = sum(n for _, n, _ in shapes)
-    rec = {"workload": "distill_recsys.kmeans_cluster x2 (users 6040x64 k=604, items 3706x64 k=371; "
-                       "StandardScaler + KMeans(random_state=42, n_init='auto')), ML-1M shape",
-           "data": "synthetic SVD-like embeddings (gdd.synth.svd_like)",
-           "ms_per_pair": ms, "nodes_clustered_per_s": nodes / (ms * 1e-3), "phases_ms": phases,
-           "lloyd_assign_mfma": {"achieved": tf, "peak": FP32_MATRIX_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                 "frac": tf / FP32_MATRIX_PEAK_TFLOPS, "avg_launch_ms": a_ms,
-                                 "shape": "6040 x 64 against 604 centres"},
-           "cpu_baseline": None}
+    rec.update(phases_ms=phases,
+               lloyd_assign_mfma={"achieved": tf, "peak": FP32_MATRIX_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": tf / FP32_MATRIX_PEAK_TFLOPS, "avg_launch_ms": a_ms,
+                                  "shape": "6040 x 64 against 604 centres"})
     if with_cpu:
         rec["cpu_baseline"] = recsys_cpu_baseline(E, shapes)
     return rec
+
+
+def _timed_ms(fn, reps, world, dev, warm=1):
+    """ms per call of fn(): `warm` untimed calls, then `reps` timed ones bracketed by a barrier and a
+    device sync on both sides, the max over ranks."""
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    return 1e3 * max_over_ranks(time.perf_counter() - t0, world, dev) / reps
 
 
 def recsys_cpu_baseline(E, shapes):
@@ -583,7 +610,7 @@ def _cpu_hop_seconds(gn, X, alpha, threads):
     return s
 
 
-def products_record(dev, with_cpu):
+def products_record(dev, with_cpu, group=None, world=1):
     """Config 5 at its full shape on one GPU (BASELINE configs[4]): ogbn-products'
     N = 2,449,029 nodes, mean degree 50.5 (~126M entries), d = 100, C = 47, T = 18, alpha = 0.91,
     KMeans(k = 196) (Lloyd: clustgdd_agent_transduct.py:104-105 for every dataset but arxiv) — the
@@ -605,6 +632,8 @@ def products_record(dev, with_cpu):
     bias = torch.randn(cfg.n_classes, device=dev, generator=gen) * 0.1
     torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
+    if world > 1:
+        return _products_group_record(cfg, g, X, W, bias, gen_s, dev, group, world)
     for _ in range(2):  # the first pass loads code objects and fills the caching allocator
         ph, kph = {}, {}
         torch.cuda.synchronize()
@@ -699,49 +728,123 @@ def products_record(dev, with_cpu):
     return rec
 
 
-def reddit_record(dev, with_cpu):
-    """Config 3's train graph at full shape on one GPU (BASELINE configs[2]; main_induct.sh:16-21:
-    T = 20, alpha = 0.95; clustgdd_agent_induct.py:72-94, 131-134): 153,932 nodes, mean degree 66
-    (~10M entries), d = 602, C = 41 logits, MiniBatchKMeans(k = 769, b = 1000, random_state = 15).
-    k > b/2, so the fit is the one whose reassignment may take the argsort branch. Phases of one warm
-    pass; the fit split by two separate calls of its first and last stages (k-means++ on the
-    3,000-point init subset, the final labels pass). CPU baseline per unit: one torch CPU hop and
-    scikit-learn's MiniBatchKMeans.fit(max_iter=1)."""
+def _products_group_record(cfg, g, X, W, bias, gen_s, dev, group, world):
+    """Config 5's pass distilling ONE graph over all ranks (every rank generates the same graph):
+    propagation row-partitioned when gdd.sharded.propagation_shards_pay says so (one all-gather of
+    each hop's output), KMeans as gdd.sharded.ShardedKMeans (its size model picks rows or
+    replication), cluster means by cluster slices. Bit-identical to one GPU (tests/test_gpu_sharded.py)."""
     import gdd
+    from gdd.pipeline import _lloyd
+    from gdd.sharded import lloyd_rows_pay, propagation_shards_pay
+
+    def one_pass(ph=None):
+        tp = time.perf_counter()
+        gn = gdd.normalize_adj(g)
+        tp = _sync_mark(ph, "normalize", tp) if ph is not None else tp
+        target, _ = gdd.propagate(gn, X, cfg.T, cfg.alpha, group=group)
+        tp = _sync_mark(ph, "propagate", tp) if ph is not None else tp
+        logits = torch.addmm(bias, target, W)
+        km = _lloyd(cfg.k, group, random_state=cfg.seed, device=dev).fit(logits)
+        tp = _sync_mark(ph, "logits_kmeans", tp) if ph is not None else tp
+        gdd.cluster_mean(target, km.labels_device_, cfg.k, group=group)
+        gdd.argmax_rows(km.cluster_centers_device_)
+        if ph is not None:
+            _sync_mark(ph, "cluster_mean", tp)
+        return int(km.n_iter_), gn.nnz
+    ms = _timed_ms(one_pass, 2, world, dev)
+    ph = {}
+    n_iter, nnz = one_pass(ph)
+    return {"workload": f"ogbn-products shape (config 5): N={cfg.n}, nnz_norm={nnz}, d={cfg.d}, "
+                        f"{cfg.T - 1} hops, KMeans(k={cfg.k}), cluster means — ONE graph over {world} ranks",
+            "data": "synthetic: Chung-Lu power-law graph sampled on the device (same seed on every rank)",
+            "parallelism": (f"{world} ranks (gdd.sharded): propagation "
+                            f"{'row-partitioned, one all-gather per hop' if propagation_shards_pay(cfg.n, nnz, cfg.d, world) else 'replicated'}"
+                            f"; Lloyd {'rows' if lloyd_rows_pay(cfg.n, cfg.n_classes, cfg.k, world) else 'replicated'}"
+                            "; cluster means by cluster slices"),
+            "graph_generation_s": gen_s, "ms_total": ms, "nodes_per_s": cfg.n / (ms * 1e-3),
+            "phases_ms_rank0": ph, "kmeans_n_iter": n_iter, "cpu_baseline": None}
+
+
+REDDIT_ROLES = (153932, 23699, 55334)  # GraphSAINT Reddit role.json sizes (train, val, test)
+REDDIT_FULL_DEGREE = 101.7  # 232,965 nodes; the induced train graph then holds ~10.4M entries
+
+
+def reddit_record(dev, with_cpu, group=None, world=1, reps=2):
+    """Config 3's whole inductive hot path at full shape (BASELINE configs[2]; main_induct.sh:16-21:
+    T = 20, alpha = 0.95; clustgdd_agent_induct.py:37-156): a 232,965-node graph (~23.7M entries)
+    split with GraphSAINT's Reddit role sizes (153,932 train / 23,699 val / 55,334 test), d = 602 raw
+    features; one pass = gdd.pipeline.graphsaint_split (train-fitted StandardScaler, three induced
+    role graphs) + pretrained_clustering_induct_hot_path (three normalisations, 3 x 19 hops, 41
+    logits from the train targets, MiniBatchKMeans(k = 769, b = 1000, random_state = 15), cluster
+    means). At N > 1 the role graphs propagate on different ranks (gdd.sharded.role_owners: train on
+    rank 0 — row-partitioned over ranks 0, 3.. where that pays — val on 1, test on 2) and the
+    targets are broadcast; bit-identical to one GPU. Per-role phases of one more pass on rank 0; at
+    N = 1 also the train hop's roofline, the fit split (k-means++ on the 3,000-point init subset, the
+    final labels pass) and per-unit CPU baselines (one torch CPU hop per role graph, scikit-learn's
+    MiniBatchKMeans.fit(max_iter=1))."""
     from gdd import synth
     from gdd.kmeans import _Ops
+    from gdd.pipeline import graphsaint_split, pretrained_clustering_induct_hot_path
+    from gdd.sharded import role_owners
     cfg = synth.CONFIGS["reddit"]
+    n_tr, n_va, n_te = REDDIT_ROLES
+    N = n_tr + n_va + n_te
     t0 = time.perf_counter()
-    g = synth.chung_lu_device(cfg.n, cfg.avg_degree, cfg.seed, device=dev)
+    g_full = synth.chung_lu_device(N, REDDIT_FULL_DEGREE, cfg.seed, device=dev)
     gen = torch.Generator(device=dev)
     gen.manual_seed(cfg.seed)
-    X = torch.randn(cfg.n, cfg.d, device=dev, generator=gen)
+    perm = torch.randperm(N, device=dev, generator=gen)
+    idx = {"train": torch.sort(perm[:n_tr]).values, "val": torch.sort(perm[n_tr:n_tr + n_va]).values,
+           "test": torch.sort(perm[n_tr + n_va:]).values}
+    feat = torch.randn(N, cfg.d, device=dev, generator=gen) * 3.0 + 1.0  # raw: the scaler centres it
     W = torch.randn(cfg.d, cfg.n_classes, device=dev, generator=gen) / float(np.sqrt(cfg.d))
     torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
-    for _ in range(2):
-        ph = {}
-        torch.cuda.synchronize()
+    last = {}
+
+    def one_pass(ph=None):
         tp = time.perf_counter()
-        gn = gdd.normalize_adj(g)
-        tp = _sync_mark(ph, "normalize", tp)
-        target, _ = gdd.propagate(gn, X, cfg.T, cfg.alpha)
-        tp = _sync_mark(ph, "propagate", tp)
-        logits = target @ W
-        tp = _sync_mark(ph, "logits", tp)
-        km = gdd.MiniBatchKMeans(n_clusters=cfg.k, random_state=cfg.seed, batch_size=cfg.batch,
-                                 device=dev).fit(logits)
-        tp = _sync_mark(ph, "minibatch_kmeans", tp)
-        gdd.cluster_mean(target, km.labels_device_, cfg.k)
-        gdd.argmax_rows(km.cluster_centers_device_)
-        _sync_mark(ph, "cluster_mean", tp)
-    total_ms = sum(ph.values())
+        data = graphsaint_split(g_full, feat, idx["train"], idx["val"], idx["test"], device=dev)
+        if ph is not None:
+            _sync_mark(ph, "graphsaint_split", tp)
+        out = pretrained_clustering_induct_hot_path(
+            data, cfg.T, cfg.alpha, lambda t_tr, t_va: t_tr @ W, cfg.k, dataset="reddit",
+            seed=cfg.seed, cluster_minibatch=cfg.batch, device=dev, group=group, phases=ph)
+        last.update(data=data, out=out)
+    ms = _timed_ms(one_pass, reps, world, dev)
+    ph = {}
+    one_pass(ph)
+    data, out = last["data"], last["out"]
+    gn_tr, t_tr = out[4], out[3]
+    nnz = {r: int(getattr(data, "adj_" + r).nnz) for r in ("train", "val", "test")}
+    rec = {"workload": (f"Reddit inductive hot path (config 3): graphsaint_split of a {N}-node graph "
+                        f"(roles {n_tr}/{n_va}/{n_te}, role-graph entries {nnz}), d={cfg.d}, 3 x "
+                        f"{cfg.T - 1} hops (alpha {cfg.alpha}), logits C={cfg.n_classes}, "
+                        f"MiniBatchKMeans(k={cfg.k}, b={cfg.batch}, random_state={cfg.seed}), cluster means"),
+           "data": "synthetic: Chung-Lu power-law graph sampled on the device, random role split of "
+                   "GraphSAINT's Reddit sizes, N(1, 9) raw features, random linear logits",
+           "parallelism": ("single GPU" if world == 1 else
+                           f"{world} ranks: each role graph propagated by its owners "
+                           f"{role_owners(world)} (train row-partitioned over its owners when "
+                           "propagation_shards_pay), targets broadcast over RCCL; MiniBatchKMeans "
+                           "steps replicated, labels pass by rows, cluster means by clusters"),
+           "graph_generation_s": gen_s, "ms_total": ms, "nodes_per_s": N / (ms * 1e-3),
+           "phases_ms" if world == 1 else "phases_ms_rank0": ph,
+           "minibatch_steps": None, "cpu_baseline": None}
+    if world > 1:
+        del last, data, out
+        return rec
+    n_steps = None
+    logits = t_tr @ W
+    from gdd import MiniBatchKMeans
+    km = MiniBatchKMeans(n_clusters=cfg.k, random_state=cfg.seed, batch_size=cfg.batch, device=dev).fit(logits)
     n_steps = int(km.n_steps_)
-    hop = _hop_roofline(gn, X, cfg.alpha)
+    rec["minibatch_steps"] = n_steps
+    rec["hop_roofline"] = _hop_roofline(gn_tr, data.feat_train, cfg.alpha)
     # the fit's first and last stages as separate calls: k-means++ on a 3,000-point subset (k = 769,
     # T = 8) and the full labels pass against the fitted centres
-    ops = _Ops(dev, cfg.n, cfg.k, cfg.n_classes)
-    Xi = logits[torch.randperm(cfg.n, device=dev, generator=gen)[:3 * cfg.batch]].contiguous()
+    ops = _Ops(dev, n_tr, cfg.k, cfg.n_classes)
+    Xi = logits[torch.randperm(n_tr, device=dev, generator=gen)[:3 * cfg.batch]].contiguous()
     ops_i = _Ops(dev, Xi.shape[0], cfg.k, cfg.n_classes)
     ops_i.kmeans_plusplus(Xi, cfg.k, np.random.RandomState(0))
     torch.cuda.synchronize()
@@ -749,7 +852,7 @@ def reddit_record(dev, with_cpu):
     ops_i.kmeans_plusplus(Xi, cfg.k, np.random.RandomState(1))
     torch.cuda.synchronize()
     kpp_ms = (time.perf_counter() - t0) * 1e3
-    lab = torch.empty(cfg.n, dtype=torch.int32, device=dev)
+    lab = torch.empty(n_tr, dtype=torch.int32, device=dev)
     C = km.cluster_centers_device_.contiguous()
     ops.assign(logits, C, labels=lab)
     torch.cuda.synchronize()
@@ -757,41 +860,35 @@ def reddit_record(dev, with_cpu):
     ops.assign(logits, C, labels=lab)
     torch.cuda.synchronize()
     labels_ms = (time.perf_counter() - t0) * 1e3
-    steps_ms = ph["minibatch_kmeans"] - kpp_ms - labels_ms
-    rec = {"workload": f"Reddit train graph (config 3): N={cfg.n}, nnz_norm={gn.nnz}, d={cfg.d}, "
-                       f"{cfg.T - 1} hops (alpha {cfg.alpha}), logits C={cfg.n_classes}, "
-                       f"MiniBatchKMeans(k={cfg.k}, b={cfg.batch}, random_state={cfg.seed}), "
-                       "cluster means",
-           "data": "synthetic: Chung-Lu power-law graph sampled on the device, N(0,1) features, random "
-                   "linear logits",
-           "graph_generation_s": gen_s, "ms_total": total_ms, "phases_ms": ph,
-           "nodes_per_s": cfg.n / (total_ms * 1e-3), "minibatch_steps": n_steps,
-           "minibatch_split_ms": {"kmeans_plusplus_init_subset": kpp_ms, "labels_pass": labels_ms,
-                                  "steps_and_reassignment": steps_ms,
-                                  "per_step_us": 1e3 * steps_ms / max(n_steps, 1)},
-           "hop_roofline": hop, "cpu_baseline": None}
+    steps_ms = ph["kmeans"] - kpp_ms - labels_ms
+    rec["minibatch_split_ms"] = {"kmeans_plusplus_init_subset": kpp_ms, "labels_pass": labels_ms,
+                                 "steps_and_reassignment": steps_ms,
+                                 "per_step_us": 1e3 * steps_ms / max(n_steps, 1)}
     if with_cpu:
         threads, affinity, omp = _threads()
-        hop_s = _cpu_hop_seconds(gn, X, cfg.alpha, threads)
+        hop_s = {"train": _cpu_hop_seconds(gn_tr, data.feat_train, cfg.alpha, threads)}
+        from gdd.graph import normalize_adj
+        for r in ("val", "test"):
+            hop_s[r] = _cpu_hop_seconds(normalize_adj(getattr(data, "adj_" + r)),
+                                        getattr(data, "feat_" + r), cfg.alpha, threads)
         from sklearn.cluster import MiniBatchKMeans as SkMB
         L = logits.cpu().numpy()
         with _CpuThreads(threads):
             t0 = time.perf_counter()
             skm = SkMB(n_clusters=cfg.k, batch_size=cfg.batch, random_state=cfg.seed, max_iter=1).fit(L)
             mb_s = time.perf_counter() - t0
+        model_s = (cfg.T - 1) * sum(hop_s.values()) + mb_s * n_steps / max(int(skm.n_steps_), 1)
         rec["cpu_baseline"] = {
             "kind": "reference-library", "cores": threads, "affinity_cpus": affinity,
             "omp_num_threads": omp or None, "cpu_model": _cpu_model(),
             "hop_s": hop_s, "minibatch_fit_max_iter1_s": mb_s, "minibatch_fit_steps": int(skm.n_steps_),
-            "modelled_step_s": (cfg.T - 1) * hop_s + mb_s * n_steps / max(int(skm.n_steps_), 1),
-            "value": cfg.n / ((cfg.T - 1) * hop_s + mb_s * n_steps / max(int(skm.n_steps_), 1)),
-            "unit": "nodes/s (modelled)",
-            "sample": (f"per unit on {threads} threads: one torch CPU sparse hop ({cfg.n} x {cfg.d}); "
+            "modelled_step_s": model_s, "value": N / model_s, "unit": "nodes/s (modelled)",
+            "sample": (f"per unit on {threads} threads: one torch CPU sparse hop per role graph; "
                        f"scikit-learn MiniBatchKMeans(k={cfg.k}, b={cfg.batch}).fit(max_iter=1) "
                        f"({int(skm.n_steps_)} steps incl. its k-means++ init) on the same logits; "
-                       f"modelled_step_s = {cfg.T - 1} hops + the fit scaled to the GPU's "
-                       f"{n_steps} steps")}
-    del g, gn, X, target, logits, km, ops, ops_i
+                       f"modelled_step_s = {cfg.T - 1} hops of each role graph + the fit scaled to "
+                       f"the GPU's {n_steps} steps (graphsaint_split and normalisation excluded)")}
+    del g_full, feat, last, data, out, logits, km, ops, ops_i
     torch.cuda.empty_cache()
     return rec
 

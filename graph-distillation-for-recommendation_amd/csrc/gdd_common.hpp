@@ -142,6 +142,14 @@ int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const 
 // resumed after host steps, whose convergence tests the host already ran)
 constexpr int kStepNoTail = 1 << 16;
 
+// Bound of the LDS arrival-counter spins (k_mb_reassign, k-means++ speculative prefixes and draws):
+// a give-up takes the barrier redo. `make SPIN0=1` builds a twin with 0 so that every wait gives up
+// and the redo paths run (tests/test_gpu_spin0.py pins them bit-for-bit against the oracle).
+#ifndef GDD_SPIN_LIMIT
+#define GDD_SPIN_LIMIT (1 << 16)
+#endif
+constexpr int kSpinLimit = GDD_SPIN_LIMIT;
+
 // internal entry point of the k-means assignment (gdd_kmeans.hip), used by the Lloyd loop
 // (gdd_lloyd.hip): ||C||² into cn2, then labels of all n rows; every kernel skips once `stop`
 // says step `step_i` lies past the stopping decision (see stopped()).

@@ -1349,9 +1349,6 @@ __global__ __launch_bounds__(64 * W) void k_mb_assign(
   // the stop word goes out with trip 1's loads and is tested before the first global store (r05:
   // tested first it cost each launch one more dependent round trip); a block that runs on after
   // the loop stopped only writes buffers no later step reads, as a block that started first would
-#ifdef GDD_STOP_AT_ENTRY
-  if (stopped(stop, step_i)) return;  // the r04 order: the stop word alone first (A/B build)
-#endif
   const int32_t sv = stop ? __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   const bool stp = sv != 0 && sv - 1 < step_i;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1462,9 +1459,6 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
                                                         float* __restrict__ sq_out,
                                                         unsigned long long* __restrict__ keys_reset) {
   // the stop word goes out with the label loads and is tested before the first global store (r05)
-#ifdef GDD_STOP_AT_ENTRY
-  if (stopped(stop, step_i)) return;  // the r04 order: the stop word alone first (A/B build)
-#endif
   const int32_t sv = stop ? __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 20);
   extern __shared__ __attribute__((aligned(16))) float mb_lds[];
@@ -2731,7 +2725,7 @@ __device__ __forceinline__ void waves_arrive_rs(int* ctr) {
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ bool waves_wait_rs(int* ctr, int target) {
-  for (int it = 0; it < (1 << 16); ++it) {
+  for (int it = 0; it < kSpinLimit; ++it) {
     if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
     __builtin_amdgcn_s_sleep(1);
   }
@@ -2904,15 +2898,23 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
         const int q = shuffle_trace_wave4(J, (int)bs, r);
         if (lane == 0) s_pos[r] = q;
       }
+      // a wave whose wait gave up copies nothing (s_pos / s_src entries of other waves may not be
+      // written yet, and they are addresses): it raises s_bad before it arrives at the next counter,
+      // so a wave whose second wait succeeds sees every earlier give-up and skips its copies too
       waves_arrive_rs(&s_sync[0]);
       bool ok = waves_wait_rs(&s_sync[0], nc);
-      rows_in(tc, stride);
+      if (ok)
+        rows_in(tc, stride);
+      else if (lane == 0)
+        __hip_atomic_store(&s_bad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       waves_arrive_rs(&s_sync[1]);
       ok = waves_wait_rs(&s_sync[1], nc) && ok;
-      rows_out(tc, stride);
+      if (ok && __hip_atomic_load(&s_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+        rows_out(tc, stride);
+      else if (lane == 0)
+        __hip_atomic_store(&s_bad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       for (int c = tc; c < k; c += stride)
         if (counts[c] < thr) counts[c] = cmin;
-      if (!ok) s_bad = 1;
       GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 59);
     }
     __syncthreads();

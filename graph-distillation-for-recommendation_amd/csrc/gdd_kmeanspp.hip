@@ -1994,7 +1994,7 @@ __device__ __forceinline__ void waves_arrive(int* ctr) {
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ bool waves_wait(int* ctr, int target) {
-  for (int it = 0; it < (1 << 16); ++it) {
+  for (int it = 0; it < kSpinLimit; ++it) {
     if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
     __builtin_amdgcn_s_sleep(1);
   }
@@ -2004,7 +2004,7 @@ __device__ __forceinline__ bool waves_wait(int* ctr, int target) {
 __device__ __forceinline__ bool prefix_waves_sync(int* ctr, int target) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  for (int it = 0; it < (1 << 16); ++it) {
+  for (int it = 0; it < kSpinLimit; ++it) {
     if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
     __builtin_amdgcn_s_sleep(1);
   }

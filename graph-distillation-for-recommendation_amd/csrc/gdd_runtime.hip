@@ -199,6 +199,8 @@ const char* gdd_last_error(void) { return gdd::g_last_error.c_str(); }
 
 int gdd_abi_version(void) { return 1; }
 
+int gdd_spin_limit(void) { return gdd::kSpinLimit; }
+
 int gdd_device_ok(void) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;

@@ -29,6 +29,7 @@ _vp = ctypes.c_void_p
 SIGNATURES = {
     "gdd_last_error": (ctypes.c_char_p, []),
     "gdd_abi_version": (_c_int, []),
+    "gdd_spin_limit": (_c_int, []),
     "gdd_device_ok": (_c_int, []),
     "gdd_normalize_ws_bytes": (_c_size, [_c_i64, _c_i64]),
     "gdd_normalize_csr": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp,

@@ -37,7 +37,7 @@ import torch
 import torch.nn.functional as F
 
 from . import recsys as R
-from .pipeline import kmeans_cluster, teacher_means
+from .pipeline import kmeans_cluster_pair, teacher_means
 
 
 @dataclass
@@ -126,9 +126,10 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
-def run(args, out_root: str = "ClustGDD", embeddings=None, timings: Optional[dict] = None):
+def run(args, out_root: str = "ClustGDD", embeddings=None, timings: Optional[dict] = None, group=None):
     """The reference's main() body (:548-764). ``embeddings``: optional fixed (user, item) SVD
-    embeddings; ``timings``: filled with per-stage wall seconds. Returns the trained model."""
+    embeddings; ``timings``: filled with per-stage wall seconds; ``group``: a process group over the
+    node's GPUs for the clustering pair (rank 0 users, rank 1 items). Returns the trained model."""
     tm = timings if timings is not None else {}
     torch.manual_seed(args.seed)
     np.random.seed(args.seed)
@@ -153,11 +154,13 @@ def run(args, out_root: str = "ClustGDD", embeddings=None, timings: Optional[dic
     print(f"[cluster] target super nodes: users={num_cu}, items={num_ci}")
     t0 = time.perf_counter()
     print("[cluster] kmeans users...")
-    u2cu, _ = kmeans_cluster(user_emb_np, n_clusters=num_cu, seed=args.seed, minibatch=args.kmeans_minibatch,
-                             batch_size=args.kmeans_batch_size, device=device)
     print("[cluster] kmeans items...")
-    i2ci, _ = kmeans_cluster(item_emb_np, n_clusters=num_ci, seed=args.seed, minibatch=args.kmeans_minibatch,
-                             batch_size=args.kmeans_batch_size, device=device)
+    # the two fits are independent (each random_state=seed): with a group, users on rank 0 and items
+    # on rank 1, the results broadcast (gdd.pipeline.kmeans_cluster_pair; north star config 4)
+    (u2cu, _), (i2ci, _) = kmeans_cluster_pair(user_emb_np, item_emb_np, num_cu, num_ci, seed=args.seed,
+                                              minibatch=args.kmeans_minibatch,
+                                              batch_size=args.kmeans_batch_size, device=device,
+                                              group=group)
     u2cu, i2ci = np.asarray(u2cu, np.int64), np.asarray(i2ci, np.int64)
     torch.cuda.synchronize()
     tm["kmeans_s"] = time.perf_counter() - t0

@@ -222,6 +222,9 @@ def propagate(adj_norm: CSRGraph, features: torch.Tensor, T: int, alpha: float, 
         from .sharded import propagation_shards_pay, sharded_propagate, world_of
         world = world_of(group)[1]
         if world > 1 and propagation_shards_pay(adj_norm.n, adj_norm.nnz, d, world):
+            if relabel is not None:  # never drop a caller's relabel silently
+                raise ValueError("relabel cannot be combined with the row-partitioned propagation "
+                                 "this group selects (pass group=None, or relabel=None)")
             return sharded_propagate(adj_norm, X, T, alpha, group=group)
     if relabel is not None:
         rho = locality_order(adj_norm, relabel) if isinstance(relabel, str) else relabel

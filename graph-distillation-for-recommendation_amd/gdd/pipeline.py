@@ -146,6 +146,35 @@ def kmeans_cluster(X, n_clusters: int, seed: int, minibatch: bool = True, batch_
     return km.labels_.astype(np.int64), km.cluster_centers_.astype(np.float32)
 
 
+def kmeans_cluster_pair(user_emb, item_emb, n_user_clusters: int, n_item_clusters: int, seed: int,
+                        minibatch: bool = True, batch_size: int = 2048, device="cuda", n_init="auto",
+                        group=None, fit=None):
+    """Both kmeans_cluster calls of distill_recsys's main (distill_recsys.py:569-583): users, then
+    items -> ((u_labels int64, u_centres fp32), (i_labels, i_centres)), numpy.
+
+    ``group`` (north star config 4, a torch.distributed group over the GPUs of a node): the two fits
+    share nothing — each has its own ``random_state=seed`` — so the users' fit runs on rank 0 and the
+    items' on rank 1 (one rank runs both when R = 1), and each result is broadcast from its owner
+    (RCCL over xGMI). Every rank ends with the single-GPU results, bit for bit. ``fit`` (tests): a
+    stand-in with kmeans_cluster's signature."""
+    fit = fit or kmeans_cluster
+    kw = dict(seed=seed, minibatch=minibatch, batch_size=batch_size, n_init=n_init)
+    from .sharded import split_pair, world_of
+    if group is None or world_of(group)[1] == 1:
+        return (fit(user_emb, n_clusters=n_user_clusters, device=device, **kw),
+                fit(item_emb, n_clusters=n_item_clusters, device=device, **kw))
+    jobs = []
+    for E, k in ((user_emb, n_user_clusters), (item_emb, n_item_clusters)):
+        n, d = int(E.shape[0]), int(E.shape[1])
+        k_eff = max(1, min(k, n)) if k >= n else k  # kmeans_cluster's clamp
+        if k <= 0:
+            raise ValueError("n_clusters must be > 0")
+        spec = [((n,), torch.int64), ((k_eff, d), torch.float32)]
+        jobs.append((lambda E=E, k=k: fit(E, n_clusters=k, device=device, **kw), spec))
+    (ul, uc), (il, ic) = split_pair(jobs, group=group, device=device)
+    return ((ul.cpu().numpy(), uc.cpu().numpy()), (il.cpu().numpy(), ic.cpu().numpy()))
+
+
 def teacher_means(emb: torch.Tensor, assignment, num_clusters: int) -> torch.Tensor:
     """index_add_ / bincount.clamp_min(1) super-node means (empty cluster -> zero row)."""
     out, _ = cluster_mean(emb.to(torch.float32), assignment, num_clusters, empty_as_zero=True)
@@ -191,7 +220,7 @@ def pretrained_clustering_hot_path(features, adj, T: int, alpha: float, logits, 
 def pretrained_clustering_induct_hot_path(data, T: int, alpha: float, logits_train, nnodes_syn: int,
                                           dataset: str = "", seed: int = 15,
                                           cluster_minibatch: int = 1000, device="cuda",
-                                          n_init="auto", group=None):
+                                          n_init="auto", group=None, phases=None):
     """The hot path of the inductive ClustGDD.pretrained_clustering (clustgdd_agent_induct.py:37-155).
     ``n_init`` as in :func:`pretrained_clustering_hot_path` (induct:131-134 passes none).
 
@@ -203,23 +232,48 @@ def pretrained_clustering_induct_hot_path(data, T: int, alpha: float, logits_tra
     KMeans on the global numpy RNG otherwise (:129-134) — and the cluster means are taken over the
     train targets (:143-154). Returns (cluster_feat_centers, cluster_center_labels, cluster_labels
     int32, target_feat_train, adj_train_norm, target_feat_val, target_feat_test).
+
+    ``group``: the three role propagations run on different ranks (train on rank 0 — row-partitioned
+    over ranks 0, 3, 4, ... where that pays — val on rank 1, test on rank 2), their targets broadcast;
+    the k-means labels pass and the cluster means are partitioned as in the transductive path.
+    Bit-identical to one GPU. ``phases`` (optional dict): synchronised wall ms per stage on this rank.
     """
-    targets, norms = {}, {}
+    from .sharded import DeviceOps, propagate_roles
+    adjs, feats = {}, {}
+    dev = torch.device(device)
     for name in ("train", "val", "test"):
-        adj = getattr(data, "adj_" + name)
-        g = adj if isinstance(adj, CSRGraph) else to_csr(adj, device=device)
-        norms[name] = normalize_adj(g)                                              # :56-64
+        adjs[name] = getattr(data, "adj_" + name)
         X = getattr(data, "feat_" + name)
         X = X if isinstance(X, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(X, np.float32))
-        X = X.to(device=g.device, dtype=torch.float32).contiguous()
-        targets[name], _ = propagate(norms[name], X, T, alpha, group=group)         # :67-94
+        if isinstance(adjs[name], CSRGraph):
+            dev = adjs[name].device
+        feats[name] = X.to(device=dev, dtype=torch.float32).contiguous()
+    # :56-94 — each role graph normalised and propagated on its own; with a group the three loops
+    # run on different ranks (gdd.sharded.role_owners) and the targets are broadcast
+    norm_train, targets = propagate_roles(adjs, feats, T, alpha, group=group, ops=DeviceOps(dev),
+                                          phases=phases)
+    norms = {"train": norm_train}
+    import time
+    t_prev = [time.perf_counter()]
+
+    def mark(name):
+        if phases is not None:
+            torch.cuda.synchronize(dev)
+            now = time.perf_counter()
+            phases[name] = (now - t_prev[0]) * 1e3
+            t_prev[0] = now
+
+    mark("broadcast_targets_wait")
     out = logits_train(targets["train"], targets["val"]) if callable(logits_train) else logits_train
+    mark("logits")
     if dataset == "reddit":                                                         # :129-134
         km = MiniBatchKMeans(n_clusters=nnodes_syn, random_state=seed, batch_size=cluster_minibatch,
                              n_init=n_init, device=device, group=group).fit(out)
     else:
         km = _lloyd(nnodes_syn, group, n_init=n_init, device=device).fit(out)
+    mark("kmeans")
     feat_syn, _ = cluster_mean(targets["train"], km.labels_device_, nnodes_syn, group=group)     # :143-151
     labels_syn = argmax_rows(km.cluster_centers_device_)                            # :152
+    mark("cluster_mean")
     return (feat_syn, labels_syn, km.labels_device_.to(torch.int32), targets["train"], norms["train"],
             targets["val"], targets["test"])

@@ -113,6 +113,157 @@ def all_gather_slots(buf: torch.Tensor, m: int, group=None) -> None:
     buf.copy_(torch.cat(parts, 0).to(buf.device))
 
 
+def global_rank(group, r: int) -> int:
+    """The default-group rank of `group`'s rank r (collectives name their source by global rank)."""
+    if group is None or group is dist.group.WORLD:
+        return r
+    return dist.get_global_rank(group, r)
+
+
+_SUBGROUPS = {}
+
+
+def subgroup(ranks, group=None):
+    """A process group over `ranks` (ranks of `group`), created once per (group, ranks). Every rank
+    of `group` must call this with the same arguments, members or not (dist.new_group's rule)."""
+    key = (None if group is None or group is dist.group.WORLD else id(group), tuple(ranks))
+    if key not in _SUBGROUPS:
+        _SUBGROUPS[key] = dist.new_group([global_rank(group, r) for r in ranks])
+    return _SUBGROUPS[key]
+
+
+def broadcast_from(tensors, owner: int, group=None) -> None:
+    """In place: every rank's `tensors` (contiguous, same shapes on every rank) end with the values
+    that `group`'s rank `owner` holds. RCCL for device tensors (stream-ordered, no host sync); gloo
+    stages through the host."""
+    rank, world = world_of(group)
+    if world == 1:
+        return
+    src = global_rank(group, owner)
+    nccl = dist.get_backend(group) == "nccl"
+    for t in tensors:
+        if t.is_cuda and nccl:
+            dist.broadcast(t, src=src, group=group)
+            continue
+        h = t.cpu() if t.is_cuda else t
+        dist.broadcast(h, src=src, group=group)
+        if h is not t:
+            t.copy_(h)
+
+
+def comm_device(group, device):
+    """Where a tensor that crosses `group` lives: the GPU under RCCL, the host under gloo."""
+    if world_of(group)[1] > 1 and dist.get_backend(group) != "nccl":
+        return torch.device("cpu")
+    return torch.device(device)
+
+
+# ------------------------------------------------------------------------------------------------
+# independent work over the ranks: the recsys pair (config 4) and the role graphs (config 3)
+# ------------------------------------------------------------------------------------------------
+def pair_owners(world: int):
+    """Owners of distill_recsys's two kmeans_cluster calls (users, items): ranks 0 and 1 (one rank
+    runs both). The fits share nothing (each its own random_state, distill_recsys.py:569-583)."""
+    return (0, 1 % world)
+
+
+def split_pair(jobs, group=None, device="cuda"):
+    """Run independent jobs on their owner ranks and broadcast the results: ``jobs`` is a list of
+    (fn, spec) where fn() returns arrays/tensors matching spec = [(shape, torch dtype), ...]; job j
+    runs on rank ``pair_owners(R)[j]`` only. Returns, on every rank, one tuple of tensors per job
+    (on the communication device: the GPU under RCCL, the host under gloo) — bit-identical to
+    running every job on one rank, since each job is the single-rank computation itself."""
+    rank, world = world_of(group)
+    owners = pair_owners(world) if len(jobs) == 2 else tuple(j % world for j in range(len(jobs)))
+    cdev = comm_device(group, device)
+    outs = []
+    for j, (fn, spec) in enumerate(jobs):
+        if rank == owners[j]:
+            res = fn()
+            ts = tuple(torch.as_tensor(np.ascontiguousarray(r) if not isinstance(r, torch.Tensor) else r)
+                       .to(device=cdev, dtype=dt).reshape(shape).contiguous()
+                       for r, (shape, dt) in zip(res, spec))
+        else:
+            ts = tuple(torch.empty(shape, dtype=dt, device=cdev) for shape, dt in spec)
+        outs.append(ts)
+    for j, ts in enumerate(outs):  # the same broadcast order on every rank
+        broadcast_from(list(ts), owners[j], group)
+    return outs
+
+
+ROLES = ("train", "val", "test")
+
+
+def role_owners(world: int):
+    """The ranks that propagate each GraphSAINT role graph (config 3, clustgdd_agent_induct.py:72-94:
+    three independent loops): train on rank 0 and on every rank past the third, val on rank 1, test on
+    rank 2; with two ranks val and test both go to rank 1 (train is ~80% of the hops' bytes at the
+    Reddit split: 66% of the nodes and ~44% of the entries of the full graph)."""
+    if world == 1:
+        return {"train": [0], "val": [0], "test": [0]}
+    if world == 2:
+        return {"train": [0], "val": [1], "test": [1]}
+    return {"train": [0] + list(range(3, world)), "val": [1], "test": [2]}
+
+
+def propagate_roles(adjs, feats, T: int, alpha: float, group=None, ops=None, phases=None):
+    """The three propagations of the inductive agent over the ranks: each role graph is normalised
+    and propagated by its owners (:func:`role_owners`); train is row-partitioned over its owners
+    (:func:`sharded_propagate` on a sub-group) where :func:`propagation_shards_pay` says so; then one
+    broadcast per role's target. Every target is the single-GPU loop's, bit for bit. ``adjs`` and
+    ``feats`` map role -> graph / N_role x d features (val/test read only on their owners).
+    Returns (normalised train graph — computed on every rank, the agent keeps it — and a dict role ->
+    target on every rank). ``phases`` (optional dict): synchronised wall ms per stage of this rank."""
+    import time
+    ops = ops or DeviceOps(feats["train"].device)
+    rank, world = world_of(group)
+    owners = role_owners(world)
+    sync = getattr(ops, "synchronize", lambda: None)
+    t_prev = [time.perf_counter()]
+
+    def mark(name):
+        if phases is not None:
+            sync()
+            now = time.perf_counter()
+            phases[name] = phases.get(name, 0.0) + (now - t_prev[0]) * 1e3
+            t_prev[0] = now
+
+    if phases is not None:
+        sync()
+        t_prev[0] = time.perf_counter()
+    norm_train = ops.normalize(adjs["train"])          # induct:56-64, every rank
+    mark("normalize_train")
+    targets = {}
+    tr = owners["train"]
+    X = feats["train"]
+    if len(tr) > 1 and propagation_shards_pay(norm_train.n, norm_train.nnz, X.shape[1], len(tr)):
+        sub = subgroup(tr, group)  # every rank creates it; only the members use it
+        if rank in tr:
+            targets["train"] = sharded_propagate(norm_train, X, T, alpha, group=sub, ops=ops)[0]
+    elif rank == tr[0]:
+        targets["train"] = ops.propagate(norm_train, X, T, alpha)[0]
+    mark("propagate_train")
+    for role in ("val", "test"):
+        if rank == owners[role][0]:
+            gn = ops.normalize(adjs[role])
+            mark("normalize_" + role)
+            targets[role] = ops.propagate(gn, feats[role], T, alpha)[0]
+            mark("propagate_" + role)
+    if world > 1:
+        cdev = comm_device(group, ops.device)
+        for role in ROLES:  # the same order on every rank
+            n_r, d_r = int(feats[role].shape[0]), int(feats[role].shape[1])
+            t = targets.get(role)
+            if t is None:
+                t = torch.empty((n_r, d_r), dtype=torch.float32, device=cdev)
+            elif t.device != cdev:
+                t = t.to(cdev)
+            broadcast_from([t], owners[role][0], group)
+            targets[role] = t.to(ops.device)
+        mark("broadcast_targets")
+    return norm_train, targets
+
+
 # ------------------------------------------------------------------------------------------------
 # the device primitives (libgdd)
 # ------------------------------------------------------------------------------------------------
@@ -121,6 +272,8 @@ class DeviceOps:
 
     def __init__(self, device):
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.lib = _lib.device_lib()
 
     @property
@@ -131,6 +284,19 @@ class DeviceOps:
         if isinstance(a, torch.Tensor):
             return a.to(device=self.device, dtype=dtype or a.dtype).contiguous()
         return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=self.device)
+
+    def synchronize(self):
+        torch.cuda.synchronize(self.device)
+
+    def normalize(self, adj):
+        from .graph import CSRGraph, normalize_adj, to_csr
+        g = adj if isinstance(adj, CSRGraph) else to_csr(adj, device=self.device)
+        return normalize_adj(g)
+
+    def propagate(self, adj_norm, X, T, alpha):
+        from .graph import propagate
+        X = X if isinstance(X, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(X, np.float32))
+        return propagate(adj_norm, X.to(device=self.device, dtype=torch.float32).contiguous(), T, alpha)
 
     def center(self, X):
         n, dim = X.shape

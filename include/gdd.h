@@ -38,6 +38,9 @@ typedef struct ihipStream_t* gdd_stream_t; /* == hipStream_t */
 /* ---------------------------------------------------------------------------------------------- */
 const char* gdd_last_error(void);
 int gdd_abi_version(void); /* bumps on any signature change */
+/* The bound of the library's LDS arrival-counter spins (1 << 16; 0 in the `make SPIN0=1` twin
+   whose every bounded wait gives up, so that the redo paths run — tests/test_gpu_spin0.py). */
+int gdd_spin_limit(void);
 /* 1 if the current HIP device is gfx950 and the embedded code objects can run on it. */
 int gdd_device_ok(void);
 /* Streaming device copy (16-byte aligned, bytes % 16 == 0): the bench's measured HBM copy peak     */

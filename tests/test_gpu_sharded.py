@@ -102,6 +102,11 @@ def _pipelines(group, A, feat, logits, ind, logits_tr, E):
         out.update({f"{ds}_fs": fs.cpu().numpy(), f"{ds}_ls": ls.cpu().numpy(), f"{ds}_cl": cl.cpu().numpy()})
     lab, cen = kmeans_cluster(E, n_clusters=150, seed=42, minibatch=False, device="cuda:0", group=group)
     out.update(rs_labels=lab, rs_centers=cen)
+    # config 4's pair split: users on rank 0, items on rank 1, broadcast (one rank: both in turn)
+    from gdd.pipeline import kmeans_cluster_pair
+    (ul, uc), (il, ic) = kmeans_cluster_pair(E, E[:1700] * 0.5 + 0.25, 150, 90, seed=42, minibatch=False,
+                                             device="cuda:0", group=group)
+    out.update(pair_ul=ul, pair_uc=uc, pair_il=il, pair_ic=ic)
     return out
 
 
@@ -132,18 +137,21 @@ def _pipeline_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_two_ranks_pipelines_match_one():
-    """pretrained_clustering_hot_path, pretrained_clustering_induct_hot_path and kmeans_cluster with a
-    two-rank group (MiniBatchKMeans: partitioned labels pass; Lloyd: ShardedKMeans; cluster means by
-    cluster slices) give one rank's outputs bit for bit; and MiniBatchKMeans(group=None) inside an
-    initialised process group stays a single-rank fit on each rank's own data."""
+@pytest.mark.parametrize("world", [2, 3])
+def test_two_ranks_pipelines_match_one(world):
+    """pretrained_clustering_hot_path, pretrained_clustering_induct_hot_path, kmeans_cluster and
+    kmeans_cluster_pair with a two- and a three-rank group (MiniBatchKMeans: partitioned labels pass;
+    Lloyd: ShardedKMeans; cluster means by cluster slices; the inductive role graphs propagated on
+    different ranks and broadcast; the recsys pair's fits on ranks 0 and 1) give one rank's outputs bit
+    for bit; and MiniBatchKMeans(group=None) inside an initialised process group stays a single-rank
+    fit on each rank's own data."""
     one = _pipelines(None, *_pipeline_inputs())
     own = [gdd.MiniBatchKMeans(n_clusters=25, random_state=15, batch_size=400).fit(
-        synth.blobs(5000 + 1000 * r, 12, 25, seed=100 + r)) for r in range(2)]
-    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"gdd_pipes_{os.getpid()}")
+        synth.blobs(5000 + 1000 * r, 12, 25, seed=100 + r)) for r in range(world)]
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"gdd_pipes_{os.getpid()}_{world}")
     os.makedirs(out, exist_ok=True)
-    mp.spawn(_pipeline_worker, args=(2, free_port(), out), nprocs=2, join=True)
-    for r in range(2):
+    mp.spawn(_pipeline_worker, args=(world, free_port(), out), nprocs=world, join=True)
+    for r in range(world):
         p = np.load(os.path.join(out, f"p{r}.npz"))
         for key, v in one.items():
             a, b = np.ascontiguousarray(p[key]), np.ascontiguousarray(v)

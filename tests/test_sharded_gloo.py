@@ -64,8 +64,48 @@ def _worker(rank, world, port, job, out_dir):
                      rowptr.shape[0] - 1)
         t, p = sharded.sharded_propagate(g, torch.from_numpy(X), T, alpha, ops=ops)
         res = dict(target=t.numpy(), p_last=p.numpy())
+    elif kind == "pair":
+        # distill_recsys's two kmeans_cluster calls split over the ranks (config 4): users on rank 0,
+        # items on rank 1, broadcast from the owners; the oracle's scaler + Lloyd stand in for the fit
+        Eu, Ei, ku, ki = args
+        calls = []
+
+        def fit(E, n_clusters, seed, minibatch, batch_size, n_init, device):
+            calls.append(E.shape[0])
+            Xs, _, _ = O.standard_scaler(E)
+            r = O.kmeans(Xs, n_clusters, random_state=seed, n_init=n_init)
+            return r["labels_"].astype(np.int64), r["cluster_centers_"].astype(np.float32)
+        from gdd.pipeline import kmeans_cluster_pair
+        (ul, uc), (il, ic) = kmeans_cluster_pair(Eu, Ei, ku, ki, seed=42, device="cpu",
+                                                 group=dist.group.WORLD, fit=fit)
+        res = dict(ul=ul, uc=uc, il=il, ic=ic)
+        np.save(os.path.join(out_dir, f"calls{rank}.npy"), np.asarray(calls, np.int64))
+    elif kind == "roles":
+        # the inductive agent's three role propagations over the ranks (config 3)
+        graphs, feats, T, alpha, shard = args
+        if shard is not None:
+            os.environ["GDD_SHARD_PROP"] = shard
+        ops.normalize = lambda g: _oracle_norm(O, g)
+        ops.propagate = lambda gn, X, T_, a: _oracle_prop(O, gn, X, T_, a)
+        adjs = dict(graphs)
+        fts = {r: torch.from_numpy(f) for r, f in feats.items()}
+        gn, tg = sharded.propagate_roles(adjs, fts, T, alpha, group=dist.group.WORLD, ops=ops)
+        res = {"norm_val": gn.values().numpy(), **{"t_" + r: tg[r].numpy() for r in tg}}
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     dist.destroy_process_group()
+
+
+def _oracle_norm(O, A):
+    import torch
+    from gdd.graph import CSRGraph
+    ro, co, vo = O.normalize_csr(A.indptr, A.indices, None, -1)
+    return CSRGraph(torch.from_numpy(ro), torch.from_numpy(co), torch.from_numpy(vo), ro.shape[0] - 1)
+
+
+def _oracle_prop(O, gn, X, T, alpha):
+    import torch
+    t, p = O.propagate(gn.rowptr.numpy(), gn.col.numpy(), gn.values().numpy(), X.numpy(), T, alpha)
+    return torch.from_numpy(t), torch.from_numpy(p)
 
 
 def _run(world, job, tmp):
@@ -197,3 +237,64 @@ def test_propagation_size_model():
     assert propagation_shards_pay(2449029, 130_000_000, 100, 2)
     assert not propagation_shards_pay(169343, 2_560_000, 128, 8)   # ogbn-arxiv: replicate
     assert not propagation_shards_pay(169343, 2_560_000, 128, 1)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_recsys_pair_split_matches_one_rank(tmp_path, world):
+    """kmeans_cluster_pair over a group (north star config 4): the users' fit runs on rank 0 only and
+    the items' on rank 1 only (pair_owners), the results broadcast; every rank ends with the one-rank
+    results bit for bit (oracle stand-in fits: StandardScaler + Lloyd, random_state 42)."""
+    _paths()
+    from gdd import synth
+    Eu, Ei = synth.svd_like(700, 16, seed=1), synth.svd_like(450, 16, seed=2)
+    one = _run(1, ("pair", (Eu, Ei, 70, 45)), tmp_path / "w1")
+    many = _run(world, ("pair", (Eu, Ei, 70, 45)), tmp_path / f"w{world}")
+    _same(one, many)
+    calls = [np.load(tmp_path / f"w{world}" / f"calls{r}.npy").tolist() for r in range(world)]
+    assert calls[0] == [700] and calls[1] == [450] and all(c == [] for c in calls[2:])
+    assert np.load(tmp_path / "w1" / "calls0.npy").tolist() == [700, 450]
+
+
+def _role_graphs(n=900, seed=4):
+    """A GraphSAINT-style split: the induced train/val/test sub-graphs of one Chung-Lu graph."""
+    import scipy.sparse as sp
+    from gdd import synth
+    A = sp.csr_matrix(synth.chung_lu(n, 20.0, seed))
+    rs = np.random.RandomState(seed)
+    perm = rs.permutation(n)
+    idx = {"train": np.sort(perm[:600]), "val": np.sort(perm[600:700]), "test": np.sort(perm[700:])}
+    X = synth.features(n, 12, seed)
+    graphs = {r: sp.csr_matrix(A[np.ix_(i, i)]) for r, i in idx.items()}
+    for g in graphs.values():
+        g.sort_indices()
+    feats = {r: np.ascontiguousarray(X[i]) for r, i in idx.items()}
+    return graphs, feats
+
+
+@pytest.mark.parametrize("world,shard", [(2, None), (3, None), (4, "1"), (4, "0")])
+def test_role_propagations_split_matches_one_rank(tmp_path, world, shard):
+    """propagate_roles (north star config 3): train on rank 0 (row-partitioned over ranks 0 and 3 at
+    world 4 when forced), val on rank 1, test on rank 2 (rank 1 at world 2), targets broadcast —
+    every rank holds the one-rank targets and normalised train graph bit for bit, equal to the
+    oracle's loops."""
+    _paths()
+    from oracle import oracle as O
+    graphs, feats = _role_graphs()
+    T, alpha = 5, 0.9
+    one = _run(1, ("roles", (graphs, feats, T, alpha, None)), tmp_path / "w1")
+    many = _run(world, ("roles", (graphs, feats, T, alpha, shard)), tmp_path / f"w{world}")
+    _same(one, many)
+    for r, g in graphs.items():
+        ro, co, vo = O.normalize_csr(g.indptr, g.indices, None, -1)
+        t_ref, _ = O.propagate(ro, co, vo, feats[r], T, alpha)
+        assert np.array_equal(many["t_" + r].view(np.uint32), t_ref.view(np.uint32)), r
+
+
+def test_role_and_pair_owners():
+    _paths()
+    from gdd.sharded import pair_owners, role_owners
+    assert pair_owners(1) == (0, 0) and pair_owners(2) == (0, 1) and pair_owners(8) == (0, 1)
+    assert role_owners(1) == {"train": [0], "val": [0], "test": [0]}
+    assert role_owners(2) == {"train": [0], "val": [1], "test": [1]}
+    assert role_owners(3) == {"train": [0], "val": [1], "test": [2]}
+    assert role_owners(8) == {"train": [0, 3, 4, 5, 6, 7], "val": [1], "test": [2]}
