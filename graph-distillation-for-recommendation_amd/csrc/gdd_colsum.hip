@@ -506,8 +506,8 @@ extern "C" size_t gdd_center_columns_ws_bytes(int64_t n, int dim) {
 extern "C" int gdd_center_columns_ws(int64_t n, int dim, const float* X, float* X_out, float* mean, float* var,
                                      void* ws, size_t ws_bytes, gdd_stream_t stream) {
   GDD_REQUIRE(n > 0 && dim > 0 && X && X_out && mean && var, "center_columns_ws: bad arguments");
-  const char* pe = getenv("GDD_CENTER_PAR");  // 0: the sequential chains (gdd_center_columns)
-  if (n < kCsMinRows || dim < 2 || dim > kCsMaxDim || (pe && pe[0] == '0'))
+  // GDD_FORCE=center_seq: the sequential chains (gdd_center_columns) at any shape
+  if (n < kCsMinRows || dim < 2 || dim > kCsMaxDim || forced("center_seq"))
     return gdd_center_columns(n, dim, X, X_out, mean, var, stream);
   GDD_REQUIRE(ws && ws_bytes >= gdd_center_columns_ws_bytes(n, dim), "center_columns_ws: workspace too small");
   hipStream_t s = to_hip(stream);

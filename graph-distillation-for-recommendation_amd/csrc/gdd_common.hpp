@@ -85,6 +85,25 @@ int sort_pairs_i32(const int32_t* keys_in, int32_t* keys_out, const int32_t* val
 // gap is already the device's own (MiniBatchKMeans fit 14.05 ms replayed vs 14.00 eager, k-means++
 // 4.13 vs 4.20 ms) — and a recording costs a fit's worth of time, so it stays opt-in.
 // ---------------------------------------------------------------------------------------------
+// GDD_FORCE (tests and diagnostics only): a comma-separated list of tokens, each forcing a path that
+// other shapes take by default (so its bits can be pinned on a small shape), e.g.
+// GDD_FORCE=kpp_no_table,lloyd_no_prune or GDD_FORCE=kpp_big1_max=32768. Read on every call (host).
+//   kpp_no_table      k-means++ without the n x n distance table (small and multi-block plans)
+//   kpp_force_table   the multi-block table although kpp_table_pays says no (small k)
+//   kpp_no_big1       the per-block table rounds instead of one workgroup per trial (n <= 16,384)
+//   kpp_big1_max=N    one workgroup per trial up to N points (default 16,384, at most 32,768)
+//   kpp_single_round  one table round per launch instead of the pair launches (T <= 8)
+//   kpp_two_launch    the single-block rounds' distance + pick launches instead of the fused round
+//   kpp_no_split      the per-(block, trial) rounds instead of the split rounds (>= 128 blocks)
+//   lloyd_no_prune    every Lloyd E-step over every row (no bounds)
+//   fold_no_pad       the Lloyd M-step gathers X itself instead of its zero-padded copy
+//   estep_no_pad      the bounded E-step's row lists read X instead of the padded copy
+//   fold_slice=F      M-step clusters above F x the mean size fold in slices (default 1.5; 0: off)
+//   group_split       the multi-launch label grouping where the one-launch form fits
+//   center_seq        KMeans' centring by the sequential column chains
+bool forced(const char* token);
+double forced_value(const char* token, double dflt);
+
 int replay_or_run(const char* site, const void* key, size_t key_bytes, hipStream_t s,
                   const std::function<int(hipStream_t)>& enqueue);
 
@@ -102,37 +121,10 @@ int mb_loop_begin(int64_t b, int k, void* ws, size_t ws_bytes, hipStream_t s);
 int mb_loop_end(int64_t b, int k, int last_step, int64_t n_samples, int max_no_improvement,
                 void* state, void* ws, size_t ws_bytes, hipStream_t s);
 int mb_rng_launch(const DevMT* in, DevMT* out, int64_t n, int64_t bs, int64_t* rows, hipStream_t s);
-// one-launch steps of the device loop (k_mb_fused): the update of step upd_step (do_update) and the
-// assignment of step assign_step (do_assign) in one launch, plus the tail of step tail_step (>= 0)
-struct MbFusedCall {
-  int64_t b;
-  int dim;
-  const float* X;
-  int k;
-  int64_t n_samples;
-  int max_no_improvement;
-  void* state;
-  void* step_ws;
-  size_t step_ws_bytes;
-  unsigned long long* keys3;  // three key buffers of b entries (step j uses j % 3), ~0 initially
-  int do_update, do_assign;
-  int upd_step, assign_step, tail_step;
-  int gate;  // the launch is skipped once the stop word places step `gate` past the stop
-  const int64_t* rows_prev;  // batch upd_step
-  const int64_t* rows_cur;   // batch assign_step
-  const float* C_old;        // centres before the update (or the lone assignment's centres)
-  float* C_new;
-  const float* W_old;
-  float* W_new;
-  int norms_valid;  // lone assignment: the workspace norms match C_old
-};
-bool mb_fused_ok(int64_t b, int dim, int k);
-int mb_fused_launch(const MbFusedCall& c, const RngNext& rn, hipStream_t s);
 // the device reassignment (k_mb_reassign): any k whose swap table fits the LDS; a step with more
 // than b/2 centres due (np.argsort's branch) is handed to the host through MBState.handoff
 constexpr size_t kReassignLdsCap = 150 * 1024;
 size_t mb_reassign_lds(int64_t bs, int k);
-void mb_reassign_form_refresh();  // re-reads GDD_MB_REASSIGN_FORM (once per fit)
 bool mb_reassign_ok(int64_t bs, int k);
 int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const float* X,
                        const int64_t* rows, float* C_new, float* counts, void* step_ws,

@@ -496,109 +496,6 @@ __device__ inline void mt_shuffle_draws_wave(MTScratch* s, int n, int* J) {
   if (lane == 0) s->pos = pos;
 }
 
-// The same draws by the whole block (r05): 2048 words per pass (wpt = 2048 / blockDim.x consecutive
-// words per thread, the key blocks a pass spans twisted ahead into the ring as in mt_randint_ring).
-// Word q of a pass is accepted iff i_q >= 1 and (w_q & mask32(i_q)) <= i_q, i_q = i - (#accepted
-// before q). Each thread walks its words in order from a guess A_t of its start count; a block scan of
-// the per-thread counts gives the next guesses, until no count changes (Jacobi). Thread 0's count is
-// exact after the first iteration and every iteration settles at least one more thread, so the loop
-// ends within blockDim.x + 1 iterations at the sequential answer (10-25 at n = 1000: only words
-// within a few of their threshold flip; one barrier each). On entry ring slot 0 holds the key block
-// and `pos` its position (624: exhausted); returns the stream index b of the key block holding the
-// last word consumed (ring slot b % kMtRing) and sets *pos_out to the position after that word.
-// Scratch: the 64 ints after the ring.
-__device__ inline int mt_shuffle_draws_block(uint32_t* ring, int pos, int n, int* J, int* pos_out,
-                                              int* iters = nullptr) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nwv = blockDim.x >> 6;
-  int* scr = reinterpret_cast<int*>(ring + kMtRing * 624);
-  const int wpt = 2048 / (int)blockDim.x;  // 2, 4 or 8
-  int i = n - 1;                          // the next i to draw for (block-uniform)
-  int base = 0, ready = 0;                // stream index of the pass's first block; blocks in the ring
-  int last_block = 0, last_pos = pos;
-  int par = 0;
-  while (i >= 1) {
-    const int hib = base + (pos + 2047) / 624;
-    while (ready < hib) {
-      mt_twist_into(ring + (ready % kMtRing) * 624, ring + ((ready + 1) % kMtRing) * 624);
-      ++ready;
-    }
-    const int r0 = pos + wpt * t;  // this thread's first word, relative to block `base`
-    uint32_t w[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      w[u] = 0;
-      if (u < wpt) {
-        const int r = r0 + u, b = base + r / 624;
-        w[u] = mt_temper(ring[(b % kMtRing) * 624 + (r - (r / 624) * 624)]);
-      }
-    }
-    int A = min(i, (3 * wpt * t) / 4);  // first guess: three words in four accepted
-    int prev = -1, tot = 0;
-    unsigned fl = 0;
-    while (true) {
-      int a = A;
-      fl = 0;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int q = i - a;
-        if (u < wpt && q >= 1 && (w[u] & mask32((uint32_t)q)) <= (uint32_t)q) {
-          fl |= 1u << u;
-          ++a;
-        }
-      }
-      const int cnt = a - A;
-      int inc = cnt;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(inc, o);
-        if (lane >= o) inc += y;
-      }
-      const bool ch = __ballot(cnt != prev) != 0ull;
-      if (lane == 63) scr[par * 16 + wave] = inc | (ch ? 0x10000 : 0);
-      __syncthreads();
-      int wb = 0;
-      bool any = false;
-      tot = 0;
-      for (int q = 0; q < nwv; ++q) {
-        const int v = scr[par * 16 + q];
-        const int c = v & 0xffff;
-        tot += c;
-        wb += q < wave ? c : 0;
-        any = any || (v >> 16) != 0;
-      }
-      par ^= 1;  // the other slot next: this one is rewritten only after the next barrier
-      prev = cnt;
-      if (iters) ++*iters;
-      if (!any) break;  // no count changed: the scan of these counts is A itself
-      A = wb + inc - cnt;
-    }
-    int a = A;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if ((fl >> u) & 1u) {
-        const int q = i - a;
-        J[q] = (int)(w[u] & mask32((uint32_t)q));
-        if (q == 1) scr[32] = r0 + u;  // the draw for i = 1: the last word consumed
-        ++a;
-      }
-    }
-    if (tot >= i) {
-      __syncthreads();
-      const int wl = scr[32];
-      last_block = base + wl / 624;
-      last_pos = wl - (wl / 624) * 624 + 1;
-      i = 0;
-    } else {
-      i -= tot;
-      const int nx = pos + 2048;
-      base += nx / 624;
-      pos = nx - (nx / 624) * 624;
-    }
-  }
-  *pos_out = last_pos;
-  return last_block;
-}
-
 // the key block and position by one wave (the others may be busy)
 __device__ inline void mt_store_wave(const MTScratch* s, DevMT* __restrict__ dst) {
   const int lane = threadIdx.x & 63;

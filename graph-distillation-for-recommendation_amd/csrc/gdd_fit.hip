@@ -67,7 +67,6 @@ struct FitWs {
   void* assign_ws;
   size_t assign_bytes;
   DevMT* mtb;  // 4 device MT states: slot s % 4 (s % 3 in the two-launch loop) = after step s's draws
-  unsigned long long* keys3;  // one-launch loop: the assignment keys of step j in buffer j % 3
   float* counts2;             // one-launch loop: weight sums after odd steps (counts: even)
 };
 
@@ -97,7 +96,6 @@ size_t fit_ws(void* base, size_t cap, int64_t n, int dim, int k, int64_t bs, int
   f.assign_bytes = gdd_kmeans_assign_ws_bytes(std::max(n, isz));
   f.assign_ws = cv.take<char>(f.assign_bytes);
   f.mtb = cv.take<DevMT>(4);
-  f.keys3 = cv.take<unsigned long long>(3 * (size_t)bs);
   f.counts2 = cv.take<float>(k);
   if (w) *w = f;
   return cv.off + 1024;
@@ -109,24 +107,16 @@ int local_trials(int k) { return 2 + (int)std::log((double)k); }
 // Per step s: the assignment launch (plus a workgroup finishing step s-1 — its batch inertia and
 // convergence test — and, unless s reassigns, a workgroup drawing batch s+1), the update launch,
 // and at scheduled reassignment steps the reassignment launch (which then draws batch s+1). Chunks of
-// dev_chunk() steps are enqueued back to back; the host reads the stop word of chunk c while chunk
-// c+1 runs. Smaller chunks leave fewer no-op launches after the stop (about half a chunk plus the
-// lookahead's chunks) but give the host a shorter runway (GDD_MB_CHUNK, 2..64, default 16).
-int dev_chunk() {
-  static const int v = [] {
-    const char* e = getenv("GDD_MB_CHUNK");
-    const int c = e ? atoi(e) : 16;
-    return c < 2 ? 2 : (c > 64 ? 64 : c);
-  }();
-  return v;
-}
+// kDevChunk steps are enqueued back to back; the host reads the stop word of chunk c while chunk
+// c+1 runs. Smaller chunks leave fewer no-op launches after the stop but give the host a shorter
+// runway: 8, 12 and 16 measured equal within the box's noise, 4 slower.
+constexpr int kDevChunk = 16;
 
 // Steps [i0, n_steps) on the device. rr_base: the last reassignment step (the next ones every
 // rr_period steps from it); norms_valid0: the workspace norms match step i0's centres. Returns the
 // convergence stop in *stop_step, or in *handoff_step a step whose reassignment needs the host (more
 // than b/2 centres due: np.argsort's branch) — that step's update has run, its tail and reassignment
 // have not, and the generator (written back to rng) is after its batch draws.
-constexpr int kNearStopDefault = 0;  // set from the same-box A/B (DESIGN.md §4 MiniBatch)
 
 int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t i0, int64_t rr_base,
                 bool norms_valid0, int64_t n_steps, int max_no_improvement, float reassignment_ratio,
@@ -146,17 +136,9 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t i
   rc = mb_loop_begin(bs, k, w.step_ws, w.step_bytes, s);
   if (rc) return rc;
   const bool reassign = reassignment_ratio > 0.f;
-  // chunks in flight before the host waits for the oldest one's stop word (GDD_MB_LOOKAHEAD, 1..3):
-  // more absorb host-side hiccups; each extra chunk can add one chunk of no-op launches after a stop
-  static const int lookahead = [] {
-    const char* e = getenv("GDD_MB_LOOKAHEAD");
-    const int v = e ? atoi(e) : 1;
-    return v < 1 ? 1 : (v > 3 ? 3 : v);
-  }();
-  static const int near_stop = [] {
-    const char* e = getenv("GDD_MB_NEAR_STOP");
-    return e ? atoi(e) : kNearStopDefault;
-  }();
+  // one chunk in flight before the host waits for the oldest one's stop word (two or three measured
+  // equal: each extra chunk only adds a chunk of no-op launches after a stop)
+  constexpr int lookahead = 1;
   hipEvent_t ev[4];
   for (int q = 0; q < 4; ++q) GDD_HIP(hipEventCreateWithFlags(&ev[q], hipEventDisableTiming));
   struct EvGuard {
@@ -231,7 +213,7 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t i
   *stop_step = -1;
   *handoff_step = -1;
   while (i < n_steps) {
-    const int64_t m = std::min<int64_t>(dev_chunk(), n_steps - i);
+    const int64_t m = std::min<int64_t>(kDevChunk, n_steps - i);
     key.i0 = i;
     key.m = m;
     rc = replay_or_run("minibatch_chunk", &key, sizeof(key), s,
@@ -249,21 +231,6 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t i
       GDD_HIP(hipEventSynchronize(ev[old]));
       const int32_t* ho = h_flag + 32 + 4 * old;
       if (ho[0]) break;  // the later kernels already enqueued are no-ops
-      // near the stop (the no-improvement count of the chunk just read is within near_stop of
-      // max_no_improvement): wait for the chunks in flight before enqueuing more, so a stop inside
-      // them leaves no chunk of no-op launches behind (GDD_MB_NEAR_STOP, 0 = off)
-      if (near_stop > 0 && max_no_improvement > 0 && ho[3] >= max_no_improvement - near_stop &&
-          i < n_steps) {
-        bool stopped_now = false;
-        for (int64_t q = chunk - lookahead + 1; q <= chunk; ++q) {
-          GDD_HIP(hipEventSynchronize(ev[q & 3]));
-          if (h_flag[32 + 4 * (q & 3)]) {
-            stopped_now = true;
-            break;
-          }
-        }
-        if (stopped_now) break;
-      }
     }
     ++chunk;
   }
@@ -279,143 +246,6 @@ int device_loop(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t i
   // the caller's RandomState ends where sklearn's does: after the draws of the last step (at a
   // handoff: after that step's batch draws, before its reassignment's)
   GDD_HIP(hipMemcpyAsync(h_mt, w.mtb + last % 3, sizeof(DevMT), hipMemcpyDeviceToHost, s));
-  GDD_HIP(hipStreamSynchronize(s));
-  std::memcpy(rng->key, h_mt->key, sizeof(h_mt->key));
-  rng->pos = h_mt->pos;
-  return GDD_OK;
-}
-
-// The same loop with one launch per step (k_mb_fused): launch L_s updates the centres of step s-1
-// and assigns batch s; its extra workgroups fold step s-2's inertia and convergence test (the
-// terms are written by the update, one launch later than in the two-launch loop) and draw batch
-// s+1. A step followed by a reassignment (and the last step) is split: its update alone, the
-// reassignment, then the next step's assignment alone. The stop decision for step j therefore
-// lands up to three launches after step j's assignment; the kernels in between touch only
-// buffers the result does not use (centres and weight sums of steps > j+1, keys, batches > j+1,
-// MT slots (j+1..j+3) % 4), so the result is the same as stopping at once.
-int device_loop_fused(int64_t n, int dim, const float* X, int k, int64_t bs, int64_t n_steps,
-                      int max_no_improvement, float reassignment_ratio, MTState* rng, const FitWs& w,
-                      int32_t* h_flag /* pinned, >= 5 ints */, int64_t* stop_step, hipStream_t s) {
-  static_assert(sizeof(DevMT) == 624 * 4 + 8, "DevMT layout");
-  DevMT* h_mt = reinterpret_cast<DevMT*>(h_flag + 64);
-  std::memcpy(h_mt->key, rng->key, sizeof(h_mt->key));
-  h_mt->pos = rng->pos;
-  h_mt->pad = 0;
-  auto rows_of = [&](int64_t j) { return w.rows_d + (j % 3) * bs; };
-  auto wsum_of = [&](int64_t j) { return (j & 1) ? w.counts2 : w.counts; };
-  GDD_HIP(hipMemcpyAsync(w.mtb + 3, h_mt, sizeof(DevMT), hipMemcpyHostToDevice, s));  // step -1
-  int rc = mb_rng_launch(w.mtb + 3, w.mtb + 0, n, bs, rows_of(0), s);
-  if (rc) return rc;
-  GDD_HIP(hipMemsetAsync(w.keys3, 0xff, sizeof(unsigned long long) * 3 * (size_t)bs, s));
-  const bool reassign = reassignment_ratio > 0.f;
-  static const int lookahead = [] {
-    const char* e = getenv("GDD_MB_LOOKAHEAD");
-    const int v = e ? atoi(e) : 1;
-    return v < 1 ? 1 : (v > 3 ? 3 : v);
-  }();
-  hipEvent_t ev[4];
-  for (int q = 0; q < 4; ++q) GDD_HIP(hipEventCreateWithFlags(&ev[q], hipEventDisableTiming));
-  struct EvGuard {
-    hipEvent_t* e;
-    ~EvGuard() {
-      for (int q = 0; q < 4; ++q) (void)hipEventDestroy(e[q]);
-    }
-  } guard{ev};
-  int32_t* stop_word = reinterpret_cast<int32_t*>(static_cast<char*>(w.state) + 16);
-  MbFusedCall base{};
-  base.b = bs;
-  base.dim = dim;
-  base.X = X;
-  base.k = k;
-  base.n_samples = n;
-  base.max_no_improvement = max_no_improvement;
-  base.state = w.state;
-  base.step_ws = w.step_ws;
-  base.step_ws_bytes = w.step_bytes;
-  base.keys3 = w.keys3;
-  const RngNext none{nullptr, nullptr, nullptr, 0, 0};
-  int64_t n_since = 0, i = 0, chunk = 0, pending_tail = -1;
-  bool prev_split = true;  // step 0 starts with an assignment alone
-  *stop_step = -1;
-  while (i < n_steps) {
-    const int64_t m = std::min<int64_t>(dev_chunk(), n_steps - i);
-    for (int64_t j = 0; j < m; ++j) {
-      const int64_t st = i + j;
-      n_since += bs;
-      const bool rr = st == 0 || n_since >= 10 * (int64_t)k;  // _random_reassign (:2029-2043)
-      if (rr) n_since = 0;
-      const bool do_rr = rr && reassign;
-      const bool has_next = st + 1 < n_steps;
-      const RngNext next{w.mtb + st % 4, w.mtb + (st + 1) % 4, rows_of(st + 1), n, bs};
-      MbFusedCall c = base;
-      c.do_assign = 1;
-      c.assign_step = (int)st;
-      c.rows_cur = rows_of(st);
-      c.tail_step = (int)pending_tail;
-      pending_tail = -1;
-      if (prev_split) {  // the assignment alone (step 0, or after a reassignment)
-        c.do_update = 0;
-        c.gate = st > 0 ? (int)st - 1 : 0;
-        c.C_old = w.C[st % 2];
-        c.norms_valid = st > 0;
-      } else {  // update st-1 + assignment st
-        c.do_update = 1;
-        c.upd_step = (int)st - 1;
-        c.gate = (int)st - 1;
-        c.rows_prev = rows_of(st - 1);
-        c.C_old = w.C[(st - 1) % 2];
-        c.C_new = w.C[st % 2];
-        c.W_old = wsum_of(st - 1);
-        c.W_new = wsum_of(st);
-        pending_tail = st - 1;
-      }
-      rc = mb_fused_launch(c, has_next ? next : none, s);
-      if (rc) return rc;
-      const bool split = do_rr || !has_next;
-      if (split) {  // update st alone, then the reassignment
-        MbFusedCall u = base;
-        u.do_update = 1;
-        u.do_assign = 0;
-        u.upd_step = (int)st;
-        u.gate = (int)st;
-        u.tail_step = (int)pending_tail;
-        u.rows_prev = rows_of(st);
-        u.C_old = w.C[st % 2];
-        u.C_new = w.C[(st + 1) % 2];
-        u.W_old = wsum_of(st);
-        u.W_new = wsum_of(st + 1);
-        pending_tail = st;
-        rc = mb_fused_launch(u, none, s);
-        if (rc) return rc;
-        if (do_rr) {
-          rc = mb_reassign_launch((int)st, bs, dim, k, reassignment_ratio, X, rows_of(st),
-                                  w.C[(st + 1) % 2], wsum_of(st + 1), w.step_ws, w.step_bytes,
-                                  w.mtb + st % 4, w.mtb + st % 4, has_next ? next : none, w.state, s);
-          if (rc) return rc;
-        }
-      }
-      prev_split = split;
-      if (!has_next) {  // the last step's inertia and convergence test
-        rc = mb_loop_end(bs, k, (int)st, n, max_no_improvement, w.state, w.step_ws, w.step_bytes, s);
-        if (rc) return rc;
-      }
-    }
-    i += m;
-    const int slot = (int)(chunk & 3);
-    GDD_HIP(hipMemcpyAsync(h_flag + slot, stop_word, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    GDD_HIP(hipEventRecord(ev[slot], s));
-    if (chunk >= lookahead) {
-      const int old = (int)((chunk - lookahead) & 3);
-      GDD_HIP(hipEventSynchronize(ev[old]));
-      if (h_flag[old]) break;  // the later kernels already enqueued are no-ops
-    }
-    ++chunk;
-  }
-  GDD_HIP(hipMemcpyAsync(h_flag + 4, stop_word, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  GDD_HIP(hipStreamSynchronize(s));
-  if (h_flag[4]) *stop_step = h_flag[4] - 1;
-  const int64_t last = *stop_step >= 0 ? *stop_step : n_steps - 1;
-  GDD_HIP(hipMemcpyAsync(h_mt, w.mtb + last % 4, sizeof(DevMT), hipMemcpyDeviceToHost, s));
   GDD_HIP(hipStreamSynchronize(s));
   std::memcpy(rng->key, h_mt->key, sizeof(h_mt->key));
   rng->pos = h_mt->pos;
@@ -601,19 +431,7 @@ extern "C" int gdd_minibatch_kmeans_fit(
   // fire — always when k <= b/2. When it fires (k > b/2 only), the device stops at that step and
   // hands it to the host (host_reassign); the host then runs steps while some weight sum is zero
   // (sklearn reassigns at every such step) and resumes the device loop once none is.
-  mb_reassign_form_refresh();
   const bool dev_ok = n_steps > 0 && getenv("GDD_HOST_LOOP") == nullptr && mb_reassign_ok(bs, k);
-  // GDD_MB_FUSED=1: one launch per step (k_mb_fused, measured slower at the arxiv shape: every
-  // point block redoes its centre group's update); k <= b/2 only; default: the
-  // two-launch loop
-  const char* fused_e = getenv("GDD_MB_FUSED");
-  const bool fused_env = fused_e && fused_e[0] == '1';
-  if (dev_ok && fused_env && 2 * (int64_t)k <= bs && mb_fused_ok(bs, dim, k)) {
-    int rc = device_loop_fused(n, dim, X, k, bs, n_steps, max_no_improvement, reassignment_ratio,
-                               static_cast<MTState*>(rng_state), w, h_flag, &stop_step, s);
-    if (rc) return rc;
-    i = n_steps;  // skip the loops below
-  }
   bool use_dev = dev_ok;
   int64_t rr_base = 0;
   while (i < n_steps && stop_step < 0) {

@@ -898,6 +898,157 @@ __global__ __launch_bounds__(256) void k_assign_bf16p(int64_t n, int dim, int ns
   }
 }
 
+// r06: the same pass, VALU-lean. At 2.45M x 47 the r03 kernel issued ~4,300 cycles
+// per 32-point tile on its SIMD (VALU is 4 cycles per wave64 instruction): the scatter into the padded
+// LDS rows divided every element index by dim (~1,500 cycles), the epilogue 112 x (fma, compare, two
+// selects) (~1,800), the 21 MFMAs 672 — 0.36 of the HBM roof. Here:
+//   * the tile's 32 x dim floats are ONE contiguous span: copied into the wave's LDS slot as is
+//     (float4 stores, row stride = dim, no index arithmetic; 16 zero floats past the slot);
+//   * B-fragments read row r's features 16 st + 8 h .. + 7 straight from that layout (two
+//     ds_read_b128 when dim % 4 == 0, else eight ds_read_b32), the last k-step's features past dim
+//     masked to zero (the next row's values would meet zero A entries, but a NaN or inf would not);
+//   * two centre tiles per pass: their MFMA chains interleave and the first tile's epilogue runs
+//     while the second's chain completes (VALU beside the MFMAs).
+template <int PER, bool VEC4>
+__global__ __launch_bounds__(256) void k_assign_bf16q(int64_t n, int dim, int nsteps, int ktiles,
+                                                      const float* __restrict__ X, int k,
+                                                      const bf16x8_t* __restrict__ frags,
+                                                      const float* __restrict__ cn_in,
+                                                      const float* __restrict__ C,
+                                                      int32_t* __restrict__ labels,
+                                                      float* __restrict__ sq_dist) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16x8_t* Af = reinterpret_cast<bf16x8_t*>(smem);
+  float* Cn = reinterpret_cast<float*>(smem + (size_t)ktiles * nsteps * 64 * 16);
+  float* Pt = Cn + ktiles * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, r = lane & 31;
+  const int slot = 32 * dim + 16;  // floats per wave slot (a multiple of 4: dim x 32 is)
+  {  // the prebuilt fragments and norms: coalesced 16-byte copies
+    const int nfr = ktiles * nsteps * 64;
+    for (int e = tid; e < nfr; e += 256) Af[e] = frags[e];
+    for (int c = tid; c < ktiles * 32; c += 256) Cn[c] = cn_in[c];
+  }
+  float* my = Pt + wave * slot;
+  if (lane < 16) my[32 * dim + lane] = 0.f;  // past the last row: read by row 31's masked features
+  __syncthreads();
+  const int nf4 = 8 * dim;  // float4 per full tile (32 rows x dim floats)
+  const int64_t ntiles = (n + 31) / 32, nfull = n / 32;
+  const int64_t step = (int64_t)gridDim.x * 4;
+  auto fetch = [&](int64_t tt, floatx4_t (&v)[PER]) {
+    if (tt >= nfull) return;  // the partial last tile is read scalar in stage()
+    const floatx4_t* src = reinterpret_cast<const floatx4_t*>(X + tt * 32 * dim);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) v[q] = __builtin_nontemporal_load(src + min(lane + 64 * q, nf4 - 1));
+  };
+  auto stage = [&](int64_t tt, const floatx4_t (&v)[PER]) {
+    if (tt < nfull) {
+      floatx4_t* d4 = reinterpret_cast<floatx4_t*>(my);
+#pragma unroll
+      for (int q = 0; q < PER; ++q)
+        if (lane + 64 * q < nf4) d4[lane + 64 * q] = v[q];
+    } else {
+      const int64_t m = (n - tt * 32) * dim;
+      for (int e = lane; e < 32 * dim; e += 64) my[e] = e < m ? X[tt * 32 * dim + e] : 0.f;
+    }
+  };
+  const int lastf = dim - 16 * (nsteps - 1) - 8 * h;  // features of the last k-step this lane keeps
+  auto compute = [&](int64_t tt) {
+    bf16x8_t b[8];
+    const float* row = my + r * dim;
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      if (st < nsteps) {
+        float x[8];
+        if constexpr (VEC4) {
+          const floatx4_t lo = *reinterpret_cast<const floatx4_t*>(row + 16 * st + 8 * h);
+          const floatx4_t hi = *reinterpret_cast<const floatx4_t*>(row + 16 * st + 8 * h + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            x[j] = lo[j];
+            x[4 + j] = hi[j];
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = row[16 * st + 8 * h + j];
+        }
+        if (st == nsteps - 1) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = j < lastf ? x[j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[st][j] = (__bf16)x[j];
+      }
+    }
+    float bestd = __builtin_inff();
+    int bestc = 0;
+    auto epilogue = [&](const floatx16& acc, int ct) {
+      const floatx4_t* cp = reinterpret_cast<const floatx4_t*>(Cn + ct * 32 + 4 * h);
+      floatx4_t cn[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) cn[g] = cp[2 * g];  // rows 8g + 4h .. +3
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const float d = __builtin_fmaf(-2.f, acc[reg], cn[reg >> 2][reg & 3]);
+        if (d < bestd) {
+          bestd = d;
+          bestc = ct * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        }
+      }
+    };
+    int ct = 0;
+    for (; ct + 2 <= ktiles; ct += 2) {
+      floatx16 a0 = {}, a1 = {};
+#pragma unroll
+      for (int st = 0; st < 8; ++st)
+        if (st < nsteps) {
+          a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Af[(ct * nsteps + st) * 64 + lane], b[st], a0, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Af[((ct + 1) * nsteps + st) * 64 + lane], b[st], a1, 0, 0, 0);
+        }
+      epilogue(a0, ct);
+      epilogue(a1, ct + 1);
+    }
+    if (ct < ktiles) {
+      floatx16 a0 = {};
+#pragma unroll
+      for (int st = 0; st < 8; ++st)
+        if (st < nsteps) a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Af[(ct * nsteps + st) * 64 + lane], b[st], a0, 0, 0, 0);
+      epilogue(a0, ct);
+    }
+    const float od = __shfl_xor(bestd, 32);
+    const int oc = __shfl_xor(bestc, 32);
+    if (od < bestd || (od == bestd && oc < bestc)) {
+      bestd = od;
+      bestc = oc;
+    }
+    const int64_t p = tt * 32 + r;
+    if (h == 0 && p < n) {
+      labels[p] = bestc;
+      if (sq_dist) sq_dist[p] = skl_sqdist(row, C + (int64_t)bestc * dim, dim);
+    }
+  };
+  floatx4_t va[PER], vb[PER];
+  int64_t t = (int64_t)blockIdx.x * 4 + wave;
+  fetch(t, va);
+  fetch(t + step, vb);
+  while (t < ntiles) {
+    stage(t, va);
+    fetch(t + 2 * step, va);  // two tiles in flight while this one computes
+    compute(t);
+    t += step;
+    if (t >= ntiles) break;
+    stage(t, vb);
+    fetch(t + 2 * step, vb);
+    compute(t);
+    t += step;
+  }
+}
+
+__host__ __device__ inline size_t assign_bf16q_lds(int ktiles, int nsteps, int dim) {
+  return (size_t)ktiles * nsteps * 64 * 16 + (size_t)ktiles * 32 * sizeof(float) +
+         (size_t)4 * (32 * dim + 16) * sizeof(float);
+}
+
 // ---------------------------------------------------------------------------------------------
 // small batches (minibatch steps): one block of WAVES waves per 32 points. Wave w owns centre tiles
 // w, w+WAVES, ...; it stages its tile (and, without cached norms, their numpy-order norms) in LDS,
@@ -1166,43 +1317,6 @@ __device__ __forceinline__ float fold_seq_lds(const float* __restrict__ b, int m
   }
   for (int t = g << 5; t < m; ++t) acc = acc + b[t];
   return acc;
-}
-
-// ---------------------------------------------------------------------------------------------
-// inertia: sequential fp32 sum in sample order. Four waves, one per SIMD: wave 0 folds one LDS
-// buffer of 4096 products (fold_seq_lds, bound by the dependent add chain) while waves 1-3, on the
-// other SIMDs so they never take wave 0's issue slots, stage the next buffer.
-// ---------------------------------------------------------------------------------------------
-constexpr int kInertiaChunk = 4096;
-__global__ __launch_bounds__(256) void k_inertia(int64_t n, const float* __restrict__ sq,
-                                                 const float* __restrict__ w,
-                                                 float* __restrict__ out,
-                                                 const int32_t* __restrict__ stop, int step_i) {
-  if (stopped(stop, step_i)) return;
-  __shared__ __attribute__((aligned(16))) float buf[2][kInertiaChunk];
-  const int nthr = blockDim.x - 64;  // waves 1.. stage
-  const int st = threadIdx.x - 64;
-  auto stage = [&](int64_t base, float* dst) {
-    const int m = (int)min<int64_t>(kInertiaChunk, n - base);
-    for (int t = st; t < m; t += nthr) {
-      const int64_t i = base + t;
-      dst[t] = w ? sq[i] * w[i] : sq[i] * 1.0f;  // sq_dist * sample_weight[i]
-    }
-  };
-  if (threadIdx.x >= 64 && n > 0) stage(0, buf[0]);
-  __syncthreads();
-  float acc = 0.f;
-  int cur = 0;
-  for (int64_t b = 0; b < n; b += kInertiaChunk) {
-    if (threadIdx.x >= 64) {
-      if (b + kInertiaChunk < n) stage(b + kInertiaChunk, buf[cur ^ 1]);
-    } else if (threadIdx.x == 0) {
-      acc = fold_seq_lds(buf[cur], (int)min<int64_t>(kInertiaChunk, n - b), acc);
-    }
-    __syncthreads();
-    cur ^= 1;
-  }
-  if (threadIdx.x == 0) out[0] = acc;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1567,422 +1681,6 @@ __global__ __launch_bounds__(64) void k_minibatch_update(int64_t b, int dim, con
   GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 25);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Device-loop MiniBatchKMeans, the update of step s-1 and the assignment of step s in ONE launch.
-// A step has two chip-wide dependencies (the assignment needs every centre after the previous
-// update; the update of a centre needs every label of its batch), which the two-launch form pays
-// as two kernel boundaries. Here block (pb, g) — batch points [32pb, 32pb+32) against the W centre
-// tiles of group g, as in k_mb_assign — first redoes update s-1 for ITS OWN W*32 centres: the
-// update of a centre reads only its members, so every pb of group g computes the same bits
-// (_k_means_minibatch.pyx:59-108: C_old*W, then the members in batch order, then * 1/(W+count)),
-// leaves them in the LDS tiles its MFMA chains read next, and writes its share of the outputs
-// (centre c and its weight sum and norm by block c % P, the inertia term of member item i by
-// block i % P). Per step one launch and two dependent global trips (step s-1's keys and batch
-// rows, then the members' rows together with this block's batch-s point rows) before the chains.
-//   do_update = 0: an assignment alone (step 0, and the step after a reassignment);
-//   do_assign = 0: an update alone (before a reassignment, and after the last step; P = 1).
-// Buffers rotate so nothing read in a launch is written in it: centres and weight sums by step
-// parity, keys over three buffers (keys_clear = the one the next assignment uses), sq by parity.
-// ---------------------------------------------------------------------------------------------
-struct MbFused {
-  const float* X;
-  const int64_t* rows_prev;             // batch s-1 (update)
-  const int64_t* rows_cur;              // batch s (assignment)
-  const unsigned long long* keys_prev;  // step s-1 keys (update)
-  unsigned long long* keys_cur;         // step s keys (assignment; all ~0 beforehand when G > 1)
-  unsigned long long* keys_clear;       // set to ~0 here for the next assignment (nullable)
-  const float* C_old;                   // centres before update s-1 (or, alone, the assignment's)
-  float* C_new;
-  const float* W_old;
-  float* W_new;
-  const float* cn2_in;                  // assignment alone: the centres' norms (null: computed)
-  float* cn2_out;                       // update: the new centres' norms (nullable)
-  float* sq_out;                        // update: batch s-1 distances to the old centres
-  const int32_t* stop;
-  int64_t b;
-  int dim, dimp, k, G, P, mcap;
-  int gate;  // the whole launch returns once the stop word places step `gate` past the stop
-  int do_update, do_assign;
-};
-
-struct MbFusedLds {
-  size_t pl, cl, nl, kl, prow, memu, lu, mem, ictr, off, cnt, wold, mrows, total;
-};
-
-__host__ __device__ inline MbFusedLds mb_fused_layout(int W, int dim, int64_t b, int mcap) {
-  MbFusedLds L;
-  const int S = ((dim + 1) & ~1) + 1;
-  size_t o = 0;
-  auto take = [&o](size_t bytes) {
-    const size_t at = o;
-    o = (o + bytes + 15) & ~size_t(15);
-    return at;
-  };
-  L.pl = take(sizeof(float) * 32 * S);                 // the block's 32 batch-s points
-  L.cl = take(sizeof(float) * (size_t)W * 32 * S);     // W centre tiles (old, then updated)
-  L.nl = take(sizeof(float) * 32 * W);                 // their norms
-  L.kl = take(sizeof(unsigned long long) * 32 * W);    // per-wave argmin keys
-  L.prow = take(sizeof(int64_t) * (size_t)b);          // batch s-1 rows
-  L.memu = take(sizeof(int32_t) * (size_t)b);          // the group's member items, unordered
-  L.lu = take(sizeof(int32_t) * (size_t)b);            //   and their local centres
-  L.mem = take(sizeof(int32_t) * (size_t)b);           // the member items in (centre, batch) order
-  L.ictr = take(sizeof(int32_t) * (size_t)b);          //   and their local centres
-  L.off = take(sizeof(int32_t) * (32 * W + 1));        // item offset of every local centre
-  L.cnt = take(sizeof(int32_t) * 32 * W);              // counts, then placement cursors
-  L.wold = take(sizeof(float) * 32 * W);               // weight sums before the update
-  L.mrows = take(sizeof(float) * (size_t)mcap * dim);  // member rows of one pass, item-major
-  L.total = o;
-  return L;
-}
-
-template <int W, bool VEC>
-__global__ __launch_bounds__(64 * W) void k_mb_fused(MbFused a, MbTail tl, RngNext rn) {
-  if (stopped(a.stop, a.gate)) return;
-  extern __shared__ __attribute__((aligned(16))) char fl[];
-  const int blk = blockIdx.x;
-  const int nmain = a.P * a.G;
-  if (blk >= nmain) {  // extra workgroups: an earlier step's tail, then the next batch draw
-    float* lds = reinterpret_cast<float*>(fl);
-    const int e = blk - nmain;
-    if (tl.active && e == 0)
-      mb_tail_block(tl, lds);
-    else if (rn.rows)
-      mt_randint_from(rn.in, reinterpret_cast<uint32_t*>(lds), 0, rn.n, rn.bs, rn.rows, rn.out);
-    return;
-  }
-  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 60 + (a.do_assign ? 0 : 10));
-  constexpr int NT = 64 * W, NC = 32 * W;
-  constexpr int KPT = (2048 + NT - 1) / NT;  // b <= 2048 (host check)
-  const MbFusedLds L = mb_fused_layout(W, a.dim, a.b, a.mcap);
-  const int dim = a.dim, S = a.dimp + 1;
-  float* Pl = reinterpret_cast<float*>(fl + L.pl);
-  float* Cl = reinterpret_cast<float*>(fl + L.cl);
-  float* Nl = reinterpret_cast<float*>(fl + L.nl);
-  unsigned long long* Kl = reinterpret_cast<unsigned long long*>(fl + L.kl);
-  int64_t* prow = reinterpret_cast<int64_t*>(fl + L.prow);
-  int32_t* memu = reinterpret_cast<int32_t*>(fl + L.memu);
-  int32_t* lu = reinterpret_cast<int32_t*>(fl + L.lu);
-  int32_t* mem = reinterpret_cast<int32_t*>(fl + L.mem);
-  int32_t* ictr = reinterpret_cast<int32_t*>(fl + L.ictr);
-  int32_t* off = reinterpret_cast<int32_t*>(fl + L.off);
-  int32_t* cnt = reinterpret_cast<int32_t*>(fl + L.cnt);
-  float* wold = reinterpret_cast<float*>(fl + L.wold);
-  float* Mr = reinterpret_cast<float*>(fl + L.mrows);
-  __shared__ int64_t s_rows[32];
-  __shared__ int s_M;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int pb = blk / a.G, g = blk - pb * a.G;
-  const int c0 = g * NC;
-  const int nc = min(NC, a.k - c0);
-  const int cb = c0 + wave * 32;  // this wave's tile
-  const int64_t p0 = (int64_t)pb * 32;
-  const int np = a.do_assign ? (int)min<int64_t>(32, a.b - p0) : 0;
-  float* Cw = Cl + (size_t)wave * 32 * S;
-  float* Nw = Nl + wave * 32;
-
-  // ---- trip 1: step s-1's labels and rows, this block's batch-s row indices, the old tiles ----
-  if (a.keys_clear)
-    for (int64_t i = (int64_t)blk * NT + tid; i < a.b; i += (int64_t)nmain * NT) a.keys_clear[i] = ~0ull;
-  int kv[KPT];
-  int64_t rv[KPT];
-  float wv = 0.f;
-  if (a.do_update) {
-#pragma unroll
-    for (int u = 0; u < KPT; ++u) {
-      const int64_t i = (int64_t)u * NT + tid;
-      kv[u] = -1;
-      if (i < a.b) {
-        kv[u] = (int)(unsigned)(a.keys_prev[i] & 0xffffffffull) - c0;  // local centre
-        rv[u] = a.rows_prev[i];
-      }
-    }
-    if (tid < nc) wv = a.W_old[c0 + tid];
-  }
-  int64_t my_row = 0;
-  if (tid < np) my_row = a.rows_cur[p0 + tid];
-  if (cb < a.k) {
-    const float* Cb = a.C_old + (int64_t)cb * dim;
-    stage_rows32<VEC>(Cw, S, [&](int r) { return Cb + (int64_t)r * dim; }, a.k - cb, dim, a.dimp,
-                      lane, 64);
-    if (!a.do_update && a.cn2_in && lane < 32) Nw[lane] = (cb + lane < a.k) ? a.cn2_in[cb + lane] : 0.f;
-  }
-  if (a.do_update) {
-#pragma unroll
-    for (int u = 0; u < KPT; ++u) {
-      const int64_t i = (int64_t)u * NT + tid;
-      if (i < a.b) prow[i] = rv[u];
-    }
-    if (tid < NC) {
-      cnt[tid] = 0;
-      wold[tid] = wv;
-    }
-  }
-  if (tid < 32) s_rows[tid] = my_row;
-  __syncthreads();
-  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 61 + (a.do_assign ? 0 : 10));
-
-  // ---- the group's members in (centre, batch) order: counts, scan, unordered placement, then
-  //      each member's rank inside its centre's short segment ----
-  int M = 0;
-  if (a.do_update) {
-#pragma unroll
-    for (int u = 0; u < KPT; ++u)
-      if (kv[u] >= 0 && kv[u] < nc) atomicAdd(&cnt[kv[u]], 1);
-    __syncthreads();
-    if (wave == 0) {
-      constexpr int E = (NC + 63) / 64;
-      int v[E];
-      int sum = 0;
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int j = lane * E + e;
-        v[e] = j < NC ? cnt[j] : 0;
-        sum += v[e];
-      }
-      int incl = sum;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-      }
-      int run = incl - sum;
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int j = lane * E + e;
-        if (j < NC) {
-          off[j] = run;
-          cnt[j] = run;  // the placement cursor
-        }
-        run += v[e];
-      }
-      if (lane == 63) {
-        off[NC] = incl;
-        s_M = incl;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < KPT; ++u)
-      if (kv[u] >= 0 && kv[u] < nc) {
-        const int p = atomicAdd(&cnt[kv[u]], 1);
-        memu[p] = u * NT + tid;
-        lu[p] = kv[u];
-      }
-    __syncthreads();
-    M = s_M;
-    for (int p = tid; p < M; p += NT) {
-      const int l = lu[p], x = memu[p];
-      const int lo = off[l], n = off[l + 1] - lo;
-      int r = 0;
-      for (int q0 = 0; q0 < n; q0 += 16) {
-        int y[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) y[q] = q0 + q < n ? memu[lo + q0 + q] : INT_MAX;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) r += y[q] < x ? 1 : 0;
-      }
-      mem[lo + r] = x;
-      ictr[lo + r] = l;
-    }
-    __syncthreads();
-  }
-  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 62 + (a.do_assign ? 0 : 10));
-
-  // ---- trip 2: this block's point rows (held in registers) and the members' rows, pass by pass ----
-  constexpr int PU = (32 * 16 + NT - 1) / NT;  // float4 per thread of a 32 x (dim <= 64) tile
-  float4 pv[PU];
-  const int q4 = dim >> 2;
-  if (VEC && np > 0) {
-#pragma unroll
-    for (int u = 0; u < PU; ++u) {
-      const int idx = u * NT + tid, r = idx / q4;
-      pv[u] = (idx < 32 * q4 && r < np)
-                  ? *reinterpret_cast<const float4*>(a.X + s_rows[r] * dim + 4 * (idx - r * q4))
-                  : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
-  // member-row staging: thread t copies column group ct of rows rt, rt + R, rt + 2R, ...
-  const int cols = VEC ? q4 : dim;
-  const int R = NT / cols;
-  const int rt = tid / cols, ct = tid - rt * cols;
-  // the update chains, one centre per lane pair: lane jl carries the first half of centre jl's
-  // features, lane jl+32 the second half (H floats each, a multiple of 4), through its members
-  constexpr int HM = 32;  // dim <= 64 (host check)
-  const int jl = lane & 31, hh = lane >> 5, lj = wave * 32 + jl;
-  const int H = ((dim + 7) >> 3) << 2;
-  const int f0 = hh * H, f1 = min(dim, f0 + H);
-  const int beg = a.do_update ? off[lj] : 0, end = a.do_update ? off[lj + 1] : 0;
-  const float w0 = a.do_update ? wold[lj] : 0.f;
-  float acc[HM];
-  if (a.do_update) {
-#pragma unroll
-    for (int u = 0; u < HM; ++u) acc[u] = (f0 + u < f1 && cb + jl < a.k) ? Cw[jl * S + f0 + u] * w0 : 0.f;
-  }
-  for (int q0 = 0; q0 < M; q0 += a.mcap) {
-    const int q1 = min(M, q0 + a.mcap);
-    if (q0 > 0) __syncthreads();  // the previous pass's rows are consumed
-    if (rt < R) {
-      for (int it0 = q0 + rt; it0 < q1; it0 += 16 * R) {
-        if (VEC) {
-          float4 v[16];
-#pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            const int it = it0 + u * R;
-            v[u] = it < q1 ? *reinterpret_cast<const float4*>(a.X + prow[mem[it]] * dim + 4 * ct)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-#pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            const int it = it0 + u * R;
-            if (it < q1) reinterpret_cast<float4*>(Mr + (size_t)(it - q0) * dim)[ct] = v[u];
-          }
-        } else {
-          float v[16];
-#pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            const int it = it0 + u * R;
-            v[u] = it < q1 ? a.X[prow[mem[it]] * dim + ct] : 0.f;
-          }
-#pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            const int it = it0 + u * R;
-            if (it < q1) Mr[(size_t)(it - q0) * dim + ct] = v[u];
-          }
-        }
-      }
-    }
-    __syncthreads();
-    if (q0 == 0) GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 63 + (a.do_assign ? 0 : 10));
-    // the inertia terms of this block's items (i = pb mod P) against the OLD rows still in the tiles
-    if (a.sq_out) {
-      const int first = q0 + ((pb - q0 % a.P) + a.P) % a.P;  // first i >= q0 with i % P == pb
-      for (int i = first + tid * a.P; i < q1; i += NT * a.P)
-        a.sq_out[mem[i]] = skl_sqdist(Mr + (size_t)(i - q0) * dim, Cl + (size_t)ictr[i] * S, dim);
-    }
-    // chain adds of this pass, two members per trip
-    const int i1 = min(end, q1);
-    int i = max(beg, q0);
-    for (; i + 2 <= i1; i += 2) {
-      const float* r0 = Mr + (size_t)(i - q0) * dim + f0;
-      const float* r1 = r0 + dim;
-      float v0[HM], v1[HM];
-#pragma unroll
-      for (int u = 0; u < HM; u += 4) {
-        if (VEC) {
-          const bool ok = f0 + u < f1;
-          const float4 t0 = ok ? *reinterpret_cast<const float4*>(r0 + u) : make_float4(0.f, 0.f, 0.f, 0.f);
-          const float4 t1 = ok ? *reinterpret_cast<const float4*>(r1 + u) : make_float4(0.f, 0.f, 0.f, 0.f);
-          v0[u] = t0.x, v0[u + 1] = t0.y, v0[u + 2] = t0.z, v0[u + 3] = t0.w;
-          v1[u] = t1.x, v1[u + 1] = t1.y, v1[u + 2] = t1.z, v1[u + 3] = t1.w;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v0[u + e] = f0 + u + e < f1 ? r0[u + e] : 0.f;
-            v1[u + e] = f0 + u + e < f1 ? r1[u + e] : 0.f;
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < HM; ++u)
-        if (f0 + u < f1) acc[u] = (acc[u] + v0[u]) + v1[u];  // x * 1.0f == x (unit sample weights)
-    }
-    if (i < i1) {
-      const float* r0 = Mr + (size_t)(i - q0) * dim + f0;
-#pragma unroll
-      for (int u = 0; u < HM; ++u)
-        if (f0 + u < f1) acc[u] = acc[u] + r0[u];
-    }
-  }
-  if (a.do_update) {
-    __syncthreads();  // every inertia term has read its old row
-    if (end > beg) {
-      const float Wn = w0 + (float)(end - beg);
-      const float alpha = 1.0f / Wn;  // Cython `1 / weight_sums[c]` with float operands
-#pragma unroll
-      for (int u = 0; u < HM; ++u)
-        if (f0 + u < f1) Cw[jl * S + f0 + u] = acc[u] * alpha;
-    }
-  }
-  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 64 + (a.do_assign ? 0 : 10));
-  if (np > 0) {  // the point tile (zero rows past np and a zero pad column, as stage_rows32)
-    if (VEC) {
-#pragma unroll
-      for (int u = 0; u < PU; ++u) {
-        const int idx = u * NT + tid;
-        if (idx < 32 * q4) {
-          const int r = idx / q4;
-          float* d = Pl + r * S + 4 * (idx - r * q4);
-          d[0] = pv[u].x;
-          d[1] = pv[u].y;
-          d[2] = pv[u].z;
-          d[3] = pv[u].w;
-        }
-      }
-      if (a.dimp > dim)
-        for (int r = tid; r < 32; r += NT) Pl[r * S + dim] = 0.f;
-    } else {
-      stage_rows32<false>(Pl, S, [&](int r) { return a.X + s_rows[r] * dim; }, np, dim, a.dimp, tid, NT);
-    }
-  }
-  // ---- the tile's norms (numpy's four accumulators) and this block's share of the outputs ----
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (cb < a.k) {
-    if (a.do_update || !a.cn2_in) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int t = h * 64 + lane, j = t >> 2, q = t & 3;
-        const float v = (cb + j < a.k) ? npy_sumsq_acc(Cw + j * S, dim, q) : 0.f;
-        const int l0 = lane & ~3;
-        const float a0 = __shfl(v, l0), a1 = __shfl(v, l0 + 1), a2 = __shfl(v, l0 + 2),
-                    a3 = __shfl(v, l0 + 3);
-        if (q == 0) Nw[j] = (a0 + a1) + (a2 + a3);
-      }
-    }
-    if (a.do_update) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int j0 = ((pb - cb % a.P) + a.P) % a.P;  // first row of this tile with c % P == pb
-      for (int j = j0; j < 32 && cb + j < a.k; j += a.P)
-        for (int f = lane; f < dim; f += 64) a.C_new[(int64_t)(cb + j) * dim + f] = Cw[j * S + f];
-      const int c = cb + lane;
-      if (lane < 32 && c < a.k && c % a.P == pb) {
-        a.W_new[c] = end > beg ? w0 + (float)(end - beg) : w0;
-        if (a.cn2_out) a.cn2_out[c] = Nw[lane];
-      }
-    }
-  }
-  if (!a.do_assign) return;
-  __syncthreads();  // the point tile is complete
-  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 65);
-  unsigned long long best = ~0ull;
-  if (cb < a.k) {
-    const int kh = lane >> 5;
-    const floatx16 d = mfma_chain<16>(Cw + (lane & 31) * S + kh, Pl + (lane & 31) * S + kh, a.dimp);
-    best = tile_best(d, Nw, cb, kh, a.k, best);
-  }
-  const unsigned long long other = __shfl_xor(best, 32);
-  best = other < best ? other : best;
-  if (lane < 32) Kl[wave * 32 + lane] = best;
-  __syncthreads();
-  if (wave == 0 && lane < np) {
-    unsigned long long bk = Kl[lane];
-#pragma unroll
-    for (int q = 1; q < W; ++q) {
-      const unsigned long long o = Kl[q * 32 + lane];
-      bk = o < bk ? o : bk;
-    }
-    if (a.G == 1)
-      a.keys_cur[p0 + lane] = bk;
-    else
-      atomicMin(a.keys_cur + p0 + lane, bk);
-  }
-  GDD_STAMP_WHEN(g_stamps_kmeans, (threadIdx.x == 0 && blockIdx.x == 0), 66);
-}
-
 __global__ void k_point_center_sqdist(int64_t n, int dim, const float* __restrict__ X,
                                       const int32_t* __restrict__ labels,
                                       const float* __restrict__ C, float* __restrict__ out) {
@@ -2148,9 +1846,8 @@ int launch_assign(int64_t n, int dim, const float* X, const int64_t* rows, int k
     };
     // two centre tiles per pass: four accumulator chains would need 292 registers, one wave per SIMD
     // (measured 1.38 vs 0.91 ms at the products shape)
-    static const bool persist = getenv("GDD_ASSIGN_PERSIST") != nullptr;  // A/B: the r02 form
     int rc0;
-    if (persist || dimp16 > 48) {  // wave tiles: dim <= 48 (every config's k-means input)
+    if (dimp16 > 48) {  // wave tiles: dim <= 48 (every config's k-means input)
       rc0 = go(k_assign_persist<2>);
     } else {
       // wave tiles: as many waves per block as the LDS holds with every centre in one chunk (the
@@ -2355,16 +2052,25 @@ extern "C" int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const 
       const int nfr = std::max(ktiles * nsteps * 64, ktiles * 32);
       k_bf16_frags<<<(nfr + 255) / 256, 256, 0, s>>>(dim, nsteps, ktiles, k, C, c_norm2, frags, cn);
       GDD_LAUNCHED();
+      const bool v1 = !forced("bf16_v2");  // A/B (r06): the VALU-lean kernel, opt-in until measured
+      const size_t ldsq = assign_bf16q_lds(ktiles, nsteps, dim);
       auto go = [&](auto P_) -> int {
         constexpr int P = decltype(P_)::value;
-        const void* fn = (const void*)k_assign_bf16p<P>;
-        GDD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        const void* fn = v1 ? (const void*)k_assign_bf16p<P>
+                            : (dim % 4 == 0 ? (const void*)k_assign_bf16q<P, true> : (const void*)k_assign_bf16q<P, false>);
+        const size_t l = v1 ? lds : ldsq;
+        GDD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l));
         int res = 0;
-        const int rrc = resident_blocks(fn, 256, lds, &res);
+        const int rrc = resident_blocks(fn, 256, l, &res);
         if (rrc) return rrc;
         const int64_t resident = res;
         const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 3) / 4, resident));
-        k_assign_bf16p<P><<<grid, 256, lds, s>>>(n, dim, nsteps, ktiles, X, k, frags, cn, C, labels, sq_dist);
+        if (v1)
+          k_assign_bf16p<P><<<grid, 256, l, s>>>(n, dim, nsteps, ktiles, X, k, frags, cn, C, labels, sq_dist);
+        else if (dim % 4 == 0)
+          k_assign_bf16q<P, true><<<grid, 256, l, s>>>(n, dim, nsteps, ktiles, X, k, frags, cn, C, labels, sq_dist);
+        else
+          k_assign_bf16q<P, false><<<grid, 256, l, s>>>(n, dim, nsteps, ktiles, X, k, frags, cn, C, labels, sq_dist);
         GDD_LAUNCHED();
         return GDD_OK;
       };
@@ -2399,14 +2105,6 @@ extern "C" int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const 
   return GDD_OK;
 }
 
-// the one-lane fold (GDD_INERTIA_SEQ=1; gdd_inertia itself is the exact parallel form, gdd_seqsum.hip)
-namespace gdd {
-int inertia_plain_launch(int64_t n, const float* sq, const float* w, float* out, hipStream_t s) {
-  k_inertia<<<1, 256, 0, s>>>(n, sq, w, out, nullptr, 0);
-  GDD_LAUNCHED();
-  return GDD_OK;
-}
-}  // namespace gdd
 
 extern "C" size_t gdd_minibatch_update_ws_bytes(int64_t b, int k) {
   (void)b;
@@ -2606,73 +2304,6 @@ int gdd::mb_loop_end(int64_t b, int k, int last_step, int64_t n_samples, int max
   return GDD_OK;
 }
 
-// device loop, one-launch steps (k_mb_fused): update of c.upd_step and/or assignment of
-// c.assign_step, plus the tail of c.tail_step (>= 0) and, with rn, the next batch draw
-bool gdd::mb_fused_ok(int64_t b, int dim, int k) {
-  return b >= 1 && b <= 2048 && dim >= 1 && dim <= 64 && k >= 1;
-}
-
-namespace {
-constexpr int kFusedW = 4;
-constexpr size_t kFusedLdsCap = 150 * 1024;
-
-template <bool VEC>
-int launch_mb_fused_v(const MbFused& a, const MbTail& tl, const RngNext& rn, hipStream_t s) {
-  const size_t lds = std::max({mb_fused_layout(kFusedW, a.dim, a.b, a.mcap).total,
-                               sizeof(float) * 2048 + 16, kMtRingBytes + 64});
-  if (lds > 65536)
-    GDD_HIP(hipFuncSetAttribute((const void*)k_mb_fused<kFusedW, VEC>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  const unsigned grid = (unsigned)(a.P * a.G) + (tl.active ? 1u : 0u) + (rn.rows ? 1u : 0u);
-  k_mb_fused<kFusedW, VEC><<<grid, 64 * kFusedW, lds, s>>>(a, tl, rn);
-  GDD_LAUNCHED();
-  return GDD_OK;
-}
-}  // namespace
-
-int gdd::mb_fused_launch(const MbFusedCall& c, const RngNext& rn, hipStream_t s) {
-  GDD_REQUIRE(mb_fused_ok(c.b, c.dim, c.k), "mb_fused: unsupported shape");
-  GDD_REQUIRE(c.do_update || c.do_assign, "mb_fused: nothing to do");
-  StepWs w = carve_step(c.step_ws, c.step_ws_bytes, c.b, c.k);
-  MBState* st = static_cast<MBState*>(c.state);
-  MbFused a{};
-  a.X = c.X;
-  a.rows_prev = c.rows_prev;
-  a.rows_cur = c.rows_cur;
-  a.keys_prev = c.do_update ? c.keys3 + (size_t)(c.upd_step % 3) * c.b : nullptr;
-  a.keys_cur = c.do_assign ? c.keys3 + (size_t)(c.assign_step % 3) * c.b : nullptr;
-  a.keys_clear = c.do_assign ? c.keys3 + (size_t)((c.assign_step + 1) % 3) * c.b : nullptr;
-  a.C_old = c.C_old;
-  a.C_new = c.C_new;
-  a.W_old = c.W_old;
-  a.W_new = c.W_new;
-  a.cn2_in = (!c.do_update && c.norms_valid) ? w.cn2 : nullptr;
-  a.cn2_out = (c.do_update && !c.do_assign) ? w.cn2 : nullptr;  // for a reassignment / lone assignment
-  a.sq_out = c.do_update ? w.sq[c.upd_step & 1] : nullptr;
-  a.stop = &st->stop_at;
-  a.b = c.b;
-  a.dim = c.dim;
-  a.dimp = (c.dim + 1) & ~1;
-  a.k = c.k;
-  a.G = ((c.k + 31) / 32 + kFusedW - 1) / kFusedW;
-  a.P = c.do_assign ? (int)((c.b + 31) / 32) : 1;
-  a.gate = c.gate;
-  a.do_update = c.do_update;
-  a.do_assign = c.do_assign;
-  const size_t fixed = mb_fused_layout(kFusedW, c.dim, c.b, 0).total;
-  GDD_REQUIRE(fixed + 64 * sizeof(float) * (size_t)c.dim <= kFusedLdsCap, "mb_fused: batch too large");
-  a.mcap = (int)std::min<int64_t>(c.b, (int64_t)((kFusedLdsCap - fixed) / (sizeof(float) * c.dim)));
-  if (const char* e = getenv("GDD_MB_FUSED_MCAP"))  // test hook: member rows per LDS pass
-    a.mcap = std::max(1, std::min(a.mcap, atoi(e)));
-  const MbTail tl = c.tail_step >= 0
-                        ? MbTail{w.sq[c.tail_step & 1], w.inertia, st, c.b, c.n_samples,
-                                 c.max_no_improvement, c.tail_step, 1, 1}
-                        : MbTail{nullptr, nullptr, nullptr, 0, 0, 0, 0, 0, 0};
-  const bool vec = (c.dim % 4 == 0) &&
-                   ((reinterpret_cast<uintptr_t>(c.X) | reinterpret_cast<uintptr_t>(c.C_old)) & 15) == 0;
-  return vec ? launch_mb_fused_v<true>(a, tl, rn, s) : launch_mb_fused_v<false>(a, tl, rn, s);
-}
-
 extern "C" int gdd_minibatch_converge(int64_t b, int k, int step_i, int64_t n_samples,
                                       int max_no_improvement, void* state, void* ws,
                                       size_t ws_bytes, gdd_stream_t stream) {
@@ -2714,8 +2345,7 @@ __global__ __launch_bounds__(1024) void k_mb_rng(const DevMT* __restrict__ in, D
   mt_randint_from(in, ring, 0, n, bs, rows, out);
 }
 
-constexpr int kRsBlockShuffle = 1;  // k_mb_reassign: the shuffle's draws by the whole block
-constexpr int kRsParCopy = 2;       // row copies in three block trips beside a one-wave next draw
+constexpr int kRsParCopy = 2;  // k_mb_reassign: row copies in three block trips beside a one-wave next draw
 
 // LDS arrival counters among some of a workgroup's waves (the others busy elsewhere): every
 // arriving wave's earlier LDS and global writes are visible to a wave whose wait returned true;
@@ -2813,7 +2443,6 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
   }
   if (t < 624) {
     ms.key[t] = kreg;
-    if (form & kRsBlockShuffle) ring[t] = kreg;  // slot 0 of the block shuffle's ring
   }
   if (t == 0) ms.pos = preg;
   __syncthreads();
@@ -2831,23 +2460,7 @@ __global__ __launch_bounds__(1024) void k_mb_reassign(
   GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0, 42);
   RS_STAMP(42);
   GDD_STAMP_WHEN(g_stamps_kmeans, threadIdx.x == 0 && m > 0, 48);
-  if (m > 0 && (form & kRsBlockShuffle)) {
-    if (t == 0) J[0] = 0;  // swap 0 <-> 0: lets position 0 trace like the others
-    int pe, iters = 0;
-    const int lb = mt_shuffle_draws_block(ring, ms.pos, (int)bs, J, &pe, &iters);
-#ifdef GDD_STAMPS
-    if (t == 0) {
-      g_stamps_kmeans[62] = (unsigned long long)iters;
-      g_stamps_kmeans[63] = (unsigned long long)pe;
-    }
-#else
-    (void)iters;
-#endif
-    const uint32_t* kb = ring + (lb % kMtRing) * 624;
-    for (int i = t; i < 624; i += blockDim.x) ms.key[i] = kb[i];
-    if (t == 0) ms.pos = pe;
-    __syncthreads();
-  } else if (m > 0) {
+  if (m > 0) {
     if (wave == 0) {
       if (lane == 0) J[0] = 0;
       mt_shuffle_draws_wave(&ms, (int)bs, J);
@@ -2975,13 +2588,6 @@ int mb_rng_launch(const DevMT* in, DevMT* out, int64_t n, int64_t bs, int64_t* r
   return GDD_OK;
 }
 
-// GDD_MB_REASSIGN_FORM (A/B; default kRsParCopy: the block shuffle measured slower)
-static int g_rs_form = kRsParCopy;
-void mb_reassign_form_refresh() {
-  const char* fe = getenv("GDD_MB_REASSIGN_FORM");
-  g_rs_form = fe ? atoi(fe) : kRsParCopy;
-}
-
 size_t mb_reassign_lds(int64_t bs, int k) {
   return sizeof(int) * (size_t)((bs + 1) & ~1ll) + sizeof(int) * (size_t)k + kMtRingBytes;
 }
@@ -2995,9 +2601,9 @@ int mb_reassign_launch(int step, int64_t bs, int dim, int k, float ratio, const 
   StepWs w = carve_step(step_ws, step_ws_bytes, bs, k);
   size_t lds = mb_reassign_lds(bs, k);
   GDD_REQUIRE(lds <= kReassignLdsCap, "mb_reassign: batch too large for the LDS swap table");
-  // GDD_MB_REASSIGN_FORM (A/B): bit 0 the block shuffle, bit 1 the parallel copies (default 2);
-  // the copies' index tables (bs/2 + 1 rows: m <= bs/2 here) follow the base layout where they fit
-  int form = g_rs_form;  // read once per fit (mb_reassign_form_refresh): no getenv per launch
+  // the parallel copies (kRsParCopy) where their index tables (bs/2 + 1 rows: m <= bs/2 here) fit
+  // after the base layout; else one dependent copy chain per reassigned cluster
+  int form = kRsParCopy;
   const size_t par_lds =
       ((sizeof(int) * (size_t)(((bs + 1) & ~1ll) + k) + kMtRingBytes + 7) & ~(size_t)7) +
       12 * (size_t)(bs / 2 + 1);

@@ -589,8 +589,6 @@ struct KppArgs {
   SklPlan plan;
   int exact;          // cum_tol's mode
   const float* D;     // the n x n distance table (plain-chain plans, n <= kDmBigMax), or nullptr
-  int par_chain;      // the block terms' lane chains by the exact parallel runs (r05)
-  int preload;        // k_kpp_round: every trial's block totals requested with the fold (r05, A/B)
 };
 
 __device__ __forceinline__ float wv(const float* w, int64_t i) { return w ? w[i] : 1.0f; }
@@ -630,19 +628,6 @@ __device__ int fold_round(const KppArgs& a, int q, float* s_pot) {
     if (tid == 0) s_pot[0] = a.pot1[q];
   } else {
     float y = 0.f;
-    // the n % 4 tail (<= 3 entries past the sgemv_t blocks) requested with the block terms (r05:
-    // read after the blocks' barrier it was a dependent trip of its own)
-    const int64_t nt = a.n - a.m1;
-    float tx[3] = {0.f, 0.f, 0.f}, tw[3] = {1.f, 1.f, 1.f};
-    if (tid < a.T && nt <= 3 && (a.preload & 2)) {
-      const float* row = a.dist[q] + (int64_t)tid * a.n;
-#pragma unroll
-      for (int o = 0; o < 3; ++o)
-        if (o < nt) {
-          tx[o] = row[a.m1 + o];
-          tw[o] = wv(a.w, a.m1 + o);
-        }
-    }
     for (int64_t b0 = 0; b0 < a.nsg; b0 += kFoldChunk) {
       const int m = (int)min<int64_t>(kFoldChunk, a.nsg - b0);
       for (int e = tid; e < m * a.T; e += blockDim.x) {
@@ -658,17 +643,9 @@ __device__ int fold_round(const KppArgs& a, int q, float* s_pot) {
     }
     if (tid < a.T) {
       if (a.m1 < a.n) {
-        float sx;
-        if (nt <= 3 && (a.preload & 2)) {  // the same operations on the requested values
-          sx = tx[0] * tw[0];
-#pragma unroll
-          for (int o = 1; o < 3; ++o)
-            if (o < nt) sx = __builtin_fmaf(tx[o], tw[o], sx);
-        } else {
-          const float* row = a.dist[q] + (int64_t)tid * a.n;
-          sx = row[a.m1] * wv(a.w, a.m1);
-          for (int64_t o = a.m1 + 1; o < a.n; ++o) sx = __builtin_fmaf(row[o], wv(a.w, o), sx);
-        }
+        const float* row = a.dist[q] + (int64_t)tid * a.n;
+        float sx = row[a.m1] * wv(a.w, a.m1);
+        for (int64_t o = a.m1 + 1; o < a.n; ++o) sx = __builtin_fmaf(row[o], wv(a.w, o), sx);
         y = y + sx;
       }
       s_pot[tid] = y;
@@ -985,58 +962,6 @@ __device__ float sgemv_block_wave(const float* __restrict__ s_d, const float* __
   return (ql + q1) + (q2 + q3);
 }
 
-// the exact parallel sgemv_t lane chains (r05): types and run algebra; the method is described with
-// par_chain_lanes below
-constexpr int kParHead = 32;     // entries of each chain the walker adds serially first
-constexpr int kParMaxSeg = 16;   // entries per precompute lane (nl = 4: 64 lanes x 16 >= 1024 - 32)
-constexpr int kParIdE = -1;      // identity run
-constexpr int kParBadE = -2;     // two runs in different binades (never built: a failed check)
-constexpr int kParMinBlock = 2048;  // sgemv_t blocks of at least this many entries take the runs
-
-struct ParT {
-  int e, d0, d1;  // biased exponent field of the binade, advances from even / odd s/u
-};
-
-__device__ __forceinline__ ParT par_compose(ParT A, ParT B) {  // A, then B
-  if (A.e == kParIdE) return B;
-  if (B.e == kParIdE) return A;
-  if (A.e != B.e) return ParT{kParBadE, 0, 0};
-  ParT C;
-  C.e = A.e;
-  C.d0 = A.d0 + ((A.d0 & 1) ? B.d1 : B.d0);  // even start: parity after A is A.d0's
-  C.d1 = A.d1 + ((A.d1 & 1) ? B.d0 : B.d1);  // odd start: parity after A is 1 + A.d1's
-  return C;
-}
-
-// s (the exact running value) advanced by run T; false when s is not in T's binade or the run would
-// carry it out (then s is left as it was)
-__device__ __forceinline__ bool par_apply(ParT T, float& s) {
-  if (T.e == kParIdE) return true;
-  const int bs = __float_as_int(s);
-  if ((bs >> 23) != T.e) return false;  // also s < 0, and kParBadE (never an exponent field)
-  const int nb = bs + ((bs & 1) ? T.d1 : T.d0);
-  if ((nb >> 23) != T.e) return false;
-  s = __int_as_float(nb);
-  return true;
-}
-
-struct ParLane {     // one precompute lane's result (LDS)
-  int ae, ad0, ad1;  // its runs before its crossing entries (all of them when it has none)
-  int ie, id0, id1;  // the segmented inclusive scan up to and including this lane
-  int x0, x1;        // chain positions added in hardware by the walker
-  int kind;          // 0 no crossing, 1 contiguous crossing entries, 2 walked serially
-};
-
-// defined with the pair launches' folds below
-template <int S>
-__device__ __forceinline__ void par_chain_lanes(int p, const float* __restrict__ base,
-                                                const float* __restrict__ s_d, int nl, int h4, int m1,
-                                                ParLane* __restrict__ s_par,
-                                                unsigned long long* __restrict__ s_mask);
-template <int NL>
-__device__ __forceinline__ float sgemv_block0_par(const float* __restrict__ s, int NB, bool k4x2,
-                                                  int* s_parsync, const ParLane* __restrict__ s_par,
-                                                  const unsigned long long* __restrict__ s_pmask);
 __device__ __forceinline__ void waves_arrive(int* ctr);
 __device__ __forceinline__ bool waves_wait(int* ctr, int target);
 
@@ -1051,9 +976,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   __shared__ double s_P, s_tot;
   __shared__ int s_cnt[kWaves], s_amb[kWaves];
   __shared__ int64_t s_ct;
-  __shared__ ParLane s_par[PICK ? 1 : 256];  // the block terms' parallel lane chains (r05)
-  __shared__ unsigned long long s_pmask[8];
-  __shared__ int s_parsync, s_pfxsync, s_pfxfail;
+  __shared__ int s_pfxsync, s_pfxfail;
   const int t = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int pq = (c - 1) & 1, cq = c & 1;
@@ -1062,21 +985,12 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   const double u = a.uniforms[(int64_t)(c - 1) * a.T + t];
   if (tid == 0) {
     s_jmin = INT_MAX;
-    s_parsync = 0;
     s_pfxsync = 0;
     s_pfxfail = 0;
   }
-  // r05: requested with the fold's block terms instead of after the winner is known (each was a
-  // dependent trip): round c-1's candidates (lane q: trial q's) and, with one block per thread, every
-  // trial's block totals of this thread's block
-  const int64_t csl = (c >= 2 && (a.preload & 4)) ? a.cand[pq][min(lane, a.T - 1)] : 0;
-  constexpr int kFsT = 12;  // T = 2 + ln k <= 12 up to k = 22,026
-  const bool fpre = (a.preload & 1) && c >= 2 && a.nblk <= kThr && a.T <= kFsT;
-  double fs[kFsT];
-  const int fj = a.nblk <= 64 ? lane : tid;  // the block this thread folds in the search below
-#pragma unroll
-  for (int q = 0; q < kFsT; ++q)
-    fs[q] = (fpre && q < a.T && fj < a.nblk) ? a.fsum[pq][(int64_t)q * a.nblk + fj] : 0.0;
+  // r05: round c-1's candidates (lane q: trial q's) requested with the fold's block terms instead of
+  // after the winner is known (that was a dependent trip)
+  const int64_t csl = c >= 2 ? a.cand[pq][min(lane, a.T - 1)] : 0;
   // ---- fold round c-1 (round 0: the first centre)
   int bw = 0;
   float pot;
@@ -1087,7 +1001,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     wrow = a.closest0;
     wfs = a.fsum0;
     __syncthreads();
-  } else if ((a.preload & 8) && a.T > 1 && a.T <= 64 && a.nsg <= kWaveFoldBlk && a.n - a.m1 <= 3) {
+  } else if (a.T > 1 && a.T <= 64 && a.nsg <= kWaveFoldBlk && a.n - a.m1 <= 3) {
     // r05: every wave folds every trial (lane q: trial q's block terms in block order, then the
     // n % 4 tail: fold_round's operations) and takes the argmin by shuffles, so no barrier
     const int tq = min(lane, a.T - 1);
@@ -1135,11 +1049,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     wrow = a.dist[pq] + (int64_t)bw * n;
     wfs = a.fsum[pq] + (int64_t)bw * a.nblk;
   }
-  double fw = 0.0;  // the winner's total of block fj (fpre)
-#pragma unroll
-  for (int q = 0; q < kFsT; ++q)
-    if (q == bw) fw = fs[q];
-  const int64_t src_prev = (a.preload & 4) ? __shfl(csl, bw) : (c >= 2 ? a.cand[pq][bw] : 0);
+  const int64_t src_prev = __shfl(csl, bw);
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 21);
   const double r = u * (double)pot;
   // ---- the block where the cumulative potential reaches r
@@ -1149,7 +1059,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     // r05: one block per lane and every wave the same scan — wave 0's operations in the workgroup
     // form below, where wave 0's lanes hold every block and the other waves' totals are zeros — so
     // every wave knows the block without a barrier
-    const double wj = lane < a.nblk ? (fpre ? fw : wfs[lane]) : 0.0;
+    const double wj = lane < a.nblk ? wfs[lane] : 0.0;
     double inc = wj;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1170,7 +1080,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     const int64_t ch = (a.nblk + kThr - 1) / kThr;
     const int64_t lo = min<int64_t>(a.nblk, tid * ch), hi = min<int64_t>(a.nblk, lo + ch);
     double run = 0.0;
-    for (int64_t j = lo; j < hi; ++j) run = run + (fpre ? fw : wfs[j]);
+    for (int64_t j = lo; j < hi; ++j) run = run + wfs[j];
     double inc = run;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1187,7 +1097,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
     int found = INT_MAX;
     double Pf = 0.0;
     for (int64_t j = lo; j < hi; ++j) {
-      const double Pn = P + (fpre ? fw : wfs[j]);
+      const double Pn = P + wfs[j];
       if (Pn >= r) {
         found = (int)j;
         Pf = P;
@@ -1341,15 +1251,11 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 24);
   // ---- the block's terms for round c+1: cumulative total, sgemv_t lane chains
   const int64_t NB = min<int64_t>(kBlk, a.m1 - j0);
-  // the block's lane chains by the exact parallel runs (waves 12..15 precompute, wave 0 walks) when
-  // the weights are unit and the chains are long enough to pay
-  const bool par = !PICK && a.par_chain && a.w == nullptr && NB >= kParMinBlock && a.T > 1;
-  const bool k4x2 = (a.T & 2) && t >= (a.T & ~3) && t < (a.T & ~3) + 2;
-  // r05 (preload bit 32): the block prefix beside the lane chain instead of before it. Every wave posts
-  // its scan total and arrives on an LDS counter; wave 0 (no waves before it: block_prefix's B = 0)
-  // stores its prefixes and runs the chain, the others wait for the count and finish theirs. A wait
-  // that gave up is redone with block_prefix after a closing barrier.
-  const bool ovl = !PICK && !par && (a.preload & 32) && NB > 0 && a.T > 1;
+  // r05: the block prefix beside the lane chain instead of before it. Every wave posts its scan total
+  // and arrives on an LDS counter; wave 0 (no waves before it: block_prefix's B = 0) stores its
+  // prefixes and runs the chain, the others wait for the count and finish theirs. A wait that gave
+  // up is redone with block_prefix after a closing barrier.
+  const bool ovl = !PICK && NB > 0 && a.T > 1;
   {
     double v[kPer], pre[kPer];
     float xs[kPer];  // every read before the weights' branches (r04)
@@ -1415,23 +1321,6 @@ __global__ __launch_bounds__(kThr) void k_kpp_round(KppArgs a, int c) {
       }
     }
   }
-  if (!ovl && NB > 0 && a.T > 1 && wave == 0) {
-    float v;
-    if (par)
-      v = k4x2 ? sgemv_block0_par<4>(s_d, (int)NB, true, &s_parsync, s_par, s_pmask)
-               : sgemv_block0_par<8>(s_d, (int)NB, false, &s_parsync, s_par, s_pmask);
-    else
-      v = sgemv_block_wave(s_d, a.w ? a.w + j0 : nullptr, NB, t, a.T);
-    if (lane == 0) a.vblk[cq][(int64_t)t * a.nblk + blk] = v;
-  } else if (par && wave >= kWaves - 4) {
-    const int h4 = k4x2 ? 0 : (int)(NB & 4);
-    const int p = tid - 64 * (kWaves - 4);
-    if (k4x2)
-      par_chain_lanes<4>(p, s_d + h4, s_d, 4, h4, (int)NB, s_par, s_pmask);
-    else
-      par_chain_lanes<8>(p, s_d + h4, s_d, 8, h4, (int)NB, s_par, s_pmask);
-    waves_arrive(&s_parsync);
-  }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0), 25);
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && blk == 0 && t == 0 && c < 128), 128 + c);
 }
@@ -1449,7 +1338,6 @@ constexpr int kSplitMinBlocks = 128;
 template <int T>
 __global__ __launch_bounds__(kThr) void k_kpp_dists(KppArgs a, int c) {
   extern __shared__ double s_cs[];  // T * dim doubles (candidate rows), then T * kBlk floats
-  __shared__ double s_wave[kWaves];
   __shared__ double s_cn[kSplitMaxT];
   const int blk = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int dim = a.dim;
@@ -1664,9 +1552,6 @@ struct Kpp1Args {
   int64_t* candw2[2];    // [T*T][T]
   int64_t* candself2[2];  // [T*T]
   int exact;             // cum_tol's mode
-  int bsearch;           // 1: the folds' binary searches (GDD_KPP_BSEARCH, A/B); 0: two-ballot searches
-  int spec_search;       // the folds' speculative searches, T <= 12 (GDD_KPP_SPEC_SEARCH=0 turns them off)
-  int par_chain;         // k_kpp1_big: block 0's lane chains by the exact parallel runs (r05)
 };
 
 __device__ __forceinline__ int kpp1_argmin(const float* __restrict__ pot, int T) {
@@ -1805,21 +1690,7 @@ __device__ __forceinline__ void chain_add32(const float4 (&v)[8], float& acc) {
   }
 }
 
-// the plain form (reads of a group issued just before its adds), kept for A/B timing
-__device__ __forceinline__ float chain_add_plain(const float* __restrict__ p, int L, float acc) {
-  int m = 0;
-  for (; m + 32 <= L; m += 32) {
-    float4 v[8];
-    chain_load32(p + m, v);
-    chain_add32(v, acc);
-  }
-  for (; m < L; ++m) acc = acc + p[m];
-  return acc;
-}
-
-template <bool PIPE = true>
 __device__ __forceinline__ float chain_add(const float* __restrict__ p, int L, float acc) {
-  if (!PIPE) return chain_add_plain(p, L, acc);
   int m = 0;
   float4 A[8];
   chain_load32(p, A);  // past L: row padding, never added
@@ -2011,171 +1882,10 @@ __device__ __forceinline__ bool prefix_waves_sync(int* ctr, int target) {
   return false;
 }
 
-// ---- exact parallel sgemv_t lane chains (r05) -----------------------------------
-// A unit-weight lane chain (acc = acc + x over L <= 1024 non-negative fp32 entries) evaluated with
-// the bits of the sequential loop but without its L dependent adds. While the running sum s stays in
-// one binade [2^e, 2^(e+1)) it is a multiple of u = 2^(e-23), and adding x moves it by a whole number
-// of quanta that depends on x and, at an exact tie, on the parity of s/u — so a run of entries that
-// keeps the sum inside the binade maps s to s + D[parity(s/u)] u with two integers D0, D1: the run
-// evaluated in hardware from 2^e (even) and from 2^e + u (odd) — equal starting parities take equal
-// advances at every entry, by induction. Runs in one binade compose: the parity after the first run
-// picks the second run's D. Entries where the sum may change binade are added in hardware from the
-// exact running value. The binades come from an fp32 prefix of the chain, within 2^-13 of every
-// exact partial sum (the chain's own rounding is <= L 2^-24 <= 2^-14 relative, all terms >= 0); an
-// entry is a possible crossing unless the prefixes before and after it, widened by 2^-9, share an
-// exponent, so every run's binade is proven. Each applied run is checked anyway (s in its binade, no
-// carry out of it) and a failed check replays the whole chain serially.
-// Layout (512-thread workgroups): wave 0's lane c adds chain c's first kParHead entries serially
-// while waves 4..7 (256 / nl lanes per chain, <= kParMaxSeg entries each) classify the rest, evaluate
-// their runs from 2^e and 2^e + u, and compose them with a segmented scan that restarts after every
-// crossing; lane c then applies the composed runs and adds only the crossing entries.
-
-// chain c's entry m: S == 0 chain-major rows (s_ch + c kChainLd + m, the pair launches), S > 0 the
-// natural LDS row (base + c + S m, k_kpp1_big's sgemv_t blocks)
-template <int S>
-__device__ __forceinline__ const float* par_chain_src(const float* base, int c) {
-  return S == 0 ? base + c * kChainLd : base + c;
-}
-
-// 256 lanes (p = 0..255, four whole waves) precompute nl chains: lane p owns segment g of chain c.
-// L = (m1 - h4 - c + nl - 1) / nl entries per chain; acc0 the chain's start value (s_d[c] for c < h4)
-template <int S>
-__device__ __forceinline__ void par_chain_lanes(int p, const float* __restrict__ base,
-                                                const float* __restrict__ s_d, int nl, int h4, int m1,
-                                                ParLane* __restrict__ s_par,
-                                                unsigned long long* __restrict__ s_mask) {
-  const int G = 256 / nl;  // 32 (nl = 8) or 64 (nl = 4): within one wave
-  const int c = p / G, g = p - c * G;
-  const int L = max((m1 - h4 - c + nl - 1) / nl, 0);
-  const int H = min(kParHead, L);
-  const int seg = min(kParMaxSeg, ((L - H + G - 1) / G + 3) & ~3);
-  const int a = H + g * seg;
-  const int cnt = max(0, min(seg, L - a));
-  const float* src = par_chain_src<S>(base, c);
-  float x[kParMaxSeg];
-  if constexpr (S == 0) {
-#pragma unroll
-    for (int q = 0; q < kParMaxSeg / 4; ++q) {  // a is a multiple of 4; reads stay inside the padded row
-      const float4 v = *reinterpret_cast<const float4*>(src + min(a, 1024) + 4 * q);
-      x[4 * q] = v.x;
-      x[4 * q + 1] = v.y;
-      x[4 * q + 2] = v.z;
-      x[4 * q + 3] = v.w;
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < kParMaxSeg; ++q) x[q] = src[S * min(a + q, max(L - 1, 0))];
-  }
-  const float acc0 = c < h4 ? s_d[c] : 0.f;
-  float hx = g < H ? src[S == 0 ? g : S * g] : 0.f;  // head entries, one per lane (G >= kParHead)
-  float loc[kParMaxSeg];
-  float run = 0.f;
-#pragma unroll
-  for (int i = 0; i < kParMaxSeg; ++i) {
-    x[i] = i < cnt ? x[i] : 0.f;
-    run = run + x[i];
-    loc[i] = run;
-  }
-  float inc = run;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    if (o < G) {
-      const float y = __shfl_up(inc, o, G);
-      if (g >= o) inc = inc + y;
-      hx = hx + __shfl_xor(hx, o, G);
-    }
-  }
-  const float ps = (acc0 + hx) + (inc - run);  // approximate exact value before the segment
-  constexpr float kLo = 1.0f - 1.0f / 512, kHi = 1.0f + 1.0f / 512;
-  unsigned cm = 0u;  // entries where the sum may change binade
-#pragma unroll
-  for (int i = 0; i < kParMaxSeg; ++i) {
-    const float prev = i ? ps + loc[i - 1] : ps;
-    const float cur = ps + loc[i];
-    const int el = __float_as_int(prev * kLo) >> 23, eh = __float_as_int(cur * kHi) >> 23;
-    if (i < cnt && !(el == eh && el >= 1 && eh <= 253)) cm |= 1u << i;
-  }
-  const int j1 = cm ? __builtin_ctz(cm) : cnt;
-  const int j2 = cm ? 31 - __builtin_clz(cm) : cnt - 1;
-  int kind = cm == 0u ? 0 : ((cm >> j1) == ((2u << (j2 - j1)) - 1u) ? 1 : 2);
-  const int eA = j1 > 0 ? __float_as_int(ps) >> 23 : 127;
-  const int eB = (kind == 1 && j2 < cnt - 1) ? __float_as_int(ps + loc[cnt - 1]) >> 23 : 127;
-  // the runs before the crossing entries (A) and after them (B), from 2^e and 2^e + u
-  float a0 = __int_as_float(eA << 23), a1 = __int_as_float((eA << 23) + 1);
-  float b0 = __int_as_float(eB << 23), b1 = __int_as_float((eB << 23) + 1);
-#pragma unroll
-  for (int i = 0; i < kParMaxSeg; ++i) {
-    const float xa = i < j1 ? x[i] : 0.f;
-    const float xb = (i > j2 && i < cnt) ? x[i] : 0.f;
-    a0 = a0 + xa;
-    a1 = a1 + xa;
-    b0 = b0 + xb;
-    b1 = b1 + xb;
-  }
-  const ParT id{kParIdE, 0, 0};
-  ParT A = id, B = id;
-  if (j1 > 0) A = ParT{eA, __float_as_int(a0) - (eA << 23), __float_as_int(a1) - (eA << 23) - 1};
-  if (kind == 1 && j2 < cnt - 1) B = ParT{eB, __float_as_int(b0) - (eB << 23), __float_as_int(b1) - (eB << 23) - 1};
-  if ((j1 > 0 && (__float_as_int(a1) >> 23) != eA) || (kind == 1 && j2 < cnt - 1 && (__float_as_int(b1) >> 23) != eB))
-    kind = 2;  // a run left its binade (cannot happen with the margins above): walk it
-  // segmented inclusive scan: (f, T) = (f_l | f_r, f_r ? T_r : T_l then T_r)
-  int f = kind != 0;
-  ParT T = kind == 0 ? A : (kind == 1 ? B : id);
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    if (o < G) {
-      const int lf = __shfl_up(f, o, G), le = __shfl_up(T.e, o, G);
-      const int l0 = __shfl_up(T.d0, o, G), l1 = __shfl_up(T.d1, o, G);
-      if (g >= o && !f) {
-        T = par_compose(ParT{le, l0, l1}, T);
-        f = lf;
-      }
-    }
-  }
-  ParLane r;
-  r.ae = A.e;
-  r.ad0 = A.d0;
-  r.ad1 = A.d1;
-  r.ie = T.e;
-  r.id0 = T.d0;
-  r.id1 = T.d1;
-  r.x0 = kind == 2 ? a : a + j1;
-  r.x1 = kind == 2 ? a + cnt : (kind == 1 ? a + j2 + 1 : a + j1);
-  r.kind = kind;
-  s_par[p] = r;
-  const unsigned long long bal = __ballot(kind != 0);
-  const unsigned long long gm = G == 64 ? bal : ((bal >> ((threadIdx.x & 63) & 32)) & 0xffffffffull);
-  if (g == 0) s_mask[c] = gm;
-}
-
-// the walker (lane c < nl of one wave): the chain's exact value from the head result s and the
-// published runs; src = chain c's first entry (stride S, or contiguous for S == 0)
-template <int S = 0>
-__device__ __forceinline__ float par_chain_walk(const float* __restrict__ src, int c, int nl, float s,
-                                                const ParLane* __restrict__ s_par,
-                                                const unsigned long long* __restrict__ s_mask, bool& ok) {
-  const int G = 256 / nl;
-  const ParLane* rl = s_par + c * G;
-  unsigned long long m = s_mask[c];
-  while (m) {
-    const int q = __builtin_ctzll(m);
-    m &= m - 1;
-    if (q > 0) ok = par_apply(ParT{rl[q - 1].ie, rl[q - 1].id0, rl[q - 1].id1}, s) && ok;
-    const ParLane r = rl[q];
-    if (r.kind == 1) ok = par_apply(ParT{r.ae, r.ad0, r.ad1}, s) && ok;
-    for (int i = r.x0; i < r.x1; ++i) s = s + src[S == 0 ? i : S * i];
-  }
-  ok = par_apply(ParT{rl[G - 1].ie, rl[G - 1].id0, rl[G - 1].id1}, s) && ok;
-  return s;
-}
-
 // the fold of round c's trial t by one 256-thread workgroup holding the trial's row in registers
 // (r[q] = entry tid + 256 q): the exact sgemv_t potential, the fp64 cumulative potential and the
 // candidates every trial would draw in round c+1 if t wins
 // pot_out (nullable) receives the potential, cand_out[0..T) the candidates (global memory or LDS)
-// PAR (512-thread workgroups, r05): the lane chains by par_chain_lanes / par_chain_walk (waves 4..7
-// precompute, wave 0 walks); threads 0..255 hold the row as before
-template <bool PIPE = true, bool PAR = false>
 __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t, const float (&r)[16],
                                                 double ut, float* __restrict__ s_d,
                                                 float* __restrict__ s_ch, double* __restrict__ s_cum,
@@ -2189,7 +1899,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
   const bool k4x2 = (T & 2) && t >= (T & ~3) && t < (T & ~3) + 2;
   const int h4 = k4x2 ? 0 : (m1 & 4);
   const bool perm = a.w == nullptr;
-  // speculative searches (r04, a.spec_search): while wave 0 runs the lane chains (~2 us of dependent
+  // speculative searches (r04): while wave 0 runs the lane chains (~2 us of dependent
   // adds), waves 1-3 finish the cumulative potential among themselves (an LDS arrival counter, not the
   // workgroup barrier) and search every uniform with the fp64 total standing in for the potential.
   // After the chains each result is checked against the exact potential (it is numpy's index when
@@ -2198,20 +1908,15 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
   __shared__ int s_sync;
   __shared__ int s_sidx[kMaxTrials];
   __shared__ int s_sok;
-  __shared__ ParLane s_par[PAR ? 256 : 1];
-  __shared__ unsigned long long s_pmask[8];
-  __shared__ int s_parsync;
-  const bool par = PAR && perm && m1 > 0;  // uniform over the workgroup
   // measured (profiles/r04_kpp_spec_search.txt): T = 8 (3000 x 40, k = 454) 8.07 -> 7.44 us per round
   // once the prefix reads are batched (before that the prefix alone took as long as the chains and the
   // speculation lost); T = 7 (3706 x 64, k = 371) 11.33 -> 10.44, T = 6 (Cora) 9.97 -> 9.68
-  const bool spec = a.spec_search && !a.bsearch && c + 1 < a.k && T <= 12;
+  const bool spec = c + 1 < a.k && T <= 12;
   if (tid == 0) {
     s_sync = 0;
     s_sok = 1;
-    s_parsync = 0;
   }
-  if (!PAR || tid < 256) {
+  {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = tid + 256 * q;
@@ -2237,27 +1942,10 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
       if (perm) {
         const int nl = k4x2 ? 4 : 8;
         float acc = 0.f;
-        if (par) {  // head serially, then the walk over waves 4..7's runs
-          const int L = max((m1 - h4 - lane + nl - 1) / nl, 0);
-          if (lane < nl) {
-            if (lane < h4) acc = acc + s_d[lane];
-            acc = chain_add<PIPE>(s_ch + lane * kChainLd, min(L, kParHead), acc);
-          }
-          bool ok = waves_wait(&s_parsync, 4);
-          if (lane < nl) {
-            const float s = par_chain_walk(s_ch + lane * kChainLd, lane, nl, acc, s_par, s_pmask, ok);
-            if (ok) {
-              acc = s;
-            } else {  // a failed check (or a spin that gave up): the sequential loop
-              acc = 0.f;
-              if (lane < h4) acc = acc + s_d[lane];
-              acc = chain_add<PIPE>(s_ch + lane * kChainLd, L, acc);
-            }
-          }
-        } else if (lane < nl) {
+        if (lane < nl) {
           if (lane < h4) acc = acc + s_d[lane];
           const int L = (m1 - h4 - lane + nl - 1) / nl;
-          acc = chain_add<PIPE>(s_ch + lane * kChainLd, max(L, 0), acc);
+          acc = chain_add(s_ch + lane * kChainLd, max(L, 0), acc);
         }
         if (k4x2) {
           const float a1 = __shfl(acc, 1), a2 = __shfl(acc, 2), a3 = __shfl(acc, 3);
@@ -2281,11 +1969,6 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
       if (pot_out) *pot_out = y;
     }
     GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 76);
-  } else if (PAR && wave >= 4) {  // the lane chains' runs (par_chain_lanes)
-    if (par) {
-      par_chain_lanes<0>((int)threadIdx.x - 256, s_ch, s_d, k4x2 ? 4 : 8, h4, m1, s_par, s_pmask);
-      waves_arrive(&s_parsync);
-    }
   } else {  // the cumulative potential: thread runs and the wave's inclusive scan
     // every read issued before the run (a per-entry weight branch had each read waited on alone:
     // ~2 us, as long as the chains, r04 stamps); entries past n add +0.0, as before
@@ -2393,7 +2076,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
     }
   }
   if (c + 1 < a.k) {
-    if (wave > 0 && (!PAR || wave < 4) && !spec) {
+    if (wave > 0 && !spec) {
       double B = 0.0;
       for (int q = 0; q < wave - 1; ++q) B = B + s_wave[q];
       const double pot = (double)s_pot;
@@ -2405,21 +2088,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
       (void)pot;
     }
     __syncthreads();
-    if (a.bsearch) {
-      if (tid < T) {  // searchsorted_left(cum, u * pot): binary search over the LDS cumulative potential
-        const double rr = ut * (double)s_pot;
-        int lo = 0, hi = n;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (s_cum[mid] < rr) lo = mid + 1; else hi = mid;
-        }
-        // the answer's two neighbours decide it (cum_tol): replay numpy's sum when either is close
-        const double tol = cum_tol(a.exact, n, rr);
-        if ((lo > 0 && fabs(s_cum[lo - 1] - rr) <= tol) || (lo < n && fabs(s_cum[lo] - rr) <= tol))
-          lo = (int)np_cumsum_search(s_d, a.w, n, rr);
-        cand_out[tid] = min(n - 1, lo);
-      }
-    } else {
+    {
       // searchsorted_left(cum, u * pot) in two ballots: lane l of every wave holds the last value of
       // block l (64 blocks of Bk = ceil(n / 64) entries); wave w takes uniforms w, w + 4, ...: the
       // blocks below r counted by one ballot, then one LDS read per lane and a ballot inside the next
@@ -2589,54 +2258,8 @@ __global__ __launch_bounds__(256) void k_kpp1_fused(Kpp1Args a, int c) {
 // The chain's feature slots: 48 (dim <= 48) or 64 (dim <= 64, e.g. the recsys SVD embeddings);
 // slots past dim are zero, and an fma with a zero operand leaves the chain unchanged.
 constexpr int kDmX = 64;   // widest table chain (dim <= kDmX)
-constexpr int kDmJ = 32;   // candidate rows per table workgroup
 constexpr int kDmMinK = 16;  // centres from which the table is built
 
-template <int kDmX>
-__global__ __launch_bounds__(256) void k_kpp_dmat(int n, int dim, const float* __restrict__ X,
-                                                  const float* __restrict__ XT,
-                                                  const double* __restrict__ xsq,
-                                                  float* __restrict__ D) {
-  __shared__ double s_c[kDmJ * kDmX];
-  __shared__ double s_cn[kDmJ];
-  const int tid = threadIdx.x;
-  const int i = blockIdx.x * 256 + tid, ic = min(i, n - 1);
-  const int j0 = blockIdx.y * kDmJ;
-  float x[kDmX];
-#pragma unroll
-  for (int v = 0; v < kDmX; ++v) x[v] = XT[(int64_t)min(v, dim - 1) * n + ic];
-  for (int e = tid; e < kDmJ * kDmX; e += 256) {
-    const int jj = e / kDmX, v = e - jj * kDmX;
-    const int j = min(j0 + jj, n - 1);
-    s_c[e] = v < dim ? (double)X[(int64_t)j * dim + v] : 0.0;
-  }
-  if (tid < kDmJ) s_cn[tid] = xsq[min(j0 + tid, n - 1)];
-  const double xs = xsq[ic];
-  __syncthreads();
-  for (int jj = 0; jj < kDmJ; jj += 4) {
-    double dot[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int v = 0; v < kDmX; ++v)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) dot[u] = __builtin_fma(s_c[(jj + u) * kDmX + v], (double)x[v], dot[u]);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = j0 + jj + u;
-      float f = (float)(((-2.0 * dot[u]) + s_cn[jj + u]) + xs);
-      f = f < 0.f ? 0.f : f;
-      if (i < n && j < n) D[(int64_t)j * n + i] = f;
-    }
-  }
-}
-
-// The same table by register tiles (r05): a 256-thread block computes 64 points i x 64 candidates j,
-// thread (ti, tj) the 4 x 4 pairs i0 + 4 ti + b, j0 + 4 tj + a. Both operand tiles come from X^T
-// (coalesced) into LDS as fp64, feature-major, so per feature a thread reads its four x and four c
-// values with four 16-byte LDS reads and issues 16 fp64 fmas (the row form read one LDS value per
-// fma). Each pair's dot product is the same chain: fma over the features in order from 0 — the row
-// form's zero-padded tail adds +-0 products, which leave every nonzero dot unchanged and change
-// only the sign of a zero dot, invisible after + ||c||^2 — so the table has the same bits.
-// LDS: 2 x 64 x dim doubles (dynamic, dim <= kDmX).
 template <int TI, int TJ>
 __global__ __launch_bounds__(256) void k_kpp_dmat_t(int n, int dim, const float* __restrict__ XT,
                                                     const double* __restrict__ xsq,
@@ -2712,39 +2335,22 @@ __global__ __launch_bounds__(256) void k_kpp_dmat_t(int n, int dim, const float*
   }
 }
 
-// the n x n distance table (k_kpp_dmat_t; GDD_KPP_DMAT_ROWS: the r04 row form, A/B)
+// the n x n distance table (k_kpp_dmat_t: 4 x 4 fp64 register tiles per thread; r05 measured the
+// 8 x 4 and 8 x 8 tiles and the r04 one-row-per-thread form slower)
 int launch_kpp_dmat(int64_t n, int dim, const float* X, const float* XT, const double* xsq, float* D,
                     hipStream_t s) {
-  if (getenv("GDD_KPP_DMAT_ROWS") == nullptr) {
-    // GDD_KPP_DMAT_TILE (A/B): per-thread tile 44 (default), 84 or 88 (points x candidates)
-    const char* te = getenv("GDD_KPP_DMAT_TILE");
-    const int tile = te ? atoi(te) : 44;
-    auto go = [&](auto kern, int ti, int tj) -> int {
-      const size_t lds = sizeof(double) * 16 * (size_t)(ti + tj) * dim;
-      if (lds > 65536)
-        GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      const dim3 g((unsigned)((n + 16 * ti - 1) / (16 * ti)), (unsigned)((n + 16 * tj - 1) / (16 * tj)));
-      kern<<<g, 256, lds, s>>>((int)n, dim, XT, xsq, D);
-      return 0;
-    };
-    if (tile == 88)
-      go(k_kpp_dmat_t<8, 8>, 8, 8);
-    else if (tile == 84)
-      go(k_kpp_dmat_t<8, 4>, 8, 4);
-    else
-      go(k_kpp_dmat_t<4, 4>, 4, 4);
-  } else {
-    const dim3 gdm((unsigned)((n + 255) / 256), (unsigned)((n + kDmJ - 1) / kDmJ));
-    if (dim <= 48)
-      k_kpp_dmat<48><<<gdm, 256, 0, s>>>((int)n, dim, X, XT, xsq, D);
-    else
-      k_kpp_dmat<64><<<gdm, 256, 0, s>>>((int)n, dim, X, XT, xsq, D);
-  }
+  (void)X;
+  constexpr int ti = 4, tj = 4;
+  const size_t lds = sizeof(double) * 16 * (size_t)(ti + tj) * dim;
+  if (lds > 65536)
+    GDD_HIP(hipFuncSetAttribute((const void*)k_kpp_dmat_t<ti, tj>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+  const dim3 g((unsigned)((n + 16 * ti - 1) / (16 * ti)), (unsigned)((n + 16 * tj - 1) / (16 * tj)));
+  k_kpp_dmat_t<ti, tj><<<g, 256, lds, s>>>((int)n, dim, XT, xsq, D);
   GDD_LAUNCHED();
   return GDD_OK;
 }
 
-template <bool PIPE>
 __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __restrict__ D, int c) {
   __shared__ float s_d[kBlk];
   __shared__ float s_ch[8 * kChainLd];
@@ -2803,8 +2409,8 @@ __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __rest
     if (tid + 256 * q < n) orow[tid + 256 * q] = r[q];
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 62);
-  kpp1_fold_trial<PIPE>(a, c, t, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv[cq] + t,
-                        a.candw[cq] + (int64_t)t * T);
+  kpp1_fold_trial(a, c, t, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv[cq] + t,
+                  a.candw[cq] + (int64_t)t * T);
 }
 
 // ---- two rounds per launch over the distance table (default for table plans, T <= 8). Workgroup
@@ -2818,12 +2424,9 @@ __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __rest
 // launch (lq); round 1 reads the first centre's slot-0 candidates, so the first launch writes slot 1.
 // Per round this halves the launches and their two leading trips (k_kpp1_dm: 9.2 us per round).
 constexpr int kPairMaxT = 8;  // T * T <= 64: one wave lane per round-(c-1) candidate
-constexpr bool kParChainDefault = false;  // set from the same-box A/B (DESIGN.md §4 k-means++)
 
-// PAR: 512 threads, the exact parallel lane chains (threads 0..255 hold the rows)
-template <bool PIPE, bool PAR = false>
-__global__ __launch_bounds__(PAR ? 512 : 256) void k_kpp1_dm2(Kpp1Args a, const float* __restrict__ D, int c,
-                                                              int lq, int pair) {
+__global__ __launch_bounds__(256) void k_kpp1_dm2(Kpp1Args a, const float* __restrict__ D, int c, int lq,
+                                                  int pair) {
   __shared__ float s_d[kBlk];
   __shared__ float s_ch[8 * kChainLd];
   __shared__ double s_cum[kBlk];
@@ -2887,26 +2490,23 @@ __global__ __launch_bounds__(PAR ? 512 : 256) void k_kpp1_dm2(Kpp1Args a, const 
   if (tid == 0 && (!pair || t2 == 0)) a.candself[lq][w] = ct;
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && g == 0 && c == a.k - 3 + (a.k & 1)), 61);
   // trip 2: the closest distances and the candidate's table row
-  const bool rowt = !PAR || tid < 256;  // the threads that hold the row
   const float* drow = D + ct * n;
   float wi[16], dd[16], r[16];
-  if (rowt) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = min(tid + 256 * q, n - 1);
-      wi[q] = wrow[e];
-      dd[q] = drow[e];
-    }
+  for (int q = 0; q < 16; ++q) {
+    const int e = min(tid + 256 * q, n - 1);
+    wi[q] = wrow[e];
+    dd[q] = drow[e];
   }
 #pragma unroll
   for (int q = 0; q < 16; ++q) r[q] = np_minimum(wi[q], dd[q]);
   if (!pair) {  // the last round alone: as k_kpp1_dm
-    kpp1_fold_trial<PIPE, PAR>(a, c, w, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv[lq] + w,
-                               a.candw[lq] + (int64_t)w * T);
+    kpp1_fold_trial(a, c, w, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv[lq] + w,
+                    a.candw[lq] + (int64_t)w * T);
     return;
   }
-  kpp1_fold_trial<PIPE, PAR>(a, c, w, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot,
-                             t2 == 0 ? a.potv[lq] + w : nullptr, s_cand);
+  kpp1_fold_trial(a, c, w, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot, t2 == 0 ? a.potv[lq] + w : nullptr,
+                  s_cand);
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && g == 0 && c == a.k - 3 + (a.k & 1)), 62);
   // trip 3: round c+1's candidate for slot t2 if w wins, and its table row
@@ -2914,18 +2514,16 @@ __global__ __launch_bounds__(PAR ? 512 : 256) void k_kpp1_dm2(Kpp1Args a, const 
   const int j = w * T + t2;
   if (tid == 0) a.candself2[lq][j] = c1;
   const float* drow2 = D + c1 * n;
-  if (rowt) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) dd[q] = drow2[min(tid + 256 * q, n - 1)];
-    float* orow = a.dist2[lq] + (int64_t)j * n;
+  for (int q = 0; q < 16; ++q) dd[q] = drow2[min(tid + 256 * q, n - 1)];
+  float* orow = a.dist2[lq] + (int64_t)j * n;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      wi[q] = np_minimum(r[q], dd[q]);
-      if (tid + 256 * q < n) orow[tid + 256 * q] = wi[q];
-    }
+  for (int q = 0; q < 16; ++q) {
+    wi[q] = np_minimum(r[q], dd[q]);
+    if (tid + 256 * q < n) orow[tid + 256 * q] = wi[q];
   }
-  kpp1_fold_trial<PIPE, PAR>(a, c + 1, t2, wi, ut2, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv2[lq] + j,
-                             a.candw2[lq] + (int64_t)j * T);
+  kpp1_fold_trial(a, c + 1, t2, wi, ut2, s_d, s_ch, s_cum, s_wave, &s_pot, a.potv2[lq] + j,
+                  a.candw2[lq] + (int64_t)j * T);
 }
 
 // after the last launch of k_kpp1_dm2: its winner(s) and the last centre
@@ -3005,35 +2603,6 @@ __device__ __forceinline__ float sgemv_block_lds(const float* __restrict__ s, co
   return (ql + q1) + (q2 + q3);
 }
 
-// sgemv_block_lds's unit-weight block 0 (entries [0, NB)) with the exact parallel lane chains:
-// this wave's lanes < nl add each chain's head and walk the runs that waves kBigWaves - 4 .. 15
-// (par_chain_lanes<nl>, the natural row at stride nl) published; a failed check: the plain chain
-template <int NL>
-__device__ __forceinline__ float sgemv_block0_par(const float* __restrict__ s, int NB, bool k4x2,
-                                                  int* s_parsync, const ParLane* __restrict__ s_par,
-                                                  const unsigned long long* __restrict__ s_pmask) {
-  const int lane = threadIdx.x & 63;
-  const int h4 = k4x2 ? 0 : (NB & 4);
-  const float* base = s + h4;
-  const int L = lane < NL ? max((NB - h4 - lane + NL - 1) / NL, 0) : 0;
-  float acc0 = 0.f;
-  if (lane < h4) acc0 = __builtin_fmaf(s[lane], 1.0f, acc0);
-  float acc = 0.f;
-  if (lane < NL) acc = chain_unit_lds<NL>(base + lane, min(L, kParHead), acc0);
-  bool ok = waves_wait(s_parsync, 4);
-  if (lane < NL) {
-    const float r = par_chain_walk<NL>(base + lane, lane, NL, acc, s_par, s_pmask, ok);
-    acc = ok ? r : chain_unit_lds<NL>(base + lane, L, acc0);
-  }
-  if (k4x2) {
-    const float a1 = __shfl(acc, 1), a2 = __shfl(acc, 2), a3 = __shfl(acc, 3);
-    return (acc + a1) + (a2 + a3);
-  }
-  const float ql = acc + __shfl(acc, (lane + 4) & 63);
-  const float q1 = __shfl(ql, 1), q2 = __shfl(ql, 2), q3 = __shfl(ql, 3);
-  return (ql + q1) + (q2 + q3);
-}
-
 __device__ __forceinline__ double readlane_f64(double v, int l) {
   const unsigned long long b = __double_as_longlong(v);
   const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
@@ -3055,34 +2624,22 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   __shared__ int s_sidx[kMaxTrials];    // speculative draws: counts (-1: not usable)
   __shared__ double s_lo[kMaxTrials], s_hi[kMaxTrials];  // and their deciding neighbours
   __shared__ unsigned long long s_redo;  // the uniforms the regular draws take
-  constexpr bool kParOk = EPT <= 16;     // EPT = 32: no LDS to spare (132 KB of row)
-  __shared__ ParLane s_par[kParOk ? 256 : 1];  // exact parallel chains of block 0 (r05)
-  __shared__ unsigned long long s_pmask[8];
-  __shared__ int s_parsync;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = a.T;
   const int n = (int)a.n, m1 = (int)a.m1;
   const int t = blockIdx.x;
   const int cq = c & 1, pq = (c - 1) & 1;
   const int nsg = (m1 + kBlk - 1) / kBlk;  // chain waves (4096-entry sgemv_t blocks)
-  const bool k4x2 = (T & 2) && t >= (T & ~3) && t < (T & ~3) + 2;
-  // block 0's lane chains by the exact parallel runs (a.par_chain) when four waves are free of the
-  // chains and the speculative draws, the weights are unit and the chains are long enough to pay
-  const bool par = kParOk && a.par_chain && c >= 1 && a.w == nullptr && min(kBlk, m1) >= kParMinBlock &&
-                   nsg + T <= kBigWaves - 4;
   // speculative draws (r04): waves nsg .. nsg + T - 1 draw round c+1's candidates while waves < nsg
   // run the lane chains, the fp64 total standing in for the potential; checked after it (below)
-  const bool spec = a.spec_search && c >= 1 && c + 1 < a.k && nsg + T <= kBigWaves;
+  const bool spec = c >= 1 && c + 1 < a.k && nsg + T <= kBigWaves;
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 90);
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 1), 95);
   if (tid < kMaxTrials) {
     s_part[tid] = 0;
     s_amb[tid] = 0;
   }
-  if (tid == 0) {
-    s_arr = 0;
-    s_parsync = 0;
-  }
+  if (tid == 0) s_arr = 0;
   // ---- trip 1, every load at once (lane q): round c-1's potential q, this slot's candidate if q
   // won, q's own candidate, round c+1's uniform q
   const double ut = (c + 1 < a.k && lane < T) ? a.uniforms[(int64_t)c * T + lane] : 0.0;
@@ -3171,27 +2728,8 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   // the sgemv_t block terms (rounds >= 1)
   if (c >= 1 && wave < nsg) {
     const int j0 = wave * kBlk;
-    float vb;
-    if constexpr (kParOk) {
-      if (par && wave == 0)
-        vb = k4x2 ? sgemv_block0_par<4>(s_row, min(kBlk, m1), true, &s_parsync, s_par, s_pmask)
-                  : sgemv_block0_par<8>(s_row, min(kBlk, m1), false, &s_parsync, s_par, s_pmask);
-      else
-        vb = sgemv_block_lds(s_row, a.w, j0, min(kBlk, m1 - j0), t, T);
-    } else {
-      vb = sgemv_block_lds(s_row, a.w, j0, min(kBlk, m1 - j0), t, T);
-    }
+    const float vb = sgemv_block_lds(s_row, a.w, j0, min(kBlk, m1 - j0), t, T);
     if (lane == 0) s_vb[wave] = vb;
-  } else if (par && wave >= kBigWaves - 4) {  // block 0's runs for the walk above
-    if constexpr (kParOk) {
-      const int NB = min(kBlk, m1), h4 = k4x2 ? 0 : (NB & 4);
-      const int p = tid - 64 * (kBigWaves - 4);
-      if (k4x2)
-        par_chain_lanes<4>(p, s_row + h4, s_row, 4, h4, NB, s_par, s_pmask);
-      else
-        par_chain_lanes<8>(p, s_row + h4, s_row, 8, h4, NB, s_par, s_pmask);
-      waves_arrive(&s_parsync);
-    }
   } else if (spec && wave - nsg < T) {
     // searchsorted_left(cum, u * pot_s), pot_s = fp32(fp64 total), without the rounding check (the
     // check after the potential decides): the wave totals' running sum finds the group of 64
@@ -3539,10 +3077,9 @@ extern "C" size_t gdd_kmeans_plusplus_ws_bytes_k(int64_t n, int dim, int n_trial
 constexpr int64_t kDmBigMax = 32768;
 // largest n for k_kpp1_big (one workgroup per trial): beyond ~16K points one CU's share of the row
 // traffic (two rows in, one out per round) outweighs the per-block rounds' extra launch work
-// (Ali-Display users, 17,730 points: 35.2 vs 23.5 us per round); GDD_KPP_BIG1_MAX overrides (tests)
+// (Ali-Display users, 17,730 points: 35.2 vs 23.5 us per round); GDD_FORCE=kpp_big1_max=N overrides
 int64_t kpp_big1_max() {
-  const char* e = getenv("GDD_KPP_BIG1_MAX");
-  const int64_t v = e ? atoll(e) : 16384;
+  const int64_t v = (int64_t)forced_value("kpp_big1_max", 16384);
   return v < kBig1Max ? v : kBig1Max;
 }
 // the table costs n^2 dim fp64 fmas once (~0.45 ms at 6,040 x 64, i.e. ~5e12 fma/s) and saves each
@@ -3555,8 +3092,8 @@ bool kpp_table_pays(int64_t n, int dim, int k) {
 }
 bool kpp_big_table(int64_t n, int dim, int T, int k) {
   if (n <= kBlk || n > kDmBigMax || dim > kDmX || T < 2 || k < kDmMinK) return false;
-  if (getenv("GDD_KPP_NO_TABLE") != nullptr) return false;
-  if (!kpp_table_pays(n, dim, k) && getenv("GDD_KPP_FORCE_TABLE") == nullptr) return false;
+  if (forced("kpp_no_table")) return false;
+  if (!kpp_table_pays(n, dim, k) && !forced("kpp_force_table")) return false;
   return skl_all_seq(n, T, dim, skl_batch_size(T, n, dim));
 }
 // the single-block table (n <= 4096, at most 64 MiB): built from kDmMinK centres on
@@ -3633,13 +3170,9 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   b1.counter = cv.take<unsigned>((size_t)std::max(k, 1) * T);  // rounds c < k, trial t
   float* XT = (n <= kBlk || n * (int64_t)dim < INT_MAX) ? cv.take<float>((size_t)n * dim) : nullptr;
   float* Dbig = kpp_big_table(n, dim, T, k) ? cv.take<float>((size_t)n * n) : nullptr;
-  // the per-block table rounds keep each round's block prefixes (r05; GDD_KPP_STORE_PFX=0: recompute)
-  {
-    const char* pe = getenv("GDD_KPP_STORE_PFX");
-    const bool big1 = n <= kpp_big1_max() && T >= 2 && getenv("GDD_KPP_NO_BIG1") == nullptr;
-    const bool keep_pfx = Dbig && !big1 && !(pe && pe[0] == '0');
-    for (int q = 0; q < 2; ++q) a.pfx[q] = keep_pfx ? cv.take<double>((size_t)n * T) : nullptr;
-  }
+  // the per-block table rounds keep each round's block prefixes for the next round's count (r05)
+  const bool big1 = n <= kpp_big1_max() && T >= 2 && !forced("kpp_no_big1");
+  for (int q = 0; q < 2; ++q) a.pfx[q] = (Dbig && !big1) ? cv.take<double>((size_t)n * T) : nullptr;
   float* Dm = kpp_small_table(n, dim, T, k) ? cv.take<float>((size_t)n * n) : nullptr;
   if (Dm) {
     for (int q = 0; q < 2; ++q) {
@@ -3668,15 +3201,9 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   a.indices = indices;
   a.plan = SklPlan{n, skl_batch_size(T, n, dim), T, dim, 0, 0};
   a.plan.all_seq = skl_all_seq(n, T, dim, a.plan.B) ? 1 : 0;
-  {  // cum_tol's mode: GDD_KPP_EXACT=0 (never replay; tests only) / 2 (always replay)
+  {  // cum_tol's mode (diagnostic): GDD_KPP_EXACT=0 never replays (tests only), 2 always replays
     const char* ex = getenv("GDD_KPP_EXACT");
     a.exact = ex ? atoi(ex) : 1;
-    const char* pce = getenv("GDD_KPP_PAR_CHAIN");
-    a.par_chain = (pce ? pce[0] == '1' : kParChainDefault) ? 1 : 0;
-    // A/B bits (r05): 1 block totals, 2 fold tail, 4 candidates, 8 the barrier-free wave fold,
-    // 32 the block prefix beside the lane chain
-    const char* pre = getenv("GDD_KPP_ROUND_PRELOAD");
-    a.preload = pre ? atoi(pre) : (4 | 8 | 32);
   }
   const SklPlan p1{n, skl_batch_size(1, n, dim), 1, dim, 0, 0};
   const size_t lds = sizeof(double) * (size_t)dim + sizeof(float) * (kBlk + kChainPad);  // + chain read-ahead
@@ -3722,11 +3249,6 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     b1.indices = indices;
     b1.plan = a.plan;
     b1.exact = a.exact;
-    b1.bsearch = getenv("GDD_KPP_BSEARCH") != nullptr ? 1 : 0;
-    {
-      const char* ss = getenv("GDD_KPP_SPEC_SEARCH");  // 0 off; default on for T <= 12
-      b1.spec_search = (ss && ss[0] == '0') ? 0 : 1;
-    }
     if (seq) {
       k_kpp_xt<<<dim3((unsigned)((n + kXtTile - 1) / kXtTile), (unsigned)((dim + kXtTile - 1) / kXtTile)), 256, 0,
                s>>>((int)n, dim, X, XT);
@@ -3740,14 +3262,9 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
     k_kpp1_pick<<<1, kThr, 0, s>>>(b1, 0);
     GDD_LAUNCHED();
     // the distance table pays once the rounds it saves (~3 us each) cover its one-off build
-    if (seq && Dm && k >= kDmMinK && getenv("GDD_KPP_NO_TABLE") == nullptr) {
+    if (seq && Dm && k >= kDmMinK && !forced("kpp_no_table")) {
       if (const int rc = launch_kpp_dmat(n, dim, X, XT, xsq, Dm, s)) return rc;
-      const bool plain = getenv("GDD_KPP_CHAIN_PLAIN") != nullptr;
-      // GDD_KPP_PAR_CHAIN: 1 = the exact parallel lane chains (512-thread pair launches), 0 = the
-      // sequential lane chains
-      const char* pce = getenv("GDD_KPP_PAR_CHAIN");
-      const bool par_chain = pce ? pce[0] == '1' : kParChainDefault;
-      if (T <= kPairMaxT && getenv("GDD_KPP_SINGLE_ROUND") == nullptr) {
+      if (T <= kPairMaxT && !forced("kpp_single_round")) {
         // two rounds per launch (a trailing odd round alone). The chain's arguments are fixed by
         // (b1, Dm, k): it is replayed as one recorded graph (replay_or_run) — every launch then
         // starts ~1 us sooner after the previous one
@@ -3757,12 +3274,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
             lq = ((c - 1) / 2 + 1) & 1;
             pair = c + 1 < k ? 1 : 0;
             const unsigned grid = (unsigned)(pair ? T * T : T);
-            if (plain)
-              k_kpp1_dm2<false><<<grid, 256, 0, cs>>>(b1, Dm, c, lq, pair);
-            else if (par_chain)
-              k_kpp1_dm2<true, true><<<grid, 512, 0, cs>>>(b1, Dm, c, lq, pair);
-            else
-              k_kpp1_dm2<true><<<grid, 256, 0, cs>>>(b1, Dm, c, lq, pair);
+            k_kpp1_dm2<<<grid, 256, 0, cs>>>(b1, Dm, c, lq, pair);
             GDD_LAUNCHED();
           }
           k_kpp1_final2<<<1, 64, 0, cs>>>(b1, k - 1, lq, pair);
@@ -3777,21 +3289,16 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
         struct {
           Kpp1Args b1;
           const float* Dm;
-          int k, plain, par;
+          int k;
         } key;
         std::memset(&key, 0, sizeof(key));
         key.b1 = b1;
         key.Dm = Dm;
         key.k = k;
-        key.plain = plain ? 1 : 0;
-        key.par = par_chain ? 1 : 0;
         return replay_or_run("kpp_pair_chain", &key, sizeof(key), s, chain);
       }
       for (int c = 1; c < k; ++c) {
-        if (plain)
-          k_kpp1_dm<false><<<(unsigned)T, 256, 0, s>>>(b1, Dm, c);
-        else
-          k_kpp1_dm<true><<<(unsigned)T, 256, 0, s>>>(b1, Dm, c);
+        k_kpp1_dm<<<(unsigned)T, 256, 0, s>>>(b1, Dm, c);
         GDD_LAUNCHED();
       }
       k_kpp1_final<<<1, 64, 0, s>>>(b1, k - 1);
@@ -3804,7 +3311,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       return GDD_OK;
     }
     const dim3 gf((unsigned)((n + kFPts - 1) / kFPts), (unsigned)T);
-    if (dim <= kMaxDimF && gf.x * gf.y <= 256 && getenv("GDD_KPP_TWO_LAUNCH") == nullptr) {
+    if (dim <= kMaxDimF && gf.x * gf.y <= 256 && !forced("kpp_two_launch")) {
       // one launch per round: distances, then each trial's last workgroup folds it (no fences)
       GDD_HIP(hipMemsetAsync(b1.counter, 0, sizeof(unsigned) * (size_t)k * T, s));
       for (int c = 1; c < k; ++c) {
@@ -3841,7 +3348,7 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   // blocks to fill the chip (products' 2.45M points: 598 blocks). With few blocks the per-(block,
   // trial) rounds win (6,040 points: 22 vs 69 us per round; 40,000: 47 vs 84).
   const bool split = seq && a.XT && T >= 2 && T <= kSplitMaxT && lds_split <= 150 * 1024 &&
-                     nblk >= kSplitMinBlocks && getenv("GDD_KPP_FUSED_ROUND") == nullptr;
+                     nblk >= kSplitMinBlocks && !forced("kpp_no_split");
   if (split) {
     void (*dists)(KppArgs, int) = nullptr;
     switch (T) {
@@ -3871,8 +3378,8 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   if (Dbig && seq && a.XT) {  // the distances once per fit (~n^2 dim fp64 fmas), then table rounds
     if (const int rc = launch_kpp_dmat(n, dim, X, a.XT, xsq, Dbig, s)) return rc;
     a.D = Dbig;
-    if (n <= kpp_big1_max() && T >= 2 && getenv("GDD_KPP_NO_BIG1") == nullptr) {
-      // one 1024-thread workgroup per trial (k_kpp1_big); GDD_KPP_NO_BIG1 keeps the per-block rounds
+    if (big1) {
+      // one 1024-thread workgroup per trial (k_kpp1_big); GDD_FORCE=kpp_no_big1 keeps the per-block rounds
       b1.n = n;
       b1.m1 = a.m1;
       b1.dim = dim;
@@ -3889,12 +3396,6 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       b1.indices = indices;
       b1.plan = a.plan;
       b1.exact = a.exact;
-      {
-        const char* ss = getenv("GDD_KPP_SPEC_SEARCH");  // 0 off (the regular draws)
-        b1.spec_search = (ss && ss[0] == '0') ? 0 : 1;
-        const char* pce = getenv("GDD_KPP_PAR_CHAIN");
-        b1.par_chain = (pce ? pce[0] == '1' : kParChainDefault) ? 1 : 0;
-      }
       void (*big)(Kpp1Args, const float*, int) = nullptr;
       int ept = 0;
       if (n <= (int64_t)kBigThr * 8) {

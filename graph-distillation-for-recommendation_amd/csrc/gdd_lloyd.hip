@@ -248,7 +248,7 @@ size_t group_ws(int64_t n, int k) {
 int group_dev(int64_t n, const int32_t* labels, int k, int32_t* perm, int32_t* offsets, void* ws,
               size_t ws_bytes, const int32_t* stop, int step_i, hipStream_t s) {
   Carver cv(ws, ws_bytes);
-  if (n <= kGrpSmallMaxN && k <= kGrpSmallMaxK && getenv("GDD_GROUP_SPLIT") == nullptr) {
+  if (n <= kGrpSmallMaxN && k <= kGrpSmallMaxK && !forced("group_split")) {
     int bits = 1;
     while ((1ll << bits) < (long long)k) ++bits;
     const size_t lds = sizeof(int32_t) * (size_t)kGrpWaves * k;
@@ -764,9 +764,8 @@ int fold_launch_one(const FoldArgs& a0, int count, bool mean, hipStream_t s) {
   a.Rmax = std::max(a.R, a.R_big);
   if (count == 0) return GDD_OK;
   dim3 grid(nsl, (unsigned)count);
-  {  // unit-weight Lloyd sums over 16-byte aligned rows: the column-major form (GDD_FOLD_CM=0: off)
-    const char* ce = getenv("GDD_FOLD_CM");
-    if (!mean && !weighted && !small && vec && a.fw_max <= 64 && a.fw_big <= 64 && !(ce && ce[0] == '0')) {
+  {  // unit-weight Lloyd sums over 16-byte aligned rows: the column-major form
+    if (!mean && !weighted && !small && vec && a.fw_max <= 64 && a.fw_big <= 64) {
       const size_t bufsz = std::max<size_t>((size_t)a.fw_max * (a.R + 4), (size_t)a.fw_big * (a.R_big + 4));
       const size_t lds_cm = sizeof(float) * 2 * bufsz;
       GDD_HIP(hipFuncSetAttribute((const void*)k_seg_fold_cm, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1071,175 +1070,6 @@ __global__ __launch_bounds__(256) void k_lloyd_converge(int k, const float* __re
     st->iter = it;
     __hip_atomic_store(&st->stop_at, step_i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-}
-
-// The update step of a small Lloyd problem in ONE workgroup (r04, opt-in: see lloyd_update_small): the empty-cluster check of step
-// 2i (check != 0), then step 2i+1's _average_centers + shifts, labels-changed and convergence test —
-// the operations of k_lloyd_check_empty, k_avg_centers, k_lloyd_changed and k_lloyd_converge, in
-// their order, on one CU instead of four dependent launches (recsys shapes: ~4 us each, latency).
-// Empty clusters: with the check they stop the loop at step 2i+1 exactly as k_lloyd_check_empty
-// (nothing else runs); without it (the iteration resumed after the host's relocation) the heaviest
-// cluster donates its row as in k_avg_centers: raw to empties before it, averaged to those after.
-// skl_sqdist with its operands read 32 entries at a time (every load of a chunk in flight before the
-// chunk's arithmetic, which is skl_sqdist's: groups of four, then the tail)
-__device__ __forceinline__ float skl_sqdist_staged(const float* __restrict__ a, const float* __restrict__ b,
-                                                   int dim) {
-  float r = 0.f;
-  int j = 0;
-  for (; j + 32 <= dim; j += 32) {
-    float x[32], y[32];
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      x[q] = a[j + q];
-      y[q] = b[j + q];
-    }
-#pragma unroll
-    for (int q = 0; q < 32; q += 4) {
-      const float d0 = x[q] - y[q], d1 = x[q + 1] - y[q + 1], d2 = x[q + 2] - y[q + 2], d3 = x[q + 3] - y[q + 3];
-      r = r + (((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
-    }
-  }
-  for (; j + 4 <= dim; j += 4) {
-    const float d0 = a[j] - b[j], d1 = a[j + 1] - b[j + 1], d2 = a[j + 2] - b[j + 2], d3 = a[j + 3] - b[j + 3];
-    r = r + (((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
-  }
-  for (; j < dim; ++j) {
-    const float d0 = a[j] - b[j];
-    r = r + d0 * d0;
-  }
-  return r;
-}
-
-constexpr int kUpdThr = 1024;
-constexpr int64_t kUpdMaxN = 131072;      // labels compared by one workgroup
-constexpr int64_t kUpdMaxKD = 262144;     // centre entries averaged by one workgroup
-__global__ __launch_bounds__(kUpdThr) void k_lloyd_update_small(
-    int64_t n, int k, int dim, float* __restrict__ C_new, const float* __restrict__ wsum,
-    const float* __restrict__ C_old, float* __restrict__ shift, const int32_t* __restrict__ labels,
-    int32_t* __restrict__ old, double tol, LloydState* st, int it, int check, int step_i) {
-  if (stopped(&st->stop_at, step_i)) return;
-  __shared__ float sq[kShiftLds];
-  __shared__ float s_alpha[kShiftLds];
-  __shared__ PwLds pl;
-  __shared__ float s_bv[kUpdThr / 64];
-  __shared__ int s_bi[kUpdThr / 64];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // heaviest cluster (first maximum) and whether any cluster is empty
-  float bv = -1.f;
-  int bi = INT_MAX, any_empty = 0;
-  for (int j = tid; j < k; j += kUpdThr) {
-    const float v = wsum[j];
-    if (v > bv) {
-      bv = v;
-      bi = j;
-    }
-    any_empty |= !(v > 0.f);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(bv, o);
-    const int oi = __shfl_xor(bi, o);
-    if (ov > bv || (ov == bv && oi < bi)) {
-      bv = ov;
-      bi = oi;
-    }
-  }
-  if (lane == 0) {
-    s_bv[wave] = bv;
-    s_bi[wave] = bi;
-  }
-  any_empty = __syncthreads_or(any_empty);
-  bv = s_bv[0];
-  bi = s_bi[0];
-  for (int q = 1; q < kUpdThr / 64; ++q)
-    if (s_bv[q] > bv || (s_bv[q] == bv && s_bi[q] < bi)) {
-      bv = s_bv[q];
-      bi = s_bi[q];
-    }
-  if (any_empty && check) {  // k_lloyd_check_empty: the host relocates, then resumes
-    if (tid == 0) {
-      st->reason = 3;
-      st->iter = it;
-      __hip_atomic_store(&st->stop_at, step_i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return;
-  }
-  // _average_centers: empties first take the donor's row (raw, or averaged if the donor comes first)
-  if (any_empty) {
-    const float ad = (float)(1.0 / (double)wsum[bi]);
-    const int64_t db = (int64_t)bi * dim;
-    for (int j = 0; j < k; ++j) {
-      if (wsum[j] > 0.f) continue;
-      const int64_t jb = (int64_t)j * dim;
-      for (int f = tid; f < dim; f += kUpdThr) {
-        const float raw = C_new[db + f];
-        C_new[jb + f] = bi < j ? raw * ad : raw;
-      }
-    }
-    __syncthreads();
-  }
-  // every row's scale first (`1.0 / weight` is a C double division; -1: an empty row, left as is),
-  // then the rows in batches of 8 entries per thread with every load issued before the stores
-  for (int c = tid; c < k; c += kUpdThr) {
-    const float wc = wsum[c];
-    s_alpha[c] = wc > 0.f ? (float)(1.0 / (double)wc) : -1.f;
-  }
-  __syncthreads();
-  const int64_t KD = (int64_t)k * dim;
-  for (int64_t e0 = tid; e0 < KD; e0 += 8 * kUpdThr) {
-    float x[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int64_t e = e0 + (int64_t)u * kUpdThr;
-      x[u] = e < KD ? C_new[e] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int64_t e = e0 + (int64_t)u * kUpdThr;
-      if (e < KD) {
-        const float al = s_alpha[(int)(e / dim)];
-        if (al >= 0.f) C_new[e] = x[u] * al;
-      }
-    }
-  }
-  // labels changed (np.array_equal(labels, labels_old)), labels_old = labels
-  int diff = 0;
-  for (int64_t i = tid; i < n; i += kUpdThr) {
-    const int32_t a = labels[i];
-    if (a != old[i]) {
-      diff = 1;
-      old[i] = a;
-    }
-  }
-  const int changed = __syncthreads_or(diff) | st->changed;  // the barrier also publishes C_new
-  for (int c = tid; c < k; c += kUpdThr) {
-    const int64_t cb = (int64_t)c * dim;
-    const float sh = sqrtf(skl_sqdist_staged(C_new + cb, C_old + cb, dim));
-    if (shift) shift[c] = sh;
-    sq[c] = sh * sh;
-  }
-  __syncthreads();
-  float tot = 0.f;
-  if (changed != 0) tot = pw_sum_block(sq, k, pl);  // every thread takes part
-  __syncthreads();
-  if (tid != 0) return;
-  int reason = 0;
-  if (changed == 0) reason = 1;
-  else if ((double)tot <= tol) reason = 2;
-  st->changed = 0;
-  st->done = it + 1;
-  if (reason) {
-    st->reason = reason;
-    st->iter = it;
-    __hip_atomic_store(&st->stop_at, step_i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-__host__ __forceinline__ bool lloyd_update_small(int64_t n, int dim, int k) {
-  // opt-in (GDD_LLOYD_UPDATE_SMALL=1): measured slower than the four launches at the recsys shapes
-  // (ML-1M users 81.5 vs 71.5 us per iteration, profiles/r04_lloyd_small.txt) — one CU runs phases the
-  // four launches spread over the chip
-  return getenv("GDD_LLOYD_UPDATE_SMALL") != nullptr && n <= kUpdMaxN && k <= kShiftLds && (int64_t)k * dim <= kUpdMaxKD;
 }
 
 // ((X - C[labels])**2).sum(axis=1) in numpy's order: fp32 squares, pairwise per contiguous row
@@ -1616,9 +1446,8 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
   double* sep = lw.sep;
   double* glob = lw.glob;
   int64_t* count = lw.count;
-  // bounded E-steps (GDD_LLOYD_PRUNE=0: every row every iteration), from the run's first E-step on
-  const char* pe = getenv("GDD_LLOYD_PRUNE");
-  const bool prune = !(pe && pe[0] == '0') && lloyd_prune_ok(dim, k);
+  // bounded E-steps (GDD_FORCE=lloyd_no_prune: every row every iteration), from the run's first E-step on
+  const bool prune = !forced("lloyd_no_prune") && lloyd_prune_ok(dim, k);
   const int prune_first = resume ? it0 + 1 : it0;
   const double kappa = (2.0 * dim + 8.0) * kEps32;
   const unsigned fgrid = std::min<unsigned>(blocks_of(n), 2048);
@@ -1634,14 +1463,13 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
   if (!resume) GDD_HIP(hipMemsetAsync(&st->changed, 0, sizeof(int32_t), s));
   FoldArgs fa{dim, 0, 0, 0, 0, 0, 0, 0, X, nullptr, perm, offsets, nullptr, wsum, nullptr, 0, &st->stop_at, 0};
   fa.avg_rows = n / k;
-  const float* Xpad = nullptr;  // the padded copy for the bounded E-step's row lists (GDD_ESTEP_PAD=0: X)
+  const float* Xpad = nullptr;  // the padded copy for the bounded E-step's row lists (estep_no_pad: X)
   int dpad = 0;
-  {  // the fold's zero-padded copy of X at the end of the workspace (GDD_FOLD_PAD=0: gather X itself)
-    const char* pe2 = getenv("GDD_FOLD_PAD");
+  {  // the fold's zero-padded copy of X at the end of the workspace (fold_no_pad: gather X itself)
     const int dp = fold_pad_dim(n, dim);
     const size_t base = gdd_kmeans_lloyd_ws_bytes(n, dim, k) - fold_pad_ws(n, dim);
     const uintptr_t at = (reinterpret_cast<uintptr_t>(ws) + base + 255) & ~uintptr_t(255);
-    if (dp && !(pe2 && pe2[0] == '0') && ws_bytes >= base + fold_pad_ws(n, dim)) {
+    if (dp && !forced("fold_no_pad") && ws_bytes >= base + fold_pad_ws(n, dim)) {
       float* Xp = reinterpret_cast<float*>(at);
       const int64_t total = n * (dp / 4);
       k_pad_rows<<<(unsigned)std::min<int64_t>((total + 255) / 256, 8192), 256, 0, s>>>(n, dim, dp, X, Xp);
@@ -1649,21 +1477,18 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
       fa.X = Xp;
       fa.dim = dp;
       fa.out_dim = dim;
-      const char* pe3 = getenv("GDD_ESTEP_PAD");
-      if (!(pe3 && pe3[0] == '0')) {
+      if (!forced("estep_no_pad")) {
         Xpad = Xp;
         dpad = dp;
       }
     }
   }
-  {  // M-step: clusters above GDD_FOLD_SLICE x the mean size (default 1.5; 0: off) fold in slices
-    const char* fe = getenv("GDD_FOLD_SLICE");
-    const double f = fe ? atof(fe) : 1.5;
+  {  // M-step: clusters above fold_slice x the mean size (default 1.5; 0: off) fold in slices
+    const double f = forced_value("fold_slice", 1.5);
     const double rows = f * (double)n / (double)k;
     fa.big_rows = f > 0.0 ? (int)std::min<double>(std::max(rows, 4096.0), (double)INT_MAX) : 0;
   }
   const unsigned cgrid = std::min<unsigned>(blocks_of(n), 2048);
-  const bool small_update = lloyd_update_small(n, dim, k);
   auto enqueue = [&](int i, bool phase_a) -> int {
     float* cin = (i & 1) ? C1 : C0;
     float* cout = (i & 1) ? C0 : C1;
@@ -1702,14 +1527,7 @@ extern "C" int gdd_kmeans_lloyd_run(int64_t n, int dim, const float* X, int k, f
       fa.step_i = sa;
       rc = fold_launch(fa, k, false, s);
       if (rc) return rc;
-      // the empty-cluster check rides in the average's launch (check_st) unless the one-workgroup
-      // update (opt-in) does it
-    }
-    if (small_update) {  // the check (when the E-step ran), average, changed, convergence: one launch
-      k_lloyd_update_small<<<1, kUpdThr, 0, s>>>(n, k, dim, cout, wsum, cin, shift, labels, labels_old, tol,
-                                                 st, i, phase_a ? 1 : 0, sb);
-      GDD_LAUNCHED();
-      return GDD_OK;
+      // the empty-cluster check rides in the average's launch (check_st)
     }
     k_avg_centers<<<k, 64, 0, s>>>(k, dim, cout, wsum, cin, shift, &st->stop_at, sb, phase_a ? st : nullptr, i);
     GDD_LAUNCHED();
@@ -1821,8 +1639,7 @@ extern "C" int gdd_lloyd_estep(int64_t n, int64_t r0, int64_t r1, int dim, const
   const int64_t m = r1 - r0;
   if (m == 0) return GDD_OK;
   const float* Xr = X + r0 * dim;
-  const char* pe = getenv("GDD_LLOYD_PRUNE");
-  const bool prune = !(pe && pe[0] == '0') && lloyd_prune_ok(dim, k);
+  const bool prune = !forced("lloyd_no_prune") && lloyd_prune_ok(dim, k);
   if (!prune) return kmeans_assign_dev(m, dim, Xr, k, C, lw.cn2, labels + r0, lw.keys, &st->stop_at, sa, s);
   const double kappa = (2.0 * dim + 8.0) * kEps32;
   if (first) {  // the rows' norms, once per fit (the bounds start at this E-step)
@@ -1864,8 +1681,7 @@ extern "C" int gdd_lloyd_mstep(int64_t n, int dim, const float* X, const int32_t
   if (f1 > f0) {
     FoldArgs fa{f1 - f0, 0, 0, 0, 0, 0, 0, 0, X + f0, nullptr, lw.perm, lw.offsets, sums_cols, wsum,
                 nullptr, 0, &st->stop_at, sa, dim, n / k};
-    const char* fe = getenv("GDD_FOLD_SLICE");
-    const double fs = fe ? atof(fe) : 1.5;
+    const double fs = forced_value("fold_slice", 1.5);
     const double rows = fs * (double)n / (double)k;
     fa.big_rows = fs > 0.0 ? (int)std::min<double>(std::max(rows, 4096.0), (double)INT_MAX) : 0;
     rc = fold_launch(fa, k, false, s);
@@ -1894,12 +1710,6 @@ extern "C" int gdd_lloyd_update(int64_t n, int dim, int k, const float* parts, i
     k_assemble_cols<<<(unsigned)std::min<int64_t>((total + 255) / 256, 2048), 256, 0, s>>>(
         k, dim, fw, parts, C_new, &st->stop_at, sb);
     GDD_LAUNCHED();
-  }
-  if (lloyd_update_small(n, dim, k)) {  // one launch (the empty check ran in gdd_lloyd_mstep)
-    k_lloyd_update_small<<<1, kUpdThr, 0, s>>>(n, k, dim, C_new, wsum, C_old, shift, labels, labels_old, tol,
-                                               st, it, 0, sb);
-    GDD_LAUNCHED();
-    return GDD_OK;
   }
   k_avg_centers<<<k, 64, 0, s>>>(k, dim, C_new, wsum, C_old, shift, &st->stop_at, sb);
   GDD_LAUNCHED();

@@ -312,17 +312,9 @@ struct Plan {
   size_t sort_bytes;
 };
 
-// work-list schedule: 1 = longest rows first (default), 0 = row order (GDD_HOP_SCHED overrides).
-// Items are independent (each writes its own row or partial slot), so the schedule changes only
+// work-list schedule: longest rows first (r04; row order measured slower). Items are independent (each writes its own row or partial slot), so the schedule changes only
 // timing, never a result. Longest first: the long items of a power-law graph start early instead of
 // trailing the grid (arxiv shape 220 -> 204 us per hop, products 9.7 -> 9.5 ms).
-int hop_sched() {
-  static int v = [] {
-    const char* e = getenv("GDD_HOP_SCHED");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
 
 inline int64_t max_items_for(int64_t n, int64_t nnz) { return n + nnz / kSeg + 1; }
 inline int64_t max_parts_for(int64_t nnz) { return 2 * (nnz / kSeg) + 2; }
@@ -376,7 +368,7 @@ int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv,
   const unsigned gb = (unsigned)((n + 255) / 256);
   GDD_HIP(hipMemsetAsync(pl.counts, 0, sizeof(int32_t) * 4, s));
   const int32_t* order = nullptr;
-  if (hop_sched() == 1) {
+  {
     k_len_keys<<<gb, 256, 0, s>>>(n, rowptr, tmp[4], tmp[5]);
     GDD_LAUNCHED();
     // rows grouped by key, stable: the same order as a stable sort of (key, row) pairs
@@ -435,32 +427,19 @@ void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float s
         rm.y, rm.prev);
 }
 
-// lanes per item: the whole row up to 64 lanes, or (GDD_HOP_LANES=8/16/32, V = 4) narrower groups
-// that split the row into XCD slices
-int hop_lanes_override() {
-  static int v = [] {
-    const char* e = getenv("GDD_HOP_LANES");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
+// lanes per item: the whole row up to 64 lanes, or narrower groups that split the row into XCD slices
 
 template <int V>
 void launch_hop_v(const Plan& pl, const int32_t* col, const float* val, float scale, int d,
                   const float* x, float* y, float* acc, float acc_scale, const float* acc_init,
                   const float* acc_prev, RowMaps rm, hipStream_t s) {
   const int lanes = (d + V - 1) / V;
-  const int ov = hop_lanes_override();
-  if (ov == 8)
-    return launch_hop_vg<V, 8>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, rm, s);
-  if (ov == 16)
-    return launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, rm, s);
   // 29..32 lanes of float4 (d in (112, 128]): two XCD slices of 16 lanes each, so an XCD's L2 caches
   // half of every gathered row (measured at the arxiv shape, d = 128: 202 vs 208 us per hop; the
   // gathers' L2 hit rate rises, the instruction overhead of the narrower groups stays small). With
   // fewer lanes the second slice idles most of its lanes while reading the whole column/value stream
   // again: products' d = 100 (25 lanes) runs 9.5 ms per hop in one 32-lane group vs 12.4 sliced.
-  if (lanes <= 16 || (V == 4 && lanes > 28 && lanes <= 32 && ov != 32))
+  if (lanes <= 16 || (V == 4 && lanes > 28 && lanes <= 32))
     launch_hop_vg<V, 16>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, rm, s);
   else if (lanes <= 32)
     launch_hop_vg<V, 32>(pl, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, rm, s);

@@ -6,6 +6,7 @@
 
 #include <cstdlib>
 #include <mutex>
+#include <string>
 #include <vector>
 
 namespace gdd {
@@ -68,6 +69,36 @@ int sort_pairs_i32(const int32_t* keys_in, int32_t* keys_out, const int32_t* val
 }
 
 // ---- launch-sequence replay --------------------------------------------------------------------
+namespace {
+// GDD_FORCE's token `name` (or `name=value`): its value text, nullptr if absent
+bool force_token(const char* name, std::string* value) {
+  const char* e = getenv("GDD_FORCE");
+  if (e == nullptr) return false;
+  const std::string all(e), want(name);
+  size_t p = 0;
+  while (p <= all.size()) {
+    size_t q = all.find(',', p);
+    if (q == std::string::npos) q = all.size();
+    const std::string tok = all.substr(p, q - p);
+    const size_t eq = tok.find('=');
+    if (tok.substr(0, eq) == want) {
+      if (value) *value = eq == std::string::npos ? std::string() : tok.substr(eq + 1);
+      return true;
+    }
+    p = q + 1;
+  }
+  return false;
+}
+}  // namespace
+
+bool forced(const char* token) { return force_token(token, nullptr); }
+
+double forced_value(const char* token, double dflt) {
+  std::string v;
+  if (!force_token(token, &v) || v.empty()) return dflt;
+  return atof(v.c_str());
+}
+
 namespace {
 struct GraphEntry {
   std::string key;  // site, device, caller key

@@ -385,18 +385,9 @@ int64_t seg_len(int64_t n) {
   return seg;
 }
 
-bool use_plain_fold() {
-  static const bool v = [] {
-    const char* e = getenv("GDD_INERTIA_SEQ");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
 
 }  // namespace
 
-// internal (gdd_kmeans.hip keeps the one-thread fold for GDD_INERTIA_SEQ=1)
-int inertia_plain_launch(int64_t n, const float* sq, const float* w, float* out, hipStream_t s);
 
 }  // namespace gdd
 
@@ -406,7 +397,6 @@ extern "C" int gdd_inertia(int64_t n, const float* sq_dist, const float* w, floa
                            gdd_stream_t stream) {
   GDD_REQUIRE(n >= 0 && out && (n == 0 || sq_dist), "inertia: bad arguments");
   hipStream_t s = to_hip(stream);
-  if (use_plain_fold()) return inertia_plain_launch(n, sq_dist, w, out, s);
   k_seqsum_walk<<<1, kWalkThreads, 0, s>>>(n, sq_dist, w, out);
   GDD_LAUNCHED();
   return GDD_OK;
@@ -422,7 +412,6 @@ extern "C" int gdd_inertia_ws(int64_t n, const float* sq_dist, const float* w, f
                               size_t ws_bytes, gdd_stream_t stream) {
   GDD_REQUIRE(n >= 0 && out && (n == 0 || sq_dist), "inertia_ws: bad arguments");
   hipStream_t s = to_hip(stream);
-  if (use_plain_fold()) return inertia_plain_launch(n, sq_dist, w, out, s);
   const int64_t seg = seg_len(n);
   const int64_t nseg = (n + seg - 1) / seg;
   if (nseg <= 2) {  // short: the chunked walk alone

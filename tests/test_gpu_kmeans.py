@@ -12,6 +12,14 @@ from gdd import _lib, synth  # noqa: E402
 from gdd.kmeans import _Ops  # noqa: E402
 
 
+def force(monkeypatch, *tokens):
+    """GDD_FORCE (gdd_common.hpp): force the listed paths for the next calls (none: the defaults)."""
+    if tokens:
+        monkeypatch.setenv("GDD_FORCE", ",".join(tokens))
+    else:
+        monkeypatch.delenv("GDD_FORCE", raising=False)
+
+
 def bits(a):
     return np.ascontiguousarray(a).view(np.uint32)
 
@@ -272,12 +280,12 @@ def test_center_columns_parallel_matches_numpy(monkeypatch, name, n, dim, X):
     """gdd_center_columns_ws (r05): from 65,536 rows the column chains run in the exact parallel form
     (per-segment transducers of the sequential fp32 sum of signed terms, gdd_colsum.hip; CPU model in
     tests/test_signed_chain_model.py): mean, var and X - mean bit for bit against numpy and against
-    the sequential chains (GDD_CENTER_PAR=0)."""
+    the sequential chains (GDD_FORCE=center_seq)."""
     lib = _lib.device_lib()
     Xd = torch.from_numpy(X).cuda()
     res = []
     for par in ("1", "0"):
-        monkeypatch.setenv("GDD_CENTER_PAR", par)
+        force(monkeypatch, *(() if par == "1" else ("center_seq",)))
         out = torch.empty_like(Xd)
         mean = torch.empty(dim, dtype=torch.float32, device="cuda")
         var = torch.empty(dim, dtype=torch.float32, device="cuda")
@@ -297,45 +305,35 @@ def test_center_columns_parallel_matches_numpy(monkeypatch, name, n, dim, X):
         assert same(mean, m) and same(var, v) and same(out, o), name
 
 
-# One-launch MiniBatch steps (k_mb_fused, opt-in with GDD_MB_FUSED=1): bit-identical to
-# scikit-learn and to the default two-launch loop on centres, labels, inertia, n_steps_ and
-# the RandomState left behind — across key-buffer groups (G = 1 and 4), row forms (dim % 4 != 0),
-# member rows over several LDS passes (GDD_MB_FUSED_MCAP), with and without reassignment, early
-# stopping and running to max_iter (the last step's lone update).
-@pytest.mark.parametrize("n,dim,k,bs,ratio,max_iter,mcap", [
-    (20000, 40, 454, 1000, 0.01, 100, None),
-    (5000, 40, 50, 1000, 0.01, 100, None),
-    (8000, 7, 70, 300, 0.01, 100, None),
-    (6000, 64, 200, 512, 0.01, 100, None),
-    (20000, 40, 454, 1000, 0.01, 100, 16),
-    (20000, 40, 454, 1000, 0.0, 100, None),
-    (3000, 12, 100, 2048, 0.5, 100, 40),
-    (12000, 40, 300, 1000, 0.01, 1, None),
+# The device-resident MiniBatch loop: bit-identical to scikit-learn on centres, labels, inertia,
+# n_steps_ and the RandomState left behind — across key-buffer groups (G = 1 and 4), row forms
+# (dim % 4 != 0), with and without reassignment, early stopping and running to max_iter.
+@pytest.mark.parametrize("n,dim,k,bs,ratio,max_iter", [
+    (20000, 40, 454, 1000, 0.01, 100),
+    (5000, 40, 50, 1000, 0.01, 100),
+    (8000, 7, 70, 300, 0.01, 100),
+    (6000, 64, 200, 512, 0.01, 100),
+    (20000, 40, 454, 1000, 0.0, 100),
+    (3000, 12, 100, 2048, 0.5, 100),
+    (12000, 40, 300, 1000, 0.01, 1),
 ])
-def test_minibatch_fused_steps_match(monkeypatch, n, dim, k, bs, ratio, max_iter, mcap):
+def test_minibatch_device_loop_shapes(n, dim, k, bs, ratio, max_iter):
     X = synth.blobs(n, dim, k, seed=n + k)
     rs_ref = np.random.RandomState(15)
     ref = O.minibatch_kmeans(X, k, random_state=rs_ref, batch_size=bs, reassignment_ratio=ratio,
                              max_iter=max_iter)
-    if mcap:
-        monkeypatch.setenv("GDD_MB_FUSED_MCAP", str(mcap))
-    fits = []
-    for fused in ("1", "0"):
-        monkeypatch.setenv("GDD_MB_FUSED", fused)
-        rs = np.random.RandomState(15)
-        m = gdd.MiniBatchKMeans(n_clusters=k, random_state=rs, batch_size=bs,
-                                reassignment_ratio=ratio, max_iter=max_iter).fit(X)
-        fits.append((m, rs))
-    for m, rs in fits:
-        assert m.n_steps_ == ref["n_steps_"]
-        assert np.array_equal(m.labels_, ref["labels_"])
-        assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"]))
-        assert m.inertia_ == ref["inertia_"]
-        s1, s2 = rs_ref.get_state(), rs.get_state()
-        assert np.array_equal(s1[1], s2[1]) and s1[2] == s2[2]
+    rs = np.random.RandomState(15)
+    m = gdd.MiniBatchKMeans(n_clusters=k, random_state=rs, batch_size=bs,
+                            reassignment_ratio=ratio, max_iter=max_iter).fit(X)
+    assert m.n_steps_ == ref["n_steps_"]
+    assert np.array_equal(m.labels_, ref["labels_"])
+    assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"]))
+    assert m.inertia_ == ref["inertia_"]
+    s1, s2 = rs_ref.get_state(), rs.get_state()
+    assert np.array_equal(s1[1], s2[1]) and s1[2] == s2[2]
 
 
-# Bounded Lloyd E-steps (GDD_LLOYD_PRUNE, on by default where the top-2 pass fits): a row whose
+# Bounded Lloyd E-steps (on by default where the top-2 pass fits; GDD_FORCE=lloyd_no_prune: off): a row whose
 # bounds prove its label skips the distance pass. Labels, centres, inertia and n_iter_ must equal
 # the unbounded loop's bit for bit (and the oracle's where it is quick), also on data made of
 # near-ties: duplicated rows, rows on the midpoint of two others, a symmetric lattice.
@@ -359,7 +357,7 @@ def test_kmeans_lloyd_bounded_estep_matches(monkeypatch, n, dim, k, near_ties):
     X = _near_tie_data(n, dim, n + dim) if near_ties else synth.blobs(n, dim, max(2, k // 2), seed=n + k)
     fits = []
     for prune in ("1", "0"):
-        monkeypatch.setenv("GDD_LLOYD_PRUNE", prune)
+        force(monkeypatch, *(() if prune == "1" else ("lloyd_no_prune",)))
         np.random.seed(15)
         fits.append(gdd.KMeans(n_clusters=k, n_init=1).fit(X))
     a, b = fits
@@ -383,7 +381,7 @@ def test_kmeans_lloyd_relocation_with_bounds(monkeypatch, prune):
     base = rng.standard_normal((40, 8)).astype(np.float32)
     X = np.ascontiguousarray(np.repeat(base, 60, axis=0)[rng.permutation(2400)])  # 40 distinct rows
     k = 48  # > 40: duplicate centres, empty clusters, relocation (oracle == single-thread sklearn)
-    monkeypatch.setenv("GDD_LLOYD_PRUNE", prune)
+    force(monkeypatch, *(() if prune == "1" else ("lloyd_no_prune",)))
     np.random.seed(15)
     ref = O.kmeans(X, k, n_init=1)
     np.random.seed(15)
@@ -407,7 +405,7 @@ def test_kmeans_lloyd_sliced_fold_matches(monkeypatch, dim):
     k = 10
     fits = []
     for sl in ("1.5", "0"):
-        monkeypatch.setenv("GDD_FOLD_SLICE", sl)
+        force(monkeypatch, f"fold_slice={sl}")
         np.random.seed(15)
         fits.append(gdd.KMeans(n_clusters=k, n_init=1).fit(X))
     a, b = fits
@@ -427,7 +425,7 @@ def test_kmeans_lloyd_padded_fold_matches(monkeypatch, dim, prune):
     """From 65,536 rows with dim % 4 != 0 the M-step folds a zero-padded copy of X (rows of
     round4(dim) floats, 16-byte gathers; r05) and writes only the real columns, and the bounded
     E-step reads its row lists from the same copy: the fit is bit-identical to the passes over X
-    itself (GDD_FOLD_PAD=0 / GDD_ESTEP_PAD=0), sliced large clusters included, and to the oracle."""
+    itself (GDD_FORCE=fold_no_pad / estep_no_pad), sliced large clusters included, and to the oracle."""
     rng = np.random.default_rng(100 + dim)
     sizes = [30000, 16000, 9000, 6000, 4000, 2500, 1500, 800, 400, 200]  # skewed: sliced clusters
     centres = rng.standard_normal((len(sizes), dim)).astype(np.float32) * np.float32(3.0)
@@ -435,12 +433,11 @@ def test_kmeans_lloyd_padded_fold_matches(monkeypatch, dim, prune):
     X = np.ascontiguousarray(X[rng.permutation(len(X))], np.float32)
     assert len(X) >= 65536
     k = 10
-    monkeypatch.setenv("GDD_LLOYD_PRUNE", prune)
     fits = []
-    # the bounded E-step's row lists also read the padded copy (GDD_ESTEP_PAD; r05)
+    # the bounded E-step's row lists also read the padded copy (r05)
     for pad, epad in (("1", "1"), ("1", "0"), ("0", "0")):
-        monkeypatch.setenv("GDD_FOLD_PAD", pad)
-        monkeypatch.setenv("GDD_ESTEP_PAD", epad)
+        force(monkeypatch, *([] if prune == "1" else ["lloyd_no_prune"]) + ([] if pad == "1" else ["fold_no_pad"]) +
+              ([] if epad == "1" else ["estep_no_pad"]))
         np.random.seed(15)
         fits.append(gdd.KMeans(n_clusters=k, n_init=1).fit(X))
     a = fits[0]
@@ -457,13 +454,10 @@ def test_kmeans_lloyd_padded_fold_matches(monkeypatch, dim, prune):
 
 
 @pytest.mark.parametrize("case", ["ml1m_users", "ml1m_items", "relocation", "tol0", "large_n"])
-def test_kmeans_lloyd_update_forms(monkeypatch, case):
-    """The one-workgroup update (empty check, _average_centers + shifts, labels changed, convergence
-    test in one launch; opt-in GDD_LLOYD_UPDATE_SMALL for n <= 131,072 and k * dim <= 262,144) and the
-    default update (the average with the empty check folded in, labels changed, the convergence test)
-    give the same fit, bit for bit, and the oracle's: recsys shapes,
-    empty-cluster relocation (the resumed iteration's update runs without the check), a strict
-    convergence run (tol = 0) and a shape above the one-workgroup limit (both forms the four launches)."""
+def test_kmeans_lloyd_update_shapes(case):
+    """The device loop's update (the average with the empty check folded in, labels changed, the
+    convergence test) against the oracle: recsys shapes, empty-cluster relocation (the resumed
+    iteration's update runs without the check), a strict convergence run (tol = 0) and a larger n."""
     rng = np.random.default_rng(5)
     kw = {}
     if case == "ml1m_users":
@@ -479,18 +473,8 @@ def test_kmeans_lloyd_update_forms(monkeypatch, case):
     else:
         X, k = synth.blobs(140000, 8, 10, seed=14), 12
     X = np.ascontiguousarray(X, np.float32)
-    fits = []
-    for env in ("GDD_LLOYD_UPDATE_SMALL", None):
-        monkeypatch.delenv("GDD_LLOYD_UPDATE_SMALL", raising=False)
-        if env:
-            monkeypatch.setenv(env, "1")
-        np.random.seed(15)
-        fits.append(gdd.KMeans(n_clusters=k, n_init=1, **kw).fit(X))
-    a = fits[1]
-    for b in (fits[0],):
-        assert a.n_iter_ == b.n_iter_ and a.inertia_ == b.inertia_
-        assert np.array_equal(a.labels_, b.labels_)
-        assert np.array_equal(bits(a.cluster_centers_), bits(b.cluster_centers_))
+    np.random.seed(15)
+    a = gdd.KMeans(n_clusters=k, n_init=1, **kw).fit(X)
     if X.shape[0] * k <= 4_000_000:
         np.random.seed(15)
         ref = O.kmeans(X, k, n_init=1, **kw)
@@ -502,26 +486,26 @@ def test_kmeans_lloyd_update_forms(monkeypatch, case):
 @pytest.mark.parametrize("n,dim,k,bs", [(20000, 40, 454, 1000), (30000, 8, 200, 2048), (6000, 12, 400, 200),
                                         (8000, 10, 120, 64)])
 def test_minibatch_reassign_forms(monkeypatch, n, dim, k, bs):
-    """k_mb_reassign's forms (r05, GDD_MB_REASSIGN_FORM): bit 0 the shuffle's draws by the whole
-    workgroup (mt_shuffle_draws_block, a Jacobi fixed point over per-thread counts) instead of one
-    wave; bit 1 the row copies in three block trips beside a one-wave next-batch draw. Blob inputs
-    with fewer blobs than centres leave many clusters empty, so reassignments fire often and large
-    (m up to b/2; b = 2048 takes two 2048-word passes). Every form equals the oracle: labels, centres,
+    """k_mb_reassign: the row copies in three block trips beside a one-wave next-batch draw (the
+    parallel-copy form; r05), and with GDD_HOST_LOOP=1 the host-driven loop's reassignment. Blob
+    inputs with fewer blobs than centres leave many clusters empty, so reassignments fire often and
+    large (m up to b/2; b = 2048 takes two 2048-word passes). Both equal the oracle: labels, centres,
     inertia, n_steps_ and the generator's final state."""
     X = synth.blobs(n, dim, max(2, k // 4), seed=n + k)
     rs_ref = np.random.RandomState(5)
     ref = O.minibatch_kmeans(X, k, random_state=rs_ref, batch_size=bs)
     s_ref = rs_ref.get_state()
-    for form in ("0", "1", "2", "3"):
-        monkeypatch.setenv("GDD_MB_REASSIGN_FORM", form)
+    for host in (False, True):
+        if host:
+            monkeypatch.setenv("GDD_HOST_LOOP", "1")
         rs = np.random.RandomState(5)
         m = gdd.MiniBatchKMeans(n_clusters=k, random_state=rs, batch_size=bs).fit(X)
-        assert m.n_steps_ == ref["n_steps_"], form
-        assert np.array_equal(m.labels_, ref["labels_"]), form
-        assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"])), form
-        assert m.inertia_ == ref["inertia_"], form
+        assert m.n_steps_ == ref["n_steps_"], host
+        assert np.array_equal(m.labels_, ref["labels_"]), host
+        assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"])), host
+        assert m.inertia_ == ref["inertia_"], host
         s = rs.get_state()
-        assert np.array_equal(s[1], s_ref[1]) and s[2] == s_ref[2], form
+        assert np.array_equal(s[1], s_ref[1]) and s[2] == s_ref[2], host
 
 
 @pytest.mark.parametrize("n,dim,k,bs", [(6000, 12, 400, 200), (20000, 8, 300, 500), (3000, 16, 700, 256),
@@ -548,3 +532,25 @@ def test_minibatch_k_above_half_batch(monkeypatch, n, dim, k, bs):
         assert m.inertia_ == ref["inertia_"], host
         s = rs.get_state()
         assert np.array_equal(s[1], s_ref[1]) and s[2] == s_ref[2], host
+
+
+@pytest.mark.parametrize("mni", [1, 2, 3])
+@pytest.mark.parametrize("n,dim,k,bs", [(3000, 16, 700, 256), (6000, 12, 400, 200)])
+def test_minibatch_handoff_then_convergence_stop(n, dim, k, bs, mni):
+    """the k > b/2 hand-off followed closely by a convergence stop. With k >= 2b the
+    argsort branch fires at step 0 (the device loop hands that step to the host and resumes); a small
+    max_no_improvement then stops the fit within a few steps of the hand-off, on the resumed segment.
+    n_steps_, labels, centres, inertia and the generator's final state equal the oracle's."""
+    X = synth.blobs(n, dim, max(2, k // 3), seed=n + k + mni)
+    rs_ref = np.random.RandomState(23)
+    ref = O.minibatch_kmeans(X, k, random_state=rs_ref, batch_size=bs, max_no_improvement=mni)
+    s_ref = rs_ref.get_state()
+    assert ref["n_steps_"] < 100 * n // bs  # the convergence stop fired
+    rs = np.random.RandomState(23)
+    m = gdd.MiniBatchKMeans(n_clusters=k, random_state=rs, batch_size=bs, max_no_improvement=mni).fit(X)
+    assert m.n_steps_ == ref["n_steps_"]
+    assert np.array_equal(m.labels_, ref["labels_"])
+    assert np.array_equal(bits(m.cluster_centers_), bits(ref["cluster_centers_"]))
+    assert m.inertia_ == ref["inertia_"]
+    s = rs.get_state()
+    assert np.array_equal(s[1], s_ref[1]) and s[2] == s_ref[2]

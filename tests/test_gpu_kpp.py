@@ -23,6 +23,14 @@ from gdd import _lib, synth  # noqa: E402
 from gdd.kmeans import _Ops  # noqa: E402
 
 
+def force(monkeypatch, *tokens):
+    """GDD_FORCE (gdd_common.hpp): force the listed k-means++ paths for the next calls."""
+    if tokens:
+        monkeypatch.setenv("GDD_FORCE", ",".join(tokens))
+    else:
+        monkeypatch.delenv("GDD_FORCE", raising=False)
+
+
 def _skl_sqdist_dev(C, X):
     lib = _lib.device_lib()
     Cd, Xd = torch.from_numpy(C).cuda(), torch.from_numpy(X).cuda()
@@ -96,12 +104,12 @@ def test_kmeans_plusplus_orders(n, dim, k, dup, trials):
 
 
 def test_kmeans_plusplus_two_launch_path(monkeypatch):
-    """The two-launch rounds (GDD_KPP_TWO_LAUNCH) give the same seeding as the fused ones."""
+    """The two-launch rounds (the single-block path for rows wider than 512 features or more than 256
+    distance workgroups; GDD_FORCE=kpp_two_launch) give the same seeding as the fused ones."""
     n, dim, k = 3000, 40, 90
     X = np.ascontiguousarray(synth.blobs(n, dim, 20, seed=9), np.float32)
     c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(3))
-    monkeypatch.setenv("GDD_KPP_TWO_LAUNCH", "1")
-    monkeypatch.setenv("GDD_KPP_NO_TABLE", "1")
+    force(monkeypatch, "kpp_two_launch", "kpp_no_table")
     ops = _Ops("cuda", n, k, dim)
     c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(3))
     assert np.array_equal(idx.cpu().numpy(), idx_ref)
@@ -116,19 +124,17 @@ def test_kmeans_plusplus_two_launch_path(monkeypatch):
                                      (3706, 64, 371), (2000, 49, 101)])  # the 64-slot table
 def test_kmeans_plusplus_round_forms(monkeypatch, n, dim, k):
     """Every single-block round form gives the oracle's seeding, bit for bit: two rounds per launch
-    over the distance table (default for plain-chain plans, dim <= 48, k >= 16, T <= 8), one round
-    per launch over the table (GDD_KPP_SINGLE_ROUND), and the fused distance + fold rounds
-    (GDD_KPP_NO_TABLE); the folds' two-ballot searches (default) and binary searches
-    (GDD_KPP_BSEARCH)."""
+    over the distance table (default for plain-chain plans, dim <= 64, k >= 16, T <= 8), one round
+    per launch over the table (the default for T > 8; GDD_FORCE=kpp_single_round), and the fused
+    distance + fold rounds (the default for k < 16; GDD_FORCE=kpp_no_table)."""
     X = np.ascontiguousarray(synth.blobs(n, dim, max(2, k // 4), seed=n + dim + 1), np.float32)
     c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
-    for var in (None, "GDD_KPP_SINGLE_ROUND", "GDD_KPP_NO_TABLE", "GDD_KPP_BSEARCH"):
-        if var:
-            monkeypatch.setenv(var, "1")
+    for toks in ((), ("kpp_single_round",), ("kpp_no_table",)):
+        force(monkeypatch, *toks)
         ops = _Ops("cuda", n, k, dim)
         c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(15))
-        assert np.array_equal(idx.cpu().numpy(), idx_ref), var
-        assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref)), var
+        assert np.array_equal(idx.cpu().numpy(), idx_ref), toks
+        assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref)), toks
 
 
 # ---- the cumulative potential: numpy's left-to-right fp64 cumsum, exactly ---------------------------
@@ -170,16 +176,15 @@ def _kpp_dev(X, k, T, first, u, w=None):
     return centers.cpu().numpy(), idx.cpu().numpy()
 
 
-# (n, env): every search form — the pick count (round 0 of the single-block paths and the two-launch
-# rounds), the fold's two-ballot search (default) and binary search (GDD_KPP_BSEARCH) in the table
-# pair / single rounds and the fused rounds, the multi-block round (per-(block, trial) and the split
-# pick launch)
+# (n, forced paths): every search form — the pick count (round 0 of the single-block paths and the
+# two-launch rounds), the fold's two-ballot search in the table pair / single rounds and the fused
+# rounds, the multi-block round (per-(block, trial) and the split pick launch), k_kpp1_big's
+# speculative draws and their regular fallback
 CUMSUM_FORMS = [
-    (1000, ()), (4096, ()), (1000, ("GDD_KPP_SINGLE_ROUND",)), (1000, ("GDD_KPP_NO_TABLE",)),
-    (1000, ("GDD_KPP_NO_TABLE", "GDD_KPP_TWO_LAUNCH")), (1000, ("GDD_KPP_BSEARCH",)),
-    (4096, ("GDD_KPP_SINGLE_ROUND", "GDD_KPP_BSEARCH")), (9000, ()), (9000, ("GDD_KPP_NO_BIG1",)),
-    (20000, ()), (20000, ("GDD_KPP_BIG1_MAX=32768",)), (530000, ()),
-    (9000, ("GDD_KPP_SPEC_SEARCH=0",)),  # k_kpp1_big's regular draws (default: speculative + check)
+    (1000, ()), (4096, ()), (1000, ("kpp_single_round",)), (1000, ("kpp_no_table",)),
+    (1000, ("kpp_no_table", "kpp_two_launch")), (4096, ("kpp_single_round",)), (9000, ()),
+    (9000, ("kpp_no_big1",)), (20000, ()), (20000, ("kpp_big1_max=32768",)), (530000, ()),
+    (530000, ("kpp_no_split",)),
 ]
 
 
@@ -191,14 +196,11 @@ def test_kpp_cumsum_adversarial(monkeypatch, n, env, rnd):
     numpy's; with the check disabled (GDD_KPP_EXACT=0) it is not — so the case is adversarial for
     that form and the check is what makes it exact."""
     k, T = 16, 4
-    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")  # the multi-block table rounds at k = 16 too
+    force(monkeypatch, "kpp_force_table", *env)  # the multi-block table rounds at k = 16 too
     X = adversarial_points(n)
     u = adversarial_uniforms(k, T, rnd)
     c_ref, idx_ref = O.kmeans_plusplus_draws(X, k, T, 0, u)
     assert idx_ref[rnd] == n - 2
-    for var in env:
-        key, _, val = var.partition("=")
-        monkeypatch.setenv(key, val or "1")
     for mode in ("1", "2"):
         monkeypatch.setenv("GDD_KPP_EXACT", mode)
         c, idx = _kpp_dev(X, k, T, 0, u)
@@ -212,8 +214,7 @@ def test_kpp_cumsum_adversarial(monkeypatch, n, env, rnd):
 @pytest.mark.parametrize("n", [1000, 9000, 20000])
 def test_kpp_cumsum_adversarial_weighted(monkeypatch, n):
     """The same with sample weights (w * closest in fp32, then the fp64 sum)."""
-    monkeypatch.setenv("GDD_KPP_BIG1_MAX", "32768")
-    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")
+    force(monkeypatch, "kpp_big1_max=32768", "kpp_force_table")
     k, T = 16, 4
     X = adversarial_points(n)
     w = np.ones(n, np.float32)
@@ -249,17 +250,18 @@ def test_kpp_replay_every_draw(monkeypatch, n, dim, k):
     (17730, 64, 1773, False),  # Ali-Display users' shape and k: T = 9
     (32768, 16, 40, False)])
 def test_kmeans_plusplus_big_rounds(monkeypatch, n, dim, k, oracle):
-    """k_kpp1_big (the default for table plans with 4096 < n <= 32768) gives the seeding of the
-    per-(block, trial) table rounds (GDD_KPP_NO_BIG1) and, where the oracle is run, the oracle's —
-    bit for bit, over the 8-, 16- and 32-entry segment forms, odd n (the sgemv_t tail) and T = 9."""
+    """k_kpp1_big (the default for table plans with 4096 < n <= 16384) gives the seeding of the
+    per-(block, trial) table rounds (the default above 16,384; GDD_FORCE=kpp_no_big1) and, where the
+    oracle is run, the oracle's — bit for bit, over the 8-, 16- and 32-entry segment forms, odd n
+    (the sgemv_t tail) and T = 9."""
     X = synth.blobs(n, dim, max(2, k // 4), seed=n + dim + 3)
     X = np.ascontiguousarray(X - X.mean(axis=0), np.float32)
-    monkeypatch.setenv("GDD_KPP_BIG1_MAX", "32768")  # the 32-entry segments too (default limit 16,384)
-    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")  # small k: the table is built although it does not pay
+    # the 32-entry segments too (default limit 16,384); small k: the table although it does not pay
+    force(monkeypatch, "kpp_big1_max=32768", "kpp_force_table")
     ops = _Ops("cuda", n, k, dim)
     Xd = torch.from_numpy(X).cuda()
     c, idx = ops.kmeans_plusplus(Xd, k, np.random.RandomState(42))
-    monkeypatch.setenv("GDD_KPP_NO_BIG1", "1")
+    force(monkeypatch, "kpp_big1_max=32768", "kpp_force_table", "kpp_no_big1")
     c2, idx2 = ops.kmeans_plusplus(Xd, k, np.random.RandomState(42))
     assert np.array_equal(idx.cpu().numpy(), idx2.cpu().numpy())
     assert np.array_equal(bits(c.cpu().numpy()), bits(c2.cpu().numpy()))
@@ -273,7 +275,7 @@ def test_kmeans_plusplus_big_rounds_weighted_and_replayed(monkeypatch):
     """Sample weights (w * row in fp32 for the cumulative, the weighted sgemv_t lane chains) and
     every draw replayed (GDD_KPP_EXACT=2) on the one-workgroup-per-trial rounds."""
     n, dim, k, T = 9001, 24, 40, 5
-    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")
+    force(monkeypatch, "kpp_force_table")
     X = np.ascontiguousarray(synth.blobs(n, dim, 10, seed=77), np.float32)
     w = np.random.default_rng(3).uniform(0.5, 2.0, n).astype(np.float32)
     u = np.random.RandomState(9).uniform(size=(k - 1) * T)
@@ -298,13 +300,13 @@ def test_kmeans_plusplus_small_k_skips_the_table(monkeypatch, n, dim, k):
     ops = _Ops("cuda", n, k, dim)
     Xd = torch.from_numpy(X).cuda()
     c, idx = ops.kmeans_plusplus(Xd, k, np.random.RandomState(5))
-    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")
+    force(monkeypatch, "kpp_force_table")
     c2, idx2 = ops.kmeans_plusplus(Xd, k, np.random.RandomState(5))
     assert np.array_equal(idx.cpu().numpy(), idx2.cpu().numpy())
     assert np.array_equal(bits(c.cpu().numpy()), bits(c2.cpu().numpy()))
 
 
-def _par_case_points(case, n, dim, seed):
+def _hard_points(case, n, dim, seed):
     rng = np.random.default_rng(seed)
     if case == "integers":  # exact integer distances: the running sums pass 2^24, so ties are common
         return rng.integers(-300, 300, (n, dim)).astype(np.float32)
@@ -319,83 +321,38 @@ def _par_case_points(case, n, dim, seed):
 
 @pytest.mark.parametrize("case", ["blobs", "integers", "dupes", "range"])
 @pytest.mark.parametrize("n,dim,k", [(3000, 40, 454), (2708, 7, 70), (1001, 5, 33), (6040, 64, 604),
-                                     (5003, 33, 60)])
-def test_kmeans_plusplus_table_forms(monkeypatch, case, n, dim, k):
-    """The n x n distance table by 4 x 4 register tiles (k_kpp_dmat_t, r05 default) and by rows
-    (GDD_KPP_DMAT_ROWS=1, the r04 form) give the same seeding as the oracle: the single-block table
-    rounds (n <= 4096), the one-workgroup rounds on the big table, n % 4 tails (scalar stores), dim
-    64 (the 64 KB tile) and data with exact ties, zero distances and twelve decades."""
-    X = _par_case_points(case, n, dim, n + dim + k)
+                                     (5003, 33, 60), (4093, 3, 200), (3706, 64, 371)])
+def test_kmeans_plusplus_hard_data(case, n, dim, k):
+    """The n x n distance table (k_kpp_dmat_t's 4 x 4 register tiles), the table's pair and big
+    rounds and the sgemv_t lane chains on data with exact ties (integer distances past 2^24), zero
+    distances and twelve decades of magnitudes, 8- and 4-lane trials (T = 6 at the Cora shape), n % 4
+    tails and dim 64 (the 64 KB tile): the oracle's seeding, bit for bit."""
+    X = _hard_points(case, n, dim, n + dim + k)
     c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
-    for rows in (False, True):
-        if rows:
-            monkeypatch.setenv("GDD_KPP_DMAT_ROWS", "1")
-        ops = _Ops("cuda", n, k, dim)
-        c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(15))
-        assert np.array_equal(idx.cpu().numpy(), idx_ref), rows
-        assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref)), rows
+    ops = _Ops("cuda", n, k, dim)
+    c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(15))
+    assert np.array_equal(idx.cpu().numpy(), idx_ref)
+    assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref))
 
 
 @pytest.mark.parametrize("case", ["blobs", "integers", "dupes", "range"])
-@pytest.mark.parametrize("n,dim,k", [(3000, 40, 454), (2708, 7, 70), (4093, 3, 200), (3706, 64, 371),
-                                     (1001, 5, 33)])
-def test_kmeans_plusplus_parallel_chains(monkeypatch, case, n, dim, k):
-    """The exact parallel sgemv_t lane chains (GDD_KPP_PAR_CHAIN=1: runs inside one binade from
-    2^e and 2^e + u, composed by parity, crossings added in hardware) give the sequential chains'
-    bits: the seeding equals the oracle's with and without them, on data with exact ties (integer
-    distances past 2^24), zero distances, twelve decades of magnitudes, 8- and 4-lane trials
-    (T = 6 at the Cora shape) and n % 4 tails."""
-    X = _par_case_points(case, n, dim, n + dim + k)
-    c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
-    for val in ("1", "0"):
-        monkeypatch.setenv("GDD_KPP_PAR_CHAIN", val)
-        ops = _Ops("cuda", n, k, dim)
-        c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(15))
-        assert np.array_equal(idx.cpu().numpy(), idx_ref), val
-        assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref)), val
-
-
-@pytest.mark.parametrize("case", ["blobs", "integers", "dupes", "range"])
-@pytest.mark.parametrize("n,dim,k", [(6040, 64, 604), (9001, 24, 200), (12003, 7, 120), (5003, 33, 60)])
-def test_kmeans_plusplus_big_rounds_parallel_chains(monkeypatch, case, n, dim, k):
-    """k_kpp1_big (one 1024-thread workgroup per trial) with block 0's lane chains by the exact
-    parallel runs (GDD_KPP_PAR_CHAIN=1: four spare waves precompute, block 0's wave walks; the
-    natural LDS row at stride 8, or 4 for the 4-lane trials) equals the sequential chains and the
-    oracle (where run) bit for bit."""
-    X = _par_case_points(case, n, dim, n + dim + k)
-    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")
-    out = {}
-    for val in ("1", "0"):
-        monkeypatch.setenv("GDD_KPP_PAR_CHAIN", val)
-        c, idx = _Ops("cuda", n, k, dim).kmeans_plusplus(torch.from_numpy(X).cuda(), k,
-                                                         np.random.RandomState(15))
-        out[val] = (idx.cpu().numpy(), bits(c.cpu().numpy()))
-    assert np.array_equal(out["1"][0], out["0"][0])
-    assert np.array_equal(out["1"][1], out["0"][1])
+@pytest.mark.parametrize("n,dim,k,toks", [(9001, 24, 200, ()), (12003, 7, 120, ()),
+                                          (6040, 64, 604, ("kpp_no_big1",)),
+                                          (9001, 24, 200, ("kpp_no_big1",)),
+                                          (17730, 64, 300, ()),  # Ali-Display users' n: per-block rounds
+                                          (8195, 5, 30, ("kpp_no_table",))])  # distances per round
+def test_kmeans_plusplus_hard_data_multi_block(monkeypatch, case, n, dim, k, toks):
+    """The multi-block forms on the same hard data: k_kpp1_big and the per-(block, trial) rounds
+    (with and without the table) against the one-workgroup-per-trial table rounds (both compute every
+    potential with the sequential lane chains), and against the oracle where it is quick."""
+    X = _hard_points(case, n, dim, n + dim + k + 1)
+    force(monkeypatch, "kpp_force_table", *toks)
+    c, idx = _Ops("cuda", n, k, dim).kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(15))
+    force(monkeypatch, "kpp_force_table", "kpp_big1_max=32768")
+    c2, idx2 = _Ops("cuda", n, k, dim).kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(15))
+    assert np.array_equal(idx.cpu().numpy(), idx2.cpu().numpy())
+    assert np.array_equal(bits(c.cpu().numpy()), bits(c2.cpu().numpy()))
     if n * k <= 6040 * 604:
         c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
-        assert np.array_equal(out["1"][0], idx_ref)
-        assert np.array_equal(out["1"][1], bits(c_ref))
-
-
-@pytest.mark.parametrize("case", ["blobs", "integers", "range"])
-@pytest.mark.parametrize("n,dim,k,env", [(6040, 64, 604, ("GDD_KPP_NO_BIG1",)),
-                                         (17730, 64, 300, ()),  # Ali-Display users' n: per-block rounds
-                                         (9001, 24, 200, ("GDD_KPP_NO_BIG1",)),
-                                         (8195, 5, 30, ("GDD_KPP_NO_TABLE",))])  # distances per round
-def test_kmeans_plusplus_block_rounds_parallel_chains(monkeypatch, case, n, dim, k, env):
-    """The per-(block, trial) rounds (k_kpp_round) with each block's lane chains by the exact
-    parallel runs (GDD_KPP_PAR_CHAIN=1: waves 12..15 precompute, wave 0 walks) equal the sequential
-    chains bit for bit, with and without the distance table."""
-    X = _par_case_points(case, n, dim, n + dim + k + 1)
-    monkeypatch.setenv("GDD_KPP_FORCE_TABLE", "1")
-    for var in env:
-        monkeypatch.setenv(var, "1")
-    out = {}
-    for val in ("1", "0"):
-        monkeypatch.setenv("GDD_KPP_PAR_CHAIN", val)
-        c, idx = _Ops("cuda", n, k, dim).kmeans_plusplus(torch.from_numpy(X).cuda(), k,
-                                                         np.random.RandomState(15))
-        out[val] = (idx.cpu().numpy(), bits(c.cpu().numpy()))
-    assert np.array_equal(out["1"][0], out["0"][0])
-    assert np.array_equal(out["1"][1], out["0"][1])
+        assert np.array_equal(idx.cpu().numpy(), idx_ref)
+        assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref))

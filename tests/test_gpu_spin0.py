@@ -25,11 +25,13 @@ SELECTED = [
     "tests/test_gpu_kmeans.py::test_minibatch_kmeans_bitexact",
     "tests/test_gpu_kmeans.py::test_minibatch_k_above_half_batch",
     "tests/test_gpu_kmeans.py::test_minibatch_reassign_forms",
+    "tests/test_gpu_kmeans.py::test_minibatch_handoff_then_convergence_stop",
     "tests/test_gpu_kmeans.py::test_kmeans_plusplus_bitexact",
     "tests/test_gpu_kpp.py::test_kmeans_plusplus_orders",
     "tests/test_gpu_kpp.py::test_kmeans_plusplus_round_forms",
     "tests/test_gpu_kpp.py::test_kmeans_plusplus_big_rounds",
     "tests/test_gpu_kpp.py::test_kpp_replay_every_draw",
+    "tests/test_gpu_kpp.py::test_kmeans_plusplus_hard_data_multi_block",
 ]
 
 

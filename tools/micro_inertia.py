@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """The inertia (sequential fp32 sum of the per-sample distances) at the bench, Reddit and products
-shapes: device time of the one-lane fold (GDD_INERTIA_SEQ=1), the one-workgroup chunked walk
+shapes: device time of the one-workgroup chunked walk
 (gdd_inertia) and the segmented form (gdd_inertia_ws), each checked against the sequential order."""
 import os
 import sys
@@ -28,7 +28,7 @@ def timed(fn, reps=10):
 def main():
     lib = _lib.device_lib()
     s = _lib.stream_ptr()
-    mode = "one-lane fold" if os.environ.get("GDD_INERTIA_SEQ") == "1" else "parallel"
+    mode = "parallel"
     for n in (169343, 153932, 2449029):
         rng = np.random.default_rng(n)
         # inertia-like terms: squared distances in 40 / 47 dims

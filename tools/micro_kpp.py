@@ -51,10 +51,10 @@ def run(n, dim, k, reps, check=True):
 
 
 def ab(n=3000, dim=40, k=454):
-    """Same-process A/B of the round variants (devices differ by up to ~10% in clock), and of the
-    cumulative-potential rounding check (GDD_KPP_EXACT: 0 off, 1 default, 2 replay every draw)."""
-    for var, val in (("", ""), ("GDD_KPP_BSEARCH", "1"), ("", ""), ("GDD_KPP_BSEARCH", "1"),
-                     ("GDD_KPP_SINGLE_ROUND", "1"), ("GDD_KPP_NO_TABLE", "1"),
+    """Same-process A/B of the round forms (devices differ by up to ~10% in clock) through
+    GDD_FORCE, and of the cumulative-potential rounding check (GDD_KPP_EXACT: 0 off, 1 default, 2
+    replay every draw)."""
+    for var, val in (("", ""), ("GDD_FORCE", "kpp_single_round"), ("GDD_FORCE", "kpp_no_table"),
                      ("GDD_KPP_EXACT", "0"), ("", ""), ("GDD_KPP_EXACT", "2")):
         if var:
             os.environ[var] = val
@@ -65,45 +65,19 @@ def ab(n=3000, dim=40, k=454):
 
 
 def ab_big():
-    """One 1024-thread workgroup per trial (k_kpp1_big, default for 4096 < n <= 32768 table plans)
-    against the per-(block, trial) table rounds (GDD_KPP_NO_BIG1), same process."""
+    """One 1024-thread workgroup per trial (k_kpp1_big, default for 4096 < n <= 16384 table plans)
+    against the per-(block, trial) table rounds (GDD_FORCE=kpp_no_big1), same process."""
     for (n, dim, k) in [(6040, 64, 604), (9001, 24, 200), (17730, 64, 1773)]:
-        for var in ("", "GDD_KPP_NO_BIG1", "", "GDD_KPP_NO_BIG1"):
+        for var in ("", "kpp_no_big1", "", "kpp_no_big1"):
             if var:
-                os.environ[var] = "1"
+                os.environ["GDD_FORCE"] = var
             print(f"variant {var or 'default'}:", end=" ", flush=True)
             run(n, dim, k, 3, check=False)
             if var:
-                del os.environ[var]
-
-
-def ab_spec():
-    """The folds' speculative searches (default) against searching after the lane chains
-    (GDD_KPP_SPEC_SEARCH=0), same process, at the MiniBatchKMeans init shape and two others."""
-    for (n, dim, k) in [(3000, 40, 454), (3000, 41, 769), (3706, 64, 371), (2708, 7, 70)]:
-        for val in ("1", "0", "1", "0"):
-            os.environ["GDD_KPP_SPEC_SEARCH"] = val
-            print(f"variant GDD_KPP_SPEC_SEARCH={val}:", end=" ", flush=True)
-            run(n, dim, k, 5, check=(val == "1"))
-        del os.environ["GDD_KPP_SPEC_SEARCH"]
-
-
-def ab_par():
-    """The exact parallel lane chains (GDD_KPP_PAR_CHAIN=1, 512-thread pair launches) against the
-    sequential lane chains (=0), same process, parity checked on the first pass of each."""
-    for (n, dim, k) in [(3000, 40, 454), (3706, 64, 371), (2708, 7, 70), (3000, 41, 769),
-                        (6040, 64, 604), (9001, 24, 200), (17730, 64, 1773)]:
-        for i, val in enumerate(("0", "1", "0", "1")):
-            os.environ["GDD_KPP_PAR_CHAIN"] = val
-            print(f"variant GDD_KPP_PAR_CHAIN={val}:", end=" ", flush=True)
-            run(n, dim, k, 5 if n < 10000 else 2, check=i < 2 and n * k < 1e7)
-        del os.environ["GDD_KPP_PAR_CHAIN"]
+                del os.environ["GDD_FORCE"]
 
 
 if __name__ == "__main__":
-    if sys.argv[1:2] == ["par"]:
-        ab_par()
-        sys.exit(0)
     if sys.argv[1:2] == ["arxiv"]:  # timing only: the bench's init shape, ML-1M users, Ali-Display users
         for (n, dim, k, reps) in [(3000, 40, 454, 5), (6040, 64, 604, 3), (17730, 64, 1773, 1)]:
             run(n, dim, k, reps, check=False)
@@ -114,9 +88,6 @@ if __name__ == "__main__":
         sys.exit(0)
     if sys.argv[1:2] == ["one"]:  # the MiniBatchKMeans init shape alone, parity checked
         run(3000, 40, 454, 5)
-        sys.exit(0)
-    if sys.argv[1:2] == ["spec"]:
-        ab_spec()
         sys.exit(0)
     if sys.argv[1:2] == ["big"]:
         ab_big()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Bounded Lloyd E-step diagnostics at the ogbn-products k-means shape (2,449,029 x 47, k = 196):
-wall time of a fixed-iteration fit with the bounds on and off (GDD_LLOYD_PRUNE) and the large
-clusters' feature-sliced M-step on and off (GDD_FOLD_SLICE), on Gaussian
+wall time of a fixed-iteration fit with the bounds on and off (GDD_FORCE=lloyd_no_prune) and the large
+clusters' feature-sliced M-step on and off (GDD_FORCE=fold_slice=F), on Gaussian
 "logits" (no cluster structure: the hard case) and on blobs. Run under rocprofv3 --kernel-trace
 for the per-kernel split (k_ham_test, the top-2 pass over the failing rows, k_ham_finalize)."""
 import os
@@ -36,8 +36,8 @@ def main(n=2449029, dim=47, k=196, iters=int(os.environ.get("ITERS", "300"))):
     }
     for name, X in data.items():
         for prune, sl in (("1", "1.5"), ("1", "0"), ("0", "0"), ("1", "1.5"), ("1", "1.0"), ("1", "0")):
-            os.environ["GDD_LLOYD_PRUNE"] = prune
-            os.environ["GDD_FOLD_SLICE"] = sl
+            os.environ["GDD_FORCE"] = ",".join((["lloyd_no_prune"] if prune == "0" else []) +
+                                               [f"fold_slice={sl}"])
             ms, it = fit_ms(X, k, iters)
             print(f"{name:16s} prune={prune} fold_slice={sl}: {it} iterations, {ms:.1f} ms", flush=True)
 

@@ -31,16 +31,15 @@ def main():
     logits = torch.addmm(bias, target, W)
     del g, gn, target, X
     torch.cuda.synchronize()
-    # PADS="111,110,111,110": an A/B of the zero-padded copy of X (GDD_FOLD_PAD, GDD_ESTEP_PAD) and the
-    # column-major fold (GDD_FOLD_CM) and the parallel centring (GDD_CENTER_PAR) on the same data
+    # PADS="11,10,11,10": an A/B of the zero-padded copy of X for the fold and for the E-step's row lists
+    # (GDD_FORCE=fold_no_pad / estep_no_pad) on the same data
     pads = os.environ.get("PADS", "")
     forms = pads.split(",") if pads else [None] * int(os.environ.get("REPS", "2"))
     for r, pad in enumerate(forms):
         if pad is not None:  # "f" or "fe": the fold's padded copy, and the E-step's row lists on it
-            os.environ["GDD_FOLD_PAD"] = pad[0]
-            os.environ["GDD_ESTEP_PAD"] = pad[1] if len(pad) > 1 else pad[0]
-            os.environ["GDD_FOLD_CM"] = pad[2] if len(pad) > 2 else "1"
-            os.environ["GDD_CENTER_PAR"] = pad[3] if len(pad) > 3 else "1"
+            toks = (["fold_no_pad"] if pad[0] == "0" else []) + \
+                (["estep_no_pad"] if (pad[1] if len(pad) > 1 else pad[0]) == "0" else [])
+            os.environ["GDD_FORCE"] = ",".join(toks)
         kph = {}
         gk.PHASE_TIMING = kph
         t = time.perf_counter()
@@ -51,7 +50,7 @@ def main():
         gk.PHASE_TIMING = None
         cnt = torch.bincount(lab.long(), minlength=cfg.k).cpu().numpy()
         top = np.sort(cnt)[::-1]
-        print(f"rep {r}{'' if pad is None else ' GDD_FOLD_PAD/GDD_ESTEP_PAD/GDD_FOLD_CM/GDD_CENTER_PAR=' + pad}: fit {ms:.1f} ms, {int(km.n_iter_)} iterations, phases "
+        print(f"rep {r}{'' if pad is None else ' pads=' + pad}: fit {ms:.1f} ms, {int(km.n_iter_)} iterations, phases "
               + " ".join(f"{k}={v:.1f}" if isinstance(v, float) else f"{k}={v}" for k, v in kph.items())
               + f"; cluster sizes max {top[0]} mean {cnt.mean():.0f} top5 {top[:5].tolist()} "
               f"min {top[-1]}", flush=True)
