@@ -85,6 +85,13 @@ int sort_pairs_i32(const int32_t* keys_in, int32_t* keys_out, const int32_t* val
 // gap is already the device's own (MiniBatchKMeans fit 14.05 ms replayed vs 14.00 eager, k-means++
 // 4.13 vs 4.20 ms) — and a recording costs a fit's worth of time, so it stays opt-in.
 // ---------------------------------------------------------------------------------------------
+// resident workgroups of a kernel on the current device (occupancy x CUs; cached)
+int occupancy_blocks(const void* fn, int threads, size_t lds, int* out);
+// the bf16 full labels pass's r06 kernel (gdd_bf16.hip): n >= 32, dim <= 64, 16-byte aligned X, whole
+// rows; the workspace holds the centres' fragments (bf16_frag_bytes)
+int bf16q_launch(int64_t n, int dim, const float* X, int k, const float* C, const float* c_norm2,
+                 int32_t* labels, float* sq_dist, void* ws, size_t ws_bytes, hipStream_t s);
+
 // GDD_FORCE (tests and diagnostics only): a comma-separated list of tokens, each forcing a path that
 // other shapes take by default (so its bits can be pinned on a small shape), e.g.
 // GDD_FORCE=kpp_no_table,lloyd_no_prune or GDD_FORCE=kpp_big1_max=32768. Read on every call (host).

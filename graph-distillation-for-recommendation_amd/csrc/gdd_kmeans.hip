@@ -898,157 +898,6 @@ __global__ __launch_bounds__(256) void k_assign_bf16p(int64_t n, int dim, int ns
   }
 }
 
-// r06: the same pass, VALU-lean. At 2.45M x 47 the r03 kernel issued ~4,300 cycles
-// per 32-point tile on its SIMD (VALU is 4 cycles per wave64 instruction): the scatter into the padded
-// LDS rows divided every element index by dim (~1,500 cycles), the epilogue 112 x (fma, compare, two
-// selects) (~1,800), the 21 MFMAs 672 — 0.36 of the HBM roof. Here:
-//   * the tile's 32 x dim floats are ONE contiguous span: copied into the wave's LDS slot as is
-//     (float4 stores, row stride = dim, no index arithmetic; 16 zero floats past the slot);
-//   * B-fragments read row r's features 16 st + 8 h .. + 7 straight from that layout (two
-//     ds_read_b128 when dim % 4 == 0, else eight ds_read_b32), the last k-step's features past dim
-//     masked to zero (the next row's values would meet zero A entries, but a NaN or inf would not);
-//   * two centre tiles per pass: their MFMA chains interleave and the first tile's epilogue runs
-//     while the second's chain completes (VALU beside the MFMAs).
-template <int PER, bool VEC4>
-__global__ __launch_bounds__(256) void k_assign_bf16q(int64_t n, int dim, int nsteps, int ktiles,
-                                                      const float* __restrict__ X, int k,
-                                                      const bf16x8_t* __restrict__ frags,
-                                                      const float* __restrict__ cn_in,
-                                                      const float* __restrict__ C,
-                                                      int32_t* __restrict__ labels,
-                                                      float* __restrict__ sq_dist) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16x8_t* Af = reinterpret_cast<bf16x8_t*>(smem);
-  float* Cn = reinterpret_cast<float*>(smem + (size_t)ktiles * nsteps * 64 * 16);
-  float* Pt = Cn + ktiles * 32;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, r = lane & 31;
-  const int slot = 32 * dim + 16;  // floats per wave slot (a multiple of 4: dim x 32 is)
-  {  // the prebuilt fragments and norms: coalesced 16-byte copies
-    const int nfr = ktiles * nsteps * 64;
-    for (int e = tid; e < nfr; e += 256) Af[e] = frags[e];
-    for (int c = tid; c < ktiles * 32; c += 256) Cn[c] = cn_in[c];
-  }
-  float* my = Pt + wave * slot;
-  if (lane < 16) my[32 * dim + lane] = 0.f;  // past the last row: read by row 31's masked features
-  __syncthreads();
-  const int nf4 = 8 * dim;  // float4 per full tile (32 rows x dim floats)
-  const int64_t ntiles = (n + 31) / 32, nfull = n / 32;
-  const int64_t step = (int64_t)gridDim.x * 4;
-  auto fetch = [&](int64_t tt, floatx4_t (&v)[PER]) {
-    if (tt >= nfull) return;  // the partial last tile is read scalar in stage()
-    const floatx4_t* src = reinterpret_cast<const floatx4_t*>(X + tt * 32 * dim);
-#pragma unroll
-    for (int q = 0; q < PER; ++q) v[q] = __builtin_nontemporal_load(src + min(lane + 64 * q, nf4 - 1));
-  };
-  auto stage = [&](int64_t tt, const floatx4_t (&v)[PER]) {
-    if (tt < nfull) {
-      floatx4_t* d4 = reinterpret_cast<floatx4_t*>(my);
-#pragma unroll
-      for (int q = 0; q < PER; ++q)
-        if (lane + 64 * q < nf4) d4[lane + 64 * q] = v[q];
-    } else {
-      const int64_t m = (n - tt * 32) * dim;
-      for (int e = lane; e < 32 * dim; e += 64) my[e] = e < m ? X[tt * 32 * dim + e] : 0.f;
-    }
-  };
-  const int lastf = dim - 16 * (nsteps - 1) - 8 * h;  // features of the last k-step this lane keeps
-  auto compute = [&](int64_t tt) {
-    bf16x8_t b[8];
-    const float* row = my + r * dim;
-#pragma unroll
-    for (int st = 0; st < 8; ++st) {
-      if (st < nsteps) {
-        float x[8];
-        if constexpr (VEC4) {
-          const floatx4_t lo = *reinterpret_cast<const floatx4_t*>(row + 16 * st + 8 * h);
-          const floatx4_t hi = *reinterpret_cast<const floatx4_t*>(row + 16 * st + 8 * h + 4);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            x[j] = lo[j];
-            x[4 + j] = hi[j];
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) x[j] = row[16 * st + 8 * h + j];
-        }
-        if (st == nsteps - 1) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) x[j] = j < lastf ? x[j] : 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) b[st][j] = (__bf16)x[j];
-      }
-    }
-    float bestd = __builtin_inff();
-    int bestc = 0;
-    auto epilogue = [&](const floatx16& acc, int ct) {
-      const floatx4_t* cp = reinterpret_cast<const floatx4_t*>(Cn + ct * 32 + 4 * h);
-      floatx4_t cn[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) cn[g] = cp[2 * g];  // rows 8g + 4h .. +3
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const float d = __builtin_fmaf(-2.f, acc[reg], cn[reg >> 2][reg & 3]);
-        if (d < bestd) {
-          bestd = d;
-          bestc = ct * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        }
-      }
-    };
-    int ct = 0;
-    for (; ct + 2 <= ktiles; ct += 2) {
-      floatx16 a0 = {}, a1 = {};
-#pragma unroll
-      for (int st = 0; st < 8; ++st)
-        if (st < nsteps) {
-          a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Af[(ct * nsteps + st) * 64 + lane], b[st], a0, 0, 0, 0);
-          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Af[((ct + 1) * nsteps + st) * 64 + lane], b[st], a1, 0, 0, 0);
-        }
-      epilogue(a0, ct);
-      epilogue(a1, ct + 1);
-    }
-    if (ct < ktiles) {
-      floatx16 a0 = {};
-#pragma unroll
-      for (int st = 0; st < 8; ++st)
-        if (st < nsteps) a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Af[(ct * nsteps + st) * 64 + lane], b[st], a0, 0, 0, 0);
-      epilogue(a0, ct);
-    }
-    const float od = __shfl_xor(bestd, 32);
-    const int oc = __shfl_xor(bestc, 32);
-    if (od < bestd || (od == bestd && oc < bestc)) {
-      bestd = od;
-      bestc = oc;
-    }
-    const int64_t p = tt * 32 + r;
-    if (h == 0 && p < n) {
-      labels[p] = bestc;
-      if (sq_dist) sq_dist[p] = skl_sqdist(row, C + (int64_t)bestc * dim, dim);
-    }
-  };
-  floatx4_t va[PER], vb[PER];
-  int64_t t = (int64_t)blockIdx.x * 4 + wave;
-  fetch(t, va);
-  fetch(t + step, vb);
-  while (t < ntiles) {
-    stage(t, va);
-    fetch(t + 2 * step, va);  // two tiles in flight while this one computes
-    compute(t);
-    t += step;
-    if (t >= ntiles) break;
-    stage(t, vb);
-    fetch(t + 2 * step, vb);
-    compute(t);
-    t += step;
-  }
-}
-
-__host__ __device__ inline size_t assign_bf16q_lds(int ktiles, int nsteps, int dim) {
-  return (size_t)ktiles * nsteps * 64 * 16 + (size_t)ktiles * 32 * sizeof(float) +
-         (size_t)4 * (32 * dim + 16) * sizeof(float);
-}
-
 // ---------------------------------------------------------------------------------------------
 // small batches (minibatch steps): one block of WAVES waves per 32 points. Wave w owns centre tiles
 // w, w+WAVES, ...; it stages its tile (and, without cached norms, their numpy-order norms) in LDS,
@@ -1759,6 +1608,12 @@ int resident_blocks(const void* fn, int threads, size_t lds, int* out) {
   return GDD_OK;
 }
 
+}  // namespace
+int gdd::occupancy_blocks(const void* fn, int threads, size_t lds, int* out) {
+  return resident_blocks(fn, threads, lds, out);
+}
+namespace {
+
 // LDS bytes of k_assign for a given geometry
 size_t assign_lds(int waves, int dimp, int cch) {
   const int S = dimp + 1;
@@ -2052,25 +1907,18 @@ extern "C" int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const 
       const int nfr = std::max(ktiles * nsteps * 64, ktiles * 32);
       k_bf16_frags<<<(nfr + 255) / 256, 256, 0, s>>>(dim, nsteps, ktiles, k, C, c_norm2, frags, cn);
       GDD_LAUNCHED();
-      const bool v1 = !forced("bf16_v2");  // A/B (r06): the VALU-lean kernel, opt-in until measured
-      const size_t ldsq = assign_bf16q_lds(ktiles, nsteps, dim);
+      // the r06 kernel (gdd_bf16.hip) where its shapes allow; GDD_FORCE=bf16_v1: the r03 kernel (A/B)
+      if (!forced("bf16_v1") && n >= 32 && nsteps <= 4 && dim % 16 != 0)
+        return bf16q_launch(n, dim, X, k, C, c_norm2, labels, sq_dist, ws, ws_bytes, s);
       auto go = [&](auto P_) -> int {
         constexpr int P = decltype(P_)::value;
-        const void* fn = v1 ? (const void*)k_assign_bf16p<P>
-                            : (dim % 4 == 0 ? (const void*)k_assign_bf16q<P, true> : (const void*)k_assign_bf16q<P, false>);
-        const size_t l = v1 ? lds : ldsq;
-        GDD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l));
+        const void* fn = (const void*)k_assign_bf16p<P>;
+        GDD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         int res = 0;
-        const int rrc = resident_blocks(fn, 256, l, &res);
+        const int rrc = resident_blocks(fn, 256, lds, &res);
         if (rrc) return rrc;
-        const int64_t resident = res;
-        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 3) / 4, resident));
-        if (v1)
-          k_assign_bf16p<P><<<grid, 256, l, s>>>(n, dim, nsteps, ktiles, X, k, frags, cn, C, labels, sq_dist);
-        else if (dim % 4 == 0)
-          k_assign_bf16q<P, true><<<grid, 256, l, s>>>(n, dim, nsteps, ktiles, X, k, frags, cn, C, labels, sq_dist);
-        else
-          k_assign_bf16q<P, false><<<grid, 256, l, s>>>(n, dim, nsteps, ktiles, X, k, frags, cn, C, labels, sq_dist);
+        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 3) / 4, (int64_t)res));
+        k_assign_bf16p<P><<<grid, 256, lds, s>>>(n, dim, nsteps, ktiles, X, k, frags, cn, C, labels, sq_dist);
         GDD_LAUNCHED();
         return GDD_OK;
       };

@@ -15,6 +15,10 @@ import torch  # noqa: E402
 from gdd.kmeans import _Ops  # noqa: E402
 
 SHAPES = {"products": (2449029, 47, 196), "arxiv": (169343, 40, 454), "reddit": (153932, 41, 769)}
+SHAPES = {k: v for k, v in SHAPES.items() if k in os.environ.get("MICRO_SHAPES", ",".join(SHAPES)).split(",")}
+# variant -> GDD_FORCE tokens (A/B of the r06 kernel's forms; "" = the library default)
+VARIANTS = dict(v.split("=", 1) for v in os.environ.get(
+    "BF16_VARIANTS", "v1=;q2=bf16_v2;q3=bf16_v2,bf16_depth3;q4=bf16_v2,bf16_depth4;q2t=bf16_v2,bf16_temporal").split(";"))
 
 
 def timed(fn, reps=20):
@@ -37,11 +41,11 @@ def main():
              (torch.randn(100, dim, device="cuda", generator=g) / 10.0)).contiguous()
         C = X[torch.randperm(n, device="cuda", generator=g)[:k]].contiguous()
         ops = _Ops("cuda", n, k, dim)
-        labs, times = {}, {"v1": [], "v2": []}
+        labs, times = {}, {v: [] for v in VARIANTS}
         for rnd in range(3):
-            for v in ("v1", "v2"):
-                if v == "v2":
-                    os.environ["GDD_FORCE"] = "bf16_v2"
+            for v, tok in VARIANTS.items():
+                if tok:
+                    os.environ["GDD_FORCE"] = tok
                 else:
                     os.environ.pop("GDD_FORCE", None)
                 lab = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -53,8 +57,8 @@ def main():
         ms = {v: min(t) for v, t in times.items()}
         res[name] = {"n": n, "dim": dim, "k": k, "ms": ms, "all_ms": times,
                      "x_read_frac_of_8TBs": {v: 4.0 * n * dim / (m * 1e-3) / 8e12 for v, m in ms.items()},
-                     "labels_identical_v1_v2": bool(torch.equal(labs["v1"], labs["v2"])),
-                     "agreement_with_fp32": float((labs["v2"] == l32).float().mean())}
+                     "labels_identical": {v: bool(torch.equal(labs[v], labs["v1"])) for v in labs},
+                     "agreement_with_fp32": float((labs["v1"] == l32).float().mean())}
         print(name, json.dumps(res[name]), flush=True)
     print(json.dumps(res), flush=True)
 
