@@ -3,27 +3,35 @@
 // -mllvm -amdgpu-mfma-vgpr-form (Makefile), so the MFMA accumulators live in VGPRs and the epilogue
 // reads them without v_accvgpr_read copies; the fp32 kernels of gdd_kmeans.hip keep the default.
 //
-// HBM design point: X is read once (460 MB at 2.45M x 47: ~58 us at 8 TB/s). The r03 kernel
-// (gdd_kmeans.hip k_assign_bf16p, GDD_FORCE=bf16_v1) ran at 0.36 of that roof; its counters
-// (rocprofv3, profiles/r06_bf16_pmc.json) put the limit in the VALU: ~925 vector instructions per
-// 32-point tile, each 4 cycles of its SIMD (SQ_ACTIVE_INST_VALU = SQ_INSTS_VALU quad-cycles). Here:
+// HBM design point: X is read once (460 MB at 2.45M x 47: ~58 us at 8 TB/s; torch's own X.sum() takes
+// 121 us on the same box). The r03 kernel (gdd_kmeans.hip k_assign_bf16p, GDD_FORCE=bf16_v1) ran at
+// 0.36 of that roof; its counters (rocprofv3, profiles/r06_bf16_pmc.json) put the limit in the VALU:
+// ~780 vector instructions per 32-point tile, each 4 cycles of its SIMD. Here ~340:
+//   * one launch: every block builds the centres' A-fragments ([tile][k-step][lane] x 8 bf16) and
+//     their -||c||^2 / 2 in its LDS from C, after issuing its first X loads (r06 first form: a
+//     separate fragment kernel, ~5 us plus a launch gap per call);
 //   * a tile's 32 x dim floats are ONE contiguous span of X, copied into the wave's LDS slot as is
 //     (float4 stores, row stride dim: no index arithmetic); B-fragments read row r's features
 //     16 st + 8 h .. + 7 straight from it (two ds_read_b128 when dim % 4 == 0, else eight
 //     ds_read_b32), features past dim masked to zero;
-//   * the argmin runs on integer keys. The first free K slot (feature dim; the pass needs
-//     dim % 16 != 0) carries -||x||^2 / 2 in the B-fragment and 1.0 in every centre's A-fragment,
-//     so the chain yields x.c - ||x||^2 / 2 and fma(-2, acc, ||c||^2) is the squared distance,
-//     non-negative up to rounding: its float bits order as signed integers. The centre's in-tile
-//     index goes into the 5 low significand bits (one v_and_or_b32), the lane's 16 keys reduce by
-//     v_min3_i32, one compare per centre tile — per centre an fma and an and_or, where the r03
-//     epilogue spent an fma, a compare and two selects (plus a copy out of the accumulator).
+//   * the whole distance comes out of the MFMA chain: the accumulator STARTS at -||c||^2 / 2 (fp32,
+//     exact), and the first free K slot (feature dim; the pass needs dim % 16 != 0) carries
+//     -(||x||^2 / 2 + delta) in the B-fragment against 1.0 in every centre's A-fragment, so the
+//     chain yields acc = -(d / 2 + delta), d the squared distance;
+//   * the argmin runs on integer keys: acc < 0 always (below), and the bits of negative floats order
+//     as signed integers like their magnitudes, so the smallest key is the nearest centre. The
+//     centre's in-tile index goes into the 5 low significand bits (one v_and_or_b32 per centre: a
+//     larger index adds magnitude, the lower index wins a tie), and a balanced v_min3_i32 tree takes
+//     the tile's 16 keys per lane (8 per centre tile) — per centre 1.5 VALU, where the r03 epilogue
+//     spent an fma, a compare and two selects (plus a copy out of the accumulator).
 // Accuracy: the labels are those of bf16 dot products (tests/test_gpu_kmeans.py and
 // tests/test_gpu_configs.py bound every label that differs from the exact fp32 one by the bf16
-// rounding, 2^-7 ||x|| ||c|| per product). The shift by ||x||^2 is the same for every centre of a
-// point, so its own bf16 rounding cannot reorder them; dropping 5 of the 24 significand bits moves a
-// distance by < 2^-18 of itself; keys that tie may pick either centre, and a distance that rounds
-// below zero (a point on a centre) is a negative key, i.e. a winner, as it should be.
+// rounding, 2^-7 ||x|| ||c|| per product). delta = 2^-5 ||x||^2 + 2^-100 keeps acc strictly negative:
+// a centre whose acc crossed zero would need d / 2 < 2^-7 ||x|| ||c|| + 2^-10 ||x||^2 (product and
+// shift roundings) - delta, impossible for ||c|| <= 3.8 ||x|| (the right side is negative) and for
+// larger ||c|| (then d >= (||c|| - ||x||)^2 is far above it); the shift is the same for every centre
+// of a point, so neither it nor its bf16 rounding reorders them. Dropping 5 of the 24 significand
+// bits moves a key by < 2^-18 of |acc|; keys that tie may pick either centre.
 #include <algorithm>
 #include <type_traits>
 
@@ -36,51 +44,23 @@ using floatx16 = __attribute__((ext_vector_type(16))) float;
 typedef float floatx4_t __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
-inline size_t frag_bytes(int ktiles, int nsteps) {
-  return (size_t)ktiles * nsteps * 64 * 16 + (size_t)ktiles * 32 * sizeof(float);
+inline size_t bf16q_lds(int ktiles, int nsteps, int dim, int waves) {
+  return (size_t)ktiles * nsteps * 64 * 16 + (size_t)ktiles * 32 * sizeof(float) +
+         (size_t)waves * (32 * dim + 16) * sizeof(float);
 }
 
-inline size_t bf16q_lds(int ktiles, int nsteps, int dim) {
-  return frag_bytes(ktiles, nsteps) + (size_t)4 * (32 * dim + 16) * sizeof(float);
-}
-
-// the A-fragments of every centre tile ([tile][k-step][lane] x 8 bf16: centre ct*32 + (lane & 31),
-// features 16 st + 8 (lane >> 5) ..) with 1.0 at feature dim (the -||x||^2 / 2 slot), and the norms
-// (+inf past k), once per call
-__global__ void k_bf16q_frags(int dim, int nsteps, int ktiles, int k, const float* __restrict__ C,
-                              const float* __restrict__ cn2, bf16x8_t* __restrict__ frags,
-                              float* __restrict__ cn_out) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < ktiles * nsteps * 64) {
-    const int l = e & 63, rest = e >> 6;
-    const int st = rest % nsteps, ct = rest / nsteps;
-    const int c = ct * 32 + (l & 31), f0 = 16 * st + 8 * (l >> 5);
-    bf16x8_t v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int f = f0 + j;
-      v[j] = (__bf16)(f == dim ? 1.0f : ((c < k && f < dim) ? C[(int64_t)c * dim + f] : 0.f));
-    }
-    frags[e] = v;
-  }
-  if (e < ktiles * 32) cn_out[e] = e < k ? cn2[e] : __builtin_inff();
-}
-
+// the key: acc's bits with the in-tile index in the 5 low significand bits (one v_and_or_b32). Plain C,
+// not inline asm: an asm operand that reads an MFMA result directly is invisible to the compiler's
+// hazard recognizer (no wait states after the MFMA: stale accumulator values — r06, measured)
 __device__ __forceinline__ int key_with_index(float d, int idx) {
-  int out;
-  // one v_and_or_b32 (the mask comes from an SGPR: a VOP3 literal is not available on gfx950)
-  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(out) : "v"(d), "s"(0xffffffe0u), "n"(idx));
-  return out;
+  return (int)((__float_as_uint(d) & 0xffffffe0u) | (unsigned)idx);
 }
 
-template <int PER, int NST, bool VEC4>
-__global__ __launch_bounds__(256) void k_assign_bf16q(int64_t n, int dim, int ktiles,
-                                                      const float* __restrict__ X,
-                                                      const bf16x8_t* __restrict__ frags,
-                                                      const float* __restrict__ cn_in,
-                                                      const float* __restrict__ C,
-                                                      int32_t* __restrict__ labels,
-                                                      float* __restrict__ sq_dist) {
+// W waves per block, D tiles' loads in flight per wave, WPE the waves per SIMD the registers allow
+template <int PER, int NST, bool VEC4, int W, int D, int WPE>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) void k_assign_bf16q(
+    int64_t n, int dim, int k, int ktiles, const float* __restrict__ X, const float* __restrict__ C,
+    const float* __restrict__ cn2, int32_t* __restrict__ labels, float* __restrict__ sq_dist) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16x8_t* Af = reinterpret_cast<bf16x8_t*>(smem);
   float* Cn = reinterpret_cast<float*>(smem + (size_t)ktiles * NST * 64 * 16);
@@ -88,17 +68,10 @@ __global__ __launch_bounds__(256) void k_assign_bf16q(int64_t n, int dim, int kt
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, r = lane & 31;
   const int slot = 32 * dim + 16;  // floats per wave slot (a multiple of 4: dim x 32 is)
-  {  // the prebuilt fragments and norms: coalesced 16-byte copies
-    const int nfr = ktiles * NST * 64;
-    for (int e = tid; e < nfr; e += 256) Af[e] = frags[e];
-    for (int c = tid; c < ktiles * 32; c += 256) Cn[c] = cn_in[c];
-  }
   float* my = Pt + wave * slot;
-  if (lane < 16) my[32 * dim + lane] = 0.f;  // past the last row: read by row 31's masked features
-  __syncthreads();
   const int nf4 = 8 * dim;  // float4 per full tile (32 rows x dim floats)
   const int64_t ntiles = (n + 31) / 32, nfull = n / 32;
-  const int64_t step = (int64_t)gridDim.x * 4;
+  const int64_t step = (int64_t)gridDim.x * W;
   // every load unconditional (a tile past the full ones re-reads the last full tile, unused), so the
   // compiler's vmcnt waits count exactly PER loads per tile and the next tile's stay in flight
   auto fetch = [&](int64_t tt, floatx4_t (&v)[PER]) {
@@ -145,7 +118,8 @@ __global__ __launch_bounds__(256) void k_assign_bf16q(int64_t n, int dim, int kt
       for (int j = 0; j < 8; ++j) xx = __builtin_fmaf(x[st][j], x[st][j], xx);
     }
     const float oxx = __shfl_xor(xx, 32);
-    const float shift = -0.5f * (h ? oxx + xx : xx + oxx);  // the same value on both halves
+    const float xsq = h ? oxx + xx : xx + oxx;  // the same value on both halves
+    const float shift = -__builtin_fmaf(0.53125f, xsq, 0x1p-100f);  // -(||x||^2 / 2 + delta), header
     bf16x8_t b[NST];
 #pragma unroll
     for (int st = 0; st < NST; ++st) {
@@ -159,30 +133,31 @@ __global__ __launch_bounds__(256) void k_assign_bf16q(int64_t n, int dim, int kt
     int bestk = 0x7fffffff;
     int bestct = 0;
     auto chain = [&](int c) {
-      floatx16 acc = {};
+      floatx16 acc;  // rows 8g + 4h .. + 3 of centre tile c: -||c||^2 / 2
+      const floatx4_t* cp = reinterpret_cast<const floatx4_t*>(Cn + c * 32 + 4 * h);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const floatx4_t v = cp[2 * g];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[4 * g + j] = v[j];
+      }
 #pragma unroll
       for (int st = 0; st < NST; ++st)
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Af[(c * NST + st) * 64 + lane], b[st], acc, 0, 0, 0);
       return acc;
     };
     auto epilogue = [&](const floatx16& acc, int ct) {
-      const floatx4_t* cp = reinterpret_cast<const floatx4_t*>(Cn + ct * 32 + 4 * h);
-      int e[16];
-      const floatx4_t cn0 = cp[0], cn1 = cp[2], cn2 = cp[4], cn3 = cp[6];  // rows 8g + 4h .. +3
-#define GDD_KEY(g, j) e[4 * g + j] = key_with_index(__builtin_fmaf(-2.f, acc[4 * g + j], cn##g[j]), 8 * g + j)
-      GDD_KEY(0, 0); GDD_KEY(0, 1); GDD_KEY(0, 2); GDD_KEY(0, 3);
-      GDD_KEY(1, 0); GDD_KEY(1, 1); GDD_KEY(1, 2); GDD_KEY(1, 3);
-      GDD_KEY(2, 0); GDD_KEY(2, 1); GDD_KEY(2, 2); GDD_KEY(2, 3);
-      GDD_KEY(3, 0); GDD_KEY(3, 1); GDD_KEY(3, 2); GDD_KEY(3, 3);
-#undef GDD_KEY
-      int m = min(e[0], min(e[1], e[2]));
+      int e[16];  // acc = -(d / 2 + delta) < 0: its bits order as signed integers like d
 #pragma unroll
-      for (int q = 3; q < 15; q += 2) m = min(m, min(e[q], e[q + 1]));
-      m = min(m, e[15]);
-      if (m < bestk) {
-        bestk = m;
-        bestct = ct;
-      }
+      for (int q = 0; q < 16; ++q) e[q] = key_with_index(acc[q], 8 * (q >> 2) + (q & 3));
+      // a balanced v_min3_i32 tree (8 per centre tile), the running best folded into its root
+      const int m1 = min(e[0], min(e[1], e[2])), m2 = min(e[3], min(e[4], e[5]));
+      const int m3 = min(e[6], min(e[7], e[8])), m4 = min(e[9], min(e[10], e[11]));
+      const int m5 = min(e[12], min(e[13], e[14]));
+      const int m6 = min(m1, min(m2, m3)), m7 = min(m4, min(m5, e[15]));
+      const int m = min(bestk, min(m6, m7));
+      if (m != bestk) bestct = ct;
+      bestk = m;
     };
     int ct = 0;
     for (; ct + 2 <= ktiles; ct += 2) {
@@ -205,11 +180,75 @@ __global__ __launch_bounds__(256) void k_assign_bf16q(int64_t n, int dim, int kt
       if (sq_dist) sq_dist[p] = skl_sqdist(row, C + (int64_t)bestc * dim, dim);
     }
   };
-  // two tiles' loads in flight per wave (three or four measured the same: the pass did not wait on HBM)
+  // D = 2: two tiles' loads in flight per wave (three or four measured the same: the pass does not wait
+  // on HBM); D = 1 (the 8-wave form): one, the registers go to occupancy instead
   floatx4_t va[PER], vb[PER];
-  int64_t t = (int64_t)blockIdx.x * 4 + wave;
+  int64_t t = (int64_t)blockIdx.x * W + wave;
   fetch(t, va);
-  fetch(t + step, vb);
+  if constexpr (D == 2) fetch(t + step, vb);
+  {  // the centre tiles, while the first X loads are in flight: A-fragments (centre ct * 32 + (lane &
+     // 31), features 16 st + 8 (lane >> 5) .., 1.0 at feature dim, zero past it and past k) and
+     // -||c||^2 / 2 (-inf past k: never the minimum). U fragments per thread per round, their loads
+     // issued together (L2 latency once per round, not per fragment). Without given norms each
+     // fragment leaves its 8 features' sum of squares in the (not yet used) wave slots, summed per
+     // centre in a fixed order after the barrier: ||c||^2 in fp32, deterministic.
+    constexpr int U = W == 8 ? 4 : 6;  // (8 waves: within the 128 VGPRs of WPE = 4)
+    float* part = Pt;  // [centre][2 NST] partial sums (bf16q_norms_fit: they fit the wave slots)
+    const int nfr = ktiles * NST * 64;
+    for (int e0 = tid; e0 < nfr; e0 += 64 * W * U) {
+      float v[U][8];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + u * 64 * W, l = e & 63, rest = e >> 6;
+        const int st = rest % NST, ct = rest / NST;
+        const int c = ct * 32 + (l & 31), f0 = 16 * st + 8 * (l >> 5);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[u][j] = (e < nfr && c < k && f0 + j < dim) ? C[(int64_t)c * dim + f0 + j] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + u * 64 * W, l = e & 63, rest = e >> 6;
+        if (e >= nfr) break;
+        const int st = rest % NST, ct = rest / NST;
+        const int f0 = 16 * st + 8 * (l >> 5);
+        bf16x8_t fr;
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          fr[j] = (__bf16)(f0 + j == dim ? 1.0f : v[u][j]);
+          ss = __builtin_fmaf(v[u][j], v[u][j], ss);
+        }
+        Af[e] = fr;
+        if (!cn2) part[(ct * 32 + (l & 31)) * (2 * NST) + 2 * st + (l >> 5)] = ss;
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < ktiles * 32; c += 64 * W) {
+      float v = __builtin_inff();
+      if (c < k) {
+        if (cn2) {
+          v = cn2[c];
+        } else {
+          v = 0.f;
+#pragma unroll
+          for (int q = 0; q < 2 * NST; ++q) v += part[c * (2 * NST) + q];
+        }
+      }
+      Cn[c] = -0.5f * v;
+    }
+    __syncthreads();
+    if (lane < 16) my[32 * dim + lane] = 0.f;  // past the last row: read by row 31's masked features
+  }
+  if constexpr (D == 1) {
+    while (t < ntiles) {
+      stage(t, va);
+      fetch(t + step, va);
+      compute(t);
+      t += step;
+    }
+    return;
+  }
   while (t < ntiles) {
     stage(t, va);
     fetch(t + 2 * step, va);
@@ -223,41 +262,53 @@ __global__ __launch_bounds__(256) void k_assign_bf16q(int64_t n, int dim, int kt
   }
 }
 
+
 }  // namespace
 
+bool bf16q_norms_fit(int dim, int k) {
+  const int nsteps = (dim + 15) / 16, ktiles = (k + 31) / 32;
+  return (int64_t)ktiles * 32 * 2 * nsteps <= (int64_t)4 * (32 * dim + 16);  // the 4-wave slots
+}
+
 int bf16q_launch(int64_t n, int dim, const float* X, int k, const float* C, const float* c_norm2,
-                 int32_t* labels, float* sq_dist, void* ws, size_t ws_bytes, hipStream_t s) {
+                 int32_t* labels, float* sq_dist, hipStream_t s) {
   const int nsteps = (dim + 15) / 16, ktiles = (k + 31) / 32;
   GDD_REQUIRE(n >= 32 && dim % 16 != 0 && nsteps <= 4 && k > 0, "bf16 labels pass: unsupported shape");
   GDD_REQUIRE((reinterpret_cast<uintptr_t>(X) & 15) == 0, "bf16 labels pass: X must be 16-byte aligned");
-  GDD_REQUIRE(frag_bytes(ktiles, nsteps) <= ws_bytes, "bf16 labels pass: workspace too small");
-  const size_t lds = bf16q_lds(ktiles, nsteps, dim);
+  GDD_REQUIRE(c_norm2 || bf16q_norms_fit(dim, k), "bf16 labels pass: this k needs the norms given");
+  // at three k-steps (the configs' logit widths 41 .. 47) with many centre tiles, 8-wave blocks with
+  // one tile's loads in flight and at most 128 VGPRs (4 waves per SIMD): Reddit's k = 769 at 0.84 of
+  // the 4-wave form's time, products' k = 196 the same within noise (r06, tools/micro_bf16.py).
+  // GDD_FORCE=bf16_w4 / bf16_w8: either form at any k (A/B, tests)
+  const bool f3 = nsteps == 3 && dim % 4 != 0 && (8 * dim + 63) / 64 == 6;
+  const bool w8 = f3 && !forced("bf16_w4") && (ktiles > 8 || forced("bf16_w8"));
+  const int waves = w8 ? 8 : 4;
+  const size_t lds = bf16q_lds(ktiles, nsteps, dim, waves);
   GDD_REQUIRE(lds <= 150 * 1024, "bf16 labels pass: centres do not fit the LDS");
-  bf16x8_t* frags = static_cast<bf16x8_t*>(ws);
-  float* cn = reinterpret_cast<float*>(static_cast<char*>(ws) + (size_t)ktiles * nsteps * 64 * 16);
-  const int nfr = std::max(ktiles * nsteps * 64, ktiles * 32);
-  k_bf16q_frags<<<(nfr + 255) / 256, 256, 0, s>>>(dim, nsteps, ktiles, k, C, c_norm2, frags, cn);
-  GDD_LAUNCHED();
   const int64_t ntiles = (n + 31) / 32;
   const int per_need = (8 * dim + 63) / 64;
   auto go = [&](auto kern) -> int {
     GDD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int res = 0;
-    const int rc = occupancy_blocks((const void*)kern, 256, lds, &res);
+    const int rc = occupancy_blocks((const void*)kern, 64 * waves, lds, &res);
     if (rc) return rc;
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 3) / 4, (int64_t)res));
-    kern<<<grid, 256, lds, s>>>(n, dim, ktiles, X, frags, cn, C, labels, sq_dist);
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + waves - 1) / waves, (int64_t)res));
+    kern<<<grid, 64 * waves, lds, s>>>(n, dim, k, ktiles, X, C, c_norm2, labels, sq_dist);
     GDD_LAUNCHED();
     return GDD_OK;
   };
   auto pick_per = [&](auto N_, auto V_) -> int {
     constexpr int N = decltype(N_)::value;
     constexpr bool V = decltype(V_)::value;
-    if (per_need <= 1) return go(k_assign_bf16q<1, N, V>);
-    if (per_need <= 2) return go(k_assign_bf16q<2, N, V>);
-    if (per_need <= 4) return go(k_assign_bf16q<4, N, V>);
-    if (per_need <= 6) return go(k_assign_bf16q<6, N, V>);
-    return go(k_assign_bf16q<8, N, V>);
+    if (per_need <= 1) return go(k_assign_bf16q<1, N, V, 4, 2, 1>);
+    if (per_need <= 2) return go(k_assign_bf16q<2, N, V, 4, 2, 1>);
+    if (per_need <= 4) return go(k_assign_bf16q<4, N, V, 4, 2, 1>);
+    if (per_need <= 6) {
+      if constexpr (N == 3 && !V)  // dims 41 .. 47
+        if (w8) return go(k_assign_bf16q<6, 3, false, 8, 1, 4>);
+      return go(k_assign_bf16q<6, N, V, 4, 2, 1>);
+    }
+    return go(k_assign_bf16q<8, N, V, 4, 2, 1>);
   };
   using T_ = std::true_type;
   using F_ = std::false_type;

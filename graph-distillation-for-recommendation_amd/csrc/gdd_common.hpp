@@ -87,10 +87,12 @@ int sort_pairs_i32(const int32_t* keys_in, int32_t* keys_out, const int32_t* val
 // ---------------------------------------------------------------------------------------------
 // resident workgroups of a kernel on the current device (occupancy x CUs; cached)
 int occupancy_blocks(const void* fn, int threads, size_t lds, int* out);
-// the bf16 full labels pass's r06 kernel (gdd_bf16.hip): n >= 32, dim <= 64, 16-byte aligned X, whole
-// rows; the workspace holds the centres' fragments (bf16_frag_bytes)
+// the bf16 full labels pass's r06 kernel (gdd_bf16.hip): n >= 32, dim <= 64 and not a multiple of 16,
+// 16-byte aligned X, whole rows; one launch, no workspace (c_norm2 may be null if bf16q_norms_fit)
 int bf16q_launch(int64_t n, int dim, const float* X, int k, const float* C, const float* c_norm2,
-                 int32_t* labels, float* sq_dist, void* ws, size_t ws_bytes, hipStream_t s);
+                 int32_t* labels, float* sq_dist, hipStream_t s);
+// whether bf16q_launch can take the centres' norms itself (c_norm2 null) at this dim and k
+bool bf16q_norms_fit(int dim, int k);
 
 // GDD_FORCE (tests and diagnostics only): a comma-separated list of tokens, each forcing a path that
 // other shapes take by default (so its bits can be pinned on a small shape), e.g.
@@ -108,6 +110,8 @@ int bf16q_launch(int64_t n, int dim, const float* X, int k, const float* C, cons
 //   fold_slice=F      M-step clusters above F x the mean size fold in slices (default 1.5; 0: off)
 //   group_split       the multi-launch label grouping where the one-launch form fits
 //   center_seq        KMeans' centring by the sequential column chains
+//   bf16_v1           the r03 bf16 labels pass (gdd_kmeans.hip) instead of the r06 one (gdd_bf16.hip)
+//   bf16_w4, bf16_w8  the r06 pass's 4- or 8-wave block form at any k (dims 41 .. 47)
 bool forced(const char* token);
 double forced_value(const char* token, double dflt);
 

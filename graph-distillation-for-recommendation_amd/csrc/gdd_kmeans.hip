@@ -1888,10 +1888,23 @@ extern "C" int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const 
                                       const float* C, const float* c_norm2, int32_t* labels,
                                       float* sq_dist, void* ws, size_t ws_bytes, gdd_stream_t stream) {
   GDD_REQUIRE(n > 0 && dim > 0 && dim <= 512 && k > 0, "kmeans_assign_bf16: bad shape");
-  GDD_REQUIRE(X && C && c_norm2 && labels && ws, "kmeans_assign_bf16: null pointer");
+  GDD_REQUIRE(X && C && labels && ws, "kmeans_assign_bf16: null pointer");
   if (ws_bytes < gdd_kmeans_assign_ws_bytes(n))
     return fail(GDD_E_WORKSPACE, "kmeans_assign_bf16: workspace too small");
   hipStream_t s = to_hip(stream);
+  float* cn_tmp = nullptr;  // c_norm2 NULL: the r06 pass computes them in its fragment kernel, the
+  auto own_norms = [&]() -> int {  // other forms here, into a stream-ordered temporary
+    if (c_norm2) return GDD_OK;
+    GDD_HIP(hipMallocAsync(reinterpret_cast<void**>(&cn_tmp), sizeof(float) * (size_t)k, s));
+    k_row_norms<<<blocks_for(k), 256, 0, s>>>(k, dim, C, cn_tmp, nullptr, 0);
+    GDD_LAUNCHED();
+    c_norm2 = cn_tmp;
+    return GDD_OK;
+  };
+  auto done = [&](int rc) -> int {
+    if (cn_tmp) GDD_HIP(hipFreeAsync(cn_tmp, s));
+    return rc;
+  };
   unsigned long long* keys = static_cast<unsigned long long*>(ws);
   const int dimp16 = (dim + 15) & ~15;
   {  // the persistent kernel: whole rows (no gathered rows), dim <= 128, centre fragments fit LDS
@@ -1901,26 +1914,30 @@ extern "C" int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const 
     const bool aligned = (reinterpret_cast<uintptr_t>(X) & 15) == 0;
     const size_t fb = bf16_frag_bytes(ktiles, nsteps);
     if (!rows && dim <= 128 && aligned && lds <= 150 * 1024 && fb <= ws_bytes) {
+      // the r06 kernel (gdd_bf16.hip) where its shapes allow; GDD_FORCE=bf16_v1: the r03 kernel (A/B)
+      if (!forced("bf16_v1") && n >= 32 && nsteps <= 4 && dim % 16 != 0) {
+        if (!bf16q_norms_fit(dim, k))
+          if (const int rc = own_norms()) return rc;
+        return done(bf16q_launch(n, dim, X, k, C, c_norm2, labels, sq_dist, s));
+      }
+      if (const int rc = own_norms()) return rc;
       const int64_t ntiles = (n + 31) / 32;
       bf16x8_t* frags = static_cast<bf16x8_t*>(ws);  // the keys are not used on this path
       float* cn = reinterpret_cast<float*>(static_cast<char*>(ws) + (size_t)ktiles * nsteps * 64 * 16);
       const int nfr = std::max(ktiles * nsteps * 64, ktiles * 32);
       k_bf16_frags<<<(nfr + 255) / 256, 256, 0, s>>>(dim, nsteps, ktiles, k, C, c_norm2, frags, cn);
       GDD_LAUNCHED();
-      // the r06 kernel (gdd_bf16.hip) where its shapes allow; GDD_FORCE=bf16_v1: the r03 kernel (A/B)
-      if (!forced("bf16_v1") && n >= 32 && nsteps <= 4 && dim % 16 != 0)
-        return bf16q_launch(n, dim, X, k, C, c_norm2, labels, sq_dist, ws, ws_bytes, s);
       auto go = [&](auto P_) -> int {
         constexpr int P = decltype(P_)::value;
         const void* fn = (const void*)k_assign_bf16p<P>;
         GDD_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         int res = 0;
         const int rrc = resident_blocks(fn, 256, lds, &res);
-        if (rrc) return rrc;
+        if (rrc) return done(rrc);
         const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ntiles + 3) / 4, (int64_t)res));
         k_assign_bf16p<P><<<grid, 256, lds, s>>>(n, dim, nsteps, ktiles, X, k, frags, cn, C, labels, sq_dist);
         GDD_LAUNCHED();
-        return GDD_OK;
+        return done(GDD_OK);
       };
       if (per_need <= 1) return go(std::integral_constant<int, 1>());
       if (per_need <= 2) return go(std::integral_constant<int, 2>());
@@ -1942,6 +1959,7 @@ extern "C" int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const 
     gy = (k + cch - 1) / cch;
   }
   GDD_REQUIRE(gx < (1ll << 31) && gy < 65536, "kmeans_assign_bf16: grid too large");
+  if (const int rc = own_norms()) return rc;
   const size_t lds = assign_bf16_lds(kWaves, dimp16, cch);
   k_fill_u64<<<blocks_for(n), 256, 0, s>>>(n, keys, ~0ull, nullptr, 0);
   GDD_LAUNCHED();
@@ -1950,7 +1968,7 @@ extern "C" int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const 
   GDD_LAUNCHED();
   k_assign_finalize<<<blocks_for(n), 256, 0, s>>>(n, dim, X, rows, C, keys, labels, sq_dist, nullptr, 0);
   GDD_LAUNCHED();
-  return GDD_OK;
+  return done(GDD_OK);
 }
 
 

@@ -69,12 +69,13 @@ class _Ops:
 
     def assign(self, X, C, rows=None, labels=None, sq=None, n=None, precision="fp32"):
         n = (rows.shape[0] if rows is not None else X.shape[0]) if n is None else n
-        cn2 = self.row_norms(C)
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        # bf16: the library takes the centres' norms itself (c_norm2 NULL, gdd.h)
+        cn2 = self.row_norms(C) if precision == "fp32" else None
         fn = self.lib.gdd_kmeans_assign if precision == "fp32" else self.lib.gdd_kmeans_assign_bf16
         _lib.check(fn(
-            n, self.dim, X.data_ptr(), _lib.ptr(rows), C.shape[0], C.data_ptr(), cn2.data_ptr(),
+            n, self.dim, X.data_ptr(), _lib.ptr(rows), C.shape[0], C.data_ptr(), _lib.ptr(cn2),
             labels.data_ptr(), _lib.ptr(sq), self.ws_assign.data_ptr(), self.ws_assign.numel(),
             self.stream))
 

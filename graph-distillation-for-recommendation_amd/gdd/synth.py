@@ -87,11 +87,12 @@ def chung_lu_device(n: int, avg_degree: float, seed: int, device="cuda"):
 
 
 def sbm_device(n: int, avg_degree: float, seed: int, block: int = 1024, p_in: float = 0.9,
-               shuffle: bool = True, device="cuda"):
+               shuffle: bool = True, device="cuda", return_perm: bool = False):
     """A community-structured graph (stochastic block model: blocks of `block` consecutive nodes, a
     fraction p_in of each node's edges inside its block, the rest uniform), symmetric, binary, no
     self-loops, sampled on the device. With `shuffle` the node ids are permuted at random, as real
-    graphs' ids carry no locality order. Returns a gdd CSRGraph."""
+    graphs' ids carry no locality order. Returns a gdd CSRGraph (and, with `return_perm`, the id
+    permutation: block member i is node perm[i]; None without `shuffle`)."""
     import torch
     from .graph import CSRGraph
     g = torch.Generator(device=device)
@@ -104,6 +105,7 @@ def sbm_device(n: int, avg_degree: float, seed: int, block: int = 1024, p_in: fl
     dst_in = b0 + (torch.rand(m, device=device, generator=g) * bsz).long().clamp(max=block - 1)
     dst = torch.where(inside, torch.minimum(dst_in, torch.full_like(dst_in, n - 1)),
                       torch.randint(0, n, (m,), device=device, generator=g))
+    perm = None
     if shuffle:
         perm = torch.randperm(n, device=device, generator=g)
         src, dst = perm[src], perm[dst]
@@ -113,7 +115,8 @@ def sbm_device(n: int, avg_degree: float, seed: int, block: int = 1024, p_in: fl
     rows, col = keys // n, (keys % n).to(torch.int32)
     rowptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
     rowptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n), 0)
-    return CSRGraph(rowptr.to(torch.int32), col, None, n)
+    out = CSRGraph(rowptr.to(torch.int32), col, None, n)
+    return (out, perm) if return_perm else out
 
 
 def uniform_graph(n: int, avg_degree: float, seed: int) -> sp.csr_matrix:

@@ -132,7 +132,7 @@ int gdd_kmeans_assign(int64_t n, int dim, const float* X, const int64_t* rows, i
 /* bf16 distance variant (configs 2, 3, 5 carry fp32 and bf16 distances). Same        */
 /* arguments and outputs; the X and C operands are rounded to bf16 (nearest even) and the dot       */
 /* products run as v_mfma_f32_32x32x16_bf16 chains with fp32 accumulation; distances use the fp32    */
-/* c_norm2. NOT bit-compatible with sklearn: a label may differ where two centres' distances lie     */
+/* c_norm2 (NULL: computed on the device, no separate launch on the common shapes). NOT bit-compatible with sklearn: a label may differ where two centres' distances lie     */
 /* within the bf16 rounding of the dot products (|err| <= ~2^-7 ||x|| ||c||). sq_dist is the exact   */
 /* fp32 distance to the chosen centre.                                                              */
 int gdd_kmeans_assign_bf16(int64_t n, int dim, const float* X, const int64_t* rows, int k,

@@ -168,11 +168,16 @@ def test_minibatch_tol_path():
     assert abs(m.n_steps_ - ref["n_steps_"]) <= 1
 
 
-@pytest.mark.parametrize("n,dim,k", [(50000, 40, 454), (3000, 7, 70), (20000, 64, 200), (1000, 47, 1)])
-def test_assign_bf16_within_rounding(n, dim, k):
+@pytest.mark.parametrize("n,dim,k,form", [(50000, 40, 454, ""), (3000, 7, 70, ""), (20000, 64, 200, ""),
+                                          (1000, 47, 1, ""), (40000, 41, 769, ""), (40000, 41, 769, "bf16_w4"),
+                                          (9000, 45, 100, "bf16_w8"), (9000, 45, 100, "bf16_v1"),
+                                          (3000, 200, 30, "")])
+def test_assign_bf16_within_rounding(n, dim, k, form, monkeypatch):
     # the bf16 distance variant: labels equal the exact fp32 ones except where two
-    # centres' distances lie within the bf16 rounding of the dot products (2^-7 ||x|| ||c|| each)
+    # centres' distances lie within the bf16 rounding of the dot products (2^-7 ||x|| ||c|| each).
+    # form: the 4- or 8-wave block form of the r06 kernel, or the r03 kernel (gdd_bf16.hip)
     from gdd.kmeans import _Ops
+    force(monkeypatch, *([form] if form else []))
     rng = np.random.default_rng(n + k)
     X = (rng.standard_normal((n, dim)) + rng.integers(0, 5, (n, 1))).astype(np.float32)
     C = X[rng.choice(n, k, replace=False)] + rng.standard_normal((k, dim)).astype(np.float32) * 0.1
