@@ -112,6 +112,10 @@ bool bf16q_norms_fit(int dim, int k);
 //   center_seq        KMeans' centring by the sequential column chains
 //   bf16_v1           the r03 bf16 labels pass (gdd_kmeans.hip) instead of the r06 one (gdd_bf16.hip)
 //   bf16_w4, bf16_w8  the r06 pass's 4- or 8-wave block form at any k (dims 41 .. 47)
+//   hop_row_order     the propagation's work list in row order (no longest-first schedule)
+//   hop_no_probe      longest first even where the locality probe would pick row order
+//   hop_relabel_len   the relabelled hops' work list longest first instead of in the new order
+//   hop_xcd_contig    each XCD walks a contiguous eighth of the work list (one feature slice)
 bool forced(const char* token);
 double forced_value(const char* token, double dflt);
 

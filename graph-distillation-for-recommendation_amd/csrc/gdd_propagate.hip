@@ -104,11 +104,13 @@ __device__ __forceinline__ void vstore(float* p, const float (&r)[V]) {
 // ---- plan: per-row segment counts -> item offsets / partial offsets -> item records ----------
 // `order` (nullable): position i of the work list is row order[i] (rows scheduled longest first,
 // see build_plan); counts and offsets are indexed by position
+// rowwise (nullable): the locality probe's verdict (non-zero: ignore `order`, rows in row order)
 __global__ void k_seg_counts(int64_t n, const int32_t* __restrict__ rowptr,
-                             const int32_t* __restrict__ order, int32_t* nseg, int32_t* npart) {
+                             const int32_t* __restrict__ order, const int32_t* __restrict__ rowwise,
+                             int32_t* nseg, int32_t* npart) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int64_t r = order ? order[i] : i;
+  const int64_t r = (order && !(rowwise && *rowwise)) ? order[i] : i;
   int32_t len = rowptr[r + 1] - rowptr[r];
   int32_t s = len <= kSeg ? 1 : (len + kSeg - 1) / kSeg;
   nseg[i] = s;
@@ -116,12 +118,13 @@ __global__ void k_seg_counts(int64_t n, const int32_t* __restrict__ rowptr,
 }
 
 __global__ void k_make_items(int64_t n, const int32_t* __restrict__ rowptr,
-                             const int32_t* __restrict__ order, const int32_t* __restrict__ nseg, const int32_t* __restrict__ item_off,
+                             const int32_t* __restrict__ order, const int32_t* __restrict__ rowwise,
+                             const int32_t* __restrict__ nseg, const int32_t* __restrict__ item_off,
                              const int32_t* __restrict__ part_off, Item* items,
                              int32_t* long_rows, int32_t* long_off, int32_t* counts) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int32_t r = order ? order[i] : (int32_t)i;
+  const int32_t r = (order && !(rowwise && *rowwise)) ? order[i] : (int32_t)i;
   const int32_t b = rowptr[r], e = rowptr[r + 1], s = nseg[i], o = item_off[i];
   if (s == 1) {
     items[o] = Item{r, b, e, -1};
@@ -137,6 +140,37 @@ __global__ void k_make_items(int64_t n, const int32_t* __restrict__ rowptr,
     long_off[q] = po;
   }
   if (i == n - 1) counts[0] = o + s;  // number of items
+}
+
+// the locality probe (r06): kProbeRows rows sampled at a fixed stride, up to kProbeCap entries each;
+// if at least half of the sampled entries point within kProbeWindow rows of their own row, the graph's
+// ids carry locality (neighbours in nearby rows: a row range's gathers share lines in one L2) and
+// the hop walks the rows in order instead of longest first. One workgroup; *flag = 1 or 0.
+constexpr int kProbeRows = 4096;
+constexpr int kProbeCap = 64;
+constexpr int kProbeWindow = 4096;
+constexpr int64_t kProbeMinRows = 1000000;  // below: the longest-first schedule always (measured)
+__global__ __launch_bounds__(1024) void k_locality_probe(int64_t n, const int32_t* __restrict__ rowptr,
+                                                         const int32_t* __restrict__ col,
+                                                         int32_t* __restrict__ flag) {
+  __shared__ unsigned long long tot[2];
+  if (threadIdx.x < 2) tot[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned near = 0, all = 0;
+  const int64_t stride = n / kProbeRows;
+  for (int q = threadIdx.x; q < kProbeRows; q += blockDim.x) {
+    const int64_t r = q * stride;
+    const int32_t b = rowptr[r], e = min(rowptr[r + 1], b + kProbeCap);
+    for (int32_t p = b; p < e; ++p) {
+      const int64_t dlt = (int64_t)col[p] - r;
+      near += (dlt <= kProbeWindow && dlt >= -kProbeWindow) ? 1u : 0u;
+    }
+    all += (unsigned)(e - b);
+  }
+  atomicAdd(&tot[0], (unsigned long long)near);
+  atomicAdd(&tot[1], (unsigned long long)all);
+  __syncthreads();
+  if (threadIdx.x == 0) flag[0] = (tot[1] > 0 && 2 * tot[0] >= tot[1]) ? 1 : 0;
 }
 
 // sort keys for the longest-first schedule: ascending key = descending row length, rows of
@@ -167,14 +201,17 @@ __global__ __launch_bounds__(256) void k_hop(const Item* __restrict__ items,
                                              const float* __restrict__ acc_prev,
                                              float* __restrict__ partials,
                                              const int32_t* __restrict__ ymap,
-                                             const int32_t* __restrict__ pmap) {
+                                             const int32_t* __restrict__ pmap, int contig) {
   const int lane = threadIdx.x & (G - 1);
   int64_t ib;  // item block
   int chunk;   // feature chunk of G*V
   if constexpr (S > 0) {
     const int xcd = blockIdx.x & 7;
     chunk = xcd % S;
-    ib = (int64_t)(blockIdx.x >> 3) * (8 / S) + xcd / S;
+    // contig (S = 1): XCD x walks the x-th eighth of the work list, so a row range's gathered rows
+    // stay in one L2 (GDD_FORCE=hop_xcd_contig, the locality A/B)
+    ib = contig ? (int64_t)xcd * (gridDim.x >> 3) + (blockIdx.x >> 3)
+                : (int64_t)(blockIdx.x >> 3) * (8 / S) + xcd / S;
   } else {
     chunk = blockIdx.y;
     ib = blockIdx.x;
@@ -357,8 +394,10 @@ int carve_plan(int64_t n, int64_t nnz, int d, Carver& cv, Plan& pl, int32_t** tm
   return GDD_OK;
 }
 
-int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv, Plan& pl,
-               hipStream_t s) {
+// given_order (nullable): the work list's row order, taken as is (the relabelled hops: rows in their
+// new order, so that consecutive items gather neighbouring rows); null: longest rows first
+int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, const int32_t* col_for_probe,
+               Carver& cv, Plan& pl, hipStream_t s, const int32_t* given_order = nullptr) {
   int32_t* tmp[7];
   void* scan_ws;
   size_t sb;
@@ -367,8 +406,17 @@ int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv,
   int32_t *nseg = tmp[0], *npart = tmp[1], *item_off = tmp[2], *part_off = tmp[3];
   const unsigned gb = (unsigned)((n + 255) / 256);
   GDD_HIP(hipMemsetAsync(pl.counts, 0, sizeof(int32_t) * 4, s));
-  const int32_t* order = nullptr;
-  {
+  const int32_t* order = given_order;
+  // the probe's verdict in counts[2] (zeroed above): row order for graphs whose ids carry locality
+  // (GDD_FORCE=hop_row_order: row order always; hop_no_probe: longest first always — A/B)
+  const int32_t* rowwise = nullptr;
+  if (!given_order && col_for_probe && n >= kProbeMinRows && !forced("hop_no_probe") &&
+      !forced("hop_row_order")) {
+    k_locality_probe<<<1, 1024, 0, s>>>(n, rowptr, col_for_probe, pl.counts + 2);
+    GDD_LAUNCHED();
+    rowwise = pl.counts + 2;
+  }
+  if (!given_order && !forced("hop_row_order")) {
     k_len_keys<<<gb, 256, 0, s>>>(n, rowptr, tmp[4], tmp[5]);
     GDD_LAUNCHED();
     // rows grouped by key, stable: the same order as a stable sort of (key, row) pairs
@@ -382,14 +430,14 @@ int build_plan(int64_t n, int64_t nnz, int d, const int32_t* rowptr, Carver& cv,
     if (rc) return rc;
     order = tmp[6];
   }
-  k_seg_counts<<<gb, 256, 0, s>>>(n, rowptr, order, nseg, npart);
+  k_seg_counts<<<gb, 256, 0, s>>>(n, rowptr, order, rowwise, nseg, npart);
   GDD_LAUNCHED();
   int rc = exclusive_scan_i32(nseg, item_off, n, scan_ws, sb, s);
   if (rc) return rc;
   rc = exclusive_scan_i32(npart, part_off, n, scan_ws, sb, s);
   if (rc) return rc;
-  k_make_items<<<gb, 256, 0, s>>>(n, rowptr, order, nseg, item_off, part_off, pl.items, pl.long_rows,
-                                  pl.long_off, pl.counts);
+  k_make_items<<<gb, 256, 0, s>>>(n, rowptr, order, rowwise, nseg, item_off, part_off, pl.items,
+                                  pl.long_rows, pl.long_off, pl.counts);
   GDD_LAUNCHED();
   return GDD_OK;
 }
@@ -411,7 +459,8 @@ void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float s
     const int64_t groups = (iblocks + (8 / S) - 1) / (8 / S);
     k_hop<V, G, S><<<(unsigned)(groups * 8), 256, 0, s>>>(pl.items, pl.counts, col, val, scale, d,
                                                           x, y, acc, acc_scale, acc_init, acc_prev,
-                                                          pl.partials, rm.y, rm.prev);
+                                                          pl.partials, rm.y, rm.prev,
+                                                          S == 1 && forced("hop_xcd_contig") ? 1 : 0);
   };
   if (chunks == 8)
     xcd_launch(std::integral_constant<int, 8>());
@@ -424,7 +473,7 @@ void launch_hop_vg(const Plan& pl, const int32_t* col, const float* val, float s
   else
     k_hop<V, G, 0><<<dim3((unsigned)iblocks, (unsigned)chunks), 256, 0, s>>>(
         pl.items, pl.counts, col, val, scale, d, x, y, acc, acc_scale, acc_init, acc_prev, pl.partials,
-        rm.y, rm.prev);
+        rm.y, rm.prev, 0);
 }
 
 // lanes per item: the whole row up to 64 lanes, or narrower groups that split the row into XCD slices
@@ -503,7 +552,7 @@ extern "C" int gdd_spmm(int64_t n, int64_t nnz, const int32_t* rowptr, const int
   hipStream_t s = to_hip(stream);
   Carver cv(ws, ws_bytes);
   Plan pl;
-  rc = build_plan(n, nnz, d, rowptr, cv, pl, s);
+  rc = build_plan(n, nnz, d, rowptr, col, cv, pl, s);
   if (rc) return rc;
   return run_hop(pl, rowptr, col, val, scale, d, x, y, acc, acc_scale, s);
 }
@@ -514,7 +563,8 @@ extern "C" int gdd_spmm_plan(int64_t n, int64_t nnz, const int32_t* rowptr, int 
               "spmm_plan: bad arguments");
   Carver cv(ws, ws_bytes);
   Plan pl;
-  return build_plan(n, nnz, d, rowptr, cv, pl, to_hip(stream));
+  // no column ids here: the longest-first schedule (no locality probe)
+  return build_plan(n, nnz, d, rowptr, nullptr, cv, pl, to_hip(stream));
 }
 
 extern "C" int gdd_spmm_planned(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
@@ -542,6 +592,12 @@ __global__ void k_relabel_cols(int64_t nnz, const int32_t* __restrict__ col, con
   if (e < nnz) col_r[e] = rho[col[e]];
 }
 
+// the relabelled work order: position rho[r] holds row r
+__global__ void k_invert(int64_t n, const int32_t* __restrict__ rho, int32_t* __restrict__ order) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < n) order[rho[r]] = (int32_t)r;
+}
+
 // gdd_propagate; with rho the intermediate hops run in the relabelled layout (node r's row of p at
 // rho[r], gathered through col_r = rho[col]): hop 1 gathers X by the original ids, target keeps the
 // original ids throughout, the last hop stores p_last by the original ids
@@ -561,17 +617,22 @@ int propagate_impl(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t*
   }
   Carver cv(ws, ws_bytes);
   Plan pl;
-  rc = build_plan(n, nnz, d, rowptr, cv, pl, s);
-  if (rc) return rc;
   int32_t* col_r = nullptr;
+  int32_t* order = nullptr;
   if (rho) {
     col_r = cv.take<int32_t>((size_t)std::max<int64_t>(nnz, 1));
+    order = cv.take<int32_t>((size_t)n);
     if (!cv.ok()) return fail(GDD_E_WORKSPACE, "propagate_relabeled: workspace too small");
     if (nnz > 0) {
       k_relabel_cols<<<(unsigned)((nnz + 255) / 256), 256, 0, s>>>(nnz, col, rho, col_r);
       GDD_LAUNCHED();
     }
+    k_invert<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(n, rho, order);
+    GDD_LAUNCHED();
   }
+  // relabelled: every hop's work list in the new order (GDD_FORCE=hop_relabel_len: longest first)
+  rc = build_plan(n, nnz, d, rowptr, col, cv, pl, s, forced("hop_relabel_len") ? nullptr : order);
+  if (rc) return rc;
   // ping-pong so that hop T-1 lands in p_last. The target update is paired: after the first hop,
   // hop h (odd) leaves target alone and hop h+1 adds both terms, reading p_h back as its own input
   // rows — one read-modify-write of target per two hops instead of per hop (the streamed bytes that
@@ -622,7 +683,8 @@ extern "C" int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, cons
 }
 
 extern "C" size_t gdd_propagate_relabeled_ws_bytes(int64_t n, int64_t nnz, int d) {
-  return plan_ws_bytes(n, nnz, d) + align256(sizeof(int32_t) * (size_t)std::max<int64_t>(nnz, 1)) + 256;
+  return plan_ws_bytes(n, nnz, d) + align256(sizeof(int32_t) * (size_t)std::max<int64_t>(nnz, 1)) +
+         align256(sizeof(int32_t) * (size_t)n) + 256;
 }
 
 extern "C" int gdd_propagate_relabeled(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,

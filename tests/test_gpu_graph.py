@@ -106,10 +106,16 @@ def test_spmm_matches_oracle():
     assert np.array_equal(y.cpu().numpy().view(np.uint32), y_ref.view(np.uint32))
 
 
+@pytest.mark.parametrize("sched", ["", "hop_row_order", "hop_row_order,hop_xcd_contig"])
 @pytest.mark.parametrize("d", [128, 40, 7])
-def test_planned_hop_matches_oracle_and_accumulates(d):
+def test_planned_hop_matches_oracle_and_accumulates(d, sched, monkeypatch):
     # gdd_spmm_plan once, then gdd_spmm_planned hops (the unit bench.py times): bit-exact with the
-    # oracle's canonical order, including a hub row split into several segments
+    # oracle's canonical order, including a hub row split into several segments; under each work-list
+    # schedule (GDD_FORCE)
+    if sched:
+        monkeypatch.setenv("GDD_FORCE", sched)
+    else:
+        monkeypatch.delenv("GDD_FORCE", raising=False)
     n = 3000
     A = _graph(n, 12.0, 21)
     A = A.tolil()
@@ -132,14 +138,21 @@ def test_planned_hop_matches_oracle_and_accumulates(d):
         assert np.array_equal(acc.cpu().numpy().view(np.uint32), acc_ref.view(np.uint32))
 
 
+@pytest.mark.parametrize("sched", ["", "hop_relabel_len", "hop_row_order,hop_xcd_contig"])
 @pytest.mark.parametrize("relabel", ["degree", "rcm", "random"])
 @pytest.mark.parametrize("d,T,alpha", [(128, 18, 0.91), (64, 5, 0.8), (41, 4, 0.95), (602, 3, 0.95),
                                        (100, 2, 0.91), (3, 7, 0.8)])
-def test_propagate_relabeled_bitexact(relabel, d, T, alpha):
+def test_propagate_relabeled_bitexact(relabel, d, T, alpha, sched, monkeypatch):
     """gdd_propagate_relabeled: the intermediate hops in another node order (rows of
     p at rho[r], gathers through rho[col], every row's entries in CSR order), the first hop reading
     X and the last storing p_last by the original ids, target by them throughout — target and p_last
-    bit-identical to the oracle's, with the split hub row's fix-up and paired updates."""
+    bit-identical to the oracle's, with the split hub row's fix-up and paired updates. sched: the
+    work list in the new order (default, r06), longest first, or row order with XCD-contiguous
+    ranges (GDD_FORCE; a schedule changes timing, never bits)."""
+    if sched:
+        monkeypatch.setenv("GDD_FORCE", sched)
+    else:
+        monkeypatch.delenv("GDD_FORCE", raising=False)
     n = 3000
     A = _graph(n, 12.0, 5).tolil()
     A[11, :] = 0
@@ -157,3 +170,25 @@ def test_propagate_relabeled_bitexact(relabel, d, T, alpha):
     assert np.array_equal(p.cpu().numpy().view(np.uint32), p_ref.view(np.uint32))
     with pytest.raises(ValueError):
         gdd.propagate(g, torch.from_numpy(X).cuda(), T, alpha, relabel=np.zeros(n, np.int32))
+
+
+def test_locality_probe_schedule_bits(monkeypatch):
+    """The hop's locality probe (r06, graphs of >= 1M rows): a community graph whose ids are in
+    community order walks its rows in order, a shuffled one longest first — the schedule changes
+    timing only: both equal the forced longest-first (hop_no_probe) and row-order results bit for bit."""
+    for shuffle in (False, True):
+        g = synth.sbm_device(1_050_000, 8.0, 3, block=1024, p_in=0.9, shuffle=shuffle)
+        gn = gdd.normalize_adj(g)
+        gen = torch.Generator(device="cuda")
+        gen.manual_seed(1)
+        X = torch.randn(g.n, 12, device="cuda", generator=gen)
+        outs = []
+        for tok in ("", "hop_no_probe", "hop_row_order"):
+            if tok:
+                monkeypatch.setenv("GDD_FORCE", tok)
+            else:
+                monkeypatch.delenv("GDD_FORCE", raising=False)
+            t, p = gdd.propagate(gn, X, 4, 0.9)
+            outs.append((t.view(torch.int32).clone(), p.view(torch.int32).clone()))
+        for t, p in outs[1:]:
+            assert torch.equal(t, outs[0][0]) and torch.equal(p, outs[0][1])

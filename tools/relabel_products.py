@@ -9,8 +9,11 @@ no locality) and with contiguous blocks (the order a perfect relabel would recov
 products-shaped Chung-Lu graph. Orders: the original ids, "degree", "rcm" (scipy, host) and, for
 the shuffled SBM, the true community order.
 
-Prints one JSON line per (graph, order) and a summary line. RELABEL_REPS (default 3) timed calls per
-order. Between configurations it launches a marker fill of (i + 1) * 1,000,000 floats, so a
+Each order runs under three hop schedules (GDD_FORCE): "default" (original ids: longest rows first,
+or row order where the locality probe finds the ids local; relabelled: the new order), "noprobe"
+(hop_no_probe: longest first for original ids) and "contig" (hop_row_order,hop_xcd_contig: each XCD
+walks a contiguous eighth of the list, so a row range's gathers stay in one L2). Prints one JSON line per (graph, order, schedule) and a summary line. RELABEL_REPS
+(default 3) timed calls per configuration. Between configurations it launches a marker fill of (i + 1) * 1,000,000 floats, so a
 rocprofv3 --pmc FETCH_SIZE pass of this script can be split per configuration
 (tools/relabel_products_pmc.py)."""
 import json
@@ -26,6 +29,7 @@ import gdd  # noqa: E402
 from gdd import synth  # noqa: E402
 
 REPS = int(os.environ.get("RELABEL_REPS", "3"))
+SCHEDULES = {"default": "", "noprobe": "hop_no_probe", "contig": "hop_row_order,hop_xcd_contig"}
 _marks = [0]
 
 
@@ -59,17 +63,24 @@ def run(name, g, cfg, orders, res):
         t0 = time.time()
         rho = rho_fn(gn) if rho_fn else None
         order_s = time.time() - t0
-        mk = marker()
-        ms, (t, p) = timed(gn, X, cfg.T, cfg.alpha, rho)
-        if ref is None:
-            ref = (t, p)
-        same = torch.equal(t.view(torch.int32), ref[0].view(torch.int32)) and \
-            torch.equal(p.view(torch.int32), ref[1].view(torch.int32))
-        rec = {"graph": name, "order": kind, "n": g.n, "nnz": int(gn.nnz), "d": cfg.d, "hops": hops,
-               "ms_per_call": ms, "us_per_hop": ms * 1e3 / hops, "order_build_s": order_s,
-               "bit_identical_to_original_order": bool(same), "marker": mk, "calls": 1 + REPS}
-        res.append(rec)
-        print(json.dumps(rec), flush=True)
+        for sched, tok in SCHEDULES.items():
+            if tok:
+                os.environ["GDD_FORCE"] = tok
+            else:
+                os.environ.pop("GDD_FORCE", None)
+            mk = marker()
+            ms, (t, p) = timed(gn, X, cfg.T, cfg.alpha, rho)
+            if ref is None:
+                ref = (t, p)
+            same = torch.equal(t.view(torch.int32), ref[0].view(torch.int32)) and \
+                torch.equal(p.view(torch.int32), ref[1].view(torch.int32))
+            rec = {"graph": name, "order": kind, "schedule": sched, "n": g.n, "nnz": int(gn.nnz),
+                   "d": cfg.d, "hops": hops, "ms_per_call": ms, "us_per_hop": ms * 1e3 / hops,
+                   "order_build_s": order_s, "bit_identical_to_original_order": bool(same), "marker": mk,
+                   "calls": 1 + REPS}
+            res.append(rec)
+            print(json.dumps(rec), flush=True)
+        os.environ.pop("GDD_FORCE", None)
     del gn, X
 
 
@@ -81,7 +92,7 @@ def main():
     for shuffle in (True, False):
         g, perm = synth.sbm_device(pc.n, pc.avg_degree, 11, block=2048, p_in=0.9, shuffle=shuffle,
                                    return_perm=True)
-        orders = [("original", None), deg, rcm]
+        orders = [("original", None), deg, rcm] if shuffle else [("original", None)]
         if shuffle:  # node perm[i] sits in block i // 2048: the community order puts it at row i
             def community(gn, perm=perm):
                 rho = torch.empty(gn.n, dtype=torch.int32, device="cuda")
@@ -93,9 +104,9 @@ def main():
         del g, perm
         torch.cuda.empty_cache()
     g = synth.chung_lu_device(pc.n, pc.avg_degree, pc.seed)
-    run("products chung-lu (bench graph)", g, pc, [("original", None), deg, rcm], res)
-    print(json.dumps({"summary": [(r["graph"], r["order"], round(r["us_per_hop"], 1)) for r in res]}),
-          flush=True)
+    run("products chung-lu (bench graph)", g, pc, [("original", None), deg], res)
+    print(json.dumps({"summary": [(r["graph"], r["order"], r["schedule"], round(r["us_per_hop"], 1))
+                                  for r in res]}), flush=True)
 
 
 if __name__ == "__main__":
