@@ -2076,7 +2076,9 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
     }
   }
   if (c + 1 < a.k) {
-    if (wave > 0 && !spec) {
+    // the prefix again when it was not written here yet, or was written while a bounded spin gave up
+    // (s_sok = 0: another wave's total may have been missing from B); s_wave is complete now
+    if (wave > 0 && (!spec || !s_sok)) {
       double B = 0.0;
       for (int q = 0; q < wave - 1; ++q) B = B + s_wave[q];
       const double pot = (double)s_pot;
