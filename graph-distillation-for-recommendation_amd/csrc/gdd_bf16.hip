@@ -57,11 +57,14 @@ __device__ __forceinline__ int key_with_index(float d, int idx) {
 }
 
 // W waves per block, D tiles' loads in flight per wave, WPE the waves per SIMD the registers allow
-template <int PER, int NST, bool VEC4, int W, int D, int WPE>
+// DIM > 0: the feature count fixed at compile time (the configs' logit widths 47, 41, 40: the last
+// k-step's masks and the free slot then fold to one select per lane half), else the argument
+template <int PER, int NST, bool VEC4, int W, int D, int WPE, int DIM = 0>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) void k_assign_bf16q(
-    int64_t n, int dim, int k, int ktiles, const float* __restrict__ X, const float* __restrict__ C,
+    int64_t n, int dim_arg, int k, int ktiles, const float* __restrict__ X, const float* __restrict__ C,
     const float* __restrict__ cn2, int32_t* __restrict__ labels, float* __restrict__ sq_dist) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int dim = DIM > 0 ? DIM : dim_arg;
   bf16x8_t* Af = reinterpret_cast<bf16x8_t*>(smem);
   float* Cn = reinterpret_cast<float*>(smem + (size_t)ktiles * NST * 64 * 16);
   float* Pt = Cn + ktiles * 32;
@@ -304,8 +307,15 @@ int bf16q_launch(int64_t n, int dim, const float* X, int k, const float* C, cons
     if (per_need <= 2) return go(k_assign_bf16q<2, N, V, 4, 2, 1>);
     if (per_need <= 4) return go(k_assign_bf16q<4, N, V, 4, 2, 1>);
     if (per_need <= 6) {
-      if constexpr (N == 3 && !V)  // dims 41 .. 47
-        if (w8) return go(k_assign_bf16q<6, 3, false, 8, 1, 4>);
+      if constexpr (N == 3 && !V) {  // dims 41 .. 47
+        if (w8) return dim == 41 ? go(k_assign_bf16q<6, 3, false, 8, 1, 4, 41>)
+                                 : dim == 47 ? go(k_assign_bf16q<6, 3, false, 8, 1, 4, 47>)
+                                             : go(k_assign_bf16q<6, 3, false, 8, 1, 4>);
+        if (dim == 47) return go(k_assign_bf16q<6, 3, false, 4, 2, 1, 47>);
+        if (dim == 41) return go(k_assign_bf16q<6, 3, false, 4, 2, 1, 41>);
+      }
+      if constexpr (N == 3 && V)
+        if (dim == 40) return go(k_assign_bf16q<6, 3, true, 4, 2, 1, 40>);
       return go(k_assign_bf16q<6, N, V, 4, 2, 1>);
     }
     return go(k_assign_bf16q<8, N, V, 4, 2, 1>);
