@@ -11,144 +11,12 @@ kernels' arithmetic (candidate binades from an fp64 prefix, per-segment transduc
 re-walks a segment whose transducer does not apply) and must give the sequential sum bit for bit."""
 import numpy as np
 import pytest
+import sys
+import os
 
-SAT = 1 << 27
-TOP = 1 << 24
-LOW = 1 << 23
-
-
-def sat(x):
-    return max(-SAT, min(SAT, x))
-
-
-def binade(s):
-    """(e, S) of a finite fp32 s: e = -126 for |s| < 2^-125 (subnormals share binade -126's grid)."""
-    s = np.float32(s)
-    E = (int(s.view(np.uint32)) >> 23) & 0xFF
-    e = -126 if E <= 1 else E - 127
-    S = int(np.ldexp(np.float64(s), 23 - e))  # exact: s is a multiple of u
-    return e, S
-
-
-def term_tr(t, e):
-    """the transducer of one term in binade e: {parity: (advance, min, max)}"""
-    v = np.ldexp(np.float64(np.float32(t)), 23 - e)  # exact (t/u is a dyadic of <= 24 bits)
-    if not abs(v) < 2.0 ** 26:
-        q0 = q1 = SAT if v > 0 else -SAT
-    else:
-        fl = np.floor(v)
-        fr = v - fl
-        q = int(fl)
-        if fr < 0.5:
-            q0 = q1 = q
-        elif fr > 0.5:
-            q0 = q1 = q + 1
-        else:  # tie: the even one of S+q, S+q+1
-            q0 = q + (q & 1)
-            q1 = q + ((q + 1) & 1)
-    return {0: (q0, q0, q0), 1: (q1, q1, q1)}
-
-
-# the empty run: no partial sums, so its least partial advance is +SAT and its greatest -SAT (a start
-# exactly on the binade's lower edge is not itself a violation)
-IDENT = {0: (0, SAT, -SAT), 1: (0, SAT, -SAT)}
-
-
-def compose(f, g):
-    out = {}
-    for p in (0, 1):
-        a, mn, mx = f[p]
-        p2 = (p + a) & 1
-        b, mn2, mx2 = g[p2]
-        out[p] = (sat(a + b), min(mn, sat(a + mn2)), max(mx, sat(a + mx2)))
-    return out
-
-
-def applies(S0, e, f):
-    """the run applies from S0 (binade e, S0 inside it): every partial sum stays strictly inside"""
-    a, mn, mx = f[S0 & 1]
-    lo, hi = S0 + mn, S0 + mx
-    if e == -126:  # one grid from -2^-125 to 2^-125, zero included
-        return -TOP < lo and hi < TOP
-    if S0 > 0:
-        return lo > LOW and hi < TOP
-    return hi < -LOW and lo > -TOP
-
-
-def seq_sum(t, s=np.float32(0.0)):
-    s = np.float32(s)
-    for x in t:
-        s = np.float32(s + np.float32(x))
-    return s
-
-
-def run_tr(t, e):
-    f = IDENT
-    for x in t:
-        f = compose(f, term_tr(x, e))
-    return f
-
-
-def walk(t, s):
-    """the chunked walk: scan a chunk's composed path; where it stops applying, add that term in
-    hardware and resume after it (the model walks term by term inside the failing chunk)"""
-    s = np.float32(s)
-    i = 0
-    while i < len(t):
-        if not np.isfinite(s) or not np.isfinite(t[i]):
-            return seq_sum(t[i:], s)
-        e, S = binade(s)
-        f = term_tr(t[i], e)
-        if applies(S, e, f):
-            S2 = S + f[S & 1][0]
-            s = np.float32(np.ldexp(np.float64(S2), e - 23))
-        else:
-            s = np.float32(s + np.float32(t[i]))
-        i += 1
-    return s
-
-
-def guess(P):
-    p = np.float32(P)
-    if not np.isfinite(p):  # the segment is re-walked
-        return [127, 127]
-    e, _ = binade(p)
-    if e == -126:
-        return [e, -125]
-    r = abs(float(np.ldexp(np.float64(p), -e)))
-    return [e, min(e + 1, 127) if r >= 1.5 else e - 1]
-
-
-def segmented(t, L):
-    """segments of L terms: fp64 prefixes -> two candidate binades -> transducers -> resolve"""
-    n = len(t)
-    nseg = (n + L - 1) // L
-    segsum = [float(np.sum(t[b * L:(b + 1) * L], dtype=np.float64)) for b in range(nseg)]
-    recs = []
-    P = 0.0
-    for b in range(nseg):
-        es = guess(P)
-        seg = t[b * L:(b + 1) * L]
-        bad = not np.isfinite(seg).all()
-        recs.append((es, [run_tr(seg, e) for e in es], bad))
-        P += segsum[b]
-    s = np.float32(0.0)
-    rewalks = 0
-    for b in range(nseg):
-        es, fs, bad = recs[b]
-        seg = t[b * L:(b + 1) * L]
-        done = False
-        if np.isfinite(s) and not bad:
-            e, S = binade(s)
-            for ec, f in zip(es, fs):
-                if ec == e and applies(S, e, f):
-                    s = np.float32(np.ldexp(np.float64(S + f[S & 1][0]), e - 23))
-                    done = True
-                    break
-        if not done:
-            rewalks += 1
-            s = walk(seg, s)
-    return s, rewalks
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+from signed_chain import (IDENT, applies, binade, compose, guess, run_tr, seq_sum,  # noqa: E402,F401
+                          segmented, term_tr, walk)
 
 
 def cases():
