@@ -1,5 +1,5 @@
-"""CPU model of an exact parallel fp32 chain sum (test infrastructure: imported only by tests/ and
-tools/; never by the product path). A sequential fp32 sum of SIGNED terms — numpy's column sums
+"""CPU model of an exact parallel fp32 chain sum (test infrastructure: imported by tests/ and
+tools/model_lloyd_rank_split.py; never by the product path). A sequential fp32 sum of SIGNED terms — numpy's column sums
 (csrc/gdd_colsum.hip, r05) and sklearn's Lloyd M-step per (cluster, column) chain
 (_k_means_lloyd.pyx:140-152, one thread) — evaluated from per-segment two-state transducers:
 while the running sum s stays in one signed binade (sign sigma, |s| in [2^e, 2^(e+1))), s = S*u with

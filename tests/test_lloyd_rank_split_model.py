@@ -1,4 +1,4 @@
-"""CPU model of the rank-split Lloyd M-step fold (oracle/signed_chain.py
+"""CPU model of the rank-split Lloyd M-step fold (tests/signed_chain.py
 rank_split_fold): one (cluster, column) chain of sklearn's M-step (_k_means_lloyd.pyx:140-152, a
 sequential fp32 sum of the members' values in sample order) split over R ranks' contiguous row
 blocks. Each rank ships per segment either two-binade transducer records or — where its fp64 path
@@ -12,7 +12,7 @@ import sys
 import numpy as np
 import pytest
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from signed_chain import rank_split_fold, seq_sum  # noqa: E402
 
 

@@ -14,7 +14,7 @@ import pytest
 import sys
 import os
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from signed_chain import (IDENT, applies, binade, compose, guess, run_tr, seq_sum,  # noqa: E402,F401
                           segmented, term_tr, walk)
 

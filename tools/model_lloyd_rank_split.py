@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Statistics of the rank-split Lloyd M-step fold (the CPU model
-oracle/signed_chain.py rank_split_fold, pinned bit-exact by tests/test_lloyd_rank_split_model.py) at
+tests/signed_chain.py rank_split_fold, pinned bit-exact by tests/test_lloyd_rank_split_model.py) at
 the products shape: 2,449,029 x 47 logit-like rows (N(0,1) features through a random 100 x 47 map plus
 a bias, centred as KMeans.fit centres them), labels from 196 centres drawn from the rows; MODEL_CHAINS
 random (cluster, column) chains, each split over R ranks' contiguous row blocks. Prints, per (R, L):
@@ -15,7 +15,7 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
 from signed_chain import rank_split_fold, seq_sum  # noqa: E402
 
 N, D, C, K = 2449029, 100, 47, 196
