@@ -10,8 +10,10 @@
 //   var_j   = (ssq_j - corr_j*corr_j / n) / n
 //   scale_j = sqrt(var_j), or 1 when var_j <= n*eps*var_j + (n*mean_j*eps)^2 (_is_constant_feature)
 //   out_ij  = fp32( fp32(float64(x_ij) - mean_j) / scale_j )   (X -= mean_; X /= scale_ on fp32 X)
-// One lane per column runs the ordered fp64 sums (eight rows' loads in flight ahead of the adds);
-// the transform is elementwise.
+// The ordered fp64 sums run as k_scaler_stats below (the centring kernel's staging: waves 1..3 stage
+// row chunks in LDS, one lane of wave 0 folds each column; r06 — the r05 form, one lane per column
+// with eight rows' loads in flight, took 19.9 ms at the Reddit train shape, 153,932 x 602, against
+// ~1.5 ms now); the transform is elementwise.
 #include <algorithm>
 #include <climits>
 
@@ -19,48 +21,6 @@
 
 namespace gdd {
 namespace {
-
-__global__ __launch_bounds__(64) void k_col_stats(int64_t n, int dim, const float* __restrict__ X,
-                                                  double* __restrict__ mean_out,
-                                                  double* __restrict__ scale_out) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= dim) return;
-  double s = 0.0;
-  int64_t i = 0;
-  for (; i + 8 <= n; i += 8) {
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = X[(i + u) * dim + j];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) s = s + (double)v[u];
-  }
-  for (; i < n; ++i) s = s + (double)X[i * dim + j];
-  const double dn = (double)n;
-  const double mean = s / dn;
-  double corr = 0.0, ssq = 0.0;
-  for (i = 0; i + 8 <= n; i += 8) {
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = X[(i + u) * dim + j];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const double t = (double)v[u] - mean;
-      corr = corr + t;
-      ssq = ssq + t * t;
-    }
-  }
-  for (; i < n; ++i) {
-    const double t = (double)X[i * dim + j] - mean;
-    corr = corr + t;
-    ssq = ssq + t * t;
-  }
-  const double var = (ssq - (corr * corr) / dn) / dn;
-  const double eps = 2.220446049250313e-16;
-  const double nme = (dn * mean) * eps;
-  const bool constant = var <= (dn * eps) * var + nme * nme;
-  mean_out[j] = mean;
-  scale_out[j] = constant ? 1.0 : __builtin_sqrt(var);
-}
 
 __global__ void k_scale_rows(int64_t total, int dim, const float* __restrict__ X,
                              const double* __restrict__ mean, const double* __restrict__ scale,
@@ -77,19 +37,6 @@ __global__ void k_scale_rows(int64_t total, int dim, const float* __restrict__ X
 }  // namespace gdd
 
 using namespace gdd;
-
-extern "C" int gdd_standard_scaler(int64_t n, int dim, const float* X, float* X_out, double* mean,
-                                   double* scale, gdd_stream_t stream) {
-  GDD_REQUIRE(n > 0 && dim > 0 && X && X_out && mean && scale, "standard_scaler: bad arguments");
-  hipStream_t s = to_hip(stream);
-  k_col_stats<<<(unsigned)((dim + 63) / 64), 64, 0, s>>>(n, dim, X, mean, scale);
-  GDD_LAUNCHED();
-  const int64_t total = n * (int64_t)dim;
-  k_scale_rows<<<(unsigned)std::min<int64_t>((total + 255) / 256, 8192), 256, 0, s>>>(
-      total, dim, X, mean, scale, X_out);
-  GDD_LAUNCHED();
-  return GDD_OK;
-}
 
 extern "C" int gdd_standard_scaler_transform(int64_t n, int dim, const float* X, const double* mean,
                                              const double* scale, float* X_out, gdd_stream_t stream) {
@@ -254,6 +201,134 @@ __global__ __launch_bounds__(256) void k_col_stats(int64_t n, int dim, const flo
   }
 }
 
+// StandardScaler's statistics (top of file) with k_col_stats' staging: workgroup g owns columns
+// [8g, 8g + w); waves 1..3 stage 768-row chunks of x (both passes) column-major; lane j of wave 0
+// folds column j: pass 0 s = s + double(x); pass 1 t = double(x) - mean, corr = corr + t,
+// ssq = ssq + t*t — the oracle's (and numpy's axis-0) row order, one dependent fp64 add per row.
+template <int PASS>
+__device__ __forceinline__ void sc_fold32(const float4 (&v)[8], double m, double& a, double& b) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const float x4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if constexpr (PASS == 0) {
+        a = a + (double)x4[q];
+      } else {
+        const double t = (double)x4[q] - m;
+        a = a + t;
+        b = b + t * t;
+      }
+    }
+  }
+}
+
+template <int PASS>
+__device__ __forceinline__ void sc_fold(const float* __restrict__ col, int rows, double m, double& a,
+                                        double& b) {
+  int r = 0;
+  if (rows >= 64) {
+    float4 A[8], B[8];
+    col_load32(col, A);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(A[u].x), "+v"(A[u].y), "+v"(A[u].z), "+v"(A[u].w));
+    for (; r + 64 <= rows; r += 64) {
+      col_load32(col + r + 32, B);
+      __builtin_amdgcn_sched_barrier(0);
+      sc_fold32<PASS>(A, m, a, b);
+      __builtin_amdgcn_sched_barrier(0);
+      col_load32(col + r + 64, A);
+      __builtin_amdgcn_sched_barrier(0);
+      sc_fold32<PASS>(B, m, a, b);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  for (; r < rows; ++r) {
+    if constexpr (PASS == 0) {
+      a = a + (double)col[r];
+    } else {
+      const double t = (double)col[r] - m;
+      a = a + t;
+      b = b + t * t;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_scaler_stats(int64_t n, int dim, const float* __restrict__ X,
+                                                      double* __restrict__ mean_out,
+                                                      double* __restrict__ scale_out) {
+  if (blockIdx.x % kColXcd) return;
+  __shared__ __attribute__((aligned(16))) float buf[2 * kCW * kCS + 32];
+  __shared__ double s_m[kCW];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c0 = (int)(blockIdx.x / kColXcd) * kCW, w = min(kCW, dim - c0);
+  const int64_t nchunks = (n + kCR - 1) / kCR;
+  const double dn = (double)n;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (wave == 0) {
+      double a = 0.0, b = 0.0;
+      const double m = (pass == 1 && tid < w) ? s_m[tid] : 0.0;
+      __syncthreads();  // chunk 0 staged
+      for (int64_t i = 0; i < nchunks; ++i) {
+        const int rows = (int)min((int64_t)kCR, n - i * kCR);
+        if (tid < w) {
+          const float* col = buf + (i & 1) * kCW * kCS + tid * kCS;
+          if (pass == 0)
+            sc_fold<0>(col, rows, m, a, b);
+          else
+            sc_fold<1>(col, rows, m, a, b);
+        }
+        __syncthreads();
+      }
+      if (tid < w) {
+        if (pass == 0) {
+          s_m[tid] = a / dn;
+        } else {
+          const double mean = m, var = (b - (a * a) / dn) / dn;
+          const double eps = 2.220446049250313e-16;
+          const double nme = (dn * mean) * eps;
+          const bool constant = var <= (dn * eps) * var + nme * nme;  // _is_constant_feature
+          mean_out[c0 + tid] = mean;
+          scale_out[c0 + tid] = constant ? 1.0 : __builtin_sqrt(var);
+        }
+      }
+    } else {
+      const int lt = tid - 64;
+      float v[kCQ];
+      auto fetch = [&](int64_t i) {
+#pragma unroll
+        for (int q = 0; q < kCQ; ++q) {
+          const int e = lt + kCL * q;
+          const int64_t row = min(i * kCR + (e >> 3), n - 1);
+          const int c = min(e & (kCW - 1), w - 1);
+          v[q] = X[row * dim + c0 + c];
+        }
+      };
+      auto store = [&](int64_t i) {
+        float* sb = buf + (i & 1) * kCW * kCS;
+#pragma unroll
+        for (int q = 0; q < kCQ; ++q) {
+          const int e = lt + kCL * q;
+          sb[(e & (kCW - 1)) * kCS + (e >> 3)] = v[q];
+        }
+      };
+      fetch(0);
+      store(0);
+      if (nchunks > 1) fetch(1);
+      __syncthreads();
+      for (int64_t i = 0; i < nchunks; ++i) {
+        if (i + 1 < nchunks) {
+          store(i + 1);
+          if (i + 2 < nchunks) fetch(i + 2);
+        }
+        __syncthreads();
+      }
+    }
+    __syncthreads();  // the means in s_m before the second pass
+  }
+}
+
 // numpy's pairwise leaf (len <= 128) over x (pass 0) or over (x - m)^2 (pass 1, which also writes
 // x - m).
 __device__ float pw_leaf(const float* __restrict__ a, float* __restrict__ o, int len, int pass, float m) {
@@ -386,6 +461,20 @@ extern "C" int gdd_center_columns(int64_t n, int dim, const float* X, float* X_o
     const unsigned groups = (unsigned)((dim + kCW - 1) / kCW);
     k_col_stats<<<groups * kColXcd, 256, 0, s>>>(n, dim, X, X_out, mean, var);
   }
+  GDD_LAUNCHED();
+  return GDD_OK;
+}
+
+extern "C" int gdd_standard_scaler(int64_t n, int dim, const float* X, float* X_out, double* mean,
+                                   double* scale, gdd_stream_t stream) {
+  GDD_REQUIRE(n > 0 && dim > 0 && X && X_out && mean && scale, "standard_scaler: bad arguments");
+  hipStream_t s = to_hip(stream);
+  const unsigned groups = (unsigned)((dim + kCW - 1) / kCW);
+  k_scaler_stats<<<groups * kColXcd, 256, 0, s>>>(n, dim, X, mean, scale);
+  GDD_LAUNCHED();
+  const int64_t total = n * (int64_t)dim;
+  k_scale_rows<<<(unsigned)std::min<int64_t>((total + 255) / 256, 8192), 256, 0, s>>>(
+      total, dim, X, mean, scale, X_out);
   GDD_LAUNCHED();
   return GDD_OK;
 }

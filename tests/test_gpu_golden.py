@@ -114,10 +114,12 @@ def test_recsys_kmeans_cluster_device_scaler():
     assert np.array_equal(bits(cen), bits(z["rs_centers"]))
 
 
-@pytest.mark.parametrize("n,dim", [(17730, 64), (6040, 64), (6041, 100), (129, 3), (1, 5), (128, 64)])
+@pytest.mark.parametrize("n,dim", [(17730, 64), (6040, 64), (6041, 100), (129, 3), (1, 5), (128, 64),
+                                   (20000, 602), (100003, 41), (767, 9), (1537, 1)])
 def test_standard_scaler_vs_oracle(n, dim):
-    """The device scaler equals the oracle's numpy-order statistics: n % 8 tails, 64-column groups
-    with a partial last group, a single row, a constant column."""
+    """The device scaler equals the oracle's numpy-order statistics: partial staged chunks (768 rows)
+    and 64-row fold groups, 8-column groups with a partial last group, the Reddit feature width, a
+    single row or column, a constant column."""
     from oracle import oracle as O
     from gdd import pipeline
     X = (np.random.default_rng(6).standard_normal((n, dim)) * 2 - 1).astype(np.float32)
