@@ -254,15 +254,17 @@ __device__ __forceinline__ void sc_fold(const float* __restrict__ col, int rows,
   }
 }
 
+// one_xcd: only blocks with blockIdx % 8 == 0 work (k_col_stats' placement: one XCD's L2 serves every
+// column group); else block g owns group g (more groups than one XCD has CUs)
 __global__ __launch_bounds__(256) void k_scaler_stats(int64_t n, int dim, const float* __restrict__ X,
                                                       double* __restrict__ mean_out,
-                                                      double* __restrict__ scale_out) {
-  if (blockIdx.x % kColXcd) return;
+                                                      double* __restrict__ scale_out, int one_xcd) {
+  if (one_xcd && blockIdx.x % kColXcd) return;
   __shared__ __attribute__((aligned(16))) float buf[2 * kCW * kCS + 32];
   __shared__ double s_m[kCW];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int c0 = (int)(blockIdx.x / kColXcd) * kCW, w = min(kCW, dim - c0);
+  const int c0 = (int)(one_xcd ? blockIdx.x / kColXcd : blockIdx.x) * kCW, w = min(kCW, dim - c0);
   const int64_t nchunks = (n + kCR - 1) / kCR;
   const double dn = (double)n;
   for (int pass = 0; pass < 2; ++pass) {
@@ -470,7 +472,10 @@ extern "C" int gdd_standard_scaler(int64_t n, int dim, const float* X, float* X_
   GDD_REQUIRE(n > 0 && dim > 0 && X && X_out && mean && scale, "standard_scaler: bad arguments");
   hipStream_t s = to_hip(stream);
   const unsigned groups = (unsigned)((dim + kCW - 1) / kCW);
-  k_scaler_stats<<<groups * kColXcd, 256, 0, s>>>(n, dim, X, mean, scale);
+  // up to 32 column groups on one XCD (its CUs); more spread over all (GDD_FORCE=scaler_one_xcd /
+  // scaler_spread: either, A/B)
+  const bool one = forced("scaler_one_xcd") || (groups <= 32 && !forced("scaler_spread"));
+  k_scaler_stats<<<one ? groups * kColXcd : groups, 256, 0, s>>>(n, dim, X, mean, scale, one ? 1 : 0);
   GDD_LAUNCHED();
   const int64_t total = n * (int64_t)dim;
   k_scale_rows<<<(unsigned)std::min<int64_t>((total + 255) / 256, 8192), 256, 0, s>>>(
