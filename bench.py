@@ -338,7 +338,7 @@ def recsys_record(dev, with_cpu, reps=5, group=None, world=1):
            "data": "synthetic SVD-like embeddings (gdd.synth.svd_like)",
            "parallelism": ("single GPU" if world == 1 else
                            f"{world} ranks: users' fit on rank 0, items' on rank 1 (independent "
-                           "random_state each), labels and centres broadcast over RCCL"),
+                           f"random_state each), labels and centres broadcast over {_backend_name(group)}"),
            "ms_per_pair": ms, "nodes_clustered_per_s": nodes / (ms * 1e-3), "cpu_baseline": None}
     if world > 1:
         return rec
@@ -765,6 +765,12 @@ def _products_group_record(cfg, g, X, W, bias, gen_s, dev, group, world):
             "phases_ms_rank0": ph, "kmeans_n_iter": n_iter, "cpu_baseline": None}
 
 
+def _backend_name(group):
+    """The collective library a group's broadcasts use: RCCL under the nccl backend, else gloo."""
+    import torch.distributed as dist
+    return "RCCL" if dist.get_backend(group) == "nccl" else dist.get_backend(group)
+
+
 REDDIT_ROLES = (153932, 23699, 55334)  # GraphSAINT Reddit role.json sizes (train, val, test)
 REDDIT_FULL_DEGREE = 101.7  # 232,965 nodes; the induced train graph then holds ~10.4M entries
 
@@ -826,7 +832,7 @@ def reddit_record(dev, with_cpu, group=None, world=1, reps=2):
            "parallelism": ("single GPU" if world == 1 else
                            f"{world} ranks: each role graph propagated by its owners "
                            f"{role_owners(world)} (train row-partitioned over its owners when "
-                           "propagation_shards_pay), targets broadcast over RCCL; MiniBatchKMeans "
+                           f"propagation_shards_pay), targets broadcast over {_backend_name(group)}; MiniBatchKMeans "
                            "steps replicated, labels pass by rows, cluster means by clusters"),
            "graph_generation_s": gen_s, "ms_total": ms, "nodes_per_s": N / (ms * 1e-3),
            "phases_ms" if world == 1 else "phases_ms_rank0": ph,
