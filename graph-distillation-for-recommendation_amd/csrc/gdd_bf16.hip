@@ -27,8 +27,9 @@
 // Accuracy: the labels are those of bf16 dot products (tests/test_gpu_kmeans.py and
 // tests/test_gpu_configs.py bound every label that differs from the exact fp32 one by the bf16
 // rounding, 2^-7 ||x|| ||c|| per product). delta = 2^-5 ||x||^2 + 2^-100 keeps acc strictly negative:
-// a centre whose acc crossed zero would need d / 2 < 2^-7 ||x|| ||c|| + 2^-10 ||x||^2 (product and
-// shift roundings) - delta, impossible for ||c|| <= 3.8 ||x|| (the right side is negative) and for
+// a centre whose acc crossed zero would need d / 2 < 2^-7 ||x|| ||c|| + 2^-7 ||x||^2 (the products'
+// rounding; the shift's: ||x||^2 summed from the bf16-rounded features, <= 2^-8 ||x||^2 off, then
+// rounded to bf16) - delta, impossible for ||c|| <= 2.9 ||x|| (the right side is negative) and for
 // larger ||c|| (then d >= (||c|| - ||x||)^2 is far above it); the shift is the same for every centre
 // of a point, so neither it nor its bf16 rounding reorders them. Dropping 5 of the 24 significand
 // bits moves a key by < 2^-18 of |acc|; keys that tie may pick either centre.
@@ -43,6 +44,7 @@ namespace {
 using floatx16 = __attribute__((ext_vector_type(16))) float;
 typedef float floatx4_t __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
 inline size_t bf16q_lds(int ktiles, int nsteps, int dim, int waves) {
   return (size_t)ktiles * nsteps * 64 * 16 + (size_t)ktiles * 32 * sizeof(float) +
@@ -98,7 +100,6 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
   auto compute = [&](int64_t tt) {
     const float* row = my + r * dim;
     float x[NST][8];
-    float xx = 0.f;  // this lane's half of ||x||^2 (fp32)
 #pragma unroll
     for (int st = 0; st < NST; ++st) {
       if constexpr (VEC4) {
@@ -117,22 +118,26 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) v
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[st][j] = j < lastf ? x[st][j] : 0.f;
       }
+    }
+    // the B-fragments first (the free slot still zero), then this lane's half of ||x||^2 from them: one
+    // v_dot2c_f32_bf16 per pair of features instead of two fp32 fmas (the shift's error, ~2^-8 ||x||^2,
+    // stays inside delta: header)
+    bf16x8_t b[NST];
+    float xx = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) xx = __builtin_fmaf(x[st][j], x[st][j], xx);
+    for (int st = 0; st < NST; ++st) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[st][j] = (__bf16)x[st][j];
+      const bf16x2_t* pr = reinterpret_cast<const bf16x2_t*>(&b[st]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xx = __builtin_amdgcn_fdot2_f32_bf16(pr[q], pr[q], xx, false);
     }
     const float oxx = __shfl_xor(xx, 32);
     const float xsq = h ? oxx + xx : xx + oxx;  // the same value on both halves
     const float shift = -__builtin_fmaf(0.53125f, xsq, 0x1p-100f);  // -(||x||^2 / 2 + delta), header
-    bf16x8_t b[NST];
 #pragma unroll
-    for (int st = 0; st < NST; ++st) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float v = x[st][j];
-        if (st == NST - 1 && j == lastf) v = shift;  // feature dim: the free K slot
-        b[st][j] = (__bf16)v;
-      }
-    }
+    for (int j = 0; j < 8; ++j)
+      if (j == lastf) b[NST - 1][j] = (__bf16)shift;  // feature dim: the free K slot
     int bestk = 0x7fffffff;
     int bestct = 0;
     auto chain = [&](int c) {
