@@ -542,9 +542,10 @@ ESTEP_TFLOPS = 50.0  # the unbounded E-step's MFMA rate at large n (measured 46-
 def lloyd_rows_pay(n: int, dim: int, k: int, world: int) -> bool:
     """Size model for ShardedKMeans: splitting the E-step's rows over R ranks saves (R-1)/R of it and
     adds an all-gather of the n int32 labels per iteration (~25 us + 4n(R-1)/R bytes at ~300 GB/s).
-    With the bounded E-step (dim <= 48) an iteration's E-step is a bounds test of ~40 us at
-    2.45M rows, so ogbn-products replicates; an unbounded E-step (2 n k dim flops) of 1 ms and more
-    shards. The M-step is not split: its ordered per-cluster folds are bound by the longest member
+    With the bounded E-step (dim <= 48) an iteration's E-step is the bounds test plus the
+    listed rows' exact pass, ~0.23 ms at 2.45M rows (r06 trace; r04's model took it for a 40 us bounds
+    test), so ogbn-products splits at N >= 2 while the recsys shapes (a ~30 us E-step) replicate; an
+    unbounded E-step (2 n k dim flops) of 1 ms and more shards. The M-step is not split: its ordered per-cluster folds are bound by the longest member
     chain, not by the rows' bytes (a column split measured 1.53 -> 1.49 / 1.57 / 1.59 ms at 1/2, 1/4,
     1/8 of the columns, `profiles/r04_fold_cols.txt`). GDD_SHARD_LLOYD=1/0 forces the choice."""
     import os
@@ -554,7 +555,10 @@ def lloyd_rows_pay(n: int, dim: int, k: int, world: int) -> bool:
     if world <= 1:
         return False
     bounded = dim <= 48  # the bounded E-step's shapes (gdd_lloyd.hip lloyd_prune_ok)
-    estep_ms = (n * 8 / 5e12 * 1e3 + 0.03) if bounded else 2.0 * n * k * dim / (ESTEP_TFLOPS * 1e12) * 1e3
+    # bounded: the bounds test plus the listed rows' exact pass, measured 233 us per iteration at the
+    # products shape (2.45M rows, a third of them listed; r06 kernel trace, tools/prof_products_lloyd.py)
+    # the part of the E-step that shrinks with the rows (its launch floor does not)
+    estep_ms = n * 9.5e-8 if bounded else 2.0 * n * k * dim / (ESTEP_TFLOPS * 1e12) * 1e3
     frac = (world - 1) / world
     gather_ms = 0.025 + 4.0 * n * frac / 300e9 * 1e3
     return estep_ms * frac > gather_ms

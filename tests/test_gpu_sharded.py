@@ -175,6 +175,41 @@ def _prop_worker(rank, world, port, rowptr, col, X, T, alpha, out):
     dist.destroy_process_group()
 
 
+def _lloyd_rows_worker(rank, world, port, X, out):
+    sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE),
+                                                          "graph-distillation-for-recommendation_amd"), HERE]
+    os.environ["GDD_SHARD_LLOYD"] = "1"
+    import torch.distributed as dist
+    from gdd.sharded import ShardedKMeans as SK
+    from sharded_util import init_gloo
+    init_gloo(rank, world, port)
+    m = SK(n_clusters=60, random_state=15, device="cuda:0", group=dist.group.WORLD).fit(X)
+    np.savez(os.path.join(out, f"l{rank}.npz"), labels=m.labels_, centers=m.cluster_centers_,
+             n_iter=m.n_iter_, inertia=m.inertia_, mode=m.mode_)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_lloyd_rows_products_path_matches_one(world):
+    """ShardedKMeans' row split on the products-shape code path (r06: the size model now splits config
+    5's Lloyd at N > 1): >= 65,536 rows at dim 47, so the fold and the bounded E-step's row lists read
+    the zero-padded copy of X; bit-identical to gdd.KMeans on one rank."""
+    n, dim = 100003, 47
+    rng = np.random.default_rng(8)
+    X = (rng.standard_normal((n, 32)) @ rng.standard_normal((32, dim)) / 5.0 + rng.standard_normal(dim)).astype(np.float32)
+    one = gdd.KMeans(n_clusters=60, random_state=15).fit(X)
+    out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"gdd_lrows_{os.getpid()}_{world}")
+    os.makedirs(out, exist_ok=True)
+    mp.spawn(_lloyd_rows_worker, args=(world, free_port(), X, out), nprocs=world, join=True)
+    for r in range(world):
+        p = np.load(os.path.join(out, f"l{r}.npz"))
+        assert str(p["mode"]) == "rows"
+        assert int(p["n_iter"]) == one.n_iter_
+        assert np.array_equal(p["labels"], one.labels_)
+        assert np.array_equal(_bits(p["centers"]), _bits(one.cluster_centers_))
+        assert float(p["inertia"]) == one.inertia_
+
+
 @pytest.mark.parametrize("world,T", [(2, 5), (3, 4)])
 def test_ranks_row_partitioned_propagate_matches_one(world, T):
     """gdd.sharded.sharded_propagate on the device: rows partitioned over the ranks,

@@ -239,6 +239,23 @@ def test_propagation_size_model():
     assert not propagation_shards_pay(169343, 2_560_000, 128, 1)
 
 
+def test_lloyd_size_model(monkeypatch):
+    """lloyd_rows_pay (r06): the E-step's row-proportional part against the labels all-gather — the
+    products Lloyd splits from two ranks (a ~0.23 ms bounded E-step per iteration), the recsys and
+    Cora shapes replicate, one rank never splits, GDD_SHARD_LLOYD forces either."""
+    _paths()
+    from gdd.sharded import lloyd_rows_pay
+    monkeypatch.delenv("GDD_SHARD_LLOYD", raising=False)
+    assert all(lloyd_rows_pay(2449029, 47, 196, w) for w in (2, 4, 8))
+    assert not lloyd_rows_pay(2449029, 47, 196, 1)
+    assert not any(lloyd_rows_pay(n, 64, k, 8) for n, k in ((6040, 604), (3706, 371)))
+    assert not lloyd_rows_pay(2708, 7, 70, 8)
+    monkeypatch.setenv("GDD_SHARD_LLOYD", "0")
+    assert not lloyd_rows_pay(2449029, 47, 196, 8)
+    monkeypatch.setenv("GDD_SHARD_LLOYD", "1")
+    assert lloyd_rows_pay(2708, 7, 70, 2) and not lloyd_rows_pay(2708, 7, 70, 1)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_recsys_pair_split_matches_one_rank(tmp_path, world):
     """kmeans_cluster_pair over a group (north star config 4): the users' fit runs on rank 0 only and
