@@ -2,9 +2,10 @@
 """Joins tools/relabel_products.py's timings (its JSON lines) with a rocprofv3 --pmc FETCH_SIZE pass
 of the same script (RELABEL_REPS=1): per configuration, the mean FETCH_SIZE (KiB, summed over the
 XCDs by rocprofv3) of the hop kernel's dispatches between that configuration's marker fill (a fill of
-marker * 1,000,000 floats) and the next one, against the hop's algorithmic bytes (the CSR's column
-ids and values once, every gathered row of X once per entry would be the worst case; the ideal is
-each row of X once: n * d * 4 + nnz * 8 + the n * d * 4 written).
+marker * 1,000,000 floats) and the next one (doubled: the gfx950 correction for 16-byte reads),
+against the hop's algorithmic bytes as DESIGN §4 counts them
+(4 (N + 1) + 8 nnz + 16 N d: the CSR once, the previous hop read once, this hop written, target read
+and written).
 
 usage: relabel_products_pmc.py TIMINGS.log COUNTERS.csv OUT.json"""
 import csv
@@ -32,8 +33,10 @@ def main(tlog, ccsv, out):
         v = seg.get(rec["marker"], [])
         n, nnz, d = rec["n"], rec["nnz"], rec["d"]
         rec["hop_dispatches"] = len(v)
-        rec["fetch_bytes_per_hop"] = (sum(v) / len(v) * 1024.0) if v else None
-        rec["ideal_bytes_per_hop"] = 2 * n * d * 4 + nnz * 8
+        # FETCH_SIZE in KiB, doubled: gfx950 reports half the bytes of 16-byte-per-lane reads (the hop's
+        # row gathers; MI355X_MICROARCH.md HBM section, as tools/pmc_summary.py)
+        rec["fetch_bytes_per_hop"] = (2.0 * sum(v) / len(v) * 1024.0) if v else None
+        rec["ideal_bytes_per_hop"] = 4 * (n + 1) + 8 * nnz + 16 * n * d  # DESIGN §4's algorithmic bytes
         if v:
             rec["fetch_over_ideal"] = rec["fetch_bytes_per_hop"] / rec["ideal_bytes_per_hop"]
     json.dump({"what": "products-shape propagation (T = 18, d = 100) in other node orders: hop time "
