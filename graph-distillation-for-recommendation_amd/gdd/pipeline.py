@@ -148,7 +148,7 @@ def kmeans_cluster(X, n_clusters: int, seed: int, minibatch: bool = True, batch_
 
 def kmeans_cluster_pair(user_emb, item_emb, n_user_clusters: int, n_item_clusters: int, seed: int,
                         minibatch: bool = True, batch_size: int = 2048, device="cuda", n_init="auto",
-                        group=None, fit=None):
+                        group=None, fit=None, concurrent: bool = True):
     """Both kmeans_cluster calls of distill_recsys's main (distill_recsys.py:569-583): users, then
     items -> ((u_labels int64, u_centres fp32), (i_labels, i_centres)), numpy.
 
@@ -156,13 +156,23 @@ def kmeans_cluster_pair(user_emb, item_emb, n_user_clusters: int, n_item_cluster
     share nothing — each has its own ``random_state=seed`` — so the users' fit runs on rank 0 and the
     items' on rank 1 (one rank runs both when R = 1), and each result is broadcast from its owner
     (RCCL over xGMI). Every rank ends with the single-GPU results, bit for bit. ``fit`` (tests): a
-    stand-in with kmeans_cluster's signature."""
-    fit = fit or kmeans_cluster
+    stand-in with kmeans_cluster's signature.
+
+    One GPU (``concurrent``, r06): the two fits run side by side on two HIP streams, the items' fit
+    from a second host thread. Their launches are latency-bound chains that fill a fraction of the
+    CUs (k-means++ rounds of T x T workgroups, Lloyd iterations of a 6,040-row problem), so the GPU
+    overlaps them; the library's host state is lock-protected and its error string thread-local,
+    and each fit is the single-stream computation itself (the same bits)."""
     kw = dict(seed=seed, minibatch=minibatch, batch_size=batch_size, n_init=n_init)
     from .sharded import split_pair, world_of
     if group is None or world_of(group)[1] == 1:
-        return (fit(user_emb, n_clusters=n_user_clusters, device=device, **kw),
-                fit(item_emb, n_clusters=n_item_clusters, device=device, **kw))
+        dev = torch.device(device)
+        if fit is not None or not concurrent or dev.type != "cuda":
+            fit = fit or kmeans_cluster
+            return (fit(user_emb, n_clusters=n_user_clusters, device=device, **kw),
+                    fit(item_emb, n_clusters=n_item_clusters, device=device, **kw))
+        return _pair_two_streams(user_emb, item_emb, n_user_clusters, n_item_clusters, dev, kw)
+    fit = fit or kmeans_cluster
     jobs = []
     for E, k in ((user_emb, n_user_clusters), (item_emb, n_item_clusters)):
         n, d = int(E.shape[0]), int(E.shape[1])
@@ -173,6 +183,34 @@ def kmeans_cluster_pair(user_emb, item_emb, n_user_clusters: int, n_item_cluster
         jobs.append((lambda E=E, k=k: fit(E, n_clusters=k, device=device, **kw), spec))
     (ul, uc), (il, ic) = split_pair(jobs, group=group, device=device)
     return ((ul.cpu().numpy(), uc.cpu().numpy()), (il.cpu().numpy(), ic.cpu().numpy()))
+
+
+def _pair_two_streams(user_emb, item_emb, ku: int, ki: int, dev, kw):
+    """kmeans_cluster(users) on one stream of this thread, kmeans_cluster(items) on another stream
+    from a helper thread; both ordered after the caller's stream, and the caller's stream after both."""
+    import threading
+    cur = torch.cuda.current_stream(dev)
+    streams = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
+    out, err = [None, None], [None, None]
+
+    def run(j, E, k):
+        try:
+            with torch.cuda.device(dev), torch.cuda.stream(streams[j]):
+                streams[j].wait_stream(cur)
+                out[j] = kmeans_cluster(E, n_clusters=k, device=dev, **kw)
+        except BaseException as e:  # re-raised on the caller's thread
+            err[j] = e
+
+    helper = threading.Thread(target=run, args=(1, item_emb, ki))
+    helper.start()
+    run(0, user_emb, ku)
+    helper.join()
+    for s in streams:
+        cur.wait_stream(s)
+    for e in err:
+        if e is not None:
+            raise e
+    return out[0], out[1]
 
 
 def teacher_means(emb: torch.Tensor, assignment, num_clusters: int) -> torch.Tensor:

@@ -315,3 +315,20 @@ def test_edge_dots_range_guard():
     keep = np.ones(1000, bool)
     keep[[3, 999]] = False
     assert np.array_equal(got[keep].view(np.uint32), ref[keep].view(np.uint32))
+
+
+@pytest.mark.parametrize("shapes", [((6040, 604), (3706, 371)), ((1500, 150), (3000, 300)), ((700, 7), (500, 499))])
+def test_cluster_pair_two_streams_equals_serial(shapes):
+    """kmeans_cluster_pair on one GPU (r06): the users' and items' fits side by side on two streams
+    (the items' from a helper thread) give the serial pair's labels and centres bit for bit, three
+    times over (a race between the fits would show as a difference)."""
+    from gdd import synth
+    from gdd.pipeline import kmeans_cluster_pair
+    (nu, ku), (ni, ki) = shapes
+    Eu, Ei = synth.svd_like(nu, 64, seed=nu), synth.svd_like(ni, 64, seed=ni)
+    ref = kmeans_cluster_pair(Eu, Ei, ku, ki, seed=42, minibatch=True, device="cuda", concurrent=False)
+    for _ in range(3):
+        got = kmeans_cluster_pair(Eu, Ei, ku, ki, seed=42, minibatch=True, device="cuda")
+        for (gl, gc), (rl, rc) in zip(got, ref):
+            assert np.array_equal(gl, rl)
+            assert np.array_equal(gc.view(np.uint32), rc.view(np.uint32))
