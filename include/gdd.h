@@ -77,6 +77,9 @@ int gdd_normalize_csr(int64_t n, int64_t nnz, const int32_t* rowptr, const int32
 /* ---------------------------------------------------------------------------------------------- */
 #define GDD_PROP_SEG 256
 size_t gdd_propagate_ws_bytes(int64_t n, int64_t nnz, int d);
+/* r06: from 1M rows a one-workgroup probe samples the CSR; where half the sampled entries point within */
+/* 4,096 rows of their row (ids that carry locality) the hops walk the rows in order, else longest     */
+/* rows first — a schedule only, the results are the same bits.                                       */
 int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col, const float* val,
                   int d, const float* X, int T, float alpha, float* target, float* p_last,
                   float* p_tmp, void* ws, size_t ws_bytes, gdd_stream_t stream);
@@ -85,7 +88,9 @@ int gdd_propagate(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* 
 /* gathers after the first go through rho[col]; every row keeps its entries in CSR order, so target  */
 /* and p_last (both by the original ids: the first hop reads X by them, the last hop stores by them)  */
 /* are bit-identical to gdd_propagate's. A locality order (hubs first, RCM, communities) lets the    */
-/* gathered rows of a hop share cache lines and pages; no separate permutation pass.                  */
+/* gathered rows of a hop share cache lines and pages; no separate permutation pass. r06: every hop's */
+/* work list walks the rows in the new order (consecutive items gather neighbouring rows). rho is not */
+/* checked on the device: a non-permutation writes out of bounds (gdd.propagate checks it on the host).*/
 size_t gdd_propagate_relabeled_ws_bytes(int64_t n, int64_t nnz, int d);
 int gdd_propagate_relabeled(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* col,
                             const float* val, const int32_t* rho, int d, const float* X, int T,
