@@ -171,7 +171,8 @@ def test_minibatch_tol_path():
 @pytest.mark.parametrize("n,dim,k,form", [(50000, 40, 454, ""), (3000, 7, 70, ""), (20000, 64, 200, ""),
                                           (1000, 47, 1, ""), (40000, 41, 769, ""), (40000, 41, 769, "bf16_w4"),
                                           (9000, 45, 100, "bf16_w8"), (9000, 45, 100, "bf16_v1"),
-                                          (3000, 200, 30, "")])
+                                          (3000, 200, 30, ""), (33, 41, 5, ""), (95, 47, 3, ""),
+                                          (64, 45, 40, "bf16_w8")])
 def test_assign_bf16_within_rounding(n, dim, k, form, monkeypatch):
     # the bf16 distance variant: labels equal the exact fp32 ones except where two
     # centres' distances lie within the bf16 rounding of the dot products (2^-7 ||x|| ||c|| each).
@@ -190,7 +191,8 @@ def test_assign_bf16_within_rounding(n, dim, k, form, monkeypatch):
     ops.assign(Xd, Cd, labels=l16, sq=sq16, precision="bf16")
     a, b = l32.cpu().numpy(), l16.cpu().numpy()
     assert b.min() >= 0 and b.max() < k
-    assert (a == b).mean() >= 0.95  # near-ties are common here: centres sit among the points
+    if n >= 1000:  # near-ties are common here (centres sit among the points); tiny n: the bound alone
+        assert (a == b).mean() >= 0.95
     diff = np.nonzero(a != b)[0]
     X64, C64 = X.astype(np.float64), C.astype(np.float64)
     xn = np.linalg.norm(X64, axis=1)
