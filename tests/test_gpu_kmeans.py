@@ -561,3 +561,41 @@ def test_minibatch_handoff_then_convergence_stop(n, dim, k, bs, mni):
     assert m.inertia_ == ref["inertia_"]
     s = rs.get_state()
     assert np.array_equal(s[1], s_ref[1]) and s[2] == s_ref[2]
+
+
+def test_assign_bf16_gathered_rows_unaligned_and_predict():
+    """The bf16 pass's other entries: a row list (the chunked kernel + finalize), an X that is not
+    16-byte aligned (a view one row in, dim 41), and KMeans.predict(precision="bf16") — each label
+    the exact fp32 one or within the bf16 rounding bound; predict at fp32 gives the exact labels."""
+    from gdd.kmeans import _Ops
+    rng = np.random.default_rng(12)
+    n, dim, k = 20001, 41, 97
+    Xall = (rng.standard_normal((n + 1, dim)) + rng.integers(0, 4, (n + 1, 1))).astype(np.float32)
+    C = Xall[rng.choice(n, k, replace=False)] + rng.standard_normal((k, dim)).astype(np.float32) * 0.1
+    Xd_all = torch.from_numpy(Xall).cuda()
+    Xu = Xd_all[1:]  # 164 bytes in: not 16-byte aligned
+    assert Xu.data_ptr() % 16 != 0
+    Cd = torch.from_numpy(C).cuda()
+    ops = _Ops("cuda", n + 1, k, dim)
+    lab = {}
+    for name, X, rows in (("unaligned", Xu, None), ("rows", Xd_all, torch.arange(1, n + 1, device="cuda"))):
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        ops.assign(X, Cd, rows=rows, labels=out, precision="bf16")
+        lab[name] = out.cpu().numpy()
+    exact = torch.empty(n, dtype=torch.int32, device="cuda")
+    ops.assign(Xu.contiguous(), Cd, labels=exact)
+    a = exact.cpu().numpy()
+    X64, C64 = Xall[1:].astype(np.float64), C.astype(np.float64)
+    xn, cn = np.linalg.norm(X64, axis=1), np.linalg.norm(C64, axis=1)
+    for name, b in lab.items():
+        assert b.min() >= 0 and b.max() < k
+        for i in np.nonzero(a != b)[0][:2000]:
+            di = ((X64[i] - C64) ** 2).sum(-1)
+            assert di[b[i]] - di[a[i]] <= 2 * 2.0 ** -7 * xn[i] * (cn[a[i]] + cn[b[i]]) + 1e-3 * (1 + di[a[i]]), name
+    km = gdd.KMeans(n_clusters=k)
+    km.cluster_centers_ = C
+    p = km.predict(Xall[1:], precision="bf16")
+    for i in np.nonzero(a != p)[0][:2000]:
+        di = ((X64[i] - C64) ** 2).sum(-1)
+        assert di[p[i]] - di[a[i]] <= 2 * 2.0 ** -7 * xn[i] * (cn[a[i]] + cn[p[i]]) + 1e-3 * (1 + di[a[i]])
+    assert np.array_equal(km.predict(Xall[1:]), a)  # fp32 predict: the exact labels
