@@ -679,7 +679,8 @@ def products_record(dev, with_cpu, group=None, world=1):
     assign = {p: {"avg_launch_ms": times[p], "achieved": flops / (times[p] * 1e-3) / 1e12,
                   "peak": peaks[p], "unit": "TFLOP/s",
                   "frac": flops / (times[p] * 1e-3) / 1e12 / peaks[p],
-                  "x_read_gbs": 4.0 * cfg.n * cfg.n_classes / (times[p] * 1e-3) / 1e9}
+                  "x_read_gbs": 4.0 * cfg.n * cfg.n_classes / (times[p] * 1e-3) / 1e9,
+                  "x_read_frac_of_hbm": 4.0 * cfg.n * cfg.n_classes / (times[p] * 1e-3) / 1e9 / HBM_PEAK_GBS}
               for p in ("fp32", "bf16")}
     rec = {"workload": f"ogbn-products shape (config 5): N={cfg.n}, nnz_norm={gn.nnz}, d={cfg.d}, "
                        f"C={cfg.n_classes}, {cfg.T - 1} hops (alpha {cfg.alpha}), KMeans(k={cfg.k}, "
