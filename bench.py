@@ -660,19 +660,22 @@ def products_record(dev, with_cpu, group=None, world=1):
     # the labels pass at fp32 (exact, sklearn's bits) and bf16 (opt-in, config 5), same centres
     C = km.cluster_centers_device_.contiguous()
     ops = _Ops(dev, cfg.n, cfg.k, cfg.n_classes)
+    # three alternating rounds, the best of each: the two passes draw different power, and the one
+    # timed right after the other inherits its clock state (r06: ~10% either way)
     labs, times = {}, {}
-    for prec in ("fp32", "bf16"):
-        lab = torch.empty(cfg.n, dtype=torch.int32, device=dev)
-        for _ in range(3):
-            ops.assign(logits, C, labels=lab, precision=prec)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        ev[0].record()
-        for _ in range(10):
-            ops.assign(logits, C, labels=lab, precision=prec)
-        ev[1].record()
-        torch.cuda.synchronize()
-        times[prec] = ev[0].elapsed_time(ev[1]) / 10
-        labs[prec] = lab
+    for _ in range(3):
+        for prec in ("fp32", "bf16"):
+            lab = torch.empty(cfg.n, dtype=torch.int32, device=dev)
+            for _ in range(3):
+                ops.assign(logits, C, labels=lab, precision=prec)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            for _ in range(10):
+                ops.assign(logits, C, labels=lab, precision=prec)
+            ev[1].record()
+            torch.cuda.synchronize()
+            times[prec] = min(times.get(prec, 1e9), ev[0].elapsed_time(ev[1]) / 10)
+            labs[prec] = lab
     flops = 2.0 * cfg.n * cfg.k * cfg.n_classes
     agree = float((labs["fp32"] == labs["bf16"]).float().mean().item())
     peaks = {"fp32": FP32_MATRIX_PEAK_TFLOPS, "bf16": BF16_DENSE_PEAK_TFLOPS}
