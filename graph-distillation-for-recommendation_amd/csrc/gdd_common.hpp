@@ -102,6 +102,7 @@ bool bf16q_norms_fit(int dim, int k);
 //   kpp_no_big1       the per-block table rounds instead of one workgroup per trial (n <= 16,384)
 //   kpp_big1_max=N    one workgroup per trial up to N points (default 16,384, at most 32,768)
 //   kpp_single_round  one table round per launch instead of the pair launches (T <= 8)
+//   kpp_pair_serial   the single-block pair launch's two folds one after the other (not overlapped)
 //   kpp_two_launch    the single-block rounds' distance + pick launches instead of the fused round
 //   kpp_no_split      the per-(block, trial) rounds instead of the split rounds (>= 128 blocks)
 //   lloyd_no_prune    every Lloyd E-step over every row (no bounds)

@@ -1882,6 +1882,134 @@ __device__ __forceinline__ bool prefix_waves_sync(int* ctr, int target) {
   return false;
 }
 
+// ---- the fold's parts (kpp1_fold_trial, kpp1_fold_pair) ----------------------------------------------
+// wave 0: trial t's exact sgemv_t potential over the row in s_d (chain-major copy in s_ch for unit
+// weights): the lane chains, then the n % 4 trailing entries; lane 0 returns it
+__device__ __forceinline__ float fold_potential(const Kpp1Args& a, const float* __restrict__ s_d,
+                                                const float* __restrict__ s_ch, int t, bool k4x2, int h4) {
+  const int lane = threadIdx.x & 63;
+  const int T = a.T, n = (int)a.n, m1 = (int)a.m1;
+  float y = 0.f;
+  if (m1 > 0) {
+    if (a.w == nullptr) {
+      const int nl = k4x2 ? 4 : 8;
+      float acc = 0.f;
+      if (lane < nl) {
+        if (lane < h4) acc = acc + s_d[lane];
+        const int L = (m1 - h4 - lane + nl - 1) / nl;
+        acc = chain_add(s_ch + lane * kChainLd, max(L, 0), acc);
+      }
+      if (k4x2) {
+        const float a1 = __shfl(acc, 1), a2 = __shfl(acc, 2), a3 = __shfl(acc, 3);
+        y = (acc + a1) + (a2 + a3);
+      } else {
+        const float ql = acc + __shfl(acc, (lane + 4) & 63);
+        const float q1 = __shfl(ql, 1), q2 = __shfl(ql, 2), q3 = __shfl(ql, 3);
+        y = (ql + q1) + (q2 + q3);
+      }
+    } else {
+      y = sgemv_block_wave(s_d, a.w, m1, t, T);
+    }
+  }
+  if (m1 < n && lane == 0) {
+    float sx = s_d[m1] * wv(a.w, m1);
+    for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_d[o], wv(a.w, o), sx);
+    y = y + sx;
+  }
+  return y;
+}
+
+// waves 1-3 (prefix thread jp = tid - 64): the thread's run over entries kFPW jp .. + kFPW - 1 of s_d
+// (w * x in fp32, then fp64 adds), the wave's exclusive offset added; the wave total into
+// s_wave[wave - 1]. Every read issued before the run (a per-entry weight branch had each read waited
+// on alone: ~2 us, as long as the chains, r04 stamps); entries past n add +0.0
+__device__ __forceinline__ void fold_prefix(const Kpp1Args& a, const float* __restrict__ s_d, int jp,
+                                            double (&pre)[kFPW], double* __restrict__ s_wave) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = (int)a.n;
+  float xv[kFPW];
+#pragma unroll
+  for (int q = 0; q < kFPW; ++q) xv[q] = s_d[min(kFPW * jp + q, n - 1)];
+  if (a.w) {
+#pragma unroll
+    for (int q = 0; q < kFPW; ++q) {
+      const int e = kFPW * jp + q;
+      xv[q] = e < n ? a.w[min(e, n - 1)] * xv[q] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < kFPW; ++q) xv[q] = kFPW * jp + q < n ? xv[q] : 0.f;  // 1.0f * x == x
+  }
+  double run = 0.0;
+#pragma unroll
+  for (int q = 0; q < kFPW; ++q) {
+    run = run + (double)xv[q];
+    pre[q] = run;
+  }
+  double inc = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double y = __shfl_up(inc, o);
+    if (lane >= o) inc = inc + y;
+  }
+  double ex = __shfl_up(inc, 1);
+  if (lane == 0) ex = 0.0;
+  if (lane == 63) s_wave[wave - 1] = inc;
+#pragma unroll
+  for (int q = 0; q < kFPW; ++q) pre[q] = ex + pre[q];
+}
+
+// the regular draws for the uniforms in `redo` (lane q of every wave holds u_q in ut) over the complete
+// cumulative potential s_cum: searchsorted_left(cum, u * pot) in two ballots. Lane l of every wave
+// holds the last value of block l (64 blocks of Bk = ceil(n / 64) entries); wave w takes uniforms w,
+// w + 4, ...: the blocks below r counted by one ballot, then one LDS read per lane and a ballot inside
+// the next block — two LDS trips instead of log2(n) dependent ones. The rounding check covers the
+// block's entries and the entry before it (every deciding neighbour; a count that differs from
+// numpy's needs a prefix within tol of r, non-monotone rounding steps included)
+__device__ __forceinline__ void fold_search(const Kpp1Args& a, unsigned long long redo, double ut, double pot,
+                                            const double* __restrict__ s_cum, const float* __restrict__ s_d,
+                                            int64_t* cand_out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int T = a.T, n = (int)a.n;
+  const int Bk = (n + 63) >> 6;
+  const int nb = (n + Bk - 1) / Bk;
+  const double cl = s_cum[min((lane + 1) * Bk, n) - 1];
+  for (int t2 = wave; t2 < T; t2 += (int)(blockDim.x >> 6)) {
+    if (!((redo >> t2) & 1ull)) continue;
+    const double rr = __shfl(ut, t2) * pot;
+    const double tol = cum_tol(a.exact, n, rr);
+    const int c0 = __popcll(__ballot(lane < nb && cl < rr));
+    int idx;
+    bool amb;
+    if (c0 >= nb) {
+      idx = n;
+      amb = fabs(__shfl(cl, nb - 1) - rr) <= tol;
+    } else {
+      const int e = c0 * Bk + lane;
+      const bool live = lane < Bk && e < n;
+      const double v = live ? s_cum[min(e, n - 1)] : 0.0;
+      idx = c0 * Bk + __popcll(__ballot(live && v < rr));
+      const double prev = __shfl(cl, c0 > 0 ? c0 - 1 : 0);
+      amb = __ballot(live && fabs(v - rr) <= tol) != 0ull || (c0 > 0 && fabs(prev - rr) <= tol);
+    }
+    if (amb) {
+      int rep = 0;
+      if (lane == 0) rep = (int)np_cumsum_search(s_d, a.w, n, rr);
+      idx = __shfl(rep, 0);
+    }
+    if (lane == 0) cand_out[t2] = min(n - 1, idx);
+  }
+}
+
+// a speculative draw is numpy's index when the exact threshold rr falls between the same two
+// cumulative values (lo: entry idx - 1, hi: entry idx), neither within 4 cum_tol of it
+__device__ __forceinline__ bool spec_draw_good(const Kpp1Args& a, int idx, double lo, double hi, double rr) {
+  const int n = (int)a.n;
+  const double tol = cum_tol(a.exact, n, rr);
+  return tol >= 0.0 && (idx == 0 || (lo < rr && fabs(lo - rr) > 4.0 * tol)) &&
+         (idx == n || (!(hi < rr) && fabs(hi - rr) > 4.0 * tol));
+}
+
 // the fold of round c's trial t by one 256-thread workgroup holding the trial's row in registers
 // (r[q] = entry tid + 256 q): the exact sgemv_t potential, the fp64 cumulative potential and the
 // candidates every trial would draw in round c+1 if t wins
@@ -1937,71 +2065,14 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
   const int jp = tid - 64;  // prefix thread of waves 1..3
   double pre[kFPW];
   if (wave == 0) {  // sgemv_t: the lane chains, then the n % 4 trailing entries
-    float y = 0.f;
-    if (m1 > 0) {
-      if (perm) {
-        const int nl = k4x2 ? 4 : 8;
-        float acc = 0.f;
-        if (lane < nl) {
-          if (lane < h4) acc = acc + s_d[lane];
-          const int L = (m1 - h4 - lane + nl - 1) / nl;
-          acc = chain_add(s_ch + lane * kChainLd, max(L, 0), acc);
-        }
-        if (k4x2) {
-          const float a1 = __shfl(acc, 1), a2 = __shfl(acc, 2), a3 = __shfl(acc, 3);
-          y = (acc + a1) + (a2 + a3);
-        } else {
-          const float ql = acc + __shfl(acc, (lane + 4) & 63);
-          const float q1 = __shfl(ql, 1), q2 = __shfl(ql, 2), q3 = __shfl(ql, 3);
-          y = (ql + q1) + (q2 + q3);
-        }
-      } else {
-        y = sgemv_block_wave(s_d, a.w, m1, t, T);
-      }
-    }
-    if (m1 < n && lane == 0) {
-      float sx = s_d[m1] * wv(a.w, m1);
-      for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_d[o], wv(a.w, o), sx);
-      y = y + sx;
-    }
+    const float y = fold_potential(a, s_d, s_ch, t, k4x2, h4);
     if (lane == 0) {
       s_pot = y;
       if (pot_out) *pot_out = y;
     }
     GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 76);
   } else {  // the cumulative potential: thread runs and the wave's inclusive scan
-    // every read issued before the run (a per-entry weight branch had each read waited on alone:
-    // ~2 us, as long as the chains, r04 stamps); entries past n add +0.0, as before
-    float xv[kFPW];
-#pragma unroll
-    for (int q = 0; q < kFPW; ++q) xv[q] = s_d[min(kFPW * jp + q, n - 1)];
-    if (a.w) {
-#pragma unroll
-      for (int q = 0; q < kFPW; ++q) {
-        const int e = kFPW * jp + q;
-        xv[q] = e < n ? a.w[min(e, n - 1)] * xv[q] : 0.f;
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < kFPW; ++q) xv[q] = kFPW * jp + q < n ? xv[q] : 0.f;  // 1.0f * x == x
-    }
-    double run = 0.0;
-#pragma unroll
-    for (int q = 0; q < kFPW; ++q) {
-      run = run + (double)xv[q];
-      pre[q] = run;
-    }
-    double inc = run;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const double y = __shfl_up(inc, o);
-      if (lane >= o) inc = inc + y;
-    }
-    double ex = __shfl_up(inc, 1);
-    if (lane == 0) ex = 0.0;
-    if (lane == 63) s_wave[wave - 1] = inc;
-#pragma unroll
-    for (int q = 0; q < kFPW; ++q) pre[q] = ex + pre[q];
+    fold_prefix(a, s_d, jp, pre, s_wave);
     GDD_STAMP_WHEN(g_stamps_kpp, (tid == 64 && t == 0 && c == a.k - 2), 75);
     if (spec) {
       bool ok = prefix_waves_sync(&s_sync, 3);
@@ -2056,13 +2127,9 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
     // the check, one lane per uniform; s_cum is complete (written before the barrier)
     bool good = false;
     if (tid < T && s_sok) {
-      const double rr = ut * (double)s_pot;
-      const double tol = cum_tol(a.exact, n, rr);
       const int idx = s_sidx[tid];
-      const double lo = idx > 0 ? s_cum[idx - 1] : -1.0;
-      const double hi = idx < n ? s_cum[idx] : 0.0;
-      good = tol >= 0.0 && (idx == 0 || (lo < rr && fabs(lo - rr) > 4.0 * tol)) &&
-             (idx == n || (!(hi < rr) && fabs(hi - rr) > 4.0 * tol));
+      good = spec_draw_good(a, idx, idx > 0 ? s_cum[idx - 1] : -1.0, idx < n ? s_cum[idx] : 0.0,
+                            ut * (double)s_pot);
       if (good) cand_out[tid] = min(n - 1, idx);
     }
     redo = __ballot(tid < T && !good);  // wave 0's lanes tid < T
@@ -2090,43 +2157,7 @@ __device__ __forceinline__ void kpp1_fold_trial(const Kpp1Args& a, int c, int t,
       (void)pot;
     }
     __syncthreads();
-    {
-      // searchsorted_left(cum, u * pot) in two ballots: lane l of every wave holds the last value of
-      // block l (64 blocks of Bk = ceil(n / 64) entries); wave w takes uniforms w, w + 4, ...: the
-      // blocks below r counted by one ballot, then one LDS read per lane and a ballot inside the next
-      // block — two LDS trips instead of log2(n) dependent ones. The rounding check covers the block's
-      // entries and the entry before it (every deciding neighbour; a count that differs from numpy's
-      // needs a prefix within tol of r, non-monotone rounding steps included)
-      const int Bk = (n + 63) >> 6;
-      const int nb = (n + Bk - 1) / Bk;
-      const double cl = s_cum[min((lane + 1) * Bk, n) - 1];
-      const double pot = (double)s_pot;
-      for (int t2 = wave; t2 < T; t2 += (int)(blockDim.x >> 6)) {
-        if (!((redo >> t2) & 1ull)) continue;
-        const double rr = __shfl(ut, t2) * pot;
-        const double tol = cum_tol(a.exact, n, rr);
-        const int c0 = __popcll(__ballot(lane < nb && cl < rr));
-        int idx;
-        bool amb;
-        if (c0 >= nb) {
-          idx = n;
-          amb = fabs(__shfl(cl, nb - 1) - rr) <= tol;
-        } else {
-          const int e = c0 * Bk + lane;
-          const bool live = lane < Bk && e < n;
-          const double v = live ? s_cum[min(e, n - 1)] : 0.0;
-          idx = c0 * Bk + __popcll(__ballot(live && v < rr));
-          const double prev = __shfl(cl, c0 > 0 ? c0 - 1 : 0);
-          amb = __ballot(live && fabs(v - rr) <= tol) != 0ull || (c0 > 0 && fabs(prev - rr) <= tol);
-        }
-        if (amb) {
-          int rep = 0;
-          if (lane == 0) rep = (int)np_cumsum_search(s_d, a.w, n, rr);
-          idx = __shfl(rep, 0);
-        }
-        if (lane == 0) cand_out[t2] = min(n - 1, idx);
-      }
-    }
+    fold_search(a, redo, ut, (double)s_pot, s_cum, s_d, cand_out);
   }
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 74);
 }
@@ -2415,6 +2446,190 @@ __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __rest
                   a.candw[cq] + (int64_t)t * T);
 }
 
+// ---- a pair launch's two folds overlapped (r06). The serial form (kpp1_fold_trial twice) runs round
+// c's fold, then loads round c+1's row, then folds it: two lane-chain runs (~2 us each at 3,000
+// entries) and the row's load one after another. Here wave 0 runs round c's chains while waves 1-3
+// finish its cumulative potential, draw slot t2's candidate with the fp64 total standing in for the
+// potential (kpp1_fold_trial's speculative search), load that candidate's table row, form round c+1's
+// row and its cumulative potential and speculatively draw round c+2's candidates; wave 0 then checks
+// the slot-t2 draw against round c's exact potential and runs round c+1's chains. Waves 1-3 meet on an
+// LDS arrival counter and never wait for wave 0. If the check fails (the threshold within 4 cum_tol of
+// a deciding prefix, or the stand-in potential moved the count), or a bounded spin gives up, the call
+// returns false after its barrier and the caller redoes the pair serially — so every result is the
+// serial form's. Level-1 row in r (entry tid + 256 q), trial w's lane form; level 2 trial t2's.
+__device__ __forceinline__ bool kpp1_fold_pair(const Kpp1Args& a, const float* __restrict__ D, int c, int w,
+                                               int t2, int lq, const float (&r)[16], double ut, double ut2,
+                                               float* __restrict__ s_d, float* __restrict__ s_ch,
+                                               float* __restrict__ s_d2, float* __restrict__ s_ch2,
+                                               double* __restrict__ s_cum, double* __restrict__ s_wave) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = a.T, n = (int)a.n, m1 = (int)a.m1;
+  const bool perm = a.w == nullptr;
+  const int j = w * T + t2;
+  const bool k4x2_1 = (T & 2) && w >= (T & ~3) && w < (T & ~3) + 2;
+  const bool k4x2_2 = (T & 2) && t2 >= (T & ~3) && t2 < (T & ~3) + 2;
+  const int h4_1 = k4x2_1 ? 0 : (m1 & 4), h4_2 = k4x2_2 ? 0 : (m1 & 4);
+  const bool spec2 = c + 2 < a.k;  // round c+1 draws round c+2's candidates
+  __shared__ int s_arr;            // waves 1-3: arrivals
+  __shared__ int s_fail;           // a check or a bounded spin failed: the caller redoes the pair
+  __shared__ int s_idx1;           // slot t2's speculative draw and its deciding neighbours
+  __shared__ double s_lo1, s_hi1;
+  __shared__ int s_sidx2[kMaxTrials];
+  __shared__ float s_pot2;
+  if (tid == 0) {
+    s_arr = 0;
+    s_fail = 0;
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = tid + 256 * q;
+    if (e < n) {
+      s_d[e] = r[q];
+      if (perm && e >= h4_1 && e < m1) {
+        const int o = e - h4_1;
+        if (k4x2_1)
+          s_ch[(o & 3) * kChainLd + (o >> 2)] = r[q];
+        else
+          s_ch[(o & 7) * kChainLd + (o >> 3)] = r[q];
+      }
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float y = fold_potential(a, s_d, s_ch, w, k4x2_1, h4_1);
+    y = __shfl(y, 0);
+    if (lane == 0 && t2 == 0) a.potv[lq][w] = y;
+    bool ok = waves_wait(&s_arr, 9);  // slot t2's draw published
+    ok = ok && spec_draw_good(a, s_idx1, s_lo1, s_hi1, __shfl(ut, t2) * (double)y);
+    ok = ok && waves_wait(&s_arr, 12);  // round c+1's row complete
+    if (!ok) {
+      if (lane == 0) s_fail = 1;
+    } else {
+      const float y2 = fold_potential(a, s_d2, s_ch2, t2, k4x2_2, h4_2);
+      if (lane == 0) {
+        s_pot2 = y2;
+        a.potv2[lq][j] = y2;
+      }
+    }
+  } else {
+    const int jp = tid - 64;
+    double pre[kFPW];
+    fold_prefix(a, s_d, jp, pre, s_wave);
+    bool ok = prefix_waves_sync(&s_arr, 3);
+    double B = 0.0;
+    for (int q = 0; q < wave - 1; ++q) B = B + s_wave[q];
+#pragma unroll
+    for (int q = 0; q < kFPW; ++q) {
+      const int e = kFPW * jp + q;
+      if (e < n) s_cum[e] = B + pre[q];
+    }
+    ok = prefix_waves_sync(&s_arr, 6) && ok;
+    // slot t2's draw, by each of the three waves (same bits): searchsorted_left in two ballots
+    const int Bk = (n + 63) >> 6;
+    const int nb = (n + Bk - 1) / Bk;
+    int idx = n;
+    {
+      const double cl = s_cum[min((lane + 1) * Bk, n) - 1];
+      const double rr = __shfl(ut, t2) * (double)(float)s_cum[n - 1];
+      const int c0 = __popcll(__ballot(lane < nb && cl < rr));
+      if (c0 < nb) {
+        const int e = c0 * Bk + lane;
+        const bool live = lane < Bk && e < n;
+        const double v = s_cum[min(e, n - 1)];
+        idx = c0 * Bk + __popcll(__ballot(live && v < rr));
+      }
+    }
+    if (wave == 1 && lane == 0) {
+      s_idx1 = idx;
+      s_lo1 = idx > 0 ? s_cum[idx - 1] : -1.0;
+      s_hi1 = idx < n ? s_cum[idx] : 0.0;
+    }
+    ok = prefix_waves_sync(&s_arr, 9) && ok;  // every read of round c's s_cum and s_wave done
+    // round c+1's row: entries jp + 192 q, against the speculatively drawn candidate's table row
+    {
+      const int64_t c1 = min(n - 1, idx);
+      const float* drow = D + c1 * n;
+      float* orow = a.dist2[lq] + (int64_t)j * n;
+      float dd[kFPW];
+#pragma unroll
+      for (int q = 0; q < kFPW; ++q) dd[q] = drow[min(jp + 192 * q, n - 1)];
+#pragma unroll
+      for (int q = 0; q < kFPW; ++q) {
+        const int e = jp + 192 * q;
+        if (e < n) {
+          const float f = np_minimum(s_d[e], dd[q]);
+          orow[e] = f;
+          s_d2[e] = f;
+          if (perm && e >= h4_2 && e < m1) {
+            const int o = e - h4_2;
+            if (k4x2_2)
+              s_ch2[(o & 3) * kChainLd + (o >> 2)] = f;
+            else
+              s_ch2[(o & 7) * kChainLd + (o >> 3)] = f;
+          }
+        }
+      }
+    }
+    ok = prefix_waves_sync(&s_arr, 12) && ok;  // the row complete (wave 0 waits for it)
+    fold_prefix(a, s_d2, jp, pre, s_wave);
+    ok = prefix_waves_sync(&s_arr, 15) && ok;
+    B = 0.0;
+    for (int q = 0; q < wave - 1; ++q) B = B + s_wave[q];
+#pragma unroll
+    for (int q = 0; q < kFPW; ++q) {
+      const int e = kFPW * jp + q;
+      if (e < n) s_cum[e] = B + pre[q];
+    }
+    ok = prefix_waves_sync(&s_arr, 18) && ok;
+    if (spec2) {  // round c+2's draws with the fp64 total for round c+1's potential (4 per wave)
+      const double pot_s = (double)(float)s_cum[n - 1];
+      const double cl = s_cum[min((lane + 1) * Bk, n) - 1];
+      double rrs[4], vv[4];
+      int c0s[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int u2 = wave - 1 + 3 * i;
+        rrs[i] = __shfl(ut2, min(u2, T - 1)) * pot_s;
+        c0s[i] = __popcll(__ballot(lane < nb && cl < rrs[i]));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) vv[i] = s_cum[min(c0s[i] * Bk + lane, n - 1)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int u2 = wave - 1 + 3 * i;
+        if (u2 >= T) continue;
+        int id2 = n;
+        if (c0s[i] < nb) {
+          const int e = c0s[i] * Bk + lane;
+          const bool live = lane < Bk && e < n;
+          id2 = c0s[i] * Bk + __popcll(__ballot(live && vv[i] < rrs[i]));
+        }
+        if (lane == 0) s_sidx2[u2] = id2;
+      }
+    }
+    if (!ok && lane == 0) s_fail = 1;
+  }
+  __syncthreads();
+  if (s_fail) return false;
+  if (tid == 0) a.candself2[lq][j] = min(n - 1, s_idx1);
+  if (!spec2) return true;
+  // round c+1's draws: the check (lane q of wave 0 for uniform q), the regular search for the rest
+  int64_t* cand_out = a.candw2[lq] + (int64_t)j * T;
+  const double pot2 = (double)s_pot2;
+  bool good = false;
+  if (tid < T) {
+    const int idx = s_sidx2[tid];
+    good = spec_draw_good(a, idx, idx > 0 ? s_cum[idx - 1] : -1.0, idx < n ? s_cum[idx] : 0.0, ut2 * pot2);
+    if (good) cand_out[tid] = min(n - 1, idx);
+  }
+  __shared__ unsigned long long s_redo;
+  const unsigned long long redo = __ballot(tid < T && !good);  // wave 0's lanes tid < T
+  if (tid == 0) s_redo = redo;
+  __syncthreads();
+  if (s_redo != 0ull) fold_search(a, s_redo, ut2, pot2, s_cum, s_d2, cand_out);
+  return true;
+}
+
 // ---- two rounds per launch over the distance table (default for table plans, T <= 8). Workgroup
 // w * T + t runs round c+1's trial t on the assumption that round c's trial w wins: it forms trial w's
 // row and folds it (same operands, same slot, so bit-identical to what a round-c workgroup w would
@@ -2428,9 +2643,11 @@ __global__ __launch_bounds__(256) void k_kpp1_dm(Kpp1Args a, const float* __rest
 constexpr int kPairMaxT = 8;  // T * T <= 64: one wave lane per round-(c-1) candidate
 
 __global__ __launch_bounds__(256) void k_kpp1_dm2(Kpp1Args a, const float* __restrict__ D, int c, int lq,
-                                                  int pair) {
+                                                  int pair, int overlap) {
   __shared__ float s_d[kBlk];
   __shared__ float s_ch[8 * kChainLd];
+  __shared__ float s_d2[kBlk];             // the overlapped form: round c+1's row
+  __shared__ float s_ch2[8 * kChainLd];
   __shared__ double s_cum[kBlk];
   __shared__ double s_wave[4];
   __shared__ float s_pot;
@@ -2507,6 +2724,8 @@ __global__ __launch_bounds__(256) void k_kpp1_dm2(Kpp1Args a, const float* __res
                     a.candw[lq] + (int64_t)w * T);
     return;
   }
+  if (overlap && kpp1_fold_pair(a, D, c, w, t2, lq, r, ut, ut2, s_d, s_ch, s_d2, s_ch2, s_cum, s_wave)) return;
+  __syncthreads();  // (after a failed overlapped pair: its LDS reads done before the serial form's writes)
   kpp1_fold_trial(a, c, w, r, ut, s_d, s_ch, s_cum, s_wave, &s_pot, t2 == 0 ? a.potv[lq] + w : nullptr,
                   s_cand);
   __syncthreads();
@@ -2612,36 +2831,330 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// the 1024-thread table rounds' shared state besides the row (k_kpp1_big, k_kpp1_big2)
+struct BigLds {
+  double wt[kBigWaves];
+  float vb[8];
+  float pot;
+  int cnt[kMaxTrials];
+  int part[kMaxTrials];
+  int amb[kMaxTrials];
+  double off[kBigThr], first[kBigThr], last[kBigThr];
+  int arr;                 // speculative draws: waves that wrote their prefix data
+  int sidx[kMaxTrials];    // speculative draws: counts (-1: not usable)
+  double lo[kMaxTrials], hi[kMaxTrials];  // and their deciding neighbours
+  unsigned long long redo;  // the uniforms the regular draws take
+};
+
+// a fold's counters, zeroed before the barrier that publishes its row
+__device__ __forceinline__ void big_fold_reset(BigLds& L) {
+  const int tid = threadIdx.x;
+  if (tid < kMaxTrials) {
+    L.part[tid] = 0;
+    L.amb[tid] = 0;
+  }
+  if (tid == 0) L.arr = 0;
+}
+
+// The fold of round c's trial t over the row in s_row (entries [0, n), zeros up to kBigThr * EPT):
+// the potential (pot_out, nullable) and the candidates round c+1's T uniforms draw if t wins
+// (cand_out[0..T), global memory or LDS). Lane q < T of every wave holds u_q = uniforms[c T + q] in ut.
+// Called after a barrier that follows big_fold_reset and the row's stores.
 template <int EPT>
-__global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* __restrict__ D, int c) {
-  extern __shared__ __attribute__((aligned(16))) float s_row[];  // kBigThr * EPT + kChainPad floats
-  __shared__ double s_wt[kBigWaves];
-  __shared__ float s_vb[8];
-  __shared__ float s_pot;
-  __shared__ int s_cnt[1][kMaxTrials];
-  __shared__ int s_part[kMaxTrials];
-  __shared__ int s_amb[kMaxTrials];
-  __shared__ double s_off[kBigThr], s_first[kBigThr], s_last[kBigThr];
-  __shared__ int s_arr;                 // speculative draws: waves that wrote their prefix data
-  __shared__ int s_sidx[kMaxTrials];    // speculative draws: counts (-1: not usable)
-  __shared__ double s_lo[kMaxTrials], s_hi[kMaxTrials];  // and their deciding neighbours
-  __shared__ unsigned long long s_redo;  // the uniforms the regular draws take
+__device__ __forceinline__ void big_fold(const Kpp1Args& a, int c, int t, double ut, const float* s_row,
+                                         BigLds& L, float* pot_out, int64_t* cand_out) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = a.T;
   const int n = (int)a.n, m1 = (int)a.m1;
-  const int t = blockIdx.x;
-  const int cq = c & 1, pq = (c - 1) & 1;
   const int nsg = (m1 + kBlk - 1) / kBlk;  // chain waves (4096-entry sgemv_t blocks)
   // speculative draws (r04): waves nsg .. nsg + T - 1 draw round c+1's candidates while waves < nsg
   // run the lane chains, the fp64 total standing in for the potential; checked after it (below)
   const bool spec = c >= 1 && c + 1 < a.k && nsg + T <= kBigWaves;
+  // ---- this thread's segment: products (fp32) and its fp64 run
+  const int e0 = EPT * tid;
+  float v[EPT];
+#pragma unroll
+  for (int q = 0; q < EPT; q += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(s_row + e0 + q);
+    v[q] = x.x;
+    v[q + 1] = x.y;
+    v[q + 2] = x.z;
+    v[q + 3] = x.w;
+  }
+  if (a.w) {
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) v[q] = e0 + q < n ? a.w[e0 + q] * v[q] : 0.f;
+  }
+  double tot = 0.0;
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) tot = tot + (double)v[q];
+  double inc = tot;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double y = __shfl_up(inc, o);
+    if (lane >= o) inc = inc + y;
+  }
+  double ex = __shfl_up(inc, 1);
+  if (lane == 0) ex = 0.0;
+  if (lane == 63) L.wt[wave] = inc;
+  if (spec) {  // until the barrier below L.off / L.last hold each segment's in-wave prefix and total
+    L.off[tid] = ex;
+    L.last[tid] = tot;
+    waves_arrive(&L.arr);
+  }
+  // the sgemv_t block terms (rounds >= 1)
+  if (c >= 1 && wave < nsg) {
+    const int j0 = wave * kBlk;
+    const float vb = sgemv_block_lds(s_row, a.w, j0, min(kBlk, m1 - j0), t, T);
+    if (lane == 0) L.vb[wave] = vb;
+  } else if (spec && wave - nsg < T) {
+    // searchsorted_left(cum, u * pot_s), pot_s = fp32(fp64 total), without the rounding check (the
+    // check after the potential decides): the wave totals' running sum finds the group of 64
+    // segments (contiguous entries) holding the threshold, one ballot over that group's segment
+    // ends counts the segments below, the segment that straddles it is walked. Offsets are the
+    // group's running sum plus the in-wave prefix — within fp64 roundings of the regular ones: a
+    // count they change has a value within 4 cum_tol of the threshold, which the check refuses.
+    // One group per uniform keeps the LDS reads beside the chains small.
+    const int t2 = wave - nsg;
+    bool ok = waves_wait(&L.arr, kBigWaves);
+    double tall = 0.0;
+    for (int q = 0; q < kBigWaves; ++q) tall = tall + L.wt[q];
+    const double rr = readlane_f64(ut, t2) * (double)(float)tall;
+    int g = 0;
+    double W = 0.0, Wg = 0.0;
+    for (int q = 0; q < kBigWaves; ++q) {
+      W = W + L.wt[q];
+      if (W < rr) {
+        g = q + 1;
+        Wg = W;
+      }
+    }
+    int full = 0, part = 0;
+    if (g >= kBigWaves) {
+      full = n;  // every entry below (idx = n)
+    } else {
+      const int j = lane + 64 * g, ej = EPT * j;
+      const bool live = ej < n;
+      const double oj = L.off[j] + Wg;
+      const double tt = L.last[j];
+      float x0 = s_row[ej];
+      if (a.w) x0 = live ? a.w[ej] * x0 : 0.f;
+      const bool below = live && ej + EPT <= n && oj + tt < rr;
+      full = 64 * EPT * g + EPT * __popcll(__ballot(below));
+      if (live && !below && oj + (double)x0 < rr) {  // may straddle the threshold: walk it
+        float vs[EPT];
+#pragma unroll
+        for (int q = 0; q < EPT; q += 4) {
+          const float4 x = *reinterpret_cast<const float4*>(s_row + ej + q);
+          vs[q] = x.x;
+          vs[q + 1] = x.y;
+          vs[q + 2] = x.z;
+          vs[q + 3] = x.w;
+        }
+        if (a.w) {
+#pragma unroll
+          for (int q = 0; q < EPT; ++q) vs[q] = ej + q < n ? a.w[ej + q] * vs[q] : 0.f;
+        }
+        double run = oj;
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) {
+          run = run + (double)vs[q];
+          if (ej + q < n) part += run < rr;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o);
+    ok = __ballot(!ok) == 0ull;
+    // the deciding neighbours for the check, independent of the potential: the walk's cumulative
+    // values of entries idx - 1 (lane 0) and idx (lane 1), with the regular offsets (in-wave prefix,
+    // then the wave totals in order) and each segment's reads issued before its run
+    const int idx = full + part;
+    double nv = lane == 0 ? -1.0 : 0.0;
+    const int e = idx - 1 + lane;
+    if (lane < 2 && e >= 0 && e < n) {
+      const int j = e / EPT, ej = EPT * j;
+      float vs[EPT];
+#pragma unroll
+      for (int q = 0; q < EPT; q += 4) {
+        const float4 x = *reinterpret_cast<const float4*>(s_row + ej + q);
+        vs[q] = x.x;
+        vs[q + 1] = x.y;
+        vs[q + 2] = x.z;
+        vs[q + 3] = x.w;
+      }
+      if (a.w) {
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) vs[q] = ej + q < n ? a.w[ej + q] * vs[q] : 0.f;
+      }
+      double run = L.off[j];  // ex of segment j until the barrier below
+      for (int q = 0; q < (j >> 6); ++q) run = run + L.wt[q];
+#pragma unroll
+      for (int q = 0; q < EPT; ++q) {
+        run = run + (double)vs[q];
+        if (ej + q == e) nv = run;
+      }
+    }
+    const double hi = __shfl(nv, 1);
+    if (lane == 0) {
+      L.sidx[t2] = ok ? idx : -1;
+      L.lo[t2] = nv;
+      L.hi[t2] = hi;
+    }
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 93);
+  double off = ex;
+  for (int q = 0; q < wave; ++q) off = off + L.wt[q];
+  if (!spec) {  // speculative draws: written only if some uniform takes the regular draws
+    L.off[tid] = off;
+    L.first[tid] = off + (double)v[0];  // the segment's first cumulative value (as the walk's)
+    L.last[tid] = off + tot;            // its last, to within EPT roundings (far inside cum_tol)
+  }
+  unsigned long long redo = ~0ull;  // the uniforms the regular draws take
+  if (spec) {
+    // wave 0: the potential (every lane the same sums), then the check, one lane per uniform — the
+    // speculative count is numpy's index when the exact threshold falls between the same two
+    // cumulative values, neither within 4 cum_tol of it (the fold's check); one barrier
+    if (wave == 0) {
+      float y = 0.f;
+      for (int b = 0; b < nsg; ++b) y = y + L.vb[b];
+      if (m1 < n) {
+        float sx = s_row[m1] * wv(a.w, m1);
+        for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_row[o], wv(a.w, o), sx);
+        y = y + sx;
+      }
+      if (lane == 0) {
+        if (pot_out) *pot_out = y;
+        L.pot = y;
+      }
+      bool good = false;
+      if (lane < T) {
+        const int idx = L.sidx[lane];
+        if (idx >= 0) {
+          const double rr = ut * (double)y;
+          const double tol = cum_tol(a.exact, n, rr);
+          const double lo = L.lo[lane], hi = L.hi[lane];
+          good = tol >= 0.0 && (idx == 0 || (lo < rr && fabs(lo - rr) > 4.0 * tol)) &&
+                 (idx == n || (!(hi < rr) && fabs(hi - rr) > 4.0 * tol));
+          if (good) cand_out[lane] = min(n - 1, idx);
+        }
+      }
+      const unsigned long long r = __ballot(lane < T && !good);
+      if (lane == 0) L.redo = r;
+    }
+    __syncthreads();
+    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 96);
+    redo = L.redo;
+    if (redo == 0ull) {
+      GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 97);
+      GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 94);
+      return;
+    }
+    L.off[tid] = off;
+    L.first[tid] = off + (double)v[0];
+    L.last[tid] = off + tot;
+    __syncthreads();
+  } else {
+    if (tid == 0) {
+      float y;
+      if (c == 0) {
+        y = a.st->pot;
+      } else {
+        y = 0.f;
+        for (int b = 0; b < nsg; ++b) y = y + L.vb[b];
+        if (m1 < n) {
+          float sx = s_row[m1] * wv(a.w, m1);
+          for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_row[o], wv(a.w, o), sx);
+          y = y + sx;
+        }
+        if (pot_out) *pot_out = y;
+      }
+      L.pot = y;
+    }
+    __syncthreads();
+    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 96);
+    if (c + 1 >= a.k) return;
+  }
+  // ---- draws for round c+1 if this trial wins: wave t2 takes uniform t2 over every segment (lane l:
+  // segments l, l + 64, ...): whole segments below are counted by ballot, a segment that straddles
+  // the threshold is walked by its lane — the owner's run, recomputed from LDS in the same order
+  if (wave < T && ((redo >> wave) & 1ull)) {
+    const int t2 = wave;
+    const double pot = (double)L.pot;
+    const double rr = readlane_f64(ut, t2) * pot;  // wave-uniform: a scalar read of lane t2
+    const double tol = cum_tol(a.exact, n, rr);
+    const bool strict = !(tol < 0.0);  // tol < 0 (GDD_KPP_EXACT=0, tests): every segment walks
+    int full = 0, part = 0;
+    bool amb = false;
+    double fj[kBigThr / 64], lj[kBigThr / 64];  // every segment's first and last value, read at once
+#pragma unroll
+    for (int i = 0; i < kBigThr / 64; ++i) {
+      fj[i] = L.first[lane + 64 * i];
+      lj[i] = L.last[lane + 64 * i];
+    }
+#pragma unroll
+    for (int i = 0; i < kBigThr / 64; ++i) {
+      const int j = lane + 64 * i;
+      const int ej = EPT * j;
+      const bool live = ej < n;
+      // a whole segment below, none of it within tol (the run only climbs)
+      const bool below = live && ej + EPT <= n && strict && lj[i] < rr - 2.0 * tol;
+      full += __popcll(__ballot(below));
+      if (live && !below && !(strict && fj[i] > rr + tol)) {  // not wholly above either: walk it
+        const double oj = L.off[j];
+        {
+          float vs[EPT];  // the segment's terms, every read issued before the run
+#pragma unroll
+          for (int q = 0; q < EPT; q += 4) {
+            const float4 x = *reinterpret_cast<const float4*>(s_row + ej + q);
+            vs[q] = x.x;
+            vs[q + 1] = x.y;
+            vs[q + 2] = x.z;
+            vs[q + 3] = x.w;
+          }
+          if (a.w) {
+#pragma unroll
+            for (int q = 0; q < EPT; ++q) vs[q] = ej + q < n ? a.w[ej + q] * vs[q] : 0.f;
+          }
+          double run = oj;
+#pragma unroll
+          for (int q = 0; q < EPT; ++q) {
+            run = run + (double)vs[q];
+            if (ej + q < n) {
+              part += run < rr;
+              amb = amb || fabs(run - rr) <= tol;
+            }
+          }
+        }
+      }
+    }
+    if (part) atomicAdd(&L.part[t2], part);
+    if (amb) L.amb[t2] = 1;
+    if (lane == 0) L.cnt[t2] = EPT * full;
+  }
+  __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 97);
+  if (tid < T && ((redo >> tid) & 1ull)) {
+    int64_t cnt = (int64_t)L.cnt[tid] + L.part[tid];
+    if (L.amb[tid]) cnt = np_cumsum_search(s_row, a.w, n, ut * (double)L.pot);  // lane tid holds u_tid
+    cand_out[tid] = min<int64_t>(n - 1, cnt);
+  }
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 94);
+}
+
+template <int EPT>
+__global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* __restrict__ D, int c) {
+  extern __shared__ __attribute__((aligned(16))) float s_row[];  // kBigThr * EPT + kChainPad floats
+  __shared__ BigLds L;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int T = a.T;
+  const int n = (int)a.n;
+  const int t = blockIdx.x;
+  const int cq = c & 1, pq = (c - 1) & 1;
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 90);
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 1), 95);
-  if (tid < kMaxTrials) {
-    s_part[tid] = 0;
-    s_amb[tid] = 0;
-  }
-  if (tid == 0) s_arr = 0;
+  big_fold_reset(L);
   // ---- trip 1, every load at once (lane q): round c-1's potential q, this slot's candidate if q
   // won, q's own candidate, round c+1's uniform q
   const double ut = (c + 1 < a.k && lane < T) ? a.uniforms[(int64_t)c * T + lane] : 0.0;
@@ -2695,277 +3208,126 @@ __global__ __launch_bounds__(kBigThr) void k_kpp1_big(Kpp1Args a, const float* _
   }
   __syncthreads();
   GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 92);
-  // ---- this thread's segment: products (fp32) and its fp64 run
-  const int e0 = EPT * tid;
-  float v[EPT];
-#pragma unroll
-  for (int q = 0; q < EPT; q += 4) {
-    const float4 x = *reinterpret_cast<const float4*>(s_row + e0 + q);
-    v[q] = x.x;
-    v[q + 1] = x.y;
-    v[q + 2] = x.z;
-    v[q + 3] = x.w;
-  }
-  if (a.w) {
-#pragma unroll
-    for (int q = 0; q < EPT; ++q) v[q] = e0 + q < n ? a.w[e0 + q] * v[q] : 0.f;
-  }
-  double tot = 0.0;
-#pragma unroll
-  for (int q = 0; q < EPT; ++q) tot = tot + (double)v[q];
-  double inc = tot;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const double y = __shfl_up(inc, o);
-    if (lane >= o) inc = inc + y;
-  }
-  double ex = __shfl_up(inc, 1);
-  if (lane == 0) ex = 0.0;
-  if (lane == 63) s_wt[wave] = inc;
-  if (spec) {  // until the barrier below s_off / s_last hold each segment's in-wave prefix and total
-    s_off[tid] = ex;
-    s_last[tid] = tot;
-    waves_arrive(&s_arr);
-  }
-  // the sgemv_t block terms (rounds >= 1)
-  if (c >= 1 && wave < nsg) {
-    const int j0 = wave * kBlk;
-    const float vb = sgemv_block_lds(s_row, a.w, j0, min(kBlk, m1 - j0), t, T);
-    if (lane == 0) s_vb[wave] = vb;
-  } else if (spec && wave - nsg < T) {
-    // searchsorted_left(cum, u * pot_s), pot_s = fp32(fp64 total), without the rounding check (the
-    // check after the potential decides): the wave totals' running sum finds the group of 64
-    // segments (contiguous entries) holding the threshold, one ballot over that group's segment
-    // ends counts the segments below, the segment that straddles it is walked. Offsets are the
-    // group's running sum plus the in-wave prefix — within fp64 roundings of the regular ones: a
-    // count they change has a value within 4 cum_tol of the threshold, which the check refuses.
-    // One group per uniform keeps the LDS reads beside the chains small.
-    const int t2 = wave - nsg;
-    bool ok = waves_wait(&s_arr, kBigWaves);
-    double tall = 0.0;
-    for (int q = 0; q < kBigWaves; ++q) tall = tall + s_wt[q];
-    const double rr = readlane_f64(ut, t2) * (double)(float)tall;
-    int g = 0;
-    double W = 0.0, Wg = 0.0;
-    for (int q = 0; q < kBigWaves; ++q) {
-      W = W + s_wt[q];
-      if (W < rr) {
-        g = q + 1;
-        Wg = W;
-      }
-    }
-    int full = 0, part = 0;
-    if (g >= kBigWaves) {
-      full = n;  // every entry below (idx = n)
-    } else {
-      const int j = lane + 64 * g, ej = EPT * j;
-      const bool live = ej < n;
-      const double oj = s_off[j] + Wg;
-      const double tt = s_last[j];
-      float x0 = s_row[ej];
-      if (a.w) x0 = live ? a.w[ej] * x0 : 0.f;
-      const bool below = live && ej + EPT <= n && oj + tt < rr;
-      full = 64 * EPT * g + EPT * __popcll(__ballot(below));
-      if (live && !below && oj + (double)x0 < rr) {  // may straddle the threshold: walk it
-        float vs[EPT];
-#pragma unroll
-        for (int q = 0; q < EPT; q += 4) {
-          const float4 x = *reinterpret_cast<const float4*>(s_row + ej + q);
-          vs[q] = x.x;
-          vs[q + 1] = x.y;
-          vs[q + 2] = x.z;
-          vs[q + 3] = x.w;
-        }
-        if (a.w) {
-#pragma unroll
-          for (int q = 0; q < EPT; ++q) vs[q] = ej + q < n ? a.w[ej + q] * vs[q] : 0.f;
-        }
-        double run = oj;
-#pragma unroll
-        for (int q = 0; q < EPT; ++q) {
-          run = run + (double)vs[q];
-          if (ej + q < n) part += run < rr;
-        }
-      }
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o);
-    ok = __ballot(!ok) == 0ull;
-    // the deciding neighbours for the check, independent of the potential: the walk's cumulative
-    // values of entries idx - 1 (lane 0) and idx (lane 1), with the regular offsets (in-wave prefix,
-    // then the wave totals in order) and each segment's reads issued before its run
-    const int idx = full + part;
-    double nv = lane == 0 ? -1.0 : 0.0;
-    const int e = idx - 1 + lane;
-    if (lane < 2 && e >= 0 && e < n) {
-      const int j = e / EPT, ej = EPT * j;
-      float vs[EPT];
-#pragma unroll
-      for (int q = 0; q < EPT; q += 4) {
-        const float4 x = *reinterpret_cast<const float4*>(s_row + ej + q);
-        vs[q] = x.x;
-        vs[q + 1] = x.y;
-        vs[q + 2] = x.z;
-        vs[q + 3] = x.w;
-      }
-      if (a.w) {
-#pragma unroll
-        for (int q = 0; q < EPT; ++q) vs[q] = ej + q < n ? a.w[ej + q] * vs[q] : 0.f;
-      }
-      double run = s_off[j];  // ex of segment j until the barrier below
-      for (int q = 0; q < (j >> 6); ++q) run = run + s_wt[q];
-#pragma unroll
-      for (int q = 0; q < EPT; ++q) {
-        run = run + (double)vs[q];
-        if (ej + q == e) nv = run;
-      }
-    }
-    const double hi = __shfl(nv, 1);
-    if (lane == 0) {
-      s_sidx[t2] = ok ? idx : -1;
-      s_lo[t2] = nv;
-      s_hi[t2] = hi;
-    }
-  }
-  __syncthreads();
-  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 93);
-  double off = ex;
-  for (int q = 0; q < wave; ++q) off = off + s_wt[q];
-  if (!spec) {  // speculative draws: written only if some uniform takes the regular draws
-    s_off[tid] = off;
-    s_first[tid] = off + (double)v[0];  // the segment's first cumulative value (as the walk's)
-    s_last[tid] = off + tot;            // its last, to within EPT roundings (far inside cum_tol)
-  }
-  unsigned long long redo = ~0ull;  // the uniforms the regular draws take
-  if (spec) {
-    // wave 0: the potential (every lane the same sums), then the check, one lane per uniform — the
-    // speculative count is numpy's index when the exact threshold falls between the same two
-    // cumulative values, neither within 4 cum_tol of it (the fold's check); one barrier
-    if (wave == 0) {
-      float y = 0.f;
-      for (int b = 0; b < nsg; ++b) y = y + s_vb[b];
-      if (m1 < n) {
-        float sx = s_row[m1] * wv(a.w, m1);
-        for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_row[o], wv(a.w, o), sx);
-        y = y + sx;
-      }
-      if (lane == 0) {
-        a.potv[cq][t] = y;
-        s_pot = y;
-      }
-      bool good = false;
-      if (lane < T) {
-        const int idx = s_sidx[lane];
-        if (idx >= 0) {
-          const double rr = ut * (double)y;
-          const double tol = cum_tol(a.exact, n, rr);
-          const double lo = s_lo[lane], hi = s_hi[lane];
-          good = tol >= 0.0 && (idx == 0 || (lo < rr && fabs(lo - rr) > 4.0 * tol)) &&
-                 (idx == n || (!(hi < rr) && fabs(hi - rr) > 4.0 * tol));
-          if (good) a.candw[cq][(int64_t)t * T + lane] = min(n - 1, idx);
-        }
-      }
-      const unsigned long long r = __ballot(lane < T && !good);
-      if (lane == 0) s_redo = r;
-    }
-    __syncthreads();
-    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 96);
-    redo = s_redo;
-    if (redo == 0ull) {
-      GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 97);
-      GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 94);
-      return;
-    }
-    s_off[tid] = off;
-    s_first[tid] = off + (double)v[0];
-    s_last[tid] = off + tot;
-    __syncthreads();
+  big_fold<EPT>(a, c, t, ut, s_row, L, c >= 1 ? a.potv[cq] + t : nullptr, a.candw[cq] + (int64_t)t * T);
+}
+
+// ---- two rounds per launch over the table (4096 < n <= kBig1Max, T <= kPairMaxT; r06): k_kpp1_dm2's
+// pairing with k_kpp1_big's 1024-thread fold. Workgroup w * T + t2 forms round c's trial w (the
+// candidate's row against the winner's, as a round-c workgroup w would: same operands, same bits),
+// folds it, takes the candidate round c+1's slot t2 draws if w wins, forms that row and folds it
+// (candidates for round c+2). Workgroup w * T publishes round c's trial w. The next launch resolves
+// both winners (k_kpp1_dm2's trip 1). A trailing odd round runs alone (pair == 0, T workgroups).
+template <int EPT>
+__global__ __launch_bounds__(kBigThr) void k_kpp1_big2(Kpp1Args a, const float* __restrict__ D, int c,
+                                                        int lq, int pair) {
+  extern __shared__ __attribute__((aligned(16))) float s_row[];  // kBigThr * EPT + kChainPad floats
+  __shared__ BigLds L;
+  __shared__ int64_t s_cand[kMaxTrials];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int T = a.T, pl = lq ^ 1, TT = T * T;
+  const int n = (int)a.n;
+  const int g = blockIdx.x;
+  const int w = pair ? g / T : g;       // round c's trial this workgroup forms first
+  const int t2 = pair ? g - w * T : 0;  // round c+1's trial (pair launches)
+  big_fold_reset(L);
+  // trip 1: the previous launch's potentials and this slot's candidates (as k_kpp1_dm2)
+  const float* wrow;
+  int64_t ct;
+  if (c == 1) {
+    wrow = a.closest0;
+    ct = a.candw[0][w];  // round 0 (k_kpp1_big, one workgroup): the first centre's candidates
   } else {
-    if (tid == 0) {
-      float y;
-      if (c == 0) {
-        y = a.st->pot;
-      } else {
-        y = 0.f;
-        for (int b = 0; b < nsg; ++b) y = y + s_vb[b];
-        if (m1 < n) {
-          float sx = s_row[m1] * wv(a.w, m1);
-          for (int o = m1 + 1; o < n; ++o) sx = __builtin_fmaf(s_row[o], wv(a.w, o), sx);
-          y = y + sx;
-        }
-        a.potv[cq][t] = y;
+    float pv[kPairMaxT];
+#pragma unroll
+    for (int q = 0; q < kPairMaxT; ++q) pv[q] = a.potv[pl][min(q, T - 1)];
+    const float p2 = a.potv2[pl][min(lane, TT - 1)];
+    const int64_t c2 = a.candw2[pl][(int64_t)min(lane, TT - 1) * T + w];
+    const int64_t cs1 = a.candself[pl][min(lane, T - 1)];
+    const int64_t cs2 = a.candself2[pl][min(lane, TT - 1)];
+    int bw = 0;  // np.argmin: first minimum, a NaN wins at once
+    float best = pv[0];
+#pragma unroll
+    for (int q = 1; q < kPairMaxT; ++q) {
+      const float pt = pv[q];
+      if (q < T && best == best && (pt < best || pt != pt)) {
+        bw = q;
+        best = pt;
       }
-      s_pot = y;
     }
-    __syncthreads();
-    GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 96);
-    if (c + 1 >= a.k) return;
+    int bv = 0;
+    float best2 = __shfl(p2, bw * T);
+    for (int q = 1; q < T; ++q) {
+      const float pt = __shfl(p2, bw * T + q);
+      if (best2 == best2 && (pt < best2 || pt != pt)) {
+        bv = q;
+        best2 = pt;
+      }
+    }
+    const int j = bw * T + bv;
+    ct = __shfl(c2, j);
+    wrow = a.dist2[pl] + (int64_t)j * n;
+    const int64_t i1 = __shfl(cs1, bw), i2 = __shfl(cs2, j);
+    if (g == 0 && tid == 0) {  // rows gathered after the rounds
+      a.indices[c - 2] = i1;
+      a.indices[c - 1] = i2;
+    }
   }
-  // ---- draws for round c+1 if this trial wins: wave t2 takes uniform t2 over every segment (lane l:
-  // segments l, l + 64, ...): whole segments below are counted by ballot, a segment that straddles
-  // the threshold is walked by its lane — the owner's run, recomputed from LDS in the same order
-  if (wave < T && ((redo >> wave) & 1ull)) {
-    const int t2 = wave;
-    const double pot = (double)s_pot;
-    const double rr = readlane_f64(ut, t2) * pot;  // wave-uniform: a scalar read of lane t2
-    const double tol = cum_tol(a.exact, n, rr);
-    const bool strict = !(tol < 0.0);  // tol < 0 (GDD_KPP_EXACT=0, tests): every segment walks
-    int full = 0, part = 0;
-    bool amb = false;
-    double fj[kBigThr / 64], lj[kBigThr / 64];  // every segment's first and last value, read at once
+  const double ut = (c + 1 < a.k && lane < T) ? a.uniforms[(int64_t)c * T + lane] : 0.0;
+  if (tid == 0 && t2 == 0) a.candself[lq][w] = ct;
+  // trip 2: the closest distances and the candidate's table row
+  {
+    constexpr int QC = EPT < 16 ? EPT : 16;
 #pragma unroll
-    for (int i = 0; i < kBigThr / 64; ++i) {
-      fj[i] = s_first[lane + 64 * i];
-      lj[i] = s_last[lane + 64 * i];
-    }
+    for (int q0 = 0; q0 < EPT; q0 += QC) {
+      float wi[QC], dd[QC];
 #pragma unroll
-    for (int i = 0; i < kBigThr / 64; ++i) {
-      const int j = lane + 64 * i;
-      const int ej = EPT * j;
-      const bool live = ej < n;
-      // a whole segment below, none of it within tol (the run only climbs)
-      const bool below = live && ej + EPT <= n && strict && lj[i] < rr - 2.0 * tol;
-      full += __popcll(__ballot(below));
-      if (live && !below && !(strict && fj[i] > rr + tol)) {  // not wholly above either: walk it
-        const double oj = s_off[j];
-        {
-          float vs[EPT];  // the segment's terms, every read issued before the run
+      for (int q = 0; q < QC; ++q) {
+        const int e = min(tid + kBigThr * (q0 + q), n - 1);
+        wi[q] = wrow[e];
+        dd[q] = D[ct * n + e];
+      }
 #pragma unroll
-          for (int q = 0; q < EPT; q += 4) {
-            const float4 x = *reinterpret_cast<const float4*>(s_row + ej + q);
-            vs[q] = x.x;
-            vs[q + 1] = x.y;
-            vs[q + 2] = x.z;
-            vs[q + 3] = x.w;
-          }
-          if (a.w) {
-#pragma unroll
-            for (int q = 0; q < EPT; ++q) vs[q] = ej + q < n ? a.w[ej + q] * vs[q] : 0.f;
-          }
-          double run = oj;
-#pragma unroll
-          for (int q = 0; q < EPT; ++q) {
-            run = run + (double)vs[q];
-            if (ej + q < n) {
-              part += run < rr;
-              amb = amb || fabs(run - rr) <= tol;
-            }
-          }
-        }
+      for (int q = 0; q < QC; ++q) {
+        const int e = tid + kBigThr * (q0 + q);
+        s_row[e] = e < n ? np_minimum(wi[q], dd[q]) : 0.f;
       }
     }
-    if (part) atomicAdd(&s_part[t2], part);
-    if (amb) s_amb[t2] = 1;
-    if (lane == 0) s_cnt[0][t2] = EPT * full;
   }
   __syncthreads();
-  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 97);
-  if (tid < T && ((redo >> tid) & 1ull)) {
-    int64_t cnt = (int64_t)s_cnt[0][tid] + s_part[tid];
-    if (s_amb[tid]) cnt = np_cumsum_search(s_row, a.w, n, ut * (double)s_pot);  // lane tid holds u_tid
-    a.candw[cq][(int64_t)t * T + tid] = min<int64_t>(n - 1, cnt);
+  if (!pair) {  // the last round alone
+    big_fold<EPT>(a, c, w, ut, s_row, L, a.potv[lq] + w, a.candw[lq] + (int64_t)w * T);
+    return;
   }
-  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && t == 0 && c == a.k - 2), 94);
+  big_fold<EPT>(a, c, w, ut, s_row, L, t2 == 0 ? a.potv[lq] + w : nullptr, s_cand);
+  __syncthreads();
+  // trip 3: round c+1's candidate for slot t2 if w wins, its table row, and round c+2's uniforms
+  // (requested here, not held in registers across the first fold)
+  const int64_t c1 = s_cand[t2];
+  const int j = w * T + t2;
+  const double ut2 = (c + 2 < a.k && lane < T) ? a.uniforms[(int64_t)(c + 1) * T + lane] : 0.0;
+  if (tid == 0) a.candself2[lq][j] = c1;
+  big_fold_reset(L);
+  {
+    constexpr int QC = EPT < 16 ? EPT : 16;
+    float* orow = a.dist2[lq] + (int64_t)j * n;
+#pragma unroll
+    for (int q0 = 0; q0 < EPT; q0 += QC) {
+      float dd[QC];
+#pragma unroll
+      for (int q = 0; q < QC; ++q) dd[q] = D[c1 * n + min(tid + kBigThr * (q0 + q), n - 1)];
+#pragma unroll
+      for (int q = 0; q < QC; ++q) {
+        const int e = tid + kBigThr * (q0 + q);
+        if (e < n) {  // the entry this thread stored in trip 2
+          const float f = np_minimum(s_row[e], dd[q]);
+          orow[e] = f;
+          s_row[e] = f;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  big_fold<EPT>(a, c + 1, t2, ut2, s_row, L, a.potv2[lq] + j, a.candw2[lq] + (int64_t)j * T);
 }
 
 // centres from their indices (fused rounds record only the index of each round's winner)
@@ -3102,6 +3464,11 @@ bool kpp_big_table(int64_t n, int dim, int T, int k) {
 bool kpp_small_table(int64_t n, int dim, int T, int k) {
   return n <= kBlk && dim <= kDmX && T >= 2 && k >= kDmMinK;
 }
+// the 1024-thread table rounds two per launch (k_kpp1_big2; T <= kPairMaxT, the 8-entry segments,
+// n <= 8192: at 16 and 32 entries two folds in one kernel spill): workspace for the pairs
+bool kpp_big_pairs(int64_t n, int dim, int T, int k) {
+  return T <= kPairMaxT && n <= (int64_t)kBigThr * 8 && kpp_big_table(n, dim, T, k);
+}
 
 size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k) {
   const size_t T = (size_t)std::max(n_trials, 1);
@@ -3126,11 +3493,10 @@ size_t kpp_ws_bytes(int64_t n, int dim, int n_trials, int k) {
     b += align256(sizeof(float) * n * (size_t)std::max(dim, 1));  // XT
   if (kpp_big_table(n, dim, (int)T, k))
     b += align256(sizeof(float) * n * n) + 2 * align256(sizeof(double) * n * T);  // table, block prefixes
-  if (kpp_small_table(n, dim, (int)T, k)) {
-    b += align256(sizeof(float) * n * n);  // distance table
+  if (kpp_small_table(n, dim, (int)T, k)) b += align256(sizeof(float) * n * n);  // distance table
+  if (kpp_small_table(n, dim, (int)T, k) || kpp_big_pairs(n, dim, (int)T, k))
     b += 2 * (align256(sizeof(float) * T * T * n) + align256(sizeof(float) * T * T) +
               align256(sizeof(int64_t) * T * T * T) + align256(sizeof(int64_t) * T * T));  // pair rounds
-  }
   return b + 1024;
 }
 
@@ -3176,7 +3542,8 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
   const bool big1 = n <= kpp_big1_max() && T >= 2 && !forced("kpp_no_big1");
   for (int q = 0; q < 2; ++q) a.pfx[q] = (Dbig && !big1) ? cv.take<double>((size_t)n * T) : nullptr;
   float* Dm = kpp_small_table(n, dim, T, k) ? cv.take<float>((size_t)n * n) : nullptr;
-  if (Dm) {
+  const bool pairs_big = Dbig && big1 && kpp_big_pairs(n, dim, T, k);
+  if (Dm || pairs_big) {
     for (int q = 0; q < 2; ++q) {
       b1.dist2[q] = cv.take<float>((size_t)T * T * n);
       b1.potv2[q] = cv.take<float>((size_t)T * T);
@@ -3270,13 +3637,15 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
         // two rounds per launch (a trailing odd round alone). The chain's arguments are fixed by
         // (b1, Dm, k): it is replayed as one recorded graph (replay_or_run) — every launch then
         // starts ~1 us sooner after the previous one
+        // the pair's two folds overlapped (kpp1_fold_pair); GDD_FORCE=kpp_pair_serial: one after the other
+        const int overlap = forced("kpp_pair_serial") ? 0 : 1;
         auto chain = [&](hipStream_t cs) -> int {
           int lq = 1, pair = 0;
           for (int c = 1; c < k; c += 2) {
             lq = ((c - 1) / 2 + 1) & 1;
             pair = c + 1 < k ? 1 : 0;
             const unsigned grid = (unsigned)(pair ? T * T : T);
-            k_kpp1_dm2<<<grid, 256, 0, cs>>>(b1, Dm, c, lq, pair);
+            k_kpp1_dm2<<<grid, 256, 0, cs>>>(b1, Dm, c, lq, pair, overlap);
             GDD_LAUNCHED();
           }
           k_kpp1_final2<<<1, 64, 0, cs>>>(b1, k - 1, lq, pair);
@@ -3291,12 +3660,13 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
         struct {
           Kpp1Args b1;
           const float* Dm;
-          int k;
+          int k, overlap;
         } key;
         std::memset(&key, 0, sizeof(key));
         key.b1 = b1;
         key.Dm = Dm;
         key.k = k;
+        key.overlap = overlap;
         return replay_or_run("kpp_pair_chain", &key, sizeof(key), s, chain);
       }
       for (int c = 1; c < k; ++c) {
@@ -3414,6 +3784,25 @@ extern "C" int gdd_kmeans_plusplus(int64_t n, int dim, const float* X, const flo
       GDD_HIP(hipFuncSetAttribute((const void*)big, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_big));
       big<<<1, kBigThr, lds_big, s>>>(b1, Dbig, 0);  // round 1's candidates from the first centre
       GDD_LAUNCHED();
+      if (pairs_big && !forced("kpp_single_round")) {  // two rounds per launch (r06)
+        void (*big2)(Kpp1Args, const float*, int, int, int) = k_kpp1_big2<8>;  // n <= 8192: ept == 8
+        GDD_HIP(hipFuncSetAttribute((const void*)big2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_big));
+        int lq = 1, pair = 0;
+        for (int c = 1; c < k; c += 2) {
+          lq = ((c - 1) / 2 + 1) & 1;
+          pair = c + 1 < k ? 1 : 0;
+          big2<<<(unsigned)(pair ? T * T : T), kBigThr, lds_big, s>>>(b1, Dbig, c, lq, pair);
+          GDD_LAUNCHED();
+        }
+        k_kpp1_final2<<<1, 64, 0, s>>>(b1, k - 1, lq, pair);
+        GDD_LAUNCHED();
+        if (k > 2) {
+          k_kpp_gather_centres<<<(unsigned)(((int64_t)k * dim + 255) / 256), 256, 0, s>>>(k, dim, X, indices,
+                                                                                           centers);
+          GDD_LAUNCHED();
+        }
+        return GDD_OK;
+      }
       for (int c = 1; c < k; ++c) {
         big<<<(unsigned)T, kBigThr, lds_big, s>>>(b1, Dbig, c);
         GDD_LAUNCHED();

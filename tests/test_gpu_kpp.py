@@ -124,12 +124,13 @@ def test_kmeans_plusplus_two_launch_path(monkeypatch):
                                      (3706, 64, 371), (2000, 49, 101)])  # the 64-slot table
 def test_kmeans_plusplus_round_forms(monkeypatch, n, dim, k):
     """Every single-block round form gives the oracle's seeding, bit for bit: two rounds per launch
-    over the distance table (default for plain-chain plans, dim <= 64, k >= 16, T <= 8), one round
+    over the distance table (default for plain-chain plans, dim <= 64, k >= 16, T <= 8; the two
+    folds overlapped, or one after the other with GDD_FORCE=kpp_pair_serial), one round
     per launch over the table (the default for T > 8; GDD_FORCE=kpp_single_round), and the fused
     distance + fold rounds (the default for k < 16; GDD_FORCE=kpp_no_table)."""
     X = np.ascontiguousarray(synth.blobs(n, dim, max(2, k // 4), seed=n + dim + 1), np.float32)
     c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
-    for toks in ((), ("kpp_single_round",), ("kpp_no_table",)):
+    for toks in ((), ("kpp_pair_serial",), ("kpp_single_round",), ("kpp_no_table",)):
         force(monkeypatch, *toks)
         ops = _Ops("cuda", n, k, dim)
         c, idx = ops.kmeans_plusplus(torch.from_numpy(X).cuda(), k, np.random.RandomState(15))
@@ -179,10 +180,12 @@ def _kpp_dev(X, k, T, first, u, w=None):
 # (n, forced paths): every search form — the pick count (round 0 of the single-block paths and the
 # two-launch rounds), the fold's two-ballot search in the table pair / single rounds and the fused
 # rounds, the multi-block round (per-(block, trial) and the split pick launch), k_kpp1_big's
-# speculative draws and their regular fallback
+# speculative draws and their regular fallback, in one round per launch and two (k_kpp1_big2, n <= 8192)
 CUMSUM_FORMS = [
     (1000, ()), (4096, ()), (1000, ("kpp_single_round",)), (1000, ("kpp_no_table",)),
-    (1000, ("kpp_no_table", "kpp_two_launch")), (4096, ("kpp_single_round",)), (9000, ()),
+    (1000, ("kpp_no_table", "kpp_two_launch")), (4096, ("kpp_single_round",)),
+    (1000, ("kpp_pair_serial",)), (6000, ()),
+    (6000, ("kpp_single_round",)), (9000, ()),
     (9000, ("kpp_no_big1",)), (20000, ()), (20000, ("kpp_big1_max=32768",)), (530000, ()),
     (530000, ("kpp_no_split",)),
 ]
@@ -250,10 +253,11 @@ def test_kpp_replay_every_draw(monkeypatch, n, dim, k):
     (17730, 64, 1773, False),  # Ali-Display users' shape and k: T = 9
     (32768, 16, 40, False)])
 def test_kmeans_plusplus_big_rounds(monkeypatch, n, dim, k, oracle):
-    """k_kpp1_big (the default for table plans with 4096 < n <= 16384) gives the seeding of the
-    per-(block, trial) table rounds (the default above 16,384; GDD_FORCE=kpp_no_big1) and, where the
-    oracle is run, the oracle's — bit for bit, over the 8-, 16- and 32-entry segment forms, odd n
-    (the sgemv_t tail) and T = 9."""
+    """k_kpp1_big (the default for table plans with 4096 < n <= 16384; two rounds per launch,
+    k_kpp1_big2, up to n = 8192 with T <= 8) gives the seeding of the per-(block, trial) table rounds
+    (the default above 16,384; GDD_FORCE=kpp_no_big1), of one round per launch (kpp_single_round)
+    and, where the oracle is run, the oracle's — bit for bit, over the 8-, 16- and 32-entry segment
+    forms, odd n (the sgemv_t tail), even and odd k (a trailing round alone) and T = 9."""
     X = synth.blobs(n, dim, max(2, k // 4), seed=n + dim + 3)
     X = np.ascontiguousarray(X - X.mean(axis=0), np.float32)
     # the 32-entry segments too (default limit 16,384); small k: the table although it does not pay
@@ -265,6 +269,11 @@ def test_kmeans_plusplus_big_rounds(monkeypatch, n, dim, k, oracle):
     c2, idx2 = ops.kmeans_plusplus(Xd, k, np.random.RandomState(42))
     assert np.array_equal(idx.cpu().numpy(), idx2.cpu().numpy())
     assert np.array_equal(bits(c.cpu().numpy()), bits(c2.cpu().numpy()))
+    # one round per launch against two (k_kpp1_big2: n <= 8192, T <= 8 — the default there)
+    force(monkeypatch, "kpp_big1_max=32768", "kpp_force_table", "kpp_single_round")
+    c3, idx3 = ops.kmeans_plusplus(Xd, k, np.random.RandomState(42))
+    assert np.array_equal(idx.cpu().numpy(), idx3.cpu().numpy())
+    assert np.array_equal(bits(c.cpu().numpy()), bits(c3.cpu().numpy()))
     if oracle:
         c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(42))
         assert np.array_equal(idx.cpu().numpy(), idx_ref)

@@ -1,9 +1,9 @@
 """The redo paths behind the bounded LDS-counter spins, pinned bit-for-bit.
 
-Three kernels hand work between waves of one workgroup through LDS arrival counters with a bounded
+Four kernels hand work between waves of one workgroup through LDS arrival counters with a bounded
 spin, and redo the work behind a barrier when a spin gives up: k_mb_reassign's parallel row copies
-(the s_bad redo), k_kpp_round's speculative prefixes (s_pfxfail) and k_kpp1_big's speculative
-draws (the sequential fallback). On the fast path a give-up never happens, so the parity tests never
+(the s_bad redo), k_kpp_round's speculative prefixes (s_pfxfail), k_kpp1_big's speculative
+draws (the sequential fallback) and k_kpp1_dm2's overlapped folds (s_fail: the serial pair). On the fast path a give-up never happens, so the parity tests never
 reach the redo code. ``make SPIN0=1`` builds ``libgdd_spin0.so`` with a spin bound of 0: every wait
 gives up at once and every redo runs. This test re-runs the MiniBatchKMeans and k-means++ parity
 tests once in a child process on that library (GDD_LIB_PATH), against the same oracle.

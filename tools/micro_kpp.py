@@ -54,7 +54,8 @@ def ab(n=3000, dim=40, k=454):
     """Same-process A/B of the round forms (devices differ by up to ~10% in clock) through
     GDD_FORCE, and of the cumulative-potential rounding check (GDD_KPP_EXACT: 0 off, 1 default, 2
     replay every draw)."""
-    for var, val in (("", ""), ("GDD_FORCE", "kpp_single_round"), ("GDD_FORCE", "kpp_no_table"),
+    for var, val in (("", ""), ("GDD_FORCE", "kpp_pair_serial"), ("GDD_FORCE", "kpp_single_round"),
+                     ("GDD_FORCE", "kpp_no_table"), ("", ""), ("GDD_FORCE", "kpp_pair_serial"),
                      ("GDD_KPP_EXACT", "0"), ("", ""), ("GDD_KPP_EXACT", "2")):
         if var:
             os.environ[var] = val
@@ -65,10 +66,13 @@ def ab(n=3000, dim=40, k=454):
 
 
 def ab_big():
-    """One 1024-thread workgroup per trial (k_kpp1_big, default for 4096 < n <= 16384 table plans)
-    against the per-(block, trial) table rounds (GDD_FORCE=kpp_no_big1), same process."""
-    for (n, dim, k) in [(6040, 64, 604), (9001, 24, 200), (17730, 64, 1773)]:
-        for var in ("", "kpp_no_big1", "", "kpp_no_big1"):
+    """One 1024-thread workgroup per trial (k_kpp1_big, default for 4096 < n <= 16384 table plans;
+    two rounds per launch, k_kpp1_big2, up to n = 8192 with T <= 8) against one round per launch
+    (GDD_FORCE=kpp_single_round) and the per-(block, trial) table rounds (kpp_no_big1), same process;
+    the ML-1M users' shape parity-checked first."""
+    run(6040, 64, 604, 1)
+    for (n, dim, k) in [(6040, 64, 604), (8000, 64, 400), (9001, 24, 200), (17730, 64, 1773)]:
+        for var in ("", "kpp_single_round", "kpp_no_big1", "", "kpp_single_round"):
             if var:
                 os.environ["GDD_FORCE"] = var
             print(f"variant {var or 'default'}:", end=" ", flush=True)
@@ -93,5 +97,6 @@ if __name__ == "__main__":
         ab_big()
         sys.exit(0)
     ab()
-    for (n, dim, k) in [(3000, 40, 454), (2708, 7, 70), (6040, 64, 604), (3000, 41, 769), (17730, 64, 1773)]:
+    for (n, dim, k) in [(3000, 40, 454), (2708, 7, 70), (3706, 64, 371), (6040, 64, 604), (3000, 41, 769),
+                        (17730, 64, 1773)]:
         run(n, dim, k, 3, check=n * k < 3e7)
