@@ -38,3 +38,19 @@ def test_choice_unit_weights_edges():
     for k in (1, 17, 3020, 6039):
         for u in (np.nextafter(k / n, 0), k / n, np.nextafter(k / n, 1)):
             assert choice_unit_weights(Fixed(float(u)), n) == int(np.searchsorted(cdf, u, side="right"))
+
+
+@pytest.mark.parametrize("seed", [0, 15, 42])
+@pytest.mark.parametrize("k,T", [(2, 2), (454, 8), (604, 8), (1773, 9)])
+def test_kpp_uniforms_in_one_draw(seed, k, T):
+    """_kmeans_plusplus draws random_state.uniform(size=n_local_trials) once per round
+    (sklearn/cluster/_kmeans.py:247); _Ops.kmeans_plusplus draws all (k - 1) * T at once. The legacy
+    RandomState stream gives the same doubles, and leaves the generator in the same state."""
+    a, b = np.random.RandomState(seed), np.random.RandomState(seed)
+    a.random_sample()
+    b.random_sample()  # the first centre's draw
+    u_rounds = np.concatenate([a.uniform(size=T) for _ in range(k - 1)])
+    u_once = b.uniform(size=(k - 1) * T)
+    assert np.array_equal(u_rounds.view(np.int64), u_once.view(np.int64))
+    sa, sb = a.get_state(), b.get_state()
+    assert np.array_equal(sa[1], sb[1]) and sa[2:] == sb[2:]

@@ -22,7 +22,7 @@ def run(n, dim, k, reps, check=True):
     rs = np.random.RandomState(15)
     w = np.ones(n, np.float32)
     first = int(rs.choice(n, p=w / w.sum()))
-    U = np.concatenate([rs.uniform(size=T) for _ in range(k - 1)])
+    U = rs.uniform(size=(k - 1) * T)
     Xd = torch.from_numpy(X).cuda()
     Ud = torch.from_numpy(U).cuda()
     C = torch.empty(k, dim, dtype=torch.float32, device="cuda")
