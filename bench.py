@@ -312,7 +312,7 @@ def main():
         dist.destroy_process_group()
 
 
-def recsys_record(dev, with_cpu, reps=5, group=None, world=1):
+def recsys_record(dev, with_cpu, reps=10, group=None, world=1):
     """Config 4's clustering stage on the bipartite recsys graph (north_star's second target):
     distill_recsys.kmeans_cluster (distill_recsys.py:158-181) as main() calls it (:565-583) — users
     then items, StandardScaler + KMeans(n_clusters=k, random_state=42, n_init="auto") — on
