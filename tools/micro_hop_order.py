@@ -18,6 +18,8 @@ from gdd import synth  # noqa: E402
 
 SCHEDULES = {"default": "", "noprobe": "hop_no_probe", "roworder": "hop_row_order",
              "contig": "hop_row_order,hop_xcd_contig"}
+if os.environ.get("HOP_AB"):  # HOP_AB=<GDD_FORCE token>: the default against that token alone
+    SCHEDULES = {"default": "", os.environ["HOP_AB"]: os.environ["HOP_AB"]}
 
 
 def timed(gn, X, T, alpha, reps):
@@ -36,6 +38,8 @@ def main():
     graphs = []
     cfg = synth.CONFIGS["arxiv"]
     graphs.append(("arxiv chung-lu", gdd.to_csr(synth.chung_lu(cfg.n, cfg.avg_degree, cfg.seed)), cfg, 20))
+    if os.environ.get("HOP_AB"):
+        graphs = graphs * 2
     rc = synth.CONFIGS["reddit"]
     graphs.append(("reddit-train chung-lu", synth.chung_lu_device(153932, rc.avg_degree, rc.seed), rc, 10))
     pc = synth.CONFIGS["products"]
