@@ -1344,12 +1344,15 @@ __global__ __launch_bounds__(kThr) void k_kpp_dists(KppArgs a, int c) {
   const int pq = (c - 1) & 1, cq = c & 1;
   const int64_t n = a.n, j0 = (int64_t)blk * kBlk;
   const float* wrow = c == 1 ? a.closest0 : a.dist[pq] + (int64_t)a.winq[cq] * n;
+  // stamps (diagnostic build, tools/stamps.py kpp-dists): round 5, block 0 and the last block
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && c == 5 && (blk == 0 || blk == a.nblk - 1)), blk == 0 ? 30 : 40);
   for (int e = tid; e < T * dim; e += kThr) {
     const int t = e / dim, j = e - t * dim;
     s_cs[e] = (double)a.X[a.cand[cq][t] * dim + j];
   }
   if (tid < T) s_cn[tid] = a.xsq[a.cand[cq][tid]];
   __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && c == 5 && (blk == 0 || blk == a.nblk - 1)), blk == 0 ? 31 : 41);
   float* s_d = reinterpret_cast<float*>(s_cs + T * dim);
   // feature f of point j0 + off[q] is xt[f * n + off[q]]: a wave-uniform row base plus a 32-bit
   // lane offset, so each load takes one scalar base and no 64-bit vector address
@@ -1419,6 +1422,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_dists(KppArgs a, int c) {
         for (int q = 0; q < kPer; ++q) dot[t][q] = __builtin_fma(cv, (double)u[q], dot[t][q]);
       }
   }
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && c == 5 && (blk == 0 || blk == a.nblk - 1)), blk == 0 ? 32 : 42);
   float wv_[kPer];
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
@@ -1444,6 +1448,7 @@ __global__ __launch_bounds__(kThr) void k_kpp_dists(KppArgs a, int c) {
     }
   }
   __syncthreads();
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && c == 5 && (blk == 0 || blk == a.nblk - 1)), blk == 0 ? 33 : 43);
   // the block's cumulative-potential total per trial: block_prefix's operations for every trial with
   // one barrier (r05; the per-trial calls paid two barriers each), the total kept by the thread that
   // owns the block's last entry
@@ -1494,11 +1499,17 @@ __global__ __launch_bounds__(kThr) void k_kpp_dists(KppArgs a, int c) {
       }
     }
   }
+  GDD_STAMP_WHEN(g_stamps_kpp, (tid == 0 && c == 5 && (blk == 0 || blk == a.nblk - 1)), blk == 0 ? 34 : 44);
   const int64_t NB = min<int64_t>(kBlk, a.m1 - j0);
   if (NB > 0 && wave < T) {  // wave t: trial t's sgemv_t block term
     const float v = sgemv_block_wave(s_d + wave * kBlk, a.w ? a.w + j0 : nullptr, NB, wave, T);
     if (lane == 0) a.vblk[cq][(int64_t)wave * a.nblk + blk] = v;
   }
+  GDD_STAMP_WHEN(g_stamps_kpp, (lane == 0 && wave == 0 && c == 5 && (blk == 0 || blk == a.nblk - 1)),
+                 blk == 0 ? 35 : 45);
+#ifdef GDD_STAMPS
+  if (lane == 0 && c == 5) atomicMax(&g_stamps_kpp[46], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 // after the last round: its potentials, winner and centre

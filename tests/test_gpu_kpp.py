@@ -365,3 +365,22 @@ def test_kmeans_plusplus_hard_data_multi_block(monkeypatch, case, n, dim, k, tok
         c_ref, idx_ref = O.kmeans_plusplus(X, k, np.random.RandomState(15))
         assert np.array_equal(idx.cpu().numpy(), idx_ref)
         assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref))
+
+
+@pytest.mark.parametrize("n,dim,k,weighted", [(524289, 5, 12, False), (600001, 33, 20, True),
+                                              (530000, 47, 9, False)])
+def test_kmeans_plusplus_split_rounds_match_block_rounds(monkeypatch, n, dim, k, weighted):
+    """The split rounds (k_kpp_dists: every trial's distances per 4096-point block, the feature rows
+    by LDS-DMA through a ring, r06) against the per-(block, trial) rounds (GDD_FORCE=kpp_no_split),
+    bit for bit: odd n (the last block's short tail and the XT row padding), dims below and above the
+    ring depth, sample weights."""
+    rng = np.random.default_rng(n + dim)
+    X = np.ascontiguousarray(rng.standard_normal((n, dim)), np.float32)
+    w = rng.uniform(0.5, 2.0, n).astype(np.float32) if weighted else None
+    T = 2 + int(np.log(k))
+    u = np.random.RandomState(n).uniform(size=(k - 1) * T)
+    c, idx = _kpp_dev(X, k, T, 7, u, w=w)
+    force(monkeypatch, "kpp_no_split")
+    c2, idx2 = _kpp_dev(X, k, T, 7, u, w=w)
+    assert np.array_equal(idx, idx2)
+    assert np.array_equal(bits(c), bits(c2))

@@ -3,7 +3,7 @@
 64 chains done, 65 point tile ready, 66 keys out; 70-74 the same for an update alone) of the MiniBatchKMeans step and k-means++ kernels (diagnostic build).
 
 Build: make -C graph-distillation-for-recommendation_amd/csrc STAMPS=1
-Run:   python tools/stamps.py   (uses lib/libgdd_stamps.so; stamps are s_memrealtime, 10 ns ticks)
+Run:   python tools/stamps.py [kpp-big | kpp-dists]   (uses lib/libgdd_stamps.so; s_memrealtime, 10 ns ticks)
 """
 import ctypes
 import os
@@ -52,9 +52,31 @@ def kpp_big():
                 f"{lab[q]} {(p[q] - t0) / 100:.2f}" for q in [90, 91, 92, 93, 96, 97, 94, 95]), flush=True)
 
 
+def kpp_dists():
+    """k_kpp_dists' phases at the products shape (round 5; block 0 and the last block, us from block 0's
+    start): candidates in LDS, the fp64 chains over the LDS-DMA ring, distances written, block totals,
+    the sgemv_t block term."""
+    lib = _lib.device_lib()
+    from gdd.kmeans import _Ops
+    n, dim, k = 2449029, 47, 196
+    X = torch.randn(n, dim, device="cuda", generator=torch.Generator(device="cuda").manual_seed(3))
+    lab = ["start", "cands", "chains", "dists", "totals", "sgemv"]
+    for rep in range(3):
+        _Ops("cuda", n, k, dim).kmeans_plusplus(X, k, np.random.RandomState(15))
+        torch.cuda.synchronize()
+        p = read(lib, "kpp")
+        t0 = p[30]
+        for base, who in ((30, "block 0"), (40, "last block")):
+            print(f"rep {rep} {who} (us): " + ", ".join(f"{lab[q]} {(p[base + q] - t0) / 100:.2f}"
+                                                      for q in range(6)), flush=True)
+        print(f"rep {rep} last wave of any block ends {(p[46] - t0) / 100:.2f} us after block 0's start", flush=True)
+
+
 def main():
     if sys.argv[1:2] == ["kpp-big"]:
         return kpp_big()
+    if sys.argv[1:2] == ["kpp-dists"]:
+        return kpp_dists()
     lib = _lib.device_lib()
     cfg = synth.CONFIGS["arxiv"]
     X = torch.from_numpy(synth.blobs(cfg.n, cfg.n_classes, cfg.k, seed=1)).cuda()
