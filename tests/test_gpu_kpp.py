@@ -214,7 +214,7 @@ def test_kpp_cumsum_adversarial(monkeypatch, n, env, rnd):
     assert idx[rnd] != idx_ref[rnd], "the blocked prefix did not cross the threshold"
 
 
-@pytest.mark.parametrize("n", [1000, 9000, 20000])
+@pytest.mark.parametrize("n", [1000, 6000, 9000, 20000])
 def test_kpp_cumsum_adversarial_weighted(monkeypatch, n):
     """The same with sample weights (w * closest in fp32, then the fp64 sum)."""
     force(monkeypatch, "kpp_big1_max=32768", "kpp_force_table")
@@ -280,10 +280,12 @@ def test_kmeans_plusplus_big_rounds(monkeypatch, n, dim, k, oracle):
         assert np.array_equal(bits(c.cpu().numpy()), bits(c_ref))
 
 
-def test_kmeans_plusplus_big_rounds_weighted_and_replayed(monkeypatch):
+@pytest.mark.parametrize("n", [9001, 6001])
+def test_kmeans_plusplus_big_rounds_weighted_and_replayed(monkeypatch, n):
     """Sample weights (w * row in fp32 for the cumulative, the weighted sgemv_t lane chains) and
-    every draw replayed (GDD_KPP_EXACT=2) on the one-workgroup-per-trial rounds."""
-    n, dim, k, T = 9001, 24, 40, 5
+    every draw replayed (GDD_KPP_EXACT=2) on the one-workgroup-per-trial rounds (6,001 points: two
+    rounds per launch, k_kpp1_big2)."""
+    dim, k, T = 24, 40, 5
     force(monkeypatch, "kpp_force_table")
     X = np.ascontiguousarray(synth.blobs(n, dim, 10, seed=77), np.float32)
     w = np.random.default_rng(3).uniform(0.5, 2.0, n).astype(np.float32)
